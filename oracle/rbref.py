@@ -1,0 +1,181 @@
+"""ctypes binding of the CPU oracle ``librbref.so`` (see rbref.h).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg as the parity checker / timed CPU baseline.  The product package
+(``roaringbitmap_amd``) never imports this module.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "librbref.so")
+
+AND, OR, XOR, ANDNOT = 0, 1, 2, 3
+FAST_OR, FAST_AND, WORKSHY_AND, NAIVE_AND, FAST_XOR, PAR_OR, PAR_XOR, NAIVE_AND_ITER = range(8)
+ARRAY, BITMAP, RUN = 0, 1, 2
+
+
+def build() -> str:
+    """Compile the oracle in place (gcc is in the image)."""
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    return _LIB_PATH
+
+
+def _load():
+    if not os.path.exists(_LIB_PATH):
+        build()
+    lib = C.CDLL(_LIB_PATH)
+    P = C.c_void_p
+    sig = {
+        "rbref_new": (P, []),
+        "rbref_free": (None, [P]),
+        "rbref_clone": (P, [P]),
+        "rbref_bitmap_of": (P, [C.POINTER(C.c_uint32), C.c_size_t]),
+        "rbref_run_optimize": (C.c_int, [P]),
+        "rbref_cardinality": (C.c_uint64, [P]),
+        "rbref_container_count": (C.c_uint32, [P]),
+        "rbref_container_info": (C.c_int, [P, C.c_uint32, C.POINTER(C.c_uint16), C.POINTER(C.c_uint8),
+                                           C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]),
+        "rbref_to_array": (C.c_uint64, [P, C.POINTER(C.c_uint32), C.c_uint64]),
+        "rbref_deserialize": (C.c_int, [C.c_char_p, C.c_size_t, C.POINTER(P)]),
+        "rbref_serialized_size": (C.c_uint64, [P]),
+        "rbref_serialize": (C.c_int, [P, C.c_void_p, C.c_uint64]),
+        "rbref_from_soa": (C.c_int, [C.c_uint32, P, P, P, P, P, P, C.POINTER(P)]),
+        "rbref_op": (P, [C.c_int, P, P]),
+        "rbref_op_cardinality": (C.c_int64, [C.c_int, P, P]),
+        "rbref_op_inplace": (C.c_int, [C.c_int, P, P]),
+        "rbref_wide": (P, [C.c_int, C.POINTER(P), C.c_size_t]),
+        "rbref_wide_cardinality": (C.c_int64, [C.c_int, C.POINTER(P), C.c_size_t]),
+        "rbref_pairwise_batch": (C.c_int, [C.c_int, C.POINTER(P), C.POINTER(P), C.c_size_t, C.c_int,
+                                           C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        _lib = _load()
+    return _lib
+
+
+class RefBitmap:
+    """Owning handle to an oracle bitmap."""
+
+    __slots__ = ("h",)
+
+    def __init__(self, handle):
+        if not handle:
+            raise RuntimeError("null oracle bitmap")
+        self.h = handle
+
+    def __del__(self):
+        if getattr(self, "h", None) and _lib is not None:
+            _lib.rbref_free(self.h)
+            self.h = None
+
+    # -- construction
+    @classmethod
+    def of(cls, values) -> "RefBitmap":
+        import numpy as np
+        arr = np.ascontiguousarray(np.asarray(values, dtype=np.uint32))
+        return cls(lib().rbref_bitmap_of(arr.ctypes.data_as(C.POINTER(C.c_uint32)), arr.size))
+
+    @classmethod
+    def deserialize(cls, data: bytes) -> "RefBitmap":
+        out = C.c_void_p()
+        rc = lib().rbref_deserialize(data, len(data), C.byref(out))
+        if rc != 0:
+            raise IOError(f"invalid RoaringFormatSpec input (rc={rc})")
+        return cls(out.value)
+
+    def clone(self) -> "RefBitmap":
+        return RefBitmap(lib().rbref_clone(self.h))
+
+    # -- queries
+    def serialize(self) -> bytes:
+        n = lib().rbref_serialized_size(self.h)
+        buf = C.create_string_buffer(int(n))
+        rc = lib().rbref_serialize(self.h, buf, n)
+        assert rc == 0
+        return buf.raw[: int(n)]
+
+    def cardinality(self) -> int:
+        return int(lib().rbref_cardinality(self.h))
+
+    def run_optimize(self) -> bool:
+        return bool(lib().rbref_run_optimize(self.h))
+
+    def containers(self):
+        """[(key, type, card, nruns)] in key order."""
+        out = []
+        k, t, c, r = C.c_uint16(), C.c_uint8(), C.c_uint32(), C.c_uint32()
+        for i in range(lib().rbref_container_count(self.h)):
+            lib().rbref_container_info(self.h, i, C.byref(k), C.byref(t), C.byref(c), C.byref(r))
+            out.append((k.value, t.value, c.value, r.value))
+        return out
+
+    def to_array(self):
+        import numpy as np
+        n = self.cardinality()
+        arr = np.empty(n, dtype=np.uint32)
+        lib().rbref_to_array(self.h, arr.ctypes.data_as(C.POINTER(C.c_uint32)), n)
+        return arr
+
+
+def op(opcode: int, a: RefBitmap, b: RefBitmap) -> RefBitmap:
+    return RefBitmap(lib().rbref_op(opcode, a.h, b.h))
+
+
+def op_cardinality(opcode: int, a: RefBitmap, b: RefBitmap) -> int:
+    return int(lib().rbref_op_cardinality(opcode, a.h, b.h))
+
+
+def op_inplace(opcode: int, a: RefBitmap, b: RefBitmap) -> None:
+    assert lib().rbref_op_inplace(opcode, a.h, b.h) == 0
+
+
+def _handles(bitmaps):
+    arr = (C.c_void_p * len(bitmaps))(*[b.h for b in bitmaps])
+    return arr
+
+
+def wide(sem: int, bitmaps) -> RefBitmap:
+    return RefBitmap(lib().rbref_wide(sem, _handles(bitmaps), len(bitmaps)))
+
+
+def wide_cardinality(opcode: int, bitmaps) -> int:
+    return int(lib().rbref_wide_cardinality(opcode, _handles(bitmaps), len(bitmaps)))
+
+
+def pairwise_batch(opcode: int, a, b, threads: int = 1):
+    card, conts = C.c_uint64(), C.c_uint64()
+    lib().rbref_pairwise_batch(opcode, _handles(a), _handles(b), len(a), threads, C.byref(card), C.byref(conts))
+    return card.value, conts.value
+
+
+def from_soa(keys, types, cards, nruns, payload, offsets) -> RefBitmap:
+    """Build one oracle bitmap from host SoA numpy arrays (one bitmap's slice)."""
+    import numpy as np
+    keys = np.ascontiguousarray(keys, dtype=np.uint16)
+    types = np.ascontiguousarray(types, dtype=np.uint8)
+    cards = np.ascontiguousarray(cards, dtype=np.uint32)
+    nruns = np.ascontiguousarray(nruns, dtype=np.uint16)
+    payload = np.ascontiguousarray(payload, dtype=np.uint8)
+    offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+    out = C.c_void_p()
+    rc = lib().rbref_from_soa(len(keys), keys.ctypes.data, types.ctypes.data, cards.ctypes.data,
+                              nruns.ctypes.data, payload.ctypes.data, offsets.ctypes.data, C.byref(out))
+    if rc != 0:
+        raise ValueError("bad SoA slice")
+    return RefBitmap(out.value)
