@@ -1,0 +1,158 @@
+/*
+ * rbgpu.h — C ABI of the MI355X-native RoaringBitmap set-algebra engine (librbgpu.so).
+ *
+ * This is the drop-in boundary: plain pointers and sizes, no torch / HIP types.  A Java
+ * host binds it through Panama FFM; the Python mirror
+ * roaringbitmap_amd/ binds it through ctypes.  Each entry point names the reference
+ * interface it replaces (paths relative to /root/reference/RoaringBitmap/src/main/java/
+ * org/roaringbitmap/).
+ *
+ * Data model.  An rbgpu_set is a device-resident batch of bitmaps in SoA form (per container:
+ * u16 key, u8 type 0=Array 1=Bitmap 2=Run, u32 cardinality, u16 run count, u64 payload
+ * offset; per bitmap: a CSR begin index).  Container payloads are byte-identical to
+ * RoaringFormatSpec container payloads (Array: sorted u16; Bitmap: 1024 LE u64; Run:
+ * (start, length-1) u16 pairs — the u16 run count lives in the metadata), so serializing a
+ * result is a copy.  Result sets have the same layout and can be fed back as inputs.
+ *
+ * Semantics.  Every result is bit-exact to the reference entry point it names: same values,
+ * same container types, hence identical serialized bytes.  Inputs are borrowed read-only;
+ * results are owned by the caller until rbgpu_set_free (the reference clones unmatched
+ * containers — RoaringArray.java:184-205 — and so do we).
+ *
+ * Errors.  Every int-returning call returns RB_OK (0) or a negative status; the message is
+ * available from rbgpu_last_error() (thread-local).  The reference's InvalidRoaringFormat /
+ * IOException (RoaringArray.java:279-288, RoaringBitmap.java:1762-1811) maps to RB_EFORMAT;
+ * IllegalArgumentException (RoaringArray.java:112-115, FastAggregation.java:53-55) maps to
+ * RB_EINVAL.  Inputs must be canonical (sorted unique keys, Array card <= 4096, Bitmap card
+ * equal to its popcount, Run lists sorted / non-overlapping / non-adjacent); the reference
+ * does not check this on deserialize (RoaringArray.java:328-337) — we do and return RB_EINVAL.
+ *
+ * Threading.  One rbgpu_ctx per host thread (it owns a HIP stream and workspaces).  Calls are
+ * synchronous, like the Java API (RoaringBitmap.java:367-369 thread-safety contract).
+ */
+#ifndef RBGPU_H
+#define RBGPU_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct rbgpu_ctx rbgpu_ctx;
+typedef struct rbgpu_set rbgpu_set;
+
+enum rb_status {
+  RB_OK = 0,
+  RB_EFORMAT = -1, /* bad cookie / size > 65536 / truncated (InvalidRoaringFormat -> IOException) */
+  RB_EINVAL = -2,  /* non-canonical input, bad index, bad argument (IllegalArgumentException) */
+  RB_ENOMEM = -3,  /* device or host allocation failed */
+  RB_EDEVICE = -4  /* HIP failure, or no MI355X visible */
+};
+
+enum rb_op { RB_AND = 0, RB_OR = 1, RB_XOR = 2, RB_ANDNOT = 3 };
+
+enum rb_type { RB_ARRAY = 0, RB_BITMAP = 1, RB_RUN = 2 };
+
+/* Wide-aggregation semantics: which reference entry point the result reproduces. */
+enum rb_wide_sem {
+  RB_FAST_OR = 0,      /* FastAggregation.or(RoaringBitmap...) == naive_or   FastAggregation.java:541-548,602 */
+  RB_FAST_AND = 1,     /* FastAggregation.and(RoaringBitmap...)              FastAggregation.java:37-42      */
+  RB_WORKSHY_AND = 2,  /* FastAggregation.workShyAnd                         FastAggregation.java:356-396    */
+  RB_NAIVE_AND = 3,    /* FastAggregation.naive_and(RoaringBitmap...)        FastAggregation.java:328-346    */
+  RB_FAST_XOR = 4,     /* FastAggregation.xor == naive_xor                   FastAggregation.java:576-582,772 */
+  RB_PAR_OR = 5,       /* ParallelAggregation.or                             ParallelAggregation.java:161-175 */
+  RB_PAR_XOR = 6,      /* ParallelAggregation.xor                            ParallelAggregation.java:182-195 */
+  RB_NAIVE_AND_ITER = 7 /* FastAggregation.and(Iterator) == naive_and(Iterator) FastAggregation.java:26,304 */
+};
+
+/* Host-side SoA description of a batch of bitmaps (used for upload and download). */
+typedef struct rb_soa {
+  uint32_t n_bitmaps;
+  uint64_t n_containers;
+  uint64_t payload_bytes;
+  uint64_t *begin;   /* [n_bitmaps + 1] CSR: containers of bitmap i are [begin[i], begin[i+1]) */
+  uint16_t *key;     /* [n_containers] high 16 bits, strictly increasing within a bitmap */
+  uint8_t *type;     /* [n_containers] rb_type */
+  uint32_t *card;    /* [n_containers] cardinality, 1..65536 */
+  uint16_t *nruns;   /* [n_containers] run count (Run containers), else 0 */
+  uint64_t *offset;  /* [n_containers] byte offset of the payload in `payload` */
+  uint8_t *payload;  /* [payload_bytes] */
+} rb_soa;
+
+/* Per-call accounting of the last operation on a context (for the roofline report). */
+typedef struct rb_stats {
+  uint64_t tasks;            /* container-level work items launched */
+  uint64_t input_bytes;      /* algorithmic input bytes (payload + 16 B metadata per container read, + 2 B per key) */
+  uint64_t output_bytes;     /* algorithmic output bytes (payload + 16 B metadata per result container) */
+  uint64_t result_containers;
+  double main_kernel_ms;     /* duration of the dominant kernel (HIP events on the ctx stream) */
+  double total_ms;           /* whole call, device time between first and last launch */
+  char main_kernel[64];      /* name of the dominant kernel */
+} rb_stats;
+
+/* ---- context ---------------------------------------------------------------------- */
+int rbgpu_device_count(void);
+int rbgpu_open(int device, rbgpu_ctx **out);
+void rbgpu_close(rbgpu_ctx *ctx);
+const char *rbgpu_last_error(void);
+int rbgpu_synchronize(rbgpu_ctx *ctx);
+int rbgpu_get_stats(rbgpu_ctx *ctx, rb_stats *out);
+
+/* ---- sets (RoaringBitmap / RoaringArray storage) ----------------------------------- */
+/* RoaringBitmap.deserialize(ByteBuffer) for n bitmaps — RoaringArray.java:547-629 */
+int rbgpu_set_from_serialized(rbgpu_ctx *ctx, const uint8_t *const *bufs, const uint64_t *lens,
+                              uint32_t n, rbgpu_set **out);
+/* Upload a host SoA batch (validated like deserialize). */
+int rbgpu_set_from_soa(rbgpu_ctx *ctx, const rb_soa *soa, rbgpu_set **out);
+void rbgpu_set_free(rbgpu_set *set);
+uint32_t rbgpu_set_bitmap_count(const rbgpu_set *set);
+uint64_t rbgpu_set_container_count(const rbgpu_set *set);
+/* RoaringBitmap.getCardinality per bitmap (computed on device). */
+int rbgpu_set_cardinalities(const rbgpu_set *set, uint64_t *out /* [n_bitmaps] */);
+/* RoaringBitmap.serializedSizeInBytes per bitmap — RoaringArray.java:947-953 */
+int rbgpu_set_serialized_sizes(const rbgpu_set *set, uint64_t *out /* [n_bitmaps] */);
+/* RoaringBitmap.serialize(ByteBuffer) of bitmaps [first, first+count) back to back into dst;
+ * offsets[count+1] receives each bitmap's start — RoaringArray.java:851-940 */
+int rbgpu_set_serialize(const rbgpu_set *set, uint32_t first, uint32_t count, uint8_t *dst,
+                        uint64_t cap, uint64_t *offsets);
+/* Download bitmaps [first, first+count) as host SoA.  Call once with soa->key == NULL to get
+ * n_containers / payload_bytes, allocate, call again to fill. */
+int rbgpu_set_download(const rbgpu_set *set, uint32_t first, uint32_t count, rb_soa *soa);
+
+/* ---- pairwise set algebra (static RoaringBitmap ops) ------------------------------- */
+/* result[i] = op(a[a_idx[i]], b[b_idx[i]]); a_idx / b_idx may be NULL (identity).
+ * RoaringBitmap.and/or/xor/andNot — RoaringBitmap.java:377-401, 860-902, 1071-1118, 444-473 */
+int rbgpu_pairwise(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu_set *b,
+                   const uint32_t *a_idx, const uint32_t *b_idx, uint32_t npairs, rbgpu_set **out);
+/* RoaringBitmap.andCardinality/orCardinality/xorCardinality/andNotCardinality
+ * — RoaringBitmap.java:413-434, 916-920, 931-933, 944-985 */
+int rbgpu_pairwise_cardinality(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu_set *b,
+                               const uint32_t *a_idx, const uint32_t *b_idx, uint32_t npairs,
+                               uint64_t *out /* [npairs] */);
+
+/* ---- wide aggregation over members[0..n) of `in` (NULL = all bitmaps, in order) ------ */
+int rbgpu_wide(rbgpu_ctx *ctx, int sem, const rbgpu_set *in, const uint32_t *members, uint32_t n,
+               rbgpu_set **out);
+/* FastAggregation.andCardinality / orCardinality — FastAggregation.java:71-101 */
+int rbgpu_wide_cardinality(rbgpu_ctx *ctx, int op, const rbgpu_set *in, const uint32_t *members,
+                           uint32_t n, uint64_t *out);
+
+/* ---- synthetic inputs for the benchmark (device-side generator, SplitMix64) ---------- */
+enum rb_workload {
+  RB_WL_FILTER_POSTING = 0, /* a = filters (4 keys, A/B/R .4/.3/.3),
+                               b = posting lists (keys w.p. .5, A/B/R .7/.1/.2), n pairs */
+  RB_WL_WIDE_DENSE = 1,     /* config 3: n bitmaps over 65536 keys, key w.p. 1/16, all Bitmap */
+  RB_WL_WIDE_MIXED = 2,     /* config 3b: as 1 with 70% B / 20% A / 10% R */
+  RB_WL_WIDE_RUNS = 3       /* config 4: n bitmaps x 65536 keys of run-heavy containers */
+};
+/* Generates a (and b for RB_WL_FILTER_POSTING; *b may be NULL otherwise).  n = pairs or
+ * bitmaps.  Every container goes through runOptimize semantics, as
+ * RoaringBitmapWriter(runCompress=true) does (ContainerAppender.java:130-137). */
+int rbgpu_generate(rbgpu_ctx *ctx, int workload, uint32_t n, uint64_t seed, rbgpu_set **a,
+                   rbgpu_set **b);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,21 @@
+"""roaringbitmap_amd — MI355X-native engine for RoaringBitmap's set-algebra hot path.
+
+Batched pairwise and/or/xor/andNot and wide FastAggregation / ParallelAggregation run as
+hand-written gfx950 HIP kernels in librbgpu.so (C ABI: include/rbgpu.h).  Results are
+bit-exact to the Java reference (identical RoaringFormatSpec bytes and cardinalities).
+"""
+from . import _lib
+from ._lib import (AND, ANDNOT, ARRAY, BITMAP, FAST_AND, FAST_OR, FAST_XOR, NAIVE_AND, NAIVE_AND_ITER, OR,
+                   PAR_OR, PAR_XOR, RUN, WL_FILTER_POSTING, WL_WIDE_DENSE, WL_WIDE_MIXED, WL_WIDE_RUNS,
+                   WORKSHY_AND, XOR, FormatError, InvalidArgument, RbError)
+from .engine import Context, DeviceSet, HostSoA, default_context, soa_from_values
+from .roaring import FastAggregation, ParallelAggregation, RoaringBitmap
+
+__all__ = [
+    "AND", "OR", "XOR", "ANDNOT", "ARRAY", "BITMAP", "RUN",
+    "FAST_OR", "FAST_AND", "WORKSHY_AND", "NAIVE_AND", "FAST_XOR", "PAR_OR", "PAR_XOR", "NAIVE_AND_ITER",
+    "WL_FILTER_POSTING", "WL_WIDE_DENSE", "WL_WIDE_MIXED", "WL_WIDE_RUNS",
+    "Context", "DeviceSet", "HostSoA", "default_context", "soa_from_values",
+    "RoaringBitmap", "FastAggregation", "ParallelAggregation",
+    "RbError", "FormatError", "InvalidArgument",
+]

@@ -1,0 +1,117 @@
+"""ctypes binding of librbgpu.so (include/rbgpu.h).
+
+The HIP extension is the only compute path: importing this module without the built
+library raises immediately (there is no CPU fallback in the product).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "librbgpu.so")
+
+RB_OK, RB_EFORMAT, RB_EINVAL, RB_ENOMEM, RB_EDEVICE = 0, -1, -2, -3, -4
+AND, OR, XOR, ANDNOT = 0, 1, 2, 3
+ARRAY, BITMAP, RUN = 0, 1, 2
+FAST_OR, FAST_AND, WORKSHY_AND, NAIVE_AND, FAST_XOR, PAR_OR, PAR_XOR, NAIVE_AND_ITER = range(8)
+WL_FILTER_POSTING, WL_WIDE_DENSE, WL_WIDE_MIXED, WL_WIDE_RUNS = range(4)
+
+
+class RbSoa(C.Structure):
+    _fields_ = [
+        ("n_bitmaps", C.c_uint32),
+        ("n_containers", C.c_uint64),
+        ("payload_bytes", C.c_uint64),
+        ("begin", C.c_void_p),
+        ("key", C.c_void_p),
+        ("type", C.c_void_p),
+        ("card", C.c_void_p),
+        ("nruns", C.c_void_p),
+        ("offset", C.c_void_p),
+        ("payload", C.c_void_p),
+    ]
+
+
+class RbStats(C.Structure):
+    _fields_ = [
+        ("tasks", C.c_uint64),
+        ("input_bytes", C.c_uint64),
+        ("output_bytes", C.c_uint64),
+        ("result_containers", C.c_uint64),
+        ("main_kernel_ms", C.c_double),
+        ("total_ms", C.c_double),
+        ("main_kernel", C.c_char * 64),
+    ]
+
+
+# every symbol include/rbgpu.h declares, with its ctypes signature
+_P = C.c_void_p
+_U32P = C.POINTER(C.c_uint32)
+_U64P = C.POINTER(C.c_uint64)
+SIGNATURES = {
+    "rbgpu_device_count": (C.c_int, []),
+    "rbgpu_open": (C.c_int, [C.c_int, C.POINTER(_P)]),
+    "rbgpu_close": (None, [_P]),
+    "rbgpu_last_error": (C.c_char_p, []),
+    "rbgpu_synchronize": (C.c_int, [_P]),
+    "rbgpu_get_stats": (C.c_int, [_P, C.POINTER(RbStats)]),
+    "rbgpu_set_from_serialized": (C.c_int, [_P, C.POINTER(C.c_char_p), _U64P, C.c_uint32, C.POINTER(_P)]),
+    "rbgpu_set_from_soa": (C.c_int, [_P, C.POINTER(RbSoa), C.POINTER(_P)]),
+    "rbgpu_set_free": (None, [_P]),
+    "rbgpu_set_bitmap_count": (C.c_uint32, [_P]),
+    "rbgpu_set_container_count": (C.c_uint64, [_P]),
+    "rbgpu_set_cardinalities": (C.c_int, [_P, _U64P]),
+    "rbgpu_set_serialized_sizes": (C.c_int, [_P, _U64P]),
+    "rbgpu_set_serialize": (C.c_int, [_P, C.c_uint32, C.c_uint32, C.c_void_p, C.c_uint64, _U64P]),
+    "rbgpu_set_download": (C.c_int, [_P, C.c_uint32, C.c_uint32, C.POINTER(RbSoa)]),
+    "rbgpu_pairwise": (C.c_int, [_P, C.c_int, _P, _P, _U32P, _U32P, C.c_uint32, C.POINTER(_P)]),
+    "rbgpu_pairwise_cardinality": (C.c_int, [_P, C.c_int, _P, _P, _U32P, _U32P, C.c_uint32, _U64P]),
+    "rbgpu_wide": (C.c_int, [_P, C.c_int, _P, _U32P, C.c_uint32, C.POINTER(_P)]),
+    "rbgpu_wide_cardinality": (C.c_int, [_P, C.c_int, _P, _U32P, C.c_uint32, _U64P]),
+    "rbgpu_generate": (C.c_int, [_P, C.c_int, C.c_uint32, C.c_uint64, C.POINTER(_P), C.POINTER(_P)]),
+}
+
+
+class RbError(Exception):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"rbgpu error {code}: {msg}")
+        self.code = code
+
+
+class FormatError(RbError, IOError):
+    """RB_EFORMAT — the reference throws IOException (InvalidRoaringFormat)."""
+
+
+class InvalidArgument(RbError, ValueError):
+    """RB_EINVAL — the reference throws IllegalArgumentException."""
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(
+                f"{LIB_PATH} is missing: build the HIP extension first "
+                "(python -c 'import __graft_entry__ as g; g.build()')")
+        L = C.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def check(rc: int) -> None:
+    if rc == RB_OK:
+        return
+    msg = (lib().rbgpu_last_error() or b"").decode(errors="replace")
+    if rc == RB_EFORMAT:
+        raise FormatError(rc, msg)
+    if rc == RB_EINVAL:
+        raise InvalidArgument(rc, msg)
+    raise RbError(rc, msg)

@@ -1,0 +1,551 @@
+// api.hip — the C ABI of librbgpu (include/rbgpu.h): contexts, device-resident sets,
+// pairwise / wide set algebra orchestration, serialization, synthetic generation.
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "format.hpp"
+#include "internal.hpp"
+#include "kernels.hpp"
+
+using namespace rbg;
+
+namespace {
+thread_local std::string g_err;
+} // namespace
+
+namespace rbg {
+int fail(int code, const char *fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+int set_alloc(rbgpu_ctx *ctx, rbgpu_set *s, uint32_t nb, uint64_t nc, uint64_t payload) {
+  s->ctx = ctx;
+  s->nb = nb;
+  s->nc = nc;
+  s->payload_bytes = payload;
+  DevPool &p = ctx->pool;
+  const uint64_t ncap = std::max<uint64_t>(nc, 1);
+  if (p.alloc((void **)&s->begin, (nb + 1) * sizeof(uint64_t)) != hipSuccess ||
+      p.alloc((void **)&s->key, ncap * 2) != hipSuccess || p.alloc((void **)&s->type, ncap) != hipSuccess ||
+      p.alloc((void **)&s->card, ncap * 4) != hipSuccess || p.alloc((void **)&s->nruns, ncap * 2) != hipSuccess ||
+      p.alloc((void **)&s->off, ncap * 8) != hipSuccess ||
+      p.alloc((void **)&s->payload, std::max<uint64_t>(payload, 16)) != hipSuccess)
+    return fail(RB_ENOMEM, "device allocation of a %u-bitmap / %llu-container set failed", nb,
+                (unsigned long long)nc);
+  return RB_OK;
+}
+void set_release(rbgpu_set *s) {
+  if (!s || !s->ctx) return;
+  DevPool &p = s->ctx->pool;
+  p.release(s->begin);
+  p.release(s->key);
+  p.release(s->type);
+  p.release(s->card);
+  p.release(s->nruns);
+  p.release(s->off);
+  p.release(s->payload);
+  s->ctx = nullptr;
+}
+int ensure_h_begin(const rbgpu_set *cs) {
+  rbgpu_set *s = const_cast<rbgpu_set *>(cs);
+  if (s->h_begin.size() == (size_t)s->nb + 1) return RB_OK;
+  s->h_begin.resize((size_t)s->nb + 1);
+  HIPCHK(hipSetDevice(s->ctx->device));
+  HIPCHK(hipMemcpyAsync(s->h_begin.data(), s->begin, (s->nb + 1) * sizeof(uint64_t), hipMemcpyDeviceToHost,
+                        s->ctx->stream));
+  HIPCHK(hipStreamSynchronize(s->ctx->stream));
+  return RB_OK;
+}
+} // namespace rbg
+
+namespace {
+// Upload a validated host SoA, re-laid out: Bitmaps first (8 KiB aligned), then the rest (16 B).
+int upload_host(rbgpu_ctx *ctx, const HostSoA &h, rbgpu_set **out) {
+  const uint64_t nc = h.nc();
+  std::vector<uint64_t> off(nc);
+  uint64_t nbig = 0, small = 0;
+  for (uint64_t i = 0; i < nc; ++i) {
+    if (h.type[i] == RB_BITMAP) ++nbig;
+    else small += round16(payload_bytes(h.type[i], h.card[i], h.nruns[i]));
+  }
+  uint64_t bi = 0, so = nbig * kBitmapBytes;
+  for (uint64_t i = 0; i < nc; ++i) {
+    if (h.type[i] == RB_BITMAP) off[i] = (bi++) * kBitmapBytes;
+    else {
+      off[i] = so;
+      so += round16(payload_bytes(h.type[i], h.card[i], h.nruns[i]));
+    }
+  }
+  const uint64_t total = nbig * kBitmapBytes + small;
+  std::vector<uint8_t> staged(std::max<uint64_t>(total, 16), 0);
+  for (uint64_t i = 0; i < nc; ++i)
+    std::memcpy(staged.data() + off[i], h.payload.data() + h.off[i], payload_bytes(h.type[i], h.card[i], h.nruns[i]));
+  rbgpu_set *s = new rbgpu_set;
+  int rc = set_alloc(ctx, s, h.nb, nc, total);
+  if (rc) {
+    delete s;
+    return rc;
+  }
+  hipStream_t st = ctx->stream;
+  auto cp = [&](void *dst, const void *src, size_t n) {
+    return n ? hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, st) : hipSuccess;
+  };
+  if (cp(s->begin, h.begin.data(), (h.nb + 1) * 8) || cp(s->key, h.key.data(), nc * 2) ||
+      cp(s->type, h.type.data(), nc) || cp(s->card, h.card.data(), nc * 4) || cp(s->nruns, h.nruns.data(), nc * 2) ||
+      cp(s->off, off.data(), nc * 8) || cp(s->payload, staged.data(), total) || hipStreamSynchronize(st)) {
+    set_release(s);
+    delete s;
+    return fail(RB_EDEVICE, "host-to-device upload failed");
+  }
+  s->h_begin = h.begin;
+  *out = s;
+  return RB_OK;
+}
+
+// Download bitmaps [first, first+count) into a HostSoA with compact 16-B aligned payloads.
+int download_host(const rbgpu_set *s, uint32_t first, uint32_t count, HostSoA &h) {
+  rbgpu_ctx *ctx = s->ctx;
+  HIPCHK(hipSetDevice(ctx->device));
+  int rc = ensure_h_begin(s);
+  if (rc) return rc;
+  const uint64_t lo = s->h_begin[first], hi = s->h_begin[first + count], n = hi - lo;
+  hipStream_t st = ctx->stream;
+  h.nb = count;
+  h.begin.resize(count + 1);
+  for (uint32_t i = 0; i <= count; ++i) h.begin[i] = s->h_begin[first + i] - lo;
+  h.key.resize(n);
+  h.type.resize(n);
+  h.card.resize(n);
+  h.nruns.resize(n);
+  h.off.resize(n);
+  std::vector<uint64_t> soff(n);
+  if (n) {
+    HIPCHK(hipMemcpyAsync(h.key.data(), s->key + lo, n * 2, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(h.type.data(), s->type + lo, n, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(h.card.data(), s->card + lo, n * 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(h.nruns.data(), s->nruns + lo, n * 2, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(soff.data(), s->off + lo, n * 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+  }
+  std::vector<uint64_t> bytes(n);
+  uint64_t total = 0;
+  for (uint64_t i = 0; i < n; ++i) {
+    bytes[i] = payload_bytes(h.type[i], h.card[i], h.nruns[i]);
+    h.off[i] = total;
+    total += round16(bytes[i]);
+  }
+  h.payload.assign(std::max<uint64_t>(total, 16), 0);
+  if (n) {
+    uint64_t *d_soff, *d_doff, *d_bytes;
+    uint8_t *d_stage;
+    if (ctx->pool.alloc((void **)&d_soff, n * 8) || ctx->pool.alloc((void **)&d_doff, n * 8) ||
+        ctx->pool.alloc((void **)&d_bytes, n * 8) || ctx->pool.alloc((void **)&d_stage, std::max<uint64_t>(total, 16)))
+      return fail(RB_ENOMEM, "download staging allocation failed");
+    HIPCHK(hipMemcpyAsync(d_soff, soff.data(), n * 8, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(d_doff, h.off.data(), n * 8, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(d_bytes, bytes.data(), n * 8, hipMemcpyHostToDevice, st));
+    launch_gather(s->payload, d_soff, d_bytes, d_stage, d_doff, n, st);
+    HIPCHK(hipMemcpyAsync(h.payload.data(), d_stage, total, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    ctx->pool.release(d_soff);
+    ctx->pool.release(d_doff);
+    ctx->pool.release(d_bytes);
+    ctx->pool.release(d_stage);
+  }
+  return RB_OK;
+}
+
+int check_ctx(rbgpu_ctx *ctx) {
+  if (!ctx) return fail(RB_EINVAL, "null context");
+  HIPCHK(hipSetDevice(ctx->device));
+  return RB_OK;
+}
+
+} // namespace
+
+namespace rbg {
+void stats_begin(rbgpu_ctx *ctx) {
+  (void)hipMemsetAsync(ctx->d_stats, 0, 4 * sizeof(uint64_t), ctx->stream);
+  (void)hipEventRecord(ctx->ev[0], ctx->stream);
+}
+int stats_end(rbgpu_ctx *ctx, const char *main_name, uint64_t tasks, uint64_t result_containers) {
+  HIPCHK(hipEventRecord(ctx->ev[3], ctx->stream));
+  HIPCHK(hipMemcpyAsync(ctx->h_pinned + 8, ctx->d_stats, 4 * sizeof(uint64_t), hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  rb_stats &s = ctx->last;
+  s.tasks = tasks;
+  s.input_bytes = ctx->h_pinned[8];
+  s.output_bytes = ctx->h_pinned[9];
+  s.result_containers = result_containers;
+  float ms = 0;
+  s.main_kernel_ms = hipEventElapsedTime(&ms, ctx->ev[1], ctx->ev[2]) == hipSuccess ? ms : 0.0;
+  s.total_ms = hipEventElapsedTime(&ms, ctx->ev[0], ctx->ev[3]) == hipSuccess ? ms : 0.0;
+  std::snprintf(s.main_kernel, sizeof s.main_kernel, "%s", main_name);
+  return RB_OK;
+}
+} // namespace rbg
+
+// ===================================================================== C ABI
+extern "C" {
+
+const char *rbgpu_last_error(void) { return g_err.c_str(); }
+
+int rbgpu_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) {
+    (void)hipGetLastError();
+    return 0;
+  }
+  return n;
+}
+
+int rbgpu_open(int device, rbgpu_ctx **out) {
+  if (!out) return fail(RB_EINVAL, "null out");
+  *out = nullptr;
+  int n = rbgpu_device_count();
+  if (device < 0 || device >= n) return fail(RB_EDEVICE, "no HIP device %d (found %d)", device, n);
+  HIPCHK(hipSetDevice(device));
+  rbgpu_ctx *c = new rbgpu_ctx;
+  c->device = device;
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipMalloc((void **)&c->d_stats, 4 * sizeof(uint64_t)) != hipSuccess ||
+      hipHostMalloc((void **)&c->h_pinned, 16 * sizeof(uint64_t)) != hipSuccess) {
+    delete c;
+    return fail(RB_EDEVICE, "context creation failed on device %d", device);
+  }
+  for (auto &e : c->ev) (void)hipEventCreate(&e);
+  *out = c;
+  return RB_OK;
+}
+
+void rbgpu_close(rbgpu_ctx *ctx) {
+  if (!ctx) return;
+  (void)hipSetDevice(ctx->device);
+  (void)hipStreamSynchronize(ctx->stream);
+  for (auto &e : ctx->ev) (void)hipEventDestroy(e);
+  (void)hipFree(ctx->d_stats);
+  (void)hipHostFree(ctx->h_pinned);
+  ctx->pool.clear();
+  ctx->ws_pairs.destroy();
+  ctx->ws_tasks.destroy();
+  ctx->ws_wide.destroy();
+  (void)hipStreamDestroy(ctx->stream);
+  delete ctx;
+}
+
+int rbgpu_synchronize(rbgpu_ctx *ctx) {
+  int rc = check_ctx(ctx);
+  if (rc) return rc;
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  return RB_OK;
+}
+
+int rbgpu_get_stats(rbgpu_ctx *ctx, rb_stats *out) {
+  if (!ctx || !out) return fail(RB_EINVAL, "null argument");
+  *out = ctx->last;
+  return RB_OK;
+}
+
+int rbgpu_set_from_serialized(rbgpu_ctx *ctx, const uint8_t *const *bufs, const uint64_t *lens, uint32_t n,
+                              rbgpu_set **out) {
+  int rc = check_ctx(ctx);
+  if (rc) return rc;
+  if (!out || (n && (!bufs || !lens))) return fail(RB_EINVAL, "null argument");
+  HostSoA h;
+  std::string err;
+  for (uint32_t i = 0; i < n; ++i) {
+    rc = parse_serialized(bufs[i], lens[i], h, err);
+    if (rc) return fail(rc, "bitmap %u: %s", i, err.c_str());
+  }
+  return upload_host(ctx, h, out);
+}
+
+int rbgpu_set_from_soa(rbgpu_ctx *ctx, const rb_soa *soa, rbgpu_set **out) {
+  int rc = check_ctx(ctx);
+  if (rc) return rc;
+  if (!soa || !out) return fail(RB_EINVAL, "null argument");
+  HostSoA h;
+  h.nb = soa->n_bitmaps;
+  h.begin.assign(soa->begin, soa->begin + soa->n_bitmaps + 1);
+  if (h.begin[0] != 0 || h.begin[h.nb] != soa->n_containers) return fail(RB_EINVAL, "bad CSR begin array");
+  const uint64_t nc = soa->n_containers;
+  h.key.assign(soa->key, soa->key + nc);
+  h.type.assign(soa->type, soa->type + nc);
+  h.card.assign(soa->card, soa->card + nc);
+  h.nruns.assign(soa->nruns, soa->nruns + nc);
+  h.off.resize(nc);
+  std::string err;
+  for (uint32_t b = 0; b < h.nb; ++b) {
+    if (h.begin[b + 1] < h.begin[b]) return fail(RB_EINVAL, "bad CSR begin array");
+    for (uint64_t i = h.begin[b]; i < h.begin[b + 1]; ++i)
+      if (i > h.begin[b] && h.key[i] <= h.key[i - 1]) return fail(RB_EINVAL, "bitmap %u: keys not increasing", b);
+  }
+  for (uint64_t i = 0; i < nc; ++i) {
+    const uint64_t bytes = payload_bytes(h.type[i], h.card[i], h.nruns[i]);
+    if (soa->offset[i] + bytes > soa->payload_bytes) return fail(RB_EINVAL, "container %llu payload out of range", (unsigned long long)i);
+    rc = validate_container(h.type[i], h.card[i], h.nruns[i], soa->payload + soa->offset[i], err);
+    if (rc) return fail(rc, "container %llu: %s", (unsigned long long)i, err.c_str());
+    h.off[i] = soa->offset[i];
+  }
+  h.payload.assign(soa->payload, soa->payload + soa->payload_bytes);
+  return upload_host(ctx, h, out);
+}
+
+void rbgpu_set_free(rbgpu_set *set) {
+  if (!set) return;
+  set_release(set);
+  delete set;
+}
+uint32_t rbgpu_set_bitmap_count(const rbgpu_set *s) { return s ? s->nb : 0; }
+uint64_t rbgpu_set_container_count(const rbgpu_set *s) { return s ? s->nc : 0; }
+
+int rbgpu_set_cardinalities(const rbgpu_set *s, uint64_t *out) {
+  if (!s || !out) return fail(RB_EINVAL, "null argument");
+  rbgpu_ctx *ctx = s->ctx;
+  int rc = check_ctx(ctx);
+  if (rc) return rc;
+  uint64_t *d;
+  if (ctx->pool.alloc((void **)&d, std::max<uint64_t>(s->nb, 1) * 8)) return fail(RB_ENOMEM, "alloc");
+  launch_bitmap_cards(s->view(), s->nb, d, ctx->stream);
+  HIPCHK(hipMemcpyAsync(out, d, s->nb * 8ull, hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  ctx->pool.release(d);
+  return RB_OK;
+}
+
+int rbgpu_set_download(const rbgpu_set *s, uint32_t first, uint32_t count, rb_soa *soa) {
+  if (!s || !soa) return fail(RB_EINVAL, "null argument");
+  if ((uint64_t)first + count > s->nb) return fail(RB_EINVAL, "bitmap range out of bounds");
+  HostSoA h;
+  int rc = download_host(s, first, count, h);
+  if (rc) return rc;
+  if (!soa->key) { // size query
+    soa->n_bitmaps = count;
+    soa->n_containers = h.nc();
+    soa->payload_bytes = h.payload.size();
+    return RB_OK;
+  }
+  if (soa->n_containers < h.nc() || soa->payload_bytes < h.payload.size())
+    return fail(RB_EINVAL, "rb_soa buffers too small");
+  soa->n_bitmaps = count;
+  soa->n_containers = h.nc();
+  soa->payload_bytes = h.payload.size();
+  std::memcpy(soa->begin, h.begin.data(), (count + 1) * 8ull);
+  std::memcpy(soa->key, h.key.data(), h.nc() * 2);
+  std::memcpy(soa->type, h.type.data(), h.nc());
+  std::memcpy(soa->card, h.card.data(), h.nc() * 4);
+  std::memcpy(soa->nruns, h.nruns.data(), h.nc() * 2);
+  std::memcpy(soa->offset, h.off.data(), h.nc() * 8);
+  std::memcpy(soa->payload, h.payload.data(), h.payload.size());
+  return RB_OK;
+}
+
+int rbgpu_set_serialized_sizes(const rbgpu_set *s, uint64_t *out) {
+  if (!s || !out) return fail(RB_EINVAL, "null argument");
+  int rc = check_ctx(s->ctx);
+  if (rc) return rc;
+  rc = ensure_h_begin(s);
+  if (rc) return rc;
+  // sizes need only metadata: download types / cards / nruns
+  const uint64_t n = s->nc;
+  std::vector<uint8_t> type(n);
+  std::vector<uint16_t> nruns(n);
+  std::vector<uint32_t> card(n);
+  if (n) {
+    HIPCHK(hipMemcpyAsync(type.data(), s->type, n, hipMemcpyDeviceToHost, s->ctx->stream));
+    HIPCHK(hipMemcpyAsync(nruns.data(), s->nruns, n * 2, hipMemcpyDeviceToHost, s->ctx->stream));
+    HIPCHK(hipMemcpyAsync(card.data(), s->card, n * 4, hipMemcpyDeviceToHost, s->ctx->stream));
+    HIPCHK(hipStreamSynchronize(s->ctx->stream));
+  }
+  for (uint32_t b = 0; b < s->nb; ++b) {
+    const uint64_t lo = s->h_begin[b], hi = s->h_begin[b + 1], k = hi - lo;
+    bool hasrun = false;
+    uint64_t bytes = 0;
+    for (uint64_t i = lo; i < hi; ++i) {
+      hasrun |= type[i] == RB_RUN;
+      bytes += type[i] == RB_ARRAY ? 2ull * card[i] : type[i] == RB_BITMAP ? 8192 : 2 + 4ull * nruns[i];
+    }
+    out[b] = (hasrun ? (k < 4 ? 4 + (k + 7) / 8 + 4 * k : 4 + (k + 7) / 8 + 8 * k) : 8 + 8 * k) + bytes;
+  }
+  return RB_OK;
+}
+
+int rbgpu_set_serialize(const rbgpu_set *s, uint32_t first, uint32_t count, uint8_t *dst, uint64_t cap,
+                        uint64_t *offsets) {
+  if (!s || (count && !dst)) return fail(RB_EINVAL, "null argument");
+  if ((uint64_t)first + count > s->nb) return fail(RB_EINVAL, "bitmap range out of bounds");
+  HostSoA h;
+  int rc = download_host(s, first, count, h);
+  if (rc) return rc;
+  uint64_t pos = 0;
+  for (uint32_t b = 0; b < count; ++b) {
+    const uint64_t k = serialized_size(h, b);
+    if (pos + k > cap) return fail(RB_EINVAL, "destination buffer too small (%llu needed)", (unsigned long long)(pos + k));
+    if (offsets) offsets[b] = pos;
+    serialize_bitmap(h, b, dst + pos);
+    pos += k;
+  }
+  if (offsets) offsets[count] = pos;
+  return RB_OK;
+}
+
+// ---------------------------------------------------------------- pairwise
+static int pairwise_impl(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu_set *b, const uint32_t *a_idx,
+                         const uint32_t *b_idx, uint32_t npairs, rbgpu_set **out, uint64_t *card_out) {
+  int rc = check_ctx(ctx);
+  if (rc) return rc;
+  if (op < RB_AND || op > RB_ANDNOT) return fail(RB_EINVAL, "bad op %d", op);
+  if (!a || !b) return fail(RB_EINVAL, "null set");
+  if (a->ctx != ctx || b->ctx != ctx) return fail(RB_EINVAL, "sets belong to another context");
+  if (!a_idx && npairs > a->nb) return fail(RB_EINVAL, "npairs exceeds bitmaps of a");
+  if (!b_idx && npairs > b->nb) return fail(RB_EINVAL, "npairs exceeds bitmaps of b");
+  for (uint32_t i = 0; a_idx && i < npairs; ++i)
+    if (a_idx[i] >= a->nb) return fail(RB_EINVAL, "a_idx[%u] out of range", i);
+  for (uint32_t i = 0; b_idx && i < npairs; ++i)
+    if (b_idx[i] >= b->nb) return fail(RB_EINVAL, "b_idx[%u] out of range", i);
+  const bool card_only = out == nullptr;
+  hipStream_t st = ctx->stream;
+  const uint64_t np = npairs;
+  const uint64_t scan_tmp = scan_tmp_words(np + 1);
+  size_t need = 0;
+  need += 2 * aligned256(np * 4);            // indices
+  need += 9 * aligned256((np + 1) * 8);      // counts, scans, result counts, pair cards
+  need += aligned256(scan_tmp * 8);
+  if (ctx->ws_pairs.reserve(need, st) != hipSuccess) return fail(RB_ENOMEM, "pair workspace");
+  Workspace &W = ctx->ws_pairs;
+  uint32_t *d_aidx = a_idx ? W.take<uint32_t>(np) : nullptr;
+  uint32_t *d_bidx = b_idx ? W.take<uint32_t>(np) : nullptr;
+  uint64_t *cnt = W.take<uint64_t>(np + 1), *nbig = W.take<uint64_t>(np + 1), *small = W.take<uint64_t>(np + 1);
+  uint64_t *tb = W.take<uint64_t>(np + 1), *bb = W.take<uint64_t>(np + 1), *sb = W.take<uint64_t>(np + 1);
+  uint64_t *rcnt = W.take<uint64_t>(np + 1), *pcard = W.take<uint64_t>(np + 1);
+  uint64_t *tmp = W.take<uint64_t>(std::max<uint64_t>(scan_tmp, 1));
+  if (d_aidx) HIPCHK(hipMemcpyAsync(d_aidx, a_idx, np * 4, hipMemcpyHostToDevice, st));
+  if (d_bidx) HIPCHK(hipMemcpyAsync(d_bidx, b_idx, np * 4, hipMemcpyHostToDevice, st));
+
+  stats_begin(ctx);
+  PairArgs pa{op, a->view(), b->view(), d_aidx, d_bidx, npairs};
+  launch_pair_count(pa, cnt, nbig, small, ctx->d_stats, st);
+  scan_exclusive(cnt, tb, np, tmp, st);
+  scan_exclusive(nbig, bb, np, tmp, st);
+  scan_exclusive(small, sb, np, tmp, st);
+  HIPCHK(hipMemcpyAsync(ctx->h_pinned + 0, tb + np, 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(ctx->h_pinned + 1, bb + np, 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(ctx->h_pinned + 2, sb + np, 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  const uint64_t ntasks = ctx->h_pinned[0], nbig_t = ctx->h_pinned[1], small_t = ctx->h_pinned[2];
+  const uint64_t small_base = nbig_t * kBitmapBytes;
+  const uint64_t arena = card_only ? 0 : small_base + small_t;
+
+  size_t tneed = aligned256(ntasks * sizeof(Task)) + 2 * aligned256(ntasks * 2) + aligned256(ntasks) +
+                 aligned256(ntasks * 4) + 256;
+  if (ctx->ws_tasks.reserve(tneed, st) != hipSuccess) return fail(RB_ENOMEM, "task workspace (%llu tasks)", (unsigned long long)ntasks);
+  Workspace &T = ctx->ws_tasks;
+  Task *tasks = T.take<Task>(std::max<uint64_t>(ntasks, 1));
+  TaskMeta tm;
+  tm.key = T.take<uint16_t>(std::max<uint64_t>(ntasks, 1));
+  tm.nruns = T.take<uint16_t>(std::max<uint64_t>(ntasks, 1));
+  tm.type = T.take<uint8_t>(std::max<uint64_t>(ntasks, 1));
+  tm.card = T.take<uint32_t>(std::max<uint64_t>(ntasks, 1));
+
+  rbgpu_set *res = nullptr;
+  if (!card_only) {
+    res = new rbgpu_set;
+    rc = set_alloc(ctx, res, npairs, ntasks, arena);
+    if (rc) {
+      delete res;
+      return rc;
+    }
+  }
+  launch_pair_emit(pa, tb, bb, sb, small_base, tasks, tm.key, st);
+  HIPCHK(hipEventRecord(ctx->ev[1], st));
+  launch_pairwise(op, card_only, pa.A, pa.B, tasks, ntasks, res ? res->payload : nullptr, tm, st);
+  HIPCHK(hipEventRecord(ctx->ev[2], st));
+  launch_compact_count(tb, npairs, tm.type, rcnt, st);
+  uint64_t *rbegin = res ? res->begin : W.take<uint64_t>(np + 1);
+  scan_exclusive(rcnt, rbegin, np, tmp, st);
+  OutView ov{};
+  if (res) ov = OutView{res->key, res->type, res->card, res->nruns, res->off};
+  launch_compact_write(tb, npairs, tm, tasks, rbegin, ov, pcard, ctx->d_stats, st);
+  HIPCHK(hipMemcpyAsync(ctx->h_pinned + 3, rbegin + np, 8, hipMemcpyDeviceToHost, st));
+  if (card_out && np) HIPCHK(hipMemcpyAsync(card_out, pcard, np * 8, hipMemcpyDeviceToHost, st));
+  rc = stats_end(ctx, "k_pairwise", ntasks, 0);
+  if (rc) return rc;
+  const uint64_t nres = ctx->h_pinned[3];
+  ctx->last.result_containers = nres;
+  if (res) {
+    res->nc = nres;
+    *out = res;
+  }
+  return RB_OK;
+}
+
+int rbgpu_pairwise(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu_set *b, const uint32_t *a_idx,
+                   const uint32_t *b_idx, uint32_t npairs, rbgpu_set **out) {
+  if (!out) return fail(RB_EINVAL, "null out");
+  *out = nullptr;
+  return pairwise_impl(ctx, op, a, b, a_idx, b_idx, npairs, out, nullptr);
+}
+
+int rbgpu_pairwise_cardinality(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu_set *b, const uint32_t *a_idx,
+                               const uint32_t *b_idx, uint32_t npairs, uint64_t *out) {
+  if (!out && npairs) return fail(RB_EINVAL, "null out");
+  return pairwise_impl(ctx, op, a, b, a_idx, b_idx, npairs, nullptr, out);
+}
+
+// ---------------------------------------------------------------- wide
+int rbgpu_wide(rbgpu_ctx *ctx, int sem, const rbgpu_set *in, const uint32_t *members, uint32_t n, rbgpu_set **out) {
+  if (!out) return fail(RB_EINVAL, "null out");
+  *out = nullptr;
+  int rc = check_ctx(ctx);
+  if (rc) return rc;
+  if (!in || in->ctx != ctx) return fail(RB_EINVAL, "bad input set");
+  if (sem < RB_FAST_OR || sem > RB_NAIVE_AND_ITER) return fail(RB_EINVAL, "bad semantics %d", sem);
+  rc = ensure_h_begin(in);
+  if (rc) return rc;
+  std::vector<uint32_t> mem;
+  if (members) {
+    mem.assign(members, members + n);
+    for (uint32_t m : mem)
+      if (m >= in->nb) return fail(RB_EINVAL, "member %u out of range", m);
+  } else {
+    if (n > in->nb) return fail(RB_EINVAL, "n exceeds the set");
+    mem.resize(n);
+    for (uint32_t i = 0; i < n; ++i) mem[i] = i;
+  }
+  return wide_run(ctx, sem, in, mem, out);
+}
+
+int rbgpu_wide_cardinality(rbgpu_ctx *ctx, int op, const rbgpu_set *in, const uint32_t *members, uint32_t n,
+                           uint64_t *out) {
+  if (!out) return fail(RB_EINVAL, "null out");
+  if (op != RB_AND && op != RB_OR) return fail(RB_EINVAL, "wide cardinality supports AND and OR");
+  rbgpu_set *r = nullptr;
+  int rc = rbgpu_wide(ctx, op == RB_AND ? RB_WORKSHY_AND : RB_FAST_OR, in, members, n, &r);
+  if (rc) return rc;
+  rc = rbgpu_set_cardinalities(r, out);
+  rbgpu_set_free(r);
+  return rc;
+}
+
+// ---------------------------------------------------------------- generator
+int rbgpu_generate(rbgpu_ctx *ctx, int workload, uint32_t n, uint64_t seed, rbgpu_set **a, rbgpu_set **b) {
+  int rc = check_ctx(ctx);
+  if (rc) return rc;
+  if (!a) return fail(RB_EINVAL, "null out");
+  *a = nullptr;
+  if (b) *b = nullptr;
+  if (workload == RB_WL_FILTER_POSTING && !b) return fail(RB_EINVAL, "filter/posting workload needs two outputs");
+  return generate_sets(ctx, workload, n, seed, a, b);
+}
+
+} // extern "C"

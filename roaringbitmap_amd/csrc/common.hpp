@@ -1,0 +1,49 @@
+// common.hpp — shared host/device definitions of librbgpu (MI355X / gfx950).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "rbgpu.h"
+
+namespace rbg {
+
+constexpr int kArray = RB_ARRAY, kBitmap = RB_BITMAP, kRun = RB_RUN;
+constexpr uint8_t kEmpty = 0xFF;      // result slot whose container was dropped (isEmpty)
+constexpr int kMaxArray = 4096;       // ArrayContainer.DEFAULT_MAX_SIZE (ArrayContainer.java:27)
+constexpr int kSpan = 65536;          // values per container
+constexpr int kBitmapBytes = 8192;    // BitmapContainer payload
+constexpr int kRunArrayThreshold = 32; // RunContainer.andNot/xor array threshold (RunContainer.java:576,2412)
+
+// Read-only device view of one rbgpu_set.
+struct SetView {
+  const uint64_t *begin;  // [n_bitmaps+1]
+  const uint16_t *key;    // [n_cont]
+  const uint8_t *type;    // [n_cont]
+  const uint32_t *card;   // [n_cont]
+  const uint16_t *nruns;  // [n_cont]
+  const uint64_t *off;    // [n_cont]
+  const uint8_t *payload;
+};
+
+// Writable device view of a result set's container arrays.
+struct OutView {
+  uint16_t *key;
+  uint8_t *type;
+  uint32_t *card;
+  uint16_t *nruns;
+  uint64_t *off;
+};
+
+// One container-level work item of a pairwise call, in result (key-merged) order.
+struct Task {
+  int32_t ia;      // container index in A, -1 if none
+  int32_t ib;      // container index in B, -1 if none
+  uint64_t out;    // byte offset of the output slot in the result arena
+};
+
+__host__ __device__ inline uint64_t payload_bytes(int type, uint32_t card, uint32_t nruns) {
+  return type == kBitmap ? (uint64_t)kBitmapBytes : type == kArray ? 2ull * card : 4ull * nruns;
+}
+__host__ __device__ inline uint64_t round16(uint64_t x) { return (x + 15) & ~15ull; }
+
+} // namespace rbg

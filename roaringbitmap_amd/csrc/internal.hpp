@@ -1,0 +1,126 @@
+// internal.hpp — host-side object model shared by the librbgpu translation units.
+#pragma once
+#include <algorithm>
+#include <map>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "common.hpp"
+
+namespace rbg {
+
+int fail(int code, const char *fmt, ...);
+
+#define HIPCHK(x)                                                                                      \
+  do {                                                                                                 \
+    hipError_t e_ = (x);                                                                               \
+    if (e_ != hipSuccess) return ::rbg::fail(RB_EDEVICE, "%s failed: %s", #x, hipGetErrorString(e_));  \
+  } while (0)
+
+// Device allocation cache: a freed block is reused for requests in [size/2, size].
+struct DevPool {
+  std::multimap<size_t, void *> free_;
+  std::unordered_map<void *, size_t> size_;
+  ~DevPool() { clear(); }
+  void clear() {
+    for (auto &kv : free_) {
+      size_.erase(kv.second);
+      (void)hipFree(kv.second);
+    }
+    free_.clear();
+  }
+  hipError_t alloc(void **p, size_t n) {
+    n = std::max<size_t>((n + 255) & ~size_t(255), 256);
+    auto it = free_.lower_bound(n);
+    if (it != free_.end() && it->first <= 2 * n) {
+      *p = it->second;
+      free_.erase(it);
+      return hipSuccess;
+    }
+    hipError_t e = hipMalloc(p, n);
+    if (e != hipSuccess) {
+      (void)hipGetLastError();
+      clear();
+      e = hipMalloc(p, n);
+      if (e != hipSuccess) return e;
+    }
+    size_[*p] = n;
+    return hipSuccess;
+  }
+  void release(void *p) {
+    if (!p) return;
+    auto it = size_.find(p);
+    if (it != size_.end()) free_.emplace(it->second, p);
+  }
+};
+
+// Grow-only scratch region with bump allocation (reset by reserve()).
+struct Workspace {
+  uint8_t *base = nullptr;
+  size_t cap = 0, used = 0;
+  void destroy() {
+    if (base) (void)hipFree(base);
+    base = nullptr;
+    cap = used = 0;
+  }
+  hipError_t reserve(size_t n, hipStream_t st) {
+    used = 0;
+    if (n <= cap) return hipSuccess;
+    if (base) {
+      (void)hipStreamSynchronize(st);
+      (void)hipFree(base);
+      base = nullptr;
+    }
+    cap = std::max(n, cap * 2);
+    return hipMalloc((void **)&base, cap);
+  }
+  template <class T> T *take(size_t count) {
+    size_t bytes = (count * sizeof(T) + 255) & ~size_t(255);
+    T *p = reinterpret_cast<T *>(base + used);
+    used += bytes;
+    return p;
+  }
+};
+inline size_t aligned256(size_t b) { return (b + 255) & ~size_t(255); }
+
+} // namespace rbg
+
+struct rbgpu_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev[4] = {};   // [0] call start, [1]/[2] around the dominant kernel, [3] call end
+  rbg::DevPool pool;
+  rbg::Workspace ws_pairs, ws_tasks, ws_wide;
+  uint64_t *d_stats = nullptr;  // [4] algorithmic byte counters written by kernels
+  uint64_t *h_pinned = nullptr; // [16]
+  rb_stats last{};
+};
+
+struct rbgpu_set {
+  rbgpu_ctx *ctx = nullptr;
+  uint32_t nb = 0;
+  uint64_t nc = 0, payload_bytes = 0;
+  uint64_t *begin = nullptr;
+  uint16_t *key = nullptr;
+  uint8_t *type = nullptr;
+  uint32_t *card = nullptr;
+  uint16_t *nruns = nullptr;
+  uint64_t *off = nullptr;
+  uint8_t *payload = nullptr;
+  std::vector<uint64_t> h_begin; // host copy of the CSR, downloaded on demand
+  rbg::SetView view() const { return rbg::SetView{begin, key, type, card, nruns, off, payload}; }
+};
+
+namespace rbg {
+int set_alloc(rbgpu_ctx *ctx, rbgpu_set *s, uint32_t nb, uint64_t nc, uint64_t payload);
+void set_release(rbgpu_set *s);
+int ensure_h_begin(const rbgpu_set *s);
+// call accounting: zero the byte counters + record the start event / read everything back
+void stats_begin(rbgpu_ctx *ctx);
+int stats_end(rbgpu_ctx *ctx, const char *main_name, uint64_t tasks, uint64_t result_containers);
+// wide.hip
+int wide_run(rbgpu_ctx *ctx, int sem, const rbgpu_set *in, const std::vector<uint32_t> &members, rbgpu_set **out);
+// generate.hip
+int generate_sets(rbgpu_ctx *ctx, int workload, uint32_t n, uint64_t seed, rbgpu_set **a, rbgpu_set **b);
+} // namespace rbg

@@ -1,0 +1,84 @@
+// scan.hip — device exclusive prefix sums (u64) used to lay out variable-size outputs.
+#include "kernels.hpp"
+
+namespace rbg {
+
+constexpr int kScanThreads = 256;
+constexpr int kScanItems = 4; // per thread -> 1024 per block
+
+__device__ __forceinline__ uint64_t block_excl_scan(uint64_t v, uint64_t *sh, uint64_t &total) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint64_t incl = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    uint64_t t = (uint64_t)__shfl_up((unsigned long long)incl, d);
+    if (lane >= d) incl += t;
+  }
+  if (lane == 63) sh[wave] = incl;
+  __syncthreads();
+  uint64_t woff = 0;
+  for (int i = 0; i < wave; ++i) woff += sh[i];
+  total = sh[0] + sh[1] + sh[2] + sh[3];
+  __syncthreads();
+  return woff + incl - v;
+}
+
+__global__ __launch_bounds__(kScanThreads) void k_scan_partials(const uint64_t *in, uint64_t n, uint64_t *partials) {
+  __shared__ uint64_t sh[4];
+  const uint64_t base = (uint64_t)blockIdx.x * kScanThreads * kScanItems + threadIdx.x * kScanItems;
+  uint64_t s = 0;
+#pragma unroll
+  for (int i = 0; i < kScanItems; ++i)
+    if (base + i < n) s += in[base + i];
+  uint64_t total;
+  block_excl_scan(s, sh, total);
+  if (threadIdx.x == 0) partials[blockIdx.x] = total;
+}
+
+__global__ __launch_bounds__(kScanThreads) void k_scan_apply(const uint64_t *in, uint64_t n, const uint64_t *offs,
+                                                             uint64_t *out) {
+  __shared__ uint64_t sh[4];
+  const uint64_t base = (uint64_t)blockIdx.x * kScanThreads * kScanItems + threadIdx.x * kScanItems;
+  uint64_t v[kScanItems], s = 0;
+#pragma unroll
+  for (int i = 0; i < kScanItems; ++i) {
+    v[i] = base + i < n ? in[base + i] : 0;
+    s += v[i];
+  }
+  uint64_t total;
+  uint64_t run = block_excl_scan(s, sh, total) + (offs ? offs[blockIdx.x] : 0);
+#pragma unroll
+  for (int i = 0; i < kScanItems; ++i) {
+    if (base + i < n) out[base + i] = run;
+    run += v[i];
+  }
+  if (blockIdx.x == gridDim.x - 1 && threadIdx.x == kScanThreads - 1)
+    out[n] = (offs ? offs[blockIdx.x] : 0) + total;
+}
+
+// out[i] = sum(in[0..i)), out[n] = total.  `tmp` must hold scan_tmp_words(n) words.
+uint64_t scan_tmp_words(uint64_t n) {
+  const uint64_t per = kScanThreads * kScanItems;
+  uint64_t nb = (n + per - 1) / per;
+  if (nb <= 1) return 0;
+  return 2 * (nb + 1) + scan_tmp_words(nb);
+}
+
+void scan_exclusive(const uint64_t *in, uint64_t *out, uint64_t n, uint64_t *tmp, hipStream_t st) {
+  const uint64_t per = kScanThreads * kScanItems;
+  uint64_t nb = (n + per - 1) / per;
+  if (nb == 0) {
+    (void)hipMemsetAsync(out, 0, sizeof(uint64_t), st);
+    return;
+  }
+  if (nb == 1) {
+    k_scan_apply<<<1, kScanThreads, 0, st>>>(in, n, nullptr, out);
+    return;
+  }
+  uint64_t *partials = tmp, *poffs = tmp + (nb + 1);
+  k_scan_partials<<<(unsigned)nb, kScanThreads, 0, st>>>(in, n, partials);
+  scan_exclusive(partials, poffs, nb, tmp + 2 * (nb + 1), st);
+  k_scan_apply<<<(unsigned)nb, kScanThreads, 0, st>>>(in, n, poffs, out);
+}
+
+} // namespace rbg

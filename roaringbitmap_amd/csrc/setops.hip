@@ -1,0 +1,48 @@
+// setops.hip — small per-set utilities: per-bitmap cardinality, payload gather for downloads.
+#include "kernels.hpp"
+#include "wave.hpp"
+
+namespace rbg {
+
+// RoaringBitmap.getCardinality (sum of container cardinalities) — one wave per bitmap.
+__global__ __launch_bounds__(256) void k_bitmap_cards(SetView s, uint32_t nb, uint64_t *out) {
+  const uint64_t b = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= nb) return;
+  const int lane = lane_id();
+  uint64_t acc = 0;
+  for (uint64_t i = s.begin[b] + lane; i < s.begin[b + 1]; i += 64) acc += s.card[i];
+  acc = wave_sum_u64(acc);
+  if (lane == 0) out[b] = acc;
+}
+void launch_bitmap_cards(const SetView &s, uint32_t nbitmaps, uint64_t *out, hipStream_t st) {
+  if (!nbitmaps) return;
+  k_bitmap_cards<<<(nbitmaps + 3) / 4, 256, 0, st>>>(s, nbitmaps, out);
+}
+
+// Copy n payloads (sizes multiple of 16 after rounding) from src offsets to dst offsets.
+__global__ __launch_bounds__(256) void k_gather(const uint8_t *src, const uint64_t *soff, const uint64_t *bytes,
+                                                uint8_t *dst, const uint64_t *doff, uint64_t n) {
+  const uint64_t i = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (i >= n) return;
+  copy_payload(src + soff[i], dst + doff[i], bytes[i], lane_id());
+}
+void launch_gather(const uint8_t *src, const uint64_t *soff, const uint64_t *bytes, uint8_t *dst,
+                   const uint64_t *doff, uint64_t n, hipStream_t st) {
+  if (!n) return;
+  k_gather<<<(unsigned)((n + 3) / 4), 256, 0, st>>>(src, soff, bytes, dst, doff, n);
+}
+
+// Payload layout of generated / uploaded sets: Bitmaps first at 8 KiB strides, then the rest.
+__global__ __launch_bounds__(256) void k_layout(const uint64_t *bigflag, const uint64_t *bidx, const uint64_t *soff,
+                                                uint64_t small_base, uint64_t *off, uint64_t n) {
+  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  off[i] = bigflag[i] ? bidx[i] * (uint64_t)kBitmapBytes : small_base + soff[i];
+}
+void launch_layout(const uint64_t *bigflag, const uint64_t *bidx, const uint64_t *soff, uint64_t small_base,
+                   uint64_t *off, uint64_t n, hipStream_t st) {
+  if (!n) return;
+  k_layout<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(bigflag, bidx, soff, small_base, off, n);
+}
+
+} // namespace rbg

@@ -1,0 +1,353 @@
+// wave.hpp — wave64 building blocks for container algebra on gfx950.
+//
+// A 65536-bit container lives in the registers of ONE wave: lane L holds 16 u64 words
+// w[j], j = 2k + h (k = 0..7, h = 0..1), which is container word 128*k + 2*L + h.  With
+// this interleaving every 16-byte-per-lane access to a Bitmap payload (global or LDS) is one
+// fully coalesced 1 KiB wave instruction: uint4 index k*64 + L holds words 2*(k*64+L), +1.
+//
+// Array and Run operands are expanded into that register form through an 8 KiB per-wave LDS
+// scratch (Array: ds_or of value bits; Run: ds_xor of start / end+1 toggles, then an
+// in-register prefix-xor with a wave parity scan).  Results are classified exactly like the
+// reference (card c, maximal run count r -> Array / Bitmap / Run) and emitted in
+// RoaringFormatSpec payload form through the same scratch so global stores stay coalesced.
+#pragma once
+#include "common.hpp"
+
+namespace rbg {
+
+constexpr int kW = 16; // words per lane
+
+__device__ __forceinline__ void wave_lds_sync() {
+  // LDS ops of one wave execute in order; this keeps the compiler from reordering across it.
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & 63); }
+
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += (uint32_t)__shfl_xor((int)v, o);
+  return v;
+}
+__device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += (uint64_t)__shfl_xor((unsigned long long)v, o);
+  return v;
+}
+// inclusive prefix sum over lanes (fields packed in a u64 must not overflow)
+__device__ __forceinline__ uint64_t wave_scan_u64(uint64_t v, int lane) {
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    uint64_t t = (uint64_t)__shfl_up((unsigned long long)v, d);
+    if (lane >= d) v += t;
+  }
+  return v;
+}
+__device__ __forceinline__ uint32_t wave_xscan_xor(uint32_t v, int lane) { // inclusive xor-scan
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    uint32_t t = (uint32_t)__shfl_up((int)v, d);
+    if (lane >= d) v ^= t;
+  }
+  return v;
+}
+
+__device__ __forceinline__ uint64_t pack2(uint32_t lo, uint32_t hi) { return (uint64_t)lo | ((uint64_t)hi << 32); }
+
+// ---------------------------------------------------------------- loading operands
+__device__ __forceinline__ void load_bitmap(const uint8_t *p, uint64_t (&w)[kW], int lane) {
+  const uint4 *q = reinterpret_cast<const uint4 *>(p);
+  uint4 v[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) v[k] = q[k * 64 + lane];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    w[2 * k] = pack2(v[k].x, v[k].y);
+    w[2 * k + 1] = pack2(v[k].z, v[k].w);
+  }
+}
+__device__ __forceinline__ void lds_zero(uint32_t *s, int lane) {
+  uint4 *s4 = reinterpret_cast<uint4 *>(s);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) s4[k * 64 + lane] = make_uint4(0, 0, 0, 0);
+}
+__device__ __forceinline__ void lds_read_words(const uint32_t *s, uint64_t (&w)[kW], int lane) {
+  const uint4 *s4 = reinterpret_cast<const uint4 *>(s);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    uint4 v = s4[k * 64 + lane];
+    w[2 * k] = pack2(v.x, v.y);
+    w[2 * k + 1] = pack2(v.z, v.w);
+  }
+}
+
+// Sorted u16 array (payload 16-B aligned) -> register bitmap.  Each lane takes 8 consecutive
+// values per 16-B load (coalesced), folds them per 32-bit word and issues one ds_or per word.
+__device__ __forceinline__ void expand_array(const uint16_t *vals, int card, uint32_t *s,
+                                             uint64_t (&w)[kW], int lane) {
+  lds_zero(s, lane);
+  wave_lds_sync();
+  const uint4 *v4 = reinterpret_cast<const uint4 *>(vals);
+  const int nchunks = (card + 7) >> 3;
+  for (int c = lane; c < nchunks; c += 64) {
+    uint4 q = v4[c];
+    uint32_t x[8] = {q.x & 0xFFFF, q.x >> 16, q.y & 0xFFFF, q.y >> 16,
+                     q.z & 0xFFFF, q.z >> 16, q.w & 0xFFFF, q.w >> 16};
+    const int n = min(8, card - 8 * c);
+    uint32_t cw = x[0] >> 5, acc = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      if (i < n) {
+        uint32_t wi = x[i] >> 5;
+        if (wi != cw) {
+          atomicOr(&s[cw], acc);
+          cw = wi;
+          acc = 0;
+        }
+        acc |= 1u << (x[i] & 31);
+      }
+    }
+    atomicOr(&s[cw], acc);
+  }
+  wave_lds_sync();
+  lds_read_words(s, w, lane);
+  wave_lds_sync();
+}
+
+__device__ __forceinline__ uint64_t prefix_xor64(uint64_t x) {
+  x ^= x << 1;
+  x ^= x << 2;
+  x ^= x << 4;
+  x ^= x << 8;
+  x ^= x << 16;
+  x ^= x << 32;
+  return x;
+}
+
+// Run list ((start, len-1) u16 pairs) -> register bitmap: toggle bit `start` and bit
+// `start+len` (end+1) of every run into LDS, then membership = prefix-xor of the toggles.
+__device__ __forceinline__ void expand_runs(const uint16_t *runs, int nruns, uint32_t *s,
+                                            uint64_t (&w)[kW], int lane) {
+  lds_zero(s, lane);
+  wave_lds_sync();
+  const uint32_t *r32 = reinterpret_cast<const uint32_t *>(runs);
+  for (int i = lane; i < nruns; i += 64) {
+    uint32_t q = r32[i];
+    uint32_t st = q & 0xFFFF, e1 = st + (q >> 16) + 1;
+    atomicXor(&s[st >> 5], 1u << (st & 31));
+    if (e1 < (uint32_t)kSpan) atomicXor(&s[e1 >> 5], 1u << (e1 & 31));
+  }
+  wave_lds_sync();
+  uint64_t t[kW];
+  lds_read_words(s, t, lane);
+  wave_lds_sync();
+  uint32_t q = 0, p0 = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    uint32_t a = __popcll(t[2 * k]) & 1, b = __popcll(t[2 * k + 1]) & 1;
+    q |= (a ^ b) << k;
+    p0 |= a << k;
+  }
+  const uint32_t incl = wave_xscan_xor(q, lane);
+  const uint32_t excl = incl ^ q;
+  const uint32_t tot = (uint32_t)__shfl((int)incl, 63);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    uint32_t rowc = __popc(tot & ((1u << k) - 1)) & 1;
+    uint32_t c0 = rowc ^ ((excl >> k) & 1);
+    uint32_t c1 = c0 ^ ((p0 >> k) & 1);
+    w[2 * k] = prefix_xor64(t[2 * k]) ^ (c0 ? ~0ull : 0ull);
+    w[2 * k + 1] = prefix_xor64(t[2 * k + 1]) ^ (c1 ? ~0ull : 0ull);
+  }
+}
+
+// Any container -> register bitmap.
+__device__ __forceinline__ void load_container(int type, const uint8_t *p, uint32_t card, uint32_t nruns,
+                                               uint32_t *s, uint64_t (&w)[kW], int lane) {
+  if (type == kBitmap) load_bitmap(p, w, lane);
+  else if (type == kArray) expand_array(reinterpret_cast<const uint16_t *>(p), (int)card, s, w, lane);
+  else expand_runs(reinterpret_cast<const uint16_t *>(p), (int)nruns, s, w, lane);
+}
+
+// ---------------------------------------------------------------- metrics
+// "top bit of the previous word" for every word of this lane, as per-row masks.
+struct Neigh {
+  uint32_t prev_top_h0; // bit k: top bit of the word before (k, lane, 0)
+  uint32_t next_bot_h1; // bit k: bottom bit of the word after (k, lane, 1)
+};
+__device__ __forceinline__ Neigh neighbours(const uint64_t (&w)[kW], int lane) {
+  uint32_t top1 = 0, bot0 = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    top1 |= (uint32_t)(w[2 * k + 1] >> 63) << k;
+    bot0 |= (uint32_t)(w[2 * k] & 1) << k;
+  }
+  uint32_t up = (uint32_t)__shfl_up((int)top1, 1);
+  uint32_t last = (uint32_t)__shfl((int)top1, 63);
+  uint32_t dn = (uint32_t)__shfl_down((int)bot0, 1);
+  uint32_t first = (uint32_t)__shfl((int)bot0, 0);
+  Neigh n;
+  n.prev_top_h0 = lane ? up : ((last << 1) & 0xFE);
+  n.next_bot_h1 = lane < 63 ? dn : ((first >> 1) & 0x7F);
+  return n;
+}
+__device__ __forceinline__ uint64_t run_starts(const uint64_t (&w)[kW], const Neigh &n, int j) {
+  const int k = j >> 1;
+  uint64_t prev = (j & 1) ? (w[j - 1] >> 63) : (uint64_t)((n.prev_top_h0 >> k) & 1);
+  return w[j] & ~((w[j] << 1) | prev);
+}
+__device__ __forceinline__ uint64_t run_ends(const uint64_t (&w)[kW], const Neigh &n, int j) {
+  const int k = j >> 1;
+  uint64_t next = (j & 1) ? (uint64_t)((n.next_bot_h1 >> k) & 1) : (w[j + 1] & 1);
+  return w[j] & ~((w[j] >> 1) | (next << 63));
+}
+__device__ __forceinline__ uint32_t lane_card(const uint64_t (&w)[kW]) {
+  uint32_t c = 0;
+#pragma unroll
+  for (int j = 0; j < kW; ++j) c += __popcll(w[j]);
+  return c;
+}
+// cardinality (and maximal-run count if want_runs) of the register bitmap, wave-uniform.
+__device__ __forceinline__ void metrics(const uint64_t (&w)[kW], int lane, bool want_runs, int &card,
+                                        int &runs) {
+  uint32_t c = lane_card(w);
+  uint32_t r = 0;
+  if (want_runs) {
+    Neigh n = neighbours(w, lane);
+#pragma unroll
+    for (int j = 0; j < kW; ++j) r += __popcll(run_starts(w, n, j));
+  }
+  uint64_t t = wave_sum_u64(pack2(c, r));
+  card = (int)(uint32_t)t;
+  runs = (int)(t >> 32);
+}
+
+// ---------------------------------------------------------------- type rules
+// AB(c): BitmapContainer.and/xor/andNot, RunContainer.toBitmapOrArrayContainer (:2300-2323)
+__device__ __forceinline__ int type_ab(int c) { return c <= kMaxArray ? kArray : kBitmap; }
+// EFF(c,r): RunContainer.toEfficientContainer (:2326-2335), ties go to Run
+__device__ __forceinline__ int type_eff(int c, int r) {
+  return 2 + 4 * r <= min(kBitmapBytes, 2 * c + 2) ? kRun : type_ab(c);
+}
+// LR(c): BitmapContainer.repairAfterLazy (:1214-1224)
+__device__ __forceinline__ int type_lr(int c) {
+  return c <= kMaxArray ? kArray : (c == kSpan ? kRun : kBitmap);
+}
+// runOptimize on a freshly built container (ArrayContainer.java:1085-1099,
+// BitmapContainer.java:1227-1246): natural AB type, then Run iff strictly smaller.
+__device__ __forceinline__ int type_runopt(int c, int r) {
+  if (c <= kMaxArray) return 2 * c > 2 + 4 * r ? kRun : kArray;
+  return kBitmapBytes > 2 + 4 * r ? kRun : kBitmap;
+}
+
+// ---------------------------------------------------------------- emission
+// Writes the container payload for `type` at `out` (16-B aligned slot); returns payload bytes.
+// `s` is the wave's 8 KiB LDS scratch (free on entry).
+__device__ __forceinline__ uint32_t emit_container(int type, const uint64_t (&w)[kW], int card, int runs,
+                                                   uint8_t *out, uint32_t *s, int lane) {
+  if (type == kBitmap) {
+    uint4 *o = reinterpret_cast<uint4 *>(out);
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      o[k * 64 + lane] = make_uint4((uint32_t)w[2 * k], (uint32_t)(w[2 * k] >> 32),
+                                    (uint32_t)w[2 * k + 1], (uint32_t)(w[2 * k + 1] >> 32));
+    return kBitmapBytes;
+  }
+  uint16_t *s16 = reinterpret_cast<uint16_t *>(s);
+  if (type == kArray) {
+    // rank of the first value of every word: packed per-row (16-bit fields) wave scan
+    uint32_t n[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) n[k] = __popcll(w[2 * k]) + __popcll(w[2 * k + 1]);
+    const uint64_t P0 = (uint64_t)n[0] | ((uint64_t)n[1] << 16) | ((uint64_t)n[2] << 32) | ((uint64_t)n[3] << 48);
+    const uint64_t P1 = (uint64_t)n[4] | ((uint64_t)n[5] << 16) | ((uint64_t)n[6] << 32) | ((uint64_t)n[7] << 48);
+    const uint64_t S0 = wave_scan_u64(P0, lane), S1 = wave_scan_u64(P1, lane);
+    const uint64_t E0 = S0 - P0, E1 = S1 - P1;
+    const uint64_t T0 = (uint64_t)__shfl((unsigned long long)S0, 63);
+    const uint64_t T1 = (uint64_t)__shfl((unsigned long long)S1, 63);
+    uint32_t rowoff = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const uint64_t E = k < 4 ? E0 : E1, T = k < 4 ? T0 : T1;
+      const int sh = 16 * (k & 3);
+      uint32_t pos = rowoff + (uint32_t)((E >> sh) & 0xFFFF);
+      rowoff += (uint32_t)((T >> sh) & 0xFFFF);
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        uint64_t x = w[2 * k + h];
+        const uint32_t base = (uint32_t)(128 * k + 2 * lane + h) << 6;
+        while (x) {
+          s16[pos++] = (uint16_t)(base + __builtin_ctzll(x));
+          x &= x - 1;
+        }
+      }
+    }
+    wave_lds_sync();
+    const uint32_t bytes = 2u * (uint32_t)card;
+    const uint4 *s4 = reinterpret_cast<const uint4 *>(s);
+    uint4 *o = reinterpret_cast<uint4 *>(out);
+    for (uint32_t i = lane; i * 16 < bytes; i += 64) o[i] = s4[i];
+    wave_lds_sync();
+    return bytes;
+  }
+  // Run: S[rank] = start, E[rank] = end; the i-th end closes the i-th run.
+  Neigh nb = neighbours(w, lane);
+  uint32_t ns[8];
+  uint64_t st[kW];
+#pragma unroll
+  for (int j = 0; j < kW; ++j) st[j] = run_starts(w, nb, j);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) ns[k] = __popcll(st[2 * k]) + __popcll(st[2 * k + 1]);
+  const uint64_t P0 = (uint64_t)ns[0] | ((uint64_t)ns[1] << 16) | ((uint64_t)ns[2] << 32) | ((uint64_t)ns[3] << 48);
+  const uint64_t P1 = (uint64_t)ns[4] | ((uint64_t)ns[5] << 16) | ((uint64_t)ns[6] << 32) | ((uint64_t)ns[7] << 48);
+  const uint64_t S0 = wave_scan_u64(P0, lane), S1 = wave_scan_u64(P1, lane);
+  const uint64_t E0 = S0 - P0, E1 = S1 - P1;
+  const uint64_t T0 = (uint64_t)__shfl((unsigned long long)S0, 63);
+  const uint64_t T1 = (uint64_t)__shfl((unsigned long long)S1, 63);
+  uint16_t *S = s16, *E = s16 + 2048;
+  uint32_t rowoff = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const uint64_t Ex = k < 4 ? E0 : E1, T = k < 4 ? T0 : T1;
+    const int sh = 16 * (k & 3);
+    uint32_t sp = rowoff + (uint32_t)((Ex >> sh) & 0xFFFF);
+    rowoff += (uint32_t)((T >> sh) & 0xFFFF);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int j = 2 * k + h;
+      const uint32_t open = (uint32_t)(h ? (w[j - 1] >> 63) : ((nb.prev_top_h0 >> k) & 1));
+      uint32_t ep = sp - open;
+      const uint32_t base = (uint32_t)(128 * k + 2 * lane + h) << 6;
+      uint64_t x = st[j];
+      while (x) {
+        S[sp++] = (uint16_t)(base + __builtin_ctzll(x));
+        x &= x - 1;
+      }
+      uint64_t y = run_ends(w, nb, j);
+      while (y) {
+        E[ep++] = (uint16_t)(base + __builtin_ctzll(y));
+        y &= y - 1;
+      }
+    }
+  }
+  wave_lds_sync();
+  uint32_t *o = reinterpret_cast<uint32_t *>(out);
+  for (int i = lane; i < runs; i += 64) {
+    uint32_t a = S[i], b = E[i];
+    o[i] = a | ((b - a) << 16);
+  }
+  wave_lds_sync();
+  return 4u * (uint32_t)runs;
+}
+
+// Copy a payload (multiple of 16 bytes after rounding; slots are 16-B padded).
+__device__ __forceinline__ void copy_payload(const uint8_t *src, uint8_t *dst, uint64_t bytes, int lane) {
+  const uint4 *a = reinterpret_cast<const uint4 *>(src);
+  uint4 *b = reinterpret_cast<uint4 *>(dst);
+  const uint64_t n = (bytes + 15) >> 4;
+  for (uint64_t i = lane; i < n; i += 64) b[i] = a[i];
+}
+
+} // namespace rbg

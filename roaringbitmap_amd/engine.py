@@ -1,0 +1,298 @@
+"""Device-resident engine objects over the C ABI: Context (one HIP stream + workspaces on
+one MI355X) and DeviceSet (a batch of bitmaps in SoA form in HBM).
+
+Host SoA helpers build canonical containers from values the way the reference does
+(RoaringBitmap.bitmapOf: ArrayContainer up to 4096 values, BitmapContainer beyond,
+RoaringBitmap.java:498-570; runOptimize rules ArrayContainer.java:1085-1099,
+BitmapContainer.java:1227-1246).
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass, field
+from typing import List, Optional, Sequence
+
+import numpy as np
+
+from . import _lib as L
+
+
+@dataclass
+class HostSoA:
+    """A batch of bitmaps on the host, same layout as rb_soa."""
+    begin: np.ndarray                       # uint64 [nb+1]
+    key: np.ndarray                         # uint16 [nc]
+    type: np.ndarray                        # uint8  [nc]
+    card: np.ndarray                        # uint32 [nc]
+    nruns: np.ndarray                       # uint16 [nc]
+    offset: np.ndarray                      # uint64 [nc]
+    payload: np.ndarray = field(repr=False)  # uint8
+
+    @property
+    def n_bitmaps(self) -> int:
+        return len(self.begin) - 1
+
+    @property
+    def n_containers(self) -> int:
+        return len(self.key)
+
+    def container_payload(self, i: int) -> np.ndarray:
+        t, c, r = int(self.type[i]), int(self.card[i]), int(self.nruns[i])
+        n = 8192 if t == L.BITMAP else (2 * c if t == L.ARRAY else 4 * r)
+        o = int(self.offset[i])
+        return self.payload[o:o + n]
+
+    def values(self, b: int) -> np.ndarray:
+        """All uint32 values of bitmap b (ascending)."""
+        out = []
+        for i in range(int(self.begin[b]), int(self.begin[b + 1])):
+            hi = np.uint32(int(self.key[i]) << 16)
+            p = self.container_payload(i)
+            t = int(self.type[i])
+            if t == L.ARRAY:
+                low = p.view(np.uint16).astype(np.uint32)
+            elif t == L.BITMAP:
+                bits = np.unpackbits(p, bitorder="little")
+                low = np.nonzero(bits)[0].astype(np.uint32)
+            else:
+                rl = p.view(np.uint16).reshape(-1, 2).astype(np.uint32)
+                low = np.concatenate([np.arange(s, s + l + 1, dtype=np.uint32) for s, l in rl]) if len(rl) else \
+                    np.zeros(0, np.uint32)
+            out.append(low | hi)
+        return np.concatenate(out) if out else np.zeros(0, np.uint32)
+
+    def as_rb_soa(self) -> L.RbSoa:
+        s = L.RbSoa()
+        s.n_bitmaps = self.n_bitmaps
+        s.n_containers = self.n_containers
+        s.payload_bytes = len(self.payload)
+        for name in ("begin", "key", "type", "card", "nruns", "offset", "payload"):
+            arr = getattr(self, name)
+            assert arr.flags["C_CONTIGUOUS"]
+            setattr(s, name, arr.ctypes.data if arr.size else None)
+        return s
+
+
+def _runs_of_sorted(low: np.ndarray):
+    if len(low) == 0:
+        return np.zeros((0, 2), np.uint16)
+    brk = np.nonzero(np.diff(low.astype(np.int64)) != 1)[0]
+    starts = np.concatenate([[0], brk + 1])
+    ends = np.concatenate([brk, [len(low) - 1]])
+    s = low[starts].astype(np.uint32)
+    e = low[ends].astype(np.uint32)
+    return np.stack([s, e - s], axis=1).astype(np.uint16)
+
+
+def soa_from_values(bitmaps: Sequence[np.ndarray], run_optimize: bool = False) -> HostSoA:
+    """Canonical containers of each value list (bitmapOf semantics, optional runOptimize)."""
+    begin = [0]
+    key, typ, card, nruns, offset = [], [], [], [], []
+    chunks = []
+    pos = 0
+    for vals in bitmaps:
+        v = np.unique(np.asarray(vals, dtype=np.uint32))
+        hi = (v >> 16).astype(np.uint16)
+        lo = (v & 0xFFFF).astype(np.uint16)
+        cuts = np.nonzero(np.diff(hi.astype(np.int64)))[0] + 1
+        for part_hi, part_lo in zip(np.split(hi, cuts), np.split(lo, cuts)):
+            if len(part_lo) == 0:
+                continue
+            c = len(part_lo)
+            runs = _runs_of_sorted(part_lo)
+            r = len(runs)
+            t = L.ARRAY if c <= 4096 else L.BITMAP
+            if run_optimize:
+                if t == L.ARRAY and 2 * c > 2 + 4 * r:
+                    t = L.RUN
+                elif t == L.BITMAP and 8192 > 2 + 4 * r:
+                    t = L.RUN
+            if t == L.ARRAY:
+                data = part_lo.tobytes()
+            elif t == L.BITMAP:
+                bits = np.zeros(65536, np.uint8)
+                bits[part_lo] = 1
+                data = np.packbits(bits, bitorder="little").tobytes()
+            else:
+                data = runs.tobytes()
+            key.append(int(part_hi[0]))
+            typ.append(t)
+            card.append(c)
+            nruns.append(r if t == L.RUN else 0)
+            offset.append(pos)
+            pad = (-len(data)) % 16
+            chunks.append(data + b"\0" * pad)
+            pos += len(data) + pad
+        begin.append(len(key))
+    payload = np.frombuffer(b"".join(chunks) or b"\0" * 16, dtype=np.uint8).copy()
+    return HostSoA(np.array(begin, np.uint64), np.array(key, np.uint16), np.array(typ, np.uint8),
+                   np.array(card, np.uint32), np.array(nruns, np.uint16), np.array(offset, np.uint64), payload)
+
+
+class DeviceSet:
+    """A batch of bitmaps resident in HBM (rbgpu_set*).  Freed on close() / GC."""
+
+    def __init__(self, ctx: "Context", handle: int):
+        self.ctx = ctx
+        self.h = C.c_void_p(handle)
+
+    def close(self):
+        if self.h and self.h.value:
+            L.lib().rbgpu_set_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __len__(self) -> int:
+        return int(L.lib().rbgpu_set_bitmap_count(self.h))
+
+    @property
+    def n_containers(self) -> int:
+        return int(L.lib().rbgpu_set_container_count(self.h))
+
+    def cardinalities(self) -> np.ndarray:
+        out = np.zeros(len(self), np.uint64)
+        L.check(L.lib().rbgpu_set_cardinalities(self.h, out.ctypes.data_as(L._U64P)))
+        return out
+
+    def serialized_sizes(self) -> np.ndarray:
+        out = np.zeros(len(self), np.uint64)
+        L.check(L.lib().rbgpu_set_serialized_sizes(self.h, out.ctypes.data_as(L._U64P)))
+        return out
+
+    def serialize(self, first: int = 0, count: Optional[int] = None) -> List[bytes]:
+        count = len(self) - first if count is None else count
+        if count == 0:
+            return []
+        sizes = self.serialized_sizes()[first:first + count]
+        total = int(sizes.sum())
+        buf = C.create_string_buffer(max(total, 1))
+        offs = np.zeros(count + 1, np.uint64)
+        L.check(L.lib().rbgpu_set_serialize(self.h, first, count, buf, total, offs.ctypes.data_as(L._U64P)))
+        raw = buf.raw
+        return [raw[int(offs[i]):int(offs[i + 1])] for i in range(count)]
+
+    def download(self, first: int = 0, count: Optional[int] = None) -> HostSoA:
+        count = len(self) - first if count is None else count
+        q = L.RbSoa()
+        L.check(L.lib().rbgpu_set_download(self.h, first, count, C.byref(q)))
+        nc, nbytes = int(q.n_containers), int(q.payload_bytes)
+        h = HostSoA(np.zeros(count + 1, np.uint64), np.zeros(nc, np.uint16), np.zeros(nc, np.uint8),
+                    np.zeros(nc, np.uint32), np.zeros(nc, np.uint16), np.zeros(nc, np.uint64),
+                    np.zeros(max(nbytes, 16), np.uint8))
+        s = h.as_rb_soa()
+        s.n_containers, s.payload_bytes = max(nc, 0), len(h.payload)
+        if nc == 0:  # still need a non-null key pointer to mean "fill"
+            h.begin[:] = 0
+            return h
+        L.check(L.lib().rbgpu_set_download(self.h, first, count, C.byref(s)))
+        return h
+
+
+def _idx(arr):
+    if arr is None:
+        return None, None
+    a = np.ascontiguousarray(np.asarray(arr, dtype=np.uint32))
+    return a, a.ctypes.data_as(L._U32P)
+
+
+class Context:
+    """One MI355X: a HIP stream, workspaces and an allocation cache (rbgpu_ctx*)."""
+
+    def __init__(self, device: int = 0):
+        h = C.c_void_p()
+        L.check(L.lib().rbgpu_open(device, C.byref(h)))
+        self.h = h
+        self.device = device
+
+    def close(self):
+        if self.h and self.h.value:
+            L.lib().rbgpu_close(self.h)
+            self.h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    @staticmethod
+    def device_count() -> int:
+        return int(L.lib().rbgpu_device_count())
+
+    def synchronize(self):
+        L.check(L.lib().rbgpu_synchronize(self.h))
+
+    def stats(self) -> dict:
+        s = L.RbStats()
+        L.check(L.lib().rbgpu_get_stats(self.h, C.byref(s)))
+        return {k: (getattr(s, k).decode() if k == "main_kernel" else getattr(s, k)) for k, _ in s._fields_}
+
+    # ---- sets
+    def upload_serialized(self, blobs: Sequence[bytes]) -> DeviceSet:
+        n = len(blobs)
+        arr = (C.c_char_p * max(n, 1))(*blobs)
+        lens = np.array([len(b) for b in blobs] or [0], np.uint64)
+        out = C.c_void_p()
+        L.check(L.lib().rbgpu_set_from_serialized(self.h, arr, lens.ctypes.data_as(L._U64P), n, C.byref(out)))
+        return DeviceSet(self, out.value)
+
+    def upload_soa(self, soa: HostSoA) -> DeviceSet:
+        s = soa.as_rb_soa()
+        out = C.c_void_p()
+        L.check(L.lib().rbgpu_set_from_soa(self.h, C.byref(s), C.byref(out)))
+        return DeviceSet(self, out.value)
+
+    def upload_values(self, bitmaps: Sequence[np.ndarray], run_optimize: bool = False) -> DeviceSet:
+        return self.upload_soa(soa_from_values(bitmaps, run_optimize))
+
+    def generate(self, workload: int, n: int, seed: int = 42):
+        a, b = C.c_void_p(), C.c_void_p()
+        L.check(L.lib().rbgpu_generate(self.h, workload, n, seed, C.byref(a), C.byref(b)))
+        return DeviceSet(self, a.value), (DeviceSet(self, b.value) if b.value else None)
+
+    # ---- algebra
+    def pairwise(self, op: int, a: DeviceSet, b: DeviceSet, a_idx=None, b_idx=None, npairs=None) -> DeviceSet:
+        ai, ap = _idx(a_idx)
+        bi, bp = _idx(b_idx)
+        n = npairs if npairs is not None else (len(ai) if ai is not None else min(len(a), len(b)))
+        out = C.c_void_p()
+        L.check(L.lib().rbgpu_pairwise(self.h, op, a.h, b.h, ap, bp, n, C.byref(out)))
+        return DeviceSet(self, out.value)
+
+    def pairwise_cardinality(self, op: int, a: DeviceSet, b: DeviceSet, a_idx=None, b_idx=None,
+                             npairs=None) -> np.ndarray:
+        ai, ap = _idx(a_idx)
+        bi, bp = _idx(b_idx)
+        n = npairs if npairs is not None else (len(ai) if ai is not None else min(len(a), len(b)))
+        out = np.zeros(max(n, 1), np.uint64)
+        L.check(L.lib().rbgpu_pairwise_cardinality(self.h, op, a.h, b.h, ap, bp, n, out.ctypes.data_as(L._U64P)))
+        return out[:n]
+
+    def wide(self, sem: int, s: DeviceSet, members=None) -> DeviceSet:
+        mi, mp = _idx(members)
+        n = len(mi) if mi is not None else len(s)
+        out = C.c_void_p()
+        L.check(L.lib().rbgpu_wide(self.h, sem, s.h, mp, n, C.byref(out)))
+        return DeviceSet(self, out.value)
+
+    def wide_cardinality(self, op: int, s: DeviceSet, members=None) -> int:
+        mi, mp = _idx(members)
+        n = len(mi) if mi is not None else len(s)
+        out = C.c_uint64()
+        L.check(L.lib().rbgpu_wide_cardinality(self.h, op, s.h, mp, n, C.byref(out)))
+        return int(out.value)
+
+
+_default: Optional[Context] = None
+
+
+def default_context() -> Context:
+    global _default
+    if _default is None:
+        _default = Context(0)
+    return _default

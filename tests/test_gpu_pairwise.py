@@ -1,0 +1,126 @@
+"""Parity of the MI355X pairwise path (librbgpu k_pairwise) with the oracle: identical
+RoaringFormatSpec bytes for every result, identical cardinalities."""
+import numpy as np
+import pytest
+
+from datasets import DATASETS, EXPECTED, fixture_bytes, load_realdata, synthetic_bitmaps
+
+pytestmark = pytest.mark.gpu
+OPS = {"AND": 0, "OR": 1, "XOR": 2, "ANDNOT": 3}
+
+
+def _ref_list(oracle, blobs):
+    return [oracle.RefBitmap.deserialize(b) for b in blobs]
+
+
+@pytest.mark.parametrize("name", DATASETS)
+@pytest.mark.parametrize("run_optimize", [False, True])
+def test_realdata_pairwise_bytes_and_golden(ctx, oracle, name, run_optimize):
+    vals = load_realdata(name)
+    s = ctx.upload_values(vals, run_optimize=run_optimize)
+    refs = _ref_list(oracle, s.serialize())
+    n = len(vals) - 1
+    a_idx = np.arange(n, dtype=np.uint32)
+    b_idx = a_idx + 1
+    for opname, op in OPS.items():
+        out = ctx.pairwise(op, s, s, a_idx, b_idx)
+        got = out.serialize()
+        for k in range(n):
+            assert got[k] == oracle.op(op, refs[k], refs[k + 1]).serialize(), (opname, k)
+        assert int(out.cardinalities().sum()) == EXPECTED[name][opname]
+        cards = ctx.pairwise_cardinality(op, s, s, a_idx, b_idx)
+        assert int(cards.sum()) == EXPECTED[name][opname]
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+@pytest.mark.parametrize("opname", list(OPS))
+def test_synthetic_all_type_pairs(ctx, oracle, seed, opname):
+    op = OPS[opname]
+    bms = synthetic_bitmaps(80, seed=seed)
+    for ro in (False, True):
+        s = ctx.upload_values(bms, run_optimize=ro)
+        refs = _ref_list(oracle, s.serialize())
+        rng = np.random.default_rng(seed + 100)
+        a_idx = rng.integers(0, len(bms), size=300).astype(np.uint32)
+        b_idx = rng.integers(0, len(bms), size=300).astype(np.uint32)
+        out = ctx.pairwise(op, s, s, a_idx, b_idx)
+        got = out.serialize()
+        cards = ctx.pairwise_cardinality(op, s, s, a_idx, b_idx)
+        for i in range(len(a_idx)):
+            ref = oracle.op(op, refs[a_idx[i]], refs[b_idx[i]])
+            assert got[i] == ref.serialize(), (opname, ro, i)
+            assert int(cards[i]) == oracle.op_cardinality(op, refs[a_idx[i]], refs[b_idx[i]])
+
+
+def test_two_sets_and_identity_pairs(ctx, oracle):
+    a_vals = synthetic_bitmaps(50, seed=21)
+    b_vals = synthetic_bitmaps(50, seed=22)
+    a = ctx.upload_values(a_vals, run_optimize=True)
+    b = ctx.upload_values(b_vals, run_optimize=False)
+    ra, rbs = _ref_list(oracle, a.serialize()), _ref_list(oracle, b.serialize())
+    for op in OPS.values():
+        got = ctx.pairwise(op, a, b).serialize()
+        assert got == [oracle.op(op, ra[i], rbs[i]).serialize() for i in range(50)]
+
+
+def test_fixtures_through_the_device(ctx, oracle):
+    w, wo = fixture_bytes("bitmapwithruns.bin"), fixture_bytes("bitmapwithoutruns.bin")
+    s = ctx.upload_serialized([w, wo])
+    assert s.serialize() == [w, wo]
+    assert list(s.cardinalities()) == [200100, 200100]
+    refs = _ref_list(oracle, [w, wo])
+    for op in OPS.values():
+        got = ctx.pairwise(op, s, s, [0, 1, 0], [1, 0, 0]).serialize()
+        assert got == [oracle.op(op, refs[i], refs[j]).serialize() for i, j in ((0, 1), (1, 0), (0, 0))]
+
+
+def test_empty_bitmaps_and_empty_batch(ctx, oracle):
+    bms = [np.zeros(0, np.uint32), np.array([1, 2, 3], np.uint32), np.zeros(0, np.uint32)]
+    s = ctx.upload_values(bms)
+    refs = _ref_list(oracle, s.serialize())
+    for op in OPS.values():
+        got = ctx.pairwise(op, s, s, [0, 0, 1, 2], [0, 1, 0, 2]).serialize()
+        assert got == [oracle.op(op, refs[i], refs[j]).serialize() for i, j in ((0, 0), (0, 1), (1, 0), (2, 2))]
+        empty = ctx.pairwise(op, s, s, np.zeros(0, np.uint32), np.zeros(0, np.uint32))
+        assert len(empty) == 0
+
+
+def test_bad_inputs_raise(ctx):
+    import roaringbitmap_amd as rb
+    for i in range(1, 8):
+        with pytest.raises(IOError):
+            ctx.upload_serialized([fixture_bytes(f"crashproneinput{i}.bin")])
+    s = ctx.upload_values([np.array([1], np.uint32)])
+    with pytest.raises(ValueError):
+        ctx.pairwise(rb.AND, s, s, [5], [0])
+    # non-canonical run list (two touching runs) is rejected (RB_EINVAL)
+    soa = rb.soa_from_values([np.array([1, 2, 3], np.uint32)], run_optimize=True)
+    soa.type[0] = rb.RUN
+    soa.nruns[0] = 2
+    soa.payload[:8] = np.array([1, 0, 2, 1], np.uint16).view(np.uint8)
+    soa.card[0] = 3
+    with pytest.raises(ValueError):
+        ctx.upload_soa(soa)
+
+
+def test_generated_filter_posting_sample_parity(ctx, oracle):
+    """Device-generated config-2 data: a downloaded sample must match the oracle byte for byte."""
+    import roaringbitmap_amd as rb
+    a, b = ctx.generate(rb.WL_FILTER_POSTING, 3000, seed=42)
+    assert len(a) == 3000 and len(b) == 3000
+    out = ctx.pairwise(rb.AND, a, b)
+    ra = _ref_list(oracle, a.serialize(0, 400))
+    rbs = _ref_list(oracle, b.serialize(0, 400))
+    got = out.serialize(0, 400)
+    for i in range(400):
+        assert got[i] == oracle.op(rb.AND, ra[i], rbs[i]).serialize()
+    # generated containers are canonical and runOptimize-stable
+    h = a.download(0, 400)
+    for i in range(h.n_containers):
+        t, c, r = int(h.type[i]), int(h.card[i]), int(h.nruns[i])
+        if t == rb.ARRAY:
+            assert 1 <= c <= 4096
+        elif t == rb.BITMAP:
+            assert c > 4096
+        else:
+            assert 2 + 4 * r < min(8192, 2 * c)

@@ -1,0 +1,88 @@
+"""The CPU oracle against the reference's own known answers (no GPU needed)."""
+import numpy as np
+import pytest
+
+from datasets import DATASETS, EXPECTED, fixture_bytes, load_realdata
+
+OPS = ["AND", "OR", "XOR", "ANDNOT"]
+
+
+@pytest.mark.parametrize("name", DATASETS)
+@pytest.mark.parametrize("run_optimize", [False, True])
+def test_realdata_golden_cardinalities(oracle, name, run_optimize):
+    # RealDataBenchmark{And,Or,Xor,AndNot}Test: sum over consecutive pairs (k, k+1);
+    # RealDataBenchmarkWide{OrNaive,AndNaive}Test: wide aggregate over all bitmaps.
+    R = oracle
+    bms = [R.RefBitmap.of(v) for v in load_realdata(name)]
+    if run_optimize:  # the ROARING_WITH_RUN variant (BitmapFactory: bitmapOf + runOptimize)
+        for b in bms:
+            b.run_optimize()
+    for opname in OPS:
+        op = getattr(R, opname)
+        total = sum(R.op(op, bms[k], bms[k + 1]).cardinality() for k in range(len(bms) - 1))
+        assert total == EXPECTED[name][opname]
+        total_c = sum(R.op_cardinality(op, bms[k], bms[k + 1]) for k in range(len(bms) - 1))
+        assert total_c == EXPECTED[name][opname]
+    assert R.wide(R.FAST_OR, bms).cardinality() == EXPECTED[name]["WIDE_OR"]
+    assert R.wide(R.PAR_OR, bms).cardinality() == EXPECTED[name]["WIDE_OR"]
+    assert R.wide(R.FAST_AND, bms).cardinality() == EXPECTED[name]["WIDE_AND"]
+    assert R.wide_cardinality(R.OR, bms) == EXPECTED[name]["WIDE_OR"]
+
+
+def test_fixture_round_trip_and_run_optimize_kat(oracle):
+    # TestAdversarialInputs.testInputGoodFile1/2 (TestAdversarialInputs.java:32-48)
+    R = oracle
+    with_runs, without_runs = fixture_bytes("bitmapwithruns.bin"), fixture_bytes("bitmapwithoutruns.bin")
+    a, b = R.RefBitmap.deserialize(with_runs), R.RefBitmap.deserialize(without_runs)
+    assert a.cardinality() == 200100 and b.cardinality() == 200100
+    assert a.serialize() == with_runs and b.serialize() == without_runs
+    assert [c[1] for c in a.containers()] == [0, 0, 1, 1, 1, 1, 1, 0, 2, 2, 2]
+    b.run_optimize()
+    assert b.serialize() == with_runs  # runOptimize(withoutruns) reproduces withruns byte for byte
+
+
+@pytest.mark.parametrize("i", range(1, 8))
+def test_crashprone_inputs_rejected(oracle, i):
+    # TestAdversarialInputs.testInputBadFile8 (TestAdversarialInputs.java:18-21, 50-62)
+    with pytest.raises(IOError):
+        oracle.RefBitmap.deserialize(fixture_bytes(f"crashproneinput{i}.bin"))
+
+
+def _one(oracle, values, run_optimize):
+    b = oracle.RefBitmap.of(np.asarray(values, np.uint32))
+    if run_optimize:
+        b.run_optimize()
+    return b
+
+
+def test_type_pins_full_or_is_run(oracle):
+    # TestRunContainer.orFullToRunContainer{,2,3} (TestRunContainer.java:2634-2662)
+    R = oracle
+    cases = [
+        (_one(R, range(0, 1 << 15), True), _one(R, range(1 << 15, 1 << 16), False)),   # Run | Bitmap
+        (_one(R, range(1024 - 200, 1 << 16), True), _one(R, range(0, 1024), False)),   # Run | Array
+        (_one(R, range(0, 1 << 15), True), _one(R, range((1 << 15) - 200, 1 << 16), True)),  # Run | Run
+    ]
+    for x, y in cases:
+        assert [c[1] for c in x.containers()][0] == R.RUN
+        r = R.op(R.OR, x, y)
+        assert r.containers() == [(0, R.RUN, 65536, 1)]
+
+
+def test_type_pins_lazy_or_full(oracle):
+    # TestRunContainer.testLazyORFull (TestRunContainer.java:3219-3228): naive_or repairs to a full Run
+    R = oracle
+    x = _one(R, range(0, 1 << 15), True)
+    y = _one(R, range(3210, 1 << 16), False)
+    assert R.wide(R.FAST_OR, [x, y]).containers() == [(0, R.RUN, 65536, 1)]
+
+
+def test_in_place_vs_static_or_full(oracle):
+    # BitmapContainer.ior(ArrayContainer) never converts a full bitmap (BitmapContainer.java:749-766)
+    R = oracle
+    x = _one(R, range(0, 65535), False)  # Bitmap, one value short of full
+    y = _one(R, [65535], False)
+    assert R.op(R.OR, x, y).containers()[0][1] == R.RUN
+    z = x.clone()
+    R.op_inplace(R.OR, z, y)
+    assert z.containers()[0][1] == R.BITMAP
