@@ -1,0 +1,211 @@
+#!/usr/bin/env python3
+"""Benchmark of the MI355X RoaringBitmap set-algebra path (BASELINE.json metric).
+
+Default workload (N=1): SURVEY §8d config 2 — batched pairwise AND of 1M (filter,
+posting-list) bitmap pairs with mixed Array/Bitmap/Run containers, generated on the device
+(SplitMix64, seed 42 + rank).  One "step" = one rbgpu_pairwise(AND) call over every pair,
+inputs already resident in HBM, results materialized in HBM (RoaringFormatSpec payloads).
+
+Multi-GPU (torchrun, one process per GPU): pairs are independent, so each rank owns its own
+1M pairs (weak scaling, no data-path collective); barrier + max-over-ranks timing.
+
+Output: one JSON line on rank 0 with `roofline` (dominant kernel k_pairwise: algorithmic bytes
+per launch / HIP-event duration on the library stream, against 8 TB/s HBM) and `cpu_baseline`
+(the oracle — C++ restatement of RoaringBitmap.and — on a bounded sample, host threads).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "input GB/s (HBM roofline %) for batched and/or/xor + wide-OR, 1/2/4/8 GPU"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=10)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--pairs", type=int, default=1_000_000, help="pairs per GPU (config 2)")
+    p.add_argument("--workload", default="pairwise_and", choices=["pairwise_and", "pairwise_or", "pairwise_xor",
+                                                                   "pairwise_andnot", "wide_or"])
+    p.add_argument("--wide-bitmaps", type=int, default=1024)
+    p.add_argument("--cpu-seconds", type=float, default=10.0)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    return p.parse_args()
+
+
+def dist_setup(args):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as td
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        td.init_process_group("nccl", rank=rank, world_size=world)
+        dist = td
+    return world, rank, local, dist
+
+
+def barrier_max(dist, value: float) -> float:
+    if dist is None:
+        return value
+    import torch
+    t = torch.tensor([value], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def allreduce_sum(dist, value: float) -> float:
+    if dist is None:
+        return value
+    import torch
+    t = torch.tensor([value], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return float(t.item())
+
+
+def barrier(dist):
+    if dist is not None:
+        dist.barrier()
+
+
+def cpu_baseline(ctx, rb, a, b, op, seconds: float):
+    """Oracle (C++ restatement of RoaringBitmap.and etc.) on a bounded sample, host threads."""
+    from oracle import rbref as R
+    n_total = len(a)
+    sample = min(n_total, 20000)
+    ra = [R.RefBitmap.deserialize(x) for x in a.serialize(0, sample)]
+    rbb = [R.RefBitmap.deserialize(x) for x in b.serialize(0, sample)]
+    # algorithmic input bytes of the sample, counted exactly like the device run
+    tmp = ctx.pairwise(op, a, b, np.arange(sample, dtype=np.uint32), np.arange(sample, dtype=np.uint32))
+    sample_bytes = ctx.stats()["input_bytes"]
+    tmp.close()
+    threads = min(16, os.cpu_count() or 1)
+    res = {}
+    for th in (1, threads):
+        passes, t0 = 0, time.perf_counter()
+        while True:
+            R.pairwise_batch(op, ra, rbb, threads=th)
+            passes += 1
+            el = time.perf_counter() - t0
+            if el >= seconds / 2:
+                break
+        res[th] = passes * sample_bytes / el / 1e9
+    return {
+        "value": round(res[threads], 3), "unit": "GB/s", "cores": threads, "kind": "port",
+        "value_1thread": round(res[1], 3),
+        "sample": f"first {sample} of the {n_total} generated pairs, looped for ~{seconds / 2:.0f}s per thread count; "
+                  f"oracle/rbref.cpp RoaringBitmap.{['and', 'or', 'xor', 'andNot'][op]} (C++ restatement, -O3)",
+    }
+
+
+def main():
+    args = parse()
+    world, rank, local, dist = dist_setup(args)
+    import roaringbitmap_amd as rb
+    ctx = rb.Context(local)
+    seed = 42 + rank
+
+    op = {"pairwise_and": rb.AND, "pairwise_or": rb.OR, "pairwise_xor": rb.XOR, "pairwise_andnot": rb.ANDNOT,
+          "wide_or": None}[args.workload]
+    if op is not None:
+        a, b = ctx.generate(rb.WL_FILTER_POSTING, args.pairs, seed=seed)
+        run = lambda: ctx.pairwise(op, a, b)  # noqa: E731
+        workload = (f"config2: batched pairwise {['AND', 'OR', 'XOR', 'ANDNOT'][op]} of {args.pairs} "
+                    f"(filter, posting-list) pairs per GPU, mixed Array/Bitmap/Run, 2^18 universe")
+        units = args.pairs
+        unit_name = "pairs"
+    else:
+        a, _ = ctx.generate(rb.WL_WIDE_DENSE, args.wide_bitmaps, seed=seed)
+        run = lambda: ctx.wide(rb.FAST_OR, a)  # noqa: E731
+        workload = f"config3: FastAggregation.or of {args.wide_bitmaps} dense bitmaps over 2^32 per GPU"
+        units = a.n_containers
+        unit_name = "input containers"
+    ctx.synchronize()
+
+    for _ in range(args.warmup):
+        r = run()
+        r.close()
+    ctx.synchronize()
+
+    kernel_ms, in_bytes, out_bytes = [], 0, 0
+    barrier(dist)
+    ctx.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        r = run()
+        st = ctx.stats()
+        kernel_ms.append(st["main_kernel_ms"])
+        in_bytes += st["input_bytes"]
+        out_bytes += st["output_bytes"]
+        r.close()
+    ctx.synchronize()
+    barrier(dist)
+    elapsed = time.perf_counter() - t0
+    elapsed = barrier_max(dist, elapsed)
+    total_in = allreduce_sum(dist, float(in_bytes))
+    main_name = st["main_kernel"]
+
+    if rank == 0:
+        ms_per_step = elapsed / args.steps * 1e3
+        value = total_in / elapsed / 1e9
+        per_launch = (in_bytes + out_bytes) / args.steps
+        k_ms = float(np.mean(kernel_ms))
+        achieved = per_launch / (k_ms * 1e-3) / 1e9
+        line = {
+            "metric": METRIC,
+            "value": round(value, 3),
+            "unit": "GB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u64",
+            "data": "synthetic (device SplitMix64 generator, runOptimize'd containers; SURVEY §8d)",
+            "config": {
+                "workload": workload,
+                "units_per_gpu": units,
+                "unit": unit_name,
+                "input_bytes_per_step_per_gpu": in_bytes // args.steps,
+                "output_bytes_per_step_per_gpu": out_bytes // args.steps,
+                "roofline_pct_whole_step": round(100.0 * (total_in + allreduce_sum(dist, float(out_bytes)))
+                                                 / elapsed / 1e9 / (HBM_PEAK_GBS * world), 2),
+                "parallelism": f"key-range/pair sharding x{world} (replicas, no data-path collective)",
+            },
+            "roofline": {
+                "bound": "hbm",
+                "kernel": main_name,
+                "achieved": round(achieved, 2),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": None,
+                "kernel_ms": round(k_ms, 4),
+                "algorithmic_bytes_per_launch": int(per_launch),
+            },
+        }
+        if world == 1 and not args.no_cpu_baseline and op is not None:
+            line["cpu_baseline"] = cpu_baseline(ctx, rb, a, b, op, args.cpu_seconds)
+        print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

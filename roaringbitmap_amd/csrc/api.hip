@@ -30,6 +30,7 @@ int fail(int code, const char *fmt, ...) {
 
 int set_alloc(rbgpu_ctx *ctx, rbgpu_set *s, uint32_t nb, uint64_t nc, uint64_t payload) {
   s->ctx = ctx;
+  ctx->refs++;
   s->nb = nb;
   s->nc = nc;
   s->payload_bytes = payload;
@@ -54,7 +55,23 @@ void set_release(rbgpu_set *s) {
   p.release(s->nruns);
   p.release(s->off);
   p.release(s->payload);
+  rbgpu_ctx *ctx = s->ctx;
   s->ctx = nullptr;
+  ctx_unref(ctx);
+}
+void ctx_unref(rbgpu_ctx *ctx) {
+  if (--ctx->refs > 0) return;
+  (void)hipSetDevice(ctx->device);
+  (void)hipStreamSynchronize(ctx->stream);
+  for (auto &e : ctx->ev) (void)hipEventDestroy(e);
+  (void)hipFree(ctx->d_stats);
+  (void)hipHostFree(ctx->h_pinned);
+  ctx->pool.clear();
+  ctx->ws_pairs.destroy();
+  ctx->ws_tasks.destroy();
+  ctx->ws_wide.destroy();
+  (void)hipStreamDestroy(ctx->stream);
+  delete ctx;
 }
 int ensure_h_begin(const rbgpu_set *cs) {
   rbgpu_set *s = const_cast<rbgpu_set *>(cs);
@@ -229,18 +246,10 @@ int rbgpu_open(int device, rbgpu_ctx **out) {
 }
 
 void rbgpu_close(rbgpu_ctx *ctx) {
-  if (!ctx) return;
-  (void)hipSetDevice(ctx->device);
-  (void)hipStreamSynchronize(ctx->stream);
-  for (auto &e : ctx->ev) (void)hipEventDestroy(e);
-  (void)hipFree(ctx->d_stats);
-  (void)hipHostFree(ctx->h_pinned);
-  ctx->pool.clear();
-  ctx->ws_pairs.destroy();
-  ctx->ws_tasks.destroy();
-  ctx->ws_wide.destroy();
-  (void)hipStreamDestroy(ctx->stream);
-  delete ctx;
+  // sets still alive keep the context (stream, pool) alive until they are freed
+  if (!ctx || ctx->closed) return;
+  ctx->closed = true;
+  ctx_unref(ctx);
 }
 
 int rbgpu_synchronize(rbgpu_ctx *ctx) {

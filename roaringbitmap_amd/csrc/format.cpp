@@ -93,7 +93,8 @@ int parse_serialized(const uint8_t *buf, uint64_t len, HostSoA &out, std::string
     if (!c.need(4ull * size)) { err = "truncated offset table"; return RB_EFORMAT; }
     c.pos += 4ull * size;
   }
-  // stage into a temporary so a failure leaves `out` untouched
+  // stage into a temporary so a failure leaves `out` untouched; all format (truncation) errors
+  // are reported before any canonical-form check, like the reference which only fails on EOF.
   HostSoA t;
   for (uint32_t k = 0; k < size; ++k) {
     const bool is_run = hasrun && ((runmark[k / 8] >> (k % 8)) & 1);
@@ -118,14 +119,16 @@ int parse_serialized(const uint8_t *buf, uint64_t len, HostSoA &out, std::string
     t.payload.resize(at + round16(bytes), 0);
     std::memcpy(t.payload.data() + at, buf + c.pos, bytes);
     c.pos += bytes;
-    if (k > 0 && keys[k] <= keys[k - 1]) { err = "container keys not strictly increasing"; return RB_EINVAL; }
-    int rc = validate_container(ty, cards[k], nr, t.payload.data() + at, err);
-    if (rc) return rc;
     t.key.push_back(keys[k]);
     t.type.push_back(ty);
     t.card.push_back(cards[k]);
     t.nruns.push_back((uint16_t)nr);
     t.off.push_back(at);
+  }
+  for (uint32_t k = 0; k < size; ++k) {
+    if (k > 0 && t.key[k] <= t.key[k - 1]) { err = "container keys not strictly increasing"; return RB_EINVAL; }
+    int rc = validate_container(t.type[k], t.card[k], t.nruns[k], t.payload.data() + t.off[k], err);
+    if (rc) return rc;
   }
   // append
   const uint64_t base = out.payload.size();

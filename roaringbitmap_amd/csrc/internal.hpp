@@ -95,6 +95,8 @@ struct rbgpu_ctx {
   uint64_t *d_stats = nullptr;  // [4] algorithmic byte counters written by kernels
   uint64_t *h_pinned = nullptr; // [16]
   rb_stats last{};
+  int refs = 1;                 // the handle + one per live set; destroyed at zero
+  bool closed = false;
 };
 
 struct rbgpu_set {
@@ -114,6 +116,7 @@ struct rbgpu_set {
 
 namespace rbg {
 int set_alloc(rbgpu_ctx *ctx, rbgpu_set *s, uint32_t nb, uint64_t nc, uint64_t payload);
+void ctx_unref(rbgpu_ctx *ctx);
 void set_release(rbgpu_set *s);
 int ensure_h_begin(const rbgpu_set *s);
 // call accounting: zero the byte counters + record the start event / read everything back

@@ -180,8 +180,10 @@ __global__ __launch_bounds__(256) void k_pairwise(SetView A, SetView B, const Ta
   int ty;
   if (OP != RB_OR && c == 0) ty = kEmpty;
   else if (eff) ty = type_eff(c, r);
-  else if (OP == RB_OR && (ta == kBitmap || tb == kBitmap)) ty = type_lr(c);
-  else ty = type_ab(c);
+  else if (OP == RB_OR && (ta == kBitmap || tb == kBitmap)) {
+    ty = type_lr(c);
+    if (ty == kRun) r = 1; // LR's Run is the full container: one run
+  } else ty = type_ab(c);
   if (CARD_ONLY) {
     if (lane == 0) {
       tm.type[t] = c ? (uint8_t)kArray : kEmpty;

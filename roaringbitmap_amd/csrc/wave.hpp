@@ -317,7 +317,9 @@ __device__ __forceinline__ uint32_t emit_container(int type, const uint64_t (&w)
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int j = 2 * k + h;
-      const uint32_t open = (uint32_t)(h ? (w[j - 1] >> 63) : ((nb.prev_top_h0 >> k) & 1));
+      // a run is open into this word iff the bit before it AND its bit 0 are set (a run that ends on
+      // the previous word's last bit was already counted there)
+      const uint32_t open = (uint32_t)(h ? (w[j - 1] >> 63) : ((nb.prev_top_h0 >> k) & 1)) & (uint32_t)(w[j] & 1);
       uint32_t ep = sp - open;
       const uint32_t base = (uint32_t)(128 * k + 2 * lane + h) << 6;
       uint64_t x = st[j];
