@@ -141,7 +141,8 @@ def main():
         r.close()
     ctx.synchronize()
 
-    kernel_ms, in_bytes, out_bytes = [], 0, 0
+    kernel_ms, kernel_bytes, in_bytes, out_bytes = [], [], 0, 0
+    per_kernel = {}
     barrier(dist)
     ctx.synchronize()
     t0 = time.perf_counter()
@@ -149,6 +150,12 @@ def main():
         r = run()
         st = ctx.stats()
         kernel_ms.append(st["main_kernel_ms"])
+        kernel_bytes.append(st["main_kernel_bytes"])
+        for k in st["kernels"]:
+            agg = per_kernel.setdefault(k["name"], {"ms": 0.0, "bytes": 0, "items": 0})
+            agg["ms"] += k["ms"] / args.steps
+            agg["bytes"] += k["bytes"] // args.steps
+            agg["items"] += k["items"] // args.steps
         in_bytes += st["input_bytes"]
         out_bytes += st["output_bytes"]
         r.close()
@@ -162,7 +169,7 @@ def main():
     if rank == 0:
         ms_per_step = elapsed / args.steps * 1e3
         value = total_in / elapsed / 1e9
-        per_launch = (in_bytes + out_bytes) / args.steps
+        per_launch = float(np.mean(kernel_bytes))
         k_ms = float(np.mean(kernel_ms))
         achieved = per_launch / (k_ms * 1e-3) / 1e9
         line = {
@@ -198,6 +205,9 @@ def main():
                 "traffic": None,
                 "kernel_ms": round(k_ms, 4),
                 "algorithmic_bytes_per_launch": int(per_launch),
+                "kernels": {n: {"ms": round(v["ms"], 4), "bytes": v["bytes"], "items": v["items"],
+                                "GB/s": round(v["bytes"] / max(v["ms"], 1e-9) / 1e6, 1)}
+                            for n, v in per_kernel.items()},
             },
         }
         if world == 1 and not args.no_cpu_baseline and op is not None:

@@ -87,8 +87,14 @@ typedef struct rb_stats {
   uint64_t output_bytes;     /* algorithmic output bytes (payload + 16 B metadata per result container) */
   uint64_t result_containers;
   double main_kernel_ms;     /* duration of the dominant kernel (HIP events on the ctx stream) */
+  uint64_t main_kernel_bytes; /* algorithmic bytes (in + out) of the work that kernel did */
   double total_ms;           /* whole call, device time between first and last launch */
   char main_kernel[64];      /* name of the dominant kernel */
+  uint32_t n_kernels;        /* per-kernel breakdown of the compute phase */
+  char kernel_name[4][48];
+  double kernel_ms[4];
+  uint64_t kernel_bytes[4];
+  uint64_t kernel_items[4];
 } rb_stats;
 
 /* ---- context ---------------------------------------------------------------------- */

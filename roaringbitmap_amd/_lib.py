@@ -40,8 +40,14 @@ class RbStats(C.Structure):
         ("output_bytes", C.c_uint64),
         ("result_containers", C.c_uint64),
         ("main_kernel_ms", C.c_double),
+        ("main_kernel_bytes", C.c_uint64),
         ("total_ms", C.c_double),
         ("main_kernel", C.c_char * 64),
+        ("n_kernels", C.c_uint32),
+        ("kernel_name", (C.c_char * 48) * 4),
+        ("kernel_ms", C.c_double * 4),
+        ("kernel_bytes", C.c_uint64 * 4),
+        ("kernel_items", C.c_uint64 * 4),
     ]
 
 

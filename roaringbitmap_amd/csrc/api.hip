@@ -66,6 +66,7 @@ void ctx_unref(rbgpu_ctx *ctx) {
   for (auto &e : ctx->ev) (void)hipEventDestroy(e);
   (void)hipFree(ctx->d_stats);
   (void)hipHostFree(ctx->h_pinned);
+  (void)hipHostFree(ctx->h_stats);
   ctx->pool.clear();
   ctx->ws_pairs.destroy();
   ctx->ws_tasks.destroy();
@@ -192,22 +193,39 @@ int check_ctx(rbgpu_ctx *ctx) {
 
 namespace rbg {
 void stats_begin(rbgpu_ctx *ctx) {
-  (void)hipMemsetAsync(ctx->d_stats, 0, 4 * sizeof(uint64_t), ctx->stream);
+  (void)hipMemsetAsync(ctx->d_stats, 0, kStatWords * kStripes * sizeof(uint64_t), ctx->stream);
   (void)hipEventRecord(ctx->ev[0], ctx->stream);
 }
-int stats_end(rbgpu_ctx *ctx, const char *main_name, uint64_t tasks, uint64_t result_containers) {
-  HIPCHK(hipEventRecord(ctx->ev[3], ctx->stream));
-  HIPCHK(hipMemcpyAsync(ctx->h_pinned + 8, ctx->d_stats, 4 * sizeof(uint64_t), hipMemcpyDeviceToHost, ctx->stream));
+int stats_end(rbgpu_ctx *ctx, uint64_t tasks, uint64_t result_containers, const KernelSpan *k, int n) {
+  HIPCHK(hipEventRecord(ctx->ev[5], ctx->stream));
+  HIPCHK(hipMemcpyAsync(ctx->h_stats, ctx->d_stats, kStatWords * kStripes * sizeof(uint64_t), hipMemcpyDeviceToHost,
+                        ctx->stream));
   HIPCHK(hipStreamSynchronize(ctx->stream));
+  uint64_t w[kStatWords] = {};
+  for (int i = 0; i < kStatWords; ++i)
+    for (int j = 0; j < kStripes; ++j) w[i] += ctx->h_stats[i * kStripes + j];
   rb_stats &s = ctx->last;
+  s = rb_stats{};
   s.tasks = tasks;
-  s.input_bytes = ctx->h_pinned[8];
-  s.output_bytes = ctx->h_pinned[9];
+  s.input_bytes = w[0];
+  s.output_bytes = w[1];
   s.result_containers = result_containers;
   float ms = 0;
-  s.main_kernel_ms = hipEventElapsedTime(&ms, ctx->ev[1], ctx->ev[2]) == hipSuccess ? ms : 0.0;
-  s.total_ms = hipEventElapsedTime(&ms, ctx->ev[0], ctx->ev[3]) == hipSuccess ? ms : 0.0;
-  std::snprintf(s.main_kernel, sizeof s.main_kernel, "%s", main_name);
+  s.total_ms = hipEventElapsedTime(&ms, ctx->ev[0], ctx->ev[5]) == hipSuccess ? ms : 0.0;
+  s.n_kernels = (uint32_t)std::min(n, 4);
+  int best = -1;
+  for (int i = 0; i < (int)s.n_kernels; ++i) {
+    std::snprintf(s.kernel_name[i], sizeof s.kernel_name[i], "%s", k[i].name);
+    s.kernel_ms[i] = hipEventElapsedTime(&ms, ctx->ev[1 + i], ctx->ev[2 + i]) == hipSuccess ? ms : 0.0;
+    s.kernel_bytes[i] = (k[i].in_word >= 0 ? w[k[i].in_word] : 0) + (k[i].out_word >= 0 ? w[k[i].out_word] : 0);
+    s.kernel_items[i] = k[i].items;
+    if (best < 0 || s.kernel_ms[i] > s.kernel_ms[best]) best = i;
+  }
+  if (best >= 0) {
+    s.main_kernel_ms = s.kernel_ms[best];
+    s.main_kernel_bytes = s.kernel_bytes[best];
+    std::snprintf(s.main_kernel, sizeof s.main_kernel, "%s", s.kernel_name[best]);
+  }
   return RB_OK;
 }
 } // namespace rbg
@@ -235,7 +253,8 @@ int rbgpu_open(int device, rbgpu_ctx **out) {
   rbgpu_ctx *c = new rbgpu_ctx;
   c->device = device;
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-      hipMalloc((void **)&c->d_stats, 4 * sizeof(uint64_t)) != hipSuccess ||
+      hipMalloc((void **)&c->d_stats, kStatWords * kStripes * sizeof(uint64_t)) != hipSuccess ||
+      hipHostMalloc((void **)&c->h_stats, kStatWords * kStripes * sizeof(uint64_t)) != hipSuccess ||
       hipHostMalloc((void **)&c->h_pinned, 16 * sizeof(uint64_t)) != hipSuccess) {
     delete c;
     return fail(RB_EDEVICE, "context creation failed on device %d", device);
@@ -428,14 +447,16 @@ static int pairwise_impl(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu
   const uint64_t scan_tmp = scan_tmp_words(np + 1);
   size_t need = 0;
   need += 2 * aligned256(np * 4);            // indices
-  need += 9 * aligned256((np + 1) * 8);      // counts, scans, result counts, pair cards
+  need += 13 * aligned256((np + 1) * 8);     // 5 counts, 5 scans, result counts, pair cards, spare
   need += aligned256(scan_tmp * 8);
   if (ctx->ws_pairs.reserve(need, st) != hipSuccess) return fail(RB_ENOMEM, "pair workspace");
   Workspace &W = ctx->ws_pairs;
   uint32_t *d_aidx = a_idx ? W.take<uint32_t>(np) : nullptr;
   uint32_t *d_bidx = b_idx ? W.take<uint32_t>(np) : nullptr;
-  uint64_t *cnt = W.take<uint64_t>(np + 1), *nbig = W.take<uint64_t>(np + 1), *small = W.take<uint64_t>(np + 1);
-  uint64_t *tb = W.take<uint64_t>(np + 1), *bb = W.take<uint64_t>(np + 1), *sb = W.take<uint64_t>(np + 1);
+  PairCountArrays cnt{W.take<uint64_t>(np + 1), W.take<uint64_t>(np + 1), W.take<uint64_t>(np + 1),
+                      W.take<uint64_t>(np + 1), W.take<uint64_t>(np + 1)};
+  PairCountArrays scn{W.take<uint64_t>(np + 1), W.take<uint64_t>(np + 1), W.take<uint64_t>(np + 1),
+                      W.take<uint64_t>(np + 1), W.take<uint64_t>(np + 1)};
   uint64_t *rcnt = W.take<uint64_t>(np + 1), *pcard = W.take<uint64_t>(np + 1);
   uint64_t *tmp = W.take<uint64_t>(std::max<uint64_t>(scan_tmp, 1));
   if (d_aidx) HIPCHK(hipMemcpyAsync(d_aidx, a_idx, np * 4, hipMemcpyHostToDevice, st));
@@ -443,28 +464,39 @@ static int pairwise_impl(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu
 
   stats_begin(ctx);
   PairArgs pa{op, a->view(), b->view(), d_aidx, d_bidx, npairs};
-  launch_pair_count(pa, cnt, nbig, small, ctx->d_stats, st);
-  scan_exclusive(cnt, tb, np, tmp, st);
-  scan_exclusive(nbig, bb, np, tmp, st);
-  scan_exclusive(small, sb, np, tmp, st);
-  HIPCHK(hipMemcpyAsync(ctx->h_pinned + 0, tb + np, 8, hipMemcpyDeviceToHost, st));
-  HIPCHK(hipMemcpyAsync(ctx->h_pinned + 1, bb + np, 8, hipMemcpyDeviceToHost, st));
-  HIPCHK(hipMemcpyAsync(ctx->h_pinned + 2, sb + np, 8, hipMemcpyDeviceToHost, st));
+  launch_pair_count(pa, cnt, ctx->d_stats, st);
+  scan_exclusive(cnt.task, scn.task, np, tmp, st);
+  scan_exclusive(cnt.light, scn.light, np, tmp, st);
+  scan_exclusive(cnt.heavy, scn.heavy, np, tmp, st);
+  scan_exclusive(cnt.big, scn.big, np, tmp, st);
+  scan_exclusive(cnt.small, scn.small, np, tmp, st);
+  uint64_t *const tot = ctx->h_pinned;
+  HIPCHK(hipMemcpyAsync(tot + 0, scn.task + np, 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(tot + 1, scn.light + np, 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(tot + 2, scn.heavy + np, 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(tot + 3, scn.big + np, 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(tot + 4, scn.small + np, 8, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
-  const uint64_t ntasks = ctx->h_pinned[0], nbig_t = ctx->h_pinned[1], small_t = ctx->h_pinned[2];
+  const uint64_t ntasks = tot[0], nlight = tot[1], nheavy = tot[2], nbig_t = tot[3], small_t = tot[4];
   const uint64_t small_base = nbig_t * kBitmapBytes;
   const uint64_t arena = card_only ? 0 : small_base + small_t;
 
-  size_t tneed = aligned256(ntasks * sizeof(Task)) + 2 * aligned256(ntasks * 2) + aligned256(ntasks) +
-                 aligned256(ntasks * 4) + 256;
-  if (ctx->ws_tasks.reserve(tneed, st) != hipSuccess) return fail(RB_ENOMEM, "task workspace (%llu tasks)", (unsigned long long)ntasks);
+  const uint64_t nt1 = std::max<uint64_t>(ntasks, 1);
+  size_t tneed = aligned256(std::max<uint64_t>(nlight, 1) * sizeof(TaskRec)) +
+                 aligned256(std::max<uint64_t>(nheavy, 1) * sizeof(TaskRec)) + 2 * aligned256(nt1 * 2) +
+                 2 * aligned256(nt1) + aligned256(nt1 * 4) + aligned256(nt1 * 8) + 256;
+  if (ctx->ws_tasks.reserve(tneed, st) != hipSuccess)
+    return fail(RB_ENOMEM, "task workspace (%llu tasks)", (unsigned long long)ntasks);
   Workspace &T = ctx->ws_tasks;
-  Task *tasks = T.take<Task>(std::max<uint64_t>(ntasks, 1));
+  TaskRec *light = T.take<TaskRec>(std::max<uint64_t>(nlight, 1));
+  TaskRec *heavy = T.take<TaskRec>(std::max<uint64_t>(nheavy, 1));
   TaskMeta tm;
-  tm.key = T.take<uint16_t>(std::max<uint64_t>(ntasks, 1));
-  tm.nruns = T.take<uint16_t>(std::max<uint64_t>(ntasks, 1));
-  tm.type = T.take<uint8_t>(std::max<uint64_t>(ntasks, 1));
-  tm.card = T.take<uint32_t>(std::max<uint64_t>(ntasks, 1));
+  tm.key = T.take<uint16_t>(nt1);
+  tm.nruns = T.take<uint16_t>(nt1);
+  tm.type = T.take<uint8_t>(nt1);
+  tm.cat = T.take<uint8_t>(nt1);
+  tm.card = T.take<uint32_t>(nt1);
+  tm.out = T.take<uint64_t>(nt1);
 
   rbgpu_set *res = nullptr;
   if (!card_only) {
@@ -475,21 +507,23 @@ static int pairwise_impl(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu
       return rc;
     }
   }
-  launch_pair_emit(pa, tb, bb, sb, small_base, tasks, tm.key, st);
+  launch_pair_emit(pa, scn, small_base, light, heavy, tm, st);
   HIPCHK(hipEventRecord(ctx->ev[1], st));
-  launch_pairwise(op, card_only, pa.A, pa.B, tasks, ntasks, res ? res->payload : nullptr, tm, st);
-  HIPCHK(hipEventRecord(ctx->ev[2], st));
-  launch_compact_count(tb, npairs, tm.type, rcnt, st);
+  launch_pairwise(op, card_only, a->payload, b->payload, light, nlight, heavy, nheavy, res ? res->payload : nullptr,
+                  tm, st, ctx->ev[2]);
+  HIPCHK(hipEventRecord(ctx->ev[3], st));
+  launch_compact_count(scn.task, npairs, tm.type, rcnt, st);
   uint64_t *rbegin = res ? res->begin : W.take<uint64_t>(np + 1);
   scan_exclusive(rcnt, rbegin, np, tmp, st);
   OutView ov{};
   if (res) ov = OutView{res->key, res->type, res->card, res->nruns, res->off};
-  launch_compact_write(tb, npairs, tm, tasks, rbegin, ov, pcard, ctx->d_stats, st);
-  HIPCHK(hipMemcpyAsync(ctx->h_pinned + 3, rbegin + np, 8, hipMemcpyDeviceToHost, st));
+  launch_compact_write(scn.task, npairs, tm, rbegin, ov, pcard, ctx->d_stats, st);
+  HIPCHK(hipMemcpyAsync(ctx->h_pinned + 5, rbegin + np, 8, hipMemcpyDeviceToHost, st));
   if (card_out && np) HIPCHK(hipMemcpyAsync(card_out, pcard, np * 8, hipMemcpyDeviceToHost, st));
-  rc = stats_end(ctx, "k_pairwise", ntasks, 0);
+  const KernelSpan spans[2] = {{"k_pair_light", 2, 4, nlight}, {"k_pair_heavy", 3, 5, nheavy}};
+  rc = stats_end(ctx, ntasks, 0, spans, 2);
   if (rc) return rc;
-  const uint64_t nres = ctx->h_pinned[3];
+  const uint64_t nres = ctx->h_pinned[5];
   ctx->last.result_containers = nres;
   if (res) {
     res->nc = nres;

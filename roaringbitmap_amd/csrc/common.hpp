@@ -34,12 +34,21 @@ struct OutView {
   uint64_t *off;
 };
 
-// One container-level work item of a pairwise call, in result (key-merged) order.
-struct Task {
-  int32_t ia;      // container index in A, -1 if none
-  int32_t ib;      // container index in B, -1 if none
+// One container-level work item of a pairwise call, self-contained so the compute kernels reach
+// the payloads after a single (scalar) record load.  Records are stored per kernel category.
+struct TaskRec {
+  uint64_t pa, pb; // payload byte offsets in A / B (unused side: 0)
   uint64_t out;    // byte offset of the output slot in the result arena
+  uint32_t t;      // merged (result-order) task index
+  uint32_t da, db; // descriptor: type | card << 2; type 3 = no container on that side
+  uint16_t ra, rb; // run counts
 };
+constexpr uint32_t kAbsent = 3;
+__host__ __device__ inline uint32_t desc_type(uint32_t d) { return d & 3; }
+__host__ __device__ inline uint32_t desc_card(uint32_t d) { return d >> 2; }
+
+// Striped accounting counters (stats word w, stripe s): d_stats[w * kStripes + s].
+constexpr int kStatWords = 8, kStripes = 64;
 
 __host__ __device__ inline uint64_t payload_bytes(int type, uint32_t card, uint32_t nruns) {
   return type == kBitmap ? (uint64_t)kBitmapBytes : type == kArray ? 2ull * card : 4ull * nruns;

@@ -89,11 +89,12 @@ inline size_t aligned256(size_t b) { return (b + 255) & ~size_t(255); }
 struct rbgpu_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
-  hipEvent_t ev[4] = {};   // [0] call start, [1]/[2] around the dominant kernel, [3] call end
+  hipEvent_t ev[6] = {};   // [0] call start, [1..n] around the compute kernels, [5] call end
   rbg::DevPool pool;
   rbg::Workspace ws_pairs, ws_tasks, ws_wide;
-  uint64_t *d_stats = nullptr;  // [4] algorithmic byte counters written by kernels
+  uint64_t *d_stats = nullptr;  // [kStatWords * kStripes] striped algorithmic byte counters
   uint64_t *h_pinned = nullptr; // [16]
+  uint64_t *h_stats = nullptr;  // [kStatWords * kStripes]
   rb_stats last{};
   int refs = 1;                 // the handle + one per live set; destroyed at zero
   bool closed = false;
@@ -121,7 +122,14 @@ void set_release(rbgpu_set *s);
 int ensure_h_begin(const rbgpu_set *s);
 // call accounting: zero the byte counters + record the start event / read everything back
 void stats_begin(rbgpu_ctx *ctx);
-int stats_end(rbgpu_ctx *ctx, const char *main_name, uint64_t tasks, uint64_t result_containers);
+// Compute-phase kernels k = 0..n-1 ran between events ev[1+k] and ev[2+k]; their algorithmic
+// bytes are d_stats[in_word[k]] + d_stats[out_word[k]] (-1: none).
+struct KernelSpan {
+  const char *name;
+  int in_word, out_word;
+  uint64_t items;
+};
+int stats_end(rbgpu_ctx *ctx, uint64_t tasks, uint64_t result_containers, const KernelSpan *k, int n);
 // wide.hip
 int wide_run(rbgpu_ctx *ctx, int sem, const rbgpu_set *in, const std::vector<uint32_t> &members, rbgpu_set **out);
 // generate.hip

@@ -22,20 +22,32 @@ struct TaskMeta {
   uint8_t *type;   // kEmpty when dropped
   uint32_t *card;
   uint16_t *nruns;
+  uint8_t *cat;    // 0 light, 1 heavy
+  uint64_t *out;   // output slot offset
 };
-// stats[0] += algorithmic input bytes, stats[1] += output bytes (see rb_stats)
-void launch_pair_count(const PairArgs &a, uint64_t *ntask, uint64_t *nbig, uint64_t *small, uint64_t *stats,
-                       hipStream_t st);
-void launch_pair_emit(const PairArgs &a, const uint64_t *task_begin, const uint64_t *big_begin,
-                      const uint64_t *small_begin, uint64_t small_base, Task *tasks, uint16_t *task_key,
-                      hipStream_t st);
-void launch_pairwise(int op, bool card_only, const SetView &A, const SetView &B, const Task *tasks,
-                     uint64_t ntasks, uint8_t *out_payload, const TaskMeta &tm, hipStream_t st);
-void launch_compact_count(const uint64_t *task_begin, uint32_t npairs, const uint8_t *ttype,
-                          uint64_t *cnt, hipStream_t st);
-void launch_compact_write(const uint64_t *task_begin, uint32_t npairs, const TaskMeta &tm, const Task *tasks,
-                          const uint64_t *rbegin, const OutView &out, uint64_t *pair_card, uint64_t *stats,
+struct PairCounts {
+  uint64_t task, light, heavy, big, small;
+};
+struct PairBases {
+  uint64_t task, light, heavy, big, small;
+};
+// per pair arrays (counts, or their exclusive scans), each [npairs + 1]
+struct PairCountArrays {
+  uint64_t *task, *light, *heavy, *big, *small;
+};
+// stats words (striped, see common.hpp): 0/1 total input/output bytes, 2/3 light/heavy input,
+// 4/5 light/heavy output
+void launch_pair_count(const PairArgs &a, const PairCountArrays &c, uint64_t *stats, hipStream_t st);
+void launch_pair_emit(const PairArgs &a, const PairCountArrays &scans, uint64_t small_base, TaskRec *light,
+                      TaskRec *heavy, const TaskMeta &tm, hipStream_t st);
+// light: copies and subset-of-an-Array results; heavy: full register path
+void launch_pairwise(int op, bool card_only, const uint8_t *pa, const uint8_t *pb, const TaskRec *light,
+                     uint64_t nl, const TaskRec *heavy, uint64_t nh, uint8_t *out, const TaskMeta &tm,
+                     hipStream_t st, hipEvent_t mid);
+void launch_compact_count(const uint64_t *task_begin, uint32_t npairs, const uint8_t *ttype, uint64_t *cnt,
                           hipStream_t st);
+void launch_compact_write(const uint64_t *task_begin, uint32_t npairs, const TaskMeta &tm, const uint64_t *rbegin,
+                          const OutView &out, uint64_t *pair_card, uint64_t *stats, hipStream_t st);
 
 // ---- setops.hip
 void launch_bitmap_cards(const SetView &s, uint32_t nbitmaps, uint64_t *out, hipStream_t st);

@@ -2,14 +2,17 @@
 //
 // Pipeline (one HIP stream):
 //   k_pair_count   thread per pair: merge the two sorted u16 key lists (RoaringBitmap.and/or/
-//                  xor/andNot key loops, RoaringBitmap.java:377-473, 860-902, 1071-1118) and
-//                  count result slots + an output-byte bound per slot;
-//   scans          exclusive prefix sums -> task index and arena offset of every slot;
-//   k_pair_emit    thread per pair: write the task list in result (key) order;
-//   k_pairwise     ONE WAVE PER TASK: both containers -> 65536-bit register bitmaps, word op,
+//                  xor/andNot key loops, RoaringBitmap.java:377-473, 860-902, 1071-1118), count
+//                  result slots per kernel category + an output-byte bound per slot;
+//   scans          exclusive prefix sums -> record index and arena offset of every slot;
+//   k_pair_emit    thread per pair: write self-contained task records (payload offsets,
+//                  descriptors) per category, plus result-order metadata;
+//   k_pair_light   ONE WAVE PER TASK: unmatched copies and results that are a subset of an
+//                  Array operand (filter against an 8 KiB LDS membership image);
+//   k_pair_heavy   ONE WAVE PER TASK: both containers as 65536-bit register bitmaps, word op,
 //                  card + maximal runs, reference type decision, coalesced emission;
-//   k_compact_*    drop empty results (isEmpty, RoaringBitmap.java:389-391 etc.) and build
-//                  the result CSR.
+//   k_compact_*    drop empty results (isEmpty, RoaringBitmap.java:389-391 etc.) and build the
+//                  result CSR.
 #include "kernels.hpp"
 #include "wave.hpp"
 
@@ -39,25 +42,61 @@ __device__ __forceinline__ void copy_bound(const SetView &S, uint64_t i, bool &b
   bytes = big ? 0 : round16(payload_bytes(t, S.card[i], S.nruns[i]));
 }
 
+// A task is "light" when its result is a subset of one Array operand (AND with an Array, ANDNOT
+// with an Array on the left) or when it is an unmatched copy; everything else is "heavy".
+__device__ __forceinline__ bool light_task(int op, int ta, int tb) {
+  if (ta < 0 || tb < 0) return true;
+  if (op == RB_AND) return ta == kArray || tb == kArray;
+  if (op == RB_ANDNOT) return ta == kArray;
+  return false;
+}
+
+// Striped accounting add: one atomic per wave onto one of kStripes copies of the counter.
+__device__ __forceinline__ void stat_add(uint64_t *stats, int word, uint64_t v) {
+  v = wave_sum_u64(v);
+  if ((threadIdx.x & 63) == 0 && v) {
+    const int stripe = (blockIdx.x * 4 + (threadIdx.x >> 6)) & (kStripes - 1);
+    atomicAdd((unsigned long long *)&stats[word * kStripes + stripe], (unsigned long long)v);
+  }
+}
+
+// inb[0]: key bytes, inb[1]: light-task input bytes, inb[2]: heavy-task input bytes
 template <bool EMIT>
-__device__ __forceinline__ void pair_walk(const PairArgs &a, uint32_t p, uint64_t &nt, uint64_t &nb, uint64_t &sm,
-                                          uint64_t &inb, Task *tasks, uint16_t *tkey, uint64_t big_base_idx,
-                                          uint64_t small_off) {
+__device__ __forceinline__ void pair_walk(const PairArgs &a, uint32_t p, PairCounts &n, uint64_t (&inb)[3],
+                                          const PairBases &base, TaskRec *light, TaskRec *heavy, TaskMeta tm) {
   const uint32_t ai = a.aidx ? a.aidx[p] : p, bi = a.bidx ? a.bidx[p] : p;
   uint64_t i = a.A.begin[ai], i1 = a.A.begin[ai + 1], j = a.B.begin[bi], j1 = a.B.begin[bi + 1];
-  inb += 2 * ((i1 - i) + (j1 - j));
+  inb[0] += 2 * ((i1 - i) + (j1 - j));
   auto slot = [&](int64_t ia, int64_t ib, uint16_t key, bool big, uint64_t bytes) {
-    if (EMIT) {
-      Task t;
-      t.ia = (int32_t)ia;
-      t.ib = (int32_t)ib;
-      t.out = big ? (big_base_idx + nb) * (uint64_t)kBitmapBytes : small_off + sm;
-      tasks[nt] = t;
-      tkey[nt] = key;
+    const int ta = ia >= 0 ? a.A.type[ia] : -1, tb = ib >= 0 ? a.B.type[ib] : -1;
+    const bool lt = light_task(a.op, ta, tb);
+    if (!EMIT) {
+      uint64_t b = 0;
+      if (ia >= 0) b += alg_bytes(ta, a.A.card[ia], a.A.nruns[ia]) + 16;
+      if (ib >= 0) b += alg_bytes(tb, a.B.card[ib], a.B.nruns[ib]) + 16;
+      inb[lt ? 1 : 2] += b;
+    } else {
+      const uint64_t t = base.task + n.task;
+      TaskRec r;
+      r.out = big ? (base.big + n.big) * (uint64_t)kBitmapBytes : base.small + n.small;
+      r.t = (uint32_t)t;
+      r.pa = ia >= 0 ? a.A.off[ia] : 0;
+      r.pb = ib >= 0 ? a.B.off[ib] : 0;
+      r.da = ia >= 0 ? ((uint32_t)ta | (a.A.card[ia] << 2)) : kAbsent;
+      r.db = ib >= 0 ? ((uint32_t)tb | (a.B.card[ib] << 2)) : kAbsent;
+      r.ra = ia >= 0 ? a.A.nruns[ia] : 0;
+      r.rb = ib >= 0 ? a.B.nruns[ib] : 0;
+      if (lt) light[base.light + n.light] = r;
+      else heavy[base.heavy + n.heavy] = r;
+      tm.key[t] = key;
+      tm.cat[t] = lt ? 0 : 1;
+      tm.out[t] = r.out;
     }
-    ++nt;
-    if (big) ++nb;
-    else sm += bytes;
+    ++n.task;
+    if (lt) ++n.light;
+    else ++n.heavy;
+    if (big) ++n.big;
+    else n.small += bytes;
   };
   bool big;
   uint64_t bytes;
@@ -65,22 +104,18 @@ __device__ __forceinline__ void pair_walk(const PairArgs &a, uint32_t p, uint64_
     uint16_t ka = a.A.key[i], kb = a.B.key[j];
     if (ka == kb) {
       matched_bound(a.op, a.A.card[i], a.B.card[j], big, bytes);
-      if (!EMIT)
-        inb += alg_bytes(a.A.type[i], a.A.card[i], a.A.nruns[i]) + alg_bytes(a.B.type[j], a.B.card[j], a.B.nruns[j]) + 32;
       slot((int64_t)i, (int64_t)j, ka, big, bytes);
       ++i;
       ++j;
     } else if (ka < kb) {
       if (keeps_a_only(a.op)) {
         copy_bound(a.A, i, big, bytes);
-        if (!EMIT) inb += alg_bytes(a.A.type[i], a.A.card[i], a.A.nruns[i]) + 16;
         slot((int64_t)i, -1, ka, big, bytes);
       }
       ++i;
     } else {
       if (keeps_b_only(a.op)) {
         copy_bound(a.B, j, big, bytes);
-        if (!EMIT) inb += alg_bytes(a.B.type[j], a.B.card[j], a.B.nruns[j]) + 16;
         slot(-1, (int64_t)j, kb, big, bytes);
       }
       ++j;
@@ -89,78 +124,151 @@ __device__ __forceinline__ void pair_walk(const PairArgs &a, uint32_t p, uint64_
   if (keeps_a_only(a.op))
     for (; i < i1; ++i) {
       copy_bound(a.A, i, big, bytes);
-      if (!EMIT) inb += alg_bytes(a.A.type[i], a.A.card[i], a.A.nruns[i]) + 16;
       slot((int64_t)i, -1, a.A.key[i], big, bytes);
     }
   if (keeps_b_only(a.op))
     for (; j < j1; ++j) {
       copy_bound(a.B, j, big, bytes);
-      if (!EMIT) inb += alg_bytes(a.B.type[j], a.B.card[j], a.B.nruns[j]) + 16;
       slot(-1, (int64_t)j, a.B.key[j], big, bytes);
     }
 }
 
-__global__ __launch_bounds__(kPairThreads) void k_pair_count(PairArgs a, uint64_t *ntask, uint64_t *nbig,
-                                                             uint64_t *small, uint64_t *stats) {
+__global__ __launch_bounds__(kPairThreads) void k_pair_count(PairArgs a, PairCountArrays c, uint64_t *stats) {
   const uint32_t p = blockIdx.x * kPairThreads + threadIdx.x;
-  uint64_t nt = 0, nb = 0, sm = 0, inb = 0;
+  uint64_t inb[3] = {0, 0, 0};
   if (p < a.npairs) {
-    pair_walk<false>(a, p, nt, nb, sm, inb, nullptr, nullptr, 0, 0);
-    ntask[p] = nt;
-    nbig[p] = nb;
-    small[p] = sm;
+    PairCounts n{};
+    PairBases b{};
+    pair_walk<false>(a, p, n, inb, b, nullptr, nullptr, TaskMeta{});
+    c.task[p] = n.task;
+    c.light[p] = n.light;
+    c.heavy[p] = n.heavy;
+    c.big[p] = n.big;
+    c.small[p] = n.small;
   }
-  uint64_t w = wave_sum_u64(inb);
-  if ((threadIdx.x & 63) == 0 && w) atomicAdd((unsigned long long *)&stats[0], (unsigned long long)w);
+  // stats words: 0 total input, 2 light-task input, 3 heavy-task input
+  stat_add(stats, 0, inb[0] + inb[1] + inb[2]);
+  stat_add(stats, 2, inb[1]);
+  stat_add(stats, 3, inb[2]);
 }
 
-__global__ __launch_bounds__(kPairThreads) void k_pair_emit(PairArgs a, const uint64_t *task_begin,
-                                                            const uint64_t *big_begin, const uint64_t *small_begin,
-                                                            uint64_t small_base, Task *tasks, uint16_t *tkey) {
+__global__ __launch_bounds__(kPairThreads) void k_pair_emit(PairArgs a, PairCountArrays scans, uint64_t small_base,
+                                                            TaskRec *light, TaskRec *heavy, TaskMeta tm) {
   const uint32_t p = blockIdx.x * kPairThreads + threadIdx.x;
   if (p >= a.npairs) return;
-  uint64_t nt = 0, nb = 0, sm = 0, inb = 0;
-  pair_walk<true>(a, p, nt, nb, sm, inb, tasks + task_begin[p], tkey + task_begin[p], big_begin[p],
-                  small_base + small_begin[p]);
+  PairCounts n{};
+  PairBases b{scans.task[p], scans.light[p], scans.heavy[p], scans.big[p], small_base + scans.small[p]};
+  uint64_t inb[3] = {0, 0, 0};
+  pair_walk<true>(a, p, n, inb, b, light, heavy, tm);
 }
 
-// ---------------------------------------------------------------- the per-task kernel
+// ---------------------------------------------------------------- the per-task kernels
 // Result type of a matched pair (derived from the container implementations):
 //   AND:    R&R -> EFF, else AB                      (RunContainer.java:381-456; BitmapContainer.java:162-188)
 //   OR:     any Bitmap -> LR, A|A -> AB, else EFF     (BitmapContainer.java:1073-1110; RunContainer.java:1926-1986;
 //                                                      ArrayContainer.java:949-973)
 //   XOR:    R^R, R^A(|A|<32) -> EFF, else AB         (RunContainer.java:2410-2482; ArrayContainer.java:1311-1336)
 //   ANDNOT: R\R, R\A(|A|<32) -> EFF, else AB         (RunContainer.java:574-692; BitmapContainer.java:221-274)
+// An AND with an Array operand, or an ANDNOT with an Array on the left, is a subset of that
+// Array, so AB == Array: those run as filters in k_pair_light.
+
+struct RecU { // the wave-uniform view of one TaskRec
+  uint64_t pa, pb, out;
+  uint32_t t, da, db, ra, rb;
+};
+__device__ __forceinline__ RecU load_rec(const TaskRec *r) {
+  RecU u;
+  u.pa = r->pa;
+  u.pb = r->pb;
+  u.out = r->out;
+  u.t = r->t;
+  u.da = r->da;
+  u.db = r->db;
+  u.ra = r->ra;
+  u.rb = r->rb;
+  return u;
+}
+
+// Unmatched containers (cloned unchanged, RoaringArray.appendCopy :184-205) and subset-of-an-Array
+// results.  ONE WAVE PER TASK, few registers, one 8 KiB LDS membership image per wave.
 template <int OP, bool CARD_ONLY>
-__global__ __launch_bounds__(256) void k_pairwise(SetView A, SetView B, const Task *__restrict__ tasks,
-                                                  uint64_t ntasks, uint8_t *__restrict__ out, TaskMeta tm) {
+__global__ __launch_bounds__(256) void k_pair_light(const uint8_t *__restrict__ pay_a,
+                                                    const uint8_t *__restrict__ pay_b,
+                                                    const TaskRec *__restrict__ recs, uint64_t n,
+                                                    uint8_t *__restrict__ out, TaskMeta tm) {
   __shared__ __attribute__((aligned(16))) uint32_t lds[4][2048];
   const int lane = lane_id();
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint64_t t = (uint64_t)blockIdx.x * 4 + wv;
-  if (t >= ntasks) return;
+  const uint64_t g = (uint64_t)blockIdx.x * 4 + wv;
+  if (g >= n) return;
   uint32_t *s = lds[wv];
-  const int32_t ia = __builtin_amdgcn_readfirstlane(tasks[t].ia);
-  const int32_t ib = __builtin_amdgcn_readfirstlane(tasks[t].ib);
-  const uint64_t o = tasks[t].out;
-  if (ia < 0 || ib < 0) { // unmatched container: cloned unchanged (RoaringArray.appendCopy :184-205)
-    const SetView &S = ia >= 0 ? A : B;
-    const int64_t i = ia >= 0 ? ia : ib;
-    const int ty = S.type[i];
-    const uint32_t c = S.card[i], nr = S.nruns[i];
-    if (!CARD_ONLY) copy_payload(S.payload + S.off[i], out + o, payload_bytes(ty, c, nr), lane);
+  const RecU r = load_rec(recs + g);
+  const uint32_t ta = desc_type(r.da), tb = desc_type(r.db);
+  if (ta == kAbsent || tb == kAbsent) {
+    const bool from_a = ta != kAbsent;
+    const uint32_t d = from_a ? r.da : r.db, nr = from_a ? r.ra : r.rb;
+    const int ty = (int)desc_type(d);
+    const uint32_t c = desc_card(d);
+    if (!CARD_ONLY)
+      copy_payload((from_a ? pay_a + r.pa : pay_b + r.pb), out + r.out, payload_bytes(ty, c, nr), lane);
     if (lane == 0) {
-      tm.type[t] = (uint8_t)ty;
-      tm.card[t] = c;
-      tm.nruns[t] = (uint16_t)nr;
+      tm.type[r.t] = (uint8_t)ty;
+      tm.card[r.t] = c;
+      tm.nruns[r.t] = (uint16_t)nr;
     }
     return;
   }
-  const int ta = A.type[ia], tb = B.type[ib];
-  const uint32_t ca = A.card[ia], cb = B.card[ib];
+  const uint32_t ca = desc_card(r.da), cb = desc_card(r.db);
+  // F: the Array whose subset is the result; X: the other operand, staged as a membership image
+  bool f_is_a;
+  if (OP == RB_ANDNOT) f_is_a = true;
+  else if (ta == kArray && tb == kArray) f_is_a = ca <= cb;
+  else f_is_a = ta == kArray;
+  const uint8_t *pf = f_is_a ? pay_a + r.pa : pay_b + r.pb;
+  const uint8_t *px = f_is_a ? pay_b + r.pb : pay_a + r.pa;
+  const int nf = (int)(f_is_a ? ca : cb);
+  const uint32_t tx = f_is_a ? tb : ta, cx = f_is_a ? cb : ca, rx = f_is_a ? r.rb : r.ra;
+  // issue every F load before staging X (one round trip for the whole filter operand)
+  const int nfc = (nf + 7) >> 3;
+  const uint4 *f4 = reinterpret_cast<const uint4 *>(pf);
+  uint4 fq[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int c = lane + 64 * i;
+    fq[i] = c < nfc ? f4[c] : make_uint4(0, 0, 0, 0);
+  }
+  stage_container((int)tx, px, cx, rx, s, lane);
+  uint16_t *dst = CARD_ONLY ? nullptr : reinterpret_cast<uint16_t *>(out + r.out);
+  const int c = filter_chunks<OP == RB_ANDNOT>(fq, nfc, nf, s, dst, lane);
+  if (lane == 0) {
+    tm.type[r.t] = c ? (uint8_t)kArray : kEmpty;
+    tm.card[r.t] = (uint32_t)c;
+    tm.nruns[r.t] = 0;
+  }
+}
+
+// Everything else: ONE WAVE PER TASK, both containers as 65536-bit register bitmaps, word op,
+// card + maximal runs, reference type decision, coalesced emission.
+template <int OP, bool CARD_ONLY>
+__global__ __launch_bounds__(256) void k_pair_heavy(const uint8_t *__restrict__ pay_a,
+                                                    const uint8_t *__restrict__ pay_b,
+                                                    const TaskRec *__restrict__ recs, uint64_t n,
+                                                    uint8_t *__restrict__ out, TaskMeta tm) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds[4][2048];
+  const int lane = lane_id();
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint64_t g = (uint64_t)blockIdx.x * 4 + wv;
+  if (g >= n) return;
+  uint32_t *s = lds[wv];
+  const RecU rc = load_rec(recs + g);
+  const int ta = (int)desc_type(rc.da), tb = (int)desc_type(rc.db);
+  const uint32_t ca = desc_card(rc.da), cb = desc_card(rc.db);
   uint64_t wa[kW], wb[kW];
-  load_container(ta, A.payload + A.off[ia], ca, A.nruns[ia], s, wa, lane);
-  load_container(tb, B.payload + B.off[ib], cb, B.nruns[ib], s, wb, lane);
+  // issue the coalesced Bitmap loads first so they are in flight during any LDS expansion
+  if (ta == kBitmap) load_bitmap(pay_a + rc.pa, wa, lane);
+  if (tb == kBitmap) load_bitmap(pay_b + rc.pb, wb, lane);
+  if (ta != kBitmap) load_container(ta, pay_a + rc.pa, ca, rc.ra, s, wa, lane);
+  if (tb != kBitmap) load_container(tb, pay_b + rc.pb, cb, rc.rb, s, wb, lane);
 #pragma unroll
   for (int j = 0; j < kW; ++j) {
     if (OP == RB_AND) wa[j] &= wb[j];
@@ -186,17 +294,17 @@ __global__ __launch_bounds__(256) void k_pairwise(SetView A, SetView B, const Ta
   } else ty = type_ab(c);
   if (CARD_ONLY) {
     if (lane == 0) {
-      tm.type[t] = c ? (uint8_t)kArray : kEmpty;
-      tm.card[t] = (uint32_t)c;
-      tm.nruns[t] = 0;
+      tm.type[rc.t] = c ? (uint8_t)kArray : kEmpty;
+      tm.card[rc.t] = (uint32_t)c;
+      tm.nruns[rc.t] = 0;
     }
     return;
   }
-  if (ty != kEmpty) emit_container(ty, wa, c, r, out + o, s, lane);
+  if (ty != kEmpty) emit_container(ty, wa, c, r, out + rc.out, s, lane);
   if (lane == 0) {
-    tm.type[t] = (uint8_t)ty;
-    tm.card[t] = (uint32_t)c;
-    tm.nruns[t] = (uint16_t)(ty == kRun ? r : 0);
+    tm.type[rc.t] = (uint8_t)ty;
+    tm.card[rc.t] = (uint32_t)c;
+    tm.nruns[rc.t] = (uint16_t)(ty == kRun ? r : 0);
   }
 }
 
@@ -210,10 +318,10 @@ __global__ __launch_bounds__(kPairThreads) void k_compact_count(const uint64_t *
   cnt[p] = n;
 }
 __global__ __launch_bounds__(kPairThreads) void k_compact_write(const uint64_t *tb, uint32_t npairs, TaskMeta tm,
-                                                                const Task *tasks, const uint64_t *rbegin, OutView out,
+                                                                const uint64_t *rbegin, OutView out,
                                                                 uint64_t *pair_card, uint64_t *stats) {
   const uint32_t p = blockIdx.x * kPairThreads + threadIdx.x;
-  uint64_t outb = 0;
+  uint64_t outb[2] = {0, 0};
   if (p < npairs) {
     uint64_t r = rbegin ? rbegin[p] : 0, card = 0;
     for (uint64_t t = tb[p]; t < tb[p + 1]; ++t) {
@@ -225,47 +333,55 @@ __global__ __launch_bounds__(kPairThreads) void k_compact_write(const uint64_t *
         out.type[r] = ty;
         out.card[r] = tm.card[t];
         out.nruns[r] = tm.nruns[t];
-        out.off[r] = tasks[t].out;
-        outb += alg_bytes(ty, tm.card[t], tm.nruns[t]) + 16;
+        out.off[r] = tm.out[t];
+        outb[tm.cat[t] ? 1 : 0] += alg_bytes(ty, tm.card[t], tm.nruns[t]) + 16;
       }
       ++r;
     }
     if (pair_card) pair_card[p] = card;
   }
-  uint64_t w = wave_sum_u64(outb);
-  if (stats && (threadIdx.x & 63) == 0 && w) atomicAdd((unsigned long long *)&stats[1], (unsigned long long)w);
+  // stats words: 1 total output, 4 light-task output, 5 heavy-task output
+  if (stats) {
+    stat_add(stats, 1, outb[0] + outb[1]);
+    stat_add(stats, 4, outb[0]);
+    stat_add(stats, 5, outb[1]);
+  }
 }
 
 // ---------------------------------------------------------------- launchers
 static unsigned blocks_for(uint64_t n, unsigned per) { return (unsigned)((n + per - 1) / per); }
 
-void launch_pair_count(const PairArgs &a, uint64_t *ntask, uint64_t *nbig, uint64_t *small, uint64_t *stats,
-                       hipStream_t st) {
+void launch_pair_count(const PairArgs &a, const PairCountArrays &c, uint64_t *stats, hipStream_t st) {
   if (!a.npairs) return;
-  k_pair_count<<<blocks_for(a.npairs, kPairThreads), kPairThreads, 0, st>>>(a, ntask, nbig, small, stats);
+  k_pair_count<<<blocks_for(a.npairs, kPairThreads), kPairThreads, 0, st>>>(a, c, stats);
 }
-void launch_pair_emit(const PairArgs &a, const uint64_t *task_begin, const uint64_t *big_begin,
-                      const uint64_t *small_begin, uint64_t small_base, Task *tasks, uint16_t *task_key,
-                      hipStream_t st) {
+void launch_pair_emit(const PairArgs &a, const PairCountArrays &scans, uint64_t small_base, TaskRec *light,
+                      TaskRec *heavy, const TaskMeta &tm, hipStream_t st) {
   if (!a.npairs) return;
-  k_pair_emit<<<blocks_for(a.npairs, kPairThreads), kPairThreads, 0, st>>>(a, task_begin, big_begin, small_begin,
-                                                                           small_base, tasks, task_key);
+  k_pair_emit<<<blocks_for(a.npairs, kPairThreads), kPairThreads, 0, st>>>(a, scans, small_base, light, heavy, tm);
 }
 template <int OP>
-static void launch_op(bool card_only, const SetView &A, const SetView &B, const Task *tasks, uint64_t ntasks,
-                      uint8_t *out, const TaskMeta &tm, hipStream_t st) {
-  const unsigned g = blocks_for(ntasks, 4);
-  if (card_only) k_pairwise<OP, true><<<g, 256, 0, st>>>(A, B, tasks, ntasks, out, tm);
-  else k_pairwise<OP, false><<<g, 256, 0, st>>>(A, B, tasks, ntasks, out, tm);
+static void launch_op(bool card_only, const uint8_t *pa, const uint8_t *pb, const TaskRec *light, uint64_t nl,
+                      const TaskRec *heavy, uint64_t nh, uint8_t *out, const TaskMeta &tm, hipStream_t st,
+                      hipEvent_t mid) {
+  if (nl) {
+    if (card_only) k_pair_light<OP, true><<<blocks_for(nl, 4), 256, 0, st>>>(pa, pb, light, nl, out, tm);
+    else k_pair_light<OP, false><<<blocks_for(nl, 4), 256, 0, st>>>(pa, pb, light, nl, out, tm);
+  }
+  (void)hipEventRecord(mid, st);
+  if (nh) {
+    if (card_only) k_pair_heavy<OP, true><<<blocks_for(nh, 4), 256, 0, st>>>(pa, pb, heavy, nh, out, tm);
+    else k_pair_heavy<OP, false><<<blocks_for(nh, 4), 256, 0, st>>>(pa, pb, heavy, nh, out, tm);
+  }
 }
-void launch_pairwise(int op, bool card_only, const SetView &A, const SetView &B, const Task *tasks, uint64_t ntasks,
-                     uint8_t *out, const TaskMeta &tm, hipStream_t st) {
-  if (!ntasks) return;
+void launch_pairwise(int op, bool card_only, const uint8_t *pa, const uint8_t *pb, const TaskRec *light,
+                     uint64_t nl, const TaskRec *heavy, uint64_t nh, uint8_t *out, const TaskMeta &tm,
+                     hipStream_t st, hipEvent_t mid) {
   switch (op) {
-  case RB_AND: launch_op<RB_AND>(card_only, A, B, tasks, ntasks, out, tm, st); break;
-  case RB_OR: launch_op<RB_OR>(card_only, A, B, tasks, ntasks, out, tm, st); break;
-  case RB_XOR: launch_op<RB_XOR>(card_only, A, B, tasks, ntasks, out, tm, st); break;
-  default: launch_op<RB_ANDNOT>(card_only, A, B, tasks, ntasks, out, tm, st); break;
+  case RB_AND: launch_op<RB_AND>(card_only, pa, pb, light, nl, heavy, nh, out, tm, st, mid); break;
+  case RB_OR: launch_op<RB_OR>(card_only, pa, pb, light, nl, heavy, nh, out, tm, st, mid); break;
+  case RB_XOR: launch_op<RB_XOR>(card_only, pa, pb, light, nl, heavy, nh, out, tm, st, mid); break;
+  default: launch_op<RB_ANDNOT>(card_only, pa, pb, light, nl, heavy, nh, out, tm, st, mid); break;
   }
 }
 void launch_compact_count(const uint64_t *task_begin, uint32_t npairs, const uint8_t *ttype, uint64_t *cnt,
@@ -273,12 +389,11 @@ void launch_compact_count(const uint64_t *task_begin, uint32_t npairs, const uin
   if (!npairs) return;
   k_compact_count<<<blocks_for(npairs, kPairThreads), kPairThreads, 0, st>>>(task_begin, npairs, ttype, cnt);
 }
-void launch_compact_write(const uint64_t *task_begin, uint32_t npairs, const TaskMeta &tm, const Task *tasks,
-                          const uint64_t *rbegin, const OutView &out, uint64_t *pair_card, uint64_t *stats,
-                          hipStream_t st) {
+void launch_compact_write(const uint64_t *task_begin, uint32_t npairs, const TaskMeta &tm, const uint64_t *rbegin,
+                          const OutView &out, uint64_t *pair_card, uint64_t *stats, hipStream_t st) {
   if (!npairs) return;
-  k_compact_write<<<blocks_for(npairs, kPairThreads), kPairThreads, 0, st>>>(task_begin, npairs, tm, tasks, rbegin,
-                                                                             out, pair_card, stats);
+  k_compact_write<<<blocks_for(npairs, kPairThreads), kPairThreads, 0, st>>>(task_begin, npairs, tm, rbegin, out,
+                                                                             pair_card, stats);
 }
 
 } // namespace rbg

@@ -83,12 +83,10 @@ __device__ __forceinline__ void lds_read_words(const uint32_t *s, uint64_t (&w)[
   }
 }
 
-// Sorted u16 array (payload 16-B aligned) -> register bitmap.  Each lane takes 8 consecutive
-// values per 16-B load (coalesced), folds them per 32-bit word and issues one ds_or per word.
-__device__ __forceinline__ void expand_array(const uint16_t *vals, int card, uint32_t *s,
-                                             uint64_t (&w)[kW], int lane) {
-  lds_zero(s, lane);
-  wave_lds_sync();
+// OR the values of a sorted u16 array (payload 16-B aligned) into the LDS bitmap `s`.  Each lane
+// takes 8 consecutive values per 16-B load (coalesced), folds them per 32-bit word and issues
+// one ds_or per word.
+__device__ __forceinline__ void lds_or_array(const uint16_t *vals, int card, uint32_t *s, int lane) {
   const uint4 *v4 = reinterpret_cast<const uint4 *>(vals);
   const int nchunks = (card + 7) >> 3;
   for (int c = lane; c < nchunks; c += 64) {
@@ -111,6 +109,14 @@ __device__ __forceinline__ void expand_array(const uint16_t *vals, int card, uin
     }
     atomicOr(&s[cw], acc);
   }
+}
+
+// Sorted u16 array -> register bitmap (through the LDS scratch).
+__device__ __forceinline__ void expand_array(const uint16_t *vals, int card, uint32_t *s,
+                                             uint64_t (&w)[kW], int lane) {
+  lds_zero(s, lane);
+  wave_lds_sync();
+  lds_or_array(vals, card, s, lane);
   wave_lds_sync();
   lds_read_words(s, w, lane);
   wave_lds_sync();
@@ -169,6 +175,93 @@ __device__ __forceinline__ void load_container(int type, const uint8_t *p, uint3
   if (type == kBitmap) load_bitmap(p, w, lane);
   else if (type == kArray) expand_array(reinterpret_cast<const uint16_t *>(p), (int)card, s, w, lane);
   else expand_runs(reinterpret_cast<const uint16_t *>(p), (int)nruns, s, w, lane);
+}
+
+__device__ __forceinline__ void lds_write_words(uint32_t *s, const uint64_t (&w)[kW], int lane) {
+  uint4 *s4 = reinterpret_cast<uint4 *>(s);
+#pragma unroll
+  for (int k = 0; k < 8; ++k)
+    s4[k * 64 + lane] = make_uint4((uint32_t)w[2 * k], (uint32_t)(w[2 * k] >> 32), (uint32_t)w[2 * k + 1],
+                                   (uint32_t)(w[2 * k + 1] >> 32));
+}
+
+// Any container -> membership bitmap in the wave's LDS scratch (bit v of the 65536-bit image).
+__device__ __forceinline__ void stage_container(int type, const uint8_t *p, uint32_t card, uint32_t nruns,
+                                                uint32_t *s, int lane) {
+  if (type == kBitmap) {
+    const uint4 *q = reinterpret_cast<const uint4 *>(p);
+    uint4 v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = q[k * 64 + lane];
+    uint4 *s4 = reinterpret_cast<uint4 *>(s);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) s4[k * 64 + lane] = v[k];
+  } else if (type == kArray) {
+    lds_zero(s, lane);
+    wave_lds_sync();
+    lds_or_array(reinterpret_cast<const uint16_t *>(p), (int)card, s, lane);
+  } else {
+    uint64_t w[kW];
+    expand_runs(reinterpret_cast<const uint16_t *>(p), (int)nruns, s, w, lane);
+    lds_write_words(s, w, lane);
+  }
+  wave_lds_sync();
+}
+
+// Filter a sorted u16 array F against the LDS membership image `s`: keep the values whose bit
+// equals !NEGATE.  F is preloaded as up to 8 uint4 chunks per lane (chunk c = lane + 64*i holds
+// values 8c..8c+7; nfc chunks, nf values).  Kept values are written in order to `out` (unless
+// null); returns their count (wave-uniform).  This is the whole of A&x, x&A and A\x: the result
+// is a subset of an Array, hence an Array (ArrayContainer.and/andNot, BitmapContainer.and(Array),
+// RunContainer.and(Array): ArrayContainer.java:184-271, BitmapContainer.java:162-172,
+// RunContainer.java:305-336).
+template <bool NEGATE>
+__device__ __forceinline__ int filter_chunks(const uint4 (&fq)[8], int nfc, int nf, const uint32_t *s, uint16_t *out,
+                                             int lane) {
+  const int iters = (nfc + 63) >> 6; // wave-uniform, <= 8
+  uint32_t keep[8];
+  uint64_t P0 = 0, P1 = 0; // per-iteration kept counts, 10-bit fields (<= 512 per iteration)
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    keep[i] = 0;
+    if (i < iters) {
+      const int c = lane + 64 * i;
+      const int n = c < nfc ? min(8, nf - 8 * c) : 0;
+      const uint32_t x[8] = {fq[i].x & 0xFFFF, fq[i].x >> 16, fq[i].y & 0xFFFF, fq[i].y >> 16,
+                             fq[i].z & 0xFFFF, fq[i].z >> 16, fq[i].w & 0xFFFF, fq[i].w >> 16};
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const uint32_t m = (s[x[k] >> 5] >> (x[k] & 31)) & 1;
+        if (k < n && (m ^ (NEGATE ? 1u : 0u))) keep[i] |= 1u << k;
+      }
+      const uint64_t cnt = (uint64_t)__popc(keep[i]);
+      if (i < 6) P0 |= cnt << (10 * i);
+      else P1 |= cnt << (10 * (i - 6));
+    }
+  }
+  const uint64_t S0 = wave_scan_u64(P0, lane);
+  const uint64_t S1 = iters > 6 ? wave_scan_u64(P1, lane) : 0;
+  const uint64_t T0 = (uint64_t)__shfl((unsigned long long)S0, 63);
+  const uint64_t T1 = iters > 6 ? (uint64_t)__shfl((unsigned long long)S1, 63) : 0;
+  uint32_t total = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    if (i < iters) {
+      const uint64_t S = i < 6 ? S0 : S1, P = i < 6 ? P0 : P1, T = i < 6 ? T0 : T1;
+      const int sh = 10 * (i < 6 ? i : i - 6);
+      const uint32_t excl = (uint32_t)(((S - P) >> sh) & 0x3FF);
+      if (out) {
+        uint32_t pos = total + excl;
+        const uint32_t x[8] = {fq[i].x & 0xFFFF, fq[i].x >> 16, fq[i].y & 0xFFFF, fq[i].y >> 16,
+                               fq[i].z & 0xFFFF, fq[i].z >> 16, fq[i].w & 0xFFFF, fq[i].w >> 16};
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+          if ((keep[i] >> k) & 1) out[pos++] = (uint16_t)x[k];
+      }
+      total += (uint32_t)((T >> sh) & 0x3FF);
+    }
+  }
+  return (int)total;
 }
 
 // ---------------------------------------------------------------- metrics

@@ -230,7 +230,12 @@ class Context:
     def stats(self) -> dict:
         s = L.RbStats()
         L.check(L.lib().rbgpu_get_stats(self.h, C.byref(s)))
-        return {k: (getattr(s, k).decode() if k == "main_kernel" else getattr(s, k)) for k, _ in s._fields_}
+        out = {k: getattr(s, k) for k, _ in s._fields_ if not k.startswith("kernel_")}
+        out["main_kernel"] = s.main_kernel.decode()
+        out["kernels"] = [{"name": s.kernel_name[i].value.decode(), "ms": s.kernel_ms[i],
+                           "bytes": int(s.kernel_bytes[i]), "items": int(s.kernel_items[i])}
+                          for i in range(s.n_kernels)]
+        return out
 
     # ---- sets
     def upload_serialized(self, blobs: Sequence[bytes]) -> DeviceSet:
