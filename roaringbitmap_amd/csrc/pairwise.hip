@@ -172,6 +172,11 @@ __global__ __launch_bounds__(kPairThreads) void k_pair_emit(PairArgs a, PairCoun
 // An AND with an Array operand, or an ANDNOT with an Array on the left, is a subset of that
 // Array, so AB == Array: those run as filters in k_pair_light.
 
+// Out of line: keeps the rare > 2047-run staging from inflating the pipelined kernel's registers.
+__device__ __noinline__ void stage_big_runs(const uint8_t *p, uint32_t nruns, uint32_t *s, int lane) {
+  stage_container(kRun, p, 0, nruns, s, lane);
+}
+
 struct RecU { // the wave-uniform view of one TaskRec
   uint64_t pa, pb, out;
   uint32_t t, da, db, ra, rb;
@@ -189,8 +194,59 @@ __device__ __forceinline__ RecU load_rec(const TaskRec *r) {
   return u;
 }
 
+// Decoded light task: F is the Array whose subset is the result (or the payload to clone), X the
+// operand staged as a membership image.
+struct LightTask {
+  bool copy, big;      // big: a payload exceeds 8 KiB (Run with > 2047 runs) -> direct path
+  const uint8_t *pf, *px;
+  uint32_t fbytes, xbytes, nf, cx, rx;
+  int tx;
+  int cty;             // copy: type, card, runs of the clone
+  uint32_t ccard, cnr;
+};
+template <int OP>
+__device__ __forceinline__ LightTask decode_light(const RecU &r, const uint8_t *pay_a, const uint8_t *pay_b) {
+  LightTask L;
+  const uint32_t ta = desc_type(r.da), tb = desc_type(r.db);
+  L.copy = ta == kAbsent || tb == kAbsent;
+  if (L.copy) {
+    const bool from_a = ta != kAbsent;
+    const uint32_t d = from_a ? r.da : r.db;
+    L.cty = (int)desc_type(d);
+    L.ccard = desc_card(d);
+    L.cnr = from_a ? r.ra : r.rb;
+    L.pf = from_a ? pay_a + r.pa : pay_b + r.pb;
+    L.fbytes = (uint32_t)payload_bytes(L.cty, L.ccard, L.cnr);
+    L.px = nullptr;
+    L.xbytes = 0;
+    L.nf = L.cx = L.rx = 0;
+    L.tx = 0;
+    L.big = L.fbytes > (uint32_t)kBitmapBytes;
+    return L;
+  }
+  const uint32_t ca = desc_card(r.da), cb = desc_card(r.db);
+  bool f_is_a;
+  if (OP == RB_ANDNOT) f_is_a = true;
+  else if (ta == kArray && tb == kArray) f_is_a = ca <= cb;
+  else f_is_a = ta == kArray;
+  L.pf = f_is_a ? pay_a + r.pa : pay_b + r.pb;
+  L.px = f_is_a ? pay_b + r.pb : pay_a + r.pa;
+  L.nf = f_is_a ? ca : cb;
+  L.fbytes = 2 * L.nf;
+  L.tx = (int)(f_is_a ? tb : ta);
+  L.cx = f_is_a ? cb : ca;
+  L.rx = f_is_a ? r.rb : r.ra;
+  L.xbytes = (uint32_t)payload_bytes(L.tx, L.cx, L.rx);
+  L.big = L.xbytes > (uint32_t)kBitmapBytes;
+  L.cty = 0;
+  L.ccard = L.cnr = 0;
+  return L;
+}
+
 // Unmatched containers (cloned unchanged, RoaringArray.appendCopy :184-205) and subset-of-an-Array
-// results.  ONE WAVE PER TASK, few registers, one 8 KiB LDS membership image per wave.
+// results.  Persistent waves walk the task list with a one-task software pipeline: the next
+// task's record and both payloads (<= 8 KiB each, 8 x 16 B per lane) are in flight while the
+// current X is staged as an 8 KiB LDS membership image and the current F is filtered.
 template <int OP, bool CARD_ONLY>
 __global__ __launch_bounds__(256) void k_pair_light(const uint8_t *__restrict__ pay_a,
                                                     const uint8_t *__restrict__ pay_b,
@@ -199,51 +255,62 @@ __global__ __launch_bounds__(256) void k_pair_light(const uint8_t *__restrict__ 
   __shared__ __attribute__((aligned(16))) uint32_t lds[4][2048];
   const int lane = lane_id();
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint64_t g = (uint64_t)blockIdx.x * 4 + wv;
+  const uint64_t stride = (uint64_t)gridDim.x * 4;
+  uint64_t g = (uint64_t)blockIdx.x * 4 + wv;
   if (g >= n) return;
   uint32_t *s = lds[wv];
-  const RecU r = load_rec(recs + g);
-  const uint32_t ta = desc_type(r.da), tb = desc_type(r.db);
-  if (ta == kAbsent || tb == kAbsent) {
-    const bool from_a = ta != kAbsent;
-    const uint32_t d = from_a ? r.da : r.db, nr = from_a ? r.ra : r.rb;
-    const int ty = (int)desc_type(d);
-    const uint32_t c = desc_card(d);
-    if (!CARD_ONLY)
-      copy_payload((from_a ? pay_a + r.pa : pay_b + r.pb), out + r.out, payload_bytes(ty, c, nr), lane);
-    if (lane == 0) {
-      tm.type[r.t] = (uint8_t)ty;
-      tm.card[r.t] = c;
-      tm.nruns[r.t] = (uint16_t)nr;
+  RecU cur = load_rec(recs + g);
+  LightTask pc = decode_light<OP>(cur, pay_a, pay_b);
+  uint4 fq[8], xq[8];
+  if (!pc.big) {
+    load_chunks(fq, pc.pf, pc.fbytes, lane);
+    if (!pc.copy) load_chunks(xq, pc.px, pc.xbytes, lane);
+  }
+  while (true) {
+    const uint64_t gn = g + stride;
+    const bool has_next = gn < n;
+    const RecU nx = load_rec(recs + (has_next ? gn : g));
+    const LightTask pn = decode_light<OP>(nx, pay_a, pay_b);
+    const bool pre = has_next && !pn.big;
+    int ty, c;
+    uint32_t nr = 0;
+    if (pc.copy) {
+      if (!CARD_ONLY) {
+        if (pc.big) copy_payload(pc.pf, out + cur.out, pc.fbytes, lane);
+        else store_chunks(fq, out + cur.out, pc.fbytes, lane);
+      }
+      ty = pc.cty;
+      c = (int)pc.ccard;
+      nr = pc.cnr;
+      if (pre) {
+        load_chunks(fq, pn.pf, pn.fbytes, lane);
+        if (!pn.copy) load_chunks(xq, pn.px, pn.xbytes, lane);
+      }
+    } else {
+      if (pc.big) {
+        load_chunks(fq, pc.pf, pc.fbytes, lane);
+        stage_big_runs(pc.px, pc.rx, s, lane); // only a Run payload exceeds 8 KiB
+      } else {
+        stage_from_chunks(pc.tx, xq, pc.cx, pc.rx, s, lane);
+      }
+      if (pre && !pn.copy) load_chunks(xq, pn.px, pn.xbytes, lane);
+      uint16_t *dst = CARD_ONLY ? nullptr : reinterpret_cast<uint16_t *>(out + cur.out);
+      const int nfc = (int)((pc.nf + 7) >> 3);
+      c = OP == RB_ANDNOT ? filter_chunks<true>(fq, nfc, (int)pc.nf, s, dst, lane)
+                          : filter_chunks<false>(fq, nfc, (int)pc.nf, s, dst, lane);
+      ty = c ? kArray : kEmpty;
+      if (pre) load_chunks(fq, pn.pf, pn.fbytes, lane);
+      wave_lds_sync(); // the next task restages the same LDS image
     }
-    return;
-  }
-  const uint32_t ca = desc_card(r.da), cb = desc_card(r.db);
-  // F: the Array whose subset is the result; X: the other operand, staged as a membership image
-  bool f_is_a;
-  if (OP == RB_ANDNOT) f_is_a = true;
-  else if (ta == kArray && tb == kArray) f_is_a = ca <= cb;
-  else f_is_a = ta == kArray;
-  const uint8_t *pf = f_is_a ? pay_a + r.pa : pay_b + r.pb;
-  const uint8_t *px = f_is_a ? pay_b + r.pb : pay_a + r.pa;
-  const int nf = (int)(f_is_a ? ca : cb);
-  const uint32_t tx = f_is_a ? tb : ta, cx = f_is_a ? cb : ca, rx = f_is_a ? r.rb : r.ra;
-  // issue every F load before staging X (one round trip for the whole filter operand)
-  const int nfc = (nf + 7) >> 3;
-  const uint4 *f4 = reinterpret_cast<const uint4 *>(pf);
-  uint4 fq[8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int c = lane + 64 * i;
-    fq[i] = c < nfc ? f4[c] : make_uint4(0, 0, 0, 0);
-  }
-  stage_container((int)tx, px, cx, rx, s, lane);
-  uint16_t *dst = CARD_ONLY ? nullptr : reinterpret_cast<uint16_t *>(out + r.out);
-  const int c = filter_chunks<OP == RB_ANDNOT>(fq, nfc, nf, s, dst, lane);
-  if (lane == 0) {
-    tm.type[r.t] = c ? (uint8_t)kArray : kEmpty;
-    tm.card[r.t] = (uint32_t)c;
-    tm.nruns[r.t] = 0;
+    if (lane == 0) {
+      tm.type[cur.t] = (uint8_t)ty;
+      tm.card[cur.t] = (uint32_t)c;
+      tm.nruns[cur.t] = (uint16_t)nr;
+    }
+    if (!has_next) break;
+    g = gn;
+    cur = nx;
+    pc = pn;
   }
 }
 
@@ -360,13 +427,30 @@ void launch_pair_emit(const PairArgs &a, const PairCountArrays &scans, uint64_t 
   if (!a.npairs) return;
   k_pair_emit<<<blocks_for(a.npairs, kPairThreads), kPairThreads, 0, st>>>(a, scans, small_base, light, heavy, tm);
 }
+// Persistent grid: every CU filled to the kernel's occupancy, waves stride over the tasks.
+template <class K> static unsigned persistent_blocks(K kernel, uint64_t tasks) {
+  static int cus = 0, occ = 0;
+  if (!cus) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kernel, 256, 0);
+    if (cus <= 0) cus = 256;
+    if (occ <= 0) occ = 4;
+  }
+  const uint64_t want = (tasks + 3) / 4, cap = (uint64_t)cus * (uint64_t)occ;
+  return (unsigned)(want < cap ? want : cap);
+}
+
 template <int OP>
 static void launch_op(bool card_only, const uint8_t *pa, const uint8_t *pb, const TaskRec *light, uint64_t nl,
                       const TaskRec *heavy, uint64_t nh, uint8_t *out, const TaskMeta &tm, hipStream_t st,
                       hipEvent_t mid) {
   if (nl) {
-    if (card_only) k_pair_light<OP, true><<<blocks_for(nl, 4), 256, 0, st>>>(pa, pb, light, nl, out, tm);
-    else k_pair_light<OP, false><<<blocks_for(nl, 4), 256, 0, st>>>(pa, pb, light, nl, out, tm);
+    if (card_only)
+      k_pair_light<OP, true><<<persistent_blocks(k_pair_light<OP, true>, nl), 256, 0, st>>>(pa, pb, light, nl, out, tm);
+    else
+      k_pair_light<OP, false><<<persistent_blocks(k_pair_light<OP, false>, nl), 256, 0, st>>>(pa, pb, light, nl, out, tm);
   }
   (void)hipEventRecord(mid, st);
   if (nh) {

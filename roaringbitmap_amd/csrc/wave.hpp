@@ -83,6 +83,14 @@ __device__ __forceinline__ void lds_read_words(const uint32_t *s, uint64_t (&w)[
   }
 }
 
+__device__ __forceinline__ void lds_write_words(uint32_t *s, const uint64_t (&w)[kW], int lane) {
+  uint4 *s4 = reinterpret_cast<uint4 *>(s);
+#pragma unroll
+  for (int k = 0; k < 8; ++k)
+    s4[k * 64 + lane] = make_uint4((uint32_t)w[2 * k], (uint32_t)(w[2 * k] >> 32), (uint32_t)w[2 * k + 1],
+                                   (uint32_t)(w[2 * k + 1] >> 32));
+}
+
 // OR the values of a sorted u16 array (payload 16-B aligned) into the LDS bitmap `s`.  Each lane
 // takes 8 consecutive values per 16-B load (coalesced), folds them per 32-bit word and issues
 // one ds_or per word.
@@ -132,23 +140,9 @@ __device__ __forceinline__ uint64_t prefix_xor64(uint64_t x) {
   return x;
 }
 
-// Run list ((start, len-1) u16 pairs) -> register bitmap: toggle bit `start` and bit
-// `start+len` (end+1) of every run into LDS, then membership = prefix-xor of the toggles.
-__device__ __forceinline__ void expand_runs(const uint16_t *runs, int nruns, uint32_t *s,
-                                            uint64_t (&w)[kW], int lane) {
-  lds_zero(s, lane);
-  wave_lds_sync();
-  const uint32_t *r32 = reinterpret_cast<const uint32_t *>(runs);
-  for (int i = lane; i < nruns; i += 64) {
-    uint32_t q = r32[i];
-    uint32_t st = q & 0xFFFF, e1 = st + (q >> 16) + 1;
-    atomicXor(&s[st >> 5], 1u << (st & 31));
-    if (e1 < (uint32_t)kSpan) atomicXor(&s[e1 >> 5], 1u << (e1 & 31));
-  }
-  wave_lds_sync();
-  uint64_t t[kW];
-  lds_read_words(s, t, lane);
-  wave_lds_sync();
+// Toggle image (bit `start` and bit `end+1` of every run set in t) -> membership words:
+// in-register prefix-xor per word plus a wave parity scan for the carry into each word.
+__device__ __forceinline__ void toggles_to_words(uint64_t (&t)[kW], int lane) { // in place
   uint32_t q = 0, p0 = 0;
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
@@ -164,9 +158,29 @@ __device__ __forceinline__ void expand_runs(const uint16_t *runs, int nruns, uin
     uint32_t rowc = __popc(tot & ((1u << k) - 1)) & 1;
     uint32_t c0 = rowc ^ ((excl >> k) & 1);
     uint32_t c1 = c0 ^ ((p0 >> k) & 1);
-    w[2 * k] = prefix_xor64(t[2 * k]) ^ (c0 ? ~0ull : 0ull);
-    w[2 * k + 1] = prefix_xor64(t[2 * k + 1]) ^ (c1 ? ~0ull : 0ull);
+    t[2 * k] = prefix_xor64(t[2 * k]) ^ (c0 ? ~0ull : 0ull);
+    t[2 * k + 1] = prefix_xor64(t[2 * k + 1]) ^ (c1 ? ~0ull : 0ull);
   }
+}
+
+__device__ __forceinline__ void toggle_run(uint32_t *s, uint32_t q) {
+  const uint32_t st = q & 0xFFFF, e1 = st + (q >> 16) + 1;
+  atomicXor(&s[st >> 5], 1u << (st & 31));
+  if (e1 < (uint32_t)kSpan) atomicXor(&s[e1 >> 5], 1u << (e1 & 31));
+}
+
+// Run list ((start, len-1) u16 pairs) -> register bitmap: toggle bit `start` and bit
+// `start+len` (end+1) of every run into LDS, then membership = prefix-xor of the toggles.
+__device__ __forceinline__ void expand_runs(const uint16_t *runs, int nruns, uint32_t *s,
+                                            uint64_t (&w)[kW], int lane) {
+  lds_zero(s, lane);
+  wave_lds_sync();
+  const uint32_t *r32 = reinterpret_cast<const uint32_t *>(runs);
+  for (int i = lane; i < nruns; i += 64) toggle_run(s, r32[i]);
+  wave_lds_sync();
+  lds_read_words(s, w, lane);
+  wave_lds_sync();
+  toggles_to_words(w, lane);
 }
 
 // Any container -> register bitmap.
@@ -175,14 +189,6 @@ __device__ __forceinline__ void load_container(int type, const uint8_t *p, uint3
   if (type == kBitmap) load_bitmap(p, w, lane);
   else if (type == kArray) expand_array(reinterpret_cast<const uint16_t *>(p), (int)card, s, w, lane);
   else expand_runs(reinterpret_cast<const uint16_t *>(p), (int)nruns, s, w, lane);
-}
-
-__device__ __forceinline__ void lds_write_words(uint32_t *s, const uint64_t (&w)[kW], int lane) {
-  uint4 *s4 = reinterpret_cast<uint4 *>(s);
-#pragma unroll
-  for (int k = 0; k < 8; ++k)
-    s4[k * 64 + lane] = make_uint4((uint32_t)w[2 * k], (uint32_t)(w[2 * k] >> 32), (uint32_t)w[2 * k + 1],
-                                   (uint32_t)(w[2 * k + 1] >> 32));
 }
 
 // Any container -> membership bitmap in the wave's LDS scratch (bit v of the 65536-bit image).
@@ -262,6 +268,82 @@ __device__ __forceinline__ int filter_chunks(const uint4 (&fq)[8], int nfc, int 
     }
   }
   return (int)total;
+}
+
+// ---------------------------------------------------------------- register-preloaded payloads
+// A payload of at most 8 KiB as 8 uint4 per lane: chunk c = lane + 64*i (16 bytes) in q[i].
+__device__ __forceinline__ void load_chunks(uint4 (&q)[8], const uint8_t *p, uint32_t bytes, int lane) {
+  const uint4 *p4 = reinterpret_cast<const uint4 *>(p);
+  const int n = (int)((bytes + 15) >> 4);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int c = lane + 64 * i;
+    q[i] = c < n ? p4[c] : make_uint4(0, 0, 0, 0);
+  }
+}
+__device__ __forceinline__ void store_chunks(const uint4 (&q)[8], uint8_t *p, uint32_t bytes, int lane) {
+  uint4 *p4 = reinterpret_cast<uint4 *>(p);
+  const int n = (int)((bytes + 15) >> 4);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int c = lane + 64 * i;
+    if (c < n) p4[c] = q[i];
+  }
+}
+
+// Membership image in LDS from a register-preloaded payload (Array <= 4096 values, Run <= 2047
+// runs, Bitmap 8 KiB — i.e. every canonical container whose payload fits 8 KiB).
+__device__ __forceinline__ void stage_from_chunks(int type, const uint4 (&q)[8], uint32_t card, uint32_t nruns,
+                                                  uint32_t *s, int lane) {
+  uint4 *s4 = reinterpret_cast<uint4 *>(s);
+  if (type == kBitmap) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) s4[i * 64 + lane] = q[i];
+  } else {
+    lds_zero(s, lane);
+    wave_lds_sync();
+    if (type == kArray) {
+      const int nchunks = (int)((card + 7) >> 3);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int c = lane + 64 * i;
+        if (c < nchunks) {
+          const uint32_t x[8] = {q[i].x & 0xFFFF, q[i].x >> 16, q[i].y & 0xFFFF, q[i].y >> 16,
+                                 q[i].z & 0xFFFF, q[i].z >> 16, q[i].w & 0xFFFF, q[i].w >> 16};
+          const int n = min(8, (int)card - 8 * c);
+          uint32_t cw = x[0] >> 5, acc = 0;
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            if (k < n) {
+              const uint32_t wi = x[k] >> 5;
+              if (wi != cw) {
+                atomicOr(&s[cw], acc);
+                cw = wi;
+                acc = 0;
+              }
+              acc |= 1u << (x[k] & 31);
+            }
+          }
+          atomicOr(&s[cw], acc);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const uint32_t base = 4u * (uint32_t)(lane + 64 * i);
+        const uint32_t r[4] = {q[i].x, q[i].y, q[i].z, q[i].w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          if (base + k < nruns) toggle_run(s, r[k]);
+      }
+      wave_lds_sync();
+      uint64_t w[kW];
+      lds_read_words(s, w, lane);
+      toggles_to_words(w, lane);
+      lds_write_words(s, w, lane); // each lane rewrites only the words it read
+    }
+  }
+  wave_lds_sync();
 }
 
 // ---------------------------------------------------------------- metrics

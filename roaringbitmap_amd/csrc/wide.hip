@@ -1,10 +1,477 @@
-// wide.hip — wide FastAggregation / ParallelAggregation over many bitmaps (filled in below).
+// wide.hip — wide aggregation over many bitmaps: FastAggregation.or/and/xor, naive_and,
+// workShyAnd and ParallelAggregation.or/xor (FastAggregation.java:26-42, 328-396, 541-582,
+// 602, 772; ParallelAggregation.java:137-229).
+//
+// Every high-16-bit key is independent.  Pipeline:
+//   k_wide_flatten   one thread per input container of the member list -> (key, container id)
+//   radix sort       stable by key (rocPRIM), so each key's containers stay in member order —
+//                    the order that naive_and / naive_xor / the ParallelAggregation chains depend on
+//   k_wide_bounds    per key segment [begin, end) in the sorted list
+//   k_wide_select    keys that produce work (any container; for AND: present in every member)
+//   k_wide_reduce    ONE WAVE PER KEY: the key's containers folded in registers (65536-bit
+//                    register bitmap, Bitmaps streamed two at a time), reference type decision,
+//                    emission into an 8 KiB slot
+//   compaction       drop empty results, result CSR
+#include <cstring>
+
+#include <rocprim/rocprim.hpp>
+
 #include "internal.hpp"
 #include "kernels.hpp"
+#include "wave.hpp"
 
 namespace rbg {
-int wide_run(rbgpu_ctx *ctx, int sem, const rbgpu_set *in, const std::vector<uint32_t> &members, rbgpu_set **out) {
-  (void)ctx; (void)sem; (void)in; (void)members; (void)out;
-  return fail(RB_EINVAL, "wide aggregation not implemented yet");
+
+struct WideOut {
+  uint8_t *type;   // per active key, kEmpty if dropped
+  uint32_t *card;
+  uint16_t *nruns;
+};
+
+__device__ __forceinline__ uint64_t alg_bytes_w(int t, uint32_t c, uint32_t r) {
+  return t == kBitmap ? 8192ull : t == kArray ? 2ull * c : 4ull * r + 2;
 }
+__device__ __forceinline__ void stat_add_w(uint64_t *stats, int word, uint64_t v) {
+  if ((threadIdx.x & 63) == 0 && v) {
+    const int stripe = (blockIdx.x * 4 + (threadIdx.x >> 6)) & (kStripes - 1);
+    atomicAdd((unsigned long long *)&stats[word * kStripes + stripe], (unsigned long long)v);
+  }
+}
+
+__global__ __launch_bounds__(256) void k_wide_flatten(SetView s, const uint32_t *mem, const uint64_t *mstart,
+                                                      uint32_t M, uint64_t N, uint16_t *keys, uint32_t *cid) {
+  const uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (j >= N) return;
+  uint32_t lo = 0, hi = M; // last m with mstart[m] <= j
+  while (hi - lo > 1) {
+    uint32_t mid = (lo + hi) >> 1;
+    if (mstart[mid] <= j) lo = mid;
+    else hi = mid;
+  }
+  const uint64_t c = s.begin[mem[lo]] + (j - mstart[lo]);
+  keys[j] = s.key[c];
+  cid[j] = (uint32_t)c;
+}
+
+// seg[k] = first index of key k in the sorted key list (k = 0..65536)
+__global__ __launch_bounds__(256) void k_wide_bounds(const uint16_t *sorted, uint64_t N, uint64_t *seg) {
+  const uint32_t k = blockIdx.x * 256 + threadIdx.x;
+  if (k > 65536) return;
+  uint64_t lo = 0, hi = N;
+  while (lo < hi) {
+    uint64_t mid = (lo + hi) >> 1;
+    if (sorted[mid] < k) lo = mid + 1;
+    else hi = mid;
+  }
+  seg[k] = lo;
+}
+
+// active[k] = 1 when key k produces work: any container, or (AND semantics) one per member
+__global__ __launch_bounds__(256) void k_wide_select(const uint64_t *seg, uint64_t need, uint64_t *active) {
+  const uint32_t k = blockIdx.x * 256 + threadIdx.x;
+  if (k >= 65536) return;
+  const uint64_t m = seg[k + 1] - seg[k];
+  active[k] = need ? (m == need) : (m > 0);
+}
+__global__ __launch_bounds__(256) void k_wide_list(const uint64_t *active, const uint64_t *pos, uint32_t *klist) {
+  const uint32_t k = blockIdx.x * 256 + threadIdx.x;
+  if (k >= 65536) return;
+  if (active[k]) klist[pos[k]] = k;
+}
+
+// ---------------------------------------------------------------- per-key folding helpers
+struct CRef {
+  int type;
+  uint32_t card, nruns;
+  const uint8_t *p;
+};
+__device__ __forceinline__ CRef cref(const SetView &s, uint32_t c) {
+  CRef r;
+  r.type = s.type[c];
+  r.card = s.card[c];
+  r.nruns = s.nruns[c];
+  r.p = s.payload + s.off[c];
+  return r;
+}
+
+template <int OP> __device__ __forceinline__ void fold(uint64_t (&acc)[kW], const uint64_t (&x)[kW]) {
+#pragma unroll
+  for (int j = 0; j < kW; ++j) {
+    if (OP == RB_AND) acc[j] &= x[j];
+    else if (OP == RB_OR) acc[j] |= x[j];
+    else acc[j] ^= x[j];
+  }
+}
+
+// Fold every container of [lo, hi) into acc with OP; Bitmaps are streamed two per step so 16
+// coalesced 1 KiB loads per wave are in flight.  Returns algorithmic bytes read.
+template <int OP>
+__device__ __forceinline__ uint64_t fold_all(const SetView &s, const uint32_t *cid, uint64_t lo, uint64_t hi,
+                                             uint64_t (&acc)[kW], uint32_t *lds, int lane) {
+  uint64_t bytes = 0;
+  uint64_t i = lo;
+  while (i < hi) {
+    const CRef a = cref(s, cid[i]);
+    bytes += alg_bytes_w(a.type, a.card, a.nruns) + 16;
+    if (a.type == kBitmap && i + 1 < hi) {
+      const CRef b = cref(s, cid[i + 1]);
+      if (b.type == kBitmap) {
+        bytes += 8192 + 16;
+        uint64_t x[kW], y[kW];
+        load_bitmap(a.p, x, lane);
+        load_bitmap(b.p, y, lane);
+        fold<OP>(acc, x);
+        fold<OP>(acc, y);
+        i += 2;
+        continue;
+      }
+    }
+    uint64_t x[kW];
+    load_container(a.type, a.p, a.card, a.nruns, lds, x, lane);
+    fold<OP>(acc, x);
+    i += 1;
+  }
+  return bytes;
+}
+
+__device__ __forceinline__ int type_xor_step(int ta, int tb, uint32_t ca, uint32_t cb, int c, int r) {
+  // RunContainer.xor / ArrayContainer.xor / BitmapContainer.xor types
+  if ((ta == kRun && tb == kRun) || (ta == kArray && tb == kRun && ca < (uint32_t)kRunArrayThreshold) ||
+      (ta == kRun && tb == kArray && cb < (uint32_t)kRunArrayThreshold))
+    return type_eff(c, r);
+  return type_ab(c);
+}
+
+// lazyIOR chain states (Container.lazyIOR, Container.java:717-740)
+enum { kStA = 0, kStBValid = 1, kStRun = 2, kStBLazy = 3 };
+
+template <int SEM>
+__global__ __launch_bounds__(256) void k_wide_reduce(SetView s, const uint32_t *__restrict__ cid,
+                                                     const uint64_t *__restrict__ seg, const uint32_t *__restrict__ klist,
+                                                     uint32_t nk, uint8_t *__restrict__ out, WideOut wo,
+                                                     uint64_t *stats) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds_all[4][2048];
+  const int lane = lane_id();
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t q = blockIdx.x * 4 + wv;
+  if (q >= nk) return;
+  uint32_t *lds = lds_all[wv];
+  const uint32_t key = klist[q];
+  const uint64_t lo = seg[key], hi = seg[key + 1];
+  const uint64_t m = hi - lo;
+  uint8_t *dst = out + (uint64_t)q * kBitmapBytes;
+  uint64_t acc[kW];
+  uint64_t inb = 0;
+  int ty = kEmpty, c = 0, r = 0;
+
+  if ((SEM == RB_FAST_OR || SEM == RB_PAR_OR) && m == 1) {
+    // a key seen once: clone, then repairAfterLazy (A, B unchanged; Run -> toEfficientContainer)
+    const CRef a = cref(s, cid[lo]);
+    inb = alg_bytes_w(a.type, a.card, a.nruns) + 16;
+    if (a.type != kRun || 2 + 4 * (int)a.nruns <= min(kBitmapBytes, 2 * (int)a.card + 2)) {
+      copy_payload(a.p, dst, payload_bytes(a.type, a.card, a.nruns), lane);
+      ty = a.type;
+      c = (int)a.card;
+      r = (int)a.nruns;
+    } else {
+      load_container(a.type, a.p, a.card, a.nruns, lds, acc, lane);
+      c = (int)a.card;
+      r = (int)a.nruns;
+      ty = type_ab(c);
+      emit_container(ty, acc, c, r, dst, lds, lane);
+    }
+  } else if (SEM == RB_FAST_OR || (SEM == RB_PAR_OR && m >= 16)) {
+    // naive_or: BitmapContainer.lazyIOR over everything, then repairAfterLazy -> LR(c)
+#pragma unroll
+    for (int j = 0; j < kW; ++j) acc[j] = 0;
+    inb = fold_all<RB_OR>(s, cid, lo, hi, acc, lds, lane);
+    metrics(acc, lane, false, c, r);
+    ty = type_lr(c);
+    if (ty == kRun) r = 1;
+    emit_container(ty, acc, c, r, dst, lds, lane);
+  } else if (SEM == RB_WORKSHY_AND) {
+    // workShyAnd: all-ones lazy BitmapContainer.iand over the key's containers, repair -> LR(c)
+#pragma unroll
+    for (int j = 0; j < kW; ++j) acc[j] = ~0ull;
+    inb = fold_all<RB_AND>(s, cid, lo, hi, acc, lds, lane);
+    metrics(acc, lane, false, c, r);
+    ty = c ? type_lr(c) : kEmpty;
+    if (ty == kRun) r = 1;
+    if (ty != kEmpty) emit_container(ty, acc, c, r, dst, lds, lane);
+  } else if (SEM == RB_NAIVE_AND || SEM == RB_NAIVE_AND_ITER) {
+    // clone of the first (smallest) bitmap's container, then in-place and() in member order:
+    // R&R -> EFF, otherwise AB; the key disappears once empty (RoaringBitmap.and(x2) :1272-1296)
+    const CRef a = cref(s, cid[lo]);
+    inb = alg_bytes_w(a.type, a.card, a.nruns) + 16;
+    int t = a.type;
+    c = (int)a.card;
+    r = (int)a.nruns;
+    load_container(a.type, a.p, a.card, a.nruns, lds, acc, lane);
+    for (uint64_t i = lo + 1; i < hi && c > 0; ++i) {
+      const CRef b = cref(s, cid[i]);
+      inb += alg_bytes_w(b.type, b.card, b.nruns) + 16;
+      uint64_t x[kW];
+      load_container(b.type, b.p, b.card, b.nruns, lds, x, lane);
+      fold<RB_AND>(acc, x);
+      const bool eff = t == kRun && b.type == kRun;
+      metrics(acc, lane, eff, c, r);
+      t = eff ? type_eff(c, r) : type_ab(c);
+    }
+    ty = c ? t : kEmpty;
+    if (ty != kEmpty) emit_container(ty, acc, c, r, dst, lds, lane);
+  } else if (SEM == RB_FAST_XOR || SEM == RB_PAR_XOR) {
+    // naive_xor: in-place xor() per bitmap — absent key -> clone; empty -> key removed
+    //   (RoaringBitmap.xor(x2) :3296-3348).  ParallelAggregation.xor: clone + ixor fold with no
+    //   removal (ParallelAggregation.java:189-195); an empty Run accumulator returns the other
+    //   operand (RunContainer.lazyxor :1816-1821, xor(Run) :2450-2455).
+    bool present = false;
+    int t = kArray;
+    for (uint64_t i = lo; i < hi; ++i) {
+      const CRef b = cref(s, cid[i]);
+      inb += alg_bytes_w(b.type, b.card, b.nruns) + 16;
+      uint64_t x[kW];
+      load_container(b.type, b.p, b.card, b.nruns, lds, x, lane);
+      if (!present) {
+#pragma unroll
+        for (int j = 0; j < kW; ++j) acc[j] = x[j];
+        t = b.type;
+        c = (int)b.card;
+        r = (int)b.nruns;
+        present = true;
+        continue;
+      }
+      const int ct = t;
+      const uint32_t cc = (uint32_t)c;
+      fold<RB_XOR>(acc, x);
+      metrics(acc, lane, true, c, r);
+      if (SEM == RB_PAR_XOR && ct == kRun && cc == 0 && b.type != kBitmap) t = b.type;
+      else t = type_xor_step(ct, b.type, cc, b.card, c, r);
+      if (SEM == RB_FAST_XOR && c == 0) present = false;
+    }
+    ty = present && c > 0 ? t : kEmpty;
+    if (ty != kEmpty) emit_container(ty, acc, c, r, dst, lds, lane);
+  } else { // RB_PAR_OR with 2..15 containers: clone + lazyIOR chain + repairAfterLazy
+    const CRef a = cref(s, cid[lo]);
+    inb = alg_bytes_w(a.type, a.card, a.nruns) + 16;
+    load_container(a.type, a.p, a.card, a.nruns, lds, acc, lane);
+    int st = a.type == kArray ? kStA : a.type == kBitmap ? kStBValid : kStRun;
+    c = (int)a.card;
+    r = (int)a.nruns;
+    for (uint64_t i = lo + 1; i < hi; ++i) {
+      const CRef b = cref(s, cid[i]);
+      inb += alg_bytes_w(b.type, b.card, b.nruns) + 16;
+      const bool acc_full = st == kStRun && c == kSpan;
+      uint64_t x[kW];
+      load_container(b.type, b.p, b.card, b.nruns, lds, x, lane);
+      if (acc_full) continue; // RunContainer.ilazyor / ior return a full `this`
+      const int prev = st;
+      const uint32_t cprev = (uint32_t)c;
+      fold<RB_OR>(acc, x);
+      metrics(acc, lane, true, c, r);
+      if (prev == kStBValid || prev == kStBLazy) {
+        st = kStBLazy; // BitmapContainer.ilazyor
+      } else if (prev == kStA) {
+        if (b.type == kArray) st = cprev + b.card > 1024u ? kStBLazy : kStA;     // ArrayContainer.lazyor :1449
+        else if (b.type == kBitmap) st = c == kSpan ? kStRun : kStBValid;        // BitmapContainer.or(Array)
+        else st = c == kSpan ? kStRun : (r > kMaxArray ? kStBLazy : kStRun);     // RunContainer.lazyorToRun
+      } else { // Run accumulator
+        if (b.type == kArray) st = r > kMaxArray ? kStBLazy : kStRun;            // ilazyorToRun
+        else if (b.type == kBitmap) st = c == kSpan ? kStRun : kStBValid;        // RunContainer.or(Bitmap)
+        else {                                                                    // ior(Run) -> toEfficientContainer
+          const int e = type_eff(c, r);
+          st = e == kRun ? kStRun : e == kBitmap ? kStBValid : kStA;
+        }
+      }
+    }
+    if (st == kStA) ty = kArray;
+    else if (st == kStBValid) ty = kBitmap;
+    else if (st == kStRun) ty = type_eff(c, r);
+    else {
+      ty = type_lr(c);
+      if (ty == kRun) r = 1;
+    }
+    emit_container(ty, acc, c, r, dst, lds, lane);
+  }
+  if (lane == 0) {
+    wo.type[q] = (uint8_t)ty;
+    wo.card[q] = (uint32_t)c;
+    wo.nruns[q] = (uint16_t)(ty == kRun ? r : 0);
+  }
+  stat_add_w(stats, 0, inb);
+  if (ty != kEmpty) stat_add_w(stats, 1, alg_bytes_w(ty, (uint32_t)c, (uint32_t)r) + 16);
+}
+
+__global__ __launch_bounds__(256) void k_wide_keep(const uint8_t *type, uint32_t nk, uint64_t *keep) {
+  const uint32_t q = blockIdx.x * 256 + threadIdx.x;
+  if (q < nk) keep[q] = type[q] != kEmpty;
+}
+__global__ __launch_bounds__(256) void k_wide_write(const uint32_t *klist, uint32_t nk, WideOut wo,
+                                                    const uint64_t *pos, OutView ov) {
+  const uint32_t q = blockIdx.x * 256 + threadIdx.x;
+  if (q >= nk || wo.type[q] == kEmpty) return;
+  const uint64_t r = pos[q];
+  ov.key[r] = (uint16_t)klist[q];
+  ov.type[r] = wo.type[q];
+  ov.card[r] = wo.card[q];
+  ov.nruns[r] = wo.nruns[q];
+  ov.off[r] = (uint64_t)q * kBitmapBytes;
+}
+
+// ---------------------------------------------------------------- host orchestration
+static unsigned nblk(uint64_t n, unsigned per) { return (unsigned)((n + per - 1) / per); }
+
+template <int SEM>
+static void launch_reduce(const SetView &s, const uint32_t *cid, const uint64_t *seg, const uint32_t *klist,
+                          uint32_t nk, uint8_t *out, const WideOut &wo, uint64_t *stats, hipStream_t st) {
+  k_wide_reduce<SEM><<<nblk(nk, 4), 256, 0, st>>>(s, cid, seg, klist, nk, out, wo, stats);
+}
+
+int wide_run(rbgpu_ctx *ctx, int sem, const rbgpu_set *in, const std::vector<uint32_t> &members_in,
+             rbgpu_set **out) {
+  hipStream_t st = ctx->stream;
+  DevPool &pool = ctx->pool;
+  // effective member order: FastAggregation.and(varargs) picks workShyAnd above 10 inputs;
+  // naive_and starts from the smallest bitmap (first on ties) and skips it by identity.
+  std::vector<uint32_t> members = members_in;
+  if (sem == RB_FAST_AND) sem = members.size() > 10 ? RB_WORKSHY_AND : RB_NAIVE_AND;
+  if (sem == RB_NAIVE_AND && !members.empty()) {
+    uint32_t smallest = members[0];
+    for (uint32_t m : members)
+      if (in->h_begin[m + 1] - in->h_begin[m] < in->h_begin[smallest + 1] - in->h_begin[smallest]) smallest = m;
+    std::vector<uint32_t> ord{smallest};
+    for (uint32_t m : members)
+      if (m != smallest) ord.push_back(m);
+    members.swap(ord);
+  }
+  const uint32_t M = (uint32_t)members.size();
+  std::vector<uint64_t> mstart(M + 1, 0);
+  for (uint32_t i = 0; i < M; ++i) mstart[i + 1] = mstart[i] + (in->h_begin[members[i] + 1] - in->h_begin[members[i]]);
+  const uint64_t N = mstart[M];
+  if (in->nc >= (1ull << 32)) return fail(RB_EINVAL, "wide aggregation supports < 2^32 containers per set");
+  const bool and_sem = sem == RB_WORKSHY_AND || sem == RB_NAIVE_AND || sem == RB_NAIVE_AND_ITER;
+
+  stats_begin(ctx);
+  // ---- group by key (stable)
+  uint32_t *d_mem = nullptr, *d_cid = nullptr, *d_cid2 = nullptr, *d_klist = nullptr;
+  uint64_t *d_mstart = nullptr, *d_seg = nullptr, *d_active = nullptr, *d_apos = nullptr, *d_tmp = nullptr;
+  uint16_t *d_keys = nullptr, *d_keys2 = nullptr;
+  void *d_sort = nullptr;
+  size_t sort_bytes = 0;
+  const uint64_t N1 = std::max<uint64_t>(N, 1);
+  (void)rocprim::radix_sort_pairs(nullptr, sort_bytes, (const uint16_t *)nullptr, (uint16_t *)nullptr,
+                                  (const uint32_t *)nullptr, (uint32_t *)nullptr, (size_t)N1, 0, 16, st);
+  const uint64_t tmpw = std::max<uint64_t>(scan_tmp_words(65537), 1);
+  if (pool.alloc((void **)&d_mem, std::max<uint32_t>(M, 1) * 4ull) ||
+      pool.alloc((void **)&d_mstart, (M + 1) * 8ull) || pool.alloc((void **)&d_keys, N1 * 2) ||
+      pool.alloc((void **)&d_keys2, N1 * 2) || pool.alloc((void **)&d_cid, N1 * 4) ||
+      pool.alloc((void **)&d_cid2, N1 * 4) || pool.alloc(&d_sort, std::max<size_t>(sort_bytes, 16)) ||
+      pool.alloc((void **)&d_seg, 65537 * 8ull) || pool.alloc((void **)&d_active, 65537 * 8ull) ||
+      pool.alloc((void **)&d_apos, 65537 * 8ull) || pool.alloc((void **)&d_klist, 65536 * 4ull) ||
+      pool.alloc((void **)&d_tmp, tmpw * 8))
+    return fail(RB_ENOMEM, "wide workspace (%llu containers)", (unsigned long long)N);
+  auto release = [&]() {
+    for (void *p : {(void *)d_mem, (void *)d_mstart, (void *)d_keys, (void *)d_keys2, (void *)d_cid, (void *)d_cid2,
+                    d_sort, (void *)d_seg, (void *)d_active, (void *)d_apos, (void *)d_klist, (void *)d_tmp})
+      pool.release(p);
+  };
+  if (M) {
+    HIPCHK(hipMemcpyAsync(d_mem, members.data(), M * 4ull, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(d_mstart, mstart.data(), (M + 1) * 8ull, hipMemcpyHostToDevice, st));
+  }
+  const SetView sv = in->view();
+  if (N) {
+    k_wide_flatten<<<nblk(N, 256), 256, 0, st>>>(sv, d_mem, d_mstart, M, N, d_keys, d_cid);
+    size_t sb = sort_bytes;
+    if (rocprim::radix_sort_pairs(d_sort, sb, d_keys, d_keys2, d_cid, d_cid2, (size_t)N, 0, 16, st) != hipSuccess) {
+      release();
+      return fail(RB_EDEVICE, "radix sort failed");
+    }
+  }
+  k_wide_bounds<<<nblk(65537, 256), 256, 0, st>>>(d_keys2, N, d_seg);
+  k_wide_select<<<nblk(65536, 256), 256, 0, st>>>(d_seg, and_sem ? (uint64_t)M : 0, d_active);
+  scan_exclusive(d_active, d_apos, 65536, d_tmp, st);
+  k_wide_list<<<nblk(65536, 256), 256, 0, st>>>(d_active, d_apos, d_klist);
+  uint64_t *pin = ctx->h_pinned;
+  HIPCHK(hipMemcpyAsync(pin, d_apos + 65536, 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  const uint32_t nk = (and_sem && M == 0) ? 0 : (uint32_t)pin[0];
+
+  // ---- per-key reduction into 8 KiB slots
+  rbgpu_set *res = new rbgpu_set;
+  int rc = set_alloc(ctx, res, 1, nk, (uint64_t)std::max<uint32_t>(nk, 1) * kBitmapBytes);
+  if (rc) {
+    delete res;
+    release();
+    return rc;
+  }
+  uint8_t *w_type;
+  uint32_t *w_card;
+  uint16_t *w_nruns;
+  uint64_t *w_keep, *w_pos;
+  const uint64_t nk1 = std::max<uint32_t>(nk, 1);
+  if (pool.alloc((void **)&w_type, nk1) || pool.alloc((void **)&w_card, nk1 * 4) ||
+      pool.alloc((void **)&w_nruns, nk1 * 2) || pool.alloc((void **)&w_keep, (nk1 + 1) * 8) ||
+      pool.alloc((void **)&w_pos, (nk1 + 1) * 8)) {
+    rbgpu_set_free(res);
+    release();
+    return fail(RB_ENOMEM, "wide result workspace");
+  }
+  WideOut wo{w_type, w_card, w_nruns};
+  HIPCHK(hipEventRecord(ctx->ev[1], st));
+  if (nk) {
+    switch (sem) {
+    case RB_FAST_OR: launch_reduce<RB_FAST_OR>(sv, d_cid2, d_seg, d_klist, nk, res->payload, wo, ctx->d_stats, st); break;
+    case RB_WORKSHY_AND: launch_reduce<RB_WORKSHY_AND>(sv, d_cid2, d_seg, d_klist, nk, res->payload, wo, ctx->d_stats, st); break;
+    case RB_NAIVE_AND: launch_reduce<RB_NAIVE_AND>(sv, d_cid2, d_seg, d_klist, nk, res->payload, wo, ctx->d_stats, st); break;
+    case RB_NAIVE_AND_ITER: launch_reduce<RB_NAIVE_AND_ITER>(sv, d_cid2, d_seg, d_klist, nk, res->payload, wo, ctx->d_stats, st); break;
+    case RB_FAST_XOR: launch_reduce<RB_FAST_XOR>(sv, d_cid2, d_seg, d_klist, nk, res->payload, wo, ctx->d_stats, st); break;
+    case RB_PAR_OR: launch_reduce<RB_PAR_OR>(sv, d_cid2, d_seg, d_klist, nk, res->payload, wo, ctx->d_stats, st); break;
+    default: launch_reduce<RB_PAR_XOR>(sv, d_cid2, d_seg, d_klist, nk, res->payload, wo, ctx->d_stats, st); break;
+    }
+  }
+  HIPCHK(hipEventRecord(ctx->ev[2], st));
+  // ---- compaction
+  if (nk) {
+    k_wide_keep<<<nblk(nk, 256), 256, 0, st>>>(w_type, nk, w_keep);
+    uint64_t *tmp2 = nullptr;
+    const uint64_t tw = std::max<uint64_t>(scan_tmp_words(nk), 1);
+    if (pool.alloc((void **)&tmp2, tw * 8)) {
+      rbgpu_set_free(res);
+      release();
+      return fail(RB_ENOMEM, "wide scan workspace");
+    }
+    scan_exclusive(w_keep, w_pos, nk, tmp2, st);
+    k_wide_write<<<nblk(nk, 256), 256, 0, st>>>(d_klist, nk, wo, w_pos,
+                                                OutView{res->key, res->type, res->card, res->nruns, res->off});
+    HIPCHK(hipMemcpyAsync(pin + 1, w_pos + nk, 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    pool.release(tmp2);
+  } else {
+    pin[1] = 0;
+  }
+  const uint64_t nres = pin[1];
+  const uint64_t hb[2] = {0, nres};
+  HIPCHK(hipMemcpyAsync(res->begin, hb, 16, hipMemcpyHostToDevice, st));
+  const char *name = sem == RB_FAST_OR ? "k_wide_reduce<FAST_OR>" : sem == RB_WORKSHY_AND ? "k_wide_reduce<WORKSHY_AND>"
+                     : sem == RB_FAST_XOR ? "k_wide_reduce<FAST_XOR>" : sem == RB_PAR_OR ? "k_wide_reduce<PAR_OR>"
+                     : sem == RB_PAR_XOR ? "k_wide_reduce<PAR_XOR>" : "k_wide_reduce<NAIVE_AND>";
+  const KernelSpan spans[1] = {{name, 0, 1, nk}};
+  // ev[2] -> ev[3]: nothing; stats_end reads ev[1]..ev[2] for kernel 0
+  rc = stats_end(ctx, N, nres, spans, 1);
+  pool.release(w_type);
+  pool.release(w_card);
+  pool.release(w_nruns);
+  pool.release(w_keep);
+  pool.release(w_pos);
+  release();
+  if (rc) {
+    rbgpu_set_free(res);
+    return rc;
+  }
+  res->nc = nres;
+  res->h_begin = {0, nres};
+  *out = res;
+  return RB_OK;
+}
+
 } // namespace rbg
