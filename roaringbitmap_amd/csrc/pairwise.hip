@@ -248,7 +248,7 @@ __device__ __forceinline__ LightTask decode_light(const RecU &r, const uint8_t *
 // task's record and both payloads (<= 8 KiB each, 8 x 16 B per lane) are in flight while the
 // current X is staged as an 8 KiB LDS membership image and the current F is filtered.
 template <int OP, bool CARD_ONLY>
-__global__ __launch_bounds__(256) void k_pair_light(const uint8_t *__restrict__ pay_a,
+__global__ __launch_bounds__(256, 4) void k_pair_light(const uint8_t *__restrict__ pay_a,
                                                     const uint8_t *__restrict__ pay_b,
                                                     const TaskRec *__restrict__ recs, uint64_t n,
                                                     uint8_t *__restrict__ out, TaskMeta tm) {
@@ -261,17 +261,25 @@ __global__ __launch_bounds__(256) void k_pair_light(const uint8_t *__restrict__ 
   uint32_t *s = lds[wv];
   RecU cur = load_rec(recs + g);
   LightTask pc = decode_light<OP>(cur, pay_a, pay_b);
+  // Loads sit at two fixed points of the loop body and are unconditional (a task without an X
+  // reads one chunk of its F again), so the prefetch registers carry no per-path phis.
   uint4 fq[8], xq[8];
-  if (!pc.big) {
-    load_chunks(fq, pc.pf, pc.fbytes, lane);
-    if (!pc.copy) load_chunks(xq, pc.px, pc.xbytes, lane);
-  }
+  load_chunks(fq, pc.pf, min(pc.fbytes, (uint32_t)kBitmapBytes), lane);
+  if (pc.copy || pc.big) load_chunks(xq, pc.pf, 16, lane);
+  else load_chunks(xq, pc.px, pc.xbytes, lane);
   while (true) {
     const uint64_t gn = g + stride;
     const bool has_next = gn < n;
     const RecU nx = load_rec(recs + (has_next ? gn : g));
     const LightTask pn = decode_light<OP>(nx, pay_a, pay_b);
-    const bool pre = has_next && !pn.big;
+    if (!pc.copy) {
+      if (pc.big) stage_big_runs(pc.px, pc.rx, s, lane); // only a Run payload exceeds 8 KiB
+      else stage_from_chunks(pc.tx, xq, pc.cx, pc.rx, s, lane);
+    }
+    {
+      const bool real = has_next && !pn.copy && !pn.big;
+      load_chunks(xq, real ? pn.px : pn.pf, real ? pn.xbytes : 16u, lane);
+    }
     int ty, c;
     uint32_t nr = 0;
     if (pc.copy) {
@@ -282,26 +290,15 @@ __global__ __launch_bounds__(256) void k_pair_light(const uint8_t *__restrict__ 
       ty = pc.cty;
       c = (int)pc.ccard;
       nr = pc.cnr;
-      if (pre) {
-        load_chunks(fq, pn.pf, pn.fbytes, lane);
-        if (!pn.copy) load_chunks(xq, pn.px, pn.xbytes, lane);
-      }
     } else {
-      if (pc.big) {
-        load_chunks(fq, pc.pf, pc.fbytes, lane);
-        stage_big_runs(pc.px, pc.rx, s, lane); // only a Run payload exceeds 8 KiB
-      } else {
-        stage_from_chunks(pc.tx, xq, pc.cx, pc.rx, s, lane);
-      }
-      if (pre && !pn.copy) load_chunks(xq, pn.px, pn.xbytes, lane);
       uint16_t *dst = CARD_ONLY ? nullptr : reinterpret_cast<uint16_t *>(out + cur.out);
       const int nfc = (int)((pc.nf + 7) >> 3);
       c = OP == RB_ANDNOT ? filter_chunks<true>(fq, nfc, (int)pc.nf, s, dst, lane)
                           : filter_chunks<false>(fq, nfc, (int)pc.nf, s, dst, lane);
       ty = c ? kArray : kEmpty;
-      if (pre) load_chunks(fq, pn.pf, pn.fbytes, lane);
-      wave_lds_sync(); // the next task restages the same LDS image
     }
+    load_chunks(fq, pn.pf, min(pn.fbytes, (uint32_t)kBitmapBytes), lane);
+    wave_lds_sync(); // the next task restages the same LDS image
     if (lane == 0) {
       tm.type[cur.t] = (uint8_t)ty;
       tm.card[cur.t] = (uint32_t)c;

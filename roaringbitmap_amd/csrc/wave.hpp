@@ -45,6 +45,14 @@ __device__ __forceinline__ uint64_t wave_scan_u64(uint64_t v, int lane) {
   }
   return v;
 }
+__device__ __forceinline__ uint32_t wave_scan_u32(uint32_t v, int lane) {
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    uint32_t t = (uint32_t)__shfl_up((int)v, d);
+    if (lane >= d) v += t;
+  }
+  return v;
+}
 __device__ __forceinline__ uint32_t wave_xscan_xor(uint32_t v, int lane) { // inclusive xor-scan
 #pragma unroll
   for (int d = 1; d < 64; d <<= 1) {
@@ -163,6 +171,34 @@ __device__ __forceinline__ void toggles_to_words(uint64_t (&t)[kW], int lane) { 
   }
 }
 
+// The same transform in place on the LDS image, one 16-B row per step (two passes over LDS
+// instead of 32 live VGPRs: used where the caller already holds prefetched payloads).
+__device__ __forceinline__ void toggles_to_words_lds(uint32_t *s, int lane) {
+  uint4 *s4 = reinterpret_cast<uint4 *>(s);
+  uint32_t q = 0, p0 = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const uint4 v = s4[k * 64 + lane];
+    const uint32_t a = (__popc(v.x) + __popc(v.y)) & 1, b = (__popc(v.z) + __popc(v.w)) & 1;
+    q |= (a ^ b) << k;
+    p0 |= a << k;
+  }
+  const uint32_t incl = wave_xscan_xor(q, lane);
+  const uint32_t excl = incl ^ q;
+  const uint32_t tot = (uint32_t)__shfl((int)incl, 63);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const uint4 v = s4[k * 64 + lane];
+    const uint32_t rowc = __popc(tot & ((1u << k) - 1)) & 1;
+    const uint32_t c0 = rowc ^ ((excl >> k) & 1);
+    const uint32_t c1 = c0 ^ ((p0 >> k) & 1);
+    const uint64_t w0 = prefix_xor64(pack2(v.x, v.y)) ^ (c0 ? ~0ull : 0ull);
+    const uint64_t w1 = prefix_xor64(pack2(v.z, v.w)) ^ (c1 ? ~0ull : 0ull);
+    s4[k * 64 + lane] = make_uint4((uint32_t)w0, (uint32_t)(w0 >> 32), (uint32_t)w1, (uint32_t)(w1 >> 32));
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
 __device__ __forceinline__ void toggle_run(uint32_t *s, uint32_t q) {
   const uint32_t st = q & 0xFFFF, e1 = st + (q >> 16) + 1;
   atomicXor(&s[st >> 5], 1u << (st & 31));
@@ -225,47 +261,34 @@ template <bool NEGATE>
 __device__ __forceinline__ int filter_chunks(const uint4 (&fq)[8], int nfc, int nf, const uint32_t *s, uint16_t *out,
                                              int lane) {
   const int iters = (nfc + 63) >> 6; // wave-uniform, <= 8
-  uint32_t keep[8];
-  uint64_t P0 = 0, P1 = 0; // per-iteration kept counts, 10-bit fields (<= 512 per iteration)
+  uint32_t total = 0;
+  // One chunk row per step, kept values written in the same step: a scan per row keeps only
+  // one row's values live (the scheduling fence stops the compiler from hoisting all 64 LDS
+  // probes of the unrolled loop, which would double the kernel's VGPR footprint).
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
-    keep[i] = 0;
     if (i < iters) {
       const int c = lane + 64 * i;
       const int n = c < nfc ? min(8, nf - 8 * c) : 0;
       const uint32_t x[8] = {fq[i].x & 0xFFFF, fq[i].x >> 16, fq[i].y & 0xFFFF, fq[i].y >> 16,
                              fq[i].z & 0xFFFF, fq[i].z >> 16, fq[i].w & 0xFFFF, fq[i].w >> 16};
+      uint32_t keep = 0;
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         const uint32_t m = (s[x[k] >> 5] >> (x[k] & 31)) & 1;
-        if (k < n && (m ^ (NEGATE ? 1u : 0u))) keep[i] |= 1u << k;
+        if (k < n && (m ^ (NEGATE ? 1u : 0u))) keep |= 1u << k;
       }
-      const uint64_t cnt = (uint64_t)__popc(keep[i]);
-      if (i < 6) P0 |= cnt << (10 * i);
-      else P1 |= cnt << (10 * (i - 6));
-    }
-  }
-  const uint64_t S0 = wave_scan_u64(P0, lane);
-  const uint64_t S1 = iters > 6 ? wave_scan_u64(P1, lane) : 0;
-  const uint64_t T0 = (uint64_t)__shfl((unsigned long long)S0, 63);
-  const uint64_t T1 = iters > 6 ? (uint64_t)__shfl((unsigned long long)S1, 63) : 0;
-  uint32_t total = 0;
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    if (i < iters) {
-      const uint64_t S = i < 6 ? S0 : S1, P = i < 6 ? P0 : P1, T = i < 6 ? T0 : T1;
-      const int sh = 10 * (i < 6 ? i : i - 6);
-      const uint32_t excl = (uint32_t)(((S - P) >> sh) & 0x3FF);
+      const uint32_t cnt = (uint32_t)__popc(keep);
+      const uint32_t incl = wave_scan_u32(cnt, lane);
       if (out) {
-        uint32_t pos = total + excl;
-        const uint32_t x[8] = {fq[i].x & 0xFFFF, fq[i].x >> 16, fq[i].y & 0xFFFF, fq[i].y >> 16,
-                               fq[i].z & 0xFFFF, fq[i].z >> 16, fq[i].w & 0xFFFF, fq[i].w >> 16};
+        uint32_t pos = total + incl - cnt;
 #pragma unroll
         for (int k = 0; k < 8; ++k)
-          if ((keep[i] >> k) & 1) out[pos++] = (uint16_t)x[k];
+          if ((keep >> k) & 1) out[pos++] = (uint16_t)x[k];
       }
-      total += (uint32_t)((T >> sh) & 0x3FF);
+      total += (uint32_t)__shfl((int)incl, 63);
     }
+    __builtin_amdgcn_sched_barrier(0);
   }
   return (int)total;
 }
@@ -273,12 +296,15 @@ __device__ __forceinline__ int filter_chunks(const uint4 (&fq)[8], int nfc, int 
 // ---------------------------------------------------------------- register-preloaded payloads
 // A payload of at most 8 KiB as 8 uint4 per lane: chunk c = lane + 64*i (16 bytes) in q[i].
 __device__ __forceinline__ void load_chunks(uint4 (&q)[8], const uint8_t *p, uint32_t bytes, int lane) {
-  const uint4 *p4 = reinterpret_cast<const uint4 *>(p);
-  const int n = (int)((bytes + 15) >> 4);
+  // Buffer loads: a 32-bit per-lane offset against a wave-uniform descriptor, and lanes past the
+  // (16-B padded) payload get zeros from the range check without touching memory.
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(p), (short)0, (int)((bytes + 15) & ~15u), 0x00020000);
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
-    const int c = lane + 64 * i;
-    q[i] = c < n ? p4[c] : make_uint4(0, 0, 0, 0);
+    typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+    const v4u v = __builtin_amdgcn_raw_buffer_load_b128(rs, (lane + 64 * i) * 16, 0, 0);
+    q[i] = make_uint4(v.x, v.y, v.z, v.w);
   }
 }
 __device__ __forceinline__ void store_chunks(const uint4 (&q)[8], uint8_t *p, uint32_t bytes, int lane) {
@@ -337,10 +363,7 @@ __device__ __forceinline__ void stage_from_chunks(int type, const uint4 (&q)[8],
           if (base + k < nruns) toggle_run(s, r[k]);
       }
       wave_lds_sync();
-      uint64_t w[kW];
-      lds_read_words(s, w, lane);
-      toggles_to_words(w, lane);
-      lds_write_words(s, w, lane); // each lane rewrites only the words it read
+      toggles_to_words_lds(s, lane);
     }
   }
   wave_lds_sync();
