@@ -9,7 +9,8 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "librbgpu.so")
+# RBGPU_LIB selects an alternative in-tree build (kernel variants under scripts/ experiments)
+LIB_PATH = os.environ.get("RBGPU_LIB") or os.path.join(_HERE, "librbgpu.so")
 
 RB_OK, RB_EFORMAT, RB_EINVAL, RB_ENOMEM, RB_EDEVICE = 0, -1, -2, -3, -4
 AND, OR, XOR, ANDNOT = 0, 1, 2, 3

@@ -25,19 +25,22 @@ def _newer(src_list, target):
     return any(os.path.getmtime(s) > t for s in src_list)
 
 
-def build(verbose: bool = False) -> str:
-    os.makedirs(OBJ, exist_ok=True)
+def build(verbose: bool = False, defines=(), out: str = OUT, obj: str = OBJ) -> str:
+    """Compiles every csrc/*.hip|*.cpp for gfx950 and links `out`.  `defines` / `out` / `obj` are for
+    kernel-variant experiments (scripts/variants.py); the product is the default build."""
+    os.makedirs(obj, exist_ok=True)
     headers = glob.glob(os.path.join(CSRC, "*.hpp")) + [os.path.join(ROOT, "include", "rbgpu.h")]
     sources = sorted(glob.glob(os.path.join(CSRC, "*.hip")) + glob.glob(os.path.join(CSRC, "*.cpp")))
     objs = []
     jobs = []
     for s in sources:
-        o = os.path.join(OBJ, os.path.basename(s) + ".o")
+        o = os.path.join(obj, os.path.basename(s) + ".o")
         objs.append(o)
         if _newer([s] + headers, o):
-            cmd = [HIPCC] + FLAGS + ["-c", s, "-o", o]
+            dflags = [f"-D{d}" for d in defines]
+            cmd = [HIPCC] + FLAGS + dflags + ["-c", s, "-o", o]
             if s.endswith(".cpp"):
-                cmd = [HIPCC, "-x", "hip"] + FLAGS + ["-c", s, "-o", o]
+                cmd = [HIPCC, "-x", "hip"] + FLAGS + dflags + ["-c", s, "-o", o]
             jobs.append(cmd)
 
     def run(cmd):
@@ -52,9 +55,9 @@ def build(verbose: bool = False) -> str:
         for err in ex.map(run, jobs):
             if err and verbose:
                 print(err, file=sys.stderr)
-    if jobs or _newer(objs, OUT):
-        run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", OUT] + objs)
-    return OUT
+    if jobs or _newer(objs, out):
+        run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out] + objs)
+    return out
 
 
 if __name__ == "__main__":

@@ -428,8 +428,11 @@ int rbgpu_set_serialize(const rbgpu_set *s, uint32_t first, uint32_t count, uint
 }
 
 // ---------------------------------------------------------------- pairwise
+// probe: 0 = the product path; 1 / 2 = measurement probes (rbgpu_internal_probe) in place of the
+// task kernel — results are not produced.
 static int pairwise_impl(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu_set *b, const uint32_t *a_idx,
-                         const uint32_t *b_idx, uint32_t npairs, rbgpu_set **out, uint64_t *card_out) {
+                         const uint32_t *b_idx, uint32_t npairs, rbgpu_set **out, uint64_t *card_out,
+                         int probe = 0) {
   int rc = check_ctx(ctx);
   if (rc) return rc;
   if (op < RB_AND || op > RB_ANDNOT) return fail(RB_EINVAL, "bad op %d", op);
@@ -447,16 +450,16 @@ static int pairwise_impl(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu
   const uint64_t scan_tmp = scan_tmp_words(np + 1);
   size_t need = 0;
   need += 2 * aligned256(np * 4);            // indices
-  need += 13 * aligned256((np + 1) * 8);     // 5 counts, 5 scans, result counts, pair cards, spare
+  need += 11 * aligned256((np + 1) * 8);     // 4 counts, 4 scans, result counts, pair cards, spare
   need += aligned256(scan_tmp * 8);
   if (ctx->ws_pairs.reserve(need, st) != hipSuccess) return fail(RB_ENOMEM, "pair workspace");
   Workspace &W = ctx->ws_pairs;
   uint32_t *d_aidx = a_idx ? W.take<uint32_t>(np) : nullptr;
   uint32_t *d_bidx = b_idx ? W.take<uint32_t>(np) : nullptr;
   PairCountArrays cnt{W.take<uint64_t>(np + 1), W.take<uint64_t>(np + 1), W.take<uint64_t>(np + 1),
-                      W.take<uint64_t>(np + 1), W.take<uint64_t>(np + 1)};
+                      W.take<uint64_t>(np + 1)};
   PairCountArrays scn{W.take<uint64_t>(np + 1), W.take<uint64_t>(np + 1), W.take<uint64_t>(np + 1),
-                      W.take<uint64_t>(np + 1), W.take<uint64_t>(np + 1)};
+                      W.take<uint64_t>(np + 1)};
   uint64_t *rcnt = W.take<uint64_t>(np + 1), *pcard = W.take<uint64_t>(np + 1);
   uint64_t *tmp = W.take<uint64_t>(std::max<uint64_t>(scan_tmp, 1));
   if (d_aidx) HIPCHK(hipMemcpyAsync(d_aidx, a_idx, np * 4, hipMemcpyHostToDevice, st));
@@ -467,17 +470,15 @@ static int pairwise_impl(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu
   launch_pair_count(pa, cnt, ctx->d_stats, st);
   scan_exclusive(cnt.task, scn.task, np, tmp, st);
   scan_exclusive(cnt.light, scn.light, np, tmp, st);
-  scan_exclusive(cnt.heavy, scn.heavy, np, tmp, st);
   scan_exclusive(cnt.big, scn.big, np, tmp, st);
   scan_exclusive(cnt.small, scn.small, np, tmp, st);
   uint64_t *const tot = ctx->h_pinned;
   HIPCHK(hipMemcpyAsync(tot + 0, scn.task + np, 8, hipMemcpyDeviceToHost, st));
   HIPCHK(hipMemcpyAsync(tot + 1, scn.light + np, 8, hipMemcpyDeviceToHost, st));
-  HIPCHK(hipMemcpyAsync(tot + 2, scn.heavy + np, 8, hipMemcpyDeviceToHost, st));
-  HIPCHK(hipMemcpyAsync(tot + 3, scn.big + np, 8, hipMemcpyDeviceToHost, st));
-  HIPCHK(hipMemcpyAsync(tot + 4, scn.small + np, 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(tot + 2, scn.big + np, 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(tot + 3, scn.small + np, 8, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
-  const uint64_t ntasks = tot[0], nlight = tot[1], nheavy = tot[2], nbig_t = tot[3], small_t = tot[4];
+  const uint64_t ntasks = tot[0], nlight = tot[1], nheavy = ntasks - nlight, nbig_t = tot[2], small_t = tot[3];
   const uint64_t small_base = nbig_t * kBitmapBytes;
   const uint64_t arena = card_only ? 0 : small_base + small_t;
 
@@ -509,6 +510,21 @@ static int pairwise_impl(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu
   }
   launch_pair_emit(pa, scn, small_base, light, heavy, tm, st);
   HIPCHK(hipEventRecord(ctx->ev[1], st));
+  if (probe) {
+    uint32_t *sink = nullptr;
+    const unsigned blocks = 256 * 4;
+    if (ctx->pool.alloc((void **)&sink, blocks * 256ull * 4)) return fail(RB_ENOMEM, "probe sink");
+    launch_probe(op, probe, a->payload, b->payload, a->payload_bytes, light, nlight, sink, blocks, st);
+    if (probe == 1) launch_probe(op, probe, a->payload, b->payload, 0, heavy, nheavy, sink, blocks, st);
+    HIPCHK(hipEventRecord(ctx->ev[2], st));
+    HIPCHK(hipStreamSynchronize(st));
+    ctx->pool.release(sink);
+    if (res) rbgpu_set_free(res);
+    const KernelSpan spans[1] = {{probe == 1 ? "k_probe_tasks" : "k_probe_stream", 6, -1, ntasks}};
+    rc = stats_end(ctx, ntasks, 0, spans, 1);
+    if (probe == 2) ctx->last.main_kernel_bytes = ctx->last.kernel_bytes[0] = a->payload_bytes / 8192 * 8192;
+    return rc;
+  }
   launch_pairwise(op, card_only, a->payload, b->payload, light, nlight, heavy, nheavy, res ? res->payload : nullptr,
                   tm, st, ctx->ev[2]);
   HIPCHK(hipEventRecord(ctx->ev[3], st));
@@ -520,7 +536,7 @@ static int pairwise_impl(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu
   launch_compact_write(scn.task, npairs, tm, rbegin, ov, pcard, ctx->d_stats, st);
   HIPCHK(hipMemcpyAsync(ctx->h_pinned + 5, rbegin + np, 8, hipMemcpyDeviceToHost, st));
   if (card_out && np) HIPCHK(hipMemcpyAsync(card_out, pcard, np * 8, hipMemcpyDeviceToHost, st));
-  const KernelSpan spans[2] = {{"k_pair_light", 2, 4, nlight}, {"k_pair_heavy", 3, 5, nheavy}};
+  const KernelSpan spans[2] = {{"k_pair_tasks<light>", 2, 4, nlight}, {"k_pair_tasks<heavy>", 3, 5, nheavy}};
   rc = stats_end(ctx, ntasks, 0, spans, 2);
   if (rc) return rc;
   const uint64_t nres = ctx->h_pinned[5];
@@ -543,6 +559,15 @@ int rbgpu_pairwise_cardinality(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const
                                const uint32_t *b_idx, uint32_t npairs, uint64_t *out) {
   if (!out && npairs) return fail(RB_EINVAL, "null out");
   return pairwise_impl(ctx, op, a, b, a_idx, b_idx, npairs, nullptr, out);
+}
+
+// Measurement hook (not part of rbgpu.h): runs the pairwise setup, then a read-only probe kernel
+// in place of the task kernel (mode 1: the task kernel's payload loads; 2: a streaming read of
+// a's arena).  The probe's time is in rbgpu_get_stats().main_kernel_ms.
+int rbgpu_internal_probe(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu_set *b, uint32_t npairs, int mode) {
+  if (mode != 1 && mode != 2) return fail(RB_EINVAL, "probe mode");
+  rbgpu_set *res = nullptr;
+  return pairwise_impl(ctx, op, a, b, nullptr, nullptr, npairs, &res, nullptr, mode);
 }
 
 // ---------------------------------------------------------------- wide

@@ -31,19 +31,23 @@ struct PairCounts {
 struct PairBases {
   uint64_t task, light, heavy, big, small;
 };
-// per pair arrays (counts, or their exclusive scans), each [npairs + 1]
+// per pair arrays (counts, or their exclusive scans), each [npairs + 1]; heavy = task - light
 struct PairCountArrays {
-  uint64_t *task, *light, *heavy, *big, *small;
+  uint64_t *task, *light, *big, *small;
 };
-// stats words (striped, see common.hpp): 0/1 total input/output bytes, 2/3 light/heavy input,
-// 4/5 light/heavy output
+// stats words (striped, see common.hpp): 0/1 total input/output bytes, 2/3 filter+copy / register-path
+// input, 4/5 filter+copy / register-path output
 void launch_pair_count(const PairArgs &a, const PairCountArrays &c, uint64_t *stats, hipStream_t st);
 void launch_pair_emit(const PairArgs &a, const PairCountArrays &scans, uint64_t small_base, TaskRec *light,
                       TaskRec *heavy, const TaskMeta &tm, hipStream_t st);
-// light: copies and subset-of-an-Array results; heavy: full register path
+// light records: copies + subset-of-an-Array filters; heavy records: the register path.  `mid` is
+// recorded between the two persistent launches.
 void launch_pairwise(int op, bool card_only, const uint8_t *pa, const uint8_t *pb, const TaskRec *light,
                      uint64_t nl, const TaskRec *heavy, uint64_t nh, uint8_t *out, const TaskMeta &tm,
                      hipStream_t st, hipEvent_t mid);
+// measurement probes (rbgpu_internal_probe): mode 1 = task-order payload reads, 2 = streaming read
+void launch_probe(int op, int mode, const uint8_t *pa, const uint8_t *pb, uint64_t a_bytes, const TaskRec *recs,
+                  uint64_t n, uint32_t *sink, unsigned blocks, hipStream_t st);
 void launch_compact_count(const uint64_t *task_begin, uint32_t npairs, const uint8_t *ttype, uint64_t *cnt,
                           hipStream_t st);
 void launch_compact_write(const uint64_t *task_begin, uint32_t npairs, const TaskMeta &tm, const uint64_t *rbegin,

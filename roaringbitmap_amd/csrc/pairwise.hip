@@ -6,11 +6,11 @@
 //                  result slots per kernel category + an output-byte bound per slot;
 //   scans          exclusive prefix sums -> record index and arena offset of every slot;
 //   k_pair_emit    thread per pair: write self-contained task records (payload offsets,
-//                  descriptors) per category, plus result-order metadata;
-//   k_pair_light   ONE WAVE PER TASK: unmatched copies and results that are a subset of an
-//                  Array operand (filter against an 8 KiB LDS membership image);
-//   k_pair_heavy   ONE WAVE PER TASK: both containers as 65536-bit register bitmaps, word op,
-//                  card + maximal runs, reference type decision, coalesced emission;
+//                  descriptors) in result order;
+//   k_pair_tasks   persistent, ONE WAVE PER TASK, software-pipelined: unmatched copies, results
+//                  that are a subset of an Array operand (filter against an 8 KiB LDS membership
+//                  image), and everything else as 65536-bit register bitmaps (word op, card +
+//                  maximal runs, reference type decision, coalesced emission);
 //   k_compact_*    drop empty results (isEmpty, RoaringBitmap.java:389-391 etc.) and build the
 //                  result CSR.
 #include "kernels.hpp"
@@ -142,14 +142,15 @@ __global__ __launch_bounds__(kPairThreads) void k_pair_count(PairArgs a, PairCou
     pair_walk<false>(a, p, n, inb, b, nullptr, nullptr, TaskMeta{});
     c.task[p] = n.task;
     c.light[p] = n.light;
-    c.heavy[p] = n.heavy;
     c.big[p] = n.big;
     c.small[p] = n.small;
   }
-  // stats words: 0 total input, 2 light-task input, 3 heavy-task input
+  // stats words: 0 total input (with key arrays), 2 filter+copy task input, 3 register-path input,
+  // 6 all task input (what k_pair_tasks reads)
   stat_add(stats, 0, inb[0] + inb[1] + inb[2]);
   stat_add(stats, 2, inb[1]);
   stat_add(stats, 3, inb[2]);
+  stat_add(stats, 6, inb[1] + inb[2]);
 }
 
 __global__ __launch_bounds__(kPairThreads) void k_pair_emit(PairArgs a, PairCountArrays scans, uint64_t small_base,
@@ -157,7 +158,8 @@ __global__ __launch_bounds__(kPairThreads) void k_pair_emit(PairArgs a, PairCoun
   const uint32_t p = blockIdx.x * kPairThreads + threadIdx.x;
   if (p >= a.npairs) return;
   PairCounts n{};
-  PairBases b{scans.task[p], scans.light[p], scans.heavy[p], scans.big[p], small_base + scans.small[p]};
+  PairBases b{scans.task[p], scans.light[p], scans.task[p] - scans.light[p], scans.big[p],
+              small_base + scans.small[p]};
   uint64_t inb[3] = {0, 0, 0};
   pair_walk<true>(a, p, n, inb, b, light, heavy, tm);
 }
@@ -170,11 +172,18 @@ __global__ __launch_bounds__(kPairThreads) void k_pair_emit(PairArgs a, PairCoun
 //   XOR:    R^R, R^A(|A|<32) -> EFF, else AB         (RunContainer.java:2410-2482; ArrayContainer.java:1311-1336)
 //   ANDNOT: R\R, R\A(|A|<32) -> EFF, else AB         (RunContainer.java:574-692; BitmapContainer.java:221-274)
 // An AND with an Array operand, or an ANDNOT with an Array on the left, is a subset of that
-// Array, so AB == Array: those run as filters in k_pair_light.
+// Array, so AB == Array: those run as filters.
 
-// Out of line: keeps the rare > 2047-run staging from inflating the pipelined kernel's registers.
+// A Run payload over 8 KiB (> 2047 runs) is staged straight from global memory; the toggle->
+// membership transform runs in LDS so it needs no register bitmap.
 __device__ __noinline__ void stage_big_runs(const uint8_t *p, uint32_t nruns, uint32_t *s, int lane) {
-  stage_container(kRun, p, 0, nruns, s, lane);
+  lds_zero(s, lane);
+  wave_lds_sync();
+  const uint32_t *r32 = reinterpret_cast<const uint32_t *>(p);
+  for (uint32_t i = lane; i < nruns; i += 64) toggle_run(s, r32[i]);
+  wave_lds_sync();
+  toggles_to_words_lds(s, lane);
+  wave_lds_sync();
 }
 
 struct RecU { // the wave-uniform view of one TaskRec
@@ -194,110 +203,192 @@ __device__ __forceinline__ RecU load_rec(const TaskRec *r) {
   return u;
 }
 
-// Decoded light task: F is the Array whose subset is the result (or the payload to clone), X the
-// operand staged as a membership image.
-struct LightTask {
-  bool copy, big;      // big: a payload exceeds 8 KiB (Run with > 2047 runs) -> direct path
-  const uint8_t *pf, *px;
-  uint32_t fbytes, xbytes, nf, cx, rx;
-  int tx;
-  int cty;             // copy: type, card, runs of the clone
-  uint32_t ccard, cnr;
+// One decoded task.  P and Q are the two payloads the task reads (each preloaded as <= 8 x 16 B
+// per lane unless it exceeds 8 KiB):
+//   kCopy   unmatched container, cloned unchanged (RoaringArray.appendCopy :184-205): P = it;
+//   kFilter result is a subset of an Array operand F (AND with an Array, ANDNOT with an Array on
+//           the left; ArrayContainer.and/andNot :184-271, BitmapContainer.and(Array) :162-172,
+//           RunContainer.and(Array) :305-336): P = F, Q = the other operand X, staged in LDS;
+//   kHeavy  everything else: P = A, Q = B as 65536-bit register bitmaps.
+#ifndef RBG_HEAVY_PERSISTENT
+#define RBG_HEAVY_PERSISTENT 1 // 0: the one-launch-sized-grid register path (k_pair_heavy_np)
+#endif
+#ifndef RBG_LIGHT_WAVES
+#define RBG_LIGHT_WAVES 4 // waves per SIMD of the copy + filter kernel (128 VGPRs)
+#endif
+#ifndef RBG_HEAVY_WAVES
+#define RBG_HEAVY_WAVES 2 // waves per SIMD the register-path kernel is allocated for (prefetch + bitmap)
+#endif
+enum { kCopy = 0, kFilter = 1, kHeavy = 2 };
+struct Task {
+  int kind;
+  bool bigp, bigq;       // payload exceeds 8 KiB (Run with > 2047 runs): direct path from global
+  const uint8_t *pp, *pq;
+  uint32_t pbytes, qbytes;
+  int tp, tq;            // container types of P and Q
+  uint32_t cp, cq, rp, rq;
 };
 template <int OP>
-__device__ __forceinline__ LightTask decode_light(const RecU &r, const uint8_t *pay_a, const uint8_t *pay_b) {
-  LightTask L;
+__device__ __forceinline__ Task decode_task(const RecU &r, const uint8_t *pay_a, const uint8_t *pay_b) {
+  Task T;
   const uint32_t ta = desc_type(r.da), tb = desc_type(r.db);
-  L.copy = ta == kAbsent || tb == kAbsent;
-  if (L.copy) {
-    const bool from_a = ta != kAbsent;
-    const uint32_t d = from_a ? r.da : r.db;
-    L.cty = (int)desc_type(d);
-    L.ccard = desc_card(d);
-    L.cnr = from_a ? r.ra : r.rb;
-    L.pf = from_a ? pay_a + r.pa : pay_b + r.pb;
-    L.fbytes = (uint32_t)payload_bytes(L.cty, L.ccard, L.cnr);
-    L.px = nullptr;
-    L.xbytes = 0;
-    L.nf = L.cx = L.rx = 0;
-    L.tx = 0;
-    L.big = L.fbytes > (uint32_t)kBitmapBytes;
-    return L;
-  }
   const uint32_t ca = desc_card(r.da), cb = desc_card(r.db);
-  bool f_is_a;
-  if (OP == RB_ANDNOT) f_is_a = true;
-  else if (ta == kArray && tb == kArray) f_is_a = ca <= cb;
-  else f_is_a = ta == kArray;
-  L.pf = f_is_a ? pay_a + r.pa : pay_b + r.pb;
-  L.px = f_is_a ? pay_b + r.pb : pay_a + r.pa;
-  L.nf = f_is_a ? ca : cb;
-  L.fbytes = 2 * L.nf;
-  L.tx = (int)(f_is_a ? tb : ta);
-  L.cx = f_is_a ? cb : ca;
-  L.rx = f_is_a ? r.rb : r.ra;
-  L.xbytes = (uint32_t)payload_bytes(L.tx, L.cx, L.rx);
-  L.big = L.xbytes > (uint32_t)kBitmapBytes;
-  L.cty = 0;
-  L.ccard = L.cnr = 0;
-  return L;
+  const bool p_is_a = ta != kAbsent && !(light_task(OP, (int)ta, (int)tb) && tb == kArray &&
+                                         (ta != kArray || (OP != RB_ANDNOT && cb < ca)));
+  if (ta == kAbsent || tb == kAbsent) T.kind = kCopy;
+  else T.kind = light_task(OP, (int)ta, (int)tb) ? kFilter : kHeavy;
+  // kFilter: F is the Array (ANDNOT: always A; AND of two Arrays: the smaller, A on ties)
+  T.pp = p_is_a ? pay_a + r.pa : pay_b + r.pb;
+  T.pq = p_is_a ? pay_b + r.pb : pay_a + r.pa;
+  T.tp = (int)(p_is_a ? ta : tb);
+  T.tq = (int)(p_is_a ? tb : ta);
+  T.cp = p_is_a ? ca : cb;
+  T.cq = p_is_a ? cb : ca;
+  T.rp = p_is_a ? r.ra : r.rb;
+  T.rq = p_is_a ? r.rb : r.ra;
+  T.pbytes = (uint32_t)payload_bytes(T.tp, T.cp, T.rp);
+  T.qbytes = T.kind == kCopy ? 0u : (uint32_t)payload_bytes(T.tq, T.cq, T.rq);
+  T.bigp = T.pbytes > (uint32_t)kBitmapBytes;
+  T.bigq = T.qbytes > (uint32_t)kBitmapBytes;
+  return T;
 }
 
-// Unmatched containers (cloned unchanged, RoaringArray.appendCopy :184-205) and subset-of-an-Array
-// results.  Persistent waves walk the task list with a one-task software pipeline: the next
-// task's record and both payloads (<= 8 KiB each, 8 x 16 B per lane) are in flight while the
-// current X is staged as an 8 KiB LDS membership image and the current F is filtered.
-template <int OP, bool CARD_ONLY>
-__global__ __launch_bounds__(256, 4) void k_pair_light(const uint8_t *__restrict__ pay_a,
-                                                    const uint8_t *__restrict__ pay_b,
-                                                    const TaskRec *__restrict__ recs, uint64_t n,
-                                                    uint8_t *__restrict__ out, TaskMeta tm) {
+// Result type of a matched pair for the register path:
+//   AND: R&R -> EFF, else AB; OR: any Bitmap -> LR, A|A -> AB, else EFF;
+//   XOR / ANDNOT: R^R, R\R, and R^A / A^R / R\A with |A| < 32 -> EFF, else AB.
+template <int OP> __device__ __forceinline__ bool eff_rule(int ta, int tb, uint32_t ca, uint32_t cb) {
+  if (OP == RB_AND) return ta == kRun && tb == kRun;
+  if (OP == RB_OR) return ta != kBitmap && tb != kBitmap && !(ta == kArray && tb == kArray);
+  if (OP == RB_XOR)
+    return (ta == kRun && tb == kRun) || (ta == kArray && tb == kRun && ca < (uint32_t)kRunArrayThreshold) ||
+           (ta == kRun && tb == kArray && cb < (uint32_t)kRunArrayThreshold);
+  return (ta == kRun && tb == kRun) || (ta == kRun && tb == kArray && cb < (uint32_t)kRunArrayThreshold);
+}
+template <int OP> __device__ __forceinline__ void word_op(uint64_t &a, uint64_t b) {
+  if (OP == RB_AND) a &= b;
+  else if (OP == RB_OR) a |= b;
+  else if (OP == RB_XOR) a ^= b;
+  else a &= ~b;
+}
+
+// The task kernel, ONE WAVE PER TASK, persistent waves striding over one record list with a
+// one-task software pipeline: the next task's record and both payloads are in flight while the
+// current one computes.  Loads sit at fixed points of the loop body (a task with fewer payloads
+// re-reads 16 B of its first one) so the prefetch registers carry no phis.
+//   ROLE kRoleLight (copies + filters, 4 waves/SIMD): stage X in LDS, load the next Q, filter F
+//                   (or store the copy), load the next P;
+//   ROLE kRoleHeavy (register path): build the 65536-bit result in registers from P and Q, load
+//                   both next payloads, then classify and emit.
+enum { kRoleLight = 0, kRoleHeavy = 1 };
+template <int OP, bool CARD_ONLY, int ROLE>
+__global__ __launch_bounds__(256, ROLE == kRoleHeavy ? RBG_HEAVY_WAVES : RBG_LIGHT_WAVES) void k_pair_tasks(
+    const uint8_t *__restrict__ pay_a, const uint8_t *__restrict__ pay_b, const TaskRec *__restrict__ recs,
+    uint64_t n, uint8_t *__restrict__ out, TaskMeta tm) {
   __shared__ __attribute__((aligned(16))) uint32_t lds[4][2048];
+  __shared__ __attribute__((aligned(16))) uint16_t stage[ROLE == kRoleLight ? 4 : 1][kStageVals];
   const int lane = lane_id();
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint64_t stride = (uint64_t)gridDim.x * 4;
   uint64_t g = (uint64_t)blockIdx.x * 4 + wv;
   if (g >= n) return;
   uint32_t *s = lds[wv];
+  uint16_t *ob = stage[ROLE == kRoleLight ? wv : 0];
   RecU cur = load_rec(recs + g);
-  LightTask pc = decode_light<OP>(cur, pay_a, pay_b);
-  // Loads sit at two fixed points of the loop body and are unconditional (a task without an X
-  // reads one chunk of its F again), so the prefetch registers carry no per-path phis.
-  uint4 fq[8], xq[8];
-  load_chunks(fq, pc.pf, min(pc.fbytes, (uint32_t)kBitmapBytes), lane);
-  if (pc.copy || pc.big) load_chunks(xq, pc.pf, 16, lane);
-  else load_chunks(xq, pc.px, pc.xbytes, lane);
+  Task tc = decode_task<OP>(cur, pay_a, pay_b);
+  uint4 pq[8], qq[8];
+  load_chunks(pq, tc.pp, tc.bigp ? 16u : tc.pbytes, lane);
+  if (tc.kind == kCopy || tc.bigq) load_chunks(qq, tc.pp, 16, lane);
+  else load_chunks(qq, tc.pq, tc.qbytes, lane);
   while (true) {
     const uint64_t gn = g + stride;
     const bool has_next = gn < n;
     const RecU nx = load_rec(recs + (has_next ? gn : g));
-    const LightTask pn = decode_light<OP>(nx, pay_a, pay_b);
-    if (!pc.copy) {
-      if (pc.big) stage_big_runs(pc.px, pc.rx, s, lane); // only a Run payload exceeds 8 KiB
-      else stage_from_chunks(pc.tx, xq, pc.cx, pc.rx, s, lane);
-    }
-    {
-      const bool real = has_next && !pn.copy && !pn.big;
-      load_chunks(xq, real ? pn.px : pn.pf, real ? pn.xbytes : 16u, lane);
-    }
-    int ty, c;
+    const Task tn = decode_task<OP>(nx, pay_a, pay_b);
+    int ty = kEmpty, c = 0;
     uint32_t nr = 0;
-    if (pc.copy) {
-      if (!CARD_ONLY) {
-        if (pc.big) copy_payload(pc.pf, out + cur.out, pc.fbytes, lane);
-        else store_chunks(fq, out + cur.out, pc.fbytes, lane);
+    uint8_t *dst = out + cur.out;
+    if (ROLE == kRoleHeavy) {
+      // ---- the result as a register bitmap: P = A, Q = B (never swapped: ANDNOT and the type
+      //      rules are ordered)
+      uint64_t w[kW];
+      if (tc.tp == kBitmap) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          w[2 * k] = pack2(pq[k].x, pq[k].y);
+          w[2 * k + 1] = pack2(pq[k].z, pq[k].w);
+        }
+      } else {
+        if (tc.bigp) stage_big_runs(tc.pp, tc.rp, s, lane);
+        else stage_from_chunks(tc.tp, pq, tc.cp, tc.rp, s, lane);
+        lds_read_words(s, w, lane);
+        wave_lds_sync();
       }
-      ty = pc.cty;
-      c = (int)pc.ccard;
-      nr = pc.cnr;
+      if (tc.tq == kBitmap) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          word_op<OP>(w[2 * k], pack2(qq[k].x, qq[k].y));
+          word_op<OP>(w[2 * k + 1], pack2(qq[k].z, qq[k].w));
+        }
+      } else {
+        if (tc.bigq) stage_big_runs(tc.pq, tc.rq, s, lane);
+        else stage_from_chunks(tc.tq, qq, tc.cq, tc.rq, s, lane);
+        const uint4 *s4 = reinterpret_cast<const uint4 *>(s);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const uint4 v = s4[k * 64 + lane];
+          word_op<OP>(w[2 * k], pack2(v.x, v.y));
+          word_op<OP>(w[2 * k + 1], pack2(v.z, v.w));
+        }
+        wave_lds_sync();
+      }
+      // ---- both next payloads in flight during classification and emission (the fence keeps the
+      //      scheduler from hoisting these loads above the consumption of the current ones)
+      __builtin_amdgcn_sched_barrier(0);
+      {
+        const bool real = has_next && !tn.bigq;
+        load_chunks(qq, real ? tn.pq : tn.pp, real ? tn.qbytes : 16u, lane);
+      }
+      load_chunks(pq, tn.pp, tn.bigp ? 16u : tn.pbytes, lane);
+      const int ta = tc.tp, tb = tc.tq;
+      const bool eff = eff_rule<OP>(ta, tb, tc.cp, tc.cq);
+      int r;
+      metrics(w, lane, eff && !CARD_ONLY, c, r);
+      if (OP != RB_OR && c == 0) ty = kEmpty;
+      else if (eff) ty = type_eff(c, r);
+      else if (OP == RB_OR && (ta == kBitmap || tb == kBitmap)) {
+        ty = type_lr(c);
+        if (ty == kRun) r = 1; // LR's Run is the full container: one run
+      } else ty = type_ab(c);
+      if (CARD_ONLY) ty = c ? kArray : kEmpty;
+      else if (ty != kEmpty) emit_container(ty, w, c, r, dst, s, lane);
+      nr = ty == kRun ? (uint32_t)r : 0u;
     } else {
-      uint16_t *dst = CARD_ONLY ? nullptr : reinterpret_cast<uint16_t *>(out + cur.out);
-      const int nfc = (int)((pc.nf + 7) >> 3);
-      c = OP == RB_ANDNOT ? filter_chunks<true>(fq, nfc, (int)pc.nf, s, dst, lane)
-                          : filter_chunks<false>(fq, nfc, (int)pc.nf, s, dst, lane);
-      ty = c ? kArray : kEmpty;
+      // ---- phase 1: stage X (filter) or store the clone (copy)
+      if (tc.kind == kFilter) {
+        if (tc.bigq) stage_big_runs(tc.pq, tc.rq, s, lane); // only a Run payload exceeds 8 KiB
+        else stage_from_chunks(tc.tq, qq, tc.cq, tc.rq, s, lane);
+      } else if (!CARD_ONLY) {
+        if (tc.bigp) copy_payload(tc.pp, dst, tc.pbytes, lane);
+        else store_chunks(pq, dst, tc.pbytes, lane);
+      }
+      {
+        const bool real = has_next && tn.kind != kCopy && !tn.bigq;
+        load_chunks(qq, real ? tn.pq : tn.pp, real ? tn.qbytes : 16u, lane);
+      }
+      // ---- phase 2: filter F against the staged X
+      if (tc.kind == kFilter) {
+        const int nfc = (int)((tc.cp + 7) >> 3);
+        uint16_t *o = CARD_ONLY ? nullptr : reinterpret_cast<uint16_t *>(dst);
+        c = OP == RB_ANDNOT ? filter_chunks_staged<true>(pq, nfc, (int)tc.cp, s, ob, o, lane)
+                            : filter_chunks_staged<false>(pq, nfc, (int)tc.cp, s, ob, o, lane);
+        ty = c ? kArray : kEmpty;
+      } else {
+        ty = tc.tp;
+        c = (int)tc.cp;
+        nr = tc.rp;
+      }
+      load_chunks(pq, tn.pp, tn.bigp ? 16u : tn.pbytes, lane);
     }
-    load_chunks(fq, pn.pf, min(pn.fbytes, (uint32_t)kBitmapBytes), lane);
     wave_lds_sync(); // the next task restages the same LDS image
     if (lane == 0) {
       tm.type[cur.t] = (uint8_t)ty;
@@ -307,14 +398,15 @@ __global__ __launch_bounds__(256, 4) void k_pair_light(const uint8_t *__restrict
     if (!has_next) break;
     g = gn;
     cur = nx;
-    pc = pn;
+    tc = tn;
   }
 }
 
-// Everything else: ONE WAVE PER TASK, both containers as 65536-bit register bitmaps, word op,
-// card + maximal runs, reference type decision, coalesced emission.
+// The register path without a software pipeline: ONE WAVE PER TASK, one launch-sized grid (3
+// waves per SIMD; the hardware dispatcher supplies the next task).  Both containers as 65536-bit
+// register bitmaps, word op, card + maximal runs, reference type decision, coalesced emission.
 template <int OP, bool CARD_ONLY>
-__global__ __launch_bounds__(256) void k_pair_heavy(const uint8_t *__restrict__ pay_a,
+__global__ __launch_bounds__(256) void k_pair_heavy_np(const uint8_t *__restrict__ pay_a,
                                                     const uint8_t *__restrict__ pay_b,
                                                     const TaskRec *__restrict__ recs, uint64_t n,
                                                     uint8_t *__restrict__ out, TaskMeta tm) {
@@ -372,6 +464,79 @@ __global__ __launch_bounds__(256) void k_pair_heavy(const uint8_t *__restrict__ 
   }
 }
 
+// ---------------------------------------------------------------- measurement probes
+// Read-only twins of k_pair_tasks for the roofline study (rbgpu_internal_probe): the same
+// persistent schedule, records and payload loads, with the compute replaced by an XOR fold, and a
+// plain streaming read of one payload arena.  They bound what the memory system delivers for
+// this access pattern; nothing in the product calls them.
+__device__ __forceinline__ uint32_t fold_chunks(const uint4 (&q)[8]) {
+  uint32_t x = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) x ^= q[i].x ^ q[i].y ^ q[i].z ^ q[i].w;
+  return x;
+}
+template <int OP>
+__global__ __launch_bounds__(256, 4) void k_probe_tasks(const uint8_t *__restrict__ pay_a,
+                                                     const uint8_t *__restrict__ pay_b,
+                                                     const TaskRec *__restrict__ recs, uint64_t n, uint32_t *sink) {
+  const int lane = lane_id();
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint64_t stride = (uint64_t)gridDim.x * 4;
+  uint64_t g = (uint64_t)blockIdx.x * 4 + wv;
+  if (g >= n) return;
+  RecU cur = load_rec(recs + g);
+  Task tc = decode_task<OP>(cur, pay_a, pay_b);
+  uint4 pq[8], qq[8];
+  load_chunks(pq, tc.pp, tc.bigp ? 16u : tc.pbytes, lane);
+  if (tc.kind == kCopy || tc.bigq) load_chunks(qq, tc.pp, 16, lane);
+  else load_chunks(qq, tc.pq, tc.qbytes, lane);
+  uint32_t acc = 0;
+  while (true) {
+    const uint64_t gn = g + stride;
+    const bool has_next = gn < n;
+    const RecU nx = load_rec(recs + (has_next ? gn : g));
+    const Task tn = decode_task<OP>(nx, pay_a, pay_b);
+    acc ^= fold_chunks(qq);
+    {
+      const bool real = has_next && tn.kind != kCopy && !tn.bigq;
+      load_chunks(qq, real ? tn.pq : tn.pp, real ? tn.qbytes : 16u, lane);
+    }
+    acc ^= fold_chunks(pq);
+    load_chunks(pq, tn.pp, tn.bigp ? 16u : tn.pbytes, lane);
+    if (!has_next) break;
+    g = gn;
+    tc = tn;
+  }
+  sink[(uint64_t)blockIdx.x * 256 + threadIdx.x] = acc;
+}
+__global__ __launch_bounds__(256, 4) void k_probe_stream(const uint8_t *__restrict__ p, uint64_t bytes,
+                                                      uint32_t *sink) {
+  const int lane = lane_id();
+  const uint64_t w = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6), nw = (uint64_t)gridDim.x * 4;
+  const uint64_t chunks = bytes / 8192;
+  uint32_t acc = 0;
+  for (uint64_t c = w; c < chunks; c += nw) {
+    uint4 q[8];
+    load_chunks(q, p + c * 8192, 8192, lane);
+    acc ^= fold_chunks(q);
+  }
+  sink[(uint64_t)blockIdx.x * 256 + threadIdx.x] = acc;
+}
+void launch_probe(int op, int mode, const uint8_t *pa, const uint8_t *pb, uint64_t a_bytes, const TaskRec *recs,
+                  uint64_t n, uint32_t *sink, unsigned blocks, hipStream_t st) {
+  if (mode == 2) {
+    k_probe_stream<<<blocks, 256, 0, st>>>(pa, a_bytes, sink);
+    return;
+  }
+  if (!n) return;
+  switch (op) {
+  case RB_AND: k_probe_tasks<RB_AND><<<blocks, 256, 0, st>>>(pa, pb, recs, n, sink); break;
+  case RB_OR: k_probe_tasks<RB_OR><<<blocks, 256, 0, st>>>(pa, pb, recs, n, sink); break;
+  case RB_XOR: k_probe_tasks<RB_XOR><<<blocks, 256, 0, st>>>(pa, pb, recs, n, sink); break;
+  default: k_probe_tasks<RB_ANDNOT><<<blocks, 256, 0, st>>>(pa, pb, recs, n, sink); break;
+  }
+}
+
 // ---------------------------------------------------------------- compaction
 __global__ __launch_bounds__(kPairThreads) void k_compact_count(const uint64_t *tb, uint32_t npairs,
                                                                 const uint8_t *ttype, uint64_t *cnt) {
@@ -426,34 +591,42 @@ void launch_pair_emit(const PairArgs &a, const PairCountArrays &scans, uint64_t 
 }
 // Persistent grid: every CU filled to the kernel's occupancy, waves stride over the tasks.
 template <class K> static unsigned persistent_blocks(K kernel, uint64_t tasks) {
-  static int cus = 0, occ = 0;
-  if (!cus) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kernel, 256, 0);
-    if (cus <= 0) cus = 256;
-    if (occ <= 0) occ = 4;
-  }
+  int dev = 0, cus = 0, occ = 0;
+  (void)hipGetDevice(&dev);
+  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kernel, 256, 0);
+  if (cus <= 0) cus = 256;
+  if (occ <= 0) occ = 4;
   const uint64_t want = (tasks + 3) / 4, cap = (uint64_t)cus * (uint64_t)occ;
   return (unsigned)(want < cap ? want : cap);
 }
 
+template <int OP, bool CARD_ONLY, int ROLE>
+static void launch_tasks(const uint8_t *pa, const uint8_t *pb, const TaskRec *recs, uint64_t n, uint8_t *out,
+                         const TaskMeta &tm, hipStream_t st) {
+  if (!n) return;
+  static unsigned cap = 0; // occupancy-derived grid cap, per template instance
+  if (!cap) cap = persistent_blocks(k_pair_tasks<OP, CARD_ONLY, ROLE>, ~0ull >> 8);
+  const uint64_t want = (n + 3) / 4;
+  const unsigned blocks = (unsigned)(want < cap ? want : cap);
+  k_pair_tasks<OP, CARD_ONLY, ROLE><<<blocks, 256, 0, st>>>(pa, pb, recs, n, out, tm);
+}
 template <int OP>
 static void launch_op(bool card_only, const uint8_t *pa, const uint8_t *pb, const TaskRec *light, uint64_t nl,
                       const TaskRec *heavy, uint64_t nh, uint8_t *out, const TaskMeta &tm, hipStream_t st,
                       hipEvent_t mid) {
-  if (nl) {
-    if (card_only)
-      k_pair_light<OP, true><<<persistent_blocks(k_pair_light<OP, true>, nl), 256, 0, st>>>(pa, pb, light, nl, out, tm);
-    else
-      k_pair_light<OP, false><<<persistent_blocks(k_pair_light<OP, false>, nl), 256, 0, st>>>(pa, pb, light, nl, out, tm);
-  }
+  if (card_only) launch_tasks<OP, true, kRoleLight>(pa, pb, light, nl, out, tm, st);
+  else launch_tasks<OP, false, kRoleLight>(pa, pb, light, nl, out, tm, st);
   (void)hipEventRecord(mid, st);
+#if RBG_HEAVY_PERSISTENT
+  if (card_only) launch_tasks<OP, true, kRoleHeavy>(pa, pb, heavy, nh, out, tm, st);
+  else launch_tasks<OP, false, kRoleHeavy>(pa, pb, heavy, nh, out, tm, st);
+#else
   if (nh) {
-    if (card_only) k_pair_heavy<OP, true><<<blocks_for(nh, 4), 256, 0, st>>>(pa, pb, heavy, nh, out, tm);
-    else k_pair_heavy<OP, false><<<blocks_for(nh, 4), 256, 0, st>>>(pa, pb, heavy, nh, out, tm);
+    if (card_only) k_pair_heavy_np<OP, true><<<blocks_for(nh, 4), 256, 0, st>>>(pa, pb, heavy, nh, out, tm);
+    else k_pair_heavy_np<OP, false><<<blocks_for(nh, 4), 256, 0, st>>>(pa, pb, heavy, nh, out, tm);
   }
+#endif
 }
 void launch_pairwise(int op, bool card_only, const uint8_t *pa, const uint8_t *pb, const TaskRec *light,
                      uint64_t nl, const TaskRec *heavy, uint64_t nh, uint8_t *out, const TaskMeta &tm,

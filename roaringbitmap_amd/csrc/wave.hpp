@@ -26,39 +26,46 @@ __device__ __forceinline__ void wave_lds_sync() {
 
 __device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & 63); }
 
-__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += (uint32_t)__shfl_xor((int)v, o);
+// ---- wave collectives on DPP (VALU lane crossbar: no LDS round trip, no bpermute chain).
+// dpp_ctrl: row_shr:n = 0x110+n, wave_shl:1 = 0x130, wave_shr:1 = 0x138, row_bcast:15 = 0x142,
+// row_bcast:31 = 0x143.  Lanes without a source (or in rows masked off) read 0.
+template <int CTRL, int ROW_MASK = 0xf, bool BOUND_ZERO = true>
+__device__ __forceinline__ uint32_t dpp(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, ROW_MASK, 0xf, BOUND_ZERO);
+}
+__device__ __forceinline__ uint32_t readlane(uint32_t x, int l) {
+  return (uint32_t)__builtin_amdgcn_readlane((int)x, l);
+}
+// inclusive prefix sum over the 64 lanes: Hillis-Steele within each row of 16, then the row
+// totals broadcast forward (row_bcast:15 into rows 1 and 3, row_bcast:31 into rows 2 and 3)
+__device__ __forceinline__ uint32_t wave_scan_u32(uint32_t v, int /*lane*/) {
+  v += dpp<0x111>(v);
+  v += dpp<0x112>(v);
+  v += dpp<0x114>(v);
+  v += dpp<0x118>(v);
+  v += dpp<0x142, 0xa, false>(v);
+  v += dpp<0x143, 0xc, false>(v);
   return v;
 }
+__device__ __forceinline__ uint32_t wave_xscan_xor(uint32_t v, int /*lane*/) { // inclusive xor-scan
+  v ^= dpp<0x111>(v);
+  v ^= dpp<0x112>(v);
+  v ^= dpp<0x114>(v);
+  v ^= dpp<0x118>(v);
+  v ^= dpp<0x142, 0xa, false>(v);
+  v ^= dpp<0x143, 0xc, false>(v);
+  return v;
+}
+// inclusive prefix sum of packed 16-bit fields (no field may reach 65536 over the wave): the two
+// 32-bit halves scan independently
+__device__ __forceinline__ uint64_t wave_scan_u64(uint64_t v, int lane) {
+  return (uint64_t)wave_scan_u32((uint32_t)v, lane) | ((uint64_t)wave_scan_u32((uint32_t)(v >> 32), lane) << 32);
+}
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) { return readlane(wave_scan_u32(v, 0), 63); }
+// 64-bit sum (accounting counters): shuffles, off the hot loops
 __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += (uint64_t)__shfl_xor((unsigned long long)v, o);
-  return v;
-}
-// inclusive prefix sum over lanes (fields packed in a u64 must not overflow)
-__device__ __forceinline__ uint64_t wave_scan_u64(uint64_t v, int lane) {
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    uint64_t t = (uint64_t)__shfl_up((unsigned long long)v, d);
-    if (lane >= d) v += t;
-  }
-  return v;
-}
-__device__ __forceinline__ uint32_t wave_scan_u32(uint32_t v, int lane) {
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    uint32_t t = (uint32_t)__shfl_up((int)v, d);
-    if (lane >= d) v += t;
-  }
-  return v;
-}
-__device__ __forceinline__ uint32_t wave_xscan_xor(uint32_t v, int lane) { // inclusive xor-scan
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    uint32_t t = (uint32_t)__shfl_up((int)v, d);
-    if (lane >= d) v ^= t;
-  }
   return v;
 }
 
@@ -99,6 +106,30 @@ __device__ __forceinline__ void lds_write_words(uint32_t *s, const uint64_t (&w)
                                    (uint32_t)(w[2 * k + 1] >> 32));
 }
 
+// OR one lane's chunk of sorted values (n <= 8) into the LDS bitmap, one access per 32-bit word
+// group.  Only the first and last group of a chunk can share a word with another lane's chunk (the
+// array is sorted), so those use ds_or; the groups between are owned by this lane: plain stores
+// (the image was zeroed).
+__device__ __forceinline__ void or_chunk_values(const uint32_t (&x)[8], int n, uint32_t *s) {
+  uint32_t cw = x[0] >> 5, acc = 0;
+  bool first = true;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    if (i < n) {
+      const uint32_t wi = x[i] >> 5;
+      if (wi != cw) {
+        if (first) atomicOr(&s[cw], acc);
+        else s[cw] = acc;
+        first = false;
+        cw = wi;
+        acc = 0;
+      }
+      acc |= 1u << (x[i] & 31);
+    }
+  }
+  atomicOr(&s[cw], acc);
+}
+
 // OR the values of a sorted u16 array (payload 16-B aligned) into the LDS bitmap `s`.  Each lane
 // takes 8 consecutive values per 16-B load (coalesced), folds them per 32-bit word and issues
 // one ds_or per word.
@@ -109,21 +140,7 @@ __device__ __forceinline__ void lds_or_array(const uint16_t *vals, int card, uin
     uint4 q = v4[c];
     uint32_t x[8] = {q.x & 0xFFFF, q.x >> 16, q.y & 0xFFFF, q.y >> 16,
                      q.z & 0xFFFF, q.z >> 16, q.w & 0xFFFF, q.w >> 16};
-    const int n = min(8, card - 8 * c);
-    uint32_t cw = x[0] >> 5, acc = 0;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      if (i < n) {
-        uint32_t wi = x[i] >> 5;
-        if (wi != cw) {
-          atomicOr(&s[cw], acc);
-          cw = wi;
-          acc = 0;
-        }
-        acc |= 1u << (x[i] & 31);
-      }
-    }
-    atomicOr(&s[cw], acc);
+    or_chunk_values(x, min(8, card - 8 * c), s);
   }
 }
 
@@ -160,7 +177,7 @@ __device__ __forceinline__ void toggles_to_words(uint64_t (&t)[kW], int lane) { 
   }
   const uint32_t incl = wave_xscan_xor(q, lane);
   const uint32_t excl = incl ^ q;
-  const uint32_t tot = (uint32_t)__shfl((int)incl, 63);
+  const uint32_t tot = readlane(incl, 63);
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
     uint32_t rowc = __popc(tot & ((1u << k) - 1)) & 1;
@@ -185,7 +202,7 @@ __device__ __forceinline__ void toggles_to_words_lds(uint32_t *s, int lane) {
   }
   const uint32_t incl = wave_xscan_xor(q, lane);
   const uint32_t excl = incl ^ q;
-  const uint32_t tot = (uint32_t)__shfl((int)incl, 63);
+  const uint32_t tot = readlane(incl, 63);
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
     const uint4 v = s4[k * 64 + lane];
@@ -286,11 +303,88 @@ __device__ __forceinline__ int filter_chunks(const uint4 (&fq)[8], int nfc, int 
         for (int k = 0; k < 8; ++k)
           if ((keep >> k) & 1) out[pos++] = (uint16_t)x[k];
       }
-      total += (uint32_t)__shfl((int)incl, 63);
+      total += readlane(incl, 63);
     }
     __builtin_amdgcn_sched_barrier(0);
   }
   return (int)total;
+}
+
+// Exclusive prefix (over lanes) and wave total of a per-lane count in [0, 16), by bit-sliced ballots
+// and mbcnt: no cross-lane data movement through LDS, no dependency chain of shuffles.
+__device__ __forceinline__ uint32_t mbcnt64(uint64_t m) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+__device__ __forceinline__ void ballot_scan4(uint32_t cnt, uint32_t &excl, uint32_t &total) {
+  excl = 0;
+  total = 0;
+#pragma unroll
+  for (int b = 0; b < 4; ++b) {
+    const uint64_t m = __ballot((cnt >> b) & 1);
+    excl += mbcnt64(m) << b;
+    total += (uint32_t)__popcll(m) << b;
+  }
+}
+
+// The same filter with coalesced output.  Kept values are ranked into a per-wave LDS ring `ob` of
+// kStageRing u16 (16-B aligned); after each row every complete 16-B block of ranked values is
+// written with one 16-B-per-lane store.  At most 7 + 512 values are pending, so a ring of 640
+// never overwrites a pending value, and a block never straddles the wrap (640 % 8 == 0).  One
+// wave's LDS operations execute in order, so the ranked writes, the block reads and the next
+// row's writes need no drains between them.  The final partial block is written whole: result
+// slots are round16(2 * bound) bytes, so bytes past the last value stay in the slot's padding.
+// Rejected values go to a per-lane dummy slot instead of being branched around.
+constexpr int kStageRing = 640;
+constexpr int kStageVals = kStageRing + 64;   // + one dummy slot per lane
+template <bool NEGATE>
+__device__ __forceinline__ int filter_chunks_staged(const uint4 (&fq)[8], int nfc, int nf, const uint32_t *s,
+                                                    uint16_t *ob, uint16_t *out, int lane) {
+  const int iters = (nfc + 63) >> 6; // wave-uniform, <= 8
+  uint32_t flushed = 0, tot = 0;     // values written out / ranked so far (wave-uniform)
+  uint4 *out4 = reinterpret_cast<uint4 *>(out);
+  const uint4 *ob4 = reinterpret_cast<const uint4 *>(ob);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    if (i < iters) {
+      const int c = lane + 64 * i;
+      const int n = c < nfc ? min(8, nf - 8 * c) : 0;
+      const uint32_t x[8] = {fq[i].x & 0xFFFF, fq[i].x >> 16, fq[i].y & 0xFFFF, fq[i].y >> 16,
+                             fq[i].z & 0xFFFF, fq[i].z >> 16, fq[i].w & 0xFFFF, fq[i].w >> 16};
+      // all 8 probes in flight before the first wait: one LDS round trip per row, not eight
+      uint32_t m[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) m[k] = s[x[k] >> 5];
+      __builtin_amdgcn_sched_group_barrier(0x100, 8, 0); // DS reads first
+      __builtin_amdgcn_sched_group_barrier(0x002, 64, 0); // then the VALU work
+      uint32_t keep = 0;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) keep |= (((m[k] >> (x[k] & 31)) & 1) ^ (NEGATE ? 1u : 0u)) << k;
+      keep &= (1u << n) - 1; // n <= 8: lanes past the payload keep nothing
+      uint32_t excl, rowtot;
+      ballot_scan4((uint32_t)__popc(keep), excl, rowtot);
+      if (out) {
+        uint32_t base = tot % kStageRing + excl; // < 640 + 512
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          uint32_t pos = base + (uint32_t)__popc(keep & ((1u << k) - 1));
+          pos = pos >= (uint32_t)kStageRing ? pos - kStageRing : pos;
+          ob[((keep >> k) & 1) ? pos : (uint32_t)(kStageRing + lane)] = (uint16_t)x[k];
+        }
+        const uint32_t full = (tot + rowtot) & ~7u; // values in complete blocks
+        const uint32_t nb = (full - flushed) >> 3, b0 = flushed >> 3;
+        if ((uint32_t)lane < nb) {
+          uint32_t rb = b0 + lane; // ring block
+          rb %= (uint32_t)(kStageRing / 8);
+          out4[b0 + lane] = ob4[rb];
+        }
+        flushed = full;
+      }
+      tot += rowtot;
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  if (out && tot > flushed && lane == 0) out4[flushed >> 3] = ob4[(flushed >> 3) % (kStageRing / 8)];
+  return (int)tot;
 }
 
 // ---------------------------------------------------------------- register-preloaded payloads
@@ -336,31 +430,32 @@ __device__ __forceinline__ void stage_from_chunks(int type, const uint4 (&q)[8],
         if (c < nchunks) {
           const uint32_t x[8] = {q[i].x & 0xFFFF, q[i].x >> 16, q[i].y & 0xFFFF, q[i].y >> 16,
                                  q[i].z & 0xFFFF, q[i].z >> 16, q[i].w & 0xFFFF, q[i].w >> 16};
-          const int n = min(8, (int)card - 8 * c);
-          uint32_t cw = x[0] >> 5, acc = 0;
-#pragma unroll
-          for (int k = 0; k < 8; ++k) {
-            if (k < n) {
-              const uint32_t wi = x[k] >> 5;
-              if (wi != cw) {
-                atomicOr(&s[cw], acc);
-                cw = wi;
-                acc = 0;
-              }
-              acc |= 1u << (x[k] & 31);
-            }
-          }
-          atomicOr(&s[cw], acc);
+          or_chunk_values(x, min(8, (int)card - 8 * c), s);
         }
       }
     } else {
+      // A lane's chunk of 4 canonical runs gives 8 strictly increasing toggle positions (start,
+      // end+1; runs are sorted and non-adjacent), so they group by word exactly like sorted Array
+      // values: only the first and last word of a chunk can be shared with a neighbour chunk, and
+      // within a word the toggles are distinct bits (OR == XOR).  An end+1 of 65536 is dropped.
+      const int nchunks = (int)((nruns + 3) >> 2);
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
-        const uint32_t base = 4u * (uint32_t)(lane + 64 * i);
-        const uint32_t r[4] = {q[i].x, q[i].y, q[i].z, q[i].w};
+        const int c = lane + 64 * i;
+        if (c < nchunks) {
+          const uint32_t r[4] = {q[i].x, q[i].y, q[i].z, q[i].w};
+          uint32_t x[8];
 #pragma unroll
-        for (int k = 0; k < 4; ++k)
-          if (base + k < nruns) toggle_run(s, r[k]);
+          for (int k = 0; k < 4; ++k) {
+            x[2 * k] = r[k] & 0xFFFF;
+            x[2 * k + 1] = (r[k] & 0xFFFF) + (r[k] >> 16) + 1;
+          }
+          const int nr = min(4, (int)nruns - 4 * c);
+          int n = 2 * nr;
+          const uint32_t last = nr == 4 ? x[7] : nr == 3 ? x[5] : nr == 2 ? x[3] : x[1];
+          if (last >= (uint32_t)kSpan) --n; // only the container's last run can end at 65535
+          or_chunk_values(x, n, s);
+        }
       }
       wave_lds_sync();
       toggles_to_words_lds(s, lane);
@@ -382,10 +477,10 @@ __device__ __forceinline__ Neigh neighbours(const uint64_t (&w)[kW], int lane) {
     top1 |= (uint32_t)(w[2 * k + 1] >> 63) << k;
     bot0 |= (uint32_t)(w[2 * k] & 1) << k;
   }
-  uint32_t up = (uint32_t)__shfl_up((int)top1, 1);
-  uint32_t last = (uint32_t)__shfl((int)top1, 63);
-  uint32_t dn = (uint32_t)__shfl_down((int)bot0, 1);
-  uint32_t first = (uint32_t)__shfl((int)bot0, 0);
+  const uint32_t up = dpp<0x138>(top1);  // wave_shr:1 — lane L reads lane L-1
+  const uint32_t last = readlane(top1, 63);
+  const uint32_t dn = dpp<0x130>(bot0);  // wave_shl:1 — lane L reads lane L+1
+  const uint32_t first = readlane(bot0, 0);
   Neigh n;
   n.prev_top_h0 = lane ? up : ((last << 1) & 0xFE);
   n.next_bot_h1 = lane < 63 ? dn : ((first >> 1) & 0x7F);
@@ -417,9 +512,8 @@ __device__ __forceinline__ void metrics(const uint64_t (&w)[kW], int lane, bool 
 #pragma unroll
     for (int j = 0; j < kW; ++j) r += __popcll(run_starts(w, n, j));
   }
-  uint64_t t = wave_sum_u64(pack2(c, r));
-  card = (int)(uint32_t)t;
-  runs = (int)(t >> 32);
+  card = (int)wave_sum_u32(c);
+  runs = want_runs ? (int)wave_sum_u32(r) : 0;
 }
 
 // ---------------------------------------------------------------- type rules
@@ -463,8 +557,8 @@ __device__ __forceinline__ uint32_t emit_container(int type, const uint64_t (&w)
     const uint64_t P1 = (uint64_t)n[4] | ((uint64_t)n[5] << 16) | ((uint64_t)n[6] << 32) | ((uint64_t)n[7] << 48);
     const uint64_t S0 = wave_scan_u64(P0, lane), S1 = wave_scan_u64(P1, lane);
     const uint64_t E0 = S0 - P0, E1 = S1 - P1;
-    const uint64_t T0 = (uint64_t)__shfl((unsigned long long)S0, 63);
-    const uint64_t T1 = (uint64_t)__shfl((unsigned long long)S1, 63);
+    const uint64_t T0 = pack2(readlane((uint32_t)S0, 63), readlane((uint32_t)(S0 >> 32), 63));
+    const uint64_t T1 = pack2(readlane((uint32_t)S1, 63), readlane((uint32_t)(S1 >> 32), 63));
     uint32_t rowoff = 0;
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
@@ -490,20 +584,18 @@ __device__ __forceinline__ uint32_t emit_container(int type, const uint64_t (&w)
     wave_lds_sync();
     return bytes;
   }
-  // Run: S[rank] = start, E[rank] = end; the i-th end closes the i-th run.
+  // Run: S[rank] = start, E[rank] = end; the i-th end closes the i-th run.  Run starts are
+  // recomputed where they are used (3 ops per word) rather than held in 32 more VGPRs.
   Neigh nb = neighbours(w, lane);
   uint32_t ns[8];
-  uint64_t st[kW];
 #pragma unroll
-  for (int j = 0; j < kW; ++j) st[j] = run_starts(w, nb, j);
-#pragma unroll
-  for (int k = 0; k < 8; ++k) ns[k] = __popcll(st[2 * k]) + __popcll(st[2 * k + 1]);
+  for (int k = 0; k < 8; ++k) ns[k] = __popcll(run_starts(w, nb, 2 * k)) + __popcll(run_starts(w, nb, 2 * k + 1));
   const uint64_t P0 = (uint64_t)ns[0] | ((uint64_t)ns[1] << 16) | ((uint64_t)ns[2] << 32) | ((uint64_t)ns[3] << 48);
   const uint64_t P1 = (uint64_t)ns[4] | ((uint64_t)ns[5] << 16) | ((uint64_t)ns[6] << 32) | ((uint64_t)ns[7] << 48);
   const uint64_t S0 = wave_scan_u64(P0, lane), S1 = wave_scan_u64(P1, lane);
   const uint64_t E0 = S0 - P0, E1 = S1 - P1;
-  const uint64_t T0 = (uint64_t)__shfl((unsigned long long)S0, 63);
-  const uint64_t T1 = (uint64_t)__shfl((unsigned long long)S1, 63);
+  const uint64_t T0 = pack2(readlane((uint32_t)S0, 63), readlane((uint32_t)(S0 >> 32), 63));
+  const uint64_t T1 = pack2(readlane((uint32_t)S1, 63), readlane((uint32_t)(S1 >> 32), 63));
   uint16_t *S = s16, *E = s16 + 2048;
   uint32_t rowoff = 0;
 #pragma unroll
@@ -520,7 +612,7 @@ __device__ __forceinline__ uint32_t emit_container(int type, const uint64_t (&w)
       const uint32_t open = (uint32_t)(h ? (w[j - 1] >> 63) : ((nb.prev_top_h0 >> k) & 1)) & (uint32_t)(w[j] & 1);
       uint32_t ep = sp - open;
       const uint32_t base = (uint32_t)(128 * k + 2 * lane + h) << 6;
-      uint64_t x = st[j];
+      uint64_t x = run_starts(w, nb, j);
       while (x) {
         S[sp++] = (uint16_t)(base + __builtin_ctzll(x));
         x &= x - 1;
