@@ -36,25 +36,42 @@ def parse():
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--pairs", type=int, default=1_000_000, help="pairs per GPU (config 2)")
-    p.add_argument("--workload", default="pairwise_and", choices=["pairwise_and", "pairwise_or", "pairwise_xor",
-                                                                   "pairwise_andnot", "wide_or"])
-    p.add_argument("--wide-bitmaps", type=int, default=1024)
+    p.add_argument("--workload", default="pairwise_and",
+                   choices=["pairwise_and", "pairwise_or", "pairwise_xor", "pairwise_andnot", "wide_or",
+                            "wide_and_runs", "wide_xor_runs"])
+    p.add_argument("--wide-bitmaps", type=int, default=0, help="bitmaps of a wide workload (0: the config's)")
+    p.add_argument("--secondary", default="wide_or", choices=["none", "wide_or", "wide_and_runs", "wide_xor_runs"],
+                   help="key-range-sharded wide workload reported beside the headline (strong scaling)")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
     return p.parse_args()
+
+
+# Rehearsal knobs (not used by the driver): RBGPU_DIST_BACKEND=gloo keeps the collectives on the
+# host, RBGPU_SAME_DEVICE=1 puts every rank on device 0 — together they exercise the N>1 path on a
+# one-GPU box.  The production path is one rank per GPU over RCCL ("nccl").
+BACKEND = os.environ.get("RBGPU_DIST_BACKEND", "nccl")
+
+
+def coll_device(local: int = 0):
+    import torch
+    return torch.device("cuda", local) if BACKEND == "nccl" else torch.device("cpu")
 
 
 def dist_setup(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if os.environ.get("RBGPU_SAME_DEVICE") == "1":
+        local = 0
     dist = None
     if world > 1:
         import torch
         import torch.distributed as td
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        td.init_process_group("nccl", rank=rank, world_size=world)
+        if BACKEND == "nccl":
+            torch.cuda.set_device(local)
+        td.init_process_group(BACKEND, rank=rank, world_size=world)
         dist = td
     return world, rank, local, dist
 
@@ -63,7 +80,8 @@ def barrier_max(dist, value: float) -> float:
     if dist is None:
         return value
     import torch
-    t = torch.tensor([value], dtype=torch.float64, device="cuda")
+    t = torch.tensor([value], dtype=torch.float64, device=coll_device(torch.cuda.current_device()
+                                                                       if BACKEND == "nccl" else 0))
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
@@ -72,7 +90,8 @@ def allreduce_sum(dist, value: float) -> float:
     if dist is None:
         return value
     import torch
-    t = torch.tensor([value], dtype=torch.float64, device="cuda")
+    t = torch.tensor([value], dtype=torch.float64, device=coll_device(torch.cuda.current_device()
+                                                                       if BACKEND == "nccl" else 0))
     dist.all_reduce(t, op=dist.ReduceOp.SUM)
     return float(t.item())
 
@@ -112,6 +131,100 @@ def cpu_baseline(ctx, rb, a, b, op, seconds: float):
     }
 
 
+WIDE_WORKLOADS = {
+    # name: (generator workload, semantics, default bitmaps, description)
+    "wide_or": ("WL_WIDE_DENSE", "FAST_OR", 1024,
+                "config3: FastAggregation.or of {n} dense bitmaps over the full 2^32 universe"),
+    "wide_and_runs": ("WL_WIDE_RUNS", "FAST_AND", 4096,
+                      "config4: FastAggregation.and (workShyAnd) of {n} run-heavy bitmaps x 65536 keys"),
+    "wide_xor_runs": ("WL_WIDE_RUNS", "FAST_XOR", 4096,
+                      "config4: FastAggregation.xor (naive_xor) of {n} run-heavy bitmaps x 65536 keys"),
+}
+
+
+def run_wide(args, name, world, rank, local, dist, ctx, rb, nbitmaps, steps, warmup):
+    """Key-range-sharded wide aggregation: rank r generates and aggregates keys [lo_r, hi_r) of the
+    one global dataset (strong scaling: total work fixed), then the RCCL exchange of the shard
+    summaries (roaringbitmap_amd.sharding).  The synthetic data is uniform over keys, so equal key
+    ranges are byte-balanced; partition_keys() does the same from rbgpu_set_key_bytes for real data."""
+    from roaringbitmap_amd.sharding import ShardedWide
+    wl, sem_name, _, desc = WIDE_WORKLOADS[name]
+    lo, hi = (65536 * rank) // world, (65536 * (rank + 1)) // world
+    a = ctx.generate_keys(getattr(rb, wl), nbitmaps, lo, hi, seed=42)
+    sem = getattr(rb, sem_name)
+    sw = ShardedWide(dist, rank, world, device=coll_device(local)) if dist is not None else None
+
+    def step():
+        if sw is None:
+            return ctx.wide(sem, a, key_range=(lo, hi)), None
+        res = sw.aggregate(ctx, sem, a, (lo, hi))
+        return res.local, res
+
+    ctx.synchronize()
+    for _ in range(warmup):
+        r, _ = step()
+        r.close()
+    kernel_ms, kernel_bytes, in_bytes, out_bytes = [], [], 0, 0
+    barrier(dist)
+    ctx.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        r, res = step()
+        st = ctx.stats()
+        kernel_ms.append(st["main_kernel_ms"])
+        kernel_bytes.append(st["main_kernel_bytes"])
+        in_bytes += st["input_bytes"]
+        out_bytes += st["output_bytes"]
+        r.close()
+    ctx.synchronize()
+    barrier(dist)
+    elapsed = barrier_max(dist, time.perf_counter() - t0)
+    total_in = allreduce_sum(dist, float(in_bytes))
+    k_ms = barrier_max(dist, float(np.mean(kernel_ms)))
+    k_bytes = float(np.mean(kernel_bytes))
+    out = {
+        "workload": desc.format(n=nbitmaps),
+        "value": round(total_in / elapsed / 1e9, 3), "unit": "GB/s", "n_gpus": world, "steps": steps,
+        "ms_per_step": round(elapsed / steps * 1e3, 4), "scaling": "strong",
+        "input_bytes_per_step": int(total_in // steps),
+        "key_range_rank0": [lo, hi],
+        "parallelism": f"key-range shards x{world}; RCCL all_gather of shard summaries (cardinality, "
+                       f"containers, Run containers, payload bytes) per step" if world > 1 else "single GPU",
+        "roofline": {"bound": "hbm", "kernel": st["main_kernel"], "achieved": round(k_bytes / (k_ms * 1e-3) / 1e9, 2),
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(k_bytes / (k_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                     "kernel_ms_max_over_ranks": round(k_ms, 4), "algorithmic_bytes_per_launch_rank0": int(k_bytes)},
+    }
+    if res is not None:
+        out["result_cardinality"] = res.cardinality
+        out["result_serialized_bytes"] = res.serialized_size
+    a.close()
+    return out
+
+
+def wide_cpu_baseline(ctx, rb, name, seconds: float):
+    """The oracle's FastAggregation (C++ restatement) on keys [0, 64) of the same dataset, 1 thread."""
+    from oracle import rbref as R
+    wl, sem_name, n, _ = WIDE_WORKLOADS[name]
+    a = ctx.generate_keys(getattr(rb, wl), n, 0, 64, seed=42)
+    refs = [R.RefBitmap.deserialize(x) for x in a.serialize()]
+    r = ctx.wide(getattr(rb, sem_name), a)
+    sample_bytes = ctx.stats()["input_bytes"]
+    r.close()
+    a.close()
+    sem = getattr(R, sem_name)
+    passes, t0 = 0, time.perf_counter()
+    while True:
+        R.wide(sem, refs)
+        passes += 1
+        if time.perf_counter() - t0 >= seconds:
+            break
+    el = time.perf_counter() - t0
+    return {"value": round(passes * sample_bytes / el / 1e9, 3), "unit": "GB/s", "cores": 1, "kind": "port",
+            "sample": f"keys [0, 64) of the {n} generated bitmaps ({sample_bytes} algorithmic input bytes), "
+                      f"oracle/rbref.cpp {sem_name} looped for ~{seconds:.0f}s"}
+
+
 def main():
     args = parse()
     world, rank, local, dist = dist_setup(args)
@@ -119,21 +232,31 @@ def main():
     ctx = rb.Context(local)
     seed = 42 + rank
 
-    op = {"pairwise_and": rb.AND, "pairwise_or": rb.OR, "pairwise_xor": rb.XOR, "pairwise_andnot": rb.ANDNOT,
-          "wide_or": None}[args.workload]
-    if op is not None:
-        a, b = ctx.generate(rb.WL_FILTER_POSTING, args.pairs, seed=seed)
-        run = lambda: ctx.pairwise(op, a, b)  # noqa: E731
-        workload = (f"config2: batched pairwise {['AND', 'OR', 'XOR', 'ANDNOT'][op]} of {args.pairs} "
-                    f"(filter, posting-list) pairs per GPU, mixed Array/Bitmap/Run, 2^18 universe")
-        units = args.pairs
-        unit_name = "pairs"
-    else:
-        a, _ = ctx.generate(rb.WL_WIDE_DENSE, args.wide_bitmaps, seed=seed)
-        run = lambda: ctx.wide(rb.FAST_OR, a)  # noqa: E731
-        workload = f"config3: FastAggregation.or of {args.wide_bitmaps} dense bitmaps over 2^32 per GPU"
-        units = a.n_containers
-        unit_name = "input containers"
+    if args.workload in WIDE_WORKLOADS:
+        nb = args.wide_bitmaps or WIDE_WORKLOADS[args.workload][2]
+        w = run_wide(args, args.workload, world, rank, local, dist, ctx, rb, nb, args.steps, args.warmup)
+        if rank == 0:
+            line = {"metric": METRIC, "value": w["value"], "unit": "GB/s", "n_gpus": world, "steps": args.steps,
+                    "warmup": args.warmup, "ms_per_step": w["ms_per_step"], "higher_is_better": True,
+                    "scaling": "strong", "vs_baseline": None, "dtype": "u64",
+                    "data": "synthetic (device SplitMix64 generator keyed by (bitmap, key); SURVEY §8d)",
+                    "config": {k: v for k, v in w.items() if k not in ("value", "roofline", "ms_per_step")},
+                    "roofline": dict(w["roofline"], traffic=None)}
+            if world == 1 and not args.no_cpu_baseline:
+                line["cpu_baseline"] = wide_cpu_baseline(ctx, rb, args.workload, args.cpu_seconds / 2)
+            print(json.dumps(line), flush=True)
+        if dist is not None:
+            dist.destroy_process_group()
+        return
+
+    op = {"pairwise_and": rb.AND, "pairwise_or": rb.OR, "pairwise_xor": rb.XOR, "pairwise_andnot": rb.ANDNOT}[
+        args.workload]
+    a, b = ctx.generate(rb.WL_FILTER_POSTING, args.pairs, seed=seed)
+    run = lambda: ctx.pairwise(op, a, b)  # noqa: E731
+    workload = (f"config2: batched pairwise {['AND', 'OR', 'XOR', 'ANDNOT'][op]} of {args.pairs} "
+                f"(filter, posting-list) pairs per GPU, mixed Array/Bitmap/Run, 2^18 universe")
+    units = args.pairs
+    unit_name = "pairs"
     ctx.synchronize()
 
     for _ in range(args.warmup):
@@ -210,8 +333,18 @@ def main():
                             for n, v in per_kernel.items()},
             },
         }
-        if world == 1 and not args.no_cpu_baseline and op is not None:
+        if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(ctx, rb, a, b, op, args.cpu_seconds)
+    if args.secondary != "none":
+        a.close()
+        b.close()
+        w = run_wide(args, args.secondary, world, rank, local, dist, ctx, rb,
+                     WIDE_WORKLOADS[args.secondary][2], max(3, args.steps // 3), 1)
+        if rank == 0:
+            if world == 1 and not args.no_cpu_baseline:
+                w["cpu_baseline"] = wide_cpu_baseline(ctx, rb, args.secondary, args.cpu_seconds / 2)
+            line["secondary"] = {args.secondary: w}
+    if rank == 0:
         print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()

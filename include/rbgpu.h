@@ -122,6 +122,19 @@ int rbgpu_set_serialized_sizes(const rbgpu_set *set, uint64_t *out /* [n_bitmaps
  * offsets[count+1] receives each bitmap's start — RoaringArray.java:851-940 */
 int rbgpu_set_serialize(const rbgpu_set *set, uint32_t first, uint32_t count, uint8_t *dst,
                         uint64_t cap, uint64_t *offsets);
+/* Per-bitmap summary: what a RoaringFormatSpec header over a sharded result needs
+ * (RoaringBitmap.getCardinality, RoaringArray.size / hasRunContainer / serializedSizeInBytes,
+ * RoaringArray.java:851-953). */
+typedef struct rb_bitmap_summary {
+  uint64_t cardinality;
+  uint64_t n_containers;
+  uint64_t n_run_containers;
+  uint64_t payload_bytes; /* serialized container payloads (Run: 2 + 4 * nruns), no header */
+} rb_bitmap_summary;
+int rbgpu_set_summaries(const rbgpu_set *set, uint32_t first, uint32_t count, rb_bitmap_summary *out);
+/* Algorithmic bytes (payload + 16 B metadata) per high key over every container of the set:
+ * out[65536].  Feeds the byte-balanced key-range partition of a sharded wide aggregation. */
+int rbgpu_set_key_bytes(const rbgpu_set *set, uint64_t *out);
 /* Download bitmaps [first, first+count) as host SoA.  Call once with soa->key == NULL to get
  * n_containers / payload_bytes, allocate, call again to fill. */
 int rbgpu_set_download(const rbgpu_set *set, uint32_t first, uint32_t count, rb_soa *soa);
@@ -140,6 +153,13 @@ int rbgpu_pairwise_cardinality(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const
 /* ---- wide aggregation over members[0..n) of `in` (NULL = all bitmaps, in order) ------ */
 int rbgpu_wide(rbgpu_ctx *ctx, int sem, const rbgpu_set *in, const uint32_t *members, uint32_t n,
                rbgpu_set **out);
+/* The same aggregation restricted to high keys in [key_lo, key_hi): one key-range shard of it.
+ * Every key is independent and keeps its member order, so the shards of a partition of
+ * [0, 65536), concatenated in key order, are exactly rbgpu_wide's result.  For
+ * RB_NAIVE_AND the smallest member is chosen within the shard's containers; a sharded caller
+ * passes the globally ordered member list with RB_NAIVE_AND_ITER instead. */
+int rbgpu_wide_keys(rbgpu_ctx *ctx, int sem, const rbgpu_set *in, const uint32_t *members, uint32_t n,
+                    uint32_t key_lo, uint32_t key_hi, rbgpu_set **out);
 /* FastAggregation.andCardinality / orCardinality — FastAggregation.java:71-101 */
 int rbgpu_wide_cardinality(rbgpu_ctx *ctx, int op, const rbgpu_set *in, const uint32_t *members,
                            uint32_t n, uint64_t *out);
@@ -152,6 +172,11 @@ enum rb_workload {
   RB_WL_WIDE_MIXED = 2,     /* config 3b: as 1 with 70% B / 20% A / 10% R */
   RB_WL_WIDE_RUNS = 3       /* config 4: n bitmaps x 65536 keys of run-heavy containers */
 };
+/* Only the containers with high keys in [key_lo, key_hi) of a wide workload (1..3): the shard a
+ * rank owns.  Container contents are keyed by (bitmap, key), so the shards of a partition are
+ * exactly the full dataset's containers. */
+int rbgpu_generate_keys(rbgpu_ctx *ctx, int workload, uint32_t n, uint64_t seed, uint32_t key_lo, uint32_t key_hi,
+                        rbgpu_set **a);
 /* Generates a (and b for RB_WL_FILTER_POSTING; *b may be NULL otherwise).  n = pairs or
  * bitmaps.  Every container goes through runOptimize semantics, as
  * RoaringBitmapWriter(runCompress=true) does (ContainerAppender.java:130-137). */

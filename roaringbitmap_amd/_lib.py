@@ -34,6 +34,11 @@ class RbSoa(C.Structure):
     ]
 
 
+class RbBitmapSummary(C.Structure):
+    _fields_ = [("cardinality", C.c_uint64), ("n_containers", C.c_uint64), ("n_run_containers", C.c_uint64),
+                ("payload_bytes", C.c_uint64)]
+
+
 class RbStats(C.Structure):
     _fields_ = [
         ("tasks", C.c_uint64),
@@ -75,7 +80,11 @@ SIGNATURES = {
     "rbgpu_pairwise": (C.c_int, [_P, C.c_int, _P, _P, _U32P, _U32P, C.c_uint32, C.POINTER(_P)]),
     "rbgpu_pairwise_cardinality": (C.c_int, [_P, C.c_int, _P, _P, _U32P, _U32P, C.c_uint32, _U64P]),
     "rbgpu_wide": (C.c_int, [_P, C.c_int, _P, _U32P, C.c_uint32, C.POINTER(_P)]),
+    "rbgpu_wide_keys": (C.c_int, [_P, C.c_int, _P, _U32P, C.c_uint32, C.c_uint32, C.c_uint32, C.POINTER(_P)]),
     "rbgpu_wide_cardinality": (C.c_int, [_P, C.c_int, _P, _U32P, C.c_uint32, _U64P]),
+    "rbgpu_set_key_bytes": (C.c_int, [_P, _U64P]),
+    "rbgpu_set_summaries": (C.c_int, [_P, C.c_uint32, C.c_uint32, C.POINTER(RbBitmapSummary)]),
+    "rbgpu_generate_keys": (C.c_int, [_P, C.c_int, C.c_uint32, C.c_uint64, C.c_uint32, C.c_uint32, C.POINTER(_P)]),
     "rbgpu_generate": (C.c_int, [_P, C.c_int, C.c_uint32, C.c_uint64, C.POINTER(_P), C.POINTER(_P)]),
 }
 

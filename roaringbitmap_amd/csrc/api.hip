@@ -408,6 +408,57 @@ int rbgpu_set_serialized_sizes(const rbgpu_set *s, uint64_t *out) {
   return RB_OK;
 }
 
+int rbgpu_set_summaries(const rbgpu_set *s, uint32_t first, uint32_t count, rb_bitmap_summary *out) {
+  if (!s || (count && !out)) return fail(RB_EINVAL, "null argument");
+  if ((uint64_t)first + count > s->nb) return fail(RB_EINVAL, "bitmap range out of bounds");
+  int rc = check_ctx(s->ctx);
+  if (rc) return rc;
+  rc = ensure_h_begin(s);
+  if (rc) return rc;
+  const uint64_t lo = s->h_begin[first], n = s->h_begin[first + count] - lo;
+  std::vector<uint16_t> nruns(n);
+  std::vector<uint8_t> type(n);
+  std::vector<uint32_t> card(n);
+  if (n) {
+    HIPCHK(hipMemcpyAsync(type.data(), s->type + lo, n, hipMemcpyDeviceToHost, s->ctx->stream));
+    HIPCHK(hipMemcpyAsync(nruns.data(), s->nruns + lo, n * 2, hipMemcpyDeviceToHost, s->ctx->stream));
+    HIPCHK(hipMemcpyAsync(card.data(), s->card + lo, n * 4, hipMemcpyDeviceToHost, s->ctx->stream));
+    HIPCHK(hipStreamSynchronize(s->ctx->stream));
+  }
+  for (uint32_t b = 0; b < count; ++b) {
+    rb_bitmap_summary &o = out[b];
+    o = rb_bitmap_summary{};
+    for (uint64_t i = s->h_begin[first + b] - lo; i < s->h_begin[first + b + 1] - lo; ++i) {
+      o.cardinality += card[i];
+      o.n_containers += 1;
+      o.n_run_containers += type[i] == RB_RUN;
+      o.payload_bytes += type[i] == RB_BITMAP ? 8192ull : type[i] == RB_ARRAY ? 2ull * card[i] : 2 + 4ull * nruns[i];
+    }
+  }
+  return RB_OK;
+}
+
+int rbgpu_set_key_bytes(const rbgpu_set *s, uint64_t *out) {
+  if (!s || !out) return fail(RB_EINVAL, "null argument");
+  int rc = check_ctx(s->ctx);
+  if (rc) return rc;
+  const uint64_t n = s->nc;
+  std::vector<uint16_t> key(n), nruns(n);
+  std::vector<uint8_t> type(n);
+  std::vector<uint32_t> card(n);
+  if (n) {
+    HIPCHK(hipMemcpyAsync(key.data(), s->key, n * 2, hipMemcpyDeviceToHost, s->ctx->stream));
+    HIPCHK(hipMemcpyAsync(type.data(), s->type, n, hipMemcpyDeviceToHost, s->ctx->stream));
+    HIPCHK(hipMemcpyAsync(nruns.data(), s->nruns, n * 2, hipMemcpyDeviceToHost, s->ctx->stream));
+    HIPCHK(hipMemcpyAsync(card.data(), s->card, n * 4, hipMemcpyDeviceToHost, s->ctx->stream));
+    HIPCHK(hipStreamSynchronize(s->ctx->stream));
+  }
+  std::fill(out, out + 65536, 0ull);
+  for (uint64_t i = 0; i < n; ++i)
+    out[key[i]] += (type[i] == RB_BITMAP ? 8192ull : type[i] == RB_ARRAY ? 2ull * card[i] : 4ull * nruns[i] + 2) + 16;
+  return RB_OK;
+}
+
 int rbgpu_set_serialize(const rbgpu_set *s, uint32_t first, uint32_t count, uint8_t *dst, uint64_t cap,
                         uint64_t *offsets) {
   if (!s || (count && !dst)) return fail(RB_EINVAL, "null argument");
@@ -572,7 +623,13 @@ int rbgpu_internal_probe(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu
 
 // ---------------------------------------------------------------- wide
 int rbgpu_wide(rbgpu_ctx *ctx, int sem, const rbgpu_set *in, const uint32_t *members, uint32_t n, rbgpu_set **out) {
+  return rbgpu_wide_keys(ctx, sem, in, members, n, 0, 65536, out);
+}
+
+int rbgpu_wide_keys(rbgpu_ctx *ctx, int sem, const rbgpu_set *in, const uint32_t *members, uint32_t n,
+                    uint32_t key_lo, uint32_t key_hi, rbgpu_set **out) {
   if (!out) return fail(RB_EINVAL, "null out");
+  if (key_lo > key_hi || key_hi > 65536) return fail(RB_EINVAL, "bad key range [%u, %u)", key_lo, key_hi);
   *out = nullptr;
   int rc = check_ctx(ctx);
   if (rc) return rc;
@@ -590,7 +647,7 @@ int rbgpu_wide(rbgpu_ctx *ctx, int sem, const rbgpu_set *in, const uint32_t *mem
     mem.resize(n);
     for (uint32_t i = 0; i < n; ++i) mem[i] = i;
   }
-  return wide_run(ctx, sem, in, mem, out);
+  return wide_run(ctx, sem, in, mem, key_lo, key_hi, out);
 }
 
 int rbgpu_wide_cardinality(rbgpu_ctx *ctx, int op, const rbgpu_set *in, const uint32_t *members, uint32_t n,
@@ -613,7 +670,17 @@ int rbgpu_generate(rbgpu_ctx *ctx, int workload, uint32_t n, uint64_t seed, rbgp
   *a = nullptr;
   if (b) *b = nullptr;
   if (workload == RB_WL_FILTER_POSTING && !b) return fail(RB_EINVAL, "filter/posting workload needs two outputs");
-  return generate_sets(ctx, workload, n, seed, a, b);
+  return generate_sets(ctx, workload, n, seed, 0, 65536, a, b);
+}
+
+int rbgpu_generate_keys(rbgpu_ctx *ctx, int workload, uint32_t n, uint64_t seed, uint32_t key_lo, uint32_t key_hi,
+                        rbgpu_set **a) {
+  int rc = check_ctx(ctx);
+  if (rc) return rc;
+  if (!a) return fail(RB_EINVAL, "null out");
+  *a = nullptr;
+  if (workload == RB_WL_FILTER_POSTING) return fail(RB_EINVAL, "key ranges apply to the wide workloads");
+  return generate_sets(ctx, workload, n, seed, key_lo, key_hi, a, nullptr);
 }
 
 } // extern "C"

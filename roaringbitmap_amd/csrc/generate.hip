@@ -26,8 +26,11 @@ __device__ __forceinline__ uint64_t range_mask(int wi, int a, int b) {
 __device__ void gen_container(const GenSpec &g, uint64_t cid, uint32_t *s, uint64_t (&w)[kW], int lane) {
   const int target = g.target[cid];
   const uint32_t param = g.param[cid];
-  uint64_t ls = g.seed ^ (cid * 0xD1B54A32D192ED03ull) ^ ((uint64_t)(lane + 1) * 0x8CB92BA72F3D8DD7ull);
-  uint64_t us = g.seed ^ (cid * 0xD1B54A32D192ED03ull) ^ 0x5851F42D4C957F2Dull; // wave-uniform stream
+  // content streams are keyed by the container's uid (not its position in the set), so a key-range
+  // shard regenerates exactly the containers of the full dataset
+  const uint64_t uid = g.uid[cid];
+  uint64_t ls = g.seed ^ (uid * 0xD1B54A32D192ED03ull) ^ ((uint64_t)(lane + 1) * 0x8CB92BA72F3D8DD7ull);
+  uint64_t us = g.seed ^ (uid * 0xD1B54A32D192ED03ull) ^ 0x5851F42D4C957F2Dull; // wave-uniform stream
   if (target == kGenBitmap) {
 #pragma unroll
     for (int j = 0; j < kW; ++j) {
@@ -69,7 +72,7 @@ __device__ void gen_container(const GenSpec &g, uint64_t cid, uint32_t *s, uint6
       p0 |= a << k;
     }
     const uint32_t incl = wave_xscan_xor(q, lane), excl = incl ^ q;
-    const uint32_t tot = (uint32_t)__shfl((int)incl, 63);
+    const uint32_t tot = readlane(incl, 63);
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       uint32_t c0 = (__popc(tot & ((1u << k) - 1)) & 1) ^ ((excl >> k) & 1);
@@ -177,7 +180,9 @@ struct GenStructure {
   std::vector<uint16_t> key;
   std::vector<uint8_t> target;
   std::vector<uint32_t> param;
-  void add(uint16_t k, uint8_t t, uint32_t p) {
+  std::vector<uint64_t> uid;
+  void add(uint16_t k, uint8_t t, uint32_t p, uint64_t u = ~0ull) {
+    uid.push_back(u == ~0ull ? (uint64_t)key.size() : u);
     key.push_back(k);
     target.push_back(t);
     param.push_back(p);
@@ -190,7 +195,17 @@ struct GenStructure {
 // Bitmap density U[0.07, 0.93] as a numerator over 256
 uint32_t dense_num(HostRng &r) { return 18 + r.below(238 - 18 + 1); }
 
-void structure(int workload, uint32_t n, uint64_t seed, std::vector<GenStructure> &out) {
+// Per-(bitmap, key) decision stream for the wide workloads: independent of the key range asked
+// for, so shards [lo, hi) of one seed partition the same dataset.
+HostRng key_rng(uint64_t seed, uint32_t i, uint32_t k) {
+  HostRng r{seed * 0x2545F4914F6CDD1Dull ^ ((uint64_t)i << 20) * 0x9E3779B97F4A7C15ull ^
+            ((uint64_t)k + 1) * 0xD6E8FEB86659FD93ull};
+  r.next();
+  return r;
+}
+
+void structure(int workload, uint32_t n, uint64_t seed, uint32_t key_lo, uint32_t key_hi,
+               std::vector<GenStructure> &out) {
   HostRng r{seed * 0x2545F4914F6CDD1Dull + 0x9E3779B97F4A7C15ull};
   if (workload == RB_WL_FILTER_POSTING) {
     out.resize(2);
@@ -221,21 +236,23 @@ void structure(int workload, uint32_t n, uint64_t seed, std::vector<GenStructure
   out.resize(1);
   GenStructure &g = out[0];
   for (uint32_t i = 0; i < n; ++i) {
-    for (uint32_t k = 0; k < 65536; ++k) {
+    for (uint32_t k = key_lo; k < key_hi; ++k) {
+      const uint64_t uid = ((uint64_t)i << 16) | k;
       if (workload == RB_WL_WIDE_RUNS) { // every key; shared core run per key (config 4)
         uint64_t h = (uint64_t)k * 0x9E3779B97F4A7C15ull;
         h ^= h >> 29;
-        g.add((uint16_t)k, kGenCoreRuns, (uint32_t)(h >> 32));
+        g.add((uint16_t)k, kGenCoreRuns, (uint32_t)(h >> 32), uid);
         continue;
       }
-      if (r.below(16) != 0) continue; // key present w.p. 1/16 (config 3)
+      HostRng kr = key_rng(seed, i, k);
+      if (kr.below(16) != 0) continue; // key present w.p. 1/16 (config 3)
       if (workload == RB_WL_WIDE_DENSE) {
-        g.add((uint16_t)k, kGenBitmap, 16 + r.below(9)); // d ~ U[1/16, 3/32]
+        g.add((uint16_t)k, kGenBitmap, 16 + kr.below(9), uid); // d ~ U[1/16, 3/32]
       } else {
-        uint32_t u = r.below(1000);
-        if (u < 700) g.add((uint16_t)k, kGenBitmap, 16 + r.below(9));
-        else if (u < 900) g.add((uint16_t)k, kGenArray, 1 + r.below(4096));
-        else g.add((uint16_t)k, kGenRuns, 1 + r.below(2047));
+        uint32_t u = kr.below(1000);
+        if (u < 700) g.add((uint16_t)k, kGenBitmap, 16 + kr.below(9), uid);
+        else if (u < 900) g.add((uint16_t)k, kGenArray, 1 + kr.below(4096), uid);
+        else g.add((uint16_t)k, kGenRuns, 1 + kr.below(2047), uid);
       }
     }
     g.close();
@@ -254,10 +271,12 @@ int materialize(rbgpu_ctx *ctx, const GenStructure &gs, uint64_t seed, rbgpu_set
   }
   uint8_t *d_target;
   uint32_t *d_param;
+  uint64_t *d_uid;
   uint64_t *d_big, *d_small, *d_bidx, *d_soff, *d_tmp;
   const uint64_t tmpw = std::max<uint64_t>(scan_tmp_words(n + 1), 1);
   const uint64_t nn = std::max<uint64_t>(n, 1);
   if (pool.alloc((void **)&d_target, nn) || pool.alloc((void **)&d_param, nn * 4) ||
+      pool.alloc((void **)&d_uid, nn * 8) ||
       pool.alloc((void **)&d_big, (nn + 1) * 8) || pool.alloc((void **)&d_small, (nn + 1) * 8) ||
       pool.alloc((void **)&d_bidx, (nn + 1) * 8) || pool.alloc((void **)&d_soff, (nn + 1) * 8) ||
       pool.alloc((void **)&d_tmp, tmpw * 8)) {
@@ -270,8 +289,9 @@ int materialize(rbgpu_ctx *ctx, const GenStructure &gs, uint64_t seed, rbgpu_set
     HIPCHK(hipMemcpyAsync(s->key, gs.key.data(), n * 2, hipMemcpyHostToDevice, st));
     HIPCHK(hipMemcpyAsync(d_target, gs.target.data(), n, hipMemcpyHostToDevice, st));
     HIPCHK(hipMemcpyAsync(d_param, gs.param.data(), n * 4, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(d_uid, gs.uid.data(), n * 8, hipMemcpyHostToDevice, st));
   }
-  GenSpec g{s->key, d_target, d_param, seed};
+  GenSpec g{s->key, d_target, d_param, d_uid, seed};
   launch_gen_measure(g, n, s->type, s->card, s->nruns, d_big, d_small, st);
   scan_exclusive(d_big, d_bidx, n, d_tmp, st);
   scan_exclusive(d_small, d_soff, n, d_tmp, st);
@@ -291,7 +311,7 @@ int materialize(rbgpu_ctx *ctx, const GenStructure &gs, uint64_t seed, rbgpu_set
   s->payload_bytes = total;
   launch_gen_emit(g, n, s->type, s->off, s->payload, st);
   HIPCHK(hipStreamSynchronize(st));
-  for (void *p : {(void *)d_target, (void *)d_param, (void *)d_big, (void *)d_small, (void *)d_bidx, (void *)d_soff,
+  for (void *p : {(void *)d_target, (void *)d_param, (void *)d_uid, (void *)d_big, (void *)d_small, (void *)d_bidx, (void *)d_soff,
                   (void *)d_tmp})
     pool.release(p);
   s->h_begin = gs.begin;
@@ -300,10 +320,12 @@ int materialize(rbgpu_ctx *ctx, const GenStructure &gs, uint64_t seed, rbgpu_set
 }
 } // namespace
 
-int generate_sets(rbgpu_ctx *ctx, int workload, uint32_t n, uint64_t seed, rbgpu_set **a, rbgpu_set **b) {
+int generate_sets(rbgpu_ctx *ctx, int workload, uint32_t n, uint64_t seed, uint32_t key_lo, uint32_t key_hi,
+                  rbgpu_set **a, rbgpu_set **b) {
   if (workload < RB_WL_FILTER_POSTING || workload > RB_WL_WIDE_RUNS) return fail(RB_EINVAL, "bad workload %d", workload);
+  if (key_lo > key_hi || key_hi > 65536) return fail(RB_EINVAL, "bad key range [%u, %u)", key_lo, key_hi);
   std::vector<GenStructure> gs;
-  structure(workload, n, seed, gs);
+  structure(workload, n, seed, key_lo, key_hi, gs);
   int rc = materialize(ctx, gs[0], seed * 31 + 1, a);
   if (rc) return rc;
   if (gs.size() > 1) {

@@ -131,7 +131,10 @@ struct KernelSpan {
 };
 int stats_end(rbgpu_ctx *ctx, uint64_t tasks, uint64_t result_containers, const KernelSpan *k, int n);
 // wide.hip
-int wide_run(rbgpu_ctx *ctx, int sem, const rbgpu_set *in, const std::vector<uint32_t> &members, rbgpu_set **out);
+// keys outside [key_lo, key_hi) produce no result containers (key-range shard of the aggregation)
+int wide_run(rbgpu_ctx *ctx, int sem, const rbgpu_set *in, const std::vector<uint32_t> &members, uint32_t key_lo,
+             uint32_t key_hi, rbgpu_set **out);
 // generate.hip
-int generate_sets(rbgpu_ctx *ctx, int workload, uint32_t n, uint64_t seed, rbgpu_set **a, rbgpu_set **b);
+int generate_sets(rbgpu_ctx *ctx, int workload, uint32_t n, uint64_t seed, uint32_t key_lo, uint32_t key_hi,
+                  rbgpu_set **a, rbgpu_set **b);
 } // namespace rbg

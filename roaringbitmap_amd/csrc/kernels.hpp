@@ -67,6 +67,7 @@ struct GenSpec {
   const uint16_t *key;
   const uint8_t *target;
   const uint32_t *param;
+  const uint64_t *uid;   // content stream id: position (config 2) or (bitmap << 16 | key) (wide)
   uint64_t seed;
 };
 // pass 1: card / runs / final type / payload bytes per container

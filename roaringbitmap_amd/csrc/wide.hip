@@ -66,12 +66,14 @@ __global__ __launch_bounds__(256) void k_wide_bounds(const uint16_t *sorted, uin
   seg[k] = lo;
 }
 
-// active[k] = 1 when key k produces work: any container, or (AND semantics) one per member
-__global__ __launch_bounds__(256) void k_wide_select(const uint64_t *seg, uint64_t need, uint64_t *active) {
+// active[k] = 1 when key k (inside the shard's [lo, hi)) produces work: any container, or (AND
+// semantics) one per member
+__global__ __launch_bounds__(256) void k_wide_select(const uint64_t *seg, uint64_t need, uint32_t lo, uint32_t hi,
+                                                     uint64_t *active) {
   const uint32_t k = blockIdx.x * 256 + threadIdx.x;
   if (k >= 65536) return;
   const uint64_t m = seg[k + 1] - seg[k];
-  active[k] = need ? (m == need) : (m > 0);
+  active[k] = (k >= lo && k < hi) && (need ? (m == need) : (m > 0));
 }
 __global__ __launch_bounds__(256) void k_wide_list(const uint64_t *active, const uint64_t *pos, uint32_t *klist) {
   const uint32_t k = blockIdx.x * 256 + threadIdx.x;
@@ -327,7 +329,7 @@ static void launch_reduce(const SetView &s, const uint32_t *cid, const uint64_t 
 }
 
 int wide_run(rbgpu_ctx *ctx, int sem, const rbgpu_set *in, const std::vector<uint32_t> &members_in,
-             rbgpu_set **out) {
+             uint32_t key_lo, uint32_t key_hi, rbgpu_set **out) {
   hipStream_t st = ctx->stream;
   DevPool &pool = ctx->pool;
   // effective member order: FastAggregation.and(varargs) picks workShyAnd above 10 inputs;
@@ -388,7 +390,7 @@ int wide_run(rbgpu_ctx *ctx, int sem, const rbgpu_set *in, const std::vector<uin
     }
   }
   k_wide_bounds<<<nblk(65537, 256), 256, 0, st>>>(d_keys2, N, d_seg);
-  k_wide_select<<<nblk(65536, 256), 256, 0, st>>>(d_seg, and_sem ? (uint64_t)M : 0, d_active);
+  k_wide_select<<<nblk(65536, 256), 256, 0, st>>>(d_seg, and_sem ? (uint64_t)M : 0, key_lo, key_hi, d_active);
   scan_exclusive(d_active, d_apos, 65536, d_tmp, st);
   k_wide_list<<<nblk(65536, 256), 256, 0, st>>>(d_active, d_apos, d_klist);
   uint64_t *pin = ctx->h_pinned;

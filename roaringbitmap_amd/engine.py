@@ -129,6 +129,63 @@ def soa_from_values(bitmaps: Sequence[np.ndarray], run_optimize: bool = False) -
                    np.array(card, np.uint32), np.array(nruns, np.uint16), np.array(offset, np.uint64), payload)
 
 
+def soa_from_serialized(blobs: Sequence[bytes]) -> HostSoA:
+    """Host SoA of RoaringFormatSpec bitmaps, container types as stored (the layout that
+    RoaringArray.deserialize reads, RoaringArray.java:276-348).  A host-side helper for splitting
+    and re-assembling shards; device uploads go through rbgpu_set_from_serialized, which also
+    validates."""
+    import struct
+    begin, key, typ, card, nruns, offset, chunks = [0], [], [], [], [], [], []
+    pos = 0
+    for data in blobs:
+        cookie = struct.unpack_from("<I", data, 0)[0]
+        if (cookie & 0xFFFF) == 12347:
+            n = (cookie >> 16) + 1
+            flags = data[4:4 + (n + 7) // 8]
+            p = 4 + (n + 7) // 8
+            is_run = [bool(flags[i >> 3] >> (i & 7) & 1) for i in range(n)]
+            has_offsets = n >= 4
+        elif cookie == 12346:
+            n = struct.unpack_from("<I", data, 4)[0]
+            p = 8
+            is_run = [False] * n
+            has_offsets = True
+        else:
+            raise L.FormatError(L.RB_EFORMAT, "bad cookie")
+        desc = np.frombuffer(data, np.uint16, 2 * n, p).reshape(-1, 2)
+        p += 4 * n + (4 * n if has_offsets else 0)
+        for i in range(n):
+            c = int(desc[i, 1]) + 1
+            if is_run[i]:
+                r = struct.unpack_from("<H", data, p)[0]
+                raw, t, p = data[p + 2:p + 2 + 4 * r], L.RUN, p + 2 + 4 * r
+            elif c > 4096:
+                raw, t, r, p = data[p:p + 8192], L.BITMAP, 0, p + 8192
+            else:
+                raw, t, r, p = data[p:p + 2 * c], L.ARRAY, 0, p + 2 * c
+            key.append(int(desc[i, 0]))
+            typ.append(t)
+            card.append(c)
+            nruns.append(r)
+            offset.append(pos)
+            pad = (-len(raw)) % 16
+            chunks.append(bytes(raw) + b"\0" * pad)
+            pos += len(raw) + pad
+        begin.append(len(key))
+    payload = np.frombuffer(b"".join(chunks) or b"\0" * 16, dtype=np.uint8).copy()
+    return HostSoA(np.array(begin, np.uint64), np.array(key, np.uint16), np.array(typ, np.uint8),
+                   np.array(card, np.uint32), np.array(nruns, np.uint16), np.array(offset, np.uint64), payload)
+
+
+def host_summary(h: HostSoA, b: int = 0) -> dict:
+    """rb_bitmap_summary of bitmap b of a host SoA (cf. DeviceSet.summaries)."""
+    lo, hi = int(h.begin[b]), int(h.begin[b + 1])
+    t, c, r = h.type[lo:hi].astype(np.int64), h.card[lo:hi].astype(np.int64), h.nruns[lo:hi].astype(np.int64)
+    pay = np.where(t == L.BITMAP, 8192, np.where(t == L.ARRAY, 2 * c, 2 + 4 * r))
+    return {"cardinality": int(c.sum()), "n_containers": hi - lo, "n_run_containers": int((t == L.RUN).sum()),
+            "payload_bytes": int(pay.sum())}
+
+
 class DeviceSet:
     """A batch of bitmaps resident in HBM (rbgpu_set*).  Freed on close() / GC."""
 
@@ -162,6 +219,19 @@ class DeviceSet:
     def serialized_sizes(self) -> np.ndarray:
         out = np.zeros(len(self), np.uint64)
         L.check(L.lib().rbgpu_set_serialized_sizes(self.h, out.ctypes.data_as(L._U64P)))
+        return out
+
+    def summaries(self, first: int = 0, count: Optional[int] = None) -> List[dict]:
+        """Per-bitmap cardinality / container counts / payload bytes (rbgpu_set_summaries)."""
+        count = len(self) - first if count is None else count
+        arr = (L.RbBitmapSummary * max(count, 1))()
+        L.check(L.lib().rbgpu_set_summaries(self.h, first, count, arr))
+        return [{k: int(getattr(arr[i], k)) for k, _ in L.RbBitmapSummary._fields_} for i in range(count)]
+
+    def key_bytes(self) -> np.ndarray:
+        """Algorithmic bytes per high key (rbgpu_set_key_bytes), shape [65536]."""
+        out = np.zeros(65536, np.uint64)
+        L.check(L.lib().rbgpu_set_key_bytes(self.h, out.ctypes.data_as(L._U64P)))
         return out
 
     def serialize(self, first: int = 0, count: Optional[int] = None) -> List[bytes]:
@@ -255,6 +325,12 @@ class Context:
     def upload_values(self, bitmaps: Sequence[np.ndarray], run_optimize: bool = False) -> DeviceSet:
         return self.upload_soa(soa_from_values(bitmaps, run_optimize))
 
+    def generate_keys(self, workload: int, n: int, key_lo: int, key_hi: int, seed: int = 42) -> DeviceSet:
+        """The [key_lo, key_hi) shard of a wide synthetic workload (rbgpu_generate_keys)."""
+        a = C.c_void_p()
+        L.check(L.lib().rbgpu_generate_keys(self.h, workload, n, seed, key_lo, key_hi, C.byref(a)))
+        return DeviceSet(self, a.value)
+
     def generate(self, workload: int, n: int, seed: int = 42):
         a, b = C.c_void_p(), C.c_void_p()
         L.check(L.lib().rbgpu_generate(self.h, workload, n, seed, C.byref(a), C.byref(b)))
@@ -278,11 +354,17 @@ class Context:
         L.check(L.lib().rbgpu_pairwise_cardinality(self.h, op, a.h, b.h, ap, bp, n, out.ctypes.data_as(L._U64P)))
         return out[:n]
 
-    def wide(self, sem: int, s: DeviceSet, members=None) -> DeviceSet:
+    def wide(self, sem: int, s: DeviceSet, members=None, key_range=None) -> DeviceSet:
+        """FastAggregation / ParallelAggregation over members of s; key_range=(lo, hi) computes only
+        that key-range shard (rbgpu_wide_keys)."""
         mi, mp = _idx(members)
         n = len(mi) if mi is not None else len(s)
         out = C.c_void_p()
-        L.check(L.lib().rbgpu_wide(self.h, sem, s.h, mp, n, C.byref(out)))
+        if key_range is None:
+            L.check(L.lib().rbgpu_wide(self.h, sem, s.h, mp, n, C.byref(out)))
+        else:
+            lo, hi = key_range
+            L.check(L.lib().rbgpu_wide_keys(self.h, sem, s.h, mp, n, int(lo), int(hi), C.byref(out)))
         return DeviceSet(self, out.value)
 
     def wide_cardinality(self, op: int, s: DeviceSet, members=None) -> int:

@@ -78,3 +78,49 @@ def test_generated_wide_or_sample(ctx, oracle):
     refs = [oracle.RefBitmap.deserialize(b) for b in a.serialize()]
     for sem in ("FAST_OR", "PAR_OR", "FAST_XOR", "PAR_XOR", "FAST_AND"):
         _check(ctx, oracle, a, refs, sem, np.arange(24, dtype=np.uint32))
+
+
+def test_key_range_shards_reassemble(ctx, oracle):
+    """rbgpu_wide_keys over a byte-balanced partition, concatenated in key order, gives the
+    single-call result byte for byte; NAIVE_AND via the globally ordered member list."""
+    import roaringbitmap_amd as rb
+    from roaringbitmap_amd.sharding import partition_keys, serialize_parts
+    bms = synthetic_bitmaps(40, seed=31, max_keys=8, key_space=12)
+    s = ctx.upload_values(bms, run_optimize=True)
+    kb = s.key_bytes()
+    refs = [oracle.RefBitmap.deserialize(b) for b in s.serialize()]
+    for n in (8, 11, 17):
+        members = np.arange(n, dtype=np.uint32)
+        for sem in SEMS:
+            want = oracle.wide(getattr(oracle, sem), [refs[m] for m in members]).serialize()
+            mem, sem_shard = members, getattr(rb, sem)
+            if sem == "NAIVE_AND" or (sem == "FAST_AND" and n <= 10):
+                sizes = [len(refs[m].containers()) for m in members]
+                first = int(np.argmin(sizes))  # the smallest, first on ties (FastAggregation.java:328-346)
+                mem = np.array([members[first]] + [m for i, m in enumerate(members) if i != first], np.uint32)
+                sem_shard = rb.NAIVE_AND_ITER
+            for parts in (3, 5):
+                shards = [ctx.wide(sem_shard, s, mem, key_range=r) for r in partition_keys(kb, parts)]
+                got = serialize_parts([sh.download() for sh in shards])
+                assert got == want, (sem, n, parts)
+                summ = [sh.summaries()[0] for sh in shards]
+                assert sum(x["cardinality"] for x in summ) == oracle.RefBitmap.deserialize(want).cardinality()
+
+
+def test_generated_key_shards_equal_full_dataset(ctx):
+    """rbgpu_generate_keys: shards of a partition hold exactly the full dataset's containers."""
+    import roaringbitmap_amd as rb
+    for wl in (rb.WL_WIDE_DENSE, rb.WL_WIDE_MIXED, rb.WL_WIDE_RUNS):
+        n = 3 if wl == rb.WL_WIDE_RUNS else 8
+        full, _ = ctx.generate(wl, n, seed=17)
+        hf = full.download()
+        ranges = [(0, 1000), (1000, 40000), (40000, 65536)]
+        shards = [ctx.generate_keys(wl, n, lo, hi, seed=17).download() for lo, hi in ranges]
+        for b in range(n):
+            want = [hf.container_payload(i).tobytes() + bytes([hf.type[i]]) + int(hf.key[i]).to_bytes(2, "little")
+                    for i in range(int(hf.begin[b]), int(hf.begin[b + 1]))]
+            got = []
+            for h in shards:
+                got += [h.container_payload(i).tobytes() + bytes([h.type[i]]) + int(h.key[i]).to_bytes(2, "little")
+                        for i in range(int(h.begin[b]), int(h.begin[b + 1]))]
+            assert got == want, (wl, b)

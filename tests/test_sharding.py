@@ -1,0 +1,131 @@
+"""Key-range sharding of the wide aggregations, on the CPU: the byte-balanced key
+partition, the RoaringFormatSpec writer over key-ordered parts, and the 2-rank gloo exchange
+(summary all_gather + container gather) — the shard results themselves come from the oracle here,
+the MI355X shards are covered by tests/test_gpu_wide.py."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from datasets import fixture_bytes, load_realdata, synthetic_bitmaps
+from roaringbitmap_amd import _lib as L
+from roaringbitmap_amd.engine import HostSoA, host_summary, soa_from_serialized
+from roaringbitmap_amd.sharding import ShardedWide, header_size, partition_keys, serialize_parts
+
+SEMS = {"FAST_OR": L.FAST_OR, "WORKSHY_AND": L.WORKSHY_AND, "FAST_XOR": L.FAST_XOR, "PAR_OR": L.PAR_OR,
+        "PAR_XOR": L.PAR_XOR}
+
+
+def _subset(h: HostSoA, lo: int, hi: int) -> HostSoA:
+    """Containers of bitmap 0 with keys in [lo, hi), as a one-bitmap host SoA."""
+    sel = np.nonzero((h.key >= lo) & (h.key < hi))[0]
+    return HostSoA(np.array([0, len(sel)], np.uint64), h.key[sel].copy(), h.type[sel].copy(), h.card[sel].copy(),
+                   h.nruns[sel].copy(), h.offset[sel].copy(), h.payload)
+
+
+def test_partition_keys_balanced():
+    rng = np.random.default_rng(3)
+    kb = np.zeros(65536, np.uint64)
+    kb[rng.integers(0, 65536, 5000)] = rng.integers(1, 9000, 5000)
+    for n in (1, 2, 3, 8):
+        parts = partition_keys(kb, n)
+        assert parts[0][0] == 0 and parts[-1][1] == 65536
+        assert all(parts[i][1] == parts[i + 1][0] for i in range(n - 1))
+        share = kb.sum() / n
+        for lo, hi in parts:
+            assert int(kb[lo:hi].sum()) <= share + int(kb.max())
+    # a single heavy key: the other ranges may be empty, nothing is lost
+    kb = np.zeros(65536, np.uint64)
+    kb[7] = 100
+    parts = partition_keys(kb, 4)
+    assert sum(int(kb[lo:hi].sum()) for lo, hi in parts) == 100
+
+
+def test_writer_matches_reference_fixtures():
+    # testdata/bitmapwithruns.bin / bitmapwithoutruns.bin (TestAdversarialInputs.java:32-48)
+    for name in ("bitmapwithruns.bin", "bitmapwithoutruns.bin"):
+        data = fixture_bytes(name)
+        assert serialize_parts([soa_from_serialized([data])]) == data
+
+
+@pytest.mark.parametrize("run_optimize", [False, True])
+def test_split_and_reassemble(oracle, run_optimize):
+    bms = synthetic_bitmaps(40, seed=11, max_keys=8, key_space=12)
+    for v in bms:
+        r = oracle.RefBitmap.of(v)
+        if run_optimize:
+            r.run_optimize()
+        data = r.serialize()
+        h = soa_from_serialized([data])
+        for n in (2, 3, 5):
+            kb = np.zeros(65536, np.uint64)
+            np.add.at(kb, h.key.astype(np.int64), 1)
+            parts = [_subset(h, lo, hi) for lo, hi in partition_keys(kb, n)]
+            assert serialize_parts(parts) == data
+            s = host_summary(h)
+            assert len(data) == header_size(s["n_containers"], s["n_run_containers"] > 0) + s["payload_bytes"]
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _rank_main(rank, world, port, q):
+    import torch.distributed as dist
+
+    from oracle import rbref as R
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        vals = load_realdata("census1881_srt")[:64] + synthetic_bitmaps(24, seed=5, max_keys=10, key_space=40)
+        full = [R.RefBitmap.of(v) for v in vals]
+        for r in full[::3]:
+            r.run_optimize()
+        hs = soa_from_serialized([r.serialize() for r in full])
+        kb = np.zeros(65536, np.uint64)
+        np.add.at(kb, hs.key.astype(np.int64), 1)
+        parts = partition_keys(kb, world)
+        lo, hi = parts[rank]
+        sw = ShardedWide(dist, rank, world)
+        out = {}
+        for name, sem in SEMS.items():
+            # this rank's key range of every input, in member order
+            shard_in = []
+            for i, r in enumerate(full):
+                v = r.to_array()
+                key = v >> 16
+                sub = R.RefBitmap.of(v[(key >= lo) & (key < hi)])
+                if i % 3 == 0:
+                    sub.run_optimize()
+                shard_in.append(sub)
+            local = soa_from_serialized([R.wide(sem, shard_in).serialize()])
+            res = sw.finish(local, (lo, hi), host_summary(local))
+            data = sw.gather_serialized(res)
+            if rank == 0:
+                want = R.wide(sem, full)
+                out[name] = (data == want.serialize(), res.cardinality == want.cardinality(),
+                             res.serialized_size == len(want.serialize()))
+        if rank == 0:
+            q.put(out)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_two_rank_sharded_wide():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank_main, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for name, ok in out.items():
+        assert all(ok), (name, ok)
