@@ -287,6 +287,7 @@ def main():
     elapsed = time.perf_counter() - t0
     elapsed = barrier_max(dist, elapsed)
     total_in = allreduce_sum(dist, float(in_bytes))
+    total_out = allreduce_sum(dist, float(out_bytes))  # every rank joins every collective
     main_name = st["main_kernel"]
 
     if rank == 0:
@@ -314,8 +315,8 @@ def main():
                 "unit": unit_name,
                 "input_bytes_per_step_per_gpu": in_bytes // args.steps,
                 "output_bytes_per_step_per_gpu": out_bytes // args.steps,
-                "roofline_pct_whole_step": round(100.0 * (total_in + allreduce_sum(dist, float(out_bytes)))
-                                                 / elapsed / 1e9 / (HBM_PEAK_GBS * world), 2),
+                "roofline_pct_whole_step": round(100.0 * (total_in + total_out) / elapsed / 1e9 / (HBM_PEAK_GBS * world),
+                                                 2),
                 "parallelism": f"key-range/pair sharding x{world} (replicas, no data-path collective)",
             },
             "roofline": {
