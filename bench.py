@@ -43,6 +43,7 @@ def parse():
     p.add_argument("--secondary", default="wide_or", choices=["none", "wide_or", "wide_and_runs", "wide_xor_runs"],
                    help="key-range-sharded wide workload reported beside the headline (strong scaling)")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
+    p.add_argument("--census", type=int, default=1, help="also report config 1 (census1881) at N=1")
     p.add_argument("--no-cpu-baseline", action="store_true")
     return p.parse_args()
 
@@ -225,6 +226,64 @@ def wide_cpu_baseline(ctx, rb, name, seconds: float):
                       f"oracle/rbref.cpp {sem_name} looped for ~{seconds:.0f}s"}
 
 
+CENSUS_EXPECTED = {"AND": 23, "OR": 2007691, "XOR": 2007668, "ANDNOT": 1003836}  # RealDataBenchmark*Test.java
+
+
+def load_census(name="census1881"):
+    """real-roaring-dataset zip (copied under tests/golden/realdata), entries in zip order like
+    ZipRealDataRetriever (real-roaring-dataset/.../ZipRealDataRetriever.java:50-67)."""
+    import zipfile
+    z = zipfile.ZipFile(os.path.join(ROOT, "tests", "golden", "realdata", name + ".zip"))
+    out = []
+    for info in z.infolist():
+        txt = z.read(info).decode().strip()
+        out.append(np.array([int(x) for x in txt.split(",") if x.strip()], dtype=np.uint32))
+    return out
+
+
+def run_census(args, ctx, rb):
+    """Config 1: RealDataBenchmark{And,Or,Xor,AndNot} on census1881 — 199 consecutive pairs (k, k+1)
+    of the 200 bitmaps (bitmapOf), one batched call per op; a step is the four ops."""
+    vals = load_census()
+    s = ctx.upload_values(vals)
+    n = len(vals) - 1
+    ai = np.arange(n, dtype=np.uint32)
+    bi = ai + 1
+    ops = {"AND": rb.AND, "OR": rb.OR, "XOR": rb.XOR, "ANDNOT": rb.ANDNOT}
+    cards = {k: int(ctx.pairwise(op, s, s, ai, bi).cardinalities().sum()) for k, op in ops.items()}
+    for _ in range(args.warmup):
+        for op in ops.values():
+            ctx.pairwise(op, s, s, ai, bi).close()
+    ctx.synchronize()
+    in_bytes = 0
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        for op in ops.values():
+            ctx.pairwise(op, s, s, ai, bi).close()
+            in_bytes += ctx.stats()["input_bytes"]
+    ctx.synchronize()
+    el = time.perf_counter() - t0
+    out = {"workload": "config1: census1881 RealDataBenchmark and/or/xor/andNot, 199 consecutive pairs per op",
+           "value": round(in_bytes / el / 1e9, 3), "unit": "GB/s", "ms_per_step": round(el / args.steps * 1e3, 4),
+           "us_per_op_sweep": round(el / args.steps / 4 * 1e6, 1), "cardinality_sums": cards,
+           "golden_ok": cards == CENSUS_EXPECTED}
+    if not args.no_cpu_baseline:
+        from oracle import rbref as R
+        refs = [R.RefBitmap.deserialize(x) for x in s.serialize()]
+        a_r, b_r = refs[:-1], refs[1:]
+        passes, t0 = 0, time.perf_counter()
+        while time.perf_counter() - t0 < 2.0:
+            for op in ops.values():
+                R.pairwise_batch(op, a_r, b_r, threads=1)
+            passes += 1
+        el = time.perf_counter() - t0
+        out["cpu_baseline"] = {"value": round(passes * in_bytes / args.steps / el / 1e9, 3), "unit": "GB/s",
+                               "cores": 1, "kind": "port", "us_per_op_sweep": round(el / passes / 4 * 1e6, 1),
+                               "sample": "the whole config (199 pairs x 4 ops), oracle/rbref.cpp, 1 thread"}
+    s.close()
+    return out
+
+
 def main():
     args = parse()
     world, rank, local, dist = dist_setup(args)
@@ -336,15 +395,20 @@ def main():
         }
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(ctx, rb, a, b, op, args.cpu_seconds)
-    if args.secondary != "none":
+    if args.secondary != "none" or (world == 1 and args.census):
         a.close()
         b.close()
+    if world == 1 and args.census:
+        c1 = run_census(args, ctx, rb)
+        if rank == 0:
+            line.setdefault("secondary", {})["census1881"] = c1
+    if args.secondary != "none":
         w = run_wide(args, args.secondary, world, rank, local, dist, ctx, rb,
                      WIDE_WORKLOADS[args.secondary][2], max(3, args.steps // 3), 1)
         if rank == 0:
             if world == 1 and not args.no_cpu_baseline:
                 w["cpu_baseline"] = wide_cpu_baseline(ctx, rb, args.secondary, args.cpu_seconds / 2)
-            line["secondary"] = {args.secondary: w}
+            line.setdefault("secondary", {})[args.secondary] = w
     if rank == 0:
         print(json.dumps(line), flush=True)
     if dist is not None:

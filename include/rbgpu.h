@@ -164,6 +164,22 @@ int rbgpu_wide_keys(rbgpu_ctx *ctx, int sem, const rbgpu_set *in, const uint32_t
 int rbgpu_wide_cardinality(rbgpu_ctx *ctx, int op, const rbgpu_set *in, const uint32_t *members,
                            uint32_t n, uint64_t *out);
 
+/* ---- bit-sliced index (bsi module) ------------------------------------------------------ */
+/* BitmapSliceIndex.Operation ordinals (bsi/.../BitmapSliceIndex.java:9-25) */
+enum rb_bsi_op { RB_BSI_EQ = 0, RB_BSI_NEQ = 1, RB_BSI_LE = 2, RB_BSI_LT = 3, RB_BSI_GE = 4, RB_BSI_GT = 5,
+                 RB_BSI_RANGE = 6 };
+/* Roaring64BitmapSliceIndex.compare(operation, startOrValue, end, foundSet) /
+ * RoaringBitmapSliceIndex.compare (bsi/.../longlong/Roaring64BitmapSliceIndex.java:460-503,
+ * bsi/.../RoaringBitmapSliceIndex.java:475-503): `bsi` holds the bitCount slices bA[0..n) followed
+ * by the existence bitmap ebM (n + 1 bitmaps); min_value / max_value are the BSI's fields (they
+ * drive compareUsingMinMax); `found` is a one-bitmap set or NULL (= ebM).  Values and predicates are
+ * unsigned 64-bit (the reference's signed longs agree for values < 2^63).  The result is a
+ * one-bitmap set, byte-identical to the reference's Roaring(64)Bitmap containers. */
+int rbgpu_bsi_compare(rbgpu_ctx *ctx, const rbgpu_set *bsi, int op, uint64_t start_or_value, uint64_t end,
+                      uint64_t min_value, uint64_t max_value, const rbgpu_set *found, rbgpu_set **out);
+/* RoaringBitmap.clone of bitmaps [first, first+count) into a new set (device copy). */
+int rbgpu_set_extract(const rbgpu_set *set, uint32_t first, uint32_t count, rbgpu_set **out);
+
 /* ---- synthetic inputs for the benchmark (device-side generator, SplitMix64) ---------- */
 enum rb_workload {
   RB_WL_FILTER_POSTING = 0, /* a = filters (4 keys, A/B/R .4/.3/.3),
@@ -177,6 +193,9 @@ enum rb_workload {
  * exactly the full dataset's containers. */
 int rbgpu_generate_keys(rbgpu_ctx *ctx, int workload, uint32_t n, uint64_t seed, uint32_t key_lo, uint32_t key_hi,
                         rbgpu_set **a);
+/* a runOptimize'd BSI over rows [0, nrows) with nslices random value bits per
+ * row (every slice container Bernoulli(1/2)), i.e. nslices + 1 bitmaps (slices, then ebM). */
+int rbgpu_generate_bsi(rbgpu_ctx *ctx, uint32_t nslices, uint64_t nrows, uint64_t seed, rbgpu_set **out);
 /* Generates a (and b for RB_WL_FILTER_POSTING; *b may be NULL otherwise).  n = pairs or
  * bitmaps.  Every container goes through runOptimize semantics, as
  * RoaringBitmapWriter(runCompress=true) does (ContainerAppender.java:130-137). */

@@ -179,3 +179,114 @@ def from_soa(keys, types, cards, nruns, payload, offsets) -> RefBitmap:
     if rc != 0:
         raise ValueError("bad SoA slice")
     return RefBitmap(out.value)
+
+
+# ---------------------------------------------------------------------------------------------
+# Bit-sliced index (bsi module): a restatement of Roaring64BitmapSliceIndex / RoaringBitmapSliceIndex
+# compare on top of the oracle's static container ops (the slices, the existence bitmap and every
+# intermediate are RoaringBitmaps combined with the static and/or/andNot, exactly like the
+# reference — bsi/src/main/java/org/roaringbitmap/bsi/longlong/Roaring64BitmapSliceIndex.java and
+# .../bsi/RoaringBitmapSliceIndex.java).
+BSI_EQ, BSI_NEQ, BSI_LE, BSI_LT, BSI_GE, BSI_GT, BSI_RANGE = range(7)  # BitmapSliceIndex.Operation
+
+
+def bsi_build(columns, values):
+    """setValue(column, value) for each pair on a fresh BSI (Roaring64BitmapSliceIndex.java:291-326):
+    slices are bitmapOf-built (add() only), bitCount = binary length of the largest value, min/max
+    tracked by ensureCapacityInternal.  Values are taken as unsigned 64-bit."""
+    import numpy as np
+    cols = np.asarray(columns, dtype=np.uint64)
+    vals = np.asarray(values, dtype=np.uint64)
+    if len(cols) == 0:
+        return [], RefBitmap.of(np.zeros(0, np.uint32)), 0, 0
+    # last write wins per column (setValue overwrites every slice bit and re-adds to ebM)
+    _, last = np.unique(cols[::-1], return_index=True)
+    keep = len(cols) - 1 - last
+    cols, vals = cols[keep], vals[keep]
+    vmax, vmin = int(vals.max()), int(vals.min())
+    nbits = max(1, vmax.bit_length())
+    slices = [RefBitmap.of(cols[((vals >> np.uint64(i)) & np.uint64(1)) == 1].astype(np.uint32))
+              for i in range(nbits)]
+    return slices, RefBitmap.of(cols.astype(np.uint32)), vmin, vmax
+
+
+def _empty():
+    import numpy as np
+    return RefBitmap.of(np.zeros(0, np.uint32))
+
+
+def _compare_using_min_max(ebm, op_, start, end, found, vmin, vmax):
+    """Roaring64BitmapSliceIndex.compareUsingMinMax (RoaringBitmapSliceIndex.java:505-577)."""
+    all_ = ebm.clone() if found is None else op(AND, ebm, found)
+    empty = _empty()
+    if op_ == BSI_LT:
+        if start > vmax:
+            return all_
+        if start <= vmin:
+            return empty
+    elif op_ == BSI_LE:
+        if start >= vmax:
+            return all_
+        if start < vmin:
+            return empty
+    elif op_ == BSI_GT:
+        if start < vmin:
+            return all_
+        if start >= vmax:
+            return empty
+    elif op_ == BSI_GE:
+        if start <= vmin:
+            return all_
+        if start > vmax:
+            return empty
+    elif op_ == BSI_EQ:
+        if vmin == vmax and vmin == start:
+            return all_
+        if start < vmin or start > vmax:
+            return empty
+    elif op_ == BSI_NEQ:
+        if vmin == vmax:
+            return empty if vmin == start else all_
+    elif op_ == BSI_RANGE:
+        if start <= vmin and end >= vmax:
+            return all_
+        if start > vmax or end < vmin:
+            return empty
+    return None
+
+
+def _oneil(slices, ebm, op_, predicate, found):
+    """oNeilCompare (RoaringBitmapSliceIndex.java:432-472)."""
+    fixed = ebm if found is None else found
+    gt, lt, eq = _empty(), _empty(), ebm
+    for i in range(len(slices) - 1, -1, -1):
+        if (predicate >> i) & 1:
+            lt = op(OR, lt, op(ANDNOT, eq, slices[i]))
+            eq = op(AND, eq, slices[i])
+        else:
+            gt = op(OR, gt, op(AND, eq, slices[i]))
+            eq = op(ANDNOT, eq, slices[i])
+    eq = op(AND, fixed, eq)
+    if op_ == BSI_EQ:
+        return eq
+    if op_ == BSI_NEQ:
+        return op(ANDNOT, fixed, eq)
+    if op_ == BSI_GT:
+        return op(AND, gt, fixed)
+    if op_ == BSI_LT:
+        return op(AND, lt, fixed)
+    if op_ == BSI_LE:
+        return op(AND, op(OR, lt, eq), fixed)
+    if op_ == BSI_GE:
+        return op(AND, op(OR, gt, eq), fixed)
+    raise ValueError(op_)
+
+
+def bsi_compare(slices, ebm, op_, start, end, found, vmin, vmax):
+    """compare(operation, startOrValue, end, foundSet) (RoaringBitmapSliceIndex.java:475-503)."""
+    r = _compare_using_min_max(ebm, op_, start, end, found, vmin, vmax)
+    if r is not None:
+        return r
+    if op_ == BSI_RANGE:
+        return op(AND, _oneil(slices, ebm, BSI_GE, start, found), _oneil(slices, ebm, BSI_LE, end, found))
+    return _oneil(slices, ebm, op_, start, found)

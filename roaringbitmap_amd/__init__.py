@@ -10,6 +10,8 @@ from ._lib import (AND, ANDNOT, ARRAY, BITMAP, FAST_AND, FAST_OR, FAST_XOR, NAIV
                    WORKSHY_AND, XOR, FormatError, InvalidArgument, RbError)
 from .engine import Context, DeviceSet, HostSoA, default_context, soa_from_values
 from .roaring import FastAggregation, ParallelAggregation, RoaringBitmap
+from .bsi import Operation, Roaring64BitmapSliceIndex, RoaringBitmapSliceIndex
+from ._lib import BSI_EQ, BSI_GE, BSI_GT, BSI_LE, BSI_LT, BSI_NEQ, BSI_RANGE
 
 __all__ = [
     "AND", "OR", "XOR", "ANDNOT", "ARRAY", "BITMAP", "RUN",
@@ -17,5 +19,7 @@ __all__ = [
     "WL_FILTER_POSTING", "WL_WIDE_DENSE", "WL_WIDE_MIXED", "WL_WIDE_RUNS",
     "Context", "DeviceSet", "HostSoA", "default_context", "soa_from_values",
     "RoaringBitmap", "FastAggregation", "ParallelAggregation",
+    "Roaring64BitmapSliceIndex", "RoaringBitmapSliceIndex", "Operation",
+    "BSI_EQ", "BSI_NEQ", "BSI_LE", "BSI_LT", "BSI_GE", "BSI_GT", "BSI_RANGE",
     "RbError", "FormatError", "InvalidArgument",
 ]

@@ -17,6 +17,7 @@ AND, OR, XOR, ANDNOT = 0, 1, 2, 3
 ARRAY, BITMAP, RUN = 0, 1, 2
 FAST_OR, FAST_AND, WORKSHY_AND, NAIVE_AND, FAST_XOR, PAR_OR, PAR_XOR, NAIVE_AND_ITER = range(8)
 WL_FILTER_POSTING, WL_WIDE_DENSE, WL_WIDE_MIXED, WL_WIDE_RUNS = range(4)
+BSI_EQ, BSI_NEQ, BSI_LE, BSI_LT, BSI_GE, BSI_GT, BSI_RANGE = range(7)  # BitmapSliceIndex.Operation
 
 
 class RbSoa(C.Structure):
@@ -84,6 +85,10 @@ SIGNATURES = {
     "rbgpu_wide_cardinality": (C.c_int, [_P, C.c_int, _P, _U32P, C.c_uint32, _U64P]),
     "rbgpu_set_key_bytes": (C.c_int, [_P, _U64P]),
     "rbgpu_set_summaries": (C.c_int, [_P, C.c_uint32, C.c_uint32, C.POINTER(RbBitmapSummary)]),
+    "rbgpu_bsi_compare": (C.c_int, [_P, _P, C.c_int, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64, _P,
+                                    C.POINTER(_P)]),
+    "rbgpu_set_extract": (C.c_int, [_P, C.c_uint32, C.c_uint32, C.POINTER(_P)]),
+    "rbgpu_generate_bsi": (C.c_int, [_P, C.c_uint32, C.c_uint64, C.c_uint64, C.POINTER(_P)]),
     "rbgpu_generate_keys": (C.c_int, [_P, C.c_int, C.c_uint32, C.c_uint64, C.c_uint32, C.c_uint32, C.POINTER(_P)]),
     "rbgpu_generate": (C.c_int, [_P, C.c_int, C.c_uint32, C.c_uint64, C.POINTER(_P), C.POINTER(_P)]),
 }

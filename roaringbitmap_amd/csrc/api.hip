@@ -662,6 +662,40 @@ int rbgpu_wide_cardinality(rbgpu_ctx *ctx, int op, const rbgpu_set *in, const ui
   return rc;
 }
 
+// ---------------------------------------------------------------- bit-sliced index
+int rbgpu_bsi_compare(rbgpu_ctx *ctx, const rbgpu_set *bsi, int op, uint64_t start_or_value, uint64_t end,
+                      uint64_t min_value, uint64_t max_value, const rbgpu_set *found, rbgpu_set **out) {
+  if (!out) return fail(RB_EINVAL, "null out");
+  *out = nullptr;
+  int rc = check_ctx(ctx);
+  if (rc) return rc;
+  if (!bsi || bsi->ctx != ctx) return fail(RB_EINVAL, "bad bsi set");
+  if (bsi->nb < 1 || bsi->nb > 65) return fail(RB_EINVAL, "a bsi set holds 0..64 slices and the existence bitmap");
+  if (found && (found->ctx != ctx || found->nb != 1)) return fail(RB_EINVAL, "foundSet must be a one-bitmap set");
+  if (op < RB_BSI_EQ || op > RB_BSI_RANGE) return fail(RB_EINVAL, "not support operation!");
+  rc = ensure_h_begin(bsi);
+  if (rc) return rc;
+  return bsi_compare(ctx, bsi, op, start_or_value, end, min_value, max_value, found, out);
+}
+
+int rbgpu_set_extract(const rbgpu_set *s, uint32_t first, uint32_t count, rbgpu_set **out) {
+  if (!s || !out) return fail(RB_EINVAL, "null argument");
+  *out = nullptr;
+  if ((uint64_t)first + count > s->nb) return fail(RB_EINVAL, "bitmap range out of bounds");
+  HostSoA h;
+  int rc = download_host(s, first, count, h);
+  if (rc) return rc;
+  return upload_host(s->ctx, h, out);
+}
+
+int rbgpu_generate_bsi(rbgpu_ctx *ctx, uint32_t nslices, uint64_t nrows, uint64_t seed, rbgpu_set **out) {
+  int rc = check_ctx(ctx);
+  if (rc) return rc;
+  if (!out) return fail(RB_EINVAL, "null out");
+  *out = nullptr;
+  return generate_bsi(ctx, nslices, nrows, seed, out);
+}
+
 // ---------------------------------------------------------------- generator
 int rbgpu_generate(rbgpu_ctx *ctx, int workload, uint32_t n, uint64_t seed, rbgpu_set **a, rbgpu_set **b) {
   int rc = check_ctx(ctx);

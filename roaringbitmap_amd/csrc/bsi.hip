@@ -1,0 +1,417 @@
+// bsi.hip — bit-sliced index compare (bsi module: Roaring64BitmapSliceIndex.compare /
+// RoaringBitmapSliceIndex.compare, the O'Neil chains of oNeilCompare) as ONE fused pass per high key.
+//
+// The reference evaluates a query as ~2 static RoaringBitmap ops per slice over whole bitmaps
+// (RoaringBitmapSliceIndex.java:432-472), materialising EQ / GT / LT after every slice.  Every high
+// key is independent, so here ONE WAVE PER KEY walks the slices once: EQ lives in registers as a
+// 65536-bit register bitmap, the GT or LT accumulator in an 8 KiB LDS image, the current slice is
+// staged in a second LDS image while the next slice's payload is already in flight (registers).
+// Each intermediate carries the container type the reference's static op would have produced
+// (pairwise contract, SURVEY §8a: AND R&R->EFF else AB, ANDNOT R\R, R\A(|A|<32)->EFF else AB, OR any
+// Bitmap->LR, A|A->AB, else EFF; absent keys: and -> absent, andNot(x, absent) -> clone x,
+// or(x, absent) -> clone x; empty results dropped), so the result is byte-identical.
+#include <algorithm>
+#include <cstring>
+
+#include "internal.hpp"
+#include "kernels.hpp"
+#include "wave.hpp"
+
+namespace rbg {
+
+struct Meta {
+  int present, type, card, runs;
+};
+
+// table[row * 65536 + key] = container index of bitmap (first + row) at key, else -1
+__global__ __launch_bounds__(256) void k_bsi_index(SetView s, uint32_t first, int32_t *table) {
+  const uint32_t row = blockIdx.y;
+  const uint64_t lo = s.begin[first + row], hi = s.begin[first + row + 1];
+  for (uint64_t c = lo + (uint64_t)blockIdx.x * 256 + threadIdx.x; c < hi; c += (uint64_t)gridDim.x * 256)
+    table[(uint64_t)row * 65536 + s.key[c]] = (int32_t)c;
+}
+__global__ __launch_bounds__(256) void k_bsi_active(const int32_t *frow, uint64_t *active) {
+  const uint32_t k = blockIdx.x * 256 + threadIdx.x;
+  if (k < 65536) active[k] = frow[k] >= 0;
+}
+__global__ __launch_bounds__(256) void k_bsi_list(const uint64_t *active, const uint64_t *pos, uint32_t *klist) {
+  const uint32_t k = blockIdx.x * 256 + threadIdx.x;
+  if (k < 65536 && active[k]) klist[pos[k]] = k;
+}
+
+// ---- per-key value algebra with the reference's type rules --------------------------------
+__device__ __forceinline__ uint64_t lds_word(const uint32_t *s, int j, int lane) {
+  const uint2 v = reinterpret_cast<const uint2 *>(s)[(j >> 1) * 128 + 2 * lane + (j & 1)];
+  return pack2(v.x, v.y);
+}
+__device__ __forceinline__ void lds_put_word(uint32_t *s, int j, int lane, uint64_t w) {
+  reinterpret_cast<uint2 *>(s)[(j >> 1) * 128 + 2 * lane + (j & 1)] = make_uint2((uint32_t)w, (uint32_t)(w >> 32));
+}
+// metadata of a fresh result in w under rule `eff` (EFF) / `or_bitmap` (LR) / otherwise AB
+__device__ __forceinline__ Meta classify(const uint64_t (&w)[kW], int lane, bool eff, bool lr, bool never_empty) {
+  Meta m;
+  int c, r;
+  metrics(w, lane, eff, c, r);
+  m.card = c;
+  m.runs = 0;
+  m.present = c > 0 || never_empty;
+  if (!m.present) return m;
+  if (eff) {
+    m.type = type_eff(c, r);
+    m.runs = m.type == kRun ? r : 0;
+  } else if (lr) {
+    m.type = type_lr(c);
+    m.runs = m.type == kRun ? 1 : 0;
+  } else {
+    m.type = type_ab(c);
+  }
+  return m;
+}
+__device__ __forceinline__ bool eff_and(const Meta &a, const Meta &b) { return a.type == kRun && b.type == kRun; }
+__device__ __forceinline__ bool eff_andnot(const Meta &a, const Meta &b) {
+  return a.type == kRun && (b.type == kRun || (b.type == kArray && b.card < kRunArrayThreshold));
+}
+__device__ __forceinline__ bool lr_or(const Meta &a, const Meta &b) { return a.type == kBitmap || b.type == kBitmap; }
+__device__ __forceinline__ bool eff_or(const Meta &a, const Meta &b) {
+  return !lr_or(a, b) && !(a.type == kArray && b.type == kArray);
+}
+
+// Any container (global payload) -> LDS image s.
+__device__ __forceinline__ Meta stage_global(const SetView &v, int32_t c, uint32_t *s, int lane) {
+  Meta m{0, 0, 0, 0};
+  if (c < 0) return m;
+  m.present = 1;
+  m.type = v.type[c];
+  m.card = (int)v.card[c];
+  m.runs = v.nruns[c];
+  stage_container(m.type, v.payload + v.off[c], (uint32_t)m.card, (uint32_t)m.runs, s, lane);
+  return m;
+}
+
+enum { kBsiEQ = 0, kBsiNEQ = 1, kBsiLE = 2, kBsiLT = 3, kBsiGE = 4, kBsiGT = 5 };
+
+template <int FINAL>
+__global__ __launch_bounds__(256, 2) void k_bsi_chain(SetView bsi, SetView fnd, int has_found,
+                                                      const int32_t *__restrict__ table, uint32_t nbits, uint64_t pred,
+                                                      const uint32_t *__restrict__ klist, uint32_t nk,
+                                                      uint8_t *__restrict__ out, WideOut wo, uint64_t *stats) {
+  constexpr int TRACK = (FINAL == kBsiGE || FINAL == kBsiGT) ? 1 : (FINAL == kBsiLE || FINAL == kBsiLT) ? 2 : 0;
+  __shared__ __attribute__((aligned(16))) uint32_t lds[4][2][2048];
+  const int lane = lane_id();
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t q = blockIdx.x * 4 + wv;
+  if (q >= nk) return;
+  uint32_t *sS = lds[wv][0], *sX = lds[wv][1];
+  const uint32_t key = klist[q];
+  uint64_t inb = 0;
+
+  // EQ = ebM's container (RoaringBitmapSliceIndex.java:438: EQ = this.ebM, no copy)
+  uint64_t e[kW];
+  Meta eq = stage_global(bsi, table[(uint64_t)nbits * 65536 + key], sS, lane);
+  if (eq.present) {
+    lds_read_words(sS, e, lane);
+    inb += payload_bytes(eq.type, eq.card, eq.runs) + 16;
+  } else {
+#pragma unroll
+    for (int j = 0; j < kW; ++j) e[j] = 0;
+  }
+  wave_lds_sync();
+  Meta x{0, 0, 0, 0};
+
+  // slice descriptors, lane i <-> slice i (nbits <= 64)
+  const int32_t sc = lane < (int)nbits ? table[(uint64_t)lane * 65536 + key] : -1;
+  int st = 0;
+  uint32_t scard = 0, sruns = 0;
+  uint64_t soff = 0;
+  if (sc >= 0) {
+    st = bsi.type[sc];
+    scard = bsi.card[sc];
+    sruns = bsi.nruns[sc];
+    soff = bsi.off[sc];
+  }
+  auto sbytes = [&](int i) -> uint32_t {
+    const int t = (int)readlane((uint32_t)st, i);
+    return (uint32_t)payload_bytes(t, readlane(scard, i), readlane(sruns, i));
+  };
+  auto sptr = [&](int i) -> const uint8_t * {
+    return bsi.payload + pack2(readlane((uint32_t)soff, i), readlane((uint32_t)(soff >> 32), i));
+  };
+  uint4 pq[8];
+  if (nbits) {
+    const int i0 = (int)nbits - 1;
+    const bool ok = (int)readlane((uint32_t)sc, i0) >= 0 && sbytes(i0) <= (uint32_t)kBitmapBytes;
+    load_chunks(pq, ok ? sptr(i0) : bsi.payload, ok ? sbytes(i0) : 16u, lane);
+  }
+  for (int i = (int)nbits - 1; i >= 0; --i) {
+    const bool spresent = (int)readlane((uint32_t)sc, i) >= 0;
+    Meta sm{0, 0, 0, 0};
+    if (spresent) {
+      sm.present = 1;
+      sm.type = (int)readlane((uint32_t)st, i);
+      sm.card = (int)readlane(scard, i);
+      sm.runs = (int)readlane(sruns, i);
+      inb += payload_bytes(sm.type, sm.card, sm.runs) + 16;
+      if (payload_bytes(sm.type, sm.card, sm.runs) > (uint64_t)kBitmapBytes) {
+        // > 2047 runs: straight from global
+        lds_zero(sS, lane);
+        wave_lds_sync();
+        const uint32_t *r32 = reinterpret_cast<const uint32_t *>(sptr(i));
+        for (int k = lane; k < sm.runs; k += 64) toggle_run(sS, r32[k]);
+        wave_lds_sync();
+        toggles_to_words_lds(sS, lane);
+        wave_lds_sync();
+      } else {
+        stage_from_chunks(sm.type, pq, (uint32_t)sm.card, (uint32_t)sm.runs, sS, lane);
+      }
+    }
+    // ---- next slice in flight during this step's algebra
+    __builtin_amdgcn_sched_barrier(0);
+    if (i > 0) {
+      const bool ok = (int)readlane((uint32_t)sc, i - 1) >= 0 && sbytes(i - 1) <= (uint32_t)kBitmapBytes;
+      load_chunks(pq, ok ? sptr(i - 1) : bsi.payload, ok ? sbytes(i - 1) : 16u, lane);
+    }
+    if (!eq.present) continue; // and/andNot of an absent EQ stay absent; GT/LT unchanged
+    const int bit = (int)((pred >> i) & 1);
+    const bool feeds = (TRACK == 2 && bit) || (TRACK == 1 && !bit);
+    // t = bit ? andNot(EQ, S) : and(EQ, S);  EQ = bit ? and(EQ, S) : andNot(EQ, S)
+    uint64_t t[kW];
+#pragma unroll
+    for (int j = 0; j < kW; ++j) {
+      const uint64_t sw = spresent ? lds_word(sS, j, lane) : 0ull;
+      t[j] = bit ? (e[j] & ~sw) : (e[j] & sw);
+      e[j] = bit ? (e[j] & sw) : (e[j] & ~sw);
+    }
+    wave_lds_sync();
+    Meta tm{0, 0, 0, 0};
+    if (!spresent) {
+      if (bit) {
+        tm = eq;          // andNot(EQ, absent) = clone of EQ
+        eq.present = 0;   // and(EQ, absent) = absent
+      } // else: t absent, EQ = clone of EQ (unchanged)
+    } else {
+      const Meta e0 = eq;
+      if (feeds) tm = classify(t, lane, bit ? eff_andnot(e0, sm) : eff_and(e0, sm), false, false);
+      eq = classify(e, lane, bit ? eff_and(e0, sm) : eff_andnot(e0, sm), false, false);
+    }
+    if (feeds && tm.present) {
+      if (!x.present) {
+        lds_write_words(sX, t, lane); // or(absent, t) = clone of t
+        x = tm;
+      } else {
+        const Meta x0 = x;
+#pragma unroll
+        for (int j = 0; j < kW; ++j) t[j] |= lds_word(sX, j, lane);
+        x = classify(t, lane, eff_or(x0, tm), lr_or(x0, tm), true);
+        lds_write_words(sX, t, lane);
+      }
+      wave_lds_sync();
+    }
+  }
+
+  // ---- the final ops with the found set F (foundSet, or ebM when null)
+  const int32_t fc = has_found ? table[(uint64_t)(nbits + 1) * 65536 + key] : table[(uint64_t)nbits * 65536 + key];
+  const Meta fm = stage_global(has_found ? fnd : bsi, fc, sS, lane); // present: keys come from F
+  if (has_found) inb += payload_bytes(fm.type, fm.card, fm.runs) + 16;
+  // EQ = and(fixedFoundSet, EQ)
+  if (eq.present) {
+    const Meta e0 = eq;
+#pragma unroll
+    for (int j = 0; j < kW; ++j) e[j] &= lds_word(sS, j, lane);
+    eq = classify(e, lane, eff_and(fm, e0), false, false);
+  }
+  Meta rm{0, 0, 0, 0};
+  uint64_t t[kW]; // the result (EQ copies e in)
+  if (FINAL == kBsiEQ) {
+    rm = eq;
+#pragma unroll
+    for (int j = 0; j < kW; ++j) t[j] = e[j];
+  } else if (FINAL == kBsiNEQ) { // andNot(fixedFoundSet, EQ)
+    if (!eq.present) {
+#pragma unroll
+      for (int j = 0; j < kW; ++j) t[j] = lds_word(sS, j, lane);
+      rm = fm;
+    } else {
+#pragma unroll
+      for (int j = 0; j < kW; ++j) t[j] = lds_word(sS, j, lane) & ~e[j];
+      rm = classify(t, lane, eff_andnot(fm, eq), false, false);
+    }
+  } else {
+    // Y = GT / LT, or or(LT|GT, EQ) for LE / GE
+    Meta ym = x;
+#pragma unroll
+    for (int j = 0; j < kW; ++j) t[j] = x.present ? lds_word(sX, j, lane) : 0ull;
+    if (FINAL == kBsiLE || FINAL == kBsiGE) {
+      if (!x.present) {
+#pragma unroll
+        for (int j = 0; j < kW; ++j) t[j] = e[j];
+        ym = eq;
+      } else if (eq.present) {
+#pragma unroll
+        for (int j = 0; j < kW; ++j) t[j] |= e[j];
+        ym = classify(t, lane, eff_or(x, eq), lr_or(x, eq), true);
+      }
+    }
+    // and(Y, fixedFoundSet)
+    if (ym.present) {
+#pragma unroll
+      for (int j = 0; j < kW; ++j) t[j] &= lds_word(sS, j, lane);
+      rm = classify(t, lane, eff_and(ym, fm), false, false);
+    }
+  }
+  wave_lds_sync();
+  const int ty = rm.present ? rm.type : kEmpty;
+  if (rm.present) emit_container(ty, t, rm.card, rm.runs, out + (uint64_t)q * kBitmapBytes, sS, lane);
+  if (lane == 0) {
+    wo.type[q] = (uint8_t)ty;
+    wo.card[q] = (uint32_t)(rm.present ? rm.card : 0);
+    wo.nruns[q] = (uint16_t)(ty == kRun ? rm.runs : 0);
+    if (inb) atomicAdd((unsigned long long *)&stats[0 * kStripes + (q & (kStripes - 1))], (unsigned long long)inb);
+    if (rm.present)
+      atomicAdd((unsigned long long *)&stats[1 * kStripes + (q & (kStripes - 1))],
+                (unsigned long long)(payload_bytes(ty, rm.card, rm.runs) + (ty == kRun ? 2 : 0) + 16));
+  }
+}
+
+// ---------------------------------------------------------------- host side
+static unsigned nblk(uint64_t n, unsigned per) { return (unsigned)((n + per - 1) / per); }
+
+// One O'Neil chain (oNeilCompare with `final_op`) over the keys of F -> one-bitmap result set.
+static int bsi_chain(rbgpu_ctx *ctx, const rbgpu_set *bsi, uint32_t nbits, int final_op, uint64_t pred,
+                     const rbgpu_set *found, const int32_t *d_table, const uint32_t *d_klist, uint32_t nk,
+                     rbgpu_set **out) {
+  hipStream_t st = ctx->stream;
+  rbgpu_set *res = new rbgpu_set;
+  int rc = set_alloc(ctx, res, 1, nk, (uint64_t)std::max<uint32_t>(nk, 1) * kBitmapBytes);
+  if (rc) {
+    delete res;
+    return rc;
+  }
+  uint8_t *w_type;
+  uint32_t *w_card;
+  uint16_t *w_nruns;
+  const uint64_t nk1 = std::max<uint32_t>(nk, 1);
+  if (ctx->pool.alloc((void **)&w_type, nk1) || ctx->pool.alloc((void **)&w_card, nk1 * 4) ||
+      ctx->pool.alloc((void **)&w_nruns, nk1 * 2)) {
+    rbgpu_set_free(res);
+    return fail(RB_ENOMEM, "bsi result workspace");
+  }
+  const WideOut wo{w_type, w_card, w_nruns};
+  const SetView bv = bsi->view();
+  const SetView fv = found ? found->view() : bv;
+  const int hf = found != nullptr;
+  if (nk) {
+    const unsigned g = nblk(nk, 4);
+    switch (final_op) {
+    case kBsiEQ: k_bsi_chain<kBsiEQ><<<g, 256, 0, st>>>(bv, fv, hf, d_table, nbits, pred, d_klist, nk, res->payload, wo, ctx->d_stats); break;
+    case kBsiNEQ: k_bsi_chain<kBsiNEQ><<<g, 256, 0, st>>>(bv, fv, hf, d_table, nbits, pred, d_klist, nk, res->payload, wo, ctx->d_stats); break;
+    case kBsiLE: k_bsi_chain<kBsiLE><<<g, 256, 0, st>>>(bv, fv, hf, d_table, nbits, pred, d_klist, nk, res->payload, wo, ctx->d_stats); break;
+    case kBsiLT: k_bsi_chain<kBsiLT><<<g, 256, 0, st>>>(bv, fv, hf, d_table, nbits, pred, d_klist, nk, res->payload, wo, ctx->d_stats); break;
+    case kBsiGE: k_bsi_chain<kBsiGE><<<g, 256, 0, st>>>(bv, fv, hf, d_table, nbits, pred, d_klist, nk, res->payload, wo, ctx->d_stats); break;
+    default: k_bsi_chain<kBsiGT><<<g, 256, 0, st>>>(bv, fv, hf, d_table, nbits, pred, d_klist, nk, res->payload, wo, ctx->d_stats); break;
+    }
+  }
+  uint64_t nres = 0;
+  rc = compact_keyed(ctx, d_klist, nk, wo, res, &nres);
+  ctx->pool.release(w_type);
+  ctx->pool.release(w_card);
+  ctx->pool.release(w_nruns);
+  if (rc) {
+    rbgpu_set_free(res);
+    return rc;
+  }
+  *out = res;
+  return RB_OK;
+}
+
+// compareUsingMinMax (RoaringBitmapSliceIndex.java:505-577), values unsigned: 1 = all, 0 = empty,
+// -1 = evaluate
+static int min_max_shortcut(int op, uint64_t a, uint64_t b, uint64_t mn, uint64_t mx) {
+  switch (op) {
+  case kBsiLT: return a > mx ? 1 : a <= mn ? 0 : -1;
+  case kBsiLE: return a >= mx ? 1 : a < mn ? 0 : -1;
+  case kBsiGT: return a < mn ? 1 : a >= mx ? 0 : -1;
+  case kBsiGE: return a <= mn ? 1 : a > mx ? 0 : -1;
+  case kBsiEQ: return (mn == mx && mn == a) ? 1 : (a < mn || a > mx) ? 0 : -1;
+  case kBsiNEQ: return mn == mx ? (mn == a ? 0 : 1) : -1;
+  default: return (a <= mn && b >= mx) ? 1 : (a > mx || b < mn) ? 0 : -1; // RANGE
+  }
+}
+
+int bsi_compare(rbgpu_ctx *ctx, const rbgpu_set *bsi, int op, uint64_t start, uint64_t end, uint64_t vmin,
+                uint64_t vmax, const rbgpu_set *found, rbgpu_set **out) {
+  const uint32_t nbits = bsi->nb - 1;
+  hipStream_t st = ctx->stream;
+  stats_begin(ctx);
+  const int sc = min_max_shortcut(op, start, end, vmin, vmax);
+  if (sc >= 0) {
+    // all = foundSet == null ? ebM.clone() : and(ebM, foundSet); empty = new bitmap
+    if (sc == 0) {
+      rbgpu_set *e = new rbgpu_set;
+      const int rc = set_alloc(ctx, e, 1, 0, 16);
+      if (rc) {
+        delete e;
+        return rc;
+      }
+      const uint64_t hb[2] = {0, 0};
+      HIPCHK(hipMemcpyAsync(e->begin, hb, 16, hipMemcpyHostToDevice, st));
+      HIPCHK(hipStreamSynchronize(st));
+      e->h_begin = {0, 0};
+      *out = e;
+      return RB_OK;
+    }
+    if (!found) return rbgpu_set_extract(bsi, nbits, 1, out);
+    const uint32_t ai = nbits, bi = 0;
+    return rbgpu_pairwise(ctx, RB_AND, bsi, found, &ai, &bi, 1, out);
+  }
+  // key -> container tables: rows 0..nbits-1 slices, nbits ebM, nbits+1 foundSet
+  const uint32_t rows = nbits + 2;
+  int32_t *d_table = nullptr;
+  uint64_t *d_active = nullptr, *d_pos = nullptr, *d_tmp = nullptr;
+  uint32_t *d_klist = nullptr;
+  const uint64_t tw = std::max<uint64_t>(scan_tmp_words(65536), 1);
+  if (ctx->pool.alloc((void **)&d_table, (uint64_t)rows * 65536 * 4) ||
+      ctx->pool.alloc((void **)&d_active, 65537 * 8ull) || ctx->pool.alloc((void **)&d_pos, 65537 * 8ull) ||
+      ctx->pool.alloc((void **)&d_tmp, tw * 8) || ctx->pool.alloc((void **)&d_klist, 65536 * 4ull))
+    return fail(RB_ENOMEM, "bsi tables");
+  auto release = [&]() {
+    for (void *p : {(void *)d_table, (void *)d_active, (void *)d_pos, (void *)d_tmp, (void *)d_klist})
+      ctx->pool.release(p);
+  };
+  HIPCHK(hipMemsetAsync(d_table, 0xFF, (uint64_t)rows * 65536 * 4, st));
+  k_bsi_index<<<dim3(64, nbits + 1), 256, 0, st>>>(bsi->view(), 0, d_table);
+  if (found) k_bsi_index<<<dim3(64, 1), 256, 0, st>>>(found->view(), 0, d_table + (uint64_t)(nbits + 1) * 65536);
+  k_bsi_active<<<256, 256, 0, st>>>(d_table + (uint64_t)(found ? nbits + 1 : nbits) * 65536, d_active);
+  scan_exclusive(d_active, d_pos, 65536, d_tmp, st);
+  k_bsi_list<<<256, 256, 0, st>>>(d_active, d_pos, d_klist);
+  HIPCHK(hipMemcpyAsync(ctx->h_pinned, d_pos + 65536, 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  const uint32_t nk = (uint32_t)ctx->h_pinned[0];
+  HIPCHK(hipEventRecord(ctx->ev[1], st));
+  int rc;
+  rbgpu_set *ge = nullptr, *le = nullptr;
+  if (op != 6) {
+    rc = bsi_chain(ctx, bsi, nbits, op, start, found, d_table, d_klist, nk, out);
+  } else { // RANGE: and(GE(start), LE(end)) — the two chains, then the static AND
+    rc = bsi_chain(ctx, bsi, nbits, kBsiGE, start, found, d_table, d_klist, nk, &ge);
+    if (!rc) rc = bsi_chain(ctx, bsi, nbits, kBsiLE, end, found, d_table, d_klist, nk, &le);
+  }
+  HIPCHK(hipEventRecord(ctx->ev[2], st));
+  release();
+  const KernelSpan spans[1] = {{"k_bsi_chain", 0, 1, op == 6 ? 2ull * nk : nk}};
+  if (!rc) rc = stats_end(ctx, nk, op == 6 ? 0 : (*out)->nc, spans, 1);
+  if (op == 6) {
+    if (!rc) {
+      const rb_stats chains = ctx->last; // the chains are the measured work; keep their stats
+      rc = rbgpu_pairwise(ctx, RB_AND, ge, le, nullptr, nullptr, 1, out);
+      const double and_ms = ctx->last.total_ms;
+      ctx->last = chains;
+      ctx->last.total_ms += and_ms;
+      if (!rc) ctx->last.result_containers = (*out)->nc;
+    }
+    rbgpu_set_free(ge);
+    rbgpu_set_free(le);
+  }
+  return rc;
+}
+
+} // namespace rbg

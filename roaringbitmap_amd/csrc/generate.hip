@@ -14,7 +14,7 @@ __device__ __forceinline__ uint64_t splitmix(uint64_t &x) {
   return z ^ (z >> 31);
 }
 
-enum { kGenArray = 0, kGenBitmap = 1, kGenRuns = 2, kGenCoreRuns = 3 };
+enum { kGenArray = 0, kGenBitmap = 1, kGenRuns = 2, kGenCoreRuns = 3, kGenHalfLimit = 4, kGenFullLimit = 5 };
 
 // word mask of [a, b) restricted to container word wi
 __device__ __forceinline__ uint64_t range_mask(int wi, int a, int b) {
@@ -79,6 +79,14 @@ __device__ void gen_container(const GenSpec &g, uint64_t cid, uint32_t *s, uint6
       uint32_t c1 = c0 ^ ((p0 >> k) & 1);
       w[2 * k] = prefix_xor64(t[2 * k]) ^ (c0 ? ~0ull : 0ull);
       w[2 * k + 1] = prefix_xor64(t[2 * k + 1]) ^ (c1 ? ~0ull : 0ull);
+    }
+  } else if (target == kGenHalfLimit || target == kGenFullLimit) {
+    // BSI slice (random value bit per row, density 1/2) / existence bitmap, rows [0, param)
+#pragma unroll
+    for (int j = 0; j < kW; ++j) {
+      const int wi = 128 * (j >> 1) + 2 * lane + (j & 1);
+      const uint64_t m = range_mask(wi, 0, (int)param);
+      w[j] = target == kGenFullLimit ? m : (splitmix(ls) & m);
     }
   } else { // kGenCoreRuns: shared core run [s_k, s_k+1024) + r-1 random runs (r ~ U[1,8], len U[1,256])
     const int core = (int)(param % 64512u);
@@ -319,6 +327,20 @@ int materialize(rbgpu_ctx *ctx, const GenStructure &gs, uint64_t seed, rbgpu_set
   return RB_OK;
 }
 } // namespace
+
+int generate_bsi(rbgpu_ctx *ctx, uint32_t nslices, uint64_t nrows, uint64_t seed, rbgpu_set **out) {
+  if (nslices > 64 || nrows > (1ull << 32)) return fail(RB_EINVAL, "bsi: at most 64 slices over 2^32 rows");
+  GenStructure g;
+  const uint64_t nkeys = (nrows + 65535) / 65536;
+  for (uint32_t b = 0; b <= nslices; ++b) { // slices 0..nslices-1, then the existence bitmap
+    for (uint64_t k = 0; k < nkeys; ++k) {
+      const uint32_t limit = (uint32_t)std::min<uint64_t>(65536, nrows - k * 65536);
+      g.add((uint16_t)k, b < nslices ? kGenHalfLimit : kGenFullLimit, limit, ((uint64_t)b << 16) | k);
+    }
+    g.close();
+  }
+  return materialize(ctx, g, seed * 31 + 5, out);
+}
 
 int generate_sets(rbgpu_ctx *ctx, int workload, uint32_t n, uint64_t seed, uint32_t key_lo, uint32_t key_hi,
                   rbgpu_set **a, rbgpu_set **b) {

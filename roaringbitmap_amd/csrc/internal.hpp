@@ -7,6 +7,7 @@
 #include <vector>
 
 #include "common.hpp"
+#include "kernels.hpp"
 
 namespace rbg {
 
@@ -134,6 +135,12 @@ int stats_end(rbgpu_ctx *ctx, uint64_t tasks, uint64_t result_containers, const 
 // keys outside [key_lo, key_hi) produce no result containers (key-range shard of the aggregation)
 int wide_run(rbgpu_ctx *ctx, int sem, const rbgpu_set *in, const std::vector<uint32_t> &members, uint32_t key_lo,
              uint32_t key_hi, rbgpu_set **out);
+int compact_keyed(rbgpu_ctx *ctx, const uint32_t *d_klist, uint32_t nk, const WideOut &wo, rbgpu_set *res,
+                  uint64_t *nres_out);
+// bsi.hip: op = BitmapSliceIndex.Operation ordinal (EQ, NEQ, LE, LT, GE, GT, RANGE)
+int bsi_compare(rbgpu_ctx *ctx, const rbgpu_set *bsi, int op, uint64_t start, uint64_t end, uint64_t vmin,
+                uint64_t vmax, const rbgpu_set *found, rbgpu_set **out);
+int generate_bsi(rbgpu_ctx *ctx, uint32_t nslices, uint64_t nrows, uint64_t seed, rbgpu_set **out);
 // generate.hip
 int generate_sets(rbgpu_ctx *ctx, int workload, uint32_t n, uint64_t seed, uint32_t key_lo, uint32_t key_hi,
                   rbgpu_set **a, rbgpu_set **b);

@@ -53,6 +53,13 @@ void launch_compact_count(const uint64_t *task_begin, uint32_t npairs, const uin
 void launch_compact_write(const uint64_t *task_begin, uint32_t npairs, const TaskMeta &tm, const uint64_t *rbegin,
                           const OutView &out, uint64_t *pair_card, uint64_t *stats, hipStream_t st);
 
+// ---- wide.hip: per-key reduction outputs (one 8 KiB slot per active key q)
+struct WideOut {
+  uint8_t *type;   // per active key, kEmpty if dropped
+  uint32_t *card;
+  uint16_t *nruns;
+};
+
 // ---- setops.hip
 void launch_bitmap_cards(const SetView &s, uint32_t nbitmaps, uint64_t *out, hipStream_t st);
 void launch_gather(const uint8_t *src, const uint64_t *soff, const uint64_t *bytes, uint8_t *dst,

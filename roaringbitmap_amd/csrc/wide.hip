@@ -22,11 +22,6 @@
 
 namespace rbg {
 
-struct WideOut {
-  uint8_t *type;   // per active key, kEmpty if dropped
-  uint32_t *card;
-  uint16_t *nruns;
-};
 
 __device__ __forceinline__ uint64_t alg_bytes_w(int t, uint32_t c, uint32_t r) {
   return t == kBitmap ? 8192ull : t == kArray ? 2ull * c : 4ull * r + 2;
@@ -322,6 +317,39 @@ __global__ __launch_bounds__(256) void k_wide_write(const uint32_t *klist, uint3
 // ---------------------------------------------------------------- host orchestration
 static unsigned nblk(uint64_t n, unsigned per) { return (unsigned)((n + per - 1) / per); }
 
+// Result of a keyed reduction (one 8 KiB slot per active key q, type kEmpty = dropped) -> the
+// one-bitmap result set: drop empties, write key/type/card/nruns/offset, set the CSR.
+int compact_keyed(rbgpu_ctx *ctx, const uint32_t *d_klist, uint32_t nk, const WideOut &wo, rbgpu_set *res,
+                  uint64_t *nres_out) {
+  hipStream_t st = ctx->stream;
+  uint64_t *pin = ctx->h_pinned;
+  if (nk) {
+    uint64_t *keep = nullptr, *pos = nullptr, *tmp2 = nullptr;
+    const uint64_t tw = std::max<uint64_t>(scan_tmp_words(nk), 1);
+    if (ctx->pool.alloc((void **)&keep, (nk + 1) * 8ull) || ctx->pool.alloc((void **)&pos, (nk + 1) * 8ull) ||
+        ctx->pool.alloc((void **)&tmp2, tw * 8))
+      return fail(RB_ENOMEM, "keyed compaction workspace");
+    k_wide_keep<<<nblk(nk, 256), 256, 0, st>>>(wo.type, nk, keep);
+    scan_exclusive(keep, pos, nk, tmp2, st);
+    k_wide_write<<<nblk(nk, 256), 256, 0, st>>>(d_klist, nk, wo, pos,
+                                                OutView{res->key, res->type, res->card, res->nruns, res->off});
+    HIPCHK(hipMemcpyAsync(pin + 1, pos + nk, 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    ctx->pool.release(keep);
+    ctx->pool.release(pos);
+    ctx->pool.release(tmp2);
+  } else {
+    pin[1] = 0;
+  }
+  const uint64_t nres = pin[1];
+  const uint64_t hb[2] = {0, nres};
+  HIPCHK(hipMemcpyAsync(res->begin, hb, 16, hipMemcpyHostToDevice, st));
+  res->nc = nres;
+  res->h_begin = {0, nres};
+  *nres_out = nres;
+  return RB_OK;
+}
+
 template <int SEM>
 static void launch_reduce(const SetView &s, const uint32_t *cid, const uint64_t *seg, const uint32_t *klist,
                           uint32_t nk, uint8_t *out, const WideOut &wo, uint64_t *stats, hipStream_t st) {
@@ -409,11 +437,9 @@ int wide_run(rbgpu_ctx *ctx, int sem, const rbgpu_set *in, const std::vector<uin
   uint8_t *w_type;
   uint32_t *w_card;
   uint16_t *w_nruns;
-  uint64_t *w_keep, *w_pos;
   const uint64_t nk1 = std::max<uint32_t>(nk, 1);
   if (pool.alloc((void **)&w_type, nk1) || pool.alloc((void **)&w_card, nk1 * 4) ||
-      pool.alloc((void **)&w_nruns, nk1 * 2) || pool.alloc((void **)&w_keep, (nk1 + 1) * 8) ||
-      pool.alloc((void **)&w_pos, (nk1 + 1) * 8)) {
+      pool.alloc((void **)&w_nruns, nk1 * 2)) {
     rbgpu_set_free(res);
     release();
     return fail(RB_ENOMEM, "wide result workspace");
@@ -433,27 +459,13 @@ int wide_run(rbgpu_ctx *ctx, int sem, const rbgpu_set *in, const std::vector<uin
   }
   HIPCHK(hipEventRecord(ctx->ev[2], st));
   // ---- compaction
-  if (nk) {
-    k_wide_keep<<<nblk(nk, 256), 256, 0, st>>>(w_type, nk, w_keep);
-    uint64_t *tmp2 = nullptr;
-    const uint64_t tw = std::max<uint64_t>(scan_tmp_words(nk), 1);
-    if (pool.alloc((void **)&tmp2, tw * 8)) {
-      rbgpu_set_free(res);
-      release();
-      return fail(RB_ENOMEM, "wide scan workspace");
-    }
-    scan_exclusive(w_keep, w_pos, nk, tmp2, st);
-    k_wide_write<<<nblk(nk, 256), 256, 0, st>>>(d_klist, nk, wo, w_pos,
-                                                OutView{res->key, res->type, res->card, res->nruns, res->off});
-    HIPCHK(hipMemcpyAsync(pin + 1, w_pos + nk, 8, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
-    pool.release(tmp2);
-  } else {
-    pin[1] = 0;
+  uint64_t nres = 0;
+  rc = compact_keyed(ctx, d_klist, nk, wo, res, &nres);
+  if (rc) {
+    rbgpu_set_free(res);
+    release();
+    return rc;
   }
-  const uint64_t nres = pin[1];
-  const uint64_t hb[2] = {0, nres};
-  HIPCHK(hipMemcpyAsync(res->begin, hb, 16, hipMemcpyHostToDevice, st));
   const char *name = sem == RB_FAST_OR ? "k_wide_reduce<FAST_OR>" : sem == RB_WORKSHY_AND ? "k_wide_reduce<WORKSHY_AND>"
                      : sem == RB_FAST_XOR ? "k_wide_reduce<FAST_XOR>" : sem == RB_PAR_OR ? "k_wide_reduce<PAR_OR>"
                      : sem == RB_PAR_XOR ? "k_wide_reduce<PAR_XOR>" : "k_wide_reduce<NAIVE_AND>";
@@ -463,8 +475,6 @@ int wide_run(rbgpu_ctx *ctx, int sem, const rbgpu_set *in, const std::vector<uin
   pool.release(w_type);
   pool.release(w_card);
   pool.release(w_nruns);
-  pool.release(w_keep);
-  pool.release(w_pos);
   release();
   if (rc) {
     rbgpu_set_free(res);

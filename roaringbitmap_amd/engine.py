@@ -367,6 +367,25 @@ class Context:
             L.check(L.lib().rbgpu_wide_keys(self.h, sem, s.h, mp, n, int(lo), int(hi), C.byref(out)))
         return DeviceSet(self, out.value)
 
+    def bsi_compare(self, op: int, bsi: DeviceSet, start: int, end: int, min_value: int, max_value: int,
+                    found: Optional[DeviceSet] = None) -> DeviceSet:
+        """Roaring64BitmapSliceIndex.compare over a device BSI (slices then ebM), rbgpu_bsi_compare."""
+        out = C.c_void_p()
+        L.check(L.lib().rbgpu_bsi_compare(self.h, bsi.h, op, start & (2**64 - 1), end & (2**64 - 1),
+                                          min_value & (2**64 - 1), max_value & (2**64 - 1),
+                                          found.h if found is not None else None, C.byref(out)))
+        return DeviceSet(self, out.value)
+
+    def generate_bsi(self, nslices: int, nrows: int, seed: int = 42) -> DeviceSet:
+        a = C.c_void_p()
+        L.check(L.lib().rbgpu_generate_bsi(self.h, nslices, nrows, seed, C.byref(a)))
+        return DeviceSet(self, a.value)
+
+    def extract(self, s: DeviceSet, first: int, count: int = 1) -> DeviceSet:
+        out = C.c_void_p()
+        L.check(L.lib().rbgpu_set_extract(s.h, first, count, C.byref(out)))
+        return DeviceSet(self, out.value)
+
     def wide_cardinality(self, op: int, s: DeviceSet, members=None) -> int:
         mi, mp = _idx(members)
         n = len(mi) if mi is not None else len(s)

@@ -1,0 +1,86 @@
+"""Parity of the fused MI355X BSI compare (rbgpu_bsi_compare) with the oracle's restatement of
+Roaring64BitmapSliceIndex.compare: identical RoaringFormatSpec bytes for every operation, with and
+without foundSet, over dense / sparse / run-optimized slices, plus the reference's own known answers."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+OPS = ["EQ", "NEQ", "LE", "LT", "GE", "GT", "RANGE"]
+
+
+def _device_bsi(ctx, oracle, slices, ebm, run_optimize):
+    vals = [s.to_array() for s in slices] + [ebm.to_array()]
+    d = ctx.upload_values(vals, run_optimize=run_optimize)
+    refs = [oracle.RefBitmap.deserialize(b) for b in d.serialize()]  # the exact containers uploaded
+    return d, refs[:-1], refs[-1]
+
+
+def _case(rng, n, nbits, universe):
+    cols = np.unique(rng.integers(0, universe, size=n))
+    vals = rng.integers(0, 2**nbits, size=len(cols), dtype=np.uint64) if nbits < 64 else \
+        rng.integers(0, 2**63, size=len(cols), dtype=np.uint64)
+    return cols, vals
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_bsi_all_ops_bytes(ctx, oracle, seed):
+    import roaringbitmap_amd as rb
+    rng = np.random.default_rng(seed)
+    shapes = [(3000, 10, 1 << 18), (200000, 20, 1 << 18), (50000, 40, 1 << 22), (500, 63, 1 << 17)]
+    for n, nbits, uni in shapes:
+        cols, vals = _case(rng, n, nbits, uni)
+        sl, ebm, mn, mx = oracle.bsi_build(cols, vals)
+        for ro in (False, True):
+            d, rsl, rebm = _device_bsi(ctx, oracle, sl, ebm, ro)
+            fcols = np.unique(rng.choice(cols, size=max(1, len(cols) // 3)))
+            fcols = np.concatenate([fcols, rng.integers(0, uni, size=50)]).astype(np.uint32)  # some not in ebM
+            found_ref = oracle.RefBitmap.of(np.unique(fcols))
+            found = ctx.upload_serialized([found_ref.serialize()])
+            preds = [int(v) for v in rng.choice(vals, size=3)] + [0, int(mn), int(mx), int(mx) + 1]
+            for name in OPS:
+                op = getattr(rb, "BSI_" + name)
+                for p in preds:
+                    end = p + int(rng.integers(0, max(1, int(mx) - p + 2)))
+                    for f_dev, f_ref in ((None, None), (found, found_ref)):
+                        got = ctx.bsi_compare(op, d, p, end, int(mn), int(mx), f_dev).serialize()[0]
+                        want = oracle.bsi_compare(rsl, rebm, op, p, end, f_ref, int(mn), int(mx)).serialize()
+                        assert got == want, (name, n, nbits, ro, p, end, f_dev is not None)
+
+
+def test_bsi_reference_known_answers(ctx, oracle):
+    """R64BSITest.java testGT / testGE / testLT / testLE / testRANGE / testNEQ / testValueZero
+    through the Python mirror of the reference API."""
+    import roaringbitmap_amd as rb
+    bsi = rb.Roaring64BitmapSliceIndex(1, 99)
+    for x in range(1, 100):
+        bsi.setValue(x, x)
+    q = lambda op, a, b=0, f=None: list(bsi.compare(op, a, b, f).toArray())  # noqa: E731
+    O = rb.Operation
+    assert q(O.GT, 50) == list(range(51, 100)) and q(O.GT, 99) == []
+    assert q(O.GE, 50) == list(range(50, 100)) and q(O.GE, 100) == []
+    assert q(O.LT, 50) == list(range(1, 50)) and q(O.LT, 1) == []
+    assert q(O.LE, 50) == list(range(1, 51)) and q(O.LE, 0) == []
+    assert q(O.RANGE, 10, 20) == list(range(10, 21)) and q(O.RANGE, 1000, 2000) == []
+    assert q(O.GE, 50, 0, rb.RoaringBitmap.bitmapOf([51, 52, 53])) == [51, 52, 53]
+    z = rb.Roaring64BitmapSliceIndex()
+    for c, v in ((0, 0), (1, 0), (2, 1)):
+        z.setValue(c, v)
+    assert list(z.compare(O.EQ, 0).toArray()) == [0, 1] and list(z.compare(O.EQ, 1).toArray()) == [2]
+    n = rb.Roaring64BitmapSliceIndex()
+    for c, v in ((1, 99), (2, 1), (3, 50)):
+        n.setValue(c, v)
+    assert list(n.compare(O.NEQ, 99).toArray()) == [2, 3]
+
+
+def test_generated_bsi_sample(ctx, oracle):
+    """The config-5 generator's shape (random value bits, full ebM, runOptimize'd), reduced."""
+    import roaringbitmap_amd as rb
+    d = ctx.generate_bsi(24, 3 * 65536 + 1234, seed=4)
+    refs = [oracle.RefBitmap.deserialize(b) for b in d.serialize()]
+    sl, ebm = refs[:-1], refs[-1]
+    lo, hi = 3 << 20, 11 << 20
+    for name in OPS:
+        op = getattr(rb, "BSI_" + name)
+        got = ctx.bsi_compare(op, d, lo, hi, 0, (1 << 24) - 1).serialize()[0]
+        want = oracle.bsi_compare(sl, ebm, op, lo, hi, None, 0, (1 << 24) - 1).serialize()
+        assert got == want, name

@@ -86,3 +86,32 @@ def test_in_place_vs_static_or_full(oracle):
     z = x.clone()
     R.op_inplace(R.OR, z, y)
     assert z.containers()[0][1] == R.BITMAP
+
+
+def test_bsi_known_answers(oracle):
+    """The oracle's restatement of Roaring64BitmapSliceIndex.compare reproduces the reference's own
+    known answers (bsi/src/test/java/org/roaringbitmap/bsi/R64BSITest.java: testGT/GE/LT/LE/RANGE/
+    NEQ/EQ/ValueZero/Sum-style foundSet, and RBBsiTest.java's 32-bit twins)."""
+    import numpy as np
+    R = oracle
+    cols = np.arange(1, 100)
+    sl, ebm, mn, mx = R.bsi_build(cols, cols)
+
+    def q(op, a, b=0, f=None, s=None):
+        s = s or (sl, ebm, mn, mx)
+        return list(R.bsi_compare(s[0], s[1], op, a, b, f, s[2], s[3]).to_array())
+    assert q(R.BSI_GT, 50) == list(range(51, 100)) and q(R.BSI_GT, 0) == list(range(1, 100)) and q(R.BSI_GT, 99) == []
+    assert q(R.BSI_GE, 50) == list(range(50, 100)) and q(R.BSI_GE, 1) == list(range(1, 100)) and q(R.BSI_GE, 100) == []
+    assert q(R.BSI_LT, 50) == list(range(1, 50)) and q(R.BSI_LT, 2**31 - 1) == list(range(1, 100)) and q(R.BSI_LT, 1) == []
+    assert q(R.BSI_LE, 50) == list(range(1, 51)) and q(R.BSI_LE, 2**31 - 1) == list(range(1, 100)) and q(R.BSI_LE, 0) == []
+    assert q(R.BSI_RANGE, 10, 20) == list(range(10, 21)) and q(R.BSI_RANGE, 1, 200) == list(range(1, 100))
+    assert q(R.BSI_RANGE, 1000, 2000) == []
+    assert q(R.BSI_GE, 50, 0, R.RefBitmap.of(np.array([51, 52, 53], np.uint32))) == [51, 52, 53]
+    neq = R.bsi_build([1, 2, 3], [99, 1, 50])
+    assert q(R.BSI_NEQ, 99, s=neq) == [2, 3] and q(R.BSI_NEQ, 100, s=neq) == [1, 2, 3]
+    same = R.bsi_build([1, 2, 3], [99, 99, 99])
+    assert q(R.BSI_NEQ, 99, s=same) == [] and q(R.BSI_NEQ, 1, s=same) == [1, 2, 3]
+    zero = R.bsi_build([0, 1, 2], [0, 0, 1])
+    assert q(R.BSI_EQ, 0, s=zero) == [0, 1] and q(R.BSI_EQ, 1, s=zero) == [2]
+    eq = R.bsi_build(list(range(1, 100)), [1 if x <= 50 else x for x in range(1, 100)])
+    assert len(q(R.BSI_EQ, 1, s=eq)) == 50
