@@ -44,6 +44,7 @@ def parse():
                    help="key-range-sharded wide workload reported beside the headline (strong scaling)")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--census", type=int, default=1, help="also report config 1 (census1881) at N=1")
+    p.add_argument("--bsi", type=int, default=1, help="also report config 5 (BSI RANGE, 64 x 100M) at N=1")
     p.add_argument("--no-cpu-baseline", action="store_true")
     return p.parse_args()
 
@@ -284,6 +285,56 @@ def run_census(args, ctx, rb):
     return out
 
 
+def run_bsi(args, ctx, rb, nslices=64, nrows=100_000_000, steps=5, warmup=2):
+    """Config 5: Roaring64BitmapSliceIndex.compare(RANGE, lo, hi, null) over 64 slices x 100M rows
+    (runOptimize'd BSI, random value bits) — one fused pass per high key for each O'Neil chain."""
+    d = ctx.generate_bsi(nslices, nrows, seed=42)
+    lo, hi = 0x3A00_0000_0000_0000, 0xB100_0000_0000_0000  # a mid-range window: no min/max shortcut
+    vmin, vmax = 0, (1 << nslices) - 1
+    for _ in range(warmup):
+        ctx.bsi_compare(rb.BSI_RANGE, d, lo, hi, vmin, vmax).close()
+    ctx.synchronize()
+    in_bytes, k_ms, k_bytes = 0, [], []
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        r = ctx.bsi_compare(rb.BSI_RANGE, d, lo, hi, vmin, vmax)
+        st = ctx.stats()
+        in_bytes += st["input_bytes"]
+        k_ms.append(st["main_kernel_ms"])
+        k_bytes.append(st["main_kernel_bytes"])
+        card = None
+        if _ == steps - 1:
+            card = int(r.cardinalities()[0])
+        r.close()
+    ctx.synchronize()
+    el = time.perf_counter() - t0
+    km, kb = float(np.mean(k_ms)), float(np.mean(k_bytes))
+    out = {"workload": f"config5: BSI compare RANGE over {nslices} slices x {nrows} rows (2 O'Neil chains + AND)",
+           "value": round(in_bytes / el / 1e9, 3), "unit": "GB/s", "ms_per_step": round(el / steps * 1e3, 4),
+           "result_cardinality": card,
+           "roofline": {"bound": "hbm", "kernel": st["main_kernel"], "achieved": round(kb / (km * 1e-3) / 1e9, 2),
+                        "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(kb / (km * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                        "kernel_ms": round(km, 4), "algorithmic_bytes_per_launch": int(kb)}}
+    if not args.no_cpu_baseline:
+        from oracle import rbref as R
+        small = ctx.generate_bsi(nslices, 4 * 65536, seed=42)  # the first 4 keys of the same shape
+        refs = [R.RefBitmap.deserialize(x) for x in small.serialize()]
+        r = ctx.bsi_compare(rb.BSI_RANGE, small, lo, hi, vmin, vmax)
+        sb = ctx.stats()["input_bytes"]
+        r.close()
+        small.close()
+        passes, t0 = 0, time.perf_counter()
+        while time.perf_counter() - t0 < 3.0:
+            R.bsi_compare(refs[:-1], refs[-1], R.BSI_RANGE, lo, hi, None, vmin, vmax)
+            passes += 1
+        el = time.perf_counter() - t0
+        out["cpu_baseline"] = {"value": round(passes * sb / el / 1e9, 3), "unit": "GB/s", "cores": 1, "kind": "port",
+                               "sample": f"the same query on 4 x 65536 rows ({sb} algorithmic input bytes), "
+                                         "oracle/rbref.py BSI restatement over rbref.cpp static ops, 1 thread"}
+    d.close()
+    return out
+
+
 def main():
     args = parse()
     world, rank, local, dist = dist_setup(args)
@@ -395,13 +446,15 @@ def main():
         }
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(ctx, rb, a, b, op, args.cpu_seconds)
-    if args.secondary != "none" or (world == 1 and args.census):
+    if args.secondary != "none" or (world == 1 and (args.census or args.bsi)):
         a.close()
         b.close()
     if world == 1 and args.census:
         c1 = run_census(args, ctx, rb)
         if rank == 0:
             line.setdefault("secondary", {})["census1881"] = c1
+    if world == 1 and args.bsi:
+        line.setdefault("secondary", {})["bsi_range"] = run_bsi(args, ctx, rb)
     if args.secondary != "none":
         w = run_wide(args, args.secondary, world, rank, local, dist, ctx, rb,
                      WIDE_WORKLOADS[args.secondary][2], max(3, args.steps // 3), 1)
