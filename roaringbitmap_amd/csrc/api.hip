@@ -70,7 +70,7 @@ void ctx_unref(rbgpu_ctx *ctx) {
   ctx->pool.clear();
   ctx->ws_pairs.destroy();
   ctx->ws_tasks.destroy();
-  ctx->ws_wide.destroy();
+  ctx->ws_segs.destroy();
   (void)hipStreamDestroy(ctx->stream);
   delete ctx;
 }
@@ -498,37 +498,52 @@ static int pairwise_impl(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu
   const bool card_only = out == nullptr;
   hipStream_t st = ctx->stream;
   const uint64_t np = npairs;
-  const uint64_t scan_tmp = scan_tmp_words(np + 1);
-  size_t need = 0;
-  need += 2 * aligned256(np * 4);            // indices
-  need += 11 * aligned256((np + 1) * 8);     // 4 counts, 4 scans, result counts, pair cards, spare
-  need += aligned256(scan_tmp * 8);
+  // ---- per pair: indices, merge-path segment counts and their scan, pair cardinalities
+  size_t need = 2 * aligned256(np * 4) + 3 * aligned256((np + 1) * 8) + aligned256(scan_tmp_words(np + 1) * 8);
   if (ctx->ws_pairs.reserve(need, st) != hipSuccess) return fail(RB_ENOMEM, "pair workspace");
   Workspace &W = ctx->ws_pairs;
   uint32_t *d_aidx = a_idx ? W.take<uint32_t>(np) : nullptr;
   uint32_t *d_bidx = b_idx ? W.take<uint32_t>(np) : nullptr;
-  PairCountArrays cnt{W.take<uint64_t>(np + 1), W.take<uint64_t>(np + 1), W.take<uint64_t>(np + 1),
-                      W.take<uint64_t>(np + 1)};
-  PairCountArrays scn{W.take<uint64_t>(np + 1), W.take<uint64_t>(np + 1), W.take<uint64_t>(np + 1),
-                      W.take<uint64_t>(np + 1)};
-  uint64_t *rcnt = W.take<uint64_t>(np + 1), *pcard = W.take<uint64_t>(np + 1);
-  uint64_t *tmp = W.take<uint64_t>(std::max<uint64_t>(scan_tmp, 1));
+  uint64_t *nseg_p = W.take<uint64_t>(np + 1), *seg_begin = W.take<uint64_t>(np + 1);
+  uint64_t *pcard = W.take<uint64_t>(np + 1);
+  uint64_t *ptmp = W.take<uint64_t>(std::max<uint64_t>(scan_tmp_words(np + 1), 1));
   if (d_aidx) HIPCHK(hipMemcpyAsync(d_aidx, a_idx, np * 4, hipMemcpyHostToDevice, st));
   if (d_bidx) HIPCHK(hipMemcpyAsync(d_bidx, b_idx, np * 4, hipMemcpyHostToDevice, st));
+  if (card_out && np) HIPCHK(hipMemsetAsync(pcard, 0, np * 8, st));
 
   stats_begin(ctx);
-  PairArgs pa{op, a->view(), b->view(), d_aidx, d_bidx, npairs};
-  launch_pair_count(pa, cnt, ctx->d_stats, st);
-  scan_exclusive(cnt.task, scn.task, np, tmp, st);
-  scan_exclusive(cnt.light, scn.light, np, tmp, st);
-  scan_exclusive(cnt.big, scn.big, np, tmp, st);
-  scan_exclusive(cnt.small, scn.small, np, tmp, st);
+  PairArgs pa{op, a->view(), b->view(), d_aidx, d_bidx, npairs, seg_begin, nullptr, 0};
+  launch_seg_count(pa, nseg_p, st);
+  scan_exclusive(nseg_p, seg_begin, np, ptmp, st);
   uint64_t *const tot = ctx->h_pinned;
-  HIPCHK(hipMemcpyAsync(tot + 0, scn.task + np, 8, hipMemcpyDeviceToHost, st));
-  HIPCHK(hipMemcpyAsync(tot + 1, scn.light + np, 8, hipMemcpyDeviceToHost, st));
-  HIPCHK(hipMemcpyAsync(tot + 2, scn.big + np, 8, hipMemcpyDeviceToHost, st));
-  HIPCHK(hipMemcpyAsync(tot + 3, scn.small + np, 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(tot + 6, seg_begin + np, 8, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
+  const uint64_t ns = np ? tot[6] : 0;
+  // ---- per segment: counts, scans, result counts / offsets
+  need = aligned256(ns * 4) + 10 * aligned256((ns + 1) * 8) + aligned256(scan_tmp_words(ns + 1) * 8);
+  if (ctx->ws_segs.reserve(need, st) != hipSuccess) return fail(RB_ENOMEM, "segment workspace");
+  Workspace &G = ctx->ws_segs;
+  uint32_t *seg_pair = G.take<uint32_t>(std::max<uint64_t>(ns, 1));
+  PairCountArrays cnt{G.take<uint64_t>(ns + 1), G.take<uint64_t>(ns + 1), G.take<uint64_t>(ns + 1),
+                      G.take<uint64_t>(ns + 1)};
+  PairCountArrays scn{G.take<uint64_t>(ns + 1), G.take<uint64_t>(ns + 1), G.take<uint64_t>(ns + 1),
+                      G.take<uint64_t>(ns + 1)};
+  uint64_t *rcnt = G.take<uint64_t>(ns + 1), *rseg = G.take<uint64_t>(ns + 1);
+  uint64_t *tmp = G.take<uint64_t>(std::max<uint64_t>(scan_tmp_words(ns + 1), 1));
+  launch_seg_fill(pa, seg_begin, seg_pair, st);
+  pa.seg_pair = seg_pair;
+  pa.nseg = ns;
+  launch_pair_count(pa, cnt, ctx->d_stats, st);
+  scan_exclusive(cnt.task, scn.task, ns, tmp, st);
+  scan_exclusive(cnt.light, scn.light, ns, tmp, st);
+  scan_exclusive(cnt.big, scn.big, ns, tmp, st);
+  scan_exclusive(cnt.small, scn.small, ns, tmp, st);
+  HIPCHK(hipMemcpyAsync(tot + 0, scn.task + ns, 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(tot + 1, scn.light + ns, 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(tot + 2, scn.big + ns, 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(tot + 3, scn.small + ns, 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  if (!ns) tot[0] = tot[1] = tot[2] = tot[3] = 0;
   const uint64_t ntasks = tot[0], nlight = tot[1], nheavy = ntasks - nlight, nbig_t = tot[2], small_t = tot[3];
   const uint64_t small_base = nbig_t * kBitmapBytes;
   const uint64_t arena = card_only ? 0 : small_base + small_t;
@@ -579,13 +594,15 @@ static int pairwise_impl(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu
   launch_pairwise(op, card_only, a->payload, b->payload, light, nlight, heavy, nheavy, res ? res->payload : nullptr,
                   tm, st, ctx->ev[2]);
   HIPCHK(hipEventRecord(ctx->ev[3], st));
-  launch_compact_count(scn.task, npairs, tm.type, rcnt, st);
-  uint64_t *rbegin = res ? res->begin : W.take<uint64_t>(np + 1);
-  scan_exclusive(rcnt, rbegin, np, tmp, st);
+  launch_compact_count(scn.task, ns, tm.type, rcnt, st);
+  scan_exclusive(rcnt, rseg, ns, tmp, st);
   OutView ov{};
   if (res) ov = OutView{res->key, res->type, res->card, res->nruns, res->off};
-  launch_compact_write(scn.task, npairs, tm, rbegin, ov, pcard, ctx->d_stats, st);
-  HIPCHK(hipMemcpyAsync(ctx->h_pinned + 5, rbegin + np, 8, hipMemcpyDeviceToHost, st));
+  launch_compact_write(scn.task, ns, tm, rseg, ov, seg_pair, card_out ? pcard : nullptr, ctx->d_stats, st);
+  if (res && np) launch_pair_rbegin(seg_begin, npairs, rseg, res->begin, st);
+  else if (res) HIPCHK(hipMemsetAsync(res->begin, 0, 8, st));
+  if (np) HIPCHK(hipMemcpyAsync(ctx->h_pinned + 5, rseg + ns, 8, hipMemcpyDeviceToHost, st));
+  else ctx->h_pinned[5] = 0;
   if (card_out && np) HIPCHK(hipMemcpyAsync(card_out, pcard, np * 8, hipMemcpyDeviceToHost, st));
   const KernelSpan spans[2] = {{"k_pair_tasks<light>", 2, 4, nlight}, {"k_pair_tasks<heavy>", 3, 5, nheavy}};
   rc = stats_end(ctx, ntasks, 0, spans, 2);

@@ -272,55 +272,81 @@ __global__ __launch_bounds__(256, 2) void k_bsi_chain(SetView bsi, SetView fnd, 
   }
 }
 
+// RANGE = and(GE(start), LE(end)) (RoaringBitmapSliceIndex.java:492-497) on the two chains' keyed
+// slots: both are indexed by the same key list, so the static AND is one wave per key (AND rule:
+// R&R -> EFF, else AB; empty or one-sided -> dropped).
+__global__ __launch_bounds__(256) void k_bsi_and(const uint8_t *__restrict__ ga, WideOut wa,
+                                                 const uint8_t *__restrict__ gb, WideOut wb, uint32_t nk,
+                                                 uint8_t *__restrict__ out, WideOut wo, uint64_t *stats) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds[4][2048];
+  const int lane = lane_id();
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t q = blockIdx.x * 4 + wv;
+  if (q >= nk) return;
+  uint32_t *s = lds[wv];
+  const int ta = wa.type[q], tb = wb.type[q];
+  Meta rm{0, 0, 0, 0};
+  uint64_t a[kW];
+  if (ta != kEmpty && tb != kEmpty) {
+    const Meta ma{1, ta, (int)wa.card[q], wa.nruns[q]}, mb{1, tb, (int)wb.card[q], wb.nruns[q]};
+    load_container(ta, ga + (uint64_t)q * kBitmapBytes, (uint32_t)ma.card, (uint32_t)ma.runs, s, a, lane);
+    stage_container(tb, gb + (uint64_t)q * kBitmapBytes, (uint32_t)mb.card, (uint32_t)mb.runs, s, lane);
+#pragma unroll
+    for (int j = 0; j < kW; ++j) a[j] &= lds_word(s, j, lane);
+    wave_lds_sync();
+    rm = classify(a, lane, eff_and(ma, mb), false, false);
+  }
+  const int ty = rm.present ? rm.type : kEmpty;
+  if (rm.present) emit_container(ty, a, rm.card, rm.runs, out + (uint64_t)q * kBitmapBytes, s, lane);
+  if (lane == 0) {
+    wo.type[q] = (uint8_t)ty;
+    wo.card[q] = (uint32_t)(rm.present ? rm.card : 0);
+    wo.nruns[q] = (uint16_t)(ty == kRun ? rm.runs : 0);
+    if (rm.present)
+      atomicAdd((unsigned long long *)&stats[1 * kStripes + (q & (kStripes - 1))],
+                (unsigned long long)(payload_bytes(ty, rm.card, rm.runs) + (ty == kRun ? 2 : 0) + 16));
+  }
+}
+
 // ---------------------------------------------------------------- host side
 static unsigned nblk(uint64_t n, unsigned per) { return (unsigned)((n + per - 1) / per); }
 
-// One O'Neil chain (oNeilCompare with `final_op`) over the keys of F -> one-bitmap result set.
-static int bsi_chain(rbgpu_ctx *ctx, const rbgpu_set *bsi, uint32_t nbits, int final_op, uint64_t pred,
-                     const rbgpu_set *found, const int32_t *d_table, const uint32_t *d_klist, uint32_t nk,
-                     rbgpu_set **out) {
+// Keyed slots of one reduction: an 8 KiB payload slot per active key plus its type / card / runs.
+struct KeyedSlots {
+  uint8_t *payload = nullptr;
+  WideOut wo{nullptr, nullptr, nullptr};
+  int alloc(rbgpu_ctx *ctx, uint32_t nk, bool with_payload) {
+    const uint64_t nk1 = std::max<uint32_t>(nk, 1);
+    if ((with_payload && ctx->pool.alloc((void **)&payload, nk1 * kBitmapBytes)) ||
+        ctx->pool.alloc((void **)&wo.type, nk1) || ctx->pool.alloc((void **)&wo.card, nk1 * 4) ||
+        ctx->pool.alloc((void **)&wo.nruns, nk1 * 2))
+      return fail(RB_ENOMEM, "bsi slots for %u keys", nk);
+    return RB_OK;
+  }
+  void release(rbgpu_ctx *ctx, bool with_payload) {
+    if (with_payload) ctx->pool.release(payload);
+    for (void *p : {(void *)wo.type, (void *)wo.card, (void *)wo.nruns}) ctx->pool.release(p);
+  }
+};
+
+// One O'Neil chain (oNeilCompare with `final_op`) over the keys of F into keyed slots.
+static void bsi_chain(rbgpu_ctx *ctx, const rbgpu_set *bsi, uint32_t nbits, int final_op, uint64_t pred,
+                      const rbgpu_set *found, const int32_t *d_table, const uint32_t *d_klist, uint32_t nk,
+                      uint8_t *o, const WideOut &wo) {
+  if (!nk) return;
   hipStream_t st = ctx->stream;
-  rbgpu_set *res = new rbgpu_set;
-  int rc = set_alloc(ctx, res, 1, nk, (uint64_t)std::max<uint32_t>(nk, 1) * kBitmapBytes);
-  if (rc) {
-    delete res;
-    return rc;
-  }
-  uint8_t *w_type;
-  uint32_t *w_card;
-  uint16_t *w_nruns;
-  const uint64_t nk1 = std::max<uint32_t>(nk, 1);
-  if (ctx->pool.alloc((void **)&w_type, nk1) || ctx->pool.alloc((void **)&w_card, nk1 * 4) ||
-      ctx->pool.alloc((void **)&w_nruns, nk1 * 2)) {
-    rbgpu_set_free(res);
-    return fail(RB_ENOMEM, "bsi result workspace");
-  }
-  const WideOut wo{w_type, w_card, w_nruns};
   const SetView bv = bsi->view();
   const SetView fv = found ? found->view() : bv;
   const int hf = found != nullptr;
-  if (nk) {
-    const unsigned g = nblk(nk, 4);
-    switch (final_op) {
-    case kBsiEQ: k_bsi_chain<kBsiEQ><<<g, 256, 0, st>>>(bv, fv, hf, d_table, nbits, pred, d_klist, nk, res->payload, wo, ctx->d_stats); break;
-    case kBsiNEQ: k_bsi_chain<kBsiNEQ><<<g, 256, 0, st>>>(bv, fv, hf, d_table, nbits, pred, d_klist, nk, res->payload, wo, ctx->d_stats); break;
-    case kBsiLE: k_bsi_chain<kBsiLE><<<g, 256, 0, st>>>(bv, fv, hf, d_table, nbits, pred, d_klist, nk, res->payload, wo, ctx->d_stats); break;
-    case kBsiLT: k_bsi_chain<kBsiLT><<<g, 256, 0, st>>>(bv, fv, hf, d_table, nbits, pred, d_klist, nk, res->payload, wo, ctx->d_stats); break;
-    case kBsiGE: k_bsi_chain<kBsiGE><<<g, 256, 0, st>>>(bv, fv, hf, d_table, nbits, pred, d_klist, nk, res->payload, wo, ctx->d_stats); break;
-    default: k_bsi_chain<kBsiGT><<<g, 256, 0, st>>>(bv, fv, hf, d_table, nbits, pred, d_klist, nk, res->payload, wo, ctx->d_stats); break;
-    }
+  const unsigned g = nblk(nk, 4);
+  switch (final_op) {
+  case kBsiEQ: k_bsi_chain<kBsiEQ><<<g, 256, 0, st>>>(bv, fv, hf, d_table, nbits, pred, d_klist, nk, o, wo, ctx->d_stats); break;
+  case kBsiNEQ: k_bsi_chain<kBsiNEQ><<<g, 256, 0, st>>>(bv, fv, hf, d_table, nbits, pred, d_klist, nk, o, wo, ctx->d_stats); break;
+  case kBsiLE: k_bsi_chain<kBsiLE><<<g, 256, 0, st>>>(bv, fv, hf, d_table, nbits, pred, d_klist, nk, o, wo, ctx->d_stats); break;
+  case kBsiLT: k_bsi_chain<kBsiLT><<<g, 256, 0, st>>>(bv, fv, hf, d_table, nbits, pred, d_klist, nk, o, wo, ctx->d_stats); break;
+  case kBsiGE: k_bsi_chain<kBsiGE><<<g, 256, 0, st>>>(bv, fv, hf, d_table, nbits, pred, d_klist, nk, o, wo, ctx->d_stats); break;
+  default: k_bsi_chain<kBsiGT><<<g, 256, 0, st>>>(bv, fv, hf, d_table, nbits, pred, d_klist, nk, o, wo, ctx->d_stats); break;
   }
-  uint64_t nres = 0;
-  rc = compact_keyed(ctx, d_klist, nk, wo, res, &nres);
-  ctx->pool.release(w_type);
-  ctx->pool.release(w_card);
-  ctx->pool.release(w_nruns);
-  if (rc) {
-    rbgpu_set_free(res);
-    return rc;
-  }
-  *out = res;
-  return RB_OK;
 }
 
 // compareUsingMinMax (RoaringBitmapSliceIndex.java:505-577), values unsigned: 1 = all, 0 = empty,
@@ -386,32 +412,46 @@ int bsi_compare(rbgpu_ctx *ctx, const rbgpu_set *bsi, int op, uint64_t start, ui
   HIPCHK(hipMemcpyAsync(ctx->h_pinned, d_pos + 65536, 8, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
   const uint32_t nk = (uint32_t)ctx->h_pinned[0];
-  HIPCHK(hipEventRecord(ctx->ev[1], st));
-  int rc;
-  rbgpu_set *ge = nullptr, *le = nullptr;
-  if (op != 6) {
-    rc = bsi_chain(ctx, bsi, nbits, op, start, found, d_table, d_klist, nk, out);
-  } else { // RANGE: and(GE(start), LE(end)) — the two chains, then the static AND
-    rc = bsi_chain(ctx, bsi, nbits, kBsiGE, start, found, d_table, d_klist, nk, &ge);
-    if (!rc) rc = bsi_chain(ctx, bsi, nbits, kBsiLE, end, found, d_table, d_klist, nk, &le);
+  // result set: one 8 KiB slot per key of F, compacted at the end
+  rbgpu_set *res = new rbgpu_set;
+  int rc = set_alloc(ctx, res, 1, nk, (uint64_t)std::max<uint32_t>(nk, 1) * kBitmapBytes);
+  if (rc) {
+    delete res;
+    release();
+    return rc;
   }
-  HIPCHK(hipEventRecord(ctx->ev[2], st));
-  release();
-  const KernelSpan spans[1] = {{"k_bsi_chain", 0, 1, op == 6 ? 2ull * nk : nk}};
-  if (!rc) rc = stats_end(ctx, nk, op == 6 ? 0 : (*out)->nc, spans, 1);
-  if (op == 6) {
-    if (!rc) {
-      const rb_stats chains = ctx->last; // the chains are the measured work; keep their stats
-      rc = rbgpu_pairwise(ctx, RB_AND, ge, le, nullptr, nullptr, 1, out);
-      const double and_ms = ctx->last.total_ms;
-      ctx->last = chains;
-      ctx->last.total_ms += and_ms;
-      if (!rc) ctx->last.result_containers = (*out)->nc;
+  KeyedSlots fin, ge, le;
+  rc = fin.alloc(ctx, nk, false);
+  if (!rc && op == 6) rc = ge.alloc(ctx, nk, true);
+  if (!rc && op == 6) rc = le.alloc(ctx, nk, true);
+  if (!rc) {
+    HIPCHK(hipEventRecord(ctx->ev[1], st));
+    if (op != 6) {
+      bsi_chain(ctx, bsi, nbits, op, start, found, d_table, d_klist, nk, res->payload, fin.wo);
+    } else { // RANGE: the two chains, then the keyed static AND
+      bsi_chain(ctx, bsi, nbits, kBsiGE, start, found, d_table, d_klist, nk, ge.payload, ge.wo);
+      bsi_chain(ctx, bsi, nbits, kBsiLE, end, found, d_table, d_klist, nk, le.payload, le.wo);
+      if (nk) k_bsi_and<<<nblk(nk, 4), 256, 0, st>>>(ge.payload, ge.wo, le.payload, le.wo, nk, res->payload, fin.wo,
+                                                    ctx->d_stats);
     }
-    rbgpu_set_free(ge);
-    rbgpu_set_free(le);
+    HIPCHK(hipEventRecord(ctx->ev[2], st));
+    uint64_t nres = 0;
+    rc = compact_keyed(ctx, d_klist, nk, fin.wo, res, &nres);
+    const KernelSpan spans[1] = {{"k_bsi_chain", 0, 1, op == 6 ? 2ull * nk : nk}};
+    if (!rc) rc = stats_end(ctx, nk, nres, spans, 1);
   }
-  return rc;
+  fin.release(ctx, false);
+  if (op == 6) {
+    ge.release(ctx, true);
+    le.release(ctx, true);
+  }
+  release();
+  if (rc) {
+    rbgpu_set_free(res);
+    return rc;
+  }
+  *out = res;
+  return RB_OK;
 }
 
 } // namespace rbg

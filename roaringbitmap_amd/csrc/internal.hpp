@@ -92,7 +92,7 @@ struct rbgpu_ctx {
   hipStream_t stream = nullptr;
   hipEvent_t ev[6] = {};   // [0] call start, [1..n] around the compute kernels, [5] call end
   rbg::DevPool pool;
-  rbg::Workspace ws_pairs, ws_tasks, ws_wide;
+  rbg::Workspace ws_pairs, ws_tasks, ws_segs; // per pair / per task / per merge-path segment
   uint64_t *d_stats = nullptr;  // [kStatWords * kStripes] striped algorithmic byte counters
   uint64_t *h_pinned = nullptr; // [16]
   uint64_t *h_stats = nullptr;  // [kStatWords * kStripes]

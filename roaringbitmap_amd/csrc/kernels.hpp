@@ -15,6 +15,9 @@ struct PairArgs {
   const uint32_t *aidx; // may be null (identity)
   const uint32_t *bidx; // may be null (identity)
   uint32_t npairs;
+  const uint64_t *seg_begin; // [npairs + 1] first merge-path segment of each pair
+  const uint32_t *seg_pair;  // [nseg] pair of each segment
+  uint64_t nseg;
 };
 // per task result metadata (workspace, indexed like tasks)
 struct TaskMeta {
@@ -37,6 +40,12 @@ struct PairCountArrays {
 };
 // stats words (striped, see common.hpp): 0/1 total input/output bytes, 2/3 filter+copy / register-path
 // input, 4/5 filter+copy / register-path output
+// merge-path segments of every pair (<= 256 merged keys each): counts, then the segment -> pair map
+void launch_seg_count(const PairArgs &a, uint64_t *nseg, hipStream_t st);
+void launch_seg_fill(const PairArgs &a, const uint64_t *seg_begin, uint32_t *seg_pair, hipStream_t st);
+void launch_pair_rbegin(const uint64_t *seg_begin, uint32_t npairs, const uint64_t *rseg, uint64_t *rbegin,
+                        hipStream_t st);
+// per segment from here on
 void launch_pair_count(const PairArgs &a, const PairCountArrays &c, uint64_t *stats, hipStream_t st);
 void launch_pair_emit(const PairArgs &a, const PairCountArrays &scans, uint64_t small_base, TaskRec *light,
                       TaskRec *heavy, const TaskMeta &tm, hipStream_t st);
@@ -48,10 +57,11 @@ void launch_pairwise(int op, bool card_only, const uint8_t *pa, const uint8_t *p
 // measurement probes (rbgpu_internal_probe): mode 1 = task-order payload reads, 2 = streaming read
 void launch_probe(int op, int mode, const uint8_t *pa, const uint8_t *pb, uint64_t a_bytes, const TaskRec *recs,
                   uint64_t n, uint32_t *sink, unsigned blocks, hipStream_t st);
-void launch_compact_count(const uint64_t *task_begin, uint32_t npairs, const uint8_t *ttype, uint64_t *cnt,
+void launch_compact_count(const uint64_t *task_begin, uint64_t nseg, const uint8_t *ttype, uint64_t *cnt,
                           hipStream_t st);
-void launch_compact_write(const uint64_t *task_begin, uint32_t npairs, const TaskMeta &tm, const uint64_t *rbegin,
-                          const OutView &out, uint64_t *pair_card, uint64_t *stats, hipStream_t st);
+void launch_compact_write(const uint64_t *task_begin, uint64_t nseg, const TaskMeta &tm, const uint64_t *rbegin,
+                          const OutView &out, const uint32_t *seg_pair, uint64_t *pair_card, uint64_t *stats,
+                          hipStream_t st);
 
 // ---- wide.hip: per-key reduction outputs (one 8 KiB slot per active key q)
 struct WideOut {

@@ -60,12 +60,59 @@ __device__ __forceinline__ void stat_add(uint64_t *stats, int word, uint64_t v) 
   }
 }
 
+// ---------------------------------------------------------------- key alignment by merge path
+// A pair is cut into segments of <= kSegKeys merged keys (merge path over the two sorted key lists,
+// A first on equal keys), one thread per segment, so a pair of large bitmaps aligns its keys in
+// parallel.  A matched key is never split: when a cut falls between A's key and its equal B
+// partner, the partner stays with A.
+constexpr uint64_t kSegKeys = 256;
+
+__device__ __forceinline__ void pair_ranges(const PairArgs &a, uint32_t p, uint64_t &i0, uint64_t &na, uint64_t &j0,
+                                            uint64_t &nb) {
+  const uint32_t ai = a.aidx ? a.aidx[p] : p, bi = a.bidx ? a.bidx[p] : p;
+  i0 = a.A.begin[ai];
+  na = a.A.begin[ai + 1] - i0;
+  j0 = a.B.begin[bi];
+  nb = a.B.begin[bi + 1] - j0;
+}
+// position after d merged keys -> (i, j) offsets into A and B
+__device__ __forceinline__ void merge_split(const uint16_t *ka, uint64_t na, const uint16_t *kb, uint64_t nb,
+                                            uint64_t d, uint64_t &i, uint64_t &j) {
+  uint64_t lo = d > nb ? d - nb : 0, hi = d < na ? d : na;
+  while (lo < hi) {
+    const uint64_t mid = (lo + hi) >> 1;
+    if (ka[mid] <= kb[d - mid - 1]) lo = mid + 1;
+    else hi = mid;
+  }
+  i = lo;
+  j = d - lo;
+  if (i > 0 && j < nb && ka[i - 1] == kb[j]) ++j;
+}
+__global__ __launch_bounds__(kPairThreads) void k_seg_count(PairArgs a, uint64_t *nseg) {
+  const uint32_t p = blockIdx.x * kPairThreads + threadIdx.x;
+  if (p >= a.npairs) return;
+  uint64_t i0, na, j0, nb;
+  pair_ranges(a, p, i0, na, j0, nb);
+  nseg[p] = (na + nb + kSegKeys - 1) / kSegKeys + (na + nb == 0);
+}
+__global__ __launch_bounds__(kPairThreads) void k_seg_fill(PairArgs a, const uint64_t *seg_begin, uint32_t *seg_pair) {
+  const uint32_t p = blockIdx.x * kPairThreads + threadIdx.x;
+  if (p >= a.npairs) return;
+  for (uint64_t s = seg_begin[p]; s < seg_begin[p + 1]; ++s) seg_pair[s] = p;
+}
+
 // inb[0]: key bytes, inb[1]: light-task input bytes, inb[2]: heavy-task input bytes
 template <bool EMIT>
-__device__ __forceinline__ void pair_walk(const PairArgs &a, uint32_t p, PairCounts &n, uint64_t (&inb)[3],
+__device__ __forceinline__ void pair_walk(const PairArgs &a, uint64_t sg, PairCounts &n, uint64_t (&inb)[3],
                                           const PairBases &base, TaskRec *light, TaskRec *heavy, TaskMeta tm) {
-  const uint32_t ai = a.aidx ? a.aidx[p] : p, bi = a.bidx ? a.bidx[p] : p;
-  uint64_t i = a.A.begin[ai], i1 = a.A.begin[ai + 1], j = a.B.begin[bi], j1 = a.B.begin[bi + 1];
+  const uint32_t p = a.seg_pair[sg];
+  uint64_t i0, na, j0, nb;
+  pair_ranges(a, p, i0, na, j0, nb);
+  const uint64_t d0 = (sg - a.seg_begin[p]) * kSegKeys, d1 = d0 + kSegKeys < na + nb ? d0 + kSegKeys : na + nb;
+  uint64_t si0, sj0, si1, sj1;
+  merge_split(a.A.key + i0, na, a.B.key + j0, nb, d0, si0, sj0);
+  merge_split(a.A.key + i0, na, a.B.key + j0, nb, d1, si1, sj1);
+  uint64_t i = i0 + si0, i1 = i0 + si1, j = j0 + sj0, j1 = j0 + sj1;
   inb[0] += 2 * ((i1 - i) + (j1 - j));
   auto slot = [&](int64_t ia, int64_t ib, uint16_t key, bool big, uint64_t bytes) {
     const int ta = ia >= 0 ? a.A.type[ia] : -1, tb = ib >= 0 ? a.B.type[ib] : -1;
@@ -134,9 +181,9 @@ __device__ __forceinline__ void pair_walk(const PairArgs &a, uint32_t p, PairCou
 }
 
 __global__ __launch_bounds__(kPairThreads) void k_pair_count(PairArgs a, PairCountArrays c, uint64_t *stats) {
-  const uint32_t p = blockIdx.x * kPairThreads + threadIdx.x;
+  const uint64_t p = (uint64_t)blockIdx.x * kPairThreads + threadIdx.x; // segment
   uint64_t inb[3] = {0, 0, 0};
-  if (p < a.npairs) {
+  if (p < a.nseg) {
     PairCounts n{};
     PairBases b{};
     pair_walk<false>(a, p, n, inb, b, nullptr, nullptr, TaskMeta{});
@@ -155,8 +202,8 @@ __global__ __launch_bounds__(kPairThreads) void k_pair_count(PairArgs a, PairCou
 
 __global__ __launch_bounds__(kPairThreads) void k_pair_emit(PairArgs a, PairCountArrays scans, uint64_t small_base,
                                                             TaskRec *light, TaskRec *heavy, TaskMeta tm) {
-  const uint32_t p = blockIdx.x * kPairThreads + threadIdx.x;
-  if (p >= a.npairs) return;
+  const uint64_t p = (uint64_t)blockIdx.x * kPairThreads + threadIdx.x; // segment
+  if (p >= a.nseg) return;
   PairCounts n{};
   PairBases b{scans.task[p], scans.light[p], scans.task[p] - scans.light[p], scans.big[p],
               small_base + scans.small[p]};
@@ -538,18 +585,21 @@ void launch_probe(int op, int mode, const uint8_t *pa, const uint8_t *pb, uint64
 }
 
 // ---------------------------------------------------------------- compaction
-__global__ __launch_bounds__(kPairThreads) void k_compact_count(const uint64_t *tb, uint32_t npairs,
+// compaction runs per segment (units u with tasks [tb[u], tb[u+1])); a pair's results are its
+// segments' results in order
+__global__ __launch_bounds__(kPairThreads) void k_compact_count(const uint64_t *tb, uint64_t npairs,
                                                                 const uint8_t *ttype, uint64_t *cnt) {
-  const uint32_t p = blockIdx.x * kPairThreads + threadIdx.x;
+  const uint64_t p = (uint64_t)blockIdx.x * kPairThreads + threadIdx.x;
   if (p >= npairs) return;
   uint64_t n = 0;
   for (uint64_t t = tb[p]; t < tb[p + 1]; ++t) n += ttype[t] != kEmpty;
   cnt[p] = n;
 }
-__global__ __launch_bounds__(kPairThreads) void k_compact_write(const uint64_t *tb, uint32_t npairs, TaskMeta tm,
+__global__ __launch_bounds__(kPairThreads) void k_compact_write(const uint64_t *tb, uint64_t npairs, TaskMeta tm,
                                                                 const uint64_t *rbegin, OutView out,
-                                                                uint64_t *pair_card, uint64_t *stats) {
-  const uint32_t p = blockIdx.x * kPairThreads + threadIdx.x;
+                                                                const uint32_t *seg_pair, uint64_t *pair_card,
+                                                                uint64_t *stats) {
+  const uint64_t p = (uint64_t)blockIdx.x * kPairThreads + threadIdx.x;
   uint64_t outb[2] = {0, 0};
   if (p < npairs) {
     uint64_t r = rbegin ? rbegin[p] : 0, card = 0;
@@ -567,7 +617,7 @@ __global__ __launch_bounds__(kPairThreads) void k_compact_write(const uint64_t *
       }
       ++r;
     }
-    if (pair_card) pair_card[p] = card;
+    if (pair_card && card) atomicAdd((unsigned long long *)&pair_card[seg_pair[p]], (unsigned long long)card);
   }
   // stats words: 1 total output, 4 light-task output, 5 heavy-task output
   if (stats) {
@@ -577,17 +627,37 @@ __global__ __launch_bounds__(kPairThreads) void k_compact_write(const uint64_t *
   }
 }
 
+// result CSR per pair from the per-segment result offsets
+__global__ __launch_bounds__(kPairThreads) void k_pair_rbegin(const uint64_t *seg_begin, uint32_t npairs,
+                                                              const uint64_t *rseg, uint64_t *rbegin) {
+  const uint32_t p = blockIdx.x * kPairThreads + threadIdx.x;
+  if (p <= npairs) rbegin[p] = rseg[seg_begin[p]];
+}
+
 // ---------------------------------------------------------------- launchers
 static unsigned blocks_for(uint64_t n, unsigned per) { return (unsigned)((n + per - 1) / per); }
 
-void launch_pair_count(const PairArgs &a, const PairCountArrays &c, uint64_t *stats, hipStream_t st) {
+void launch_seg_count(const PairArgs &a, uint64_t *nseg, hipStream_t st) {
   if (!a.npairs) return;
-  k_pair_count<<<blocks_for(a.npairs, kPairThreads), kPairThreads, 0, st>>>(a, c, stats);
+  k_seg_count<<<blocks_for(a.npairs, kPairThreads), kPairThreads, 0, st>>>(a, nseg);
+}
+void launch_seg_fill(const PairArgs &a, const uint64_t *seg_begin, uint32_t *seg_pair, hipStream_t st) {
+  if (!a.npairs) return;
+  k_seg_fill<<<blocks_for(a.npairs, kPairThreads), kPairThreads, 0, st>>>(a, seg_begin, seg_pair);
+}
+void launch_pair_rbegin(const uint64_t *seg_begin, uint32_t npairs, const uint64_t *rseg, uint64_t *rbegin,
+                        hipStream_t st) {
+  k_pair_rbegin<<<blocks_for((uint64_t)npairs + 1, kPairThreads), kPairThreads, 0, st>>>(seg_begin, npairs, rseg,
+                                                                                        rbegin);
+}
+void launch_pair_count(const PairArgs &a, const PairCountArrays &c, uint64_t *stats, hipStream_t st) {
+  if (!a.nseg) return;
+  k_pair_count<<<blocks_for(a.nseg, kPairThreads), kPairThreads, 0, st>>>(a, c, stats);
 }
 void launch_pair_emit(const PairArgs &a, const PairCountArrays &scans, uint64_t small_base, TaskRec *light,
                       TaskRec *heavy, const TaskMeta &tm, hipStream_t st) {
-  if (!a.npairs) return;
-  k_pair_emit<<<blocks_for(a.npairs, kPairThreads), kPairThreads, 0, st>>>(a, scans, small_base, light, heavy, tm);
+  if (!a.nseg) return;
+  k_pair_emit<<<blocks_for(a.nseg, kPairThreads), kPairThreads, 0, st>>>(a, scans, small_base, light, heavy, tm);
 }
 // Persistent grid: every CU filled to the kernel's occupancy, waves stride over the tasks.
 template <class K> static unsigned persistent_blocks(K kernel, uint64_t tasks) {
@@ -638,16 +708,17 @@ void launch_pairwise(int op, bool card_only, const uint8_t *pa, const uint8_t *p
   default: launch_op<RB_ANDNOT>(card_only, pa, pb, light, nl, heavy, nh, out, tm, st, mid); break;
   }
 }
-void launch_compact_count(const uint64_t *task_begin, uint32_t npairs, const uint8_t *ttype, uint64_t *cnt,
+void launch_compact_count(const uint64_t *task_begin, uint64_t nseg, const uint8_t *ttype, uint64_t *cnt,
                           hipStream_t st) {
-  if (!npairs) return;
-  k_compact_count<<<blocks_for(npairs, kPairThreads), kPairThreads, 0, st>>>(task_begin, npairs, ttype, cnt);
+  if (!nseg) return;
+  k_compact_count<<<blocks_for(nseg, kPairThreads), kPairThreads, 0, st>>>(task_begin, nseg, ttype, cnt);
 }
-void launch_compact_write(const uint64_t *task_begin, uint32_t npairs, const TaskMeta &tm, const uint64_t *rbegin,
-                          const OutView &out, uint64_t *pair_card, uint64_t *stats, hipStream_t st) {
-  if (!npairs) return;
-  k_compact_write<<<blocks_for(npairs, kPairThreads), kPairThreads, 0, st>>>(task_begin, npairs, tm, rbegin, out,
-                                                                             pair_card, stats);
+void launch_compact_write(const uint64_t *task_begin, uint64_t nseg, const TaskMeta &tm, const uint64_t *rbegin,
+                          const OutView &out, const uint32_t *seg_pair, uint64_t *pair_card, uint64_t *stats,
+                          hipStream_t st) {
+  if (!nseg) return;
+  k_compact_write<<<blocks_for(nseg, kPairThreads), kPairThreads, 0, st>>>(task_begin, nseg, tm, rbegin, out,
+                                                                           seg_pair, pair_card, stats);
 }
 
 } // namespace rbg

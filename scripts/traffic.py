@@ -1,0 +1,35 @@
+"""HBM traffic per launch from rocprofv3 PMC passes (MI355X_MICROARCH.md, HBM section):
+FETCH_SIZE and WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE reports half of the bytes of 16-B-per-lane
+streaming reads, so it is doubled (every payload load in librbgpu is a 16-B-per-lane buffer/global
+load); WRITE_SIZE is taken as is.  Writes profiles/<round>/traffic.json keyed by kernel name.
+
+usage: python scripts/traffic.py <pmc dir with p*/run_counter_collection.csv> <out.json> "<command>"
+"""
+import collections
+import csv
+import glob
+import json
+import sys
+
+root, out, cmd = sys.argv[1], sys.argv[2], sys.argv[3]
+vals = collections.defaultdict(lambda: collections.defaultdict(list))
+for f in sorted(glob.glob(f"{root}/p*/run_counter_collection.csv")):
+    for row in csv.DictReader(open(f)):
+        name = row["Kernel_Name"].split("(")[0].replace("void ", "").strip()
+        # one group per (kernel, grid): the same kernel at another problem size is another workload
+        vals[(name, int(row["Grid_Size"]))][row["Counter_Name"]].append(float(row["Counter_Value"]))
+res = {}
+for (name, grid), c in vals.items():
+    if "FETCH_SIZE" not in c or "WRITE_SIZE" not in c:
+        continue
+    fetch = 2.0 * 1024 * sum(c["FETCH_SIZE"]) / len(c["FETCH_SIZE"])
+    write = 1024.0 * sum(c["WRITE_SIZE"]) / len(c["WRITE_SIZE"])
+    g = {"grid": grid, "fetch_bytes": int(fetch), "write_bytes": int(write), "traffic_bytes": int(fetch + write),
+         "dispatches": len(c["FETCH_SIZE"])}
+    res.setdefault(name, []).append(g)
+for name in res:
+    res[name].sort(key=lambda g: -g["traffic_bytes"])
+json.dump({"command": cmd, "correction": "FETCH_SIZE x2 (gfx950 16-B/lane reads), KiB->B", "kernels": res},
+          open(out, "w"), indent=1, sort_keys=True)
+for name, gs in res.items():
+    print(name, gs[0])

@@ -124,3 +124,27 @@ def test_generated_filter_posting_sample_parity(ctx, oracle):
             assert c > 4096
         else:
             assert 2 + 4 * r < min(8192, 2 * c)
+
+
+def test_large_pairs_merge_path_segments(ctx, oracle):
+    """Pairs of bitmaps with thousands of keys: key alignment is cut into merge-path segments of
+    256 merged keys; matched keys straddling a cut must stay together and every op must still
+    give the oracle's bytes (RoaringBitmap.and/or/xor/andNot key loops)."""
+    rng = np.random.default_rng(77)
+    bms = []
+    for n_keys, space in ((3000, 5000), (2500, 5000), (700, 1400), (65536, 65536), (1, 65536), (0, 10)):
+        keys = np.sort(rng.choice(space, size=n_keys, replace=False)).astype(np.uint32)
+        vals = [np.unique(rng.integers(0, 65536, size=int(rng.integers(1, 40)))).astype(np.uint32) | (k << 16)
+                for k in keys]
+        bms.append(np.concatenate(vals) if vals else np.zeros(0, np.uint32))
+    s = ctx.upload_values(bms, run_optimize=True)
+    refs = _ref_list(oracle, s.serialize())
+    a_idx = np.array([0, 1, 0, 2, 3, 3, 4, 5, 0, 3], np.uint32)
+    b_idx = np.array([1, 0, 2, 1, 3, 0, 3, 0, 5, 4], np.uint32)
+    for opname, op in OPS.items():
+        got = ctx.pairwise(op, s, s, a_idx, b_idx).serialize()
+        cards = ctx.pairwise_cardinality(op, s, s, a_idx, b_idx)
+        for i in range(len(a_idx)):
+            ref = oracle.op(op, refs[a_idx[i]], refs[b_idx[i]])
+            assert got[i] == ref.serialize(), (opname, i)
+            assert int(cards[i]) == ref.cardinality(), (opname, i)
