@@ -30,6 +30,21 @@ METRIC = "input GB/s (HBM roofline %) for batched and/or/xor + wide-OR, 1/2/4/8 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
 
+TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r01", "traffic.json")
+
+
+def pmc_traffic(pmc_name: str):
+    """HBM bytes per launch of `pmc_name` from the committed rocprofv3 PMC summary of this same bench
+    command (scripts/traffic.py: FETCH_SIZE x2 for gfx950 16-B/lane reads + WRITE_SIZE, separate
+    passes); the dominant (largest) dispatch group is the headline launch.  None if not profiled."""
+    try:
+        with open(TRAFFIC_JSON) as f:
+            groups = json.load(f)["kernels"].get(pmc_name)
+        return int(groups[0]["traffic_bytes"]) if groups else None
+    except (OSError, ValueError, KeyError):
+        return None
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
@@ -192,7 +207,9 @@ def run_wide(args, name, world, rank, local, dist, ctx, rb, nbitmaps, steps, war
         "key_range_rank0": [lo, hi],
         "parallelism": f"key-range shards x{world}; RCCL all_gather of shard summaries (cardinality, "
                        f"containers, Run containers, payload bytes) per step" if world > 1 else "single GPU",
-        "roofline": {"bound": "hbm", "kernel": st["main_kernel"], "achieved": round(k_bytes / (k_ms * 1e-3) / 1e9, 2),
+        "roofline": {"bound": "hbm", "kernel": st["main_kernel"], "traffic": pmc_traffic(
+                         "rbg::k_wide_reduce<%d>" % getattr(rb, sem_name)) if world == 1 else None,
+                     "achieved": round(k_bytes / (k_ms * 1e-3) / 1e9, 2),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(k_bytes / (k_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                      "kernel_ms_max_over_ranks": round(k_ms, 4), "algorithmic_bytes_per_launch_rank0": int(k_bytes)},
@@ -312,7 +329,9 @@ def run_bsi(args, ctx, rb, nslices=64, nrows=100_000_000, steps=5, warmup=2):
     out = {"workload": f"config5: BSI compare RANGE over {nslices} slices x {nrows} rows (2 O'Neil chains + AND)",
            "value": round(in_bytes / el / 1e9, 3), "unit": "GB/s", "ms_per_step": round(el / steps * 1e3, 4),
            "result_cardinality": card,
-           "roofline": {"bound": "hbm", "kernel": st["main_kernel"], "achieved": round(kb / (km * 1e-3) / 1e9, 2),
+           "roofline": {"bound": "hbm", "kernel": st["main_kernel"],
+                        "traffic_per_chain": pmc_traffic("rbg::k_bsi_chain<4>"),
+                        "achieved": round(kb / (km * 1e-3) / 1e9, 2),
                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(kb / (km * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                         "kernel_ms": round(km, 4), "algorithmic_bytes_per_launch": int(kb)}}
     if not args.no_cpu_baseline:
@@ -351,7 +370,7 @@ def main():
                     "scaling": "strong", "vs_baseline": None, "dtype": "u64",
                     "data": "synthetic (device SplitMix64 generator keyed by (bitmap, key); SURVEY §8d)",
                     "config": {k: v for k, v in w.items() if k not in ("value", "roofline", "ms_per_step")},
-                    "roofline": dict(w["roofline"], traffic=None)}
+                    "roofline": w["roofline"]}
             if world == 1 and not args.no_cpu_baseline:
                 line["cpu_baseline"] = wide_cpu_baseline(ctx, rb, args.workload, args.cpu_seconds / 2)
             print(json.dumps(line), flush=True)
@@ -436,7 +455,9 @@ def main():
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": None,
+                "traffic": pmc_traffic(f"rbg::k_pair_tasks<{op}, false, 0>" if "light" in main_name
+                                       else f"rbg::k_pair_tasks<{op}, false, 1>"),
+                "traffic_source": "profiles/r01/traffic.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes)",
                 "kernel_ms": round(k_ms, 4),
                 "algorithmic_bytes_per_launch": int(per_launch),
                 "kernels": {n: {"ms": round(v["ms"], 4), "bytes": v["bytes"], "items": v["items"],
