@@ -638,6 +638,13 @@ int rbgpu_internal_probe(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu
   return pairwise_impl(ctx, op, a, b, nullptr, nullptr, npairs, &res, nullptr, mode);
 }
 
+// Kernel-study hook (not part of rbgpu.h): config-2 generator type mix, cumulative per mille
+// {filter Array, filter Array+Bitmap, posting Array, posting Array+Bitmap}.
+void rbgpu_internal_set_mix(int fa, int fab, int pa, int pab) {
+  const int m[4] = {fa, fab, pa, pab};
+  set_mix(m);
+}
+
 // ---------------------------------------------------------------- wide
 int rbgpu_wide(rbgpu_ctx *ctx, int sem, const rbgpu_set *in, const uint32_t *members, uint32_t n, rbgpu_set **out) {
   return rbgpu_wide_keys(ctx, sem, in, members, n, 0, 65536, out);

@@ -212,6 +212,11 @@ HostRng key_rng(uint64_t seed, uint32_t i, uint32_t k) {
   return r;
 }
 
+// Config-2 type mix as cumulative per-mille cuts (filter A, filter A+B, posting A, posting A+B).
+// rbgpu_internal_set_mix changes it for kernel studies (scripts/mix_study.py); the bench uses the
+// SURVEY §8d defaults.
+int g_mix[4] = {400, 700, 700, 800};
+
 void structure(int workload, uint32_t n, uint64_t seed, uint32_t key_lo, uint32_t key_hi,
                std::vector<GenStructure> &out) {
   HostRng r{seed * 0x2545F4914F6CDD1Dull + 0x9E3779B97F4A7C15ull};
@@ -221,8 +226,8 @@ void structure(int workload, uint32_t n, uint64_t seed, uint32_t key_lo, uint32_
     for (uint32_t i = 0; i < n; ++i) { // filters: all 4 keys of the 2^18 universe, A/B/R = .4/.3/.3
       for (uint16_t k = 0; k < 4; ++k) {
         uint32_t u = r.below(1000);
-        if (u < 400) f.add(k, kGenArray, 1 + r.below(4096));
-        else if (u < 700) f.add(k, kGenBitmap, dense_num(r));
+        if (u < (uint32_t)g_mix[0]) f.add(k, kGenArray, 1 + r.below(4096));
+        else if (u < (uint32_t)g_mix[1]) f.add(k, kGenBitmap, dense_num(r));
         else f.add(k, kGenRuns, 1 + r.below(1024));
       }
       f.close();
@@ -233,8 +238,8 @@ void structure(int workload, uint32_t n, uint64_t seed, uint32_t key_lo, uint32_
       for (uint16_t k = 0; k < 4; ++k) {
         if (!((mask >> k) & 1)) continue;
         uint32_t u = r.below(1000);
-        if (u < 700) p.add(k, kGenArray, 1 + r.below(2048));
-        else if (u < 800) p.add(k, kGenBitmap, dense_num(r));
+        if (u < (uint32_t)g_mix[2]) p.add(k, kGenArray, 1 + r.below(2048));
+        else if (u < (uint32_t)g_mix[3]) p.add(k, kGenBitmap, dense_num(r));
         else p.add(k, kGenRuns, 1 + r.below(1024));
       }
       p.close();
@@ -327,6 +332,10 @@ int materialize(rbgpu_ctx *ctx, const GenStructure &gs, uint64_t seed, rbgpu_set
   return RB_OK;
 }
 } // namespace
+
+void set_mix(const int *m) {
+  for (int i = 0; i < 4; ++i) g_mix[i] = m[i];
+}
 
 int generate_bsi(rbgpu_ctx *ctx, uint32_t nslices, uint64_t nrows, uint64_t seed, rbgpu_set **out) {
   if (nslices > 64 || nrows > (1ull << 32)) return fail(RB_EINVAL, "bsi: at most 64 slices over 2^32 rows");

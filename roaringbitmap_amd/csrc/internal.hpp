@@ -140,6 +140,7 @@ int compact_keyed(rbgpu_ctx *ctx, const uint32_t *d_klist, uint32_t nk, const Wi
 // bsi.hip: op = BitmapSliceIndex.Operation ordinal (EQ, NEQ, LE, LT, GE, GT, RANGE)
 int bsi_compare(rbgpu_ctx *ctx, const rbgpu_set *bsi, int op, uint64_t start, uint64_t end, uint64_t vmin,
                 uint64_t vmax, const rbgpu_set *found, rbgpu_set **out);
+void set_mix(const int *m);
 int generate_bsi(rbgpu_ctx *ctx, uint32_t nslices, uint64_t nrows, uint64_t seed, rbgpu_set **out);
 // generate.hip
 int generate_sets(rbgpu_ctx *ctx, int workload, uint32_t n, uint64_t seed, uint32_t key_lo, uint32_t key_hi,

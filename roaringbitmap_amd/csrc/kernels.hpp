@@ -70,6 +70,11 @@ struct WideOut {
   uint16_t *nruns;
 };
 
+// ---- wide_runs.hip: Run-list fast path for naive_or / workShyAnd / naive_xor keys whose containers
+// are all Runs with <= 8 runs; route[q] = 0 where done, 1 where the generic kernel must run
+bool launch_wide_runs(int sem, const SetView &s, const uint32_t *cid, const uint64_t *seg, const uint32_t *klist,
+                      uint32_t nk, uint8_t *out, const WideOut &wo, uint8_t *route, uint64_t *stats, hipStream_t st);
+
 // ---- setops.hip
 void launch_bitmap_cards(const SetView &s, uint32_t nbitmaps, uint64_t *out, hipStream_t st);
 void launch_gather(const uint8_t *src, const uint64_t *soff, const uint64_t *bytes, uint8_t *dst,

@@ -12,6 +12,7 @@
 //                    register bitmap, Bitmaps streamed two at a time), reference type decision,
 //                    emission into an 8 KiB slot
 //   compaction       drop empty results, result CSR
+#include <cstdlib>
 #include <cstring>
 
 #include <rocprim/rocprim.hpp>
@@ -146,12 +147,13 @@ template <int SEM>
 __global__ __launch_bounds__(256) void k_wide_reduce(SetView s, const uint32_t *__restrict__ cid,
                                                      const uint64_t *__restrict__ seg, const uint32_t *__restrict__ klist,
                                                      uint32_t nk, uint8_t *__restrict__ out, WideOut wo,
-                                                     uint64_t *stats) {
+                                                     const uint8_t *__restrict__ route, uint64_t *stats) {
   __shared__ __attribute__((aligned(16))) uint32_t lds_all[4][2048];
   const int lane = lane_id();
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t q = blockIdx.x * 4 + wv;
   if (q >= nk) return;
+  if (route && route[q] == 0) return; // done by the Run-list fast path (wide_runs.hip)
   uint32_t *lds = lds_all[wv];
   const uint32_t key = klist[q];
   const uint64_t lo = seg[key], hi = seg[key + 1];
@@ -352,8 +354,9 @@ int compact_keyed(rbgpu_ctx *ctx, const uint32_t *d_klist, uint32_t nk, const Wi
 
 template <int SEM>
 static void launch_reduce(const SetView &s, const uint32_t *cid, const uint64_t *seg, const uint32_t *klist,
-                          uint32_t nk, uint8_t *out, const WideOut &wo, uint64_t *stats, hipStream_t st) {
-  k_wide_reduce<SEM><<<nblk(nk, 4), 256, 0, st>>>(s, cid, seg, klist, nk, out, wo, stats);
+                          uint32_t nk, uint8_t *out, const WideOut &wo, uint64_t *stats, hipStream_t st,
+                          const uint8_t *route = nullptr) {
+  k_wide_reduce<SEM><<<nblk(nk, 4), 256, 0, st>>>(s, cid, seg, klist, nk, out, wo, route, stats);
 }
 
 int wide_run(rbgpu_ctx *ctx, int sem, const rbgpu_set *in, const std::vector<uint32_t> &members_in,
@@ -445,14 +448,23 @@ int wide_run(rbgpu_ctx *ctx, int sem, const rbgpu_set *in, const std::vector<uin
     return fail(RB_ENOMEM, "wide result workspace");
   }
   WideOut wo{w_type, w_card, w_nruns};
+  uint8_t *d_route = nullptr;
+  bool fast_ok = !getenv("RBGPU_NO_RUN_FASTPATH"); // parity tests run both paths
+  if (pool.alloc((void **)&d_route, nk1)) d_route = nullptr;
   HIPCHK(hipEventRecord(ctx->ev[1], st));
   if (nk) {
+    // Run-heavy keys first (all Run containers with <= 8 runs): route[q] = 0 when done there
+    const bool fast = sem == RB_FAST_OR || sem == RB_WORKSHY_AND || sem == RB_FAST_XOR;
+    if (fast && !d_route) fast_ok = false;
+    if (fast && fast_ok)
+      launch_wide_runs(sem, sv, d_cid2, d_seg, d_klist, nk, res->payload, wo, d_route, ctx->d_stats, st);
+    const uint8_t *rt = fast && fast_ok ? d_route : nullptr;
     switch (sem) {
-    case RB_FAST_OR: launch_reduce<RB_FAST_OR>(sv, d_cid2, d_seg, d_klist, nk, res->payload, wo, ctx->d_stats, st); break;
-    case RB_WORKSHY_AND: launch_reduce<RB_WORKSHY_AND>(sv, d_cid2, d_seg, d_klist, nk, res->payload, wo, ctx->d_stats, st); break;
+    case RB_FAST_OR: launch_reduce<RB_FAST_OR>(sv, d_cid2, d_seg, d_klist, nk, res->payload, wo, ctx->d_stats, st, rt); break;
+    case RB_WORKSHY_AND: launch_reduce<RB_WORKSHY_AND>(sv, d_cid2, d_seg, d_klist, nk, res->payload, wo, ctx->d_stats, st, rt); break;
     case RB_NAIVE_AND: launch_reduce<RB_NAIVE_AND>(sv, d_cid2, d_seg, d_klist, nk, res->payload, wo, ctx->d_stats, st); break;
     case RB_NAIVE_AND_ITER: launch_reduce<RB_NAIVE_AND_ITER>(sv, d_cid2, d_seg, d_klist, nk, res->payload, wo, ctx->d_stats, st); break;
-    case RB_FAST_XOR: launch_reduce<RB_FAST_XOR>(sv, d_cid2, d_seg, d_klist, nk, res->payload, wo, ctx->d_stats, st); break;
+    case RB_FAST_XOR: launch_reduce<RB_FAST_XOR>(sv, d_cid2, d_seg, d_klist, nk, res->payload, wo, ctx->d_stats, st, rt); break;
     case RB_PAR_OR: launch_reduce<RB_PAR_OR>(sv, d_cid2, d_seg, d_klist, nk, res->payload, wo, ctx->d_stats, st); break;
     default: launch_reduce<RB_PAR_XOR>(sv, d_cid2, d_seg, d_klist, nk, res->payload, wo, ctx->d_stats, st); break;
     }
@@ -475,6 +487,7 @@ int wide_run(rbgpu_ctx *ctx, int sem, const rbgpu_set *in, const std::vector<uin
   pool.release(w_type);
   pool.release(w_card);
   pool.release(w_nruns);
+  pool.release(d_route);
   release();
   if (rc) {
     rbgpu_set_free(res);

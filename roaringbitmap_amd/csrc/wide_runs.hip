@@ -1,0 +1,301 @@
+// wide_runs.hip — wide aggregation over Run-heavy keys (thousands of small Run
+// containers per key) without expanding each container to 65536 bits.
+//
+// The generic k_wide_reduce expands every container into a register bitmap (~6 µs of latency-bound
+// work per 20-byte container).  Here, for a key whose containers are all Runs with <= 8 runs:
+//   * 64 containers are prefetched per batch, one per lane (cid, descriptor, both 16-B halves of
+//     the run list), double-buffered; container j's runs are broadcast with readlane;
+//   * naive_xor (FastAggregation.xor, FastAggregation.java:576-582): the accumulator is an 8 KiB
+//     LDS bitmap; XOR with a run = complement of its words, done lane-parallel.  Cardinality after
+//     the step = c + |run| - 2 |acc ∩ run| (range popcount of the same words); the number of
+//     maximal runs changes only at the run's boundary bits s-1, s, e, e+1 (interior rising and
+//     falling edges swap and their difference telescopes to M[e] - M[s]) — so the reference's
+//     per-step type automaton (RoaringBitmap.xor in place, :3296-3348; RunContainer.xor /
+//     ArrayContainer.xor types) runs exactly with O(words of the runs) work per container;
+//   * naive_or (FastAggregation.java:541-548): range OR into the LDS bitmap, LR(c) at the end;
+//   * workShyAnd (FastAggregation.java:356-396): the accumulator is a list of <= 64 intervals, one per
+//     lane, intersected with each container's runs; LR(c) at the end.
+// A key that does not qualify (another container type, > 8 runs, > 64 intervals) is routed to the
+// generic kernel (route[q] = 1) — results are identical either way.
+#include "internal.hpp"
+#include "kernels.hpp"
+#include "wave.hpp"
+
+namespace rbg {
+
+constexpr int kMaxRunsFast = 8;
+
+// dword mask of [lo, hi] (inclusive bit positions) restricted to dword w
+__device__ __forceinline__ uint32_t dword_mask(uint32_t w, uint32_t lo, uint32_t hi) {
+  const uint32_t a = max(lo, w * 32), b = min(hi, w * 32 + 31);
+  if (a > b) return 0u;
+  return (0xFFFFFFFFu >> (31 - (b - a))) << (a - w * 32);
+}
+__device__ __forceinline__ uint32_t lds_bit(const uint32_t *s, uint32_t x) { return (s[x >> 5] >> (x & 31)) & 1; }
+
+struct RunBatch {
+  uint32_t card, nr, typ;
+  uint4 r0, r1;
+};
+__device__ __forceinline__ RunBatch load_batch(const SetView &s, const uint32_t *cid, uint64_t i, uint64_t hi) {
+  RunBatch b;
+  b.card = 0;
+  b.nr = 0;
+  b.typ = kRun;
+  b.r0 = make_uint4(0, 0, 0, 0);
+  b.r1 = make_uint4(0, 0, 0, 0);
+  if (i < hi) {
+    const uint32_t c = cid[i];
+    b.typ = s.type[c];
+    b.card = s.card[c];
+    b.nr = s.nruns[c];
+    if (b.typ == kRun && b.nr <= kMaxRunsFast) {
+      const uint4 *p = reinterpret_cast<const uint4 *>(s.payload + s.off[c]);
+      b.r0 = p[0];
+      if (b.nr > 4) b.r1 = p[1];
+    }
+  }
+  return b;
+}
+__device__ __forceinline__ uint32_t run_word(const RunBatch &b, int t) {
+  switch (t) {
+  case 0: return b.r0.x;
+  case 1: return b.r0.y;
+  case 2: return b.r0.z;
+  case 3: return b.r0.w;
+  case 4: return b.r1.x;
+  case 5: return b.r1.y;
+  case 6: return b.r1.z;
+  default: return b.r1.w;
+  }
+}
+
+template <int SEM>
+__global__ __launch_bounds__(256) void k_wide_runs(SetView s, const uint32_t *__restrict__ cid,
+                                                   const uint64_t *__restrict__ seg, const uint32_t *__restrict__ klist,
+                                                   uint32_t nk, uint8_t *__restrict__ out, WideOut wo,
+                                                   uint8_t *__restrict__ route, uint64_t *stats) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds_all[4][2048];
+  const int lane = lane_id();
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t q = blockIdx.x * 4 + wv;
+  if (q >= nk) return;
+  uint32_t *acc = lds_all[wv];
+  const uint32_t key = klist[q];
+  const uint64_t lo = seg[key], hi = seg[key + 1];
+  if (SEM == RB_FAST_OR && hi - lo < 2) { // a lone container: clone + repairAfterLazy -> generic path
+    if (lane == 0) route[q] = 1;
+    return;
+  }
+  if (SEM != RB_WORKSHY_AND) {
+    lds_zero(acc, lane);
+    wave_lds_sync();
+  }
+  // accumulator state (wave-uniform)
+  bool present = false, fail_route = false;
+  int t = kRun, c = 0, r = 0;
+  uint32_t ia = 0, ib = 0; // AND: this lane's interval [ia, ib]
+  int na = -1;            // AND: interval count, -1 = not started
+  uint64_t inb = 0;
+  RunBatch nxt = load_batch(s, cid, lo + lane, hi);
+  for (uint64_t base = lo; base < hi && !fail_route && na != 0; base += 64) {
+    const RunBatch cur = nxt;
+    __builtin_amdgcn_sched_barrier(0);
+    if (base + 64 < hi) nxt = load_batch(s, cid, base + 64 + lane, hi);
+    // eligibility of the whole batch
+    const bool bad = (base + lane < hi) && (cur.typ != kRun || cur.nr > (uint32_t)kMaxRunsFast);
+    if (__ballot(bad)) {
+      fail_route = true;
+      break;
+    }
+    const int nb = (int)min<uint64_t>(64, hi - base);
+    for (int j = 0; j < nb; ++j) {
+      const int nr = (int)readlane(cur.nr, j);
+      const int cc = (int)readlane(cur.card, j);
+      inb += 4ull * nr + 2 + 16;
+      // this container's runs, wave-uniform: start / end
+      uint32_t rs[kMaxRunsFast], re[kMaxRunsFast];
+#pragma unroll
+      for (int u = 0; u < kMaxRunsFast; ++u) {
+        const uint32_t v = readlane(run_word(cur, u), j);
+        rs[u] = v & 0xFFFF;
+        re[u] = (v & 0xFFFF) + (v >> 16);
+      }
+      if (SEM == RB_WORKSHY_AND) {
+        if (na < 0) { // the first container: its runs
+          na = nr;
+#pragma unroll
+          for (int u = 0; u < kMaxRunsFast; ++u)
+            if (lane == u) {
+              ia = rs[u];
+              ib = re[u];
+            }
+          continue;
+        }
+        // intersect this lane's interval with every run; pieces in order
+        uint32_t k = 0;
+        if (lane < na) {
+#pragma unroll
+          for (int u = 0; u < kMaxRunsFast; ++u)
+            if (u < nr && max(ia, rs[u]) <= min(ib, re[u])) ++k;
+        }
+        const uint32_t incl = wave_scan_u32(k, lane);
+        const int total = (int)readlane(incl, 63);
+        if (total > 64) {
+          fail_route = true;
+          break;
+        }
+        uint32_t pos = incl - k;
+        if (lane < na) {
+#pragma unroll
+          for (int u = 0; u < kMaxRunsFast; ++u) {
+            const uint32_t a = max(ia, rs[u]), b = min(ib, re[u]);
+            if (u < nr && a <= b) {
+              acc[2 * pos] = a;
+              acc[2 * pos + 1] = b;
+              ++pos;
+            }
+          }
+        }
+        wave_lds_sync();
+        na = total;
+        if (lane < na) {
+          ia = acc[2 * lane];
+          ib = acc[2 * lane + 1];
+        }
+        wave_lds_sync();
+        if (na == 0) break; // AND stays empty
+        continue;
+      }
+      // ---- range updates over the runs' dwords (OR: set, XOR: complement + metrics)
+      uint32_t o[kMaxRunsFast + 1];
+      o[0] = 0;
+#pragma unroll
+      for (int u = 0; u < kMaxRunsFast; ++u) o[u + 1] = o[u] + (u < nr ? (re[u] >> 5) - (rs[u] >> 5) + 1 : 0);
+      const uint32_t W = o[nr];
+      // XOR: boundary bits before the update (lane u <-> run u)
+      int dr = 0;
+      if (SEM == RB_FAST_XOR && lane < nr) {
+        uint32_t s0 = 0, e0 = 0;
+#pragma unroll
+        for (int u = 0; u < kMaxRunsFast; ++u)
+          if (lane == u) {
+            s0 = rs[u];
+            e0 = re[u];
+          }
+        const uint32_t bsm1 = s0 ? lds_bit(acc, s0 - 1) : 0, bs = lds_bit(acc, s0), be = lds_bit(acc, e0);
+        const uint32_t bep1 = e0 < 65535 ? lds_bit(acc, e0 + 1) : 0;
+        dr = -((int)be - (int)bs);                                         // interior edges
+        dr += (int)(!bs && !bsm1) - (int)(bs && !bsm1);                    // pair (s-1, s)
+        if (e0 < 65535) dr += (int)(bep1 && be) - (int)(bep1 && !be);     // pair (e, e+1)
+      }
+      uint32_t inter = 0;
+      for (uint32_t g0 = 0; g0 < W; g0 += 64) {
+        const uint32_t g = g0 + lane;
+        uint32_t m = 0, w = 0;
+        if (g < W) {
+          int u = 0;
+#pragma unroll
+          for (int v = 1; v < kMaxRunsFast; ++v) u += (v < nr && g >= o[v]) ? 1 : 0;
+          uint32_t su = 0, eu = 0, ou = 0;
+#pragma unroll
+          for (int v = 0; v < kMaxRunsFast; ++v)
+            if (u == v) {
+              su = rs[v];
+              eu = re[v];
+              ou = o[v];
+            }
+          w = (su >> 5) + (g - ou);
+          m = dword_mask(w, su, eu);
+          if (SEM == RB_FAST_XOR) inter += (uint32_t)__popc(acc[w] & m);
+        }
+        if (g < W) {
+          if (SEM == RB_FAST_XOR) atomicXor(&acc[w], m);
+          else atomicOr(&acc[w], m);
+        }
+      }
+      if (SEM == RB_FAST_XOR) {
+        const int isum = (int)wave_sum_u32(inter);
+        const int dsum = (int)wave_sum_u32((uint32_t)(dr + 4)) - 4 * 64;
+        if (!present) { // key absent: clone (type kept)
+          present = true;
+          t = kRun;
+          c = cc;
+          r = nr;
+        } else {
+          const int ct = t, c0 = c;
+          c = c0 + cc - 2 * isum;
+          r = r + dsum;
+          // RunContainer.xor / ArrayContainer.xor / BitmapContainer.xor types, SURVEY §8a
+          if (ct == kRun || (ct == kArray && c0 < kRunArrayThreshold)) t = type_eff(c, r);
+          else t = type_ab(c);
+          if (c == 0) present = false; // RoaringBitmap.xor in place removes the empty container
+        }
+      }
+      wave_lds_sync();
+    }
+  }
+  if (fail_route) {
+    if (lane == 0) route[q] = 1;
+    return;
+  }
+  // ---- result
+  uint8_t *dst = out + (uint64_t)q * kBitmapBytes;
+  int ty = kEmpty;
+  if (SEM == RB_WORKSHY_AND) {
+    // rebuild the bitmap from the intervals (toggles at a and b+1, then the prefix transform)
+    lds_zero(acc, lane);
+    wave_lds_sync();
+    uint32_t card_part = 0;
+    if (lane < na) {
+      card_part = ib - ia + 1;
+      atomicXor(&acc[ia >> 5], 1u << (ia & 31));
+      if (ib + 1 < 65536) atomicXor(&acc[(ib + 1) >> 5], 1u << ((ib + 1) & 31));
+    }
+    wave_lds_sync();
+    toggles_to_words_lds(acc, lane);
+    wave_lds_sync();
+    c = (int)wave_sum_u32(card_part);
+    ty = c ? type_lr(c) : kEmpty;
+    r = ty == kRun ? 1 : 0;
+  } else if (SEM == RB_FAST_OR) {
+    uint64_t w[kW];
+    lds_read_words(acc, w, lane);
+    int rr;
+    metrics(w, lane, false, c, rr);
+    ty = type_lr(c);
+    r = ty == kRun ? 1 : 0;
+  } else {
+    ty = present && c > 0 ? t : kEmpty;
+  }
+  if (ty != kEmpty) {
+    uint64_t w[kW];
+    lds_read_words(acc, w, lane);
+    wave_lds_sync();
+    emit_container(ty, w, c, r, dst, acc, lane);
+  }
+  if (lane == 0) {
+    route[q] = 0;
+    wo.type[q] = (uint8_t)ty;
+    wo.card[q] = (uint32_t)c;
+    wo.nruns[q] = (uint16_t)(ty == kRun ? r : 0);
+    const int stripe = q & (kStripes - 1);
+    atomicAdd((unsigned long long *)&stats[0 * kStripes + stripe], (unsigned long long)inb);
+    if (ty != kEmpty)
+      atomicAdd((unsigned long long *)&stats[1 * kStripes + stripe],
+                (unsigned long long)(payload_bytes(ty, (uint32_t)c, (uint32_t)r) + (ty == kRun ? 2 : 0) + 16));
+  }
+}
+
+bool launch_wide_runs(int sem, const SetView &s, const uint32_t *cid, const uint64_t *seg, const uint32_t *klist,
+                      uint32_t nk, uint8_t *out, const WideOut &wo, uint8_t *route, uint64_t *stats, hipStream_t st) {
+  const unsigned g = (nk + 3) / 4;
+  switch (sem) {
+  case RB_FAST_OR: k_wide_runs<RB_FAST_OR><<<g, 256, 0, st>>>(s, cid, seg, klist, nk, out, wo, route, stats); return true;
+  case RB_WORKSHY_AND: k_wide_runs<RB_WORKSHY_AND><<<g, 256, 0, st>>>(s, cid, seg, klist, nk, out, wo, route, stats); return true;
+  case RB_FAST_XOR: k_wide_runs<RB_FAST_XOR><<<g, 256, 0, st>>>(s, cid, seg, klist, nk, out, wo, route, stats); return true;
+  default: return false;
+  }
+}
+
+} // namespace rbg

@@ -124,3 +124,62 @@ def test_generated_key_shards_equal_full_dataset(ctx):
                 got += [h.container_payload(i).tobytes() + bytes([h.type[i]]) + int(h.key[i]).to_bytes(2, "little")
                         for i in range(int(h.begin[b]), int(h.begin[b + 1]))]
             assert got == want, (wl, b)
+
+
+def test_run_fastpath_config4_shape(ctx, oracle):
+    """Config-4 shape (every key, Run containers with a shared core run + <= 7 random runs): the
+    Run-list fast path (wide_runs.hip) must give the oracle's bytes for naive_or / workShyAnd /
+    naive_xor, and the same bytes as the generic per-key kernel."""
+    import os
+
+    import roaringbitmap_amd as rb
+    a, _ = ctx.generate(rb.WL_WIDE_RUNS, 24, seed=3)
+    refs = [oracle.RefBitmap.deserialize(b) for b in a.serialize()]
+    members = np.arange(24, dtype=np.uint32)
+    for sem in ("FAST_OR", "FAST_AND", "WORKSHY_AND", "FAST_XOR", "PAR_XOR"):
+        want = oracle.wide(getattr(oracle, sem), [refs[m] for m in members]).serialize()
+        got = ctx.wide(getattr(rb, sem), a, members).serialize()[0]
+        assert got == want, sem
+        os.environ["RBGPU_NO_RUN_FASTPATH"] = "1"
+        try:
+            assert ctx.wide(getattr(rb, sem), a, members).serialize()[0] == want, sem
+        finally:
+            del os.environ["RBGPU_NO_RUN_FASTPATH"]
+    # a subset and odd counts (workShyAnd vs naive_and switch at 10, xor removals)
+    for n in (2, 3, 11):
+        sub = members[:n]
+        for sem in ("FAST_OR", "FAST_AND", "FAST_XOR"):
+            want = oracle.wide(getattr(oracle, sem), [refs[m] for m in sub]).serialize()
+            assert ctx.wide(getattr(rb, sem), a, sub).serialize()[0] == want, (sem, n)
+
+
+def test_run_fastpath_mixed_keys_fall_back(ctx, oracle):
+    """Keys where some container is not a small Run (Array, Bitmap, > 8 runs) are routed to the
+    generic kernel inside the same call; XOR chains that empty a key mid-way remove it."""
+    import roaringbitmap_amd as rb
+    rng = np.random.default_rng(9)
+    bms = []
+    for i in range(30):
+        parts = []
+        for k in range(8):
+            if k < 4:  # small-run keys: shared core + few runs; some identical -> XOR cancels
+                core = 1000 * k
+                v = [np.arange(core, core + 700)]
+                for _ in range(int(rng.integers(0, 4))):
+                    s = int(rng.integers(0, 65000))
+                    v.append(np.arange(s, s + int(rng.integers(1, 200))))
+                if i % 5 == 0:
+                    v = [np.arange(core, core + 700)]
+            else:      # mixed keys
+                kind = ["a4095", "dense", "runs", "fewruns"][(i + k) % 4]
+                from datasets import _container_values
+                v = [_container_values(rng, kind)]
+            parts.append((np.unique(np.concatenate(v)) % 65536).astype(np.uint32) | np.uint32(k << 16))
+        bms.append(np.concatenate(parts))
+    s = ctx.upload_values(bms, run_optimize=True)
+    refs = [oracle.RefBitmap.deserialize(b) for b in s.serialize()]
+    for n in (2, 5, 12, 30):
+        members = np.arange(n, dtype=np.uint32)
+        for sem in ("FAST_OR", "FAST_AND", "WORKSHY_AND", "FAST_XOR"):
+            want = oracle.wide(getattr(oracle, sem), [refs[m] for m in members]).serialize()
+            assert ctx.wide(getattr(rb, sem), s, members).serialize()[0] == want, (sem, n)
