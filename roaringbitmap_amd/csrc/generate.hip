@@ -1,3 +1,4 @@
+#include <algorithm>
 // generate.hip — device-side synthetic container generator for the benchmark workloads
 // (SURVEY §8d "rbgen"): SplitMix64 streams keyed by (seed, container id, lane), every container
 // finished with runOptimize semantics like RoaringBitmapWriter(runCompress=true)
@@ -124,19 +125,21 @@ __global__ __launch_bounds__(256) void k_gen_measure(GenSpec g, uint64_t n, uint
   __shared__ __attribute__((aligned(16))) uint32_t lds[4][2048];
   const int lane = lane_id();
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint64_t cid = (uint64_t)blockIdx.x * 4 + wv;
-  if (cid >= n) return;
-  uint64_t w[kW];
-  gen_container(g, cid, lds[wv], w, lane);
-  int c, r;
-  gen_finish(w, lane, c, r);
-  const int ty = type_runopt(c, r);
-  if (lane == 0) {
-    type[cid] = (uint8_t)ty;
-    card[cid] = (uint32_t)c;
-    nruns[cid] = (uint16_t)(ty == kRun ? r : 0);
-    big[cid] = ty == kBitmap;
-    small[cid] = ty == kBitmap ? 0 : round16(payload_bytes(ty, c, r));
+  // grid-stride over containers: a launch may not exceed 2^32 work-items per dimension
+  for (uint64_t cid = (uint64_t)blockIdx.x * 4 + wv; cid < n; cid += (uint64_t)gridDim.x * 4) {
+    uint64_t w[kW];
+    gen_container(g, cid, lds[wv], w, lane);
+    int c, r;
+    gen_finish(w, lane, c, r);
+    const int ty = type_runopt(c, r);
+    if (lane == 0) {
+      type[cid] = (uint8_t)ty;
+      card[cid] = (uint32_t)c;
+      nruns[cid] = (uint16_t)(ty == kRun ? r : 0);
+      big[cid] = ty == kBitmap;
+      small[cid] = ty == kBitmap ? 0 : round16(payload_bytes(ty, c, r));
+    }
+    wave_lds_sync();
   }
 }
 
@@ -145,24 +148,25 @@ __global__ __launch_bounds__(256) void k_gen_emit(GenSpec g, uint64_t n, const u
   __shared__ __attribute__((aligned(16))) uint32_t lds[4][2048];
   const int lane = lane_id();
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint64_t cid = (uint64_t)blockIdx.x * 4 + wv;
-  if (cid >= n) return;
-  uint64_t w[kW];
-  gen_container(g, cid, lds[wv], w, lane);
-  int c, r;
-  gen_finish(w, lane, c, r);
-  emit_container(type[cid], w, c, r, payload + off[cid], lds[wv], lane);
+  for (uint64_t cid = (uint64_t)blockIdx.x * 4 + wv; cid < n; cid += (uint64_t)gridDim.x * 4) {
+    uint64_t w[kW];
+    gen_container(g, cid, lds[wv], w, lane);
+    int c, r;
+    gen_finish(w, lane, c, r);
+    emit_container(type[cid], w, c, r, payload + off[cid], lds[wv], lane);
+    wave_lds_sync();
+  }
 }
 
 void launch_gen_measure(const GenSpec &g, uint64_t n, uint8_t *type, uint32_t *card, uint16_t *nruns, uint64_t *big,
                         uint64_t *small, hipStream_t st) {
   if (!n) return;
-  k_gen_measure<<<(unsigned)((n + 3) / 4), 256, 0, st>>>(g, n, type, card, nruns, big, small);
+  k_gen_measure<<<(unsigned)std::min<uint64_t>((n + 3) / 4, 1u << 20), 256, 0, st>>>(g, n, type, card, nruns, big, small);
 }
 void launch_gen_emit(const GenSpec &g, uint64_t n, const uint8_t *type, const uint64_t *off, uint8_t *payload,
                      hipStream_t st) {
   if (!n) return;
-  k_gen_emit<<<(unsigned)((n + 3) / 4), 256, 0, st>>>(g, n, type, off, payload);
+  k_gen_emit<<<(unsigned)std::min<uint64_t>((n + 3) / 4, 1u << 20), 256, 0, st>>>(g, n, type, off, payload);
 }
 
 } // namespace rbg

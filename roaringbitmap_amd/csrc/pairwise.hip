@@ -1,3 +1,4 @@
+#include <algorithm>
 // pairwise.hip — batched static RoaringBitmap.and/or/xor/andNot on MI355X.
 //
 // Pipeline (one HIP stream):
@@ -693,8 +694,12 @@ static void launch_op(bool card_only, const uint8_t *pa, const uint8_t *pb, cons
   else launch_tasks<OP, false, kRoleHeavy>(pa, pb, heavy, nh, out, tm, st);
 #else
   if (nh) {
-    if (card_only) k_pair_heavy_np<OP, true><<<blocks_for(nh, 4), 256, 0, st>>>(pa, pb, heavy, nh, out, tm);
-    else k_pair_heavy_np<OP, false><<<blocks_for(nh, 4), 256, 0, st>>>(pa, pb, heavy, nh, out, tm);
+    // one wave per task: at most 2^32 / 64 tasks per launch
+    for (uint64_t t0 = 0; t0 < nh; t0 += (1ull << 26)) {
+      const uint64_t nt = std::min<uint64_t>(nh - t0, 1ull << 26);
+      if (card_only) k_pair_heavy_np<OP, true><<<blocks_for(nt, 4), 256, 0, st>>>(pa, pb, heavy + t0, nt, out, tm);
+      else k_pair_heavy_np<OP, false><<<blocks_for(nt, 4), 256, 0, st>>>(pa, pb, heavy + t0, nt, out, tm);
+    }
   }
 #endif
 }

@@ -22,14 +22,14 @@ void launch_bitmap_cards(const SetView &s, uint32_t nbitmaps, uint64_t *out, hip
 // Copy n payloads (sizes multiple of 16 after rounding) from src offsets to dst offsets.
 __global__ __launch_bounds__(256) void k_gather(const uint8_t *src, const uint64_t *soff, const uint64_t *bytes,
                                                 uint8_t *dst, const uint64_t *doff, uint64_t n) {
-  const uint64_t i = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (i >= n) return;
-  copy_payload(src + soff[i], dst + doff[i], bytes[i], lane_id());
+  // grid-stride (a launch may not exceed 2^32 work-items per dimension)
+  for (uint64_t i = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); i < n; i += (uint64_t)gridDim.x * 4)
+    copy_payload(src + soff[i], dst + doff[i], bytes[i], lane_id());
 }
 void launch_gather(const uint8_t *src, const uint64_t *soff, const uint64_t *bytes, uint8_t *dst,
                    const uint64_t *doff, uint64_t n, hipStream_t st) {
   if (!n) return;
-  k_gather<<<(unsigned)((n + 3) / 4), 256, 0, st>>>(src, soff, bytes, dst, doff, n);
+  k_gather<<<(unsigned)(n < (4ull << 20) ? (n + 3) / 4 : (1u << 20)), 256, 0, st>>>(src, soff, bytes, dst, doff, n);
 }
 
 // Payload layout of generated / uploaded sets: Bitmaps first at 8 KiB strides, then the rest.

@@ -62,6 +62,34 @@ __global__ __launch_bounds__(256) void k_wide_bounds(const uint16_t *sorted, uin
   seg[k] = lo;
 }
 
+// Chunked grouping (rocPRIM's radix sort is run on member-aligned chunks of <= kSortChunk items):
+// pre[c][k] = (global start of key k) + (items of key k in chunks < c) - (chunk c's first index
+// of key k) - (chunk c's start), so sorted element p of chunk c lands at pre[c][key] + p.
+constexpr uint64_t kSortChunk = 1ull << 27;
+__global__ __launch_bounds__(256) void k_wide_chunk_pre(const uint64_t *cseg, uint32_t nchunks, const uint64_t *cstart,
+                                                        uint64_t *seg, uint64_t *pre) {
+  const uint32_t k = blockIdx.x * 256 + threadIdx.x;
+  if (k > 65536) return;
+  // seg[k] = sum over chunks of the items with keys < k
+  uint64_t before = 0;
+  for (uint32_t c = 0; c < nchunks; ++c) before += cseg[(uint64_t)c * 65537 + k];
+  seg[k] = before;
+  if (k == 65536) return;
+  uint64_t run = before;
+  for (uint32_t c = 0; c < nchunks; ++c) {
+    const uint64_t lo = cseg[(uint64_t)c * 65537 + k], hi = cseg[(uint64_t)c * 65537 + k + 1];
+    pre[(uint64_t)c * 65536 + k] = run - lo - cstart[c];
+    run += hi - lo;
+  }
+}
+__global__ __launch_bounds__(256) void k_wide_chunk_scatter(const uint16_t *keys, const uint32_t *cid, uint64_t n,
+                                                            uint64_t cs, const uint64_t *pre_c, uint32_t *out) {
+  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t p = cs + i;
+  out[pre_c[keys[p]] + p] = cid[p];
+}
+
 // active[k] = 1 when key k (inside the shard's [lo, hi)) produces work: any container, or (AND
 // semantics) one per member
 __global__ __launch_bounds__(256) void k_wide_select(const uint64_t *seg, uint64_t need, uint32_t lo, uint32_t hi,
@@ -391,8 +419,25 @@ int wide_run(rbgpu_ctx *ctx, int sem, const rbgpu_set *in, const std::vector<uin
   void *d_sort = nullptr;
   size_t sort_bytes = 0;
   const uint64_t N1 = std::max<uint64_t>(N, 1);
+  // member-aligned sort chunks (a member's containers never straddle two chunks); RBGPU_SORT_CHUNK
+  // lowers the chunk size so the tests exercise the stitched path at small sizes
+  uint64_t sort_chunk = kSortChunk;
+  if (const char *e = getenv("RBGPU_SORT_CHUNK")) sort_chunk = std::max<uint64_t>(1, strtoull(e, nullptr, 10));
+  std::vector<uint64_t> cstart{0};
+  for (uint32_t i = 0; i < M; ++i)
+    if (mstart[i + 1] - cstart.back() > sort_chunk && mstart[i] > cstart.back()) cstart.push_back(mstart[i]);
+  cstart.push_back(N);
+  const uint32_t nchunks = (uint32_t)cstart.size() - 1;
+  uint64_t max_chunk = 1;
+  for (uint32_t c = 0; c < nchunks; ++c) max_chunk = std::max(max_chunk, cstart[c + 1] - cstart[c]);
   (void)rocprim::radix_sort_pairs(nullptr, sort_bytes, (const uint16_t *)nullptr, (uint16_t *)nullptr,
-                                  (const uint32_t *)nullptr, (uint32_t *)nullptr, (size_t)N1, 0, 16, st);
+                                  (const uint32_t *)nullptr, (uint32_t *)nullptr, (size_t)max_chunk, 0, 16, st);
+  uint64_t *d_cseg = nullptr, *d_pre = nullptr, *d_cstart = nullptr;
+  uint32_t *d_cid3 = nullptr;
+  if (nchunks > 1 &&
+      (pool.alloc((void **)&d_cseg, nchunks * 65537ull * 8) || pool.alloc((void **)&d_pre, nchunks * 65536ull * 8) ||
+       pool.alloc((void **)&d_cstart, (nchunks + 1) * 8ull) || pool.alloc((void **)&d_cid3, N1 * 4)))
+    return fail(RB_ENOMEM, "wide chunk tables (%llu containers)", (unsigned long long)N);
   const uint64_t tmpw = std::max<uint64_t>(scan_tmp_words(65537), 1);
   if (pool.alloc((void **)&d_mem, std::max<uint32_t>(M, 1) * 4ull) ||
       pool.alloc((void **)&d_mstart, (M + 1) * 8ull) || pool.alloc((void **)&d_keys, N1 * 2) ||
@@ -404,7 +449,8 @@ int wide_run(rbgpu_ctx *ctx, int sem, const rbgpu_set *in, const std::vector<uin
     return fail(RB_ENOMEM, "wide workspace (%llu containers)", (unsigned long long)N);
   auto release = [&]() {
     for (void *p : {(void *)d_mem, (void *)d_mstart, (void *)d_keys, (void *)d_keys2, (void *)d_cid, (void *)d_cid2,
-                    d_sort, (void *)d_seg, (void *)d_active, (void *)d_apos, (void *)d_klist, (void *)d_tmp})
+                    d_sort, (void *)d_seg, (void *)d_active, (void *)d_apos, (void *)d_klist, (void *)d_tmp,
+                    (void *)d_cseg, (void *)d_pre, (void *)d_cstart, (void *)d_cid3})
       pool.release(p);
   };
   if (M) {
@@ -414,13 +460,30 @@ int wide_run(rbgpu_ctx *ctx, int sem, const rbgpu_set *in, const std::vector<uin
   const SetView sv = in->view();
   if (N) {
     k_wide_flatten<<<nblk(N, 256), 256, 0, st>>>(sv, d_mem, d_mstart, M, N, d_keys, d_cid);
-    size_t sb = sort_bytes;
-    if (rocprim::radix_sort_pairs(d_sort, sb, d_keys, d_keys2, d_cid, d_cid2, (size_t)N, 0, 16, st) != hipSuccess) {
-      release();
-      return fail(RB_EDEVICE, "radix sort failed");
+    for (uint32_t c = 0; c < nchunks; ++c) {
+      const uint64_t cs = cstart[c], cn = cstart[c + 1] - cs;
+      size_t sb = sort_bytes;
+      const hipError_t e = rocprim::radix_sort_pairs(d_sort, sb, d_keys + cs, d_keys2 + cs, d_cid + cs, d_cid2 + cs,
+                                                     (size_t)cn, 0, 16, st);
+      if (e != hipSuccess) {
+        release();
+        return fail(RB_EDEVICE, "radix sort failed (chunk of %llu containers): %s", (unsigned long long)cn,
+                    hipGetErrorString(e));
+      }
+      if (nchunks > 1) k_wide_bounds<<<nblk(65537, 256), 256, 0, st>>>(d_keys2 + cs, cn, d_cseg + (uint64_t)c * 65537);
     }
   }
-  k_wide_bounds<<<nblk(65537, 256), 256, 0, st>>>(d_keys2, N, d_seg);
+  if (nchunks > 1) {
+    // stitch the stably sorted chunks into one key-grouped list, member order kept within a key
+    HIPCHK(hipMemcpyAsync(d_cstart, cstart.data(), (nchunks + 1) * 8ull, hipMemcpyHostToDevice, st));
+    k_wide_chunk_pre<<<nblk(65537, 256), 256, 0, st>>>(d_cseg, nchunks, d_cstart, d_seg, d_pre);
+    for (uint32_t c = 0; c < nchunks; ++c)
+      k_wide_chunk_scatter<<<nblk(cstart[c + 1] - cstart[c], 256), 256, 0, st>>>(
+          d_keys2, d_cid2, cstart[c + 1] - cstart[c], cstart[c], d_pre + (uint64_t)c * 65536, d_cid3);
+    std::swap(d_cid2, d_cid3);
+  } else {
+    k_wide_bounds<<<nblk(65537, 256), 256, 0, st>>>(d_keys2, N, d_seg);
+  }
   k_wide_select<<<nblk(65536, 256), 256, 0, st>>>(d_seg, and_sem ? (uint64_t)M : 0, key_lo, key_hi, d_active);
   scan_exclusive(d_active, d_apos, 65536, d_tmp, st);
   k_wide_list<<<nblk(65536, 256), 256, 0, st>>>(d_active, d_apos, d_klist);

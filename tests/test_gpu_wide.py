@@ -183,3 +183,21 @@ def test_run_fastpath_mixed_keys_fall_back(ctx, oracle):
         for sem in ("FAST_OR", "FAST_AND", "WORKSHY_AND", "FAST_XOR"):
             want = oracle.wide(getattr(oracle, sem), [refs[m] for m in members]).serialize()
             assert ctx.wide(getattr(rb, sem), s, members).serialize()[0] == want, (sem, n)
+
+
+def test_chunked_grouping_stitches_in_member_order(ctx, oracle):
+    """Large inputs are grouped by key in member-aligned chunks (rocPRIM radix sort per chunk, then a
+    stitch); with a tiny chunk size every semantics must still match the oracle byte for byte."""
+    import os
+
+    import roaringbitmap_amd as rb
+    a, _ = ctx.generate(rb.WL_WIDE_MIXED, 20, seed=13)
+    refs = [oracle.RefBitmap.deserialize(b) for b in a.serialize()]
+    members = np.arange(20, dtype=np.uint32)
+    wants = {sem: oracle.wide(getattr(oracle, sem), [refs[m] for m in members]).serialize() for sem in SEMS}
+    os.environ["RBGPU_SORT_CHUNK"] = "9000"
+    try:
+        for sem in SEMS:
+            assert ctx.wide(getattr(rb, sem), a, members).serialize()[0] == wants[sem], sem
+    finally:
+        del os.environ["RBGPU_SORT_CHUNK"]
