@@ -109,6 +109,12 @@ int rbgpu_get_stats(rbgpu_ctx *ctx, rb_stats *out);
 /* RoaringBitmap.deserialize(ByteBuffer) for n bitmaps — RoaringArray.java:547-629 */
 int rbgpu_set_from_serialized(rbgpu_ctx *ctx, const uint8_t *const *bufs, const uint64_t *lens,
                               uint32_t n, rbgpu_set **out);
+/* The same for serialized bytes already in device memory (e.g. read from storage straight into HBM):
+ * bitmap i is d_bytes[offsets[i], offsets[i+1]) with offsets[n+1] on the host; d_bytes must be
+ * readable up to offsets[n] rounded up to 4.  Parsed and validated on the GPU (codec.hip) with the
+ * same results and error codes as rbgpu_set_from_serialized. */
+int rbgpu_set_from_serialized_device(rbgpu_ctx *ctx, const uint8_t *d_bytes, const uint64_t *offsets,
+                                     uint32_t n, rbgpu_set **out);
 /* Upload a host SoA batch (validated like deserialize). */
 int rbgpu_set_from_soa(rbgpu_ctx *ctx, const rb_soa *soa, rbgpu_set **out);
 void rbgpu_set_free(rbgpu_set *set);
@@ -122,6 +128,9 @@ int rbgpu_set_serialized_sizes(const rbgpu_set *set, uint64_t *out /* [n_bitmaps
  * offsets[count+1] receives each bitmap's start — RoaringArray.java:851-940 */
 int rbgpu_set_serialize(const rbgpu_set *set, uint32_t first, uint32_t count, uint8_t *dst,
                         uint64_t cap, uint64_t *offsets);
+/* rbgpu_set_serialize into device memory d_dst (cap bytes); offsets[count+1] on the host. */
+int rbgpu_set_serialize_device(const rbgpu_set *set, uint32_t first, uint32_t count, uint8_t *d_dst,
+                               uint64_t cap, uint64_t *offsets);
 /* Per-bitmap summary: what a RoaringFormatSpec header over a sharded result needs
  * (RoaringBitmap.getCardinality, RoaringArray.size / hasRunContainer / serializedSizeInBytes,
  * RoaringArray.java:851-953). */

@@ -70,6 +70,7 @@ SIGNATURES = {
     "rbgpu_synchronize": (C.c_int, [_P]),
     "rbgpu_get_stats": (C.c_int, [_P, C.POINTER(RbStats)]),
     "rbgpu_set_from_serialized": (C.c_int, [_P, C.POINTER(C.c_char_p), _U64P, C.c_uint32, C.POINTER(_P)]),
+    "rbgpu_set_from_serialized_device": (C.c_int, [_P, C.c_void_p, _U64P, C.c_uint32, C.POINTER(_P)]),
     "rbgpu_set_from_soa": (C.c_int, [_P, C.POINTER(RbSoa), C.POINTER(_P)]),
     "rbgpu_set_free": (None, [_P]),
     "rbgpu_set_bitmap_count": (C.c_uint32, [_P]),
@@ -77,6 +78,7 @@ SIGNATURES = {
     "rbgpu_set_cardinalities": (C.c_int, [_P, _U64P]),
     "rbgpu_set_serialized_sizes": (C.c_int, [_P, _U64P]),
     "rbgpu_set_serialize": (C.c_int, [_P, C.c_uint32, C.c_uint32, C.c_void_p, C.c_uint64, _U64P]),
+    "rbgpu_set_serialize_device": (C.c_int, [_P, C.c_uint32, C.c_uint32, C.c_void_p, C.c_uint64, _U64P]),
     "rbgpu_set_download": (C.c_int, [_P, C.c_uint32, C.c_uint32, C.POINTER(RbSoa)]),
     "rbgpu_pairwise": (C.c_int, [_P, C.c_int, _P, _P, _U32P, _U32P, C.c_uint32, C.POINTER(_P)]),
     "rbgpu_pairwise_cardinality": (C.c_int, [_P, C.c_int, _P, _P, _U32P, _U32P, C.c_uint32, _U64P]),

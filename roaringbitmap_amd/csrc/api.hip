@@ -3,6 +3,7 @@
 #include <algorithm>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -284,18 +285,80 @@ int rbgpu_get_stats(rbgpu_ctx *ctx, rb_stats *out) {
   return RB_OK;
 }
 
+// RBGPU_HOST_CODEC=1 selects the host parser / writer (format.cpp) instead of codec.hip — an A/B
+// switch for tests; both give identical sets, bytes and error codes.
+static bool host_codec() {
+  const char *e = std::getenv("RBGPU_HOST_CODEC");
+  return e && e[0] == '1';
+}
+
 int rbgpu_set_from_serialized(rbgpu_ctx *ctx, const uint8_t *const *bufs, const uint64_t *lens, uint32_t n,
                               rbgpu_set **out) {
   int rc = check_ctx(ctx);
   if (rc) return rc;
   if (!out || (n && (!bufs || !lens))) return fail(RB_EINVAL, "null argument");
-  HostSoA h;
-  std::string err;
-  for (uint32_t i = 0; i < n; ++i) {
-    rc = parse_serialized(bufs[i], lens[i], h, err);
-    if (rc) return fail(rc, "bitmap %u: %s", i, err.c_str());
+  if (host_codec()) {
+    HostSoA h;
+    std::string err;
+    for (uint32_t i = 0; i < n; ++i) {
+      rc = parse_serialized(bufs[i], lens[i], h, err);
+      if (rc) return fail(rc, "bitmap %u: %s", i, err.c_str());
+    }
+    return upload_host(ctx, h, out);
   }
-  return upload_host(ctx, h, out);
+  // one host-to-device copy of the concatenated bytes, parsed on the GPU
+  std::vector<uint64_t> off(n + 1ull, 0);
+  for (uint32_t i = 0; i < n; ++i) off[i + 1] = off[i] + lens[i];
+  const uint64_t total = off[n];
+  uint8_t *pin = nullptr, *d_in = nullptr;
+  uint64_t *d_off = nullptr;
+  DevPool &pool = ctx->pool;
+  if (hipHostMalloc((void **)&pin, std::max<uint64_t>(total, 4) + 8 * (n + 1ull)) != hipSuccess)
+    return fail(RB_ENOMEM, "pinned staging of %llu bytes", (unsigned long long)total);
+  for (uint32_t i = 0; i < n; ++i)
+    if (lens[i]) std::memcpy(pin + off[i], bufs[i], lens[i]);
+  uint8_t *pin_off = pin + std::max<uint64_t>(total, 4);
+  std::memcpy(pin_off, off.data(), 8 * (n + 1ull));
+  if (pool.alloc((void **)&d_in, ((total + 3) & ~3ull) + 4) || pool.alloc((void **)&d_off, 8 * (n + 1ull))) {
+    (void)hipHostFree(pin);
+    pool.release(d_in);
+    return fail(RB_ENOMEM, "device staging of %llu bytes", (unsigned long long)total);
+  }
+  hipStream_t st = ctx->stream;
+  if ((total && hipMemcpyAsync(d_in, pin, total, hipMemcpyHostToDevice, st)) ||
+      hipMemcpyAsync(d_off, pin_off, 8 * (n + 1ull), hipMemcpyHostToDevice, st)) {
+    (void)hipStreamSynchronize(st);
+    (void)hipHostFree(pin);
+    pool.release(d_in);
+    pool.release(d_off);
+    return fail(RB_EDEVICE, "host-to-device copy failed");
+  }
+  rc = deserialize_device(ctx, d_in, total, d_off, n, out);
+  (void)hipStreamSynchronize(st);
+  (void)hipHostFree(pin);
+  pool.release(d_in);
+  pool.release(d_off);
+  return rc;
+}
+
+int rbgpu_set_from_serialized_device(rbgpu_ctx *ctx, const uint8_t *d_bytes, const uint64_t *offsets, uint32_t n,
+                                     rbgpu_set **out) {
+  int rc = check_ctx(ctx);
+  if (rc) return rc;
+  if (!out || !offsets || (n && !d_bytes)) return fail(RB_EINVAL, "null argument");
+  for (uint32_t i = 0; i < n; ++i)
+    if (offsets[i + 1] < offsets[i]) return fail(RB_EINVAL, "offsets not monotone at %u", i);
+  uint64_t *d_off = nullptr;
+  if (ctx->pool.alloc((void **)&d_off, 8 * (n + 1ull))) return fail(RB_ENOMEM, "offsets");
+  hipStream_t st = ctx->stream;
+  if (hipMemcpyAsync(d_off, offsets, 8 * (n + 1ull), hipMemcpyHostToDevice, st)) {
+    ctx->pool.release(d_off);
+    return fail(RB_EDEVICE, "host-to-device copy failed");
+  }
+  rc = deserialize_device(ctx, d_bytes, offsets[n], d_off, n, out);
+  (void)hipStreamSynchronize(st);
+  ctx->pool.release(d_off);
+  return rc;
 }
 
 int rbgpu_set_from_soa(rbgpu_ctx *ctx, const rb_soa *soa, rbgpu_set **out) {
@@ -463,8 +526,11 @@ int rbgpu_set_serialize(const rbgpu_set *s, uint32_t first, uint32_t count, uint
                         uint64_t *offsets) {
   if (!s || (count && !dst)) return fail(RB_EINVAL, "null argument");
   if ((uint64_t)first + count > s->nb) return fail(RB_EINVAL, "bitmap range out of bounds");
+  int rc = check_ctx(s->ctx);
+  if (rc) return rc;
+  if (!host_codec()) return serialize_device(s, first, count, dst, cap, offsets, true);
   HostSoA h;
-  int rc = download_host(s, first, count, h);
+  rc = download_host(s, first, count, h);
   if (rc) return rc;
   uint64_t pos = 0;
   for (uint32_t b = 0; b < count; ++b) {
@@ -476,6 +542,15 @@ int rbgpu_set_serialize(const rbgpu_set *s, uint32_t first, uint32_t count, uint
   }
   if (offsets) offsets[count] = pos;
   return RB_OK;
+}
+
+int rbgpu_set_serialize_device(const rbgpu_set *s, uint32_t first, uint32_t count, uint8_t *d_dst, uint64_t cap,
+                               uint64_t *offsets) {
+  if (!s || (count && !d_dst)) return fail(RB_EINVAL, "null argument");
+  if ((uint64_t)first + count > s->nb) return fail(RB_EINVAL, "bitmap range out of bounds");
+  int rc = check_ctx(s->ctx);
+  if (rc) return rc;
+  return serialize_device(s, first, count, d_dst, cap, offsets, false);
 }
 
 // ---------------------------------------------------------------- pairwise

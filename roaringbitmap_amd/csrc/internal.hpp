@@ -140,6 +140,12 @@ int compact_keyed(rbgpu_ctx *ctx, const uint32_t *d_klist, uint32_t nk, const Wi
 // bsi.hip: op = BitmapSliceIndex.Operation ordinal (EQ, NEQ, LE, LT, GE, GT, RANGE)
 int bsi_compare(rbgpu_ctx *ctx, const rbgpu_set *bsi, int op, uint64_t start, uint64_t end, uint64_t vmin,
                 uint64_t vmax, const rbgpu_set *found, rbgpu_set **out);
+// codec.hip: RoaringFormatSpec on the device.  d_in is readable up to in_lim; d_in_off[n + 1] (device).
+int deserialize_device(rbgpu_ctx *ctx, const uint8_t *d_in, uint64_t in_lim, const uint64_t *d_in_off, uint32_t n,
+                       rbgpu_set **out);
+// host_dst: dst is host memory (staged through the device); offsets[count + 1] on the host
+int serialize_device(const rbgpu_set *s, uint32_t first, uint32_t count, uint8_t *dst, uint64_t cap,
+                     uint64_t *offsets, bool host_dst);
 void set_mix(const int *m);
 int generate_bsi(rbgpu_ctx *ctx, uint32_t nslices, uint64_t nrows, uint64_t seed, rbgpu_set **out);
 // generate.hip

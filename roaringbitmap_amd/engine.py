@@ -246,6 +246,15 @@ class DeviceSet:
         raw = buf.raw
         return [raw[int(offs[i]):int(offs[i + 1])] for i in range(count)]
 
+    def serialize_device(self, dst_ptr: int, cap: int, first: int = 0, count: Optional[int] = None) -> np.ndarray:
+        """RoaringFormatSpec bytes of bitmaps [first, first+count) written by the GPU into device memory
+        at dst_ptr (rbgpu_set_serialize_device); returns the count+1 byte offsets."""
+        count = len(self) - first if count is None else count
+        offs = np.zeros(count + 1, np.uint64)
+        L.check(L.lib().rbgpu_set_serialize_device(self.h, first, count, C.c_void_p(dst_ptr), cap,
+                                                    offs.ctypes.data_as(L._U64P)))
+        return offs
+
     def download(self, first: int = 0, count: Optional[int] = None) -> HostSoA:
         count = len(self) - first if count is None else count
         q = L.RbSoa()
@@ -314,6 +323,15 @@ class Context:
         lens = np.array([len(b) for b in blobs] or [0], np.uint64)
         out = C.c_void_p()
         L.check(L.lib().rbgpu_set_from_serialized(self.h, arr, lens.ctypes.data_as(L._U64P), n, C.byref(out)))
+        return DeviceSet(self, out.value)
+
+    def upload_serialized_device(self, src_ptr: int, offsets: np.ndarray) -> DeviceSet:
+        """Bitmaps already serialized in device memory at src_ptr, bitmap i at [offsets[i], offsets[i+1])
+        (rbgpu_set_from_serialized_device): parsed and validated on the GPU."""
+        offs = np.ascontiguousarray(offsets, np.uint64)
+        out = C.c_void_p()
+        L.check(L.lib().rbgpu_set_from_serialized_device(self.h, C.c_void_p(src_ptr), offs.ctypes.data_as(L._U64P),
+                                                          len(offs) - 1, C.byref(out)))
         return DeviceSet(self, out.value)
 
     def upload_soa(self, soa: HostSoA) -> DeviceSet:
