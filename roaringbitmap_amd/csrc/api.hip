@@ -68,6 +68,7 @@ void ctx_unref(rbgpu_ctx *ctx) {
   (void)hipFree(ctx->d_stats);
   (void)hipHostFree(ctx->h_pinned);
   (void)hipHostFree(ctx->h_stats);
+  if (ctx->h_stage) (void)hipHostFree(ctx->h_stage);
   ctx->pool.clear();
   ctx->ws_pairs.destroy();
   ctx->ws_tasks.destroy();
@@ -554,6 +555,15 @@ int rbgpu_set_serialize_device(const rbgpu_set *s, uint32_t first, uint32_t coun
 }
 
 // ---------------------------------------------------------------- pairwise
+// Merge-path segment length: 256 merged keys per thread for large batches; shorter when the batch's
+// expected key count would leave fewer than ~128K walking threads (the walk is latency-bound).
+static uint32_t pairwise_seg_keys(const rbgpu_set *a, const rbgpu_set *b, uint64_t np) {
+  const double per = (double)a->nc / std::max<uint32_t>(a->nb, 1) + (double)b->nc / std::max<uint32_t>(b->nb, 1);
+  const double est = per * (double)np;
+  uint32_t seg = 256;
+  while (seg > 8 && est / seg < 131072.0) seg >>= 1;
+  return seg;
+}
 // probe: 0 = the product path; 1 / 2 = measurement probes (rbgpu_internal_probe) in place of the
 // task kernel — results are not produced.
 static int pairwise_impl(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu_set *b, const uint32_t *a_idx,
@@ -582,12 +592,30 @@ static int pairwise_impl(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu
   uint64_t *nseg_p = W.take<uint64_t>(np + 1), *seg_begin = W.take<uint64_t>(np + 1);
   uint64_t *pcard = W.take<uint64_t>(np + 1);
   uint64_t *ptmp = W.take<uint64_t>(std::max<uint64_t>(scan_tmp_words(np + 1), 1));
-  if (d_aidx) HIPCHK(hipMemcpyAsync(d_aidx, a_idx, np * 4, hipMemcpyHostToDevice, st));
-  if (d_bidx) HIPCHK(hipMemcpyAsync(d_bidx, b_idx, np * 4, hipMemcpyHostToDevice, st));
+  if (d_aidx || d_bidx) { // through pinned staging: a pageable copy would block the host
+    const size_t bytes = np * 4 * ((d_aidx != nullptr) + (d_bidx != nullptr));
+    if (bytes > ctx->h_stage_cap) {
+      if (ctx->h_stage) (void)hipHostFree(ctx->h_stage);
+      ctx->h_stage = nullptr;
+      ctx->h_stage_cap = 0;
+      if (hipHostMalloc((void **)&ctx->h_stage, bytes) != hipSuccess) return fail(RB_ENOMEM, "pinned staging");
+      ctx->h_stage_cap = bytes;
+    }
+    uint8_t *h = ctx->h_stage;
+    if (d_aidx) {
+      std::memcpy(h, a_idx, np * 4);
+      HIPCHK(hipMemcpyAsync(d_aidx, h, np * 4, hipMemcpyHostToDevice, st));
+      h += np * 4;
+    }
+    if (d_bidx) {
+      std::memcpy(h, b_idx, np * 4);
+      HIPCHK(hipMemcpyAsync(d_bidx, h, np * 4, hipMemcpyHostToDevice, st));
+    }
+  }
   if (card_out && np) HIPCHK(hipMemsetAsync(pcard, 0, np * 8, st));
 
   stats_begin(ctx);
-  PairArgs pa{op, a->view(), b->view(), d_aidx, d_bidx, npairs, seg_begin, nullptr, 0};
+  PairArgs pa{op, a->view(), b->view(), d_aidx, d_bidx, npairs, seg_begin, nullptr, 0, pairwise_seg_keys(a, b, np)};
   launch_seg_count(pa, nseg_p, st);
   scan_exclusive(nseg_p, seg_begin, np, ptmp, st);
   uint64_t *const tot = ctx->h_pinned;
@@ -595,7 +623,7 @@ static int pairwise_impl(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu
   HIPCHK(hipStreamSynchronize(st));
   const uint64_t ns = np ? tot[6] : 0;
   // ---- per segment: counts, scans, result counts / offsets
-  need = aligned256(ns * 4) + 10 * aligned256((ns + 1) * 8) + aligned256(scan_tmp_words(ns + 1) * 8);
+  need = aligned256(ns * 4) + 10 * aligned256((ns + 1) * 8) + aligned256(scan_tmp_words(ns + 1) * 8) + 256;
   if (ctx->ws_segs.reserve(need, st) != hipSuccess) return fail(RB_ENOMEM, "segment workspace");
   Workspace &G = ctx->ws_segs;
   uint32_t *seg_pair = G.take<uint32_t>(std::max<uint64_t>(ns, 1));
@@ -605,18 +633,15 @@ static int pairwise_impl(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu
                       G.take<uint64_t>(ns + 1)};
   uint64_t *rcnt = G.take<uint64_t>(ns + 1), *rseg = G.take<uint64_t>(ns + 1);
   uint64_t *tmp = G.take<uint64_t>(std::max<uint64_t>(scan_tmp_words(ns + 1), 1));
+  uint64_t *d_tot = G.take<uint64_t>(4);
   launch_seg_fill(pa, seg_begin, seg_pair, st);
   pa.seg_pair = seg_pair;
   pa.nseg = ns;
   launch_pair_count(pa, cnt, ctx->d_stats, st);
-  scan_exclusive(cnt.task, scn.task, ns, tmp, st);
-  scan_exclusive(cnt.light, scn.light, ns, tmp, st);
-  scan_exclusive(cnt.big, scn.big, ns, tmp, st);
-  scan_exclusive(cnt.small, scn.small, ns, tmp, st);
-  HIPCHK(hipMemcpyAsync(tot + 0, scn.task + ns, 8, hipMemcpyDeviceToHost, st));
-  HIPCHK(hipMemcpyAsync(tot + 1, scn.light + ns, 8, hipMemcpyDeviceToHost, st));
-  HIPCHK(hipMemcpyAsync(tot + 2, scn.big + ns, 8, hipMemcpyDeviceToHost, st));
-  HIPCHK(hipMemcpyAsync(tot + 3, scn.small + ns, 8, hipMemcpyDeviceToHost, st));
+  const uint64_t *scan_in[4] = {cnt.task, cnt.light, cnt.big, cnt.small};
+  uint64_t *scan_out[4] = {scn.task, scn.light, scn.big, scn.small};
+  scan_exclusive_multi(scan_in, scan_out, 4, ns, tmp, d_tot, st);
+  HIPCHK(hipMemcpyAsync(tot, d_tot, 4 * 8, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
   if (!ns) tot[0] = tot[1] = tot[2] = tot[3] = 0;
   const uint64_t ntasks = tot[0], nlight = tot[1], nheavy = ntasks - nlight, nbig_t = tot[2], small_t = tot[3];

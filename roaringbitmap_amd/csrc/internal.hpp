@@ -96,6 +96,8 @@ struct rbgpu_ctx {
   uint64_t *d_stats = nullptr;  // [kStatWords * kStripes] striped algorithmic byte counters
   uint64_t *h_pinned = nullptr; // [16]
   uint64_t *h_stats = nullptr;  // [kStatWords * kStripes]
+  uint8_t *h_stage = nullptr;   // pinned staging for small host->device arguments (pair indices)
+  size_t h_stage_cap = 0;
   rb_stats last{};
   int refs = 1;                 // the handle + one per live set; destroyed at zero
   bool closed = false;

@@ -7,6 +7,9 @@ namespace rbg {
 // ---- scan.hip
 uint64_t scan_tmp_words(uint64_t n);
 void scan_exclusive(const uint64_t *in, uint64_t *out, uint64_t n, uint64_t *tmp, hipStream_t st);
+// k scans of n words each (k <= 4); totals[i] = out[i][n].  One launch when n fits one block.
+void scan_exclusive_multi(const uint64_t *const *in, uint64_t *const *out, int k, uint64_t n, uint64_t *tmp,
+                          uint64_t *totals, hipStream_t st);
 
 // ---- pairwise.hip
 struct PairArgs {
@@ -18,6 +21,7 @@ struct PairArgs {
   const uint64_t *seg_begin; // [npairs + 1] first merge-path segment of each pair
   const uint32_t *seg_pair;  // [nseg] pair of each segment
   uint64_t nseg;
+  uint32_t seg_keys; // merged keys per segment (a power of two in [8, 256])
 };
 // per task result metadata (workspace, indexed like tasks)
 struct TaskMeta {

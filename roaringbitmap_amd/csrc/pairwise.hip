@@ -62,11 +62,11 @@ __device__ __forceinline__ void stat_add(uint64_t *stats, int word, uint64_t v) 
 }
 
 // ---------------------------------------------------------------- key alignment by merge path
-// A pair is cut into segments of <= kSegKeys merged keys (merge path over the two sorted key lists,
+// A pair is cut into segments of <= a.seg_keys merged keys (merge path over the two sorted key lists,
 // A first on equal keys), one thread per segment, so a pair of large bitmaps aligns its keys in
 // parallel.  A matched key is never split: when a cut falls between A's key and its equal B
-// partner, the partner stays with A.
-constexpr uint64_t kSegKeys = 256;
+// partner, the partner stays with A.  The walk is a chain of dependent loads, so the host picks
+// shorter segments when a batch has few keys (pairwise_seg_keys) to keep enough threads walking.
 
 __device__ __forceinline__ void pair_ranges(const PairArgs &a, uint32_t p, uint64_t &i0, uint64_t &na, uint64_t &j0,
                                             uint64_t &nb) {
@@ -94,7 +94,7 @@ __global__ __launch_bounds__(kPairThreads) void k_seg_count(PairArgs a, uint64_t
   if (p >= a.npairs) return;
   uint64_t i0, na, j0, nb;
   pair_ranges(a, p, i0, na, j0, nb);
-  nseg[p] = (na + nb + kSegKeys - 1) / kSegKeys + (na + nb == 0);
+  nseg[p] = (na + nb + a.seg_keys - 1) / a.seg_keys + (na + nb == 0);
 }
 __global__ __launch_bounds__(kPairThreads) void k_seg_fill(PairArgs a, const uint64_t *seg_begin, uint32_t *seg_pair) {
   const uint32_t p = blockIdx.x * kPairThreads + threadIdx.x;
@@ -109,7 +109,7 @@ __device__ __forceinline__ void pair_walk(const PairArgs &a, uint64_t sg, PairCo
   const uint32_t p = a.seg_pair[sg];
   uint64_t i0, na, j0, nb;
   pair_ranges(a, p, i0, na, j0, nb);
-  const uint64_t d0 = (sg - a.seg_begin[p]) * kSegKeys, d1 = d0 + kSegKeys < na + nb ? d0 + kSegKeys : na + nb;
+  const uint64_t d0 = (sg - a.seg_begin[p]) * a.seg_keys, d1 = d0 + a.seg_keys < na + nb ? d0 + a.seg_keys : na + nb;
   uint64_t si0, sj0, si1, sj1;
   merge_split(a.A.key + i0, na, a.B.key + j0, nb, d0, si0, sj0);
   merge_split(a.A.key + i0, na, a.B.key + j0, nb, d1, si1, sj1);

@@ -81,4 +81,48 @@ void scan_exclusive(const uint64_t *in, uint64_t *out, uint64_t n, uint64_t *tmp
   k_scan_apply<<<(unsigned)nb, kScanThreads, 0, st>>>(in, n, poffs, out);
 }
 
+struct Multi {
+  const uint64_t *in[4];
+  uint64_t *out[4];
+};
+__global__ __launch_bounds__(kScanThreads) void k_scan_multi(Multi m, uint64_t n, uint64_t *totals) {
+  __shared__ uint64_t sh[4];
+  const uint64_t *in = m.in[blockIdx.y];
+  uint64_t *out = m.out[blockIdx.y];
+  const uint64_t base = threadIdx.x * kScanItems;
+  uint64_t v[kScanItems], s = 0;
+#pragma unroll
+  for (int i = 0; i < kScanItems; ++i) {
+    v[i] = base + i < n ? in[base + i] : 0;
+    s += v[i];
+  }
+  uint64_t total;
+  uint64_t run = block_excl_scan(s, sh, total);
+#pragma unroll
+  for (int i = 0; i < kScanItems; ++i) {
+    if (base + i < n) out[base + i] = run;
+    run += v[i];
+  }
+  if (threadIdx.x == 0) {
+    out[n] = total;
+    totals[blockIdx.y] = total;
+  }
+}
+__global__ void k_gather_totals(Multi m, uint64_t n, uint64_t *totals) { totals[threadIdx.x] = m.out[threadIdx.x][n]; }
+
+void scan_exclusive_multi(const uint64_t *const *in, uint64_t *const *out, int k, uint64_t n, uint64_t *tmp,
+                          uint64_t *totals, hipStream_t st) {
+  Multi m{};
+  for (int i = 0; i < k; ++i) {
+    m.in[i] = in[i];
+    m.out[i] = out[i];
+  }
+  if (n <= (uint64_t)kScanThreads * kScanItems) {
+    k_scan_multi<<<dim3(1, k), kScanThreads, 0, st>>>(m, n, totals);
+    return;
+  }
+  for (int i = 0; i < k; ++i) scan_exclusive(in[i], out[i], n, tmp, st);
+  k_gather_totals<<<1, k, 0, st>>>(m, n, totals);
+}
+
 } // namespace rbg
