@@ -106,28 +106,23 @@ __device__ __forceinline__ void lds_write_words(uint32_t *s, const uint64_t (&w)
                                    (uint32_t)(w[2 * k + 1] >> 32));
 }
 
-// OR one lane's chunk of sorted values (n <= 8) into the LDS bitmap, one access per 32-bit word
-// group.  Only the first and last group of a chunk can share a word with another lane's chunk (the
-// array is sorted), so those use ds_or; the groups between are owned by this lane: plain stores
-// (the image was zeroed).
+// OR one lane's chunk of sorted values (n <= 8) into the LDS bitmap: a segmented OR over runs of
+// equal word index in registers, then one ds_or per value, carrying the group's mask at the group's
+// last value and 0 elsewhere (an OR of 0 changes nothing).  No value-dependent branch: the earlier
+// form branched per value on "new word?", which cost ~16 SALU exec-mask instructions per value.
+// Values past n OR 0 into the word of the last live value.
 __device__ __forceinline__ void or_chunk_values(const uint32_t (&x)[8], int n, uint32_t *s) {
-  uint32_t cw = x[0] >> 5, acc = 0;
-  bool first = true;
+  uint32_t acc = 0, prev = x[0] >> 5;
+  const uint32_t lastw = x[n - 1 < 7 ? n - 1 : 7] >> 5;
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
-    if (i < n) {
-      const uint32_t wi = x[i] >> 5;
-      if (wi != cw) {
-        if (first) atomicOr(&s[cw], acc);
-        else s[cw] = acc;
-        first = false;
-        cw = wi;
-        acc = 0;
-      }
-      acc |= 1u << (x[i] & 31);
-    }
+    const bool live = i < n;
+    const uint32_t wi = live ? x[i] >> 5 : lastw;
+    acc = (wi == prev ? acc : 0u) | (live ? 1u << (x[i] & 31) : 0u);
+    prev = wi;
+    const bool last = i == 7 || i + 1 >= n || (x[i + 1] >> 5) != wi;
+    atomicOr(&s[wi], last ? acc : 0u);
   }
-  atomicOr(&s[cw], acc);
 }
 
 // OR the values of a sorted u16 array (payload 16-B aligned) into the LDS bitmap `s`.  Each lane
@@ -310,6 +305,24 @@ __device__ __forceinline__ int filter_chunks(const uint4 (&fq)[8], int nfc, int 
   return (int)total;
 }
 
+// ---------------------------------------------------------------- register-preloaded payloads
+// A payload of at most 8 KiB as 8 uint4 per lane: chunk c = lane + 64*i (16 bytes) in q[i].
+// Buffer loads: a 32-bit per-lane offset against a wave-uniform descriptor, and lanes past the
+// (16-B padded) payload get zeros from the range check without touching memory.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t chunk_rsrc(const uint8_t *p, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(p), (short)0, (int)((bytes + 15) & ~15u), 0x00020000);
+}
+__device__ __forceinline__ uint4 load_chunk_row(__amdgpu_buffer_rsrc_t rs, int i, int lane) {
+  typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+  const v4u v = __builtin_amdgcn_raw_buffer_load_b128(rs, (lane + 64 * i) * 16, 0, 0);
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ void load_chunks(uint4 (&q)[8], const uint8_t *p, uint32_t bytes, int lane) {
+  const __amdgpu_buffer_rsrc_t rs = chunk_rsrc(p, bytes);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) q[i] = load_chunk_row(rs, i, lane);
+}
+
 // Exclusive prefix (over lanes) and wave total of a per-lane count in [0, 16), by bit-sliced ballots
 // and mbcnt: no cross-lane data movement through LDS, no dependency chain of shuffles.
 __device__ __forceinline__ uint32_t mbcnt64(uint64_t m) {
@@ -336,13 +349,19 @@ __device__ __forceinline__ void ballot_scan4(uint32_t cnt, uint32_t &excl, uint3
 // Rejected values go to a per-lane dummy slot instead of being branched around.
 constexpr int kStageRing = 640;
 constexpr int kStageVals = kStageRing + 64;   // + one dummy slot per lane
-template <bool NEGATE>
-__device__ __forceinline__ int filter_chunks_staged(const uint4 (&fq)[8], int nfc, int nf, const uint32_t *s,
-                                                    uint16_t *ob, uint16_t *out, int lane) {
+// `reload(i)` is called once per row i as soon as fq[i] is free — right after the row's values are
+// in registers, or at the start for rows this payload does not have — so the caller can stream the
+// next task's payload into fq row by row instead of after the whole filter.
+template <bool NEGATE, class Reload>
+__device__ __forceinline__ int filter_chunks_staged(uint4 (&fq)[8], int nfc, int nf, const uint32_t *s,
+                                                    uint16_t *ob, uint16_t *out, int lane, const Reload &reload) {
   const int iters = (nfc + 63) >> 6; // wave-uniform, <= 8
   uint32_t flushed = 0, tot = 0;     // values written out / ranked so far (wave-uniform)
   uint4 *out4 = reinterpret_cast<uint4 *>(out);
   const uint4 *ob4 = reinterpret_cast<const uint4 *>(ob);
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+    if (i >= iters) reload(i);
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     if (i < iters) {
@@ -350,6 +369,7 @@ __device__ __forceinline__ int filter_chunks_staged(const uint4 (&fq)[8], int nf
       const int n = c < nfc ? min(8, nf - 8 * c) : 0;
       const uint32_t x[8] = {fq[i].x & 0xFFFF, fq[i].x >> 16, fq[i].y & 0xFFFF, fq[i].y >> 16,
                              fq[i].z & 0xFFFF, fq[i].z >> 16, fq[i].w & 0xFFFF, fq[i].w >> 16};
+      reload(i);
       // all 8 probes in flight before the first wait: one LDS round trip per row, not eight
       uint32_t m[8];
 #pragma unroll
@@ -387,20 +407,6 @@ __device__ __forceinline__ int filter_chunks_staged(const uint4 (&fq)[8], int nf
   return (int)tot;
 }
 
-// ---------------------------------------------------------------- register-preloaded payloads
-// A payload of at most 8 KiB as 8 uint4 per lane: chunk c = lane + 64*i (16 bytes) in q[i].
-__device__ __forceinline__ void load_chunks(uint4 (&q)[8], const uint8_t *p, uint32_t bytes, int lane) {
-  // Buffer loads: a 32-bit per-lane offset against a wave-uniform descriptor, and lanes past the
-  // (16-B padded) payload get zeros from the range check without touching memory.
-  const __amdgpu_buffer_rsrc_t rs =
-      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(p), (short)0, (int)((bytes + 15) & ~15u), 0x00020000);
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    typedef unsigned int v4u __attribute__((ext_vector_type(4)));
-    const v4u v = __builtin_amdgcn_raw_buffer_load_b128(rs, (lane + 64 * i) * 16, 0, 0);
-    q[i] = make_uint4(v.x, v.y, v.z, v.w);
-  }
-}
 __device__ __forceinline__ void store_chunks(const uint4 (&q)[8], uint8_t *p, uint32_t bytes, int lane) {
   uint4 *p4 = reinterpret_cast<uint4 *>(p);
   const int n = (int)((bytes + 15) >> 4);
