@@ -287,12 +287,234 @@ __global__ __launch_bounds__(256) void k_wide_runs(SetView s, const uint32_t *__
   }
 }
 
+// ---------------------------------------------------------------- workShyAnd, lane-parallel
+// AND is order-free (workShyAnd intersects whole key sets; FastAggregation.java:356-396), so the
+// containers of a key need not form one chain.  A wave takes KB consecutive keys of klist; lane
+// (kk, g) = (lane % KB, lane / KB) intersects members g, g+G, g+2G, ... (G = 64/KB) of key kk into
+// its own interval list, then the G lists of a key are intersected pairwise (log2 G levels).  With
+// KB consecutive keys per wave, the containers of one member bitmap for those keys are adjacent in
+// the SoA arrays, so each metadata load touches a few cache lines instead of 64.
+// Per-lane list: <= kAndCap intervals (start | end << 16) in LDS at L[(b*kAndCap + k)*64 + lane],
+// double-buffered (b = 0/1).  Loads run a 3-stage pipeline (cid of step t+2, metadata of t+1,
+// payload of t in flight while step t-1 computes).  A key with another container type, > 8 runs
+// or a list overflow is routed to the generic kernel (route[q] = 1): results are identical.
+constexpr int kAndCap = 16;
+struct AndMeta {
+  uint32_t typ, nr;
+  uint64_t off;
+};
+struct AndRuns {
+  uint4 r0, r1;
+};
+__device__ __forceinline__ uint32_t and_run(const AndRuns &p, int u) {
+  switch (u) {
+  case 0: return p.r0.x;
+  case 1: return p.r0.y;
+  case 2: return p.r0.z;
+  case 3: return p.r0.w;
+  case 4: return p.r1.x;
+  case 5: return p.r1.y;
+  case 6: return p.r1.z;
+  default: return p.r1.w;
+  }
+}
+__device__ __forceinline__ int and_slot(int b, int k, int lane) { return (b * kAndCap + min(k, kAndCap - 1)) * 64 + lane; }
+__device__ __forceinline__ uint32_t iv_s(uint32_t x) { return x & 0xFFFF; }
+__device__ __forceinline__ uint32_t iv_e(uint32_t x) { return x >> 16; }
+
+template <int KB>
+__global__ __launch_bounds__(256) void k_wide_runs_and(SetView s, const uint32_t *__restrict__ cid,
+                                                       const uint64_t *__restrict__ seg, const uint32_t *__restrict__ klist,
+                                                       uint32_t nk, uint8_t *__restrict__ out, WideOut wo,
+                                                       uint8_t *__restrict__ route, uint64_t *stats) {
+  constexpr int G = 64 / KB;
+  __shared__ __attribute__((aligned(16))) uint32_t lds_all[4][2 * kAndCap * 64];
+  const int lane = lane_id();
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t q0 = (blockIdx.x * 4 + wv) * KB;
+  if (q0 >= nk) return;
+  uint32_t *L = lds_all[wv];
+  const int kk = lane % KB, g = lane / KB;
+  const uint32_t q = q0 + kk;
+  uint64_t lo = 0, n = 0;
+  if (q < nk) {
+    const uint32_t key = klist[q];
+    lo = seg[key];
+    n = seg[key + 1] - lo;
+  }
+  const uint32_t cnt = n > (uint64_t)g ? (uint32_t)((n - g + G - 1) / G) : 0u; // this lane's members
+  const uint32_t tmax = __builtin_amdgcn_readfirstlane(wave_max_u32(cnt));
+  // the AND identity: one interval [0, 65535]
+  int cur = 0, na = 1;
+  L[and_slot(0, 0, lane)] = 0xFFFF0000u;
+  bool bad = false;
+  uint64_t inb = 0;
+  auto ld_cid = [&](uint32_t t) -> uint32_t { return t < cnt ? cid[lo + g + (uint64_t)G * t] : 0u; };
+  auto ld_meta = [&](uint32_t t, uint32_t c) -> AndMeta {
+    AndMeta m{kRun, 0, 0};
+    if (t < cnt) {
+      m.typ = s.type[c];
+      m.nr = s.nruns[c];
+      m.off = s.off[c];
+    }
+    return m;
+  };
+  auto ld_runs = [&](uint32_t t, const AndMeta &m) -> AndRuns {
+    AndRuns p{make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0)};
+    if (t < cnt && m.typ == kRun && m.nr <= (uint32_t)kMaxRunsFast) {
+      const uint4 *pp = reinterpret_cast<const uint4 *>(s.payload + m.off);
+      p.r0 = pp[0];
+      if (m.nr > 4) p.r1 = pp[1];
+    }
+    return p;
+  };
+  // pipeline prologue: payload(0), meta(1), cid(2) in flight at the top of step 0
+  AndMeta m0 = ld_meta(0, ld_cid(0));
+  uint32_t c1 = ld_cid(1);
+  AndRuns p0 = ld_runs(0, m0);
+  AndMeta m1 = ld_meta(1, c1);
+  uint32_t c2 = ld_cid(2);
+  for (uint32_t t = 0; t < tmax; ++t) {
+    const AndMeta mt = m0;
+    const AndRuns pt = p0;
+    __builtin_amdgcn_sched_barrier(0);
+    p0 = ld_runs(t + 1, m1);
+    m0 = m1;
+    m1 = ld_meta(t + 2, c2);
+    c2 = ld_cid(t + 3);
+    if (t < cnt && !bad) {
+      if (mt.typ != kRun || mt.nr > (uint32_t)kMaxRunsFast) {
+        bad = true;
+      } else {
+        inb += 4ull * mt.nr + 2 + 16;
+        const int nx = cur ^ 1;
+        int i = 0, k = 0;
+        uint32_t x = L[and_slot(cur, 0, lane)];
+#pragma unroll
+        for (int u = 0; u < kMaxRunsFast; ++u) {
+          if (u < (int)mt.nr && i < na) {
+            const uint32_t w = and_run(pt, u);
+            const uint32_t rs = w & 0xFFFF, re = rs + (w >> 16);
+            while (i < na && iv_e(x) < rs) x = L[and_slot(cur, ++i, lane)];
+            while (i < na && iv_s(x) <= re) {
+              const uint32_t a = max(iv_s(x), rs), b = min(iv_e(x), re);
+              if (k < kAndCap) L[and_slot(nx, k, lane)] = a | (b << 16);
+              ++k;
+              if (iv_e(x) > re) break;
+              x = L[and_slot(cur, ++i, lane)];
+            }
+          }
+        }
+        if (k > kAndCap) bad = true;
+        na = k;
+        cur = nx;
+      }
+    }
+    // every lane's list empty (or routed): the remaining containers change nothing
+    if ((t & 15) == 15 && !__ballot(t + 1 < cnt && !bad && na > 0)) break;
+  }
+  // ---- intersect the G lists of each key pairwise
+#pragma unroll
+  for (int d = 1; d < G; d *= 2) {
+    wave_lds_sync();
+    const int pl = lane + KB * d;                 // partner lane (same key, group g + d)
+    const int pcur = __shfl(cur, pl & 63), pna = __shfl(na, pl & 63);
+    const bool pbad = __shfl((int)bad, pl & 63) != 0;
+    if (g % (2 * d) == 0) {
+      bad = bad || pbad;
+      const int nx = cur ^ 1;
+      int i = 0, j = 0, k = 0;
+      uint32_t x = L[and_slot(cur, 0, lane)], y = L[(pcur * kAndCap) * 64 + (pl & 63)];
+      while (i < na && j < pna) {
+        const uint32_t a = max(iv_s(x), iv_s(y)), b = min(iv_e(x), iv_e(y));
+        if (a <= b) {
+          if (k < kAndCap) L[and_slot(nx, k, lane)] = a | (b << 16);
+          ++k;
+        }
+        if (iv_e(x) < iv_e(y)) x = L[and_slot(cur, ++i, lane)];
+        else {
+          ++j;
+          y = L[(pcur * kAndCap + min(j, kAndCap - 1)) * 64 + (pl & 63)];
+        }
+      }
+      if (k > kAndCap) bad = true;
+      na = k;
+      cur = nx;
+    }
+  }
+  wave_lds_sync();
+  // ---- per key (lane kk of group 0): cardinality, LR type (BitmapContainer.repairAfterLazy :1214-1224)
+  uint32_t c = 0;
+  if (g == 0 && !bad)
+    for (int i = 0; i < na; ++i) {
+      const uint32_t x = L[and_slot(cur, i, lane)];
+      c += iv_e(x) - iv_s(x) + 1;
+    }
+  const int ty = c ? type_lr((int)c) : kEmpty;
+  const uint64_t inb_sum = wave_sum_u64(inb);
+  uint64_t outb = 0;
+  if (g == 0 && q < nk) {
+    route[q] = bad ? 1 : 0;
+    if (!bad) {
+      wo.type[q] = (uint8_t)ty;
+      wo.card[q] = c;
+      wo.nruns[q] = (uint16_t)(ty == kRun ? 1 : 0);
+      if (ty != kEmpty) outb = payload_bytes(ty, c, 1) + (ty == kRun ? 2 : 0) + 16;
+    }
+  }
+  const uint64_t outb_sum = wave_sum_u64(outb);
+  // ---- emission, one key at a time by the whole wave, straight from the interval list
+  for (int key = 0; key < KB && q0 + key < nk; ++key) {
+    const int kty = __shfl(ty, key), kn = __shfl(na, key), kcur = __shfl(cur, key);
+    const bool kbad = __shfl((int)bad, key) != 0;
+    if (kbad || kty == kEmpty) continue;
+    uint8_t *dst = out + (uint64_t)(q0 + key) * kBitmapBytes;
+    if (kty == kRun) { // the full container: one run (0, 65535)
+      if (lane == 0) *reinterpret_cast<uint32_t *>(dst) = 0xFFFF0000u;
+    } else if (kty == kArray) {
+      uint16_t *o16 = reinterpret_cast<uint16_t *>(dst);
+      uint32_t pre = 0;
+      for (int i = 0; i < kn; ++i) {
+        const uint32_t x = L[(kcur * kAndCap + i) * 64 + key];
+        const uint32_t a = iv_s(x), len = iv_e(x) - a + 1;
+        for (uint32_t v = lane; v < len; v += 64) o16[pre + v] = (uint16_t)(a + v);
+        pre += len;
+      }
+    } else { // Bitmap: word wi = lane + 64 j, OR of the interval masks
+      uint64_t *o64 = reinterpret_cast<uint64_t *>(dst);
+      for (int j = 0; j < 16; ++j) {
+        const uint32_t wi = (uint32_t)(lane + 64 * j), w0 = wi * 64, w1 = w0 + 63;
+        uint64_t m = 0;
+        for (int i = 0; i < kn; ++i) {
+          const uint32_t x = L[(kcur * kAndCap + i) * 64 + key];
+          const uint32_t a = max(iv_s(x), w0), b = min(iv_e(x), w1);
+          if (a <= b) m |= (~0ull >> (63 - (b - a))) << (a - w0);
+        }
+        o64[wi] = m;
+      }
+    }
+  }
+  if (lane == 0) {
+    const int stripe = (q0 / KB) & (kStripes - 1);
+    atomicAdd((unsigned long long *)&stats[0 * kStripes + stripe], (unsigned long long)inb_sum);
+    atomicAdd((unsigned long long *)&stats[1 * kStripes + stripe], (unsigned long long)outb_sum);
+  }
+}
+
+#ifndef RBG_AND_KEYS
+#define RBG_AND_KEYS 16 // keys per wave of the lane-parallel workShyAnd
+#endif
+
 bool launch_wide_runs(int sem, const SetView &s, const uint32_t *cid, const uint64_t *seg, const uint32_t *klist,
                       uint32_t nk, uint8_t *out, const WideOut &wo, uint8_t *route, uint64_t *stats, hipStream_t st) {
   const unsigned g = (nk + 3) / 4;
   switch (sem) {
   case RB_FAST_OR: k_wide_runs<RB_FAST_OR><<<g, 256, 0, st>>>(s, cid, seg, klist, nk, out, wo, route, stats); return true;
-  case RB_WORKSHY_AND: k_wide_runs<RB_WORKSHY_AND><<<g, 256, 0, st>>>(s, cid, seg, klist, nk, out, wo, route, stats); return true;
+  case RB_WORKSHY_AND: {
+    const unsigned waves = (nk + RBG_AND_KEYS - 1) / RBG_AND_KEYS;
+    k_wide_runs_and<RBG_AND_KEYS><<<(waves + 3) / 4, 256, 0, st>>>(s, cid, seg, klist, nk, out, wo, route, stats);
+    return true;
+  }
   case RB_FAST_XOR: k_wide_runs<RB_FAST_XOR><<<g, 256, 0, st>>>(s, cid, seg, klist, nk, out, wo, route, stats); return true;
   default: return false;
   }

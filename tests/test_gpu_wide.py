@@ -201,3 +201,46 @@ def test_chunked_grouping_stitches_in_member_order(ctx, oracle):
             assert ctx.wide(getattr(rb, sem), a, members).serialize()[0] == wants[sem], sem
     finally:
         del os.environ["RBGPU_SORT_CHUNK"]
+
+
+def test_workshy_and_lane_lists(ctx, oracle):
+    """Lane-parallel workShyAnd (k_wide_runs_and): long member chains (several steps per lane, the
+    early exit once every list is empty), every LR result type straight from the interval lists
+    (full container -> Run, > 4096 -> Bitmap, <= 4096 -> Array, empty -> dropped), and list
+    overflow (> 16 intervals) routed to the generic kernel."""
+    rng = np.random.default_rng(21)
+    nb, nkeys = 150, 40
+    per_key = [[] for _ in range(nb)]
+    for k in range(nkeys):
+        kind = k % 5
+        holes_all = rng.choice(65000, size=(nb, 7), replace=True)
+        for b in range(nb):
+            if kind == 0:    # full container in every bitmap -> AND is full -> Run(0, 65535)
+                v = np.arange(65536)
+            elif kind == 1:  # big ranges with 7 small holes each -> > 4096 values, > 16 intervals
+                keep = np.ones(65536, bool)
+                for h in holes_all[b]:
+                    keep[h:h + 5] = False
+                v = np.nonzero(keep)[0]
+            elif kind == 2:  # a shared core of 3000 + random extra runs -> Array
+                parts = [np.arange(20000, 23000)]
+                for _ in range(int(rng.integers(0, 7))):
+                    s0 = int(rng.integers(0, 65000))
+                    parts.append(np.arange(s0, s0 + int(rng.integers(1, 300))))
+                v = np.unique(np.concatenate(parts))
+            elif kind == 3:  # two disjoint families -> AND empty
+                v = np.arange(1000, 2000) if b % 2 else np.arange(3000, 4000)
+            else:            # the same 5000-wide band with one varying hole -> Bitmap, few intervals
+                keep = np.zeros(65536, bool)
+                keep[10000:15000] = True
+                h = int(rng.integers(10000, 15000))
+                keep[h:h + 3] = False
+                v = np.nonzero(keep)[0]
+            per_key[b].append((v.astype(np.uint32) % 65536) | np.uint32(k << 16))
+    bms = [np.concatenate(p) for p in per_key]
+    s = ctx.upload_values(bms, run_optimize=True)
+    refs = [oracle.RefBitmap.deserialize(x) for x in s.serialize()]
+    for n in (11, 64, 150):
+        members = np.arange(n, dtype=np.uint32)
+        for sem in ("WORKSHY_AND", "FAST_AND"):
+            _check(ctx, oracle, s, refs, sem, members)
