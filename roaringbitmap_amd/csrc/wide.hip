@@ -3,10 +3,9 @@
 // 602, 772; ParallelAggregation.java:137-229).
 //
 // Every high-16-bit key is independent.  Pipeline:
-//   k_wide_flatten   one thread per input container of the member list -> (key, container id)
-//   radix sort       stable by key (rocPRIM), so each key's containers stay in member order —
-//                    the order that naive_and / naive_xor / the ParallelAggregation chains depend on
-//   k_wide_bounds    per key segment [begin, end) in the sorted list
+//   k_group_*        stable grouping of the members' containers by key (a tiled counting sort),
+//                    so each key's containers stay in member order — the order that naive_and /
+//                    naive_xor / the ParallelAggregation chains depend on — and seg[k] per key
 //   k_wide_select    keys that produce work (any container; for AND: present in every member)
 //   k_wide_reduce    ONE WAVE PER KEY: the key's containers folded in registers (65536-bit
 //                    register bitmap, Bitmaps streamed two at a time), reference type decision,
@@ -14,8 +13,6 @@
 //   compaction       drop empty results, result CSR
 #include <cstdlib>
 #include <cstring>
-
-#include <rocprim/rocprim.hpp>
 
 #include "internal.hpp"
 #include "kernels.hpp"
@@ -34,60 +31,153 @@ __device__ __forceinline__ void stat_add_w(uint64_t *stats, int word, uint64_t v
   }
 }
 
-__global__ __launch_bounds__(256) void k_wide_flatten(SetView s, const uint32_t *mem, const uint64_t *mstart,
-                                                      uint32_t M, uint64_t N, uint16_t *keys, uint32_t *cid) {
-  const uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-  if (j >= N) return;
-  uint32_t lo = 0, hi = M; // last m with mstart[m] <= j
-  while (hi - lo > 1) {
-    uint32_t mid = (lo + hi) >> 1;
-    if (mstart[mid] <= j) lo = mid;
-    else hi = mid;
-  }
-  const uint64_t c = s.begin[mem[lo]] + (j - mstart[lo]);
-  keys[j] = s.key[c];
-  cid[j] = (uint32_t)c;
-}
-
-// seg[k] = first index of key k in the sorted key list (k = 0..65536)
-__global__ __launch_bounds__(256) void k_wide_bounds(const uint16_t *sorted, uint64_t N, uint64_t *seg) {
-  const uint32_t k = blockIdx.x * 256 + threadIdx.x;
-  if (k > 65536) return;
-  uint64_t lo = 0, hi = N;
+// ---------------------------------------------------------------- stable grouping by key
+// A counting sort over (member block x key range) tiles.  A member holds at most one container per
+// key (its keys are sorted and unique), so the slot of member m's key-k container is (start of key
+// k) + (earlier members holding key k): member order within a key is kept, which naive_and /
+// naive_xor / the ParallelAggregation chains depend on.
+//   k_group_bounds   B[m][j] = first container of member m with key >= key_lo + j*KR (binary search)
+//   k_group_count    per tile: Hc[block][k] = members of the block holding key k (LDS counters)
+//   k_group_totals / scan / k_group_base: seg[k] = start of key k; H[block][k] = first slot of the
+//                    block's key-k containers (a column prefix over the blocks)
+//   k_group_scatter  per tile: ranks from per-key member masks, ids staged in LDS, stored per key
+// Every container of the members is read twice (its key) and its id written once, both coalesced;
+// only keys in [key_lo, key_hi) are grouped (a shard reads nothing outside its range).
+constexpr uint32_t kGrpKeys = 256;   // keys per tile (one thread per key slot)
+constexpr uint32_t kGrpMembers = 64; // members per block (a 64-bit presence mask per key)
+struct GroupArgs {
+  SetView s;
+  const uint32_t *mem;
+  const uint64_t *bnd; // [M][nkr + 1]
+  uint32_t M, MB, KR, nkr, key_lo, key_hi;
+};
+__device__ __forceinline__ uint64_t key_lower_bound(const uint16_t *key, uint64_t lo, uint64_t hi, uint32_t k) {
   while (lo < hi) {
-    uint64_t mid = (lo + hi) >> 1;
-    if (sorted[mid] < k) lo = mid + 1;
+    const uint64_t mid = (lo + hi) >> 1;
+    if (key[mid] < k) lo = mid + 1;
     else hi = mid;
   }
-  seg[k] = lo;
+  return lo;
 }
-
-// Chunked grouping (rocPRIM's radix sort is run on member-aligned chunks of <= kSortChunk items):
-// pre[c][k] = (global start of key k) + (items of key k in chunks < c) - (chunk c's first index
-// of key k) - (chunk c's start), so sorted element p of chunk c lands at pre[c][key] + p.
-constexpr uint64_t kSortChunk = 1ull << 27;
-__global__ __launch_bounds__(256) void k_wide_chunk_pre(const uint64_t *cseg, uint32_t nchunks, const uint64_t *cstart,
-                                                        uint64_t *seg, uint64_t *pre) {
-  const uint32_t k = blockIdx.x * 256 + threadIdx.x;
-  if (k > 65536) return;
-  // seg[k] = sum over chunks of the items with keys < k
-  uint64_t before = 0;
-  for (uint32_t c = 0; c < nchunks; ++c) before += cseg[(uint64_t)c * 65537 + k];
-  seg[k] = before;
-  if (k == 65536) return;
-  uint64_t run = before;
-  for (uint32_t c = 0; c < nchunks; ++c) {
-    const uint64_t lo = cseg[(uint64_t)c * 65537 + k], hi = cseg[(uint64_t)c * 65537 + k + 1];
-    pre[(uint64_t)c * 65536 + k] = run - lo - cstart[c];
-    run += hi - lo;
+__global__ __launch_bounds__(256) void k_group_bounds(GroupArgs a, uint64_t *bnd) {
+  const uint64_t t = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  const uint32_t nb = a.nkr + 1;
+  if (t >= (uint64_t)a.M * nb) return;
+  const uint32_t m = (uint32_t)(t / nb), j = (uint32_t)(t % nb);
+  const uint32_t b = a.mem[m];
+  const uint32_t k = j == a.nkr ? a.key_hi : a.key_lo + j * a.KR;
+  bnd[t] = key_lower_bound(a.s.key, a.s.begin[b], a.s.begin[b + 1], k);
+}
+// A tile has <= KR (<= 256) keys, so a member has at most one container per thread there: thread t
+// takes the t-th container of every member of the block, all loads in flight at once.
+__device__ __forceinline__ void tile_load(const GroupArgs &a, uint32_t mb, uint32_t j, uint32_t k0,
+                                          uint32_t (&kk)[kGrpMembers], uint32_t (&ci)[kGrpMembers]) {
+  const uint32_t m0 = mb * a.MB;
+#pragma unroll
+  for (int u = 0; u < (int)kGrpMembers; ++u) {
+    kk[u] = ~0u;
+    ci[u] = 0;
+    const uint32_t m = m0 + u;
+    if (u < (int)a.MB && m < a.M) {
+      const uint64_t *bm = a.bnd + (uint64_t)m * (a.nkr + 1) + j;
+      const uint64_t i = bm[0] + threadIdx.x;
+      if (i < bm[1]) {
+        kk[u] = (uint32_t)a.s.key[i] - k0;
+        ci[u] = (uint32_t)i;
+      }
+    }
   }
 }
-__global__ __launch_bounds__(256) void k_wide_chunk_scatter(const uint16_t *keys, const uint32_t *cid, uint64_t n,
-                                                            uint64_t cs, const uint64_t *pre_c, uint32_t *out) {
-  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= n) return;
-  const uint64_t p = cs + i;
-  out[pre_c[keys[p]] + p] = cid[p];
+__global__ __launch_bounds__(256) void k_group_count(GroupArgs a, uint32_t *Hc) {
+  __shared__ uint32_t cnt[kGrpKeys];
+  const uint32_t mb = blockIdx.y, j = blockIdx.x;
+  const uint32_t k0 = a.key_lo + j * a.KR, nk = min(a.KR, a.key_hi - k0);
+  cnt[threadIdx.x] = 0;
+  uint32_t kk[kGrpMembers], ci[kGrpMembers];
+  tile_load(a, mb, j, k0, kk, ci);
+  __syncthreads();
+#pragma unroll
+  for (int u = 0; u < (int)kGrpMembers; ++u)
+    if (kk[u] != ~0u) atomicAdd(&cnt[kk[u]], 1u);
+  __syncthreads();
+  if (threadIdx.x < nk) Hc[(uint64_t)mb * 65536 + k0 + threadIdx.x] = cnt[threadIdx.x];
+}
+__global__ __launch_bounds__(256) void k_group_totals(const uint32_t *Hc, uint32_t nmb, uint32_t key_lo,
+                                                      uint32_t key_hi, uint64_t *tot) {
+  const uint32_t k = blockIdx.x * 256 + threadIdx.x;
+  if (k > 65536) return;
+  uint64_t s = 0;
+  if (k >= key_lo && k < key_hi)
+    for (uint32_t b = 0; b < nmb; ++b) s += Hc[(uint64_t)b * 65536 + k];
+  tot[k] = s;
+}
+__global__ __launch_bounds__(256) void k_group_base(const uint32_t *Hc, uint64_t *H, uint32_t nmb, uint32_t key_lo,
+                                                    uint32_t key_hi, const uint64_t *seg) {
+  const uint32_t k = key_lo + blockIdx.x * 256 + threadIdx.x;
+  if (k >= key_hi) return;
+  uint64_t run = seg[k];
+  for (uint32_t b = 0; b < nmb; ++b) {
+    H[(uint64_t)b * 65536 + k] = run;
+    run += Hc[(uint64_t)b * 65536 + k];
+  }
+}
+// Per tile: a 64-bit presence mask per key (bit u = member u of the block holds the key) gives every
+// container its rank among the key's containers with one LDS atomic and one barrier; the tile's ids
+// are staged in LDS in (key, member) order, then each key's run of <= 64 ids is stored contiguously.
+// The staged entry is (member u << 8 | thread t): container id = first container of member u in the
+// tile + t, so the stage is 32 KiB of u16 (a u32 stage of the ids, RBG_GROUP_STAGE=1, halves the
+// blocks per CU).
+#ifndef RBG_GROUP_STAGE
+#define RBG_GROUP_STAGE 0
+#endif
+__global__ __launch_bounds__(256) void k_group_scatter(GroupArgs a, const uint64_t *H, uint32_t *cid) {
+  __shared__ unsigned long long mask[kGrpKeys];
+  __shared__ uint64_t gbase[kGrpKeys], mbase[kGrpMembers];
+  const uint32_t mb = blockIdx.y, j = blockIdx.x, t = threadIdx.x;
+  const uint32_t k0 = a.key_lo + j * a.KR, nk = min(a.KR, a.key_hi - k0);
+  mask[t] = 0;
+  gbase[t] = t < nk ? H[(uint64_t)mb * 65536 + k0 + t] : 0;
+  if (t < a.MB && mb * a.MB + t < a.M) mbase[t] = a.bnd[(uint64_t)(mb * a.MB + t) * (a.nkr + 1) + j];
+  uint32_t kk[kGrpMembers], ci[kGrpMembers];
+  tile_load(a, mb, j, k0, kk, ci);
+  __syncthreads();
+#pragma unroll
+  for (int u = 0; u < (int)kGrpMembers; ++u)
+    if (kk[u] != ~0u) atomicOr(&mask[kk[u]], 1ull << u);
+  __syncthreads();
+  {
+#if RBG_GROUP_STAGE
+  __shared__ uint32_t stage[kGrpMembers * kGrpKeys];
+#else
+  __shared__ uint16_t stage[kGrpMembers * kGrpKeys];
+#endif
+  __shared__ uint32_t lofs[kGrpKeys + 1], wsum[4];
+  const uint32_t lane = t & 63, wv = t >> 6;
+  // tile-local offsets of the keys: exclusive scan of the mask popcounts
+  const uint32_t c = (uint32_t)__popcll(mask[t]);
+  const uint32_t incl = wave_scan_u32(c, (int)lane);
+  if (lane == 63) wsum[wv] = incl;
+  __syncthreads();
+  uint32_t before = 0;
+  for (uint32_t w = 0; w < wv; ++w) before += wsum[w];
+  lofs[t] = before + incl - c;
+  if (t == 255) lofs[kGrpKeys] = before + incl;
+  __syncthreads();
+#pragma unroll
+  for (int u = 0; u < (int)kGrpMembers; ++u)
+    if (kk[u] != ~0u)
+      stage[lofs[kk[u]] + (uint32_t)__popcll(mask[kk[u]] & ((1ull << u) - 1))] =
+          RBG_GROUP_STAGE ? ci[u] : (uint32_t)(u << 8 | t);
+  __syncthreads();
+  // one wave per key at a time: the key's ids in member order, one contiguous store
+  for (uint32_t k = wv; k < nk; k += 4) {
+    const uint32_t o = lofs[k], n = lofs[k + 1] - o;
+    if (lane < n) {
+      const uint32_t v = stage[o + lane];
+      cid[gbase[k] + lane] = RBG_GROUP_STAGE ? v : (uint32_t)(mbase[v >> 8] + (v & 255));
+    }
+  }
+  }
 }
 
 // active[k] = 1 when key k (inside the shard's [lo, hi)) produces work: any container, or (AND
@@ -412,77 +502,48 @@ int wide_run(rbgpu_ctx *ctx, int sem, const rbgpu_set *in, const std::vector<uin
   const bool and_sem = sem == RB_WORKSHY_AND || sem == RB_NAIVE_AND || sem == RB_NAIVE_AND_ITER;
 
   stats_begin(ctx);
-  // ---- group by key (stable)
-  uint32_t *d_mem = nullptr, *d_cid = nullptr, *d_cid2 = nullptr, *d_klist = nullptr;
-  uint64_t *d_mstart = nullptr, *d_seg = nullptr, *d_active = nullptr, *d_apos = nullptr, *d_tmp = nullptr;
-  uint16_t *d_keys = nullptr, *d_keys2 = nullptr;
-  void *d_sort = nullptr;
-  size_t sort_bytes = 0;
-  const uint64_t N1 = std::max<uint64_t>(N, 1);
-  // member-aligned sort chunks (a member's containers never straddle two chunks); RBGPU_SORT_CHUNK
-  // lowers the chunk size so the tests exercise the stitched path at small sizes
-  uint64_t sort_chunk = kSortChunk;
-  if (const char *e = getenv("RBGPU_SORT_CHUNK")) sort_chunk = std::max<uint64_t>(1, strtoull(e, nullptr, 10));
-  std::vector<uint64_t> cstart{0};
-  for (uint32_t i = 0; i < M; ++i)
-    if (mstart[i + 1] - cstart.back() > sort_chunk && mstart[i] > cstart.back()) cstart.push_back(mstart[i]);
-  cstart.push_back(N);
-  const uint32_t nchunks = (uint32_t)cstart.size() - 1;
-  uint64_t max_chunk = 1;
-  for (uint32_t c = 0; c < nchunks; ++c) max_chunk = std::max(max_chunk, cstart[c + 1] - cstart[c]);
-  (void)rocprim::radix_sort_pairs(nullptr, sort_bytes, (const uint16_t *)nullptr, (uint16_t *)nullptr,
-                                  (const uint32_t *)nullptr, (uint32_t *)nullptr, (size_t)max_chunk, 0, 16, st);
-  uint64_t *d_cseg = nullptr, *d_pre = nullptr, *d_cstart = nullptr;
-  uint32_t *d_cid3 = nullptr;
-  if (nchunks > 1 &&
-      (pool.alloc((void **)&d_cseg, nchunks * 65537ull * 8) || pool.alloc((void **)&d_pre, nchunks * 65536ull * 8) ||
-       pool.alloc((void **)&d_cstart, (nchunks + 1) * 8ull) || pool.alloc((void **)&d_cid3, N1 * 4)))
-    return fail(RB_ENOMEM, "wide chunk tables (%llu containers)", (unsigned long long)N);
-  const uint64_t tmpw = std::max<uint64_t>(scan_tmp_words(65537), 1);
-  if (pool.alloc((void **)&d_mem, std::max<uint32_t>(M, 1) * 4ull) ||
-      pool.alloc((void **)&d_mstart, (M + 1) * 8ull) || pool.alloc((void **)&d_keys, N1 * 2) ||
-      pool.alloc((void **)&d_keys2, N1 * 2) || pool.alloc((void **)&d_cid, N1 * 4) ||
-      pool.alloc((void **)&d_cid2, N1 * 4) || pool.alloc(&d_sort, std::max<size_t>(sort_bytes, 16)) ||
-      pool.alloc((void **)&d_seg, 65537 * 8ull) || pool.alloc((void **)&d_active, 65537 * 8ull) ||
-      pool.alloc((void **)&d_apos, 65537 * 8ull) || pool.alloc((void **)&d_klist, 65536 * 4ull) ||
-      pool.alloc((void **)&d_tmp, tmpw * 8))
-    return fail(RB_ENOMEM, "wide workspace (%llu containers)", (unsigned long long)N);
-  auto release = [&]() {
-    for (void *p : {(void *)d_mem, (void *)d_mstart, (void *)d_keys, (void *)d_keys2, (void *)d_cid, (void *)d_cid2,
-                    d_sort, (void *)d_seg, (void *)d_active, (void *)d_apos, (void *)d_klist, (void *)d_tmp,
-                    (void *)d_cseg, (void *)d_pre, (void *)d_cstart, (void *)d_cid3})
-      pool.release(p);
-  };
-  if (M) {
-    HIPCHK(hipMemcpyAsync(d_mem, members.data(), M * 4ull, hipMemcpyHostToDevice, st));
-    HIPCHK(hipMemcpyAsync(d_mstart, mstart.data(), (M + 1) * 8ull, hipMemcpyHostToDevice, st));
-  }
-  const SetView sv = in->view();
-  if (N) {
-    k_wide_flatten<<<nblk(N, 256), 256, 0, st>>>(sv, d_mem, d_mstart, M, N, d_keys, d_cid);
-    for (uint32_t c = 0; c < nchunks; ++c) {
-      const uint64_t cs = cstart[c], cn = cstart[c + 1] - cs;
-      size_t sb = sort_bytes;
-      const hipError_t e = rocprim::radix_sort_pairs(d_sort, sb, d_keys + cs, d_keys2 + cs, d_cid + cs, d_cid2 + cs,
-                                                     (size_t)cn, 0, 16, st);
-      if (e != hipSuccess) {
-        release();
-        return fail(RB_EDEVICE, "radix sort failed (chunk of %llu containers): %s", (unsigned long long)cn,
-                    hipGetErrorString(e));
-      }
-      if (nchunks > 1) k_wide_bounds<<<nblk(65537, 256), 256, 0, st>>>(d_keys2 + cs, cn, d_cseg + (uint64_t)c * 65537);
+  // ---- group by key (stable; keys in [key_lo, key_hi) only): the tiled counting sort above.
+  // RBGPU_GROUP_TILE="members,keys" shrinks the tiles so the tests cover many-tile layouts.
+  uint32_t MB = kGrpMembers, KR = kGrpKeys;
+  if (const char *e = getenv("RBGPU_GROUP_TILE")) {
+    unsigned a = 0, b = 0;
+    if (sscanf(e, "%u,%u", &a, &b) == 2) {
+      MB = std::min<uint32_t>(std::max<uint32_t>(a, 1), kGrpMembers);
+      KR = std::min<uint32_t>(std::max<uint32_t>(b, 1), kGrpKeys);
     }
   }
-  if (nchunks > 1) {
-    // stitch the stably sorted chunks into one key-grouped list, member order kept within a key
-    HIPCHK(hipMemcpyAsync(d_cstart, cstart.data(), (nchunks + 1) * 8ull, hipMemcpyHostToDevice, st));
-    k_wide_chunk_pre<<<nblk(65537, 256), 256, 0, st>>>(d_cseg, nchunks, d_cstart, d_seg, d_pre);
-    for (uint32_t c = 0; c < nchunks; ++c)
-      k_wide_chunk_scatter<<<nblk(cstart[c + 1] - cstart[c], 256), 256, 0, st>>>(
-          d_keys2, d_cid2, cstart[c + 1] - cstart[c], cstart[c], d_pre + (uint64_t)c * 65536, d_cid3);
-    std::swap(d_cid2, d_cid3);
-  } else {
-    k_wide_bounds<<<nblk(65537, 256), 256, 0, st>>>(d_keys2, N, d_seg);
+  const uint32_t krange = key_hi > key_lo ? key_hi - key_lo : 0;
+  const uint32_t nmb = (M + MB - 1) / MB, nkr = (krange + KR - 1) / KR;
+  uint32_t *d_mem = nullptr, *d_cid2 = nullptr, *d_klist = nullptr, *d_Hc = nullptr;
+  uint64_t *d_bnd = nullptr, *d_H = nullptr, *d_tot = nullptr, *d_seg = nullptr, *d_active = nullptr,
+           *d_apos = nullptr, *d_tmp = nullptr;
+  const uint64_t N1 = std::max<uint64_t>(N, 1);
+  const uint64_t tmpw = std::max<uint64_t>(scan_tmp_words(65537), 1);
+  if (pool.alloc((void **)&d_mem, std::max<uint32_t>(M, 1) * 4ull) ||
+      pool.alloc((void **)&d_bnd, std::max<uint64_t>((uint64_t)M * (nkr + 1), 1) * 8) ||
+      pool.alloc((void **)&d_Hc, std::max<uint32_t>(nmb, 1) * 65536ull * 4) ||
+      pool.alloc((void **)&d_H, std::max<uint32_t>(nmb, 1) * 65536ull * 8) || pool.alloc((void **)&d_cid2, N1 * 4) ||
+      pool.alloc((void **)&d_tot, 65537 * 8ull) || pool.alloc((void **)&d_seg, 65537 * 8ull) ||
+      pool.alloc((void **)&d_active, 65537 * 8ull) || pool.alloc((void **)&d_apos, 65537 * 8ull) ||
+      pool.alloc((void **)&d_klist, 65536 * 4ull) || pool.alloc((void **)&d_tmp, tmpw * 8))
+    return fail(RB_ENOMEM, "wide workspace (%llu containers)", (unsigned long long)N);
+  auto release = [&]() {
+    for (void *p : {(void *)d_mem, (void *)d_bnd, (void *)d_Hc, (void *)d_H, (void *)d_cid2, (void *)d_tot,
+                    (void *)d_seg, (void *)d_active, (void *)d_apos, (void *)d_klist, (void *)d_tmp})
+      pool.release(p);
+  };
+  if (M) HIPCHK(hipMemcpyAsync(d_mem, members.data(), M * 4ull, hipMemcpyHostToDevice, st));
+  const SetView sv = in->view();
+  const GroupArgs ga{sv, d_mem, d_bnd, M, MB, KR, nkr, key_lo, key_hi};
+  if (M && nkr) {
+    k_group_bounds<<<nblk((uint64_t)M * (nkr + 1), 256), 256, 0, st>>>(ga, d_bnd);
+    k_group_count<<<dim3(nkr, nmb), 256, 0, st>>>(ga, d_Hc);
+  }
+  k_group_totals<<<nblk(65537, 256), 256, 0, st>>>(d_Hc, M && nkr ? nmb : 0, key_lo, key_hi, d_tot);
+  scan_exclusive(d_tot, d_seg, 65536, d_tmp, st);
+  if (M && nkr) {
+    k_group_base<<<nblk(krange, 256), 256, 0, st>>>(d_Hc, d_H, nmb, key_lo, key_hi, d_seg);
+    k_group_scatter<<<dim3(nkr, nmb), 256, 0, st>>>(ga, d_H, d_cid2);
   }
   k_wide_select<<<nblk(65536, 256), 256, 0, st>>>(d_seg, and_sem ? (uint64_t)M : 0, key_lo, key_hi, d_active);
   scan_exclusive(d_active, d_apos, 65536, d_tmp, st);

@@ -87,18 +87,14 @@ __global__ __launch_bounds__(256) void k_wide_runs(SetView s, const uint32_t *__
     if (lane == 0) route[q] = 1;
     return;
   }
-  if (SEM != RB_WORKSHY_AND) {
-    lds_zero(acc, lane);
-    wave_lds_sync();
-  }
+  lds_zero(acc, lane);
+  wave_lds_sync();
   // accumulator state (wave-uniform)
   bool present = false, fail_route = false;
   int t = kRun, c = 0, r = 0;
-  uint32_t ia = 0, ib = 0; // AND: this lane's interval [ia, ib]
-  int na = -1;            // AND: interval count, -1 = not started
   uint64_t inb = 0;
   RunBatch nxt = load_batch(s, cid, lo + lane, hi);
-  for (uint64_t base = lo; base < hi && !fail_route && na != 0; base += 64) {
+  for (uint64_t base = lo; base < hi && !fail_route; base += 64) {
     const RunBatch cur = nxt;
     __builtin_amdgcn_sched_barrier(0);
     if (base + 64 < hi) nxt = load_batch(s, cid, base + 64 + lane, hi);
@@ -120,52 +116,6 @@ __global__ __launch_bounds__(256) void k_wide_runs(SetView s, const uint32_t *__
         const uint32_t v = readlane(run_word(cur, u), j);
         rs[u] = v & 0xFFFF;
         re[u] = (v & 0xFFFF) + (v >> 16);
-      }
-      if (SEM == RB_WORKSHY_AND) {
-        if (na < 0) { // the first container: its runs
-          na = nr;
-#pragma unroll
-          for (int u = 0; u < kMaxRunsFast; ++u)
-            if (lane == u) {
-              ia = rs[u];
-              ib = re[u];
-            }
-          continue;
-        }
-        // intersect this lane's interval with every run; pieces in order
-        uint32_t k = 0;
-        if (lane < na) {
-#pragma unroll
-          for (int u = 0; u < kMaxRunsFast; ++u)
-            if (u < nr && max(ia, rs[u]) <= min(ib, re[u])) ++k;
-        }
-        const uint32_t incl = wave_scan_u32(k, lane);
-        const int total = (int)readlane(incl, 63);
-        if (total > 64) {
-          fail_route = true;
-          break;
-        }
-        uint32_t pos = incl - k;
-        if (lane < na) {
-#pragma unroll
-          for (int u = 0; u < kMaxRunsFast; ++u) {
-            const uint32_t a = max(ia, rs[u]), b = min(ib, re[u]);
-            if (u < nr && a <= b) {
-              acc[2 * pos] = a;
-              acc[2 * pos + 1] = b;
-              ++pos;
-            }
-          }
-        }
-        wave_lds_sync();
-        na = total;
-        if (lane < na) {
-          ia = acc[2 * lane];
-          ib = acc[2 * lane + 1];
-        }
-        wave_lds_sync();
-        if (na == 0) break; // AND stays empty
-        continue;
       }
       // ---- range updates over the runs' dwords (OR: set, XOR: complement + metrics)
       uint32_t o[kMaxRunsFast + 1];
@@ -242,23 +192,7 @@ __global__ __launch_bounds__(256) void k_wide_runs(SetView s, const uint32_t *__
   // ---- result
   uint8_t *dst = out + (uint64_t)q * kBitmapBytes;
   int ty = kEmpty;
-  if (SEM == RB_WORKSHY_AND) {
-    // rebuild the bitmap from the intervals (toggles at a and b+1, then the prefix transform)
-    lds_zero(acc, lane);
-    wave_lds_sync();
-    uint32_t card_part = 0;
-    if (lane < na) {
-      card_part = ib - ia + 1;
-      atomicXor(&acc[ia >> 5], 1u << (ia & 31));
-      if (ib + 1 < 65536) atomicXor(&acc[(ib + 1) >> 5], 1u << ((ib + 1) & 31));
-    }
-    wave_lds_sync();
-    toggles_to_words_lds(acc, lane);
-    wave_lds_sync();
-    c = (int)wave_sum_u32(card_part);
-    ty = c ? type_lr(c) : kEmpty;
-    r = ty == kRun ? 1 : 0;
-  } else if (SEM == RB_FAST_OR) {
+  if (SEM == RB_FAST_OR) {
     uint64_t w[kW];
     lds_read_words(acc, w, lane);
     int rr;

@@ -185,22 +185,30 @@ def test_run_fastpath_mixed_keys_fall_back(ctx, oracle):
             assert ctx.wide(getattr(rb, sem), s, members).serialize()[0] == want, (sem, n)
 
 
-def test_chunked_grouping_stitches_in_member_order(ctx, oracle):
-    """Large inputs are grouped by key in member-aligned chunks (rocPRIM radix sort per chunk, then a
-    stitch); with a tiny chunk size every semantics must still match the oracle byte for byte."""
+def test_tiled_grouping_keeps_member_order(ctx, oracle):
+    """Containers are grouped by key with a counting sort over (member block x key range) tiles;
+    with tiny tiles (many member blocks and key ranges, ragged last tiles, duplicate members) every
+    semantics must still match the oracle byte for byte, also over a key sub-range."""
     import os
 
     import roaringbitmap_amd as rb
     a, _ = ctx.generate(rb.WL_WIDE_MIXED, 20, seed=13)
     refs = [oracle.RefBitmap.deserialize(b) for b in a.serialize()]
-    members = np.arange(20, dtype=np.uint32)
+    members = np.array(list(range(20)) + [3, 7], dtype=np.uint32)
     wants = {sem: oracle.wide(getattr(oracle, sem), [refs[m] for m in members]).serialize() for sem in SEMS}
-    os.environ["RBGPU_SORT_CHUNK"] = "9000"
-    try:
-        for sem in SEMS:
-            assert ctx.wide(getattr(rb, sem), a, members).serialize()[0] == wants[sem], sem
-    finally:
-        del os.environ["RBGPU_SORT_CHUNK"]
+    for tile in ("3,100", "1,256", "7,33", "64,1"):
+        os.environ["RBGPU_GROUP_TILE"] = tile
+        try:
+            for sem in SEMS:
+                assert ctx.wide(getattr(rb, sem), a, members).serialize()[0] == wants[sem], (sem, tile)
+            got = ctx.wide(rb.FAST_XOR, a, members, key_range=(1234, 40000)).download()
+            full = oracle.RefBitmap.deserialize(wants["FAST_XOR"])
+            keys = [int(k) for k in got.key]
+            assert all(1234 <= k < 40000 for k in keys)
+            want_c = [(k, t, c) for k, t, c, _ in full.containers() if 1234 <= k < 40000]
+            assert list(zip(keys, got.type.tolist(), got.card.tolist())) == want_c, tile
+        finally:
+            del os.environ["RBGPU_GROUP_TILE"]
 
 
 def test_workshy_and_lane_lists(ctx, oracle):
