@@ -76,6 +76,9 @@ struct WideOut {
 
 // ---- wide_runs.hip: Run-list fast path for naive_or / workShyAnd / naive_xor keys whose containers
 // are all Runs with <= 8 runs; route[q] = 0 where done, 1 where the generic kernel must run
+void launch_wide_runs_xor(const SetView &s, const uint32_t *cid, const uint64_t *seg, const uint32_t *klist,
+                          uint32_t nk, uint8_t *out, const WideOut &wo, uint8_t *route, uint64_t *stats,
+                          hipStream_t st);
 bool launch_wide_runs(int sem, const SetView &s, const uint32_t *cid, const uint64_t *seg, const uint32_t *klist,
                       uint32_t nk, uint8_t *out, const WideOut &wo, uint8_t *route, uint64_t *stats, hipStream_t st);
 

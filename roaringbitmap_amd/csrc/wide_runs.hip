@@ -435,6 +435,9 @@ __global__ __launch_bounds__(256) void k_wide_runs_and(SetView s, const uint32_t
   }
 }
 
+#ifndef RBG_XOR_BATCHED
+#define RBG_XOR_BATCHED 1 // naive_xor over Run-heavy keys: batch-parallel metrics (wide_xor.hip)
+#endif
 #ifndef RBG_AND_KEYS
 #define RBG_AND_KEYS 16 // keys per wave of the lane-parallel workShyAnd
 #endif
@@ -449,7 +452,13 @@ bool launch_wide_runs(int sem, const SetView &s, const uint32_t *cid, const uint
     k_wide_runs_and<RBG_AND_KEYS><<<(waves + 3) / 4, 256, 0, st>>>(s, cid, seg, klist, nk, out, wo, route, stats);
     return true;
   }
-  case RB_FAST_XOR: k_wide_runs<RB_FAST_XOR><<<g, 256, 0, st>>>(s, cid, seg, klist, nk, out, wo, route, stats); return true;
+  case RB_FAST_XOR:
+#if RBG_XOR_BATCHED
+    launch_wide_runs_xor(s, cid, seg, klist, nk, out, wo, route, stats, st);
+#else
+    k_wide_runs<RB_FAST_XOR><<<g, 256, 0, st>>>(s, cid, seg, klist, nk, out, wo, route, stats);
+#endif
+    return true;
   default: return false;
   }
 }

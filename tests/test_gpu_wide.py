@@ -252,3 +252,62 @@ def test_workshy_and_lane_lists(ctx, oracle):
         members = np.arange(n, dtype=np.uint32)
         for sem in ("WORKSHY_AND", "FAST_AND"):
             _check(ctx, oracle, s, refs, sem, members)
+
+
+def test_batched_xor_long_chains(ctx, oracle):
+    """Batch-parallel naive_xor over Run-heavy keys (wide_xor.hip): chains of several 32-container
+    batches with ragged tails; keys whose XOR empties mid-batch and at batch boundaries (removal,
+    then a clone); tiny results (the Array state and its |A| < 32 rule); runs touching 0 and 65535;
+    tie groups (shared run boundaries); dense results (the Bitmap state); and a full container that
+    routes its key to the generic kernel.  Bytes must equal the oracle's and the generic path's."""
+    import os
+
+    import roaringbitmap_amd as rb
+    rng = np.random.default_rng(33)
+    nb, nkeys = 101, 12
+    per_bitmap = [[] for _ in range(nb)]
+    for k in range(nkeys):
+        kind = k % 6
+        prev = None
+        for b in range(nb):
+            if kind == 0:    # config-4 shape: shared core run + up to 7 random runs
+                parts = [np.arange(5000, 6024)]
+                for _ in range(int(rng.integers(0, 8))):
+                    s0 = int(rng.integers(0, 65000))
+                    parts.append(np.arange(s0, s0 + int(rng.integers(1, 257))))
+                v = np.unique(np.concatenate(parts))
+            elif kind == 1:  # repeats: the running XOR empties (b % 7 == 1 repeats b-1)
+                if prev is not None and b % 7 == 1:
+                    v = prev
+                else:
+                    s0 = int(rng.integers(0, 60000))
+                    v = np.arange(s0, s0 + int(rng.integers(1, 3000)))
+            elif kind == 2:  # tiny containers: small results, Array state, |A| < 32
+                s0 = int(rng.integers(0, 40))
+                v = np.unique(np.concatenate([np.arange(s0, s0 + int(rng.integers(1, 4))),
+                                              np.arange(50 + s0, 52 + s0)]))
+            elif kind == 3:  # runs at both ends of the key
+                v = np.concatenate([np.arange(0, int(rng.integers(1, 500))),
+                                    np.arange(int(rng.integers(65000, 65535)), 65536)])
+            elif kind == 4:  # shared boundaries (ties) and dense results -> Bitmap state
+                cuts = np.sort(rng.choice(np.arange(0, 65536, 4096), size=8, replace=False))
+                v = np.unique(np.concatenate([np.arange(c, c + 2000 + 7 * (b % 3)) for c in cuts]))
+            else:            # one full container in the chain -> the key takes the generic path
+                v = np.arange(65536) if b == 40 else np.arange(100 * (b % 9), 100 * (b % 9) + 900)
+            prev = v
+            per_bitmap[b].append((v.astype(np.uint32) % 65536) | np.uint32(k << 16))
+    bms = [np.unique(np.concatenate(p)).astype(np.uint32) for p in per_bitmap]
+    s = ctx.upload_values(bms, run_optimize=True)
+    refs = [oracle.RefBitmap.deserialize(x) for x in s.serialize()]
+    for n in (nb, 64, 33, 32, 31):
+        members = np.arange(n, dtype=np.uint32)
+        want = oracle.wide(oracle.FAST_XOR, [refs[m] for m in members]).serialize()
+        assert ctx.wide(rb.FAST_XOR, s, members).serialize()[0] == want, n
+    members = rng.permutation(nb).astype(np.uint32)
+    want = oracle.wide(oracle.FAST_XOR, [refs[m] for m in members]).serialize()
+    assert ctx.wide(rb.FAST_XOR, s, members).serialize()[0] == want
+    os.environ["RBGPU_NO_RUN_FASTPATH"] = "1"
+    try:
+        assert ctx.wide(rb.FAST_XOR, s, members).serialize()[0] == want
+    finally:
+        del os.environ["RBGPU_NO_RUN_FASTPATH"]
