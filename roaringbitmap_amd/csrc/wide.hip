@@ -602,8 +602,12 @@ int wide_run(rbgpu_ctx *ctx, int sem, const rbgpu_set *in, const std::vector<uin
     release();
     return rc;
   }
-  const char *name = sem == RB_FAST_OR ? "k_wide_reduce<FAST_OR>" : sem == RB_WORKSHY_AND ? "k_wide_reduce<WORKSHY_AND>"
-                     : sem == RB_FAST_XOR ? "k_wide_reduce<FAST_XOR>" : sem == RB_PAR_OR ? "k_wide_reduce<PAR_OR>"
+  // the span covers the Run-list fast path (if any) and the generic kernel for the routed keys
+  const bool fp = fast_ok && d_route;
+  const char *name = sem == RB_FAST_OR ? "k_wide_reduce<FAST_OR>"
+                     : sem == RB_WORKSHY_AND ? (fp ? "k_wide_runs_and+k_wide_reduce<WORKSHY_AND>" : "k_wide_reduce<WORKSHY_AND>")
+                     : sem == RB_FAST_XOR ? (fp ? "k_wide_runs_xor+k_wide_reduce<FAST_XOR>" : "k_wide_reduce<FAST_XOR>")
+                     : sem == RB_PAR_OR ? "k_wide_reduce<PAR_OR>"
                      : sem == RB_PAR_XOR ? "k_wide_reduce<PAR_XOR>" : "k_wide_reduce<NAIVE_AND>";
   const KernelSpan spans[1] = {{name, 0, 1, nk}};
   // ev[2] -> ev[3]: nothing; stats_end reads ev[1]..ev[2] for kernel 0

@@ -34,6 +34,9 @@ namespace {
 constexpr int kXB = 32;         // containers per batch (2 lanes per container, 4 runs per lane)
 constexpr int kXRegion = 1280;  // u32 per wave: pre16 (1024) | then MC (1024) + pos (256)
 constexpr uint32_t kNoKey = 0xFFFFFFFFu;
+#ifndef RBG_XOR_APPLY_FLAT
+#define RBG_XOR_APPLY_FLAT 0 // 1: one flattened loop over the odd intervals (measured slower: 42.8 vs 35.8 ms)
+#endif
 
 template <int CTRL> __device__ __forceinline__ uint32_t dpp_mov(uint32_t v) {
   return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xf, 0xf, false);
@@ -241,9 +244,10 @@ __global__ __launch_bounds__(256) void k_wide_runs_xor(SetView s, const uint32_t
     sort512(K, lane);
 
     // ---- per sorted position i = 8 lane + e: coverage mask, tie-group rank, P(x), P(x-1), F(x)
-    uint32_t P[8], Mv[8], F[8], B[8];
+    uint32_t P[8], Mv[8], F[8], B[8], Q[8];
     {
       uint32_t m = 0, gl = 0, prevp = dpp<0x138>(K[7] >> 9); // wave_shr:1
+      uint32_t hmask = 0;                                     // bit e: position 8 lane + e heads a tie group
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         const bool vld = K[e] != kNoKey;
@@ -252,16 +256,30 @@ __global__ __launch_bounds__(256) void k_wide_runs_xor(SetView s, const uint32_t
         Mv[e] = m;
         const uint32_t pp = e ? P[e - 1] : prevp;
         const bool head = (lane == 0 && e == 0) || P[e] != pp;
-        if (head) gl = (uint32_t)(8 * lane + e);
+        if (head) {
+          gl = (uint32_t)(8 * lane + e);
+          hmask |= 1u << e;
+        }
         B[e] = gl; // last head at or before i, within this lane (0 if none yet)
       }
       const uint32_t mx = wave_xscan_xor(m, lane) ^ m;
       const uint32_t gprev = dpp<0x138>(wave_scan_max(gl));
+      // first head after this lane: suffix max of (512 - first head) over the lanes above, via a
+      // lane reversal (ds_bpermute) and the forward max-scan
+      const uint32_t fh = hmask ? (uint32_t)(8 * lane) + __builtin_ctz(hmask) : 512u;
+      const uint32_t rv = (uint32_t)__builtin_amdgcn_ds_bpermute((63 - lane) << 2, (int)(512u - fh));
+      const uint32_t sc = (uint32_t)__builtin_amdgcn_ds_bpermute((63 - lane) << 2, (int)wave_scan_max(rv));
+      uint32_t nh = 512u - dpp<0x130>(sc); // wave_shl:1 -> lanes above only
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
+      for (int e = 7; e >= 0; --e) {
         Mv[e] ^= mx;
         const uint32_t g = max(B[e], gprev);
         B[e] = ((uint32_t)(8 * lane + e) - g) & 1u; // odd number of earlier batch containers share x
+        // interval range ends for the A loop: a start point's first positive-length interval is
+        // the last of its tie group; an end point's range stops at the first of its tie group
+        const bool is_end = K[e] & 1u;
+        Q[e] = is_end ? g : nh - 1;
+        if (hmask & (1u << e)) nh = (uint32_t)(8 * lane + e);
       }
       uint32_t RB[8];
 #pragma unroll
@@ -300,8 +318,38 @@ __global__ __launch_bounds__(256) void k_wide_runs_xor(SetView s, const uint32_t
       for (int e = 0; e < 8; e += 2) mc4[e >> 1] = make_uint4(Mv[e], Cv[e], Mv[e + 1], Cv[e + 1]);
 #pragma unroll
       for (int e = 0; e < 8; ++e)
-        if (K[e] != kNoKey) pos[K[e] & 511] = (uint16_t)((8 * lane + e) | (B[e] << 15));
+        if (K[e] != kNoKey) pos[K[e] & 511] = (uint16_t)(Q[e] | (B[e] << 15));
       // ---- P ^= the batch: complement every elementary interval with odd coverage
+#if RBG_XOR_APPLY_FLAT
+      // one flattened loop over the lane's odd intervals (a queue of up to 8), one dword per trip
+      uint32_t live = 0;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const uint32_t pn = e < 7 ? P[e + 1] : pn7;
+        if (K[e] != kNoKey && (__popc(Mv[e]) & 1) && pn > P[e]) live |= 1u << e; // (ties: zero length)
+      }
+      uint32_t w = 1, wend = 0, ia = 0, ib = 0;
+      while (true) {
+        if (w > wend) {
+          if (!live) break;
+          const int e = __builtin_ctz(live);
+          live &= live - 1;
+          uint32_t a = P[0], pn = P[1];
+#pragma unroll
+          for (int t = 1; t < 8; ++t)
+            if (e == t) {
+              a = P[t];
+              pn = t < 7 ? P[t + 1] : pn7;
+            }
+          ia = a;
+          ib = pn - 1;
+          w = a >> 5;
+          wend = ib >> 5;
+        }
+        atomicXor(&acc[w], dmask(w, ia, ib));
+        ++w;
+      }
+#else
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         const uint32_t pn = e < 7 ? P[e + 1] : pn7;
@@ -310,6 +358,7 @@ __global__ __launch_bounds__(256) void k_wide_runs_xor(SetView s, const uint32_t
           for (uint32_t w = a >> 5; w <= (b >> 5); ++w) atomicXor(&acc[w], dmask(w, a, b));
         }
       }
+#endif
     }
     wave_lds_sync();
 
@@ -327,12 +376,25 @@ __global__ __launch_bounds__(256) void k_wide_runs_xor(SetView s, const uint32_t
         qe[u] = ok ? (b & 0x7FFF) : 0;
         if (ok) match += (a >> 15) + (b >> 15);
       }
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        for (uint32_t i = qs[u]; i < qe[u]; ++i) {
-          const uint2 mc = MC[i];
-          A += (__popc(mc.x & below) & 1) ? (mc.y >> 16) : (mc.y & 0xFFFF);
+      // one flattened loop over the lane's (up to 4) interval ranges, two entries per trip
+      uint32_t cs = qs[0], ce = qe[0], s1 = qs[1], e1 = qe[1], s2 = qs[2], e2 = qe[2], s3 = qs[3], e3 = qe[3];
+      while (true) {
+        if (cs >= ce) {
+          if (s1 >= e1 && s2 >= e2 && s3 >= e3) break;
+          cs = s1;
+          ce = e1;
+          s1 = s2;
+          e1 = e2;
+          s2 = s3;
+          e2 = e3;
+          s3 = e3 = 0;
+          continue;
         }
+        const bool two = cs + 1 < ce;
+        const uint2 m0 = MC[cs], m1 = MC[two ? cs + 1 : cs];
+        A += (__popc(m0.x & below) & 1) ? (m0.y >> 16) : (m0.y & 0xFFFF);
+        if (two) A += (__popc(m1.x & below) & 1) ? (m1.y >> 16) : (m1.y & 0xFFFF);
+        cs += two ? 2 : 1;
       }
     }
     wave_lds_sync(); // the next batch rewrites the region
