@@ -33,6 +33,16 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r01", "traffic.json")
 
 
+def pair_traffic(op, main_name):
+    """PMC HBM bytes per launch of the pairwise task phase: light, heavy, or both when they run
+    concurrently (the span "k_pair_tasks<light>||<heavy>")."""
+    lt = pmc_traffic(f"rbg::k_pair_tasks<{op}, false, 0>")
+    hv = pmc_traffic(f"rbg::k_pair_tasks<{op}, false, 1>")
+    if "||" in main_name:
+        return lt + hv if lt is not None and hv is not None else None
+    return lt if "light" in main_name else hv
+
+
 def pmc_traffic(pmc_name: str):
     """HBM bytes per launch of `pmc_name` from the committed rocprofv3 PMC summary of this same bench
     command (scripts/traffic.py: FETCH_SIZE x2 for gfx950 16-B/lane reads + WRITE_SIZE, separate
@@ -455,8 +465,7 @@ def main():
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": pmc_traffic(f"rbg::k_pair_tasks<{op}, false, 0>" if "light" in main_name
-                                       else f"rbg::k_pair_tasks<{op}, false, 1>"),
+                "traffic": pair_traffic(op, main_name),
                 "traffic_source": "profiles/r01/traffic.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes)",
                 "kernel_ms": round(k_ms, 4),
                 "algorithmic_bytes_per_launch": int(per_launch),

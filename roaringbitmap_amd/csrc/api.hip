@@ -64,7 +64,9 @@ void ctx_unref(rbgpu_ctx *ctx) {
   if (--ctx->refs > 0) return;
   (void)hipSetDevice(ctx->device);
   (void)hipStreamSynchronize(ctx->stream);
+  if (ctx->side) (void)hipStreamSynchronize(ctx->side);
   for (auto &e : ctx->ev) (void)hipEventDestroy(e);
+  for (auto &e : ctx->ev_side) (void)hipEventDestroy(e);
   (void)hipFree(ctx->d_stats);
   (void)hipHostFree(ctx->h_pinned);
   (void)hipHostFree(ctx->h_stats);
@@ -74,6 +76,7 @@ void ctx_unref(rbgpu_ctx *ctx) {
   ctx->ws_tasks.destroy();
   ctx->ws_segs.destroy();
   (void)hipStreamDestroy(ctx->stream);
+  if (ctx->side) (void)hipStreamDestroy(ctx->side);
   delete ctx;
 }
 int ensure_h_begin(const rbgpu_set *cs) {
@@ -218,8 +221,10 @@ int stats_end(rbgpu_ctx *ctx, uint64_t tasks, uint64_t result_containers, const 
   int best = -1;
   for (int i = 0; i < (int)s.n_kernels; ++i) {
     std::snprintf(s.kernel_name[i], sizeof s.kernel_name[i], "%s", k[i].name);
-    s.kernel_ms[i] = hipEventElapsedTime(&ms, ctx->ev[1 + i], ctx->ev[2 + i]) == hipSuccess ? ms : 0.0;
-    s.kernel_bytes[i] = (k[i].in_word >= 0 ? w[k[i].in_word] : 0) + (k[i].out_word >= 0 ? w[k[i].out_word] : 0);
+    hipEvent_t e0 = k[i].e0 ? k[i].e0 : ctx->ev[1 + i], e1 = k[i].e1 ? k[i].e1 : ctx->ev[2 + i];
+    s.kernel_ms[i] = hipEventElapsedTime(&ms, e0, e1) == hipSuccess ? ms : 0.0;
+    s.kernel_bytes[i] = (k[i].in_word >= 0 ? w[k[i].in_word] : 0) + (k[i].out_word >= 0 ? w[k[i].out_word] : 0) +
+                        (k[i].in2 >= 0 ? w[k[i].in2] : 0) + (k[i].out2 >= 0 ? w[k[i].out2] : 0);
     s.kernel_items[i] = k[i].items;
     if (best < 0 || s.kernel_ms[i] > s.kernel_ms[best]) best = i;
   }
@@ -255,6 +260,7 @@ int rbgpu_open(int device, rbgpu_ctx **out) {
   rbgpu_ctx *c = new rbgpu_ctx;
   c->device = device;
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess ||
       hipMalloc((void **)&c->d_stats, kStatWords * kStripes * sizeof(uint64_t)) != hipSuccess ||
       hipHostMalloc((void **)&c->h_stats, kStatWords * kStripes * sizeof(uint64_t)) != hipSuccess ||
       hipHostMalloc((void **)&c->h_pinned, 16 * sizeof(uint64_t)) != hipSuccess) {
@@ -262,6 +268,7 @@ int rbgpu_open(int device, rbgpu_ctx **out) {
     return fail(RB_EDEVICE, "context creation failed on device %d", device);
   }
   for (auto &e : c->ev) (void)hipEventCreate(&e);
+  for (auto &e : c->ev_side) (void)hipEventCreate(&e);
   *out = c;
   return RB_OK;
 }
@@ -691,8 +698,20 @@ static int pairwise_impl(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu
     if (probe == 2) ctx->last.main_kernel_bytes = ctx->last.kernel_bytes[0] = a->payload_bytes / 8192 * 8192;
     return rc;
   }
-  launch_pairwise(op, card_only, a->payload, b->payload, light, nlight, heavy, nheavy, res ? res->payload : nullptr,
-                  tm, st, ctx->ev[2]);
+  // the light and heavy task kernels run concurrently (heavy on the side stream, 1 block per CU;
+  // light 2 blocks per CU: 2 x 128 + 256 VGPRs per SIMD) unless RBGPU_SERIAL_TASKS is set
+  static const bool serial = getenv("RBGPU_SERIAL_TASKS") != nullptr;
+  const bool conc = !serial && nlight && nheavy;
+  if (conc) {
+    HIPCHK(hipStreamWaitEvent(ctx->side, ctx->ev[1], 0));
+    launch_pairwise_concurrent(op, card_only, a->payload, b->payload, light, nlight, heavy, nheavy,
+                               res ? res->payload : nullptr, tm, st, ctx->side, ctx->ev[2], ctx->ev_side[0],
+                               ctx->ev_side[1]);
+    HIPCHK(hipStreamWaitEvent(st, ctx->ev_side[1], 0));
+  } else {
+    launch_pairwise(op, card_only, a->payload, b->payload, light, nlight, heavy, nheavy, res ? res->payload : nullptr,
+                    tm, st, ctx->ev[2]);
+  }
   HIPCHK(hipEventRecord(ctx->ev[3], st));
   launch_compact_count(scn.task, ns, tm.type, rcnt, st);
   scan_exclusive(rcnt, rseg, ns, tmp, st);
@@ -704,8 +723,16 @@ static int pairwise_impl(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu
   if (np) HIPCHK(hipMemcpyAsync(ctx->h_pinned + 5, rseg + ns, 8, hipMemcpyDeviceToHost, st));
   else ctx->h_pinned[5] = 0;
   if (card_out && np) HIPCHK(hipMemcpyAsync(card_out, pcard, np * 8, hipMemcpyDeviceToHost, st));
-  const KernelSpan spans[2] = {{"k_pair_tasks<light>", 2, 4, nlight}, {"k_pair_tasks<heavy>", 3, 5, nheavy}};
-  rc = stats_end(ctx, ntasks, 0, spans, 2);
+  if (conc) {
+    // [0] the concurrent task phase (both kernels' bytes over the union of their spans), then each
+    const KernelSpan spans[3] = {{"k_pair_tasks<light>||<heavy>", 2, 4, ntasks, ctx->ev[1], ctx->ev[3], 3, 5},
+                                 {"k_pair_tasks<light>", 2, 4, nlight, ctx->ev[1], ctx->ev[2]},
+                                 {"k_pair_tasks<heavy>", 3, 5, nheavy, ctx->ev_side[0], ctx->ev_side[1]}};
+    rc = stats_end(ctx, ntasks, 0, spans, 3);
+  } else {
+    const KernelSpan spans[2] = {{"k_pair_tasks<light>", 2, 4, nlight}, {"k_pair_tasks<heavy>", 3, 5, nheavy}};
+    rc = stats_end(ctx, ntasks, 0, spans, 2);
+  }
   if (rc) return rc;
   const uint64_t nres = ctx->h_pinned[5];
   ctx->last.result_containers = nres;

@@ -90,7 +90,9 @@ inline size_t aligned256(size_t b) { return (b + 255) & ~size_t(255); }
 struct rbgpu_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
+  hipStream_t side = nullptr; // second stream: the heavy task kernel runs beside the light one
   hipEvent_t ev[6] = {};   // [0] call start, [1..n] around the compute kernels, [5] call end
+  hipEvent_t ev_side[2] = {}; // around the kernel on `side`
   rbg::DevPool pool;
   rbg::Workspace ws_pairs, ws_tasks, ws_segs; // per pair / per task / per merge-path segment
   uint64_t *d_stats = nullptr;  // [kStatWords * kStripes] striped algorithmic byte counters
@@ -127,10 +129,13 @@ int ensure_h_begin(const rbgpu_set *s);
 void stats_begin(rbgpu_ctx *ctx);
 // Compute-phase kernels k = 0..n-1 ran between events ev[1+k] and ev[2+k]; their algorithmic
 // bytes are d_stats[in_word[k]] + d_stats[out_word[k]] (-1: none).
+// A span may name its own events (e0, e1) and two more byte words (in2, out2: a concurrent pair).
 struct KernelSpan {
   const char *name;
   int in_word, out_word;
   uint64_t items;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  int in2 = -1, out2 = -1;
 };
 int stats_end(rbgpu_ctx *ctx, uint64_t tasks, uint64_t result_containers, const KernelSpan *k, int n);
 // wide.hip

@@ -58,6 +58,12 @@ void launch_pair_emit(const PairArgs &a, const PairCountArrays &scans, uint64_t 
 void launch_pairwise(int op, bool card_only, const uint8_t *pa, const uint8_t *pb, const TaskRec *light,
                      uint64_t nl, const TaskRec *heavy, uint64_t nh, uint8_t *out, const TaskMeta &tm,
                      hipStream_t st, hipEvent_t mid);
+// the same two kernels launched concurrently: heavy on `side` (1 block per CU, between ev_h0 / ev_h1),
+// light on `st` (2 blocks per CU, `light_done` recorded after it)
+void launch_pairwise_concurrent(int op, bool card_only, const uint8_t *pa, const uint8_t *pb, const TaskRec *light,
+                                uint64_t nl, const TaskRec *heavy, uint64_t nh, uint8_t *out, const TaskMeta &tm,
+                                hipStream_t st, hipStream_t side, hipEvent_t light_done, hipEvent_t ev_h0,
+                                hipEvent_t ev_h1);
 // measurement probes (rbgpu_internal_probe): mode 1 = task-order payload reads, 2 = streaming read
 void launch_probe(int op, int mode, const uint8_t *pa, const uint8_t *pb, uint64_t a_bytes, const TaskRec *recs,
                   uint64_t n, uint32_t *sink, unsigned blocks, hipStream_t st);

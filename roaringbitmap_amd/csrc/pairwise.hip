@@ -675,12 +675,24 @@ template <class K> static unsigned persistent_blocks(K kernel, uint64_t tasks) {
   return (unsigned)(want < cap ? want : cap);
 }
 
+static unsigned cu_count() {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (cus <= 0) cus = 256;
+  }
+  return (unsigned)cus;
+}
+// per_cu > 0: persistent grid of per_cu blocks per CU (concurrent launches share the CUs)
 template <int OP, bool CARD_ONLY, int ROLE>
 static void launch_tasks(const uint8_t *pa, const uint8_t *pb, const TaskRec *recs, uint64_t n, uint8_t *out,
-                         const TaskMeta &tm, hipStream_t st) {
+                         const TaskMeta &tm, hipStream_t st, unsigned per_cu = 0) {
   if (!n) return;
-  static unsigned cap = 0; // occupancy-derived grid cap, per template instance
-  if (!cap) cap = persistent_blocks(k_pair_tasks<OP, CARD_ONLY, ROLE>, ~0ull >> 8);
+  static unsigned occ_cap = 0; // occupancy-derived grid cap, per template instance
+  if (!occ_cap) occ_cap = persistent_blocks(k_pair_tasks<OP, CARD_ONLY, ROLE>, ~0ull >> 8);
+  const unsigned cap = per_cu ? std::min(occ_cap, per_cu * cu_count()) : occ_cap;
   const uint64_t want = (n + 3) / 4;
   const unsigned blocks = (unsigned)(want < cap ? want : cap);
   k_pair_tasks<OP, CARD_ONLY, ROLE><<<blocks, 256, 0, st>>>(pa, pb, recs, n, out, tm);
@@ -705,6 +717,37 @@ static void launch_op(bool card_only, const uint8_t *pa, const uint8_t *pb, cons
     }
   }
 #endif
+}
+#ifndef RBG_CONC_LIGHT_PER_CU
+#define RBG_CONC_LIGHT_PER_CU 2 // light blocks per CU beside the heavy kernel (2 x 128 VGPRs per SIMD)
+#endif
+#ifndef RBG_CONC_HEAVY_PER_CU
+#define RBG_CONC_HEAVY_PER_CU 1 // heavy blocks per CU (256 VGPRs per SIMD)
+#endif
+template <int OP>
+static void launch_op_concurrent(bool card_only, const uint8_t *pa, const uint8_t *pb, const TaskRec *light,
+                                 uint64_t nl, const TaskRec *heavy, uint64_t nh, uint8_t *out, const TaskMeta &tm,
+                                 hipStream_t st, hipStream_t side, hipEvent_t light_done, hipEvent_t ev_h0,
+                                 hipEvent_t ev_h1) {
+  // heavy first: its blocks need the larger register slot
+  (void)hipEventRecord(ev_h0, side);
+  if (card_only) launch_tasks<OP, true, kRoleHeavy>(pa, pb, heavy, nh, out, tm, side, RBG_CONC_HEAVY_PER_CU);
+  else launch_tasks<OP, false, kRoleHeavy>(pa, pb, heavy, nh, out, tm, side, RBG_CONC_HEAVY_PER_CU);
+  (void)hipEventRecord(ev_h1, side);
+  if (card_only) launch_tasks<OP, true, kRoleLight>(pa, pb, light, nl, out, tm, st, RBG_CONC_LIGHT_PER_CU);
+  else launch_tasks<OP, false, kRoleLight>(pa, pb, light, nl, out, tm, st, RBG_CONC_LIGHT_PER_CU);
+  (void)hipEventRecord(light_done, st);
+}
+void launch_pairwise_concurrent(int op, bool card_only, const uint8_t *pa, const uint8_t *pb, const TaskRec *light,
+                                uint64_t nl, const TaskRec *heavy, uint64_t nh, uint8_t *out, const TaskMeta &tm,
+                                hipStream_t st, hipStream_t side, hipEvent_t light_done, hipEvent_t ev_h0,
+                                hipEvent_t ev_h1) {
+  switch (op) {
+  case RB_AND: launch_op_concurrent<RB_AND>(card_only, pa, pb, light, nl, heavy, nh, out, tm, st, side, light_done, ev_h0, ev_h1); break;
+  case RB_OR: launch_op_concurrent<RB_OR>(card_only, pa, pb, light, nl, heavy, nh, out, tm, st, side, light_done, ev_h0, ev_h1); break;
+  case RB_XOR: launch_op_concurrent<RB_XOR>(card_only, pa, pb, light, nl, heavy, nh, out, tm, st, side, light_done, ev_h0, ev_h1); break;
+  default: launch_op_concurrent<RB_ANDNOT>(card_only, pa, pb, light, nl, heavy, nh, out, tm, st, side, light_done, ev_h0, ev_h1); break;
+  }
 }
 void launch_pairwise(int op, bool card_only, const uint8_t *pa, const uint8_t *pb, const TaskRec *light,
                      uint64_t nl, const TaskRec *heavy, uint64_t nh, uint8_t *out, const TaskMeta &tm,
