@@ -599,8 +599,12 @@ static int pairwise_impl(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu
   uint64_t *nseg_p = W.take<uint64_t>(np + 1), *seg_begin = W.take<uint64_t>(np + 1);
   uint64_t *pcard = W.take<uint64_t>(np + 1);
   uint64_t *ptmp = W.take<uint64_t>(std::max<uint64_t>(scan_tmp_words(np + 1), 1));
-  if (d_aidx || d_bidx) { // through pinned staging: a pageable copy would block the host
-    const size_t bytes = np * 4 * ((d_aidx != nullptr) + (d_bidx != nullptr));
+  // small batches: the merge-path segment counts come from the host CSR copies (no count kernel,
+  // scan and host read-back before the segment phase)
+  const uint32_t seg_keys = pairwise_seg_keys(a, b, np);
+  const bool host_segs = np && np <= 4096 && !ensure_h_begin(a) && !ensure_h_begin(b);
+  if (d_aidx || d_bidx || host_segs) { // through pinned staging: a pageable copy would block the host
+    const size_t bytes = np * 4 * ((d_aidx != nullptr) + (d_bidx != nullptr)) + (host_segs ? (np + 1) * 8 : 0);
     if (bytes > ctx->h_stage_cap) {
       if (ctx->h_stage) (void)hipHostFree(ctx->h_stage);
       ctx->h_stage = nullptr;
@@ -617,18 +621,35 @@ static int pairwise_impl(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu
     if (d_bidx) {
       std::memcpy(h, b_idx, np * 4);
       HIPCHK(hipMemcpyAsync(d_bidx, h, np * 4, hipMemcpyHostToDevice, st));
+      h += np * 4;
+    }
+    if (host_segs) {
+      uint64_t *sb = reinterpret_cast<uint64_t *>(h), acc = 0;
+      for (uint64_t p = 0; p < np; ++p) { // k_seg_count's formula
+        const uint32_t ai = a_idx ? a_idx[p] : (uint32_t)p, bi = b_idx ? b_idx[p] : (uint32_t)p;
+        const uint64_t nk = (a->h_begin[ai + 1] - a->h_begin[ai]) + (b->h_begin[bi + 1] - b->h_begin[bi]);
+        sb[p] = acc;
+        acc += (nk + seg_keys - 1) / seg_keys + (nk == 0);
+      }
+      sb[np] = acc;
+      HIPCHK(hipMemcpyAsync(seg_begin, sb, (np + 1) * 8, hipMemcpyHostToDevice, st));
     }
   }
   if (card_out && np) HIPCHK(hipMemsetAsync(pcard, 0, np * 8, st));
 
   stats_begin(ctx);
-  PairArgs pa{op, a->view(), b->view(), d_aidx, d_bidx, npairs, seg_begin, nullptr, 0, pairwise_seg_keys(a, b, np)};
-  launch_seg_count(pa, nseg_p, st);
-  scan_exclusive(nseg_p, seg_begin, np, ptmp, st);
+  PairArgs pa{op, a->view(), b->view(), d_aidx, d_bidx, npairs, seg_begin, nullptr, 0, seg_keys};
   uint64_t *const tot = ctx->h_pinned;
-  HIPCHK(hipMemcpyAsync(tot + 6, seg_begin + np, 8, hipMemcpyDeviceToHost, st));
-  HIPCHK(hipStreamSynchronize(st));
-  const uint64_t ns = np ? tot[6] : 0;
+  uint64_t ns = 0;
+  if (host_segs) {
+    ns = reinterpret_cast<const uint64_t *>(ctx->h_stage + np * 4 * ((d_aidx != nullptr) + (d_bidx != nullptr)))[np];
+  } else {
+    launch_seg_count(pa, nseg_p, st);
+    scan_exclusive(nseg_p, seg_begin, np, ptmp, st);
+    HIPCHK(hipMemcpyAsync(tot + 6, seg_begin + np, 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    ns = np ? tot[6] : 0;
+  }
   // ---- per segment: counts, scans, result counts / offsets
   need = aligned256(ns * 4) + 10 * aligned256((ns + 1) * 8) + aligned256(scan_tmp_words(ns + 1) * 8) + 256;
   if (ctx->ws_segs.reserve(need, st) != hipSuccess) return fail(RB_ENOMEM, "segment workspace");
@@ -701,7 +722,8 @@ static int pairwise_impl(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu
   // the light and heavy task kernels run concurrently (heavy on the side stream, 1 block per CU;
   // light 2 blocks per CU: 2 x 128 + 256 VGPRs per SIMD) unless RBGPU_SERIAL_TASKS is set
   static const bool serial = getenv("RBGPU_SERIAL_TASKS") != nullptr;
-  const bool conc = !serial && nlight && nheavy;
+  const bool conc = !serial && nlight && nheavy && nlight + nheavy >= 65536; // small batches: the
+                                                  // cross-stream waits cost more than the overlap
   if (conc) {
     HIPCHK(hipStreamWaitEvent(ctx->side, ctx->ev[1], 0));
     launch_pairwise_concurrent(op, card_only, a->payload, b->payload, light, nlight, heavy, nheavy,
