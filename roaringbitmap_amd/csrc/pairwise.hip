@@ -261,6 +261,9 @@ __device__ __forceinline__ RecU load_rec(const TaskRec *r) {
 #ifndef RBG_HEAVY_PERSISTENT
 #define RBG_HEAVY_PERSISTENT 1 // 0: the one-launch-sized-grid register path (k_pair_heavy_np)
 #endif
+#ifndef RBG_FILTER_TRANSPOSE
+#define RBG_FILTER_TRANSPOSE 1 // probe a row in value order (adjacent lanes, adjacent values)
+#endif
 #ifndef RBG_LIGHT_WAVES
 #define RBG_LIGHT_WAVES 4 // waves per SIMD of the copy + filter kernel (128 VGPRs)
 #endif
@@ -334,6 +337,9 @@ __global__ __launch_bounds__(256, ROLE == kRoleHeavy ? RBG_HEAVY_WAVES : RBG_LIG
     uint64_t n, uint8_t *__restrict__ out, TaskMeta tm) {
   __shared__ __attribute__((aligned(16))) uint32_t lds[4][2048];
   __shared__ __attribute__((aligned(16))) uint16_t stage[ROLE == kRoleLight ? 4 : 1][kStageVals];
+#if RBG_FILTER_TRANSPOSE
+  __shared__ uint4 tbuf[ROLE == kRoleLight ? 4 : 1][32]; // per-wave half-row transpose (filter_rows_transposed)
+#endif
   const int lane = lane_id();
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint64_t stride = (uint64_t)gridDim.x * 4;
@@ -430,8 +436,16 @@ __global__ __launch_bounds__(256, ROLE == kRoleHeavy ? RBG_HEAVY_WAVES : RBG_LIG
         const int nfc = (int)((tc.cp + 7) >> 3);
         uint16_t *o = CARD_ONLY ? nullptr : reinterpret_cast<uint16_t *>(dst);
         auto none = [](int) {};
+#if RBG_FILTER_TRANSPOSE
+        (void)nfc;
+        (void)none;
+        uint4 *tb = tbuf[ROLE == kRoleLight ? wv : 0];
+        c = OP == RB_ANDNOT ? filter_rows_transposed<true>(pq, (int)tc.cp, s, ob, tb, o, lane)
+                            : filter_rows_transposed<false>(pq, (int)tc.cp, s, ob, tb, o, lane);
+#else
         c = OP == RB_ANDNOT ? filter_chunks_staged<true>(pq, nfc, (int)tc.cp, s, ob, o, lane, none)
                             : filter_chunks_staged<false>(pq, nfc, (int)tc.cp, s, ob, o, lane, none);
+#endif
         ty = c ? kArray : kEmpty;
       } else {
         ty = tc.tp;

@@ -346,13 +346,13 @@ __device__ __forceinline__ void ballot_scan4(uint32_t cnt, uint32_t &excl, uint3
 
 // The same filter with coalesced output.  Kept values are ranked into a per-wave LDS ring `ob` of
 // kStageRing u16 (16-B aligned); after each row every complete 16-B block of ranked values is
-// written with one 16-B-per-lane store.  At most 7 + 512 values are pending, so a ring of 640
-// never overwrites a pending value, and a block never straddles the wrap (640 % 8 == 0).  One
+// written with one 16-B-per-lane store.  At most 7 + 512 values are pending, so a ring of 576
+// never overwrites a pending value, and a block never straddles the wrap (576 % 8 == 0).  One
 // wave's LDS operations execute in order, so the ranked writes, the block reads and the next
 // row's writes need no drains between them.  The final partial block is written whole: result
 // slots are round16(2 * bound) bytes, so bytes past the last value stay in the slot's padding.
 // Rejected values go to a per-lane dummy slot instead of being branched around.
-constexpr int kStageRing = 640;
+constexpr int kStageRing = 576; // >= 7 + 512 pending values, a multiple of 8
 constexpr int kStageVals = kStageRing + 64;   // + one dummy slot per lane
 // `reload(i)` is called once per row i as soon as fq[i] is free — right after the row's values are
 // in registers, or at the start for rows this payload does not have — so the caller can stream the
@@ -405,6 +405,60 @@ __device__ __forceinline__ int filter_chunks_staged(uint4 (&fq)[8], int nfc, int
         flushed = full;
       }
       tot += rowtot;
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  if (out && tot > flushed && lane == 0) out4[flushed >> 3] = ob4[(flushed >> 3) % (kStageRing / 8)];
+  return (int)tot;
+}
+
+// The staged filter with the row transposed before probing: a row's 512 values arrive as chunks of
+// 8 consecutive values per lane, so in chunk order the 64 lanes of one probe instruction read
+// words ~8 values apart — for a sparse F that is a fixed stride of many words and a 16-way LDS bank
+// conflict (SQ_LDS_BANK_CONFLICT ≈ 13 extra cycles per probe, profiles/r01/v7).  Written once to a
+// per-wave 1 KiB buffer `tb` and read back as value 64k + lane, adjacent lanes probe adjacent
+// values (nearby or shared words).  Kept values are then ranked per k by one ballot, which also
+// keeps them in sorted order for the same ring / 16-B block flush as filter_chunks_staged.
+template <bool NEGATE>
+__device__ __forceinline__ int filter_rows_transposed(const uint4 (&fq)[8], int nf, const uint32_t *s, uint16_t *ob,
+                                                      uint4 *tb, uint16_t *out, int lane) {
+  const int iters = (nf + 511) >> 9; // wave-uniform, <= 8
+  uint32_t flushed = 0, tot = 0;
+  uint4 *out4 = reinterpret_cast<uint4 *>(out);
+  const uint4 *ob4 = reinterpret_cast<const uint4 *>(ob);
+  const uint16_t *t16 = reinterpret_cast<const uint16_t *>(tb);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    if (i < iters) {
+      // two halves of 256 values (lanes 0-31's chunks, then lanes 32-63's) through a 512-B buffer
+#pragma unroll
+      for (int hf = 0; hf < 2; ++hf) {
+        if ((lane >> 5) == hf) tb[lane & 31] = fq[i];
+        wave_lds_sync(); // other lanes' stores: without the fence the compiler may reuse the last reads
+        const int nh = min(256, nf - 512 * i - 256 * hf); // values of this half (may be <= 0)
+        uint32_t y[4], m[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) y[k] = t16[64 * k + lane];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) m[k] = s[y[k] >> 5];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const bool keep = ((((m[k] >> (y[k] & 31)) & 1) ^ (NEGATE ? 1u : 0u)) != 0) && (64 * k + lane < nh);
+          const uint64_t b = __ballot(keep);
+          if (out) {
+            const uint32_t pos = (tot + mbcnt64(b)) % (uint32_t)kStageRing;
+            ob[keep ? pos : (uint32_t)(kStageRing + lane)] = (uint16_t)y[k];
+          }
+          tot += (uint32_t)__popcll(b);
+        }
+      }
+      if (out) {
+        wave_lds_sync(); // the blocks hold other lanes' ranked values
+        const uint32_t full = tot & ~7u; // values in complete blocks
+        const uint32_t nb = (full - flushed) >> 3, b0 = flushed >> 3;
+        if ((uint32_t)lane < nb) out4[b0 + lane] = ob4[(b0 + lane) % (uint32_t)(kStageRing / 8)];
+        flushed = full;
+      }
     }
     __builtin_amdgcn_sched_barrier(0);
   }
