@@ -48,10 +48,8 @@ template <int M> __device__ __forceinline__ uint32_t xor_lane(uint32_t v, int la
   else if constexpr (M == 3) return dpp_mov<0x1B>(v);     // quad_perm [3,2,1,0]
   else if constexpr (M == 7) return dpp_mov<0x141>(v);    // row_half_mirror
   else if constexpr (M == 15) return dpp_mov<0x140>(v);   // row_mirror
-  else if constexpr (M == 4 || M == 8) {
-    const uint32_t up = dpp_mov<0x100 + M>(v), dn = dpp_mov<0x110 + M>(v); // row_shl / row_shr
-    return (lane & M) ? dn : up;
-  } else if constexpr (M < 32) {
+  else if constexpr (M == 8) return dpp_mov<0x128>(v);    // row_ror:8 (swap the halves of a row of 16)
+  else if constexpr (M < 32) {                            // 4, 16, 31: swizzle (xor mode)
     return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x1F | (M << 10));
   } else {
     return (uint32_t)__builtin_amdgcn_ds_bpermute((lane ^ M) << 2, (int)v);
@@ -60,13 +58,21 @@ template <int M> __device__ __forceinline__ uint32_t xor_lane(uint32_t v, int la
 
 // one cross-lane compare-exchange step of the bitonic merge: FLIP pairs element e with element 7-e
 // of lane (lane ^ M) (M = 2^j - 1), otherwise element e with element e of lane (lane ^ M).
+// median of (a, b, c): with c = 0 it is min(a, b), with c = ~0 it is max(a, b) — one VALU op for
+// the lower lane's min / the upper lane's max instead of min + max + select
+__device__ __forceinline__ uint32_t med3_u32(uint32_t a, uint32_t b, uint32_t c) {
+  uint32_t r;
+  asm("v_med3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
 template <int M, bool FLIP> __device__ __forceinline__ void cross_step(uint32_t (&k)[8], int lane) {
   const bool lower = FLIP ? (lane & ((M + 1) >> 1)) == 0 : (lane & M) == 0;
+  const uint32_t sel = lower ? 0u : 0xFFFFFFFFu;
   uint32_t t[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) t[e] = xor_lane<M>(k[FLIP ? 7 - e : e], lane);
 #pragma unroll
-  for (int e = 0; e < 8; ++e) k[e] = lower ? min(k[e], t[e]) : max(k[e], t[e]);
+  for (int e = 0; e < 8; ++e) k[e] = med3_u32(k[e], t[e], sel);
 }
 __device__ __forceinline__ void inlane_merge(uint32_t (&k)[8]) {
 #pragma unroll
