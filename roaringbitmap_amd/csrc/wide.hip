@@ -130,6 +130,19 @@ __global__ __launch_bounds__(256) void k_group_base(const uint32_t *Hc, uint64_t
 #ifndef RBG_GROUP_STAGE
 #define RBG_GROUP_STAGE 0
 #endif
+// Dense members (every member holds all 65536 keys: container index = begin + key) need no sort:
+// key k's containers are begin[mem[i]] + k in member order, seg[k] = (k - key_lo) * M.
+__global__ __launch_bounds__(256) void k_group_dense(const uint64_t *__restrict__ begin, const uint32_t *__restrict__ mem,
+                                                     uint32_t M, uint32_t key_lo, uint32_t key_hi, uint64_t *seg,
+                                                     uint32_t *cid) {
+  const uint64_t krange = key_hi - key_lo, n = krange * M;
+  for (uint64_t t = (uint64_t)blockIdx.x * 256 + threadIdx.x; t < n; t += (uint64_t)gridDim.x * 256) {
+    const uint64_t kr = t / M, i = t - kr * M;
+    cid[t] = (uint32_t)(begin[mem[i]] + key_lo + kr);
+  }
+  for (uint64_t k = (uint64_t)blockIdx.x * 256 + threadIdx.x; k <= 65536; k += (uint64_t)gridDim.x * 256)
+    seg[k] = (k < key_lo ? 0 : k >= key_hi ? krange : k - key_lo) * M;
+}
 __global__ __launch_bounds__(256) void k_group_scatter(GroupArgs a, const uint64_t *H, uint32_t *cid) {
   __shared__ unsigned long long mask[kGrpKeys];
   __shared__ uint64_t gbase[kGrpKeys], mbase[kGrpMembers];
@@ -535,15 +548,23 @@ int wide_run(rbgpu_ctx *ctx, int sem, const rbgpu_set *in, const std::vector<uin
   if (M) HIPCHK(hipMemcpyAsync(d_mem, members.data(), M * 4ull, hipMemcpyHostToDevice, st));
   const SetView sv = in->view();
   const GroupArgs ga{sv, d_mem, d_bnd, M, MB, KR, nkr, key_lo, key_hi};
-  if (M && nkr) {
-    k_group_bounds<<<nblk((uint64_t)M * (nkr + 1), 256), 256, 0, st>>>(ga, d_bnd);
-    k_group_count<<<dim3(nkr, nmb), 256, 0, st>>>(ga, d_Hc);
-  }
-  k_group_totals<<<nblk(65537, 256), 256, 0, st>>>(d_Hc, M && nkr ? nmb : 0, key_lo, key_hi, d_tot);
-  scan_exclusive(d_tot, d_seg, 65536, d_tmp, st);
-  if (M && nkr) {
-    k_group_base<<<nblk(krange, 256), 256, 0, st>>>(d_Hc, d_H, nmb, key_lo, key_hi, d_seg);
-    k_group_scatter<<<dim3(nkr, nmb), 256, 0, st>>>(ga, d_H, d_cid2);
+  static const bool no_dense = getenv("RBGPU_NO_DENSE_GROUPING") != nullptr;
+  bool dense = M && nkr && !no_dense;
+  for (uint32_t i = 0; dense && i < M; ++i) dense = in->h_begin[members[i] + 1] - in->h_begin[members[i]] == 65536;
+  if (dense) {
+    k_group_dense<<<(unsigned)std::min<uint64_t>(nblk((uint64_t)krange * M, 256), 65536), 256, 0, st>>>(
+        sv.begin, d_mem, M, key_lo, key_hi, d_seg, d_cid2);
+  } else {
+    if (M && nkr) {
+      k_group_bounds<<<nblk((uint64_t)M * (nkr + 1), 256), 256, 0, st>>>(ga, d_bnd);
+      k_group_count<<<dim3(nkr, nmb), 256, 0, st>>>(ga, d_Hc);
+    }
+    k_group_totals<<<nblk(65537, 256), 256, 0, st>>>(d_Hc, M && nkr ? nmb : 0, key_lo, key_hi, d_tot);
+    scan_exclusive(d_tot, d_seg, 65536, d_tmp, st);
+    if (M && nkr) {
+      k_group_base<<<nblk(krange, 256), 256, 0, st>>>(d_Hc, d_H, nmb, key_lo, key_hi, d_seg);
+      k_group_scatter<<<dim3(nkr, nmb), 256, 0, st>>>(ga, d_H, d_cid2);
+    }
   }
   k_wide_select<<<nblk(65536, 256), 256, 0, st>>>(d_seg, and_sem ? (uint64_t)M : 0, key_lo, key_hi, d_active);
   scan_exclusive(d_active, d_apos, 65536, d_tmp, st);
