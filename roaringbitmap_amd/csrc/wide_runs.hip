@@ -87,6 +87,10 @@ __global__ __launch_bounds__(256) void k_wide_runs(SetView s, const uint32_t *__
     if (lane == 0) route[q] = 1;
     return;
   }
+  if (hi > lo && s.type[cid[lo]] != kRun) { // first container not a Run: route before any batch load
+    if (lane == 0) route[q] = 1;
+    return;
+  }
   lds_zero(acc, lane);
   wave_lds_sync();
   // accumulator state (wave-uniform)

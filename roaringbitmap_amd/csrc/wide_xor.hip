@@ -186,6 +186,10 @@ __global__ __launch_bounds__(256) void k_wide_runs_xor(SetView s, const uint32_t
   uint2 *MC = reinterpret_cast<uint2 *>(R);         // [512] (coverage mask, c0 | c1 << 16)
   const uint32_t key = klist[q];
   const uint64_t lo = seg[key], hi = seg[key + 1];
+  if (hi > lo && s.type[cid[lo]] != kRun) { // first container not a Run: route before any batch load
+    if (lane == 0) route[q] = 1;
+    return;
+  }
   lds_zero(acc, lane);
   wave_lds_sync();
   const int cj = lane >> 1, h = lane & 1;
