@@ -272,6 +272,195 @@ __global__ __launch_bounds__(256, 2) void k_bsi_chain(SetView bsi, SetView fnd, 
   }
 }
 
+// ---- RANGE fused: both O'Neil chains (GE(start) and LE(end)) walk the slices in ONE pass, so every
+// slice container is staged once for the two comparators; the keyed static AND of the two results
+// (RoaringBitmapSliceIndex.java:492-497; AND rule R&R -> EFF else AB, empty / one-sided dropped)
+// closes the kernel.  Each chain keeps its own EQ (registers) and GT / LT accumulator (LDS image)
+// with the same per-step type rules as k_bsi_chain.
+// One chain step (k_bsi_chain's loop body after the slice is staged): TRACK 1 = GT (GE), 2 = LT (LE).
+__device__ __forceinline__ void bsi_step(uint64_t (&e)[kW], Meta &eq, Meta &x, uint32_t *sX, int bit, int track,
+                                         bool spresent, const Meta &sm, const uint32_t *sS, int lane) {
+  if (!eq.present) return; // and/andNot of an absent EQ stay absent; GT/LT unchanged
+  const bool feeds = (track == 2 && bit) || (track == 1 && !bit);
+  uint64_t t[kW];
+#pragma unroll
+  for (int j = 0; j < kW; ++j) {
+    const uint64_t sw = spresent ? lds_word(sS, j, lane) : 0ull;
+    t[j] = bit ? (e[j] & ~sw) : (e[j] & sw);
+    e[j] = bit ? (e[j] & sw) : (e[j] & ~sw);
+  }
+  wave_lds_sync();
+  Meta tm{0, 0, 0, 0};
+  if (!spresent) {
+    if (bit) {
+      tm = eq;        // andNot(EQ, absent) = clone of EQ
+      eq.present = 0; // and(EQ, absent) = absent
+    }
+  } else {
+    const Meta e0 = eq;
+    if (feeds) tm = classify(t, lane, bit ? eff_andnot(e0, sm) : eff_and(e0, sm), false, false);
+    eq = classify(e, lane, bit ? eff_and(e0, sm) : eff_andnot(e0, sm), false, false);
+  }
+  if (feeds && tm.present) {
+    if (!x.present) {
+      lds_write_words(sX, t, lane); // or(absent, t) = clone of t
+      x = tm;
+    } else {
+      const Meta x0 = x;
+#pragma unroll
+      for (int j = 0; j < kW; ++j) t[j] |= lds_word(sX, j, lane);
+      x = classify(t, lane, eff_or(x0, tm), lr_or(x0, tm), true);
+      lds_write_words(sX, t, lane);
+    }
+    wave_lds_sync();
+  }
+}
+// GE / LE result of one chain: Y = or(GT|LT, EQ), then and(Y, fixedFoundSet) (F staged in sS)
+__device__ __forceinline__ Meta bsi_final_ge_le(uint64_t (&t)[kW], const uint64_t (&e)[kW], const Meta &eq,
+                                                const Meta &x, const uint32_t *sX, const Meta &fm,
+                                                const uint32_t *sS, int lane) {
+  Meta ym = x;
+#pragma unroll
+  for (int j = 0; j < kW; ++j) t[j] = x.present ? lds_word(sX, j, lane) : 0ull;
+  if (!x.present) {
+#pragma unroll
+    for (int j = 0; j < kW; ++j) t[j] = e[j];
+    ym = eq;
+  } else if (eq.present) {
+#pragma unroll
+    for (int j = 0; j < kW; ++j) t[j] |= e[j];
+    ym = classify(t, lane, eff_or(x, eq), lr_or(x, eq), true);
+  }
+  Meta rm{0, 0, 0, 0};
+  if (ym.present) {
+#pragma unroll
+    for (int j = 0; j < kW; ++j) t[j] &= lds_word(sS, j, lane);
+    rm = classify(t, lane, eff_and(ym, fm), false, false);
+  }
+  return rm;
+}
+__global__ __launch_bounds__(128, 2) void k_bsi_range(SetView bsi, SetView fnd, int has_found,
+                                                      const int32_t *__restrict__ table, uint32_t nbits,
+                                                      uint64_t start, uint64_t end, const uint32_t *__restrict__ klist,
+                                                      uint32_t nk, uint8_t *__restrict__ out, WideOut wo,
+                                                      uint64_t *stats) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds[2][3][2048];
+  const int lane = lane_id();
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t q = blockIdx.x * 2 + wv;
+  if (q >= nk) return;
+  uint32_t *sS = lds[wv][0], *sG = lds[wv][1], *sL = lds[wv][2];
+  const uint32_t key = klist[q];
+  uint64_t inb = 0;
+  uint64_t eg[kW], el[kW];
+  Meta eqg = stage_global(bsi, table[(uint64_t)nbits * 65536 + key], sS, lane);
+  if (eqg.present) {
+    lds_read_words(sS, eg, lane);
+    inb += payload_bytes(eqg.type, eqg.card, eqg.runs) + 16; // ebM, read once for both comparators
+  } else {
+#pragma unroll
+    for (int j = 0; j < kW; ++j) eg[j] = 0;
+  }
+#pragma unroll
+  for (int j = 0; j < kW; ++j) el[j] = eg[j];
+  Meta eql = eqg;
+  wave_lds_sync();
+  Meta xg{0, 0, 0, 0}, xl{0, 0, 0, 0};
+  const int32_t sc = lane < (int)nbits ? table[(uint64_t)lane * 65536 + key] : -1;
+  int st = 0;
+  uint32_t scard = 0, sruns = 0;
+  uint64_t soff = 0;
+  if (sc >= 0) {
+    st = bsi.type[sc];
+    scard = bsi.card[sc];
+    sruns = bsi.nruns[sc];
+    soff = bsi.off[sc];
+  }
+  auto sbytes = [&](int i) -> uint32_t {
+    const int t = (int)readlane((uint32_t)st, i);
+    return (uint32_t)payload_bytes(t, readlane(scard, i), readlane(sruns, i));
+  };
+  auto sptr = [&](int i) -> const uint8_t * {
+    return bsi.payload + pack2(readlane((uint32_t)soff, i), readlane((uint32_t)(soff >> 32), i));
+  };
+  uint4 pq[8];
+  if (nbits) {
+    const int i0 = (int)nbits - 1;
+    const bool ok = (int)readlane((uint32_t)sc, i0) >= 0 && sbytes(i0) <= (uint32_t)kBitmapBytes;
+    load_chunks(pq, ok ? sptr(i0) : bsi.payload, ok ? sbytes(i0) : 16u, lane);
+  }
+  for (int i = (int)nbits - 1; i >= 0; --i) {
+    const bool spresent = (int)readlane((uint32_t)sc, i) >= 0;
+    Meta sm{0, 0, 0, 0};
+    if (spresent) {
+      sm.present = 1;
+      sm.type = (int)readlane((uint32_t)st, i);
+      sm.card = (int)readlane(scard, i);
+      sm.runs = (int)readlane(sruns, i);
+      inb += payload_bytes(sm.type, sm.card, sm.runs) + 16; // one read serves both comparators
+      if (payload_bytes(sm.type, sm.card, sm.runs) > (uint64_t)kBitmapBytes) {
+        lds_zero(sS, lane);
+        wave_lds_sync();
+        const uint32_t *r32 = reinterpret_cast<const uint32_t *>(sptr(i));
+        for (int k = lane; k < sm.runs; k += 64) toggle_run(sS, r32[k]);
+        wave_lds_sync();
+        toggles_to_words_lds(sS, lane);
+        wave_lds_sync();
+      } else {
+        stage_from_chunks(sm.type, pq, (uint32_t)sm.card, (uint32_t)sm.runs, sS, lane);
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    if (i > 0) {
+      const bool ok = (int)readlane((uint32_t)sc, i - 1) >= 0 && sbytes(i - 1) <= (uint32_t)kBitmapBytes;
+      load_chunks(pq, ok ? sptr(i - 1) : bsi.payload, ok ? sbytes(i - 1) : 16u, lane);
+    }
+    bsi_step(eg, eqg, xg, sG, (int)((start >> i) & 1), 1, spresent, sm, sS, lane);
+    bsi_step(el, eql, xl, sL, (int)((end >> i) & 1), 2, spresent, sm, sS, lane);
+  }
+  // ---- the final ops with the found set F (foundSet, or ebM when null), per chain
+  const int32_t fc = has_found ? table[(uint64_t)(nbits + 1) * 65536 + key] : table[(uint64_t)nbits * 65536 + key];
+  const Meta fm = stage_global(has_found ? fnd : bsi, fc, sS, lane);
+  if (has_found) inb += payload_bytes(fm.type, fm.card, fm.runs) + 16;
+  // EQ = and(fixedFoundSet, EQ), both chains
+  if (eqg.present) {
+    const Meta e0 = eqg;
+#pragma unroll
+    for (int j = 0; j < kW; ++j) eg[j] &= lds_word(sS, j, lane);
+    eqg = classify(eg, lane, eff_and(fm, e0), false, false);
+  }
+  if (eql.present) {
+    const Meta e0 = eql;
+#pragma unroll
+    for (int j = 0; j < kW; ++j) el[j] &= lds_word(sS, j, lane);
+    eql = classify(el, lane, eff_and(fm, e0), false, false);
+  }
+  uint64_t t[kW];
+  const Meta rg = bsi_final_ge_le(t, eg, eqg, xg, sG, fm, sS, lane);
+  wave_lds_sync();
+  lds_write_words(sG, t, lane); // GE result parked in its (now free) accumulator image
+  wave_lds_sync();
+  const Meta rl = bsi_final_ge_le(t, el, eql, xl, sL, fm, sS, lane);
+  Meta rm{0, 0, 0, 0};
+  if (rg.present && rl.present) {
+#pragma unroll
+    for (int j = 0; j < kW; ++j) t[j] &= lds_word(sG, j, lane);
+    rm = classify(t, lane, eff_and(rg, rl), false, false);
+  }
+  wave_lds_sync();
+  const int ty = rm.present ? rm.type : kEmpty;
+  if (rm.present) emit_container(ty, t, rm.card, rm.runs, out + (uint64_t)q * kBitmapBytes, sS, lane);
+  if (lane == 0) {
+    wo.type[q] = (uint8_t)ty;
+    wo.card[q] = (uint32_t)(rm.present ? rm.card : 0);
+    wo.nruns[q] = (uint16_t)(ty == kRun ? rm.runs : 0);
+    if (inb) atomicAdd((unsigned long long *)&stats[0 * kStripes + (q & (kStripes - 1))], (unsigned long long)inb);
+    if (rm.present)
+      atomicAdd((unsigned long long *)&stats[1 * kStripes + (q & (kStripes - 1))],
+                (unsigned long long)(payload_bytes(ty, rm.card, rm.runs) + (ty == kRun ? 2 : 0) + 16));
+  }
+}
+
 // RANGE = and(GE(start), LE(end)) (RoaringBitmapSliceIndex.java:492-497) on the two chains' keyed
 // slots: both are indexed by the same key list, so the static AND is one wave per key (AND rule:
 // R&R -> EFF, else AB; empty or one-sided -> dropped).
@@ -420,14 +609,21 @@ int bsi_compare(rbgpu_ctx *ctx, const rbgpu_set *bsi, int op, uint64_t start, ui
     release();
     return rc;
   }
+  static const bool no_fuse = getenv("RBGPU_BSI_UNFUSED_RANGE") != nullptr;
+  const bool fused_range = op == 6 && !no_fuse;
   KeyedSlots fin, ge, le;
   rc = fin.alloc(ctx, nk, false);
-  if (!rc && op == 6) rc = ge.alloc(ctx, nk, true);
-  if (!rc && op == 6) rc = le.alloc(ctx, nk, true);
+  if (!rc && op == 6 && !fused_range) rc = ge.alloc(ctx, nk, true);
+  if (!rc && op == 6 && !fused_range) rc = le.alloc(ctx, nk, true);
   if (!rc) {
     HIPCHK(hipEventRecord(ctx->ev[1], st));
     if (op != 6) {
       bsi_chain(ctx, bsi, nbits, op, start, found, d_table, d_klist, nk, res->payload, fin.wo);
+    } else if (fused_range) { // RANGE: both chains in one pass, then the keyed static AND in-kernel
+      if (nk)
+        k_bsi_range<<<nblk(nk, 2), 128, 0, st>>>(bsi->view(), found ? found->view() : bsi->view(), found != nullptr,
+                                                 d_table, nbits, start, end, d_klist, nk, res->payload, fin.wo,
+                                                 ctx->d_stats);
     } else { // RANGE: the two chains, then the keyed static AND
       bsi_chain(ctx, bsi, nbits, kBsiGE, start, found, d_table, d_klist, nk, ge.payload, ge.wo);
       bsi_chain(ctx, bsi, nbits, kBsiLE, end, found, d_table, d_klist, nk, le.payload, le.wo);
@@ -437,11 +633,11 @@ int bsi_compare(rbgpu_ctx *ctx, const rbgpu_set *bsi, int op, uint64_t start, ui
     HIPCHK(hipEventRecord(ctx->ev[2], st));
     uint64_t nres = 0;
     rc = compact_keyed(ctx, d_klist, nk, fin.wo, res, &nres);
-    const KernelSpan spans[1] = {{"k_bsi_chain", 0, 1, op == 6 ? 2ull * nk : nk}};
+    const KernelSpan spans[1] = {{fused_range ? "k_bsi_range" : "k_bsi_chain", 0, 1, op == 6 ? 2ull * nk : nk}};
     if (!rc) rc = stats_end(ctx, nk, nres, spans, 1);
   }
   fin.release(ctx, false);
-  if (op == 6) {
+  if (op == 6 && !fused_range) {
     ge.release(ctx, true);
     le.release(ctx, true);
   }
