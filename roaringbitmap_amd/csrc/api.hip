@@ -601,8 +601,12 @@ static int pairwise_impl(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu
   uint64_t *ptmp = W.take<uint64_t>(std::max<uint64_t>(scan_tmp_words(np + 1), 1));
   // small batches: the merge-path segment counts come from the host CSR copies (no count kernel,
   // scan and host read-back before the segment phase)
-  const uint32_t seg_keys = pairwise_seg_keys(a, b, np);
   const bool host_segs = np && np <= 4096 && !ensure_h_begin(a) && !ensure_h_begin(b);
+  uint32_t seg_keys = pairwise_seg_keys(a, b, np);
+  if (host_segs) { // latency study knob: merge-path segment length of small batches
+    static const int sk = getenv("RBGPU_SMALL_SEG_KEYS") ? atoi(getenv("RBGPU_SMALL_SEG_KEYS")) : 0;
+    if (sk > 0) seg_keys = (uint32_t)sk;
+  }
   if (d_aidx || d_bidx || host_segs) { // through pinned staging: a pageable copy would block the host
     const size_t bytes = np * 4 * ((d_aidx != nullptr) + (d_bidx != nullptr)) + (host_segs ? (np + 1) * 8 : 0);
     if (bytes > ctx->h_stage_cap) {
