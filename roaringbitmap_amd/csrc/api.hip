@@ -89,6 +89,28 @@ int ensure_h_begin(const rbgpu_set *cs) {
   HIPCHK(hipStreamSynchronize(s->ctx->stream));
   return RB_OK;
 }
+// Sets are immutable, so the largest per-bitmap container count is computed once (host CSR if it
+// is already here, else one reduction kernel + read-back) and cached.
+int ensure_max_keys(const rbgpu_set *cs) {
+  rbgpu_set *s = const_cast<rbgpu_set *>(cs);
+  if (s->max_keys >= 0) return RB_OK;
+  uint64_t m = 0;
+  if (s->h_begin.size() == (size_t)s->nb + 1) {
+    for (uint32_t i = 0; i < s->nb; ++i) m = std::max<uint64_t>(m, s->h_begin[i + 1] - s->h_begin[i]);
+  } else if (s->nb) {
+    HIPCHK(hipSetDevice(s->ctx->device));
+    uint64_t *d = nullptr;
+    if (s->ctx->pool.alloc((void **)&d, 8)) return fail(RB_ENOMEM, "max-keys word");
+    HIPCHK(hipMemsetAsync(d, 0, 8, s->ctx->stream));
+    launch_max_span(s->begin, s->nb, d, s->ctx->stream);
+    HIPCHK(hipMemcpyAsync(s->ctx->h_pinned + 7, d, 8, hipMemcpyDeviceToHost, s->ctx->stream));
+    HIPCHK(hipStreamSynchronize(s->ctx->stream));
+    s->ctx->pool.release(d);
+    m = s->ctx->h_pinned[7];
+  }
+  s->max_keys = (int64_t)m;
+  return RB_OK;
+}
 } // namespace rbg
 
 namespace {
@@ -645,8 +667,14 @@ static int pairwise_impl(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu
   PairArgs pa{op, a->view(), b->view(), d_aidx, d_bidx, npairs, seg_begin, nullptr, 0, seg_keys};
   uint64_t *const tot = ctx->h_pinned;
   uint64_t ns = 0;
+  // one segment per pair when no pair can exceed seg_keys merged keys (config 2: <= 8 keys per
+  // pair): seg_begin is the identity and the count kernel, its scan and the read-back are skipped
+  const bool ident_segs = !host_segs && np && !a_idx && !b_idx && !ensure_max_keys(a) && !ensure_max_keys(b) &&
+                          (uint64_t)(a->max_keys + b->max_keys) <= seg_keys;
   if (host_segs) {
     ns = reinterpret_cast<const uint64_t *>(ctx->h_stage + np * 4 * ((d_aidx != nullptr) + (d_bidx != nullptr)))[np];
+  } else if (ident_segs) {
+    ns = np;
   } else {
     launch_seg_count(pa, nseg_p, st);
     scan_exclusive(nseg_p, seg_begin, np, ptmp, st);
@@ -655,7 +683,7 @@ static int pairwise_impl(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu
     ns = np ? tot[6] : 0;
   }
   // ---- per segment: counts, scans, result counts / offsets
-  need = aligned256(ns * 4) + 10 * aligned256((ns + 1) * 8) + aligned256(scan_tmp_words(ns + 1) * 8) + 256;
+  need = aligned256(ns * 4) + 10 * aligned256((ns + 1) * 8) + aligned256(scan_multi_tmp_words(ns + 1, 4) * 8) + 256;
   if (ctx->ws_segs.reserve(need, st) != hipSuccess) return fail(RB_ENOMEM, "segment workspace");
   Workspace &G = ctx->ws_segs;
   uint32_t *seg_pair = G.take<uint32_t>(std::max<uint64_t>(ns, 1));
@@ -664,9 +692,10 @@ static int pairwise_impl(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu
   PairCountArrays scn{G.take<uint64_t>(ns + 1), G.take<uint64_t>(ns + 1), G.take<uint64_t>(ns + 1),
                       G.take<uint64_t>(ns + 1)};
   uint64_t *rcnt = G.take<uint64_t>(ns + 1), *rseg = G.take<uint64_t>(ns + 1);
-  uint64_t *tmp = G.take<uint64_t>(std::max<uint64_t>(scan_tmp_words(ns + 1), 1));
+  uint64_t *tmp = G.take<uint64_t>(std::max<uint64_t>(scan_multi_tmp_words(ns + 1, 4), 1));
   uint64_t *d_tot = G.take<uint64_t>(4);
-  launch_seg_fill(pa, seg_begin, seg_pair, st);
+  if (ident_segs) launch_seg_identity(np, seg_begin, seg_pair, st);
+  else launch_seg_fill(pa, seg_begin, seg_pair, st);
   pa.seg_pair = seg_pair;
   pa.nseg = ns;
   launch_pair_count(pa, cnt, ctx->d_stats, st);

@@ -6,6 +6,7 @@ namespace rbg {
 
 // ---- scan.hip
 uint64_t scan_tmp_words(uint64_t n);
+uint64_t scan_multi_tmp_words(uint64_t n, int k);
 void scan_exclusive(const uint64_t *in, uint64_t *out, uint64_t n, uint64_t *tmp, hipStream_t st);
 // k scans of n words each (k <= 4); totals[i] = out[i][n].  One launch when n fits one block.
 void scan_exclusive_multi(const uint64_t *const *in, uint64_t *const *out, int k, uint64_t n, uint64_t *tmp,
@@ -47,6 +48,8 @@ struct PairCountArrays {
 // merge-path segments of every pair (<= 256 merged keys each): counts, then the segment -> pair map
 void launch_seg_count(const PairArgs &a, uint64_t *nseg, hipStream_t st);
 void launch_seg_fill(const PairArgs &a, const uint64_t *seg_begin, uint32_t *seg_pair, hipStream_t st);
+void launch_seg_identity(uint64_t np, uint64_t *seg_begin, uint32_t *seg_pair, hipStream_t st);
+void launch_max_span(const uint64_t *begin, uint32_t nb, uint64_t *out, hipStream_t st);
 void launch_pair_rbegin(const uint64_t *seg_begin, uint32_t npairs, const uint64_t *rseg, uint64_t *rbegin,
                         hipStream_t st);
 // per segment from here on

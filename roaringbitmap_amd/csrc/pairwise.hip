@@ -102,6 +102,20 @@ __global__ __launch_bounds__(kPairThreads) void k_seg_fill(PairArgs a, const uin
   for (uint64_t s = seg_begin[p]; s < seg_begin[p + 1]; ++s) seg_pair[s] = p;
 }
 
+__global__ __launch_bounds__(kPairThreads) void k_seg_identity(uint64_t np, uint64_t *seg_begin, uint32_t *seg_pair) {
+  const uint64_t p = (uint64_t)blockIdx.x * kPairThreads + threadIdx.x;
+  if (p <= np) seg_begin[p] = p;
+  if (p < np) seg_pair[p] = (uint32_t)p;
+}
+// largest begin[i+1] - begin[i] (containers of one bitmap), atomicMax into *out (zeroed)
+__global__ __launch_bounds__(kPairThreads) void k_max_span(const uint64_t *begin, uint32_t nb, uint64_t *out) {
+  uint64_t m = 0;
+  for (uint64_t i = (uint64_t)blockIdx.x * kPairThreads + threadIdx.x; i < nb; i += (uint64_t)gridDim.x * kPairThreads)
+    m = max(m, begin[i + 1] - begin[i]);
+  for (int d = 32; d; d >>= 1) m = max(m, (uint64_t)__shfl_xor((unsigned long long)m, d));
+  if ((threadIdx.x & 63) == 0 && m) atomicMax((unsigned long long *)out, (unsigned long long)m);
+}
+
 // inb[0]: key bytes, inb[1]: light-task input bytes, inb[2]: heavy-task input bytes
 template <bool EMIT>
 __device__ __forceinline__ void pair_walk(const PairArgs &a, uint64_t sg, PairCounts &n, uint64_t (&inb)[3],
@@ -662,6 +676,13 @@ void launch_seg_count(const PairArgs &a, uint64_t *nseg, hipStream_t st) {
 void launch_seg_fill(const PairArgs &a, const uint64_t *seg_begin, uint32_t *seg_pair, hipStream_t st) {
   if (!a.npairs) return;
   k_seg_fill<<<blocks_for(a.npairs, kPairThreads), kPairThreads, 0, st>>>(a, seg_begin, seg_pair);
+}
+void launch_seg_identity(uint64_t np, uint64_t *seg_begin, uint32_t *seg_pair, hipStream_t st) {
+  k_seg_identity<<<blocks_for(np + 1, kPairThreads), kPairThreads, 0, st>>>(np, seg_begin, seg_pair);
+}
+void launch_max_span(const uint64_t *begin, uint32_t nb, uint64_t *out, hipStream_t st) {
+  const unsigned blocks = std::min<unsigned>(blocks_for(nb, kPairThreads), 1024);
+  k_max_span<<<blocks, kPairThreads, 0, st>>>(begin, nb, out);
 }
 void launch_pair_rbegin(const uint64_t *seg_begin, uint32_t npairs, const uint64_t *rseg, uint64_t *rbegin,
                         hipStream_t st) {

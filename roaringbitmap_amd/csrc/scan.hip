@@ -64,6 +64,12 @@ uint64_t scan_tmp_words(uint64_t n) {
   return 2 * (nb + 1) + scan_tmp_words(nb);
 }
 
+// tmp words for scan_exclusive_multi over k arrays of n
+uint64_t scan_multi_tmp_words(uint64_t n, int k) {
+  const uint64_t per = kScanThreads * kScanItems, nb = (n + per - 1) / per;
+  return std::max<uint64_t>(scan_tmp_words(n), 2 * (uint64_t)k * (nb + 1));
+}
+
 void scan_exclusive(const uint64_t *in, uint64_t *out, uint64_t n, uint64_t *tmp, hipStream_t st) {
   const uint64_t per = kScanThreads * kScanItems;
   uint64_t nb = (n + per - 1) / per;
@@ -108,6 +114,44 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_multi(Multi m, uint64_t n
     totals[blockIdx.y] = total;
   }
 }
+// partials of array blockIdx.y at tmp + y * stride
+__global__ __launch_bounds__(kScanThreads) void k_scan_partials_multi(Multi m, uint64_t n, uint64_t *tmp,
+                                                                      uint64_t stride) {
+  __shared__ uint64_t sh[4];
+  const uint64_t *in = m.in[blockIdx.y];
+  const uint64_t base = (uint64_t)blockIdx.x * kScanThreads * kScanItems + threadIdx.x * kScanItems;
+  uint64_t s = 0;
+#pragma unroll
+  for (int i = 0; i < kScanItems; ++i)
+    if (base + i < n) s += in[base + i];
+  uint64_t total;
+  block_excl_scan(s, sh, total);
+  if (threadIdx.x == 0) tmp[blockIdx.y * stride + blockIdx.x] = total;
+}
+// out[y][i] = scanned block offset + in-block exclusive scan; the last block writes out[y][n] from
+// the array's total (pm.out[y][nb], written by k_scan_multi)
+__global__ __launch_bounds__(kScanThreads) void k_scan_apply_multi(Multi m, uint64_t n, Multi pm,
+                                                                   const uint64_t *totals) {
+  __shared__ uint64_t sh[4];
+  const uint64_t *in = m.in[blockIdx.y];
+  uint64_t *out = m.out[blockIdx.y];
+  const uint64_t off = pm.out[blockIdx.y][blockIdx.x];
+  const uint64_t base = (uint64_t)blockIdx.x * kScanThreads * kScanItems + threadIdx.x * kScanItems;
+  uint64_t v[kScanItems], s = 0;
+#pragma unroll
+  for (int i = 0; i < kScanItems; ++i) {
+    v[i] = base + i < n ? in[base + i] : 0;
+    s += v[i];
+  }
+  uint64_t total;
+  uint64_t run = block_excl_scan(s, sh, total) + off;
+#pragma unroll
+  for (int i = 0; i < kScanItems; ++i) {
+    if (base + i < n) out[base + i] = run;
+    run += v[i];
+  }
+  if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) out[n] = totals[blockIdx.y];
+}
 __global__ void k_gather_totals(Multi m, uint64_t n, uint64_t *totals) { totals[threadIdx.x] = m.out[threadIdx.x][n]; }
 
 void scan_exclusive_multi(const uint64_t *const *in, uint64_t *const *out, int k, uint64_t n, uint64_t *tmp,
@@ -119,6 +163,21 @@ void scan_exclusive_multi(const uint64_t *const *in, uint64_t *const *out, int k
   }
   if (n <= (uint64_t)kScanThreads * kScanItems) {
     k_scan_multi<<<dim3(1, k), kScanThreads, 0, st>>>(m, n, totals);
+    return;
+  }
+  const uint64_t per = kScanThreads * kScanItems, nb = (n + per - 1) / per;
+  if (nb <= per) {
+    // two levels for all k arrays at once: block partials (grid nb x k), one block per array scans
+    // its partials (and writes the totals), then every block applies its offset — 3 launches
+    // instead of 3k + 1 (config 2: 1M segments, 4 count arrays)
+    Multi pm{};
+    for (int i = 0; i < k; ++i) {
+      pm.in[i] = tmp + i * (nb + 1);
+      pm.out[i] = tmp + (k + i) * (nb + 1);
+    }
+    k_scan_partials_multi<<<dim3((unsigned)nb, k), kScanThreads, 0, st>>>(m, n, tmp, nb + 1);
+    k_scan_multi<<<dim3(1, k), kScanThreads, 0, st>>>(pm, nb, totals);
+    k_scan_apply_multi<<<dim3((unsigned)nb, k), kScanThreads, 0, st>>>(m, n, pm, totals);
     return;
   }
   for (int i = 0; i < k; ++i) scan_exclusive(in[i], out[i], n, tmp, st);
