@@ -712,7 +712,7 @@ static int pairwise_impl(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu
   const uint64_t nt1 = std::max<uint64_t>(ntasks, 1);
   size_t tneed = aligned256(std::max<uint64_t>(nlight, 1) * sizeof(TaskRec)) +
                  aligned256(std::max<uint64_t>(nheavy, 1) * sizeof(TaskRec)) + 2 * aligned256(nt1 * 2) +
-                 2 * aligned256(nt1) + aligned256(nt1 * 4) + aligned256(nt1 * 8) + 256;
+                 2 * aligned256(nt1) + aligned256(nt1 * 4) + aligned256(nt1 * 8) + aligned256(8) + 256;
   if (ctx->ws_tasks.reserve(tneed, st) != hipSuccess)
     return fail(RB_ENOMEM, "task workspace (%llu tasks)", (unsigned long long)ntasks);
   Workspace &T = ctx->ws_tasks;
@@ -725,6 +725,7 @@ static int pairwise_impl(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu
   tm.cat = T.take<uint8_t>(nt1);
   tm.card = T.take<uint32_t>(nt1);
   tm.out = T.take<uint64_t>(nt1);
+  unsigned long long *queue = T.take<unsigned long long>(1); // light-task chunk counter
 
   rbgpu_set *res = nullptr;
   if (!card_only) {
@@ -755,14 +756,18 @@ static int pairwise_impl(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu
   // the light and heavy task kernels run concurrently (heavy on the side stream, 1 block per CU;
   // light 2 blocks per CU: 2 x 128 + 256 VGPRs per SIMD) unless RBGPU_SERIAL_TASKS is set
   static const bool serial = getenv("RBGPU_SERIAL_TASKS") != nullptr;
+  // light tasks from a shared chunk queue (a second light launch takes over the heavy kernel's CUs
+  // when it finishes) unless RBGPU_STATIC_LIGHT is set
+  static const bool static_light = getenv("RBGPU_STATIC_LIGHT") != nullptr;
   const bool conc = !serial && nlight && nheavy && nlight + nheavy >= 65536; // small batches: the
                                                   // cross-stream waits cost more than the overlap
   if (conc) {
     HIPCHK(hipStreamWaitEvent(ctx->side, ctx->ev[1], 0));
     launch_pairwise_concurrent(op, card_only, a->payload, b->payload, light, nlight, heavy, nheavy,
                                res ? res->payload : nullptr, tm, st, ctx->side, ctx->ev[2], ctx->ev_side[0],
-                               ctx->ev_side[1]);
-    HIPCHK(hipStreamWaitEvent(st, ctx->ev_side[1], 0));
+                               ctx->ev_side[1], static_light ? nullptr : queue);
+    HIPCHK(hipEventRecord(ctx->ev_side[2], ctx->side));
+    HIPCHK(hipStreamWaitEvent(st, ctx->ev_side[2], 0));
   } else {
     launch_pairwise(op, card_only, a->payload, b->payload, light, nlight, heavy, nheavy, res ? res->payload : nullptr,
                     tm, st, ctx->ev[2]);

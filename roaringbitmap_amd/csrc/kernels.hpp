@@ -66,7 +66,7 @@ void launch_pairwise(int op, bool card_only, const uint8_t *pa, const uint8_t *p
 void launch_pairwise_concurrent(int op, bool card_only, const uint8_t *pa, const uint8_t *pb, const TaskRec *light,
                                 uint64_t nl, const TaskRec *heavy, uint64_t nh, uint8_t *out, const TaskMeta &tm,
                                 hipStream_t st, hipStream_t side, hipEvent_t light_done, hipEvent_t ev_h0,
-                                hipEvent_t ev_h1);
+                                hipEvent_t ev_h1, unsigned long long *queue);
 // measurement probes (rbgpu_internal_probe): mode 1 = task-order payload reads, 2 = streaming read
 void launch_probe(int op, int mode, const uint8_t *pa, const uint8_t *pb, uint64_t a_bytes, const TaskRec *recs,
                   uint64_t n, uint32_t *sink, unsigned blocks, hipStream_t st);

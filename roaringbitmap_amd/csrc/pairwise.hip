@@ -336,6 +336,98 @@ template <int OP> __device__ __forceinline__ void word_op(uint64_t &a, uint64_t 
   else a &= ~b;
 }
 
+// Run AND Run as an interval intersection (RunContainer.and(RunContainer), RunContainer.java:381-456):
+// the two-pointer walk over both run lists advances the list whose current run ends first (A on
+// ties), i.e. it visits the states of a merge of the two lists by run END.  Each lane takes an
+// equal stretch of that merge (merge-path split by binary search over the runs staged in LDS),
+// counts the overlapping pairs and their lengths, and after a wave scan writes its intersections as
+// Run pairs.  Intersections of canonical run lists are never adjacent (two consecutive ones lie in
+// different runs of A or of B, which leave a gap), so they are the result's maximal runs: c and r
+// are exact.  Returns false (nothing written) when EFF(c, r) is not Run — the caller then builds the
+// register bitmap.  Needs round4(ra) + rb <= 2048 (both lists in the wave's 8 KiB scratch).
+__device__ __forceinline__ uint32_t run_end(uint32_t x) { return (x & 0xFFFF) + (x >> 16); }
+template <bool CARD_ONLY>
+__device__ __forceinline__ bool and_runs_intervals(const uint4 (&pq)[8], const uint4 (&qq)[8], uint32_t ra,
+                                                   uint32_t rb, uint32_t *s, uint8_t *dst, int lane, int &card,
+                                                   int &runs) {
+  const uint32_t oa = (ra + 3) & ~3u;
+  uint4 *s4 = reinterpret_cast<uint4 *>(s);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const uint32_t c = (uint32_t)(lane + 64 * i);
+    if (4 * c < ra) s4[c] = pq[i];
+    if (4 * c < rb) s4[oa / 4 + c] = qq[i];
+  }
+  wave_lds_sync();
+  const uint32_t *SA = s, *SB = s + oa;
+  const uint32_t total = ra + rb, per = (total + 63) >> 6;
+  const uint32_t d0 = min((uint32_t)lane * per, total), d1 = min(d0 + per, total);
+  uint32_t lo = d0 > rb ? d0 - rb : 0, hi = min(d0, ra);
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (run_end(SA[mid]) <= run_end(SB[d0 - mid - 1])) lo = mid + 1;
+    else hi = mid;
+  }
+  const uint32_t i0 = lo, j0 = d0 - lo;
+  uint32_t cnt = 0, sum = 0;
+  {
+    uint32_t i = i0, j = j0;
+    uint32_t a = i < ra ? SA[i] : 0, b = j < rb ? SB[j] : 0;
+    for (uint32_t d = d0; d < d1 && i < ra && j < rb; ++d) {
+      const uint32_t ea = run_end(a), eb = run_end(b);
+      const uint32_t st = max(a & 0xFFFF, b & 0xFFFF), en = min(ea, eb);
+      if (st <= en) {
+        ++cnt;
+        sum += en - st + 1;
+      }
+      if (ea <= eb) {
+        ++i;
+        a = i < ra ? SA[i] : 0;
+      } else {
+        ++j;
+        b = j < rb ? SB[j] : 0;
+      }
+    }
+  }
+  card = (int)wave_sum_u32(sum);
+  runs = (int)wave_sum_u32(cnt);
+  if (CARD_ONLY || card == 0) return true;
+  if (type_eff(card, runs) != kRun) {
+    wave_lds_sync(); // the register path restages this scratch
+    return false;
+  }
+  uint32_t pos = wave_scan_u32(cnt, lane) - cnt;
+  uint32_t *o = reinterpret_cast<uint32_t *>(dst);
+  uint32_t i = i0, j = j0;
+  uint32_t a = i < ra ? SA[i] : 0, b = j < rb ? SB[j] : 0;
+  for (uint32_t d = d0; d < d1 && i < ra && j < rb; ++d) {
+    const uint32_t ea = run_end(a), eb = run_end(b);
+    const uint32_t st = max(a & 0xFFFF, b & 0xFFFF), en = min(ea, eb);
+    if (st <= en) o[pos++] = st | ((en - st) << 16);
+    if (ea <= eb) {
+      ++i;
+      a = i < ra ? SA[i] : 0;
+    } else {
+      ++j;
+      b = j < rb ? SB[j] : 0;
+    }
+  }
+  wave_lds_sync();
+  return true;
+}
+#ifndef RBG_RUN_INTERVALS
+#define RBG_RUN_INTERVALS 1 // Run AND Run by interval intersection (0: always the register bitmap)
+#endif
+
+constexpr uint64_t kQueueChunk = 8;
+// first task of the next chunk: one vector atomic by lane 0, broadcast (wave-uniform)
+__device__ __forceinline__ uint64_t claim_chunk(unsigned long long *queue, int lane) {
+  unsigned long long v = 0;
+  if (lane == 0) v = __hip_atomic_fetch_add(queue, (unsigned long long)kQueueChunk, __ATOMIC_RELAXED,
+                                            __HIP_MEMORY_SCOPE_AGENT);
+  return pack2(__builtin_amdgcn_readfirstlane((uint32_t)v), __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)));
+}
+
 // The task kernel, ONE WAVE PER TASK, persistent waves striding over one record list with a
 // one-task software pipeline: the next task's record and both payloads are in flight while the
 // current one computes.  Loads sit at fixed points of the loop body (a task with fewer payloads
@@ -348,7 +440,7 @@ enum { kRoleLight = 0, kRoleHeavy = 1 };
 template <int OP, bool CARD_ONLY, int ROLE>
 __global__ __launch_bounds__(256, ROLE == kRoleHeavy ? RBG_HEAVY_WAVES : RBG_LIGHT_WAVES) void k_pair_tasks(
     const uint8_t *__restrict__ pay_a, const uint8_t *__restrict__ pay_b, const TaskRec *__restrict__ recs,
-    uint64_t n, uint8_t *__restrict__ out, TaskMeta tm) {
+    uint64_t n, uint8_t *__restrict__ out, TaskMeta tm, unsigned long long *queue) {
   __shared__ __attribute__((aligned(16))) uint32_t lds[4][2048];
   __shared__ __attribute__((aligned(16))) uint16_t stage[ROLE == kRoleLight ? 4 : 1][kStageVals];
 #if RBG_FILTER_TRANSPOSE
@@ -356,8 +448,17 @@ __global__ __launch_bounds__(256, ROLE == kRoleHeavy ? RBG_HEAVY_WAVES : RBG_LIG
 #endif
   const int lane = lane_id();
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  // static schedule (queue == nullptr): wave w takes tasks w, w + stride, ...; dynamic: chunks of
+  // kQueueChunk consecutive tasks from a device counter shared by every launch on it (the
+  // concurrent phase's second light launch fills the CUs the heavy kernel leaves), the next chunk
+  // claimed one chunk ahead so the atomic's latency is hidden
   const uint64_t stride = (uint64_t)gridDim.x * 4;
-  uint64_t g = (uint64_t)blockIdx.x * 4 + wv;
+  uint64_t g = (uint64_t)blockIdx.x * 4 + wv, cend = 0, nxt = 0;
+  if (queue) {
+    g = claim_chunk(queue, lane);
+    cend = g + kQueueChunk;
+    nxt = claim_chunk(queue, lane);
+  }
   if (g >= n) return;
   uint32_t *s = lds[wv];
   uint16_t *ob = stage[ROLE == kRoleLight ? wv : 0];
@@ -368,14 +469,38 @@ __global__ __launch_bounds__(256, ROLE == kRoleHeavy ? RBG_HEAVY_WAVES : RBG_LIG
   if (tc.kind == kCopy || tc.bigq) load_chunks(qq, tc.pp, 16, lane);
   else load_chunks(qq, tc.pq, tc.qbytes, lane);
   while (true) {
-    const uint64_t gn = g + stride;
+    uint64_t gn = g + stride;
+    bool new_chunk = false;
+    if (queue) {
+      gn = g + 1;
+      if (gn >= cend) { // wave-uniform branch: only here is the claimed chunk waited for
+        gn = nxt;
+        new_chunk = true;
+      }
+    }
     const bool has_next = gn < n;
     const RecU nx = load_rec(recs + (has_next ? gn : g));
     const Task tn = decode_task<OP>(nx, pay_a, pay_b);
     int ty = kEmpty, c = 0;
     uint32_t nr = 0;
     uint8_t *dst = out + cur.out;
-    if (ROLE == kRoleHeavy) {
+    bool done = false;
+    if (ROLE == kRoleHeavy && RBG_RUN_INTERVALS && OP == RB_AND && tc.tp == kRun && tc.tq == kRun && !tc.bigp &&
+        !tc.bigq && ((tc.rp + 3) & ~3u) + tc.rq <= 2048u) {
+      int r = 0;
+      done = and_runs_intervals<CARD_ONLY>(pq, qq, tc.rp, tc.rq, s, dst, lane, c, r);
+      if (done) {
+        ty = c == 0 ? kEmpty : CARD_ONLY ? kArray : kRun;
+        nr = ty == kRun ? (uint32_t)r : 0u;
+        __builtin_amdgcn_sched_barrier(0);
+        {
+          const bool real = has_next && !tn.bigq;
+          load_chunks(qq, real ? tn.pq : tn.pp, real ? tn.qbytes : 16u, lane);
+        }
+        load_chunks(pq, tn.pp, tn.bigp ? 16u : tn.pbytes, lane);
+      }
+    }
+    if (ROLE == kRoleHeavy && !done) {
       // ---- the result as a register bitmap: P = A, Q = B (never swapped: ANDNOT and the type
       //      rules are ordered)
       uint64_t w[kW];
@@ -430,7 +555,7 @@ __global__ __launch_bounds__(256, ROLE == kRoleHeavy ? RBG_HEAVY_WAVES : RBG_LIG
       if (CARD_ONLY) ty = c ? kArray : kEmpty;
       else if (ty != kEmpty) emit_container(ty, w, c, r, dst, s, lane);
       nr = ty == kRun ? (uint32_t)r : 0u;
-    } else {
+    } else if (ROLE != kRoleHeavy) {
       // ---- phase 1: stage X (filter) or store the clone (copy)
       if (tc.kind == kFilter) {
         if (tc.bigq) stage_big_runs(tc.pq, tc.rq, s, lane); // only a Run payload exceeds 8 KiB
@@ -475,6 +600,10 @@ __global__ __launch_bounds__(256, ROLE == kRoleHeavy ? RBG_HEAVY_WAVES : RBG_LIG
       tm.nruns[cur.t] = (uint16_t)nr;
     }
     if (!has_next) break;
+    if (new_chunk) {
+      cend = gn + kQueueChunk;
+      nxt = claim_chunk(queue, lane);
+    }
     g = gn;
     cur = nx;
     tc = tn;
@@ -723,14 +852,15 @@ static unsigned cu_count() {
 // per_cu > 0: persistent grid of per_cu blocks per CU (concurrent launches share the CUs)
 template <int OP, bool CARD_ONLY, int ROLE>
 static void launch_tasks(const uint8_t *pa, const uint8_t *pb, const TaskRec *recs, uint64_t n, uint8_t *out,
-                         const TaskMeta &tm, hipStream_t st, unsigned per_cu = 0) {
+                         const TaskMeta &tm, hipStream_t st, unsigned per_cu = 0,
+                         unsigned long long *queue = nullptr) {
   if (!n) return;
   static unsigned occ_cap = 0; // occupancy-derived grid cap, per template instance
   if (!occ_cap) occ_cap = persistent_blocks(k_pair_tasks<OP, CARD_ONLY, ROLE>, ~0ull >> 8);
   const unsigned cap = per_cu ? std::min(occ_cap, per_cu * cu_count()) : occ_cap;
   const uint64_t want = (n + 3) / 4;
   const unsigned blocks = (unsigned)(want < cap ? want : cap);
-  k_pair_tasks<OP, CARD_ONLY, ROLE><<<blocks, 256, 0, st>>>(pa, pb, recs, n, out, tm);
+  k_pair_tasks<OP, CARD_ONLY, ROLE><<<blocks, 256, 0, st>>>(pa, pb, recs, n, out, tm, queue);
 }
 template <int OP>
 static void launch_op(bool card_only, const uint8_t *pa, const uint8_t *pb, const TaskRec *light, uint64_t nl,
@@ -763,25 +893,32 @@ template <int OP>
 static void launch_op_concurrent(bool card_only, const uint8_t *pa, const uint8_t *pb, const TaskRec *light,
                                  uint64_t nl, const TaskRec *heavy, uint64_t nh, uint8_t *out, const TaskMeta &tm,
                                  hipStream_t st, hipStream_t side, hipEvent_t light_done, hipEvent_t ev_h0,
-                                 hipEvent_t ev_h1) {
+                                 hipEvent_t ev_h1, unsigned long long *queue) {
   // heavy first: its blocks need the larger register slot
   (void)hipEventRecord(ev_h0, side);
   if (card_only) launch_tasks<OP, true, kRoleHeavy>(pa, pb, heavy, nh, out, tm, side, RBG_CONC_HEAVY_PER_CU);
   else launch_tasks<OP, false, kRoleHeavy>(pa, pb, heavy, nh, out, tm, side, RBG_CONC_HEAVY_PER_CU);
   (void)hipEventRecord(ev_h1, side);
-  if (card_only) launch_tasks<OP, true, kRoleLight>(pa, pb, light, nl, out, tm, st, RBG_CONC_LIGHT_PER_CU);
-  else launch_tasks<OP, false, kRoleLight>(pa, pb, light, nl, out, tm, st, RBG_CONC_LIGHT_PER_CU);
+  // light tasks from a shared queue: one launch beside the heavy kernel, a second one on the side
+  // stream once the heavy kernel is done (its waves take whatever tasks are left)
+  if (queue) (void)hipMemsetAsync(queue, 0, sizeof(*queue), st);
+  if (card_only) launch_tasks<OP, true, kRoleLight>(pa, pb, light, nl, out, tm, st, RBG_CONC_LIGHT_PER_CU, queue);
+  else launch_tasks<OP, false, kRoleLight>(pa, pb, light, nl, out, tm, st, RBG_CONC_LIGHT_PER_CU, queue);
   (void)hipEventRecord(light_done, st);
+  if (queue) {
+    if (card_only) launch_tasks<OP, true, kRoleLight>(pa, pb, light, nl, out, tm, side, RBG_CONC_LIGHT_PER_CU, queue);
+    else launch_tasks<OP, false, kRoleLight>(pa, pb, light, nl, out, tm, side, RBG_CONC_LIGHT_PER_CU, queue);
+  }
 }
 void launch_pairwise_concurrent(int op, bool card_only, const uint8_t *pa, const uint8_t *pb, const TaskRec *light,
                                 uint64_t nl, const TaskRec *heavy, uint64_t nh, uint8_t *out, const TaskMeta &tm,
                                 hipStream_t st, hipStream_t side, hipEvent_t light_done, hipEvent_t ev_h0,
-                                hipEvent_t ev_h1) {
+                                hipEvent_t ev_h1, unsigned long long *queue) {
   switch (op) {
-  case RB_AND: launch_op_concurrent<RB_AND>(card_only, pa, pb, light, nl, heavy, nh, out, tm, st, side, light_done, ev_h0, ev_h1); break;
-  case RB_OR: launch_op_concurrent<RB_OR>(card_only, pa, pb, light, nl, heavy, nh, out, tm, st, side, light_done, ev_h0, ev_h1); break;
-  case RB_XOR: launch_op_concurrent<RB_XOR>(card_only, pa, pb, light, nl, heavy, nh, out, tm, st, side, light_done, ev_h0, ev_h1); break;
-  default: launch_op_concurrent<RB_ANDNOT>(card_only, pa, pb, light, nl, heavy, nh, out, tm, st, side, light_done, ev_h0, ev_h1); break;
+  case RB_AND: launch_op_concurrent<RB_AND>(card_only, pa, pb, light, nl, heavy, nh, out, tm, st, side, light_done, ev_h0, ev_h1, queue); break;
+  case RB_OR: launch_op_concurrent<RB_OR>(card_only, pa, pb, light, nl, heavy, nh, out, tm, st, side, light_done, ev_h0, ev_h1, queue); break;
+  case RB_XOR: launch_op_concurrent<RB_XOR>(card_only, pa, pb, light, nl, heavy, nh, out, tm, st, side, light_done, ev_h0, ev_h1, queue); break;
+  default: launch_op_concurrent<RB_ANDNOT>(card_only, pa, pb, light, nl, heavy, nh, out, tm, st, side, light_done, ev_h0, ev_h1, queue); break;
   }
 }
 void launch_pairwise(int op, bool card_only, const uint8_t *pa, const uint8_t *pb, const TaskRec *light,

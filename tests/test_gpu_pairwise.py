@@ -148,3 +148,62 @@ def test_large_pairs_merge_path_segments(ctx, oracle):
             ref = oracle.op(op, refs[a_idx[i]], refs[b_idx[i]])
             assert got[i] == ref.serialize(), (opname, i)
             assert int(cards[i]) == ref.cardinality(), (opname, i)
+
+
+def _run_values(rng, nruns, lo=0, hi=65536, full=False):
+    """Sorted values of `nruns` random non-adjacent runs inside [lo, hi) (one container)."""
+    if full:
+        return np.arange(lo, hi, dtype=np.uint32)
+    cuts = np.sort(rng.choice(np.arange(lo, hi + 1), size=2 * nruns, replace=False))
+    starts, ends = cuts[0::2], cuts[1::2]  # [start, end) with end < next start: gaps >= 1
+    return np.concatenate([np.arange(s, e, dtype=np.uint32) for s, e in zip(starts, ends)])
+
+
+@pytest.mark.parametrize("seed", [5, 6])
+def test_run_and_run_interval_path(ctx, oracle, seed):
+    """Run AND Run takes the interval-intersection path when EFF says Run and both lists fit the
+    wave's scratch, else the register bitmap: every run count / overlap shape against the oracle
+    (RunContainer.and(RunContainer), RunContainer.java:381-456)."""
+    rng = np.random.default_rng(seed)
+    bms = []
+    for r in (1, 2, 3, 7, 64, 100, 511, 1000, 1023, 1024, 1500, 2000, 2047):
+        bms.append(_run_values(rng, r))
+    bms.append(_run_values(rng, 0, full=True))                          # one run over the whole key
+    bms.append(np.arange(65000, 65536, dtype=np.uint32))                # run ending at 65535
+    bms.append(np.arange(0, 300, dtype=np.uint32))                      # run starting at 0
+    bms.append(np.concatenate([np.arange(0, 10), np.arange(65530, 65536)]).astype(np.uint32))
+    bms.append(_run_values(rng, 20, 30000, 31000))                     # narrow: small intersections
+    bms.append(_run_values(rng, 900, 0, 8000))                          # short runs: Array/Bitmap results
+    s = ctx.upload_values(bms, run_optimize=True)
+    refs = _ref_list(oracle, s.serialize())
+    n = len(bms)
+    a_idx = np.repeat(np.arange(n), n).astype(np.uint32)
+    b_idx = np.tile(np.arange(n), n).astype(np.uint32)
+    out = ctx.pairwise(OPS["AND"], s, s, a_idx, b_idx)
+    got = out.serialize()
+    cards = ctx.pairwise_cardinality(OPS["AND"], s, s, a_idx, b_idx)
+    for i in range(len(a_idx)):
+        ref = oracle.op(OPS["AND"], refs[a_idx[i]], refs[b_idx[i]])
+        assert got[i] == ref.serialize(), (int(a_idx[i]), int(b_idx[i]))
+        assert int(cards[i]) == ref.cardinality(), (int(a_idx[i]), int(b_idx[i]))
+
+
+def test_identity_segments_large_batch(ctx, oracle):
+    """> 4096 index-free pairs of few-key bitmaps: one merge-path segment per pair (identity
+    seg_begin, no count kernel) and the fused multi-array scan; every op against the oracle."""
+    base_a = synthetic_bitmaps(50, seed=31)
+    base_b = synthetic_bitmaps(50, seed=32)
+    a_vals = [base_a[i % 50] for i in range(5000)]
+    b_vals = [base_b[(7 * i) % 50] for i in range(5000)]
+    a = ctx.upload_values(a_vals, run_optimize=True)
+    b = ctx.upload_values(b_vals, run_optimize=True)
+    ra = _ref_list(oracle, a.serialize()[:50])
+    rbs = _ref_list(oracle, b.serialize()[:50])
+    for opname, op in OPS.items():
+        got = ctx.pairwise(op, a, b).serialize()
+        cards = ctx.pairwise_cardinality(op, a, b)
+        assert len(got) == 5000
+        for i in range(0, 5000, 7):
+            ref = oracle.op(op, ra[i % 50], rbs[i % 50])  # b_vals[i] == b_vals[i % 50]
+            assert got[i] == ref.serialize(), (opname, i)
+            assert int(cards[i]) == ref.cardinality(), (opname, i)
