@@ -36,21 +36,30 @@ TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r01", "traffic.json")
 def pair_traffic(op, main_name):
     """PMC HBM bytes per launch of the pairwise task phase: light, heavy, or both when they run
     concurrently (the span "k_pair_tasks<light>||<heavy>")."""
-    lt = pmc_traffic(f"rbg::k_pair_tasks<{op}, false, 0>")
-    hv = pmc_traffic(f"rbg::k_pair_tasks<{op}, false, 1>")
+    lt = pmc_traffic(f"rbg::k_pair_tasks<{op}, false, 0>", True)
+    hv = pmc_traffic(f"rbg::k_pair_tasks<{op}, false, 1>", True)
     if "||" in main_name:
-        return lt + hv if lt is not None and hv is not None else None
-    return lt if "light" in main_name else hv
+        # the concurrent phase launches the light kernel twice (beside the heavy kernel, then on the
+        # side stream after it; one task queue): its bytes per phase = all light dispatches' bytes
+        # over the number of phases (= heavy dispatches)
+        if lt is None or hv is None:
+            return None
+        return int(lt[0] * lt[1] / max(hv[1], 1)) + hv[0]
+    x = lt if "light" in main_name else hv
+    return x[0] if x else None
 
 
-def pmc_traffic(pmc_name: str):
+def pmc_traffic(pmc_name: str, with_count: bool = False):
     """HBM bytes per launch of `pmc_name` from the committed rocprofv3 PMC summary of this same bench
     command (scripts/traffic.py: FETCH_SIZE x2 for gfx950 16-B/lane reads + WRITE_SIZE, separate
     passes); the dominant (largest) dispatch group is the headline launch.  None if not profiled."""
     try:
         with open(TRAFFIC_JSON) as f:
             groups = json.load(f)["kernels"].get(pmc_name)
-        return int(groups[0]["traffic_bytes"]) if groups else None
+        if not groups:
+            return None
+        return (int(groups[0]["traffic_bytes"]), int(groups[0]["dispatches"])) if with_count else \
+            int(groups[0]["traffic_bytes"])
     except (OSError, ValueError, KeyError):
         return None
 

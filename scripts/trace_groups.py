@@ -26,10 +26,12 @@ for (name, grid), d in sorted(groups.items(), key=lambda kv: -sum(e - s for s, e
 lt = sorted(x for (n, g), v in groups.items() if n.endswith("0>") and "k_pair_tasks" in n for x in v)
 hv = sorted(x for (n, g), v in groups.items() if n.endswith("1>") and "k_pair_tasks" in n for x in v)
 spans = []
-for s, e in lt:
-    for s2, e2 in hv:
-        if s2 < e and s < e2:
-            spans.append((max(e, e2) - min(s, s2)) / 1e6)
+for s2, e2 in hv:
+    # the light launch beside the heavy kernel, and the second light launch that starts on the side
+    # stream when the heavy kernel ends (both take tasks from one queue)
+    ph = [(s, e) for s, e in lt if s < e2 + 50_000 and e > s2]
+    if ph:
+        spans.append((max([e2] + [e for _, e in ph]) - min([s2] + [s for s, _ in ph])) / 1e6)
 if spans:
     big = [x for x in spans if x >= 0.5 * max(spans)]
     print(f"  headline-size spans: n={len(big)} avg_ms={sum(big) / len(big):.4f}")
