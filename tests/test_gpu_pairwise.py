@@ -207,3 +207,25 @@ def test_identity_segments_large_batch(ctx, oracle):
             ref = oracle.op(op, ra[i % 50], rbs[i % 50])  # b_vals[i] == b_vals[i % 50]
             assert got[i] == ref.serialize(), (opname, i)
             assert int(cards[i]) == ref.cardinality(), (opname, i)
+
+
+@pytest.mark.parametrize("opname", list(OPS))
+def test_concurrent_task_phase_parity(ctx, oracle, opname):
+    """>= 65536 tasks: the light and heavy task kernels run concurrently and the light tasks come
+    from the shared chunk queue (two light launches).  Samples across the whole batch must match
+    the oracle byte for byte; materialised and cardinality-only results must agree."""
+    import roaringbitmap_amd as rb
+    op = OPS[opname]
+    n = 40000
+    a, b = ctx.generate(rb.WL_FILTER_POSTING, n, seed=11)
+    out = ctx.pairwise(op, a, b)
+    assert any("||" in k["name"] for k in ctx.stats()["kernels"])  # the concurrent phase ran
+    cards = ctx.pairwise_cardinality(op, a, b)
+    assert np.array_equal(out.cardinalities().astype(np.uint64), cards[:n].astype(np.uint64))
+    for first in range(0, n, 4000):
+        cnt = 60
+        ra = _ref_list(oracle, a.serialize(first, cnt))
+        rbs = _ref_list(oracle, b.serialize(first, cnt))
+        got = out.serialize(first, cnt)
+        for i in range(cnt):
+            assert got[i] == oracle.op(op, ra[i], rbs[i]).serialize(), (opname, first + i)
