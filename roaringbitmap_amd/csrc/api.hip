@@ -712,7 +712,7 @@ static int pairwise_impl(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu
   const uint64_t nt1 = std::max<uint64_t>(ntasks, 1);
   size_t tneed = aligned256(std::max<uint64_t>(nlight, 1) * sizeof(TaskRec)) +
                  aligned256(std::max<uint64_t>(nheavy, 1) * sizeof(TaskRec)) + 2 * aligned256(nt1 * 2) +
-                 2 * aligned256(nt1) + aligned256(nt1 * 4) + aligned256(nt1 * 8) + aligned256(8) + 256;
+                 2 * aligned256(nt1) + aligned256(nt1 * 4) + aligned256(nt1 * 8) + aligned256(4096) + 256;
   if (ctx->ws_tasks.reserve(tneed, st) != hipSuccess)
     return fail(RB_ENOMEM, "task workspace (%llu tasks)", (unsigned long long)ntasks);
   Workspace &T = ctx->ws_tasks;
@@ -725,7 +725,7 @@ static int pairwise_impl(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu
   tm.cat = T.take<uint8_t>(nt1);
   tm.card = T.take<uint32_t>(nt1);
   tm.out = T.take<uint64_t>(nt1);
-  unsigned long long *queue = T.take<unsigned long long>(1); // light-task chunk counter
+  unsigned long long *queue = T.take<unsigned long long>(512); // light-task chunk counters (<= 32, 128 B apart)
 
   rbgpu_set *res = nullptr;
   if (!card_only) {

@@ -420,15 +420,35 @@ __device__ __forceinline__ bool and_runs_intervals(const uint4 (&pq)[8], const u
 #endif
 
 #ifndef RBG_QUEUE_CHUNK
-#define RBG_QUEUE_CHUNK 16 // light tasks per queue claim (4: 6.0 ms steps from atomic contention, 8: 4.64, 16: 4.59-4.62, 32: 4.71-4.78)
+#define RBG_QUEUE_CHUNK 8 // light tasks per claim (one counter: 4 -> 6.0 ms steps from atomic contention, 8 -> 4.64, 16 -> 4.59-4.62, 32 -> 4.71-4.78; 8 counters: 8 -> 4.49-4.52)
 #endif
 constexpr uint64_t kQueueChunk = RBG_QUEUE_CHUNK;
-// first task of the next chunk: one vector atomic by lane 0, broadcast (wave-uniform)
-__device__ __forceinline__ uint64_t claim_chunk(unsigned long long *queue, int lane) {
-  unsigned long long v = 0;
-  if (lane == 0) v = __hip_atomic_fetch_add(queue, (unsigned long long)kQueueChunk, __ATOMIC_RELAXED,
-                                            __HIP_MEMORY_SCOPE_AGENT);
-  return pack2(__builtin_amdgcn_readfirstlane((uint32_t)v), __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)));
+#ifndef RBG_QUEUE_STRIPES
+#define RBG_QUEUE_STRIPES 8 // task sub-ranges with a counter each (a wave moves on when its is empty)
+#endif
+constexpr uint32_t kQueueStripes = RBG_QUEUE_STRIPES;
+constexpr uint32_t kQueueStride = 16; // counters 128 B apart
+static_assert(kQueueStripes >= 1 && kQueueStripes <= 32, "the API reserves 32 counters (4 KiB)");
+// Next chunk [s, e) of the wave's current sub-range, moving to the following sub-ranges as they run
+// dry; s = n when every sub-range is exhausted.  One vector atomic by lane 0 per try, broadcast.
+struct Chunk {
+  uint64_t s, e;
+};
+__device__ __forceinline__ Chunk claim_chunk(unsigned long long *queue, uint64_t n, uint32_t &k, uint32_t &tried,
+                                             int lane) {
+  while (tried < kQueueStripes) {
+    const uint64_t lo = n * k / kQueueStripes, hi = n * (k + 1) / kQueueStripes;
+    unsigned long long v = 0;
+    if (lane == 0)
+      v = __hip_atomic_fetch_add(queue + k * kQueueStride, (unsigned long long)kQueueChunk, __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t st = lo + pack2(__builtin_amdgcn_readfirstlane((uint32_t)v),
+                                   __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)));
+    if (st < hi) return Chunk{st, min(st + kQueueChunk, hi)};
+    k = (k + 1) % kQueueStripes;
+    ++tried;
+  }
+  return Chunk{n, n};
 }
 
 // The task kernel, ONE WAVE PER TASK, persistent waves striding over one record list with a
@@ -456,11 +476,15 @@ __global__ __launch_bounds__(256, ROLE == kRoleHeavy ? RBG_HEAVY_WAVES : RBG_LIG
   // concurrent phase's second light launch fills the CUs the heavy kernel leaves), the next chunk
   // claimed one chunk ahead so the atomic's latency is hidden
   const uint64_t stride = (uint64_t)gridDim.x * 4;
-  uint64_t g = (uint64_t)blockIdx.x * 4 + wv, cend = 0, nxt = 0;
+  uint64_t g = (uint64_t)blockIdx.x * 4 + wv, cend = 0, nxt = 0, nend = 0;
+  uint32_t qk = (uint32_t)(g % kQueueStripes), qtried = 0;
   if (queue) {
-    g = claim_chunk(queue, lane);
-    cend = g + kQueueChunk;
-    nxt = claim_chunk(queue, lane);
+    const Chunk c0 = claim_chunk(queue, n, qk, qtried, lane);
+    g = c0.s;
+    cend = c0.e;
+    const Chunk c1 = claim_chunk(queue, n, qk, qtried, lane);
+    nxt = c1.s;
+    nend = c1.e;
   }
   if (g >= n) return;
   uint32_t *s = lds[wv];
@@ -604,8 +628,10 @@ __global__ __launch_bounds__(256, ROLE == kRoleHeavy ? RBG_HEAVY_WAVES : RBG_LIG
     }
     if (!has_next) break;
     if (new_chunk) {
-      cend = gn + kQueueChunk;
-      nxt = claim_chunk(queue, lane);
+      cend = nend;
+      const Chunk c1 = claim_chunk(queue, n, qk, qtried, lane);
+      nxt = c1.s;
+      nend = c1.e;
     }
     g = gn;
     cur = nx;
@@ -904,7 +930,7 @@ static void launch_op_concurrent(bool card_only, const uint8_t *pa, const uint8_
   (void)hipEventRecord(ev_h1, side);
   // light tasks from a shared queue: one launch beside the heavy kernel, a second one on the side
   // stream once the heavy kernel is done (its waves take whatever tasks are left)
-  if (queue) (void)hipMemsetAsync(queue, 0, sizeof(*queue), st);
+  if (queue) (void)hipMemsetAsync(queue, 0, sizeof(*queue) * kQueueStripes * kQueueStride, st);
   if (card_only) launch_tasks<OP, true, kRoleLight>(pa, pb, light, nl, out, tm, st, RBG_CONC_LIGHT_PER_CU, queue);
   else launch_tasks<OP, false, kRoleLight>(pa, pb, light, nl, out, tm, st, RBG_CONC_LIGHT_PER_CU, queue);
   (void)hipEventRecord(light_done, st);
