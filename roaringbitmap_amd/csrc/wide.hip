@@ -232,52 +232,51 @@ template <int OP> __device__ __forceinline__ void fold(uint64_t (&acc)[kW], cons
   }
 }
 
-#ifndef RBG_FOLD_WIDTH
-#define RBG_FOLD_WIDTH 2 // Bitmaps per step of a run of Bitmaps (>= 2; 4 measured 6.5-7.1 ms config-3 steps vs 6.4-6.6)
-#endif
-// Fold every container of [lo, hi) into acc with OP; runs of Bitmaps are streamed RBG_FOLD_WIDTH
-// per step (8 coalesced 1 KiB loads each in flight per wave), the metadata of the next
-// RBG_FOLD_WIDTH containers read together.  Returns algorithmic bytes read.
+// Fold every container of [lo, hi) into acc with OP; runs of Bitmaps are streamed two per step
+// (16 coalesced 1 KiB loads in flight per wave; four per step measured slower: 6.5-7.1 ms config-3
+// steps vs 6.4-6.6).  Returns algorithmic bytes read.
 template <int OP>
+#ifndef RBG_FOLD_PREFETCH
+#define RBG_FOLD_PREFETCH 1 // the next pair's metadata loads issued before the current pair is folded
+#endif
 __device__ __forceinline__ uint64_t fold_all(const SetView &s, const uint32_t *cid, uint64_t lo, uint64_t hi,
                                              uint64_t (&acc)[kW], uint32_t *lds, int lane) {
   uint64_t bytes = 0;
   uint64_t i = lo;
+  if (i >= hi) return 0;
+  // metadata of the current pair as independent loads (one latency, not a chain)
+  CRef r0 = cref(s, cid[i]);
+  CRef r1 = i + 1 < hi ? cref(s, cid[i + 1]) : r0;
   while (i < hi) {
-    // the next four containers' metadata as independent loads (one latency, not a chain)
-    CRef r[RBG_FOLD_WIDTH];
-#pragma unroll
-    for (int j = 0; j < RBG_FOLD_WIDTH; ++j)
-      if (j == 0 || i + j < hi) r[j] = cref(s, cid[i + j]);
-    bool all = i + RBG_FOLD_WIDTH <= hi;
-#pragma unroll
-    for (int j = 0; j < RBG_FOLD_WIDTH; ++j) all = all && r[j].type == kBitmap;
-    if (all) { // RBG_FOLD_WIDTH x 8 KiB loads in flight per wave
-      uint64_t x[RBG_FOLD_WIDTH][kW];
-#pragma unroll
-      for (int j = 0; j < RBG_FOLD_WIDTH; ++j) load_bitmap(r[j].p, x[j], lane);
-#pragma unroll
-      for (int j = 0; j < RBG_FOLD_WIDTH; ++j) fold<OP>(acc, x[j]);
-      bytes += (uint64_t)RBG_FOLD_WIDTH * (8192 + 16);
-      i += RBG_FOLD_WIDTH;
-      continue;
-    }
-    const CRef a = r[0];
-    bytes += alg_bytes_w(a.type, a.card, a.nruns) + 16;
-    if (a.type == kBitmap && i + 1 < hi && r[1].type == kBitmap) {
-      bytes += 8192 + 16;
+    if (r0.type == kBitmap && i + 1 < hi && r1.type == kBitmap) {
+      bytes += 2 * (8192 + 16);
       uint64_t x[kW], y[kW];
-      load_bitmap(a.p, x, lane);
-      load_bitmap(r[1].p, y, lane);
+      load_bitmap(r0.p, x, lane);
+      load_bitmap(r1.p, y, lane);
+#if RBG_FOLD_PREFETCH
+      // the next pair's metadata is in flight while this pair's payloads arrive
+      const CRef n0 = i + 2 < hi ? cref(s, cid[i + 2]) : r0;
+      const CRef n1 = i + 3 < hi ? cref(s, cid[i + 3]) : r0;
+#endif
       fold<OP>(acc, x);
       fold<OP>(acc, y);
       i += 2;
+#if RBG_FOLD_PREFETCH
+      r0 = n0;
+      r1 = n1;
+#else
+      if (i < hi) r0 = cref(s, cid[i]);
+      if (i + 1 < hi) r1 = cref(s, cid[i + 1]);
+#endif
       continue;
     }
+    bytes += alg_bytes_w(r0.type, r0.card, r0.nruns) + 16;
     uint64_t x[kW];
-    load_container(a.type, a.p, a.card, a.nruns, lds, x, lane);
+    load_container(r0.type, r0.p, r0.card, r0.nruns, lds, x, lane);
     fold<OP>(acc, x);
     i += 1;
+    r0 = r1;
+    if (i + 1 < hi) r1 = cref(s, cid[i + 1]);
   }
   return bytes;
 }
