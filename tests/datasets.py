@@ -41,6 +41,37 @@ def fixture_bytes(name: str) -> bytes:
         return f.read()
 
 
+def ornot_fuzz_bitmaps() -> tuple:
+    """The two serialized bitmaps (l, r) of testdata/ornot-fuzz-failure.json, decoded as
+    TestRoaringBitmapOrNot.testBigOrNot does (TestRoaringBitmapOrNot.java:381-390): mixed
+    Array/Bitmap/Run containers, disjoint key sets."""
+    import base64
+    import json
+    with open(os.path.join(GOLDEN, "testdata", "ornot-fuzz-failure.json")) as f:
+        info = json.load(f)
+    return tuple(base64.b64decode(s) for s in info["bitmaps"][:2])
+
+
+def range_bitmap_bytes(limit: int) -> bytes:
+    """RoaringFormatSpec bytes of [0, limit) as Run containers (what RoaringBitmap.add(0, limit)
+    yields via Container.rangeOfOnes (Container.java:29-37), which returns a RunContainer above 2 values), written
+    directly since 2^32-scale ranges cannot go through a value list."""
+    import struct
+    assert 0 < limit <= 1 << 32 and (limit - 1) & 0xFFFF >= 2, "last container must hold > 2 values"
+    nkeys = (limit - 1 >> 16) + 1
+    lens = [0xFFFF] * (nkeys - 1) + [(limit - 1) & 0xFFFF]
+    out = [struct.pack("<I", 12347 | (nkeys - 1) << 16), b"\xff" * (nkeys // 8)]
+    if nkeys % 8:
+        out.append(bytes([(1 << (nkeys % 8)) - 1]))
+    out.append(b"".join(struct.pack("<HH", k, ln) for k, ln in enumerate(lens)))
+    header = sum(len(b) for b in out)
+    if nkeys >= 4:  # NO_OFFSET_THRESHOLD: offsets follow the descriptive header
+        header += 4 * nkeys
+        out.append(b"".join(struct.pack("<I", header + 6 * k) for k in range(nkeys)))
+    out.append(b"".join(struct.pack("<HHH", 1, 0, ln) for ln in lens))
+    return b"".join(out)
+
+
 def _container_values(rng: np.random.Generator, kind: str) -> np.ndarray:
     """Low 16-bit values of one container of a given shape."""
     if kind == "single":

@@ -3,7 +3,8 @@ RoaringFormatSpec bytes for every result, identical cardinalities."""
 import numpy as np
 import pytest
 
-from datasets import DATASETS, EXPECTED, fixture_bytes, load_realdata, synthetic_bitmaps
+from datasets import (DATASETS, EXPECTED, fixture_bytes, load_realdata, ornot_fuzz_bitmaps, range_bitmap_bytes,
+                      synthetic_bitmaps)
 
 pytestmark = pytest.mark.gpu
 OPS = {"AND": 0, "OR": 1, "XOR": 2, "ANDNOT": 3}
@@ -229,3 +230,32 @@ def test_concurrent_task_phase_parity(ctx, oracle, opname):
         got = out.serialize(first, cnt)
         for i in range(cnt):
             assert got[i] == oracle.op(op, ra[i], rbs[i]).serialize(), (opname, first + i)
+
+
+def test_ornot_fuzz_fixture_through_the_device(ctx, oracle):
+    # testdata/ornot-fuzz-failure.json (TestRoaringBitmapOrNot.java:379-425): l (144 Bitmap / 33 Run
+    # / 4 Array containers) and r (293 Array / 80 Run / 1 Bitmap), disjoint keys, plus the 65k-key
+    # range [0, limit) of that test; every op over every ordered pair, then the test's expected side
+    # l | ([0, limit) \ r) composed on the device.
+    lb, rbytes = ornot_fuzz_bitmaps()
+    l = oracle.RefBitmap.deserialize(lb)
+    limit = int(l.to_array()[-1]) + 1
+    blobs = [lb, rbytes, range_bitmap_bytes(limit)]
+    s = ctx.upload_serialized(blobs)
+    assert s.serialize() == blobs
+    refs = _ref_list(oracle, blobs)
+    a_idx = np.repeat(np.arange(3, dtype=np.uint32), 3)
+    b_idx = np.tile(np.arange(3, dtype=np.uint32), 3)
+    for opname, op in OPS.items():
+        got = ctx.pairwise(op, s, s, a_idx, b_idx).serialize()
+        cards = ctx.pairwise_cardinality(op, s, s, a_idx, b_idx)
+        for i in range(len(a_idx)):
+            ref = oracle.op(op, refs[a_idx[i]], refs[b_idx[i]])
+            assert got[i] == ref.serialize(), (opname, int(a_idx[i]), int(b_idx[i]))
+            assert int(cards[i]) == ref.cardinality(), (opname, int(a_idx[i]), int(b_idx[i]))
+    diff = ctx.pairwise(OPS["ANDNOT"], s, s, np.array([2], np.uint32), np.array([1], np.uint32))
+    got = ctx.pairwise(OPS["OR"], s, diff, np.array([0], np.uint32), np.array([0], np.uint32))
+    want = oracle.op(OPS["OR"], refs[0], oracle.op(OPS["ANDNOT"], refs[2], refs[1]))
+    assert got.serialize() == [want.serialize()]
+    ra = refs[1].to_array()
+    assert int(got.cardinalities()[0]) == limit - int((ra < limit).sum())

@@ -2,7 +2,7 @@
 import numpy as np
 import pytest
 
-from datasets import DATASETS, EXPECTED, fixture_bytes, load_realdata
+from datasets import DATASETS, EXPECTED, fixture_bytes, load_realdata, ornot_fuzz_bitmaps, range_bitmap_bytes
 
 OPS = ["AND", "OR", "XOR", "ANDNOT"]
 
@@ -39,6 +39,31 @@ def test_fixture_round_trip_and_run_optimize_kat(oracle):
     assert [c[1] for c in a.containers()] == [0, 0, 1, 1, 1, 1, 1, 0, 2, 2, 2]
     b.run_optimize()
     assert b.serialize() == with_runs  # runOptimize(withoutruns) reproduces withruns byte for byte
+
+
+def test_ornot_fuzz_fixture_mixed_types(oracle):
+    # testdata/ornot-fuzz-failure.json as TestRoaringBitmapOrNot.testBigOrNot(Static) reads it
+    # (TestRoaringBitmapOrNot.java:379-425): the expected side of that test, l | ([0, limit) \ r),
+    # composed from the oracle's OR / ANDNOT over Array/Bitmap/Run containers.
+    R = oracle
+    lb, rbytes = ornot_fuzz_bitmaps()
+    l, r = R.RefBitmap.deserialize(lb), R.RefBitmap.deserialize(rbytes)
+    assert l.serialize() == lb and r.serialize() == rbytes
+    assert sorted(t for _, t, _, _ in l.containers()).count(2) == 33  # 33 Run / 144 Bitmap / 4 Array
+    assert [sum(t == k for _, t, _, _ in r.containers()) for k in (0, 1, 2)] == [293, 1, 80]
+    assert not {c[0] for c in l.containers()} & {c[0] for c in r.containers()}  # disjoint keys
+    limit = int(l.to_array()[-1]) + 1
+    rng_bm = R.RefBitmap.deserialize(range_bitmap_bytes(limit))
+    assert rng_bm.cardinality() == limit
+    expected = R.op(R.OR, l, R.op(R.ANDNOT, rng_bm, r))
+    # l lies inside [0, limit) and shares no key with r, so the result is exactly [0, limit) \ r
+    ra = r.to_array()
+    assert expected.cardinality() == limit - int((ra < limit).sum())
+    assert R.op_cardinality(R.AND, expected, r) == 0
+    assert R.op_cardinality(R.ANDNOT, expected, rng_bm) == 0
+    assert R.op_cardinality(R.AND, l, r) == 0
+    assert R.op(R.XOR, l, r).serialize() == R.op(R.OR, l, r).serialize()
+    assert R.op(R.ANDNOT, l, r).serialize() == lb  # unmatched left containers are cloned as-is
 
 
 @pytest.mark.parametrize("i", range(1, 8))
