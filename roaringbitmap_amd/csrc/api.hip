@@ -41,9 +41,12 @@ int set_alloc(rbgpu_ctx *ctx, rbgpu_set *s, uint32_t nb, uint64_t nc, uint64_t p
       p.alloc((void **)&s->key, ncap * 2) != hipSuccess || p.alloc((void **)&s->type, ncap) != hipSuccess ||
       p.alloc((void **)&s->card, ncap * 4) != hipSuccess || p.alloc((void **)&s->nruns, ncap * 2) != hipSuccess ||
       p.alloc((void **)&s->off, ncap * 8) != hipSuccess ||
-      p.alloc((void **)&s->payload, std::max<uint64_t>(payload, 16)) != hipSuccess)
+      p.alloc((void **)&s->payload, std::max<uint64_t>(payload, 16)) != hipSuccess) {
+    // give back what was taken and the context reference: callers only `delete s` on failure
+    set_release(s);
     return fail(RB_ENOMEM, "device allocation of a %u-bitmap / %llu-container set failed", nb,
                 (unsigned long long)nc);
+  }
   return RB_OK;
 }
 void set_release(rbgpu_set *s) {
@@ -87,6 +90,7 @@ int ensure_h_begin(const rbgpu_set *cs) {
   HIPCHK(hipMemcpyAsync(s->h_begin.data(), s->begin, (s->nb + 1) * sizeof(uint64_t), hipMemcpyDeviceToHost,
                         s->ctx->stream));
   HIPCHK(hipStreamSynchronize(s->ctx->stream));
+  LAUNCHCHK();
   return RB_OK;
 }
 // Sets are immutable, so the largest per-bitmap container count is computed once (host CSR if it
@@ -105,6 +109,7 @@ int ensure_max_keys(const rbgpu_set *cs) {
     launch_max_span(s->begin, s->nb, d, s->ctx->stream);
     HIPCHK(hipMemcpyAsync(s->ctx->h_pinned + 7, d, 8, hipMemcpyDeviceToHost, s->ctx->stream));
     HIPCHK(hipStreamSynchronize(s->ctx->stream));
+    LAUNCHCHK();
     s->ctx->pool.release(d);
     m = s->ctx->h_pinned[7];
   }
@@ -181,6 +186,7 @@ int download_host(const rbgpu_set *s, uint32_t first, uint32_t count, HostSoA &h
     HIPCHK(hipMemcpyAsync(h.nruns.data(), s->nruns + lo, n * 2, hipMemcpyDeviceToHost, st));
     HIPCHK(hipMemcpyAsync(soff.data(), s->off + lo, n * 8, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
+    LAUNCHCHK();
   }
   std::vector<uint64_t> bytes(n);
   uint64_t total = 0;
@@ -202,6 +208,7 @@ int download_host(const rbgpu_set *s, uint32_t first, uint32_t count, HostSoA &h
     launch_gather(s->payload, d_soff, d_bytes, d_stage, d_doff, n, st);
     HIPCHK(hipMemcpyAsync(h.payload.data(), d_stage, total, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
+    LAUNCHCHK();
     ctx->pool.release(d_soff);
     ctx->pool.release(d_doff);
     ctx->pool.release(d_bytes);
@@ -213,6 +220,7 @@ int download_host(const rbgpu_set *s, uint32_t first, uint32_t count, HostSoA &h
 int check_ctx(rbgpu_ctx *ctx) {
   if (!ctx) return fail(RB_EINVAL, "null context");
   HIPCHK(hipSetDevice(ctx->device));
+  (void)hipGetLastError(); // LAUNCHCHK reports only what this call launches
   return RB_OK;
 }
 
@@ -228,6 +236,7 @@ int stats_end(rbgpu_ctx *ctx, uint64_t tasks, uint64_t result_containers, const 
   HIPCHK(hipMemcpyAsync(ctx->h_stats, ctx->d_stats, kStatWords * kStripes * sizeof(uint64_t), hipMemcpyDeviceToHost,
                         ctx->stream));
   HIPCHK(hipStreamSynchronize(ctx->stream));
+  LAUNCHCHK();
   uint64_t w[kStatWords] = {};
   for (int i = 0; i < kStatWords; ++i)
     for (int j = 0; j < kStripes; ++j) w[i] += ctx->h_stats[i * kStripes + j];
@@ -306,6 +315,7 @@ int rbgpu_synchronize(rbgpu_ctx *ctx) {
   int rc = check_ctx(ctx);
   if (rc) return rc;
   HIPCHK(hipStreamSynchronize(ctx->stream));
+  LAUNCHCHK();
   return RB_OK;
 }
 
@@ -440,6 +450,7 @@ int rbgpu_set_cardinalities(const rbgpu_set *s, uint64_t *out) {
   launch_bitmap_cards(s->view(), s->nb, d, ctx->stream);
   HIPCHK(hipMemcpyAsync(out, d, s->nb * 8ull, hipMemcpyDeviceToHost, ctx->stream));
   HIPCHK(hipStreamSynchronize(ctx->stream));
+  LAUNCHCHK();
   ctx->pool.release(d);
   return RB_OK;
 }
@@ -487,6 +498,7 @@ int rbgpu_set_serialized_sizes(const rbgpu_set *s, uint64_t *out) {
     HIPCHK(hipMemcpyAsync(nruns.data(), s->nruns, n * 2, hipMemcpyDeviceToHost, s->ctx->stream));
     HIPCHK(hipMemcpyAsync(card.data(), s->card, n * 4, hipMemcpyDeviceToHost, s->ctx->stream));
     HIPCHK(hipStreamSynchronize(s->ctx->stream));
+    LAUNCHCHK();
   }
   for (uint32_t b = 0; b < s->nb; ++b) {
     const uint64_t lo = s->h_begin[b], hi = s->h_begin[b + 1], k = hi - lo;
@@ -517,6 +529,7 @@ int rbgpu_set_summaries(const rbgpu_set *s, uint32_t first, uint32_t count, rb_b
     HIPCHK(hipMemcpyAsync(nruns.data(), s->nruns + lo, n * 2, hipMemcpyDeviceToHost, s->ctx->stream));
     HIPCHK(hipMemcpyAsync(card.data(), s->card + lo, n * 4, hipMemcpyDeviceToHost, s->ctx->stream));
     HIPCHK(hipStreamSynchronize(s->ctx->stream));
+    LAUNCHCHK();
   }
   for (uint32_t b = 0; b < count; ++b) {
     rb_bitmap_summary &o = out[b];
@@ -545,6 +558,7 @@ int rbgpu_set_key_bytes(const rbgpu_set *s, uint64_t *out) {
     HIPCHK(hipMemcpyAsync(nruns.data(), s->nruns, n * 2, hipMemcpyDeviceToHost, s->ctx->stream));
     HIPCHK(hipMemcpyAsync(card.data(), s->card, n * 4, hipMemcpyDeviceToHost, s->ctx->stream));
     HIPCHK(hipStreamSynchronize(s->ctx->stream));
+    LAUNCHCHK();
   }
   std::fill(out, out + 65536, 0ull);
   for (uint64_t i = 0; i < n; ++i)
@@ -680,6 +694,7 @@ static int pairwise_impl(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu
     scan_exclusive(nseg_p, seg_begin, np, ptmp, st);
     HIPCHK(hipMemcpyAsync(tot + 6, seg_begin + np, 8, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
+    LAUNCHCHK();
     ns = np ? tot[6] : 0;
   }
   // ---- per segment: counts, scans, result counts / offsets
@@ -704,6 +719,7 @@ static int pairwise_impl(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu
   scan_exclusive_multi(scan_in, scan_out, 4, ns, tmp, d_tot, st);
   HIPCHK(hipMemcpyAsync(tot, d_tot, 4 * 8, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
+  LAUNCHCHK();
   if (!ns) tot[0] = tot[1] = tot[2] = tot[3] = 0;
   const uint64_t ntasks = tot[0], nlight = tot[1], nheavy = ntasks - nlight, nbig_t = tot[2], small_t = tot[3];
   const uint64_t small_base = nbig_t * kBitmapBytes;
@@ -736,7 +752,17 @@ static int pairwise_impl(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu
       return rc;
     }
   }
+  // the light and heavy task kernels run concurrently (heavy on the side stream, 1 block per CU;
+  // light 2 blocks per CU: 2 x 128 + 256 VGPRs per SIMD) unless RBGPU_SERIAL_TASKS is set
+  static const bool serial = getenv("RBGPU_SERIAL_TASKS") != nullptr;
+  // light tasks from a shared chunk queue (a second light launch takes over the heavy kernel's CUs
+  // when it finishes) unless RBGPU_STATIC_LIGHT is set
+  static const bool static_light = getenv("RBGPU_STATIC_LIGHT") != nullptr;
+  const bool conc = !probe && !serial && nlight && nheavy && nlight + nheavy >= 65536; // small batches: the
+                                                  // cross-stream waits cost more than the overlap
   launch_pair_emit(pa, scn, small_base, light, heavy, tm, st);
+  // the queue counters are zeroed before ev[1]: the side stream waits on ev[1] before its light launch
+  if (conc && !static_light) HIPCHK(hipMemsetAsync(queue, 0, 4096, st));
   HIPCHK(hipEventRecord(ctx->ev[1], st));
   if (probe) {
     uint32_t *sink = nullptr;
@@ -746,6 +772,7 @@ static int pairwise_impl(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu
     if (probe == 1) launch_probe(op, probe, a->payload, b->payload, 0, heavy, nheavy, sink, blocks, st);
     HIPCHK(hipEventRecord(ctx->ev[2], st));
     HIPCHK(hipStreamSynchronize(st));
+    LAUNCHCHK();
     ctx->pool.release(sink);
     if (res) rbgpu_set_free(res);
     const KernelSpan spans[1] = {{probe == 1 ? "k_probe_tasks" : "k_probe_stream", 6, -1, ntasks}};
@@ -753,14 +780,6 @@ static int pairwise_impl(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu
     if (probe == 2) ctx->last.main_kernel_bytes = ctx->last.kernel_bytes[0] = a->payload_bytes / 8192 * 8192;
     return rc;
   }
-  // the light and heavy task kernels run concurrently (heavy on the side stream, 1 block per CU;
-  // light 2 blocks per CU: 2 x 128 + 256 VGPRs per SIMD) unless RBGPU_SERIAL_TASKS is set
-  static const bool serial = getenv("RBGPU_SERIAL_TASKS") != nullptr;
-  // light tasks from a shared chunk queue (a second light launch takes over the heavy kernel's CUs
-  // when it finishes) unless RBGPU_STATIC_LIGHT is set
-  static const bool static_light = getenv("RBGPU_STATIC_LIGHT") != nullptr;
-  const bool conc = !serial && nlight && nheavy && nlight + nheavy >= 65536; // small batches: the
-                                                  // cross-stream waits cost more than the overlap
   if (conc) {
     HIPCHK(hipStreamWaitEvent(ctx->side, ctx->ev[1], 0));
     launch_pairwise_concurrent(op, card_only, a->payload, b->payload, light, nlight, heavy, nheavy,

@@ -570,6 +570,7 @@ int bsi_compare(rbgpu_ctx *ctx, const rbgpu_set *bsi, int op, uint64_t start, ui
       const uint64_t hb[2] = {0, 0};
       HIPCHK(hipMemcpyAsync(e->begin, hb, 16, hipMemcpyHostToDevice, st));
       HIPCHK(hipStreamSynchronize(st));
+      LAUNCHCHK();
       e->h_begin = {0, 0};
       *out = e;
       return RB_OK;
@@ -600,6 +601,7 @@ int bsi_compare(rbgpu_ctx *ctx, const rbgpu_set *bsi, int op, uint64_t start, ui
   k_bsi_list<<<256, 256, 0, st>>>(d_active, d_pos, d_klist);
   HIPCHK(hipMemcpyAsync(ctx->h_pinned, d_pos + 65536, 8, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
+  LAUNCHCHK();
   const uint32_t nk = (uint32_t)ctx->h_pinned[0];
   // result set: one 8 KiB slot per key of F, compacted at the end
   rbgpu_set *res = new rbgpu_set;

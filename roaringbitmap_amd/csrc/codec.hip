@@ -290,20 +290,23 @@ __global__ __launch_bounds__(256) void k_de_copy(DeArgs a, uint64_t nc, const ui
       if (nr == 0) {
         why = kRunEmpty;
       } else {
-        bool bounds = false, order = false;
+        // the host walk (format.cpp validate_container) stops at the first failing run and checks its
+        // bounds before its order: the reason reported is that of the least code 2 * run + (order)
+        uint32_t first = 0xFFFFFFFFu;
         uint32_t total = 0;
         for (uint32_t i = lane; i < nr; i += 64) {
           const uint32_t r = a.in.u32(src + 4ull * i), s = r & 0xFFFF, e = s + (r >> 16);
-          bounds |= e > 65535;
+          bool order = false;
           if (i > 0) {
             const uint32_t q = a.in.u32(src + 4ull * (i - 1));
-            order |= s <= (q & 0xFFFF) + (q >> 16) + 1;
+            order = s <= (q & 0xFFFF) + (q >> 16) + 1;
           }
+          if (e > 65535) first = min(first, 2 * i);
+          else if (order) first = min(first, 2 * i + 1);
           total += (r >> 16) + 1;
         }
-        // the host walk reports the first failing run; either reason is RB_EINVAL
-        if (__ballot(bounds)) why = kRunBounds;
-        else if (__ballot(order)) why = kRunOrder;
+        first = ~wave_max_u32(~first);
+        if (first != 0xFFFFFFFFu) why = (first & 1) ? kRunOrder : kRunBounds;
         else if (wave_sum_u32(total) != card) why = kRunCard;
       }
     }
@@ -483,6 +486,7 @@ int deserialize_device(rbgpu_ctx *ctx, const uint8_t *d_in, uint64_t in_lim, con
   uint64_t nc = 0;
   HIPCHK(hipMemcpyAsync(&nc, cbase + n, 8, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
+  LAUNCHCHK();
   uint64_t *bidx, *soff, *tmp2;
   if (!w.get(a.key, nc) || !w.get(a.type, nc) || !w.get(a.card, nc) || !w.get(a.nruns, nc) || !w.get(a.src, nc) ||
       !w.get(a.owner, nc) || !w.get(a.bigflag, nc + 1) || !w.get(a.small, nc + 1) || !w.get(bidx, nc + 1) ||
@@ -501,6 +505,7 @@ int deserialize_device(rbgpu_ctx *ctx, const uint8_t *d_in, uint64_t in_lim, con
   HIPCHK(hipMemcpyAsync(&tot[0], bidx + nc, 8, hipMemcpyDeviceToHost, st));
   HIPCHK(hipMemcpyAsync(&tot[1], soff + nc, 8, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
+  LAUNCHCHK();
   const uint64_t small_base = tot[0] * kBitmapBytes, total = small_base + tot[1];
   rbgpu_set *s = new rbgpu_set;
   int rc = set_alloc(ctx, s, n, nc, total);
@@ -559,6 +564,7 @@ int serialize_device(const rbgpu_set *s, uint32_t first, uint32_t count, uint8_t
   std::vector<uint64_t> h_off(count + 1ull);
   HIPCHK(hipMemcpyAsync(h_off.data(), out_off, (count + 1ull) * 8, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
+  LAUNCHCHK();
   const uint64_t total = h_off[count];
   if (total > cap) return fail(RB_EINVAL, "destination buffer too small (%llu needed)", (unsigned long long)total);
   uint8_t *dev = d_out;
@@ -568,6 +574,7 @@ int serialize_device(const rbgpu_set *s, uint32_t first, uint32_t count, uint8_t
   if (nc) k_ser_payload<<<grid_for(nc), 256, 0, st>>>(a, owner, nc);
   if (host_dst && total) HIPCHK(hipMemcpyAsync(d_out, dev, total, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
+  LAUNCHCHK();
   if (offsets) std::copy(h_off.begin(), h_off.end(), offsets);
   return RB_OK;
 }

@@ -316,6 +316,7 @@ int materialize(rbgpu_ctx *ctx, const GenStructure &gs, uint64_t seed, rbgpu_set
   HIPCHK(hipMemcpyAsync(&tot[0], d_bidx + n, 8, hipMemcpyDeviceToHost, st));
   HIPCHK(hipMemcpyAsync(&tot[1], d_soff + n, 8, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
+  LAUNCHCHK();
   const uint64_t small_base = tot[0] * kBitmapBytes, total = small_base + tot[1];
   launch_layout(d_big, d_bidx, d_soff, small_base, s->off, n, st);
   pool.release(s->payload);
@@ -328,6 +329,7 @@ int materialize(rbgpu_ctx *ctx, const GenStructure &gs, uint64_t seed, rbgpu_set
   s->payload_bytes = total;
   launch_gen_emit(g, n, s->type, s->off, s->payload, st);
   HIPCHK(hipStreamSynchronize(st));
+  LAUNCHCHK();
   for (void *p : {(void *)d_target, (void *)d_param, (void *)d_uid, (void *)d_big, (void *)d_small, (void *)d_bidx, (void *)d_soff,
                   (void *)d_tmp})
     pool.release(p);

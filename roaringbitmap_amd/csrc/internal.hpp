@@ -19,6 +19,14 @@ int fail(int code, const char *fmt, ...);
     if (e_ != hipSuccess) return ::rbg::fail(RB_EDEVICE, "%s failed: %s", #x, hipGetErrorString(e_));  \
   } while (0)
 
+// A failed kernel launch (bad grid, out of resources) is only visible through hipGetLastError: every
+// API call checks it once its launches are queued (before it reports success).
+#define LAUNCHCHK()                                                                                    \
+  do {                                                                                                 \
+    hipError_t e_ = hipGetLastError();                                                                 \
+    if (e_ != hipSuccess) return ::rbg::fail(RB_EDEVICE, "kernel launch failed: %s", hipGetErrorString(e_)); \
+  } while (0)
+
 // Device allocation cache: a freed block is reused for requests in [size/2, size].
 struct DevPool {
   std::multimap<size_t, void *> free_;

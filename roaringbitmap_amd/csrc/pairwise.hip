@@ -928,9 +928,9 @@ static void launch_op_concurrent(bool card_only, const uint8_t *pa, const uint8_
   if (card_only) launch_tasks<OP, true, kRoleHeavy>(pa, pb, heavy, nh, out, tm, side, RBG_CONC_HEAVY_PER_CU);
   else launch_tasks<OP, false, kRoleHeavy>(pa, pb, heavy, nh, out, tm, side, RBG_CONC_HEAVY_PER_CU);
   (void)hipEventRecord(ev_h1, side);
-  // light tasks from a shared queue: one launch beside the heavy kernel, a second one on the side
-  // stream once the heavy kernel is done (its waves take whatever tasks are left)
-  if (queue) (void)hipMemsetAsync(queue, 0, sizeof(*queue) * kQueueStripes * kQueueStride, st);
+  // light tasks from a shared queue (zeroed by the caller before the side stream's wait): one launch
+  // beside the heavy kernel, a second one on the side stream once the heavy kernel is done (its
+  // waves take whatever tasks are left)
   if (card_only) launch_tasks<OP, true, kRoleLight>(pa, pb, light, nl, out, tm, st, RBG_CONC_LIGHT_PER_CU, queue);
   else launch_tasks<OP, false, kRoleLight>(pa, pb, light, nl, out, tm, st, RBG_CONC_LIGHT_PER_CU, queue);
   (void)hipEventRecord(light_done, st);

@@ -486,6 +486,7 @@ int compact_keyed(rbgpu_ctx *ctx, const uint32_t *d_klist, uint32_t nk, const Wi
                                                 OutView{res->key, res->type, res->card, res->nruns, res->off});
     HIPCHK(hipMemcpyAsync(pin + 1, pos + nk, 8, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
+    LAUNCHCHK();
     ctx->pool.release(keep);
     ctx->pool.release(pos);
     ctx->pool.release(tmp2);
@@ -590,6 +591,7 @@ int wide_run(rbgpu_ctx *ctx, int sem, const rbgpu_set *in, const std::vector<uin
   uint64_t *pin = ctx->h_pinned;
   HIPCHK(hipMemcpyAsync(pin, d_apos + 65536, 8, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
+  LAUNCHCHK();
   const uint32_t nk = (and_sem && M == 0) ? 0 : (uint32_t)pin[0];
 
   // ---- per-key reduction into 8 KiB slots

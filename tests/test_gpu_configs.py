@@ -1,0 +1,191 @@
+"""Parity of every BASELINE.json config at its FULL benchmark size, on the HIP path.
+
+The oracle cannot run a whole config in seconds (config 3 alone is 32 GiB of Bitmaps), so each test
+runs the device path on the full workload exactly as bench.py does, then checks
+  * byte-exact samples against the oracle: containers of the full result at sampled keys / pairs,
+    against oracle.op / oracle.wide / oracle.bsi_compare over the same inputs (the generator keys
+    container contents by (bitmap, key), so a key-range shard regenerates exactly those inputs);
+  * size-independent properties over the whole result: materialised == cardinality-only results,
+    sharded == unsharded bytes, canonical result containers, golden sums where the reference has
+    them (config 1).
+
+Config 1 (census1881, 199 pairs x 4 ops, byte-exact on every pair + the golden sums of
+RealDataBenchmark{And,Or,Xor,AndNot}Test) is test_gpu_pairwise.test_realdata_pairwise_bytes_and_golden.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+OPS = {"AND": 0, "OR": 1, "XOR": 2, "ANDNOT": 3}
+
+
+def _refs(oracle, blobs):
+    return [oracle.RefBitmap.deserialize(b) for b in blobs]
+
+
+def _subset_bytes(h, keys):
+    """RoaringFormatSpec bytes of the containers of one-bitmap host SoA `h` whose key is in `keys`."""
+    from roaringbitmap_amd.engine import HostSoA
+    from roaringbitmap_amd.sharding import serialize_parts
+    keys = np.asarray(sorted(keys), dtype=np.uint16)
+    sel = np.nonzero(np.isin(h.key, keys))[0]
+    part = HostSoA(np.array([0, len(sel)], np.uint64), h.key[sel].copy(), h.type[sel].copy(), h.card[sel].copy(),
+                   h.nruns[sel].copy(), h.offset[sel].copy(), h.payload)
+    return serialize_parts([part])
+
+
+def _check_canonical(h):
+    """Every result container is canonical (what the reference's type rules can produce)."""
+    import roaringbitmap_amd as rb
+    t, c, r = h.type.astype(np.int64), h.card.astype(np.int64), h.nruns.astype(np.int64)
+    assert np.all(c >= 1) and np.all(c <= 65536)
+    assert np.all(c[t == rb.ARRAY] <= 4096)
+    assert np.all(c[t == rb.BITMAP] > 4096)
+    assert np.all(r[t == rb.RUN] >= 1)
+    if len(h.key) > 1:
+        ends = h.begin.astype(np.int64)
+        for b in range(len(ends) - 1):
+            k = h.key[ends[b]:ends[b + 1]].astype(np.int64)
+            assert np.all(np.diff(k) > 0)
+
+
+# ---------------------------------------------------------------- config 2
+@pytest.mark.parametrize("opname", list(OPS))
+def test_config2_million_pairs(ctx, oracle, opname):
+    """Config 2 at bench size: 1M device-generated (filter, posting-list) pairs, one batched call.
+    2000 pairs spread over the whole batch (40 windows x 50) are byte-exact against oracle.op, and
+    the materialised cardinalities of all 1M results equal rbgpu_pairwise_cardinality's."""
+    import roaringbitmap_amd as rb
+    op = OPS[opname]
+    n = 1_000_000
+    a, b = ctx.generate(rb.WL_FILTER_POSTING, n, seed=42)
+    out = ctx.pairwise(op, a, b)
+    st = ctx.stats()
+    assert len(out) == n
+    assert any("||" in k["name"] for k in st["kernels"])  # the concurrent light || heavy task phase ran
+    cards = ctx.pairwise_cardinality(op, a, b)
+    assert np.array_equal(out.cardinalities().astype(np.uint64), cards.astype(np.uint64))
+    starts = np.linspace(0, n - 50, 40).astype(np.int64)
+    checked = 0
+    for first in starts:
+        first = int(first)
+        ra = _refs(oracle, a.serialize(first, 50))
+        rbs = _refs(oracle, b.serialize(first, 50))
+        got = out.serialize(first, 50)
+        for i in range(50):
+            want = oracle.op(op, ra[i], rbs[i])
+            assert got[i] == want.serialize(), (opname, first + i)
+            assert int(cards[first + i]) == want.cardinality(), (opname, first + i)
+            checked += 1
+    assert checked >= 2000
+    # the result CSR covers the batch and every result container is canonical (sampled block)
+    _check_canonical(out.download(0, 20000))
+    out.close()
+    a.close()
+    b.close()
+
+
+# ---------------------------------------------------------------- config 3
+def _key_windows(nwin, width, hi=65536):
+    starts = np.linspace(0, hi - width, nwin).astype(np.int64)
+    return [(int(s), int(s) + width) for s in starts]
+
+
+def test_config3_wide_or_1024_dense(ctx, oracle):
+    """Config 3 at bench size: FastAggregation.or of 1024 dense bitmaps over the full 2^32 universe
+    (32 GiB of Bitmap payload).  64 keys (8 windows of 8) of the full result are byte-exact against
+    oracle.wide(FAST_OR) over the same containers; the key-range shards of the full dataset give the
+    same bytes; the full result's cardinality equals FastAggregation.orCardinality's."""
+    import roaringbitmap_amd as rb
+    nb = 1024
+    a = ctx.generate_keys(rb.WL_WIDE_DENSE, nb, 0, 65536, seed=42)
+    res = ctx.wide(rb.FAST_OR, a)
+    assert ctx.stats()["main_kernel"].startswith("k_wide_reduce")
+    h = res.download()
+    assert len(h.key) == 65536  # 1024 members x 1/16 presence: every key is present
+    _check_canonical(h)
+    total = int(h.card.astype(np.int64).sum())
+    assert total == ctx.wide_cardinality(rb.OR, a)
+    checked = 0
+    for lo, hi in _key_windows(8, 8):
+        small = ctx.generate_keys(rb.WL_WIDE_DENSE, nb, lo, hi, seed=42)
+        want = oracle.wide(oracle.FAST_OR, _refs(oracle, small.serialize())).serialize()
+        assert _subset_bytes(h, range(lo, hi)) == want, (lo, hi)
+        shard = ctx.wide(rb.FAST_OR, a, key_range=(lo, hi))
+        assert shard.serialize()[0] == want, (lo, hi)
+        checked += hi - lo
+        small.close()
+        shard.close()
+    assert checked >= 64
+    res.close()
+    a.close()
+
+
+# ---------------------------------------------------------------- config 4
+@pytest.mark.parametrize("sem", ["FAST_AND", "FAST_XOR"])
+def test_config4_wide_runs_4096(ctx, oracle, sem):
+    """Config 4 at bench size: FastAggregation.and (workShyAnd, n > 10) and FastAggregation.xor
+    (naive_xor) over 4096 run-heavy bitmaps x 65536 keys (268M Run containers).  64 keys of the full
+    result (8 windows of 8) are byte-exact against the oracle over the same 4096 x 8 containers; the
+    Run-list fast path and the generic per-key kernel agree on a window."""
+    import os
+
+    import roaringbitmap_amd as rb
+    nb = 4096
+    a = ctx.generate_keys(rb.WL_WIDE_RUNS, nb, 0, 65536, seed=42)
+    semv = getattr(rb, sem)
+    res = ctx.wide(semv, a)
+    h = res.download()
+    _check_canonical(h)
+    if sem == "FAST_AND":
+        assert len(h.key) == 65536  # every key holds its shared core run in every member
+    checked = 0
+    for lo, hi in _key_windows(8, 8):
+        small = ctx.generate_keys(rb.WL_WIDE_RUNS, nb, lo, hi, seed=42)
+        want = oracle.wide(getattr(oracle, sem), _refs(oracle, small.serialize())).serialize()
+        assert _subset_bytes(h, range(lo, hi)) == want, (sem, lo, hi)
+        checked += hi - lo
+        if lo == 0:
+            os.environ["RBGPU_NO_RUN_FASTPATH"] = "1"
+            try:
+                assert ctx.wide(semv, small).serialize()[0] == want, sem
+            finally:
+                del os.environ["RBGPU_NO_RUN_FASTPATH"]
+        small.close()
+    assert checked >= 64
+    res.close()
+    a.close()
+
+
+# ---------------------------------------------------------------- config 5
+def test_config5_bsi_64_slices_100m_rows(ctx, oracle):
+    """Config 5 at bench size: Roaring64BitmapSliceIndex.compare over 64 slices x 100M rows.  The
+    RANGE (bench query), GE and LT results on the full BSI are byte-exact against the oracle's O'Neil
+    restatement at 9 high keys spread over the 1526 keys (including the last, partial one)."""
+    import roaringbitmap_amd as rb
+    from roaringbitmap_amd.engine import HostSoA
+    nslices, nrows = 64, 100_000_000
+    d = ctx.generate_bsi(nslices, nrows, seed=42)
+    nkeys = (nrows + 65535) // 65536
+    hin = d.download()
+    lo, hi = 0x3A00_0000_0000_0000, 0xB100_0000_0000_0000
+    vmin, vmax = 0, (1 << nslices) - 1
+    keys = sorted(set(np.linspace(0, nkeys - 1, 9).astype(int).tolist()))
+    for opname, op, a1, a2 in (("RANGE", rb.BSI_RANGE, lo, hi), ("GE", rb.BSI_GE, lo, 0), ("LT", rb.BSI_LT, hi, 0)):
+        res = ctx.bsi_compare(op, d, a1, a2, vmin, vmax)
+        hres = res.download()
+        _check_canonical(hres)
+        for k in keys:
+            per = []
+            for b in range(nslices + 1):
+                i = int(hin.begin[b]) + k
+                assert int(hin.key[i]) == k
+                one = HostSoA(np.array([0, 1], np.uint64), hin.key[i:i + 1].copy(), hin.type[i:i + 1].copy(),
+                              hin.card[i:i + 1].copy(), hin.nruns[i:i + 1].copy(), np.zeros(1, np.uint64),
+                              hin.container_payload(i).copy())
+                from roaringbitmap_amd.sharding import serialize_parts
+                per.append(oracle.RefBitmap.deserialize(serialize_parts([one])))
+            want = oracle.bsi_compare(per[:-1], per[-1], op, a1, a2, None, vmin, vmax).serialize()
+            assert _subset_bytes(hres, [k]) == want, (opname, k)
+        res.close()
+    d.close()
