@@ -95,6 +95,7 @@ typedef struct rb_stats {
   double kernel_ms[4];
   uint64_t kernel_bytes[4];
   uint64_t kernel_items[4];
+  uint64_t result_cardinality; /* Σ cardinality of every result bitmap of the call */
 } rb_stats;
 
 /* ---- context ---------------------------------------------------------------------- */
@@ -141,6 +142,9 @@ typedef struct rb_bitmap_summary {
   uint64_t payload_bytes; /* serialized container payloads (Run: 2 + 4 * nruns), no header */
 } rb_bitmap_summary;
 int rbgpu_set_summaries(const rbgpu_set *set, uint32_t first, uint32_t count, rb_bitmap_summary *out);
+/* Container mix of the whole set, what insights/BitmapAnalyser reports (insights/BitmapAnalyser.java:
+ * 1-50): out[0..2] = Array / Bitmap / Run container counts, out[3..5] = their serialized payload bytes. */
+int rbgpu_set_type_stats(const rbgpu_set *set, uint64_t *out /* [6] */);
 /* Algorithmic bytes (payload + 16 B metadata) per high key over every container of the set:
  * out[65536].  Feeds the byte-balanced key-range partition of a sharded wide aggregation. */
 int rbgpu_set_key_bytes(const rbgpu_set *set, uint64_t *out);

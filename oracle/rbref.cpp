@@ -10,6 +10,7 @@
 #include "rbref.h"
 
 #include <algorithm>
+#include <atomic>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -1070,6 +1071,87 @@ BM *wide_par(const BM *const *bs, size_t n, bool is_xor) {
   return out;
 }
 
+// ---- key-parallel restatements (the CPU baseline on all host cores).  Every wide semantics is
+// per-key independent with the key's containers in member order, so each key's result is the
+// single-threaded one; ParallelAggregation itself is key-parallel on the ForkJoin pool
+// (ParallelAggregation.java:161-195, `IntStream.range(0, n).parallel()`).  Per key:
+//   FAST_OR      naivelazyor chain + repairAfterLazy (wide_naive_or)
+//   WORKSHY_AND  keys held by every member: lazy AND + repair, empty dropped (wide_workshy_and)
+//   FAST_XOR     in-place xor chain: absent -> clone, empty -> removed (wide_naive_xor)
+//   PAR_OR/XOR   par_or_list / par_xor_list (wide_par)
+bool key_result(int sem, const std::vector<const Cont *> &cs, size_t n, Cont &out) {
+  if (cs.empty()) return false;
+  switch (sem) {
+  case RBREF_FAST_OR: {
+    Cont acc = *cs[0];
+    for (size_t i = 1; i < cs.size(); ++i) acc = c_lazy_ior(to_bitmap(acc), *cs[i]);
+    out = repair(std::move(acc));
+    return true;
+  }
+  case RBREF_WORKSHY_AND: {
+    if (cs.size() != n) return false;
+    std::vector<uint64_t> w(kWords, ~0ull);
+    for (const Cont *c : cs) {
+      if (c->t == kA) {
+        std::vector<uint64_t> aw = array_words(c->v);
+        for (int i = 0; i < kWords; ++i) w[i] &= aw[i];
+      } else if (c->t == kB) {
+        for (int i = 0; i < kWords; ++i) w[i] &= c->w[i];
+      } else {
+        std::vector<uint64_t> rw = run_words(*c);
+        for (int i = 0; i < kWords; ++i) w[i] &= rw[i];
+      }
+    }
+    out = bitmap_repair(make_bitmap(std::move(w), -1));
+    return !is_empty(out);
+  }
+  case RBREF_FAST_XOR: {
+    bool present = false;
+    Cont acc;
+    for (const Cont *c : cs) {
+      if (!present) {
+        acc = *c;
+        present = true;
+      } else {
+        acc = c_ixor(acc, *c);
+        if (is_empty(acc)) present = false;
+      }
+    }
+    if (present) out = std::move(acc);
+    return present;
+  }
+  case RBREF_PAR_OR: out = par_or_list(cs); return true;
+  case RBREF_PAR_XOR: out = par_xor_list(cs); return !is_empty(out);
+  default: return false;
+  }
+}
+BM *wide_key_parallel(int sem, const BM *const *bs, size_t n, int threads) {
+  std::vector<std::vector<const Cont *>> g(kSpan); // ParallelAggregation.groupByKey (:137-153)
+  for (size_t m = 0; m < n; ++m)
+    for (size_t i = 0; i < bs[m]->size(); ++i) g[bs[m]->keys[i]].push_back(&bs[m]->vals[i]);
+  std::vector<Cont> res(kSpan);
+  std::vector<char> has(kSpan, 0);
+  std::atomic<int> next{0};
+  auto work = [&]() {
+    for (int k0; (k0 = next.fetch_add(64)) < kSpan;)
+      for (int k = k0; k < k0 + 64; ++k) has[k] = key_result(sem, g[k], n, res[k]);
+  };
+  if (threads <= 1) {
+    work();
+  } else {
+    std::vector<std::thread> th;
+    for (int t = 0; t < threads; ++t) th.emplace_back(work);
+    for (auto &x : th) x.join();
+  }
+  BM *out = new BM;
+  for (int k = 0; k < kSpan; ++k)
+    if (has[k]) {
+      out->keys.push_back((uint16_t)k);
+      out->vals.push_back(std::move(res[k]));
+    }
+  return out;
+}
+
 // ---------------------------------------------------------------- serialization helpers
 struct Reader {
   const uint8_t *p;
@@ -1350,6 +1432,13 @@ rbref_bitmap *rbref_wide(int sem, const rbref_bitmap *const *bs, size_t n) {
   case RBREF_NAIVE_AND_ITER: return wide_naive_and_iter(bs, n);
   default: return nullptr;
   }
+}
+
+rbref_bitmap *rbref_wide_mt(int sem, const rbref_bitmap *const *bs, size_t n, int threads) {
+  if (sem == RBREF_FAST_AND) sem = n > 10 ? RBREF_WORKSHY_AND : RBREF_NAIVE_AND;
+  if (sem == RBREF_NAIVE_AND || sem == RBREF_NAIVE_AND_ITER) return rbref_wide(sem, bs, n);
+  if (n == 0) return new BM;
+  return wide_key_parallel(sem, bs, n, threads);
 }
 
 int64_t rbref_wide_cardinality(int op, const rbref_bitmap *const *bs, size_t n) {

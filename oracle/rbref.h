@@ -84,6 +84,10 @@ int rbref_op_inplace(int op, rbref_bitmap *a, const rbref_bitmap *b);
 
 /* wide aggregation over bitmaps[0..n) (pointer identity matters for naive_and) */
 rbref_bitmap *rbref_wide(int sem, const rbref_bitmap *const *bitmaps, size_t n);
+/* The same aggregation computed key-parallel on `threads` host threads (every semantics is per-key
+ * independent; ParallelAggregation.or/xor are the reference's own key-parallel entry points,
+ * ParallelAggregation.java:161-195).  Identical result; the CPU baseline on all host cores. */
+rbref_bitmap *rbref_wide_mt(int sem, const rbref_bitmap *const *bitmaps, size_t n, int threads);
 /* FastAggregation.andCardinality / orCardinality — FastAggregation.java:71-101 */
 int64_t rbref_wide_cardinality(int op, const rbref_bitmap *const *bitmaps, size_t n);
 

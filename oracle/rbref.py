@@ -49,6 +49,7 @@ def _load():
         "rbref_op_inplace": (C.c_int, [C.c_int, P, P]),
         "rbref_wide": (P, [C.c_int, C.POINTER(P), C.c_size_t]),
         "rbref_wide_cardinality": (C.c_int64, [C.c_int, C.POINTER(P), C.c_size_t]),
+        "rbref_wide_mt": (P, [C.c_int, C.POINTER(P), C.c_size_t, C.c_int]),
         "rbref_pairwise_batch": (C.c_int, [C.c_int, C.POINTER(P), C.POINTER(P), C.c_size_t, C.c_int,
                                            C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
     }
@@ -152,6 +153,11 @@ def _handles(bitmaps):
 
 def wide(sem: int, bitmaps) -> RefBitmap:
     return RefBitmap(lib().rbref_wide(sem, _handles(bitmaps), len(bitmaps)))
+
+
+def wide_mt(sem: int, bitmaps, threads: int) -> RefBitmap:
+    """The same aggregation key-parallel on `threads` host threads (rbref_wide_mt)."""
+    return RefBitmap(lib().rbref_wide_mt(sem, _handles(bitmaps), len(bitmaps), threads))
 
 
 def wide_cardinality(opcode: int, bitmaps) -> int:

@@ -245,6 +245,7 @@ int stats_end(rbgpu_ctx *ctx, uint64_t tasks, uint64_t result_containers, const 
   s.tasks = tasks;
   s.input_bytes = w[0];
   s.output_bytes = w[1];
+  s.result_cardinality = w[7];
   s.result_containers = result_containers;
   float ms = 0;
   s.total_ms = hipEventElapsedTime(&ms, ctx->ev[0], ctx->ev[5]) == hipSuccess ? ms : 0.0;
@@ -540,6 +541,29 @@ int rbgpu_set_summaries(const rbgpu_set *s, uint32_t first, uint32_t count, rb_b
       o.n_run_containers += type[i] == RB_RUN;
       o.payload_bytes += type[i] == RB_BITMAP ? 8192ull : type[i] == RB_ARRAY ? 2ull * card[i] : 2 + 4ull * nruns[i];
     }
+  }
+  return RB_OK;
+}
+
+int rbgpu_set_type_stats(const rbgpu_set *s, uint64_t *out) {
+  if (!s || !out) return fail(RB_EINVAL, "null argument");
+  int rc = check_ctx(s->ctx);
+  if (rc) return rc;
+  const uint64_t n = s->nc;
+  std::vector<uint16_t> nruns(n);
+  std::vector<uint8_t> type(n);
+  std::vector<uint32_t> card(n);
+  if (n) {
+    HIPCHK(hipMemcpyAsync(type.data(), s->type, n, hipMemcpyDeviceToHost, s->ctx->stream));
+    HIPCHK(hipMemcpyAsync(nruns.data(), s->nruns, n * 2, hipMemcpyDeviceToHost, s->ctx->stream));
+    HIPCHK(hipMemcpyAsync(card.data(), s->card, n * 4, hipMemcpyDeviceToHost, s->ctx->stream));
+    HIPCHK(hipStreamSynchronize(s->ctx->stream));
+  }
+  std::fill(out, out + 6, 0ull);
+  for (uint64_t i = 0; i < n; ++i) {
+    const int t = type[i] <= RB_RUN ? type[i] : RB_RUN;
+    out[t] += 1;
+    out[3 + t] += t == RB_BITMAP ? 8192ull : t == RB_ARRAY ? 2ull * card[i] : 2 + 4ull * nruns[i];
   }
   return RB_OK;
 }

@@ -790,7 +790,7 @@ __global__ __launch_bounds__(kPairThreads) void k_compact_write(const uint64_t *
                                                                 const uint32_t *seg_pair, uint64_t *pair_card,
                                                                 uint64_t *stats) {
   const uint64_t p = (uint64_t)blockIdx.x * kPairThreads + threadIdx.x;
-  uint64_t outb[2] = {0, 0};
+  uint64_t outb[2] = {0, 0}, card_sum = 0;
   if (p < npairs) {
     uint64_t r = rbegin ? rbegin[p] : 0, card = 0;
     for (uint64_t t = tb[p]; t < tb[p + 1]; ++t) {
@@ -808,12 +808,14 @@ __global__ __launch_bounds__(kPairThreads) void k_compact_write(const uint64_t *
       ++r;
     }
     if (pair_card && card) atomicAdd((unsigned long long *)&pair_card[seg_pair[p]], (unsigned long long)card);
+    card_sum = card;
   }
-  // stats words: 1 total output, 4 light-task output, 5 heavy-task output
+  // stats words: 1 total output, 4 light-task output, 5 heavy-task output, 7 result cardinality
   if (stats) {
     stat_add(stats, 1, outb[0] + outb[1]);
     stat_add(stats, 4, outb[0]);
     stat_add(stats, 5, outb[1]);
+    stat_add(stats, 7, card_sum);
   }
 }
 

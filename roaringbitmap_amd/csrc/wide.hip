@@ -454,9 +454,14 @@ __global__ __launch_bounds__(256) void k_wide_keep(const uint8_t *type, uint32_t
   if (q < nk) keep[q] = type[q] != kEmpty;
 }
 __global__ __launch_bounds__(256) void k_wide_write(const uint32_t *klist, uint32_t nk, WideOut wo,
-                                                    const uint64_t *pos, OutView ov) {
+                                                    const uint64_t *pos, OutView ov, uint64_t *stats) {
   const uint32_t q = blockIdx.x * 256 + threadIdx.x;
-  if (q >= nk || wo.type[q] == kEmpty) return;
+  const bool live = q < nk && wo.type[q] != kEmpty;
+  // stats word 7: the result's cardinality (RoaringBitmap.getCardinality of the aggregate)
+  const uint64_t cs = wave_sum_u64(live ? (uint64_t)wo.card[q] : 0ull);
+  if ((threadIdx.x & 63) == 0 && cs)
+    atomicAdd((unsigned long long *)&stats[7 * kStripes + ((q >> 6) & (kStripes - 1))], (unsigned long long)cs);
+  if (!live) return;
   const uint64_t r = pos[q];
   ov.key[r] = (uint16_t)klist[q];
   ov.type[r] = wo.type[q];
@@ -483,7 +488,8 @@ int compact_keyed(rbgpu_ctx *ctx, const uint32_t *d_klist, uint32_t nk, const Wi
     k_wide_keep<<<nblk(nk, 256), 256, 0, st>>>(wo.type, nk, keep);
     scan_exclusive(keep, pos, nk, tmp2, st);
     k_wide_write<<<nblk(nk, 256), 256, 0, st>>>(d_klist, nk, wo, pos,
-                                                OutView{res->key, res->type, res->card, res->nruns, res->off});
+                                                OutView{res->key, res->type, res->card, res->nruns, res->off},
+                                                ctx->d_stats);
     HIPCHK(hipMemcpyAsync(pin + 1, pos + nk, 8, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
     LAUNCHCHK();

@@ -21,8 +21,13 @@
 //   * each step's type transition is a map on {Array, Bitmap, Run, absent}; the 32 maps are
 //     composed by a wave tree reduction, so the key's state after the batch is one lookup;
 //   * P is then updated by complementing the intervals with odd coverage.
+// Such exact batches run only where a step may cross a type threshold: stretches where no step can
+// (see "Fast-forward" below) apply their whole XOR at once and re-measure (c, r) once — on config 4
+// about 2 exact batches and 70 stretches per 4096-member key (k_wide_runs_xor 29.6 -> 14.5 ms).
 // Keys with another container type, > 8 runs or a full container are routed to the generic kernel
 // (route[q] = 1); results are identical either way.
+#include <cstdlib>
+
 #include "internal.hpp"
 #include "kernels.hpp"
 #include "wave.hpp"
@@ -168,270 +173,441 @@ __device__ __forceinline__ uint32_t dmask(uint32_t w, uint32_t lo, uint32_t hi) 
 
 } // namespace
 
-__global__ __launch_bounds__(256) void k_wide_runs_xor(SetView s, const uint32_t *__restrict__ cid,
-                                                       const uint64_t *__restrict__ seg,
-                                                       const uint32_t *__restrict__ klist, uint32_t nk,
-                                                       uint8_t *__restrict__ out, WideOut wo,
-                                                       uint8_t *__restrict__ route, uint64_t *stats) {
+// The key's state between steps: container type (0 Array, 1 Bitmap, 2 Run, 3 absent), cardinality and
+// maximal run count of the accumulator, and this lane's share of the algorithmic input bytes.
+struct XState {
+  int state, c, r;
+  uint32_t inb;
+  int rvalid; // r is only tracked where a rule can read it (see the fast-forward): Run states, exact batches
+};
+
+// One exact batch of <= 32 containers starting at `base` (the accumulator P is the LDS bitmap `acc`):
+// every step's (c_j, r_j) from the sorted run boundaries, the type maps composed, P updated.  Returns
+// false when a container of the batch does not qualify (the key goes to the generic kernel).
+__device__ __forceinline__ bool exact_batch(const SetView &s, const uint32_t *cid, uint64_t base, uint64_t hi,
+                                            uint32_t *acc, uint32_t *R, int lane, XState &X) {
+  uint16_t *R16 = reinterpret_cast<uint16_t *>(R);
+  uint16_t *pos = R16 + 2048;                       // [512] sorted position | tie/boundary bit 15
+  uint2 *MC = reinterpret_cast<uint2 *>(R);         // [512] (coverage mask, c0 | c1 << 16)
+  const int cj = lane >> 1, h = lane & 1;
+  const uint32_t below = (1u << cj) - 1u;
+  const XBatch cur = load_xbatch(s, cid, base + cj, hi, h);
+  const bool valid = base + (uint64_t)cj < hi;
+  const bool bad = valid && (cur.typ != kRun || cur.nr > 8u || cur.card >= (uint32_t)kSpan);
+  if (__ballot(bad)) return false;
+  if (valid && h == 0) X.inb += 4u * cur.nr + 2u + 16u;
+
+  // ---- prefix popcounts of P: row k = dwords [256k, 256k+256), lane l holds 4l..4l+3 of it;
+  //      pre16[d] = popcount of row dwords before d (<= 8192), rb (lane k) = popcount before row k
+  uint32_t rb = 0, run_tot = 0;
+  {
+    const uint4 *a4 = reinterpret_cast<const uint4 *>(acc);
+#pragma unroll
+    for (int k2 = 0; k2 < 4; ++k2) {
+      const uint4 v0 = a4[(2 * k2) * 64 + lane], v1 = a4[(2 * k2 + 1) * 64 + lane];
+      const uint32_t p00 = __popc(v0.x), p01 = __popc(v0.y), p02 = __popc(v0.z), p03 = __popc(v0.w);
+      const uint32_t p10 = __popc(v1.x), p11 = __popc(v1.y), p12 = __popc(v1.z), p13 = __popc(v1.w);
+      const uint32_t s0 = p00 + p01 + p02 + p03, s1 = p10 + p11 + p12 + p13;
+      const uint32_t inc = wave_scan_u32(s0 | (s1 << 16), lane);
+      const uint32_t ex = inc - (s0 | (s1 << 16));
+      const uint32_t e0 = ex & 0xFFFF, e1 = ex >> 16;
+      uint2 w0, w1;
+      w0.x = e0 | ((e0 + p00) << 16);
+      w0.y = (e0 + p00 + p01) | ((e0 + p00 + p01 + p02) << 16);
+      w1.x = e1 | ((e1 + p10) << 16);
+      w1.y = (e1 + p10 + p11) | ((e1 + p10 + p11 + p12) << 16);
+      reinterpret_cast<uint2 *>(R)[(2 * k2) * 64 + lane] = w0;
+      reinterpret_cast<uint2 *>(R)[(2 * k2 + 1) * 64 + lane] = w1;
+      const uint32_t tot = readlane(inc, 63);
+      if (lane == 2 * k2) rb = run_tot;
+      run_tot += tot & 0xFFFF;
+      if (lane == 2 * k2 + 1) rb = run_tot;
+      run_tot += tot >> 16;
+    }
+  }
+
+  // ---- the batch's run boundaries as sort keys (x << 9 | slot), slot = 8 lane + 2u + (0 start | 1 end+1)
+  uint32_t K[8];
+  {
+    const uint32_t rw[4] = {cur.r.x, cur.r.y, cur.r.z, cur.r.w};
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const bool ok = valid && (uint32_t)(4 * h + u) < cur.nr;
+      const uint32_t st = rw[u] & 0xFFFF, e1 = st + (rw[u] >> 16) + 1;
+      K[2 * u] = ok ? (st << 9) | (uint32_t)(8 * lane + 2 * u) : kNoKey;
+      K[2 * u + 1] = ok ? (e1 << 9) | (uint32_t)(8 * lane + 2 * u + 1) : kNoKey;
+    }
+  }
+  sort512(K, lane);
+
+  // ---- per sorted position i = 8 lane + e: coverage mask, tie-group rank, P(x), P(x-1), F(x)
+  uint32_t P[8], Mv[8], F[8], B[8], Q[8];
+  {
+    uint32_t m = 0, gl = 0, prevp = dpp<0x138>(K[7] >> 9); // wave_shr:1
+    uint32_t hmask = 0;                                     // bit e: position 8 lane + e heads a tie group
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const bool vld = K[e] != kNoKey;
+      P[e] = K[e] >> 9;
+      if (vld) m ^= 1u << ((K[e] >> 4) & 31);
+      Mv[e] = m;
+      const uint32_t pp = e ? P[e - 1] : prevp;
+      const bool head = (lane == 0 && e == 0) || P[e] != pp;
+      if (head) {
+        gl = (uint32_t)(8 * lane + e);
+        hmask |= 1u << e;
+      }
+      B[e] = gl; // last head at or before i, within this lane (0 if none yet)
+    }
+    const uint32_t mx = wave_xscan_xor(m, lane) ^ m;
+    const uint32_t gprev = dpp<0x138>(wave_scan_max(gl));
+    // first head after this lane: suffix max of (512 - first head) over the lanes above, via a
+    // lane reversal (ds_bpermute) and the forward max-scan
+    const uint32_t fh = hmask ? (uint32_t)(8 * lane) + __builtin_ctz(hmask) : 512u;
+    const uint32_t rv = (uint32_t)__builtin_amdgcn_ds_bpermute((63 - lane) << 2, (int)(512u - fh));
+    const uint32_t sc = (uint32_t)__builtin_amdgcn_ds_bpermute((63 - lane) << 2, (int)wave_scan_max(rv));
+    uint32_t nh = 512u - dpp<0x130>(sc); // wave_shl:1 -> lanes above only
+#pragma unroll
+    for (int e = 7; e >= 0; --e) {
+      Mv[e] ^= mx;
+      const uint32_t g = max(B[e], gprev);
+      B[e] = ((uint32_t)(8 * lane + e) - g) & 1u; // odd number of earlier batch containers share x
+      // interval range ends for the A loop: a start point's first positive-length interval is
+      // the last of its tie group; an end point's range stops at the first of its tie group
+      const bool is_end = K[e] & 1u;
+      Q[e] = is_end ? g : nh - 1;
+      if (hmask & (1u << e)) nh = (uint32_t)(8 * lane + e);
+    }
+    uint32_t RB[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) // outside the divergent branch: bpermute sources must be active
+      RB[e] = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((min(P[e], 65535u) >> 13) << 2), (int)rb);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const uint32_t x = P[e];
+      if (K[e] != kNoKey) {
+        const uint32_t xq = min(x, 65535u);
+        const uint32_t w = acc[xq >> 5];
+        const uint32_t wm1 = acc[(x ? x - 1 : 0) >> 5];
+        const uint32_t bx = (w >> (xq & 31)) & 1u;
+        const uint32_t bm1 = x ? (wm1 >> ((x - 1) & 31)) & 1u : 0u;
+        uint32_t f = RB[e] + R16[xq >> 5] + __popc(w & ((1u << (xq & 31)) - 1u));
+        if (x == 65536u) f += bx;
+        F[e] = f;
+        B[e] ^= (x == 65536u ? 0u : bx) ^ bm1;
+      } else {
+        F[e] = 0;
+      }
+    }
+  }
+  wave_lds_sync(); // pre16 is dead: the region now holds MC and pos
+  {
+    const uint32_t pn7 = dpp<0x130>(P[0]), fn7 = dpp<0x130>(F[0]); // wave_shl:1
+    uint32_t Cv[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const uint32_t pn = e < 7 ? P[e + 1] : pn7, fn = e < 7 ? F[e + 1] : fn7;
+      const uint32_t c0 = fn - F[e], c1 = (pn - P[e]) - c0;
+      Cv[e] = (c0 & 0xFFFF) | (c1 << 16);
+    }
+    uint4 *mc4 = reinterpret_cast<uint4 *>(MC + 8 * lane);
+#pragma unroll
+    for (int e = 0; e < 8; e += 2) mc4[e >> 1] = make_uint4(Mv[e], Cv[e], Mv[e + 1], Cv[e + 1]);
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+      if (K[e] != kNoKey) pos[K[e] & 511] = (uint16_t)(Q[e] | (B[e] << 15));
+    // ---- P ^= the batch: complement every elementary interval with odd coverage
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const uint32_t pn = e < 7 ? P[e + 1] : pn7;
+      if (K[e] != kNoKey && (__popc(Mv[e]) & 1) && pn > P[e]) { // (tie groups: zero-length intervals)
+        const uint32_t a = P[e], b = pn - 1;
+        for (uint32_t w = a >> 5; w <= (b >> 5); ++w) atomicXor(&acc[w], dmask(w, a, b));
+      }
+    }
+  }
+  wave_lds_sync();
+
+  // ---- |P_{j-1} ∩ C_j| and |T(P_{j-1}) ∩ T(C_j)| for the lane's 4 runs
+  uint32_t A = 0, match = 0;
+  {
+    const uint4 pv = reinterpret_cast<const uint4 *>(pos)[lane];
+    const uint32_t pw[4] = {pv.x, pv.y, pv.z, pv.w};
+    uint32_t qs[4], qe[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const bool ok = valid && (uint32_t)(4 * h + u) < cur.nr;
+      const uint32_t a = pw[u] & 0xFFFF, b = pw[u] >> 16;
+      qs[u] = ok ? (a & 0x7FFF) : 0;
+      qe[u] = ok ? (b & 0x7FFF) : 0;
+      if (ok) match += (a >> 15) + (b >> 15);
+    }
+    // one flattened loop over the lane's (up to 4) interval ranges, two entries per trip
+    uint32_t cs = qs[0], ce = qe[0], s1 = qs[1], e1 = qe[1], s2 = qs[2], e2 = qe[2], s3 = qs[3], e3 = qe[3];
+    while (true) {
+      if (cs >= ce) {
+        if (s1 >= e1 && s2 >= e2 && s3 >= e3) break;
+        cs = s1;
+        ce = e1;
+        s1 = s2;
+        e1 = e2;
+        s2 = s3;
+        e2 = e3;
+        s3 = e3 = 0;
+        continue;
+      }
+      const bool two = cs + 1 < ce;
+      const uint2 m0 = MC[cs], m1 = MC[two ? cs + 1 : cs];
+      A += (__popc(m0.x & below) & 1) ? (m0.y >> 16) : (m0.y & 0xFFFF);
+      if (two) A += (__popc(m1.x & below) & 1) ? (m1.y >> 16) : (m1.y & 0xFFFF);
+      cs += two ? 2 : 1;
+    }
+  }
+  wave_lds_sync(); // the next batch rewrites the region
+  A += xor_lane<1>(A, lane);
+  match += xor_lane<1>(match, lane);
+  const bool rep = valid && h == 0;
+  const int dc = rep ? (int)cur.card - 2 * (int)A : 0;
+  const int dr = rep ? (int)cur.nr - (int)match : 0;
+  const int ic = (int)wave_scan_u32((uint32_t)dc, lane), ir = (int)wave_scan_u32((uint32_t)dr, lane);
+  // ---- this step's type map (RunContainer.xor / ArrayContainer.xor / BitmapContainer.xor)
+  uint32_t f = kIdentityMap;
+  if (rep) {
+    const int cjv = X.c + ic, rjv = X.r + ir, cprev = cjv - dc;
+    const uint32_t te = cjv == 0 ? 3u : (uint32_t)type_eff(cjv, rjv);
+    const uint32_t ta = cjv == 0 ? 3u : (uint32_t)type_ab(cjv);
+    const uint32_t fa = cprev < kRunArrayThreshold ? te : ta;
+    f = fa | (ta << 2) | (te << 4) | (2u << 6); // absent -> clone (Run)
+  }
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = (uint32_t)__builtin_amdgcn_ds_bpermute(((lane + d) & 63) << 2, (int)f);
+    f = compose(lane + d < 64 ? y : kIdentityMap, f);
+  }
+  const uint32_t G = readlane(f, 0);
+  X.state = (int)((G >> (2 * X.state)) & 3u);
+  X.c += (int)readlane((uint32_t)ic, 63);
+  X.r += (int)readlane((uint32_t)ir, 63);
+  return true;
+}
+
+// Fast-forward.  With Run members the step rules only look at the accumulator's (c, r) through a few
+// thresholds: a Bitmap accumulator becomes AB(c_j); an Array one with c_{j-1} >= 32 becomes AB(c_j) too
+// (only |A| < 32 switches ArrayContainer.xor(Run) to EFF); a Run one becomes EFF(c_j, r_j); an empty
+// result removes the key (the next member is cloned, a Run).  So two kinds of stretches need no
+// per-step metrics:
+//   AB stretch   the accumulator is a Bitmap, an Array with c >= 32, or a Run whose first step cannot
+//                stay a Run (r - nruns > 2047, or 2 (r - nruns) > c + |C|), and every step keeps
+//                c_j >= 32: every step is AB(c_j), the last one decides the type;
+//   Run stretch  the accumulator is a Run and every step keeps 2 + 4 r_j <= min(8192, 2 c_j + 2): every
+//                step stays a Run.
+// The bounds: c_j = |P ⊕ X_j| with X_j the stretch's XOR so far, so |c_j - c| <= |X_j|, and
+// |X_j| <= Σ over the stretch's member pairs (2m, 2m+1) of |C_2m ⊕ C_2m+1| (+ |C_j| for an unpaired
+// last or first member) — pairs of members sharing a core cancel most of it; r_j <= r + Σ nruns.  A
+// stretch's XOR is applied at once (XOR commutes) through a toggle image of its run boundaries, and
+// (c, r) are re-measured on the result.  Bit-exact by construction; the exact batches run only where a
+// threshold may be crossed.
+struct XWin { // one container per lane: the fast-forward window
+  uint32_t typ, card, nr;
+  uint4 r0, r1;
+  uint32_t pairx; // even lanes: |C_lane ⊕ C_lane+1| (set by pair_xor)
+};
+// A window's loads form a chain (container id -> metadata -> run list), so they are software-pipelined
+// over four windows: the id of window w+3, the metadata of w+2 and the runs of w+1 are in flight while
+// window w is processed, and every load issued at an advance only uses values loaded a window earlier.
+struct XMeta {
+  uint32_t typ, card, nr;
+  uint64_t off;
+};
+// The loads are unconditional (addresses clamped to valid memory, results selected afterwards): a load
+// under a branch makes the waitcnt pass assume the worst at the merge and wait for every load in flight,
+// which would expose the whole chain's latency at every window.
+__device__ __forceinline__ XMeta load_xmeta(const SetView &s, uint32_t c, bool valid) {
+  XMeta m;
+  m.typ = s.type[c];
+  m.card = s.card[c];
+  m.nr = s.nruns[c];
+  m.off = s.off[c];
+  if (!valid) {
+    m.typ = kRun;
+    m.card = m.nr = 0u;
+    m.off = 0ull;
+  }
+  return m;
+}
+__device__ __forceinline__ XWin xwin_from(const SetView &s, const XMeta &m) {
+  XWin w;
+  w.typ = m.typ;
+  w.card = m.card;
+  w.nr = m.nr;
+  const bool runs = m.typ == kRun && m.nr && m.nr <= 8u;
+  // a non-Run (or invalid) member reads the arena's first 16 B instead; runs 4..7 exist only if nr > 4
+  const uint4 *p = reinterpret_cast<const uint4 *>(s.payload + (runs ? m.off : 0ull));
+  const uint4 a = p[0], b = p[runs && m.nr > 4u ? 1 : 0];
+  const uint4 z = make_uint4(0, 0, 0, 0);
+  w.r0 = runs ? a : z;
+  w.r1 = runs && m.nr > 4u ? b : z;
+  w.pairx = 0;
+  return w;
+}
+// An upper bound of |C_l ⊕ C_l+1| = |C_l| + |C_l+1| - 2 |C_l ∩ C_l+1| for every lane l (meaningful on
+// even lanes whose neighbour is in the window): |C_l ∩ C_l+1| is at least the overlap of the two
+// containers' longest runs (members that share a core run overlap there); the neighbour's longest run
+// comes over by DPP.
+__device__ __forceinline__ void pair_xor(XWin &w) {
+  const uint32_t a[8] = {w.r0.x, w.r0.y, w.r0.z, w.r0.w, w.r1.x, w.r1.y, w.r1.z, w.r1.w};
+  uint32_t best = 0; // (len - 1) << 16 | start of the longest run
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const uint32_t key = (a[u] >> 16) << 16 | (a[u] & 0xFFFF);
+    if ((uint32_t)u < w.nr && (key >> 16) >= (best >> 16)) best = key;
+  }
+  const uint32_t nbest = dpp<0x130>(best), cb = dpp<0x130>(w.card); // wave_shl:1 — lane l reads lane l+1
+  const int sa = (int)(best & 0xFFFF), ea = sa + (int)(best >> 16);
+  const int sb = (int)(nbest & 0xFFFF), eb = sb + (int)(nbest >> 16);
+  const int inter = w.nr ? max(0, min(ea, eb) - max(sa, sb) + 1) : 0;
+  w.pairx = w.card + cb - 2u * (uint32_t)inter;
+}
+#ifndef RBG_XF_ABLATE
+#define RBG_XF_ABLATE 0 // timing study only (wrong results): 1 no toggles, 2 no prefix-xor, 4 no re-measure, 8 no pair bound,
+                        // 16 no window loads after the first
+#endif
+#ifndef RBG_XOR_MIN_FAST
+#define RBG_XOR_MIN_FAST 8 // shortest stretch worth a fast-forward (an exact batch costs ~32 stretches' steps)
+#endif
+
+__global__ __launch_bounds__(256, 3) void k_wide_runs_xor(SetView s, const uint32_t *__restrict__ cid,
+                                                          const uint64_t *__restrict__ seg,
+                                                          const uint32_t *__restrict__ klist, uint32_t nk,
+                                                          uint8_t *__restrict__ out, WideOut wo,
+                                                          uint8_t *__restrict__ route, uint64_t *stats,
+                                                          int fastfwd) {
   __shared__ __attribute__((aligned(16))) uint32_t acc_all[4][2048];
   __shared__ __attribute__((aligned(16))) uint32_t reg_all[4][kXRegion];
   const int lane = lane_id();
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t q = blockIdx.x * 4 + wv;
   if (q >= nk) return;
+  // acc: the accumulator P during exact batches, the (zeroed) toggle image of fast-forwards; P itself
+  // lives in registers between batches (the 65536-bit register layout of wave.hpp)
   uint32_t *acc = acc_all[wv];
   uint32_t *R = reg_all[wv];
-  uint16_t *R16 = reinterpret_cast<uint16_t *>(R);
-  uint16_t *pos = R16 + 2048;                       // [512] sorted position | tie/boundary bit 15
-  uint2 *MC = reinterpret_cast<uint2 *>(R);         // [512] (coverage mask, c0 | c1 << 16)
   const uint32_t key = klist[q];
   const uint64_t lo = seg[key], hi = seg[key + 1];
-  if (hi > lo && s.type[cid[lo]] != kRun) { // first container not a Run: route before any batch load
+  if (hi <= lo || s.type[cid[lo]] != kRun) { // (no member) / first container not a Run: the generic kernel
     if (lane == 0) route[q] = 1;
     return;
   }
   lds_zero(acc, lane);
   wave_lds_sync();
-  const int cj = lane >> 1, h = lane & 1;
-  const uint32_t below = (1u << cj) - 1u;
-  int state = 3, c = 0, r = 0;
-  uint32_t inb = 0;
+  uint64_t Pw[kW];
+#pragma unroll
+  for (int j = 0; j < kW; ++j) Pw[j] = 0;
+  XState X{3, 0, 0, 0u, 1};
   bool fail_route = false;
-  XBatch nxt = load_xbatch(s, cid, lo + cj, hi, h);
-  for (uint64_t base = lo; base < hi; base += kXB) {
-    const XBatch cur = nxt;
-    __builtin_amdgcn_sched_barrier(0);
-    if (base + kXB < hi) nxt = load_xbatch(s, cid, base + kXB + cj, hi, h);
-    const bool valid = base + (uint64_t)cj < hi;
-    const bool bad = valid && (cur.typ != kRun || cur.nr > 8u || cur.card >= (uint32_t)kSpan);
-    if (__ballot(bad)) {
+  uint64_t wbase = lo;
+  auto cid_at = [&](uint64_t i) { // unconditional load (see load_xmeta); hi > lo here
+    const uint32_t c = cid[i < hi ? i : hi - 1];
+    return i < hi ? c : 0u;
+  };
+  const uint32_t c0 = cid_at(lo + lane), c1 = cid_at(lo + 64 + lane), c2 = cid_at(lo + 128 + lane);
+  const XMeta m0 = load_xmeta(s, c0, lo + lane < hi), m1 = load_xmeta(s, c1, lo + 64 + lane < hi);
+  XWin W = xwin_from(s, m0);                                 // window w
+  XWin N = xwin_from(s, m1);                                 // w+1: runs in flight
+  XMeta NN = load_xmeta(s, c2, lo + 128 + lane < hi);        // w+2: metadata in flight
+  uint32_t NNN = cid_at(lo + 192 + lane);                    // w+3: id in flight
+  pair_xor(W);
+  uint64_t base = lo;
+  while (base < hi) {
+    const uint32_t posw = __builtin_amdgcn_readfirstlane((uint32_t)(base - wbase)); // < 64
+    const bool inwin = (uint32_t)lane >= posw && wbase + (uint64_t)lane < hi;
+    if (__ballot(inwin && (W.typ != kRun || W.nr > 8u || W.card >= (uint32_t)kSpan))) {
       fail_route = true;
       break;
     }
-    if (valid && h == 0) inb += 4u * cur.nr + 2u + 16u;
-
-    // ---- prefix popcounts of P: row k = dwords [256k, 256k+256), lane l holds 4l..4l+3 of it;
-    //      pre16[d] = popcount of row dwords before d (<= 8192), rb (lane k) = popcount before row k
-    uint32_t rb = 0, run_tot = 0;
-    {
-      const uint4 *a4 = reinterpret_cast<const uint4 *>(acc);
-#pragma unroll
-      for (int k2 = 0; k2 < 4; ++k2) {
-        const uint4 v0 = a4[(2 * k2) * 64 + lane], v1 = a4[(2 * k2 + 1) * 64 + lane];
-        const uint32_t p00 = __popc(v0.x), p01 = __popc(v0.y), p02 = __popc(v0.z), p03 = __popc(v0.w);
-        const uint32_t p10 = __popc(v1.x), p11 = __popc(v1.y), p12 = __popc(v1.z), p13 = __popc(v1.w);
-        const uint32_t s0 = p00 + p01 + p02 + p03, s1 = p10 + p11 + p12 + p13;
-        const uint32_t inc = wave_scan_u32(s0 | (s1 << 16), lane);
-        const uint32_t ex = inc - (s0 | (s1 << 16));
-        const uint32_t e0 = ex & 0xFFFF, e1 = ex >> 16;
-        uint2 w0, w1;
-        w0.x = e0 | ((e0 + p00) << 16);
-        w0.y = (e0 + p00 + p01) | ((e0 + p00 + p01 + p02) << 16);
-        w1.x = e1 | ((e1 + p10) << 16);
-        w1.y = (e1 + p10 + p11) | ((e1 + p10 + p11 + p12) << 16);
-        reinterpret_cast<uint2 *>(R)[(2 * k2) * 64 + lane] = w0;
-        reinterpret_cast<uint2 *>(R)[(2 * k2 + 1) * 64 + lane] = w1;
-        const uint32_t tot = readlane(inc, 63);
-        if (lane == 2 * k2) rb = run_tot;
-        run_tot += tot & 0xFFFF;
-        if (lane == 2 * k2 + 1) rb = run_tot;
-        run_tot += tot >> 16;
-      }
+    // ---- the longest stretch from posw that provably crosses no threshold (see above)
+    const uint32_t wlen = (uint32_t)min<uint64_t>(64, hi - wbase); // containers in the window
+    const int nr_first = (int)readlane(W.nr, (int)posw), card_first = (int)readlane(W.card, (int)posw);
+    const uint32_t first_even = posw + (posw & 1u);
+    const uint32_t pair_in = dpp<0x138>(W.pairx); // wave_shr:1 — the pair (lane-1, lane) on its odd lane
+    const bool odd_end = inwin && (lane & 1) && (uint32_t)lane >= first_even + 1u;
+    const int S = (int)wave_scan_u32(odd_end ? pair_in : 0u, lane);
+    const bool open_pair = inwin && (uint32_t)lane >= first_even && (((uint32_t)lane - first_even) & 1u) == 0;
+    const int bound = ((posw & 1u) ? card_first : 0) + S + (open_pair ? (int)W.card : 0); // >= |X_j|
+    const int ab_ok_first = X.state == kBitmap || (X.state == kArray && X.c >= kRunArrayThreshold) ||
+                            (X.state == kRun && (X.r - nr_first > 2047 || 2 * (X.r - nr_first) > X.c + card_first));
+    bool ok = false;
+    int mode = 0; // 1: AB stretch, 2: Run stretch
+    if (ab_ok_first) {
+      mode = 1;
+      ok = inwin && X.c - bound >= kRunArrayThreshold;
+    } else if (X.state == kRun) {
+      mode = 2;
+      const int rub = X.r + (int)wave_scan_u32(inwin ? W.nr : 0u, lane), clb = X.c - bound;
+      ok = inwin && clb >= 1 && 2 + 4 * rub <= min(kBitmapBytes, 2 * clb + 2);
     }
-
-    // ---- the batch's run boundaries as sort keys (x << 9 | slot), slot = 8 lane + 2u + (0 start | 1 end+1)
-    uint32_t K[8];
-    {
-      const uint32_t rw[4] = {cur.r.x, cur.r.y, cur.r.z, cur.r.w};
+    const uint64_t okm = __ballot(ok) >> posw;
+    // leading members within the bounds (all 64 when posw == 0 and ~okm == 0: ctz of 0 is undefined)
+    const uint32_t B = fastfwd ? min(~okm ? (uint32_t)__builtin_ctzll(~okm) : 64u, wlen - posw) : 0u;
+    if (B >= RBG_XOR_MIN_FAST || (B >= 1 && posw + B == wlen)) {
+      if (!(RBG_XF_ABLATE & 1) && (uint32_t)lane >= posw && (uint32_t)lane < posw + B) {
+        const uint32_t rw[8] = {W.r0.x, W.r0.y, W.r0.z, W.r0.w, W.r1.x, W.r1.y, W.r1.z, W.r1.w};
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const bool ok = valid && (uint32_t)(4 * h + u) < cur.nr;
-        const uint32_t st = rw[u] & 0xFFFF, e1 = st + (rw[u] >> 16) + 1;
-        K[2 * u] = ok ? (st << 9) | (uint32_t)(8 * lane + 2 * u) : kNoKey;
-        K[2 * u + 1] = ok ? (e1 << 9) | (uint32_t)(8 * lane + 2 * u + 1) : kNoKey;
-      }
-    }
-    sort512(K, lane);
-
-    // ---- per sorted position i = 8 lane + e: coverage mask, tie-group rank, P(x), P(x-1), F(x)
-    uint32_t P[8], Mv[8], F[8], B[8], Q[8];
-    {
-      uint32_t m = 0, gl = 0, prevp = dpp<0x138>(K[7] >> 9); // wave_shr:1
-      uint32_t hmask = 0;                                     // bit e: position 8 lane + e heads a tie group
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const bool vld = K[e] != kNoKey;
-        P[e] = K[e] >> 9;
-        if (vld) m ^= 1u << ((K[e] >> 4) & 31);
-        Mv[e] = m;
-        const uint32_t pp = e ? P[e - 1] : prevp;
-        const bool head = (lane == 0 && e == 0) || P[e] != pp;
-        if (head) {
-          gl = (uint32_t)(8 * lane + e);
-          hmask |= 1u << e;
+        for (int u = 0; u < 8; ++u) {
+          if ((uint32_t)u < W.nr) {
+            const uint32_t st = rw[u] & 0xFFFF, e1 = st + (rw[u] >> 16) + 1;
+            atomicXor(&acc[st >> 5], 1u << (st & 31));
+            if (e1 < (uint32_t)kSpan) atomicXor(&acc[e1 >> 5], 1u << (e1 & 31));
+          }
         }
-        B[e] = gl; // last head at or before i, within this lane (0 if none yet)
+        X.inb += 4u * W.nr + 2u + 16u;
       }
-      const uint32_t mx = wave_xscan_xor(m, lane) ^ m;
-      const uint32_t gprev = dpp<0x138>(wave_scan_max(gl));
-      // first head after this lane: suffix max of (512 - first head) over the lanes above, via a
-      // lane reversal (ds_bpermute) and the forward max-scan
-      const uint32_t fh = hmask ? (uint32_t)(8 * lane) + __builtin_ctz(hmask) : 512u;
-      const uint32_t rv = (uint32_t)__builtin_amdgcn_ds_bpermute((63 - lane) << 2, (int)(512u - fh));
-      const uint32_t sc = (uint32_t)__builtin_amdgcn_ds_bpermute((63 - lane) << 2, (int)wave_scan_max(rv));
-      uint32_t nh = 512u - dpp<0x130>(sc); // wave_shl:1 -> lanes above only
+      wave_lds_sync();
+      uint64_t t[kW];
+      lds_read_words(acc, t, lane);
+      wave_lds_sync();
+      lds_zero(acc, lane);
+      if (!(RBG_XF_ABLATE & 2)) toggles_to_words(t, lane);
 #pragma unroll
-      for (int e = 7; e >= 0; --e) {
-        Mv[e] ^= mx;
-        const uint32_t g = max(B[e], gprev);
-        B[e] = ((uint32_t)(8 * lane + e) - g) & 1u; // odd number of earlier batch containers share x
-        // interval range ends for the A loop: a start point's first positive-length interval is
-        // the last of its tie group; an end point's range stops at the first of its tie group
-        const bool is_end = K[e] & 1u;
-        Q[e] = is_end ? g : nh - 1;
-        if (hmask & (1u << e)) nh = (uint32_t)(8 * lane + e);
+      for (int j = 0; j < kW; ++j) Pw[j] ^= t[j];
+      // an AB stretch leaves a Bitmap / Array accumulator whose next rule reads only c (AB), so r is
+      // counted again only when a rule can read it (Run stretch, exact batch, the result)
+      int cc = X.c, rr = X.r;
+      if (!(RBG_XF_ABLATE & 4)) metrics(Pw, lane, mode == 2, cc, rr);
+      X.c = cc;
+      X.r = rr;
+      X.rvalid = mode == 2;
+      X.state = mode == 1 ? type_ab(cc) : kRun;
+      base += B;
+    } else {
+      if (!X.rvalid) {
+        int cc, rr;
+        metrics(Pw, lane, true, cc, rr);
+        X.r = rr;
+        X.rvalid = 1;
       }
-      uint32_t RB[8];
-#pragma unroll
-      for (int e = 0; e < 8; ++e) // outside the divergent branch: bpermute sources must be active
-        RB[e] = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((min(P[e], 65535u) >> 13) << 2), (int)rb);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const uint32_t x = P[e];
-        if (K[e] != kNoKey) {
-          const uint32_t xq = min(x, 65535u);
-          const uint32_t w = acc[xq >> 5];
-          const uint32_t wm1 = acc[(x ? x - 1 : 0) >> 5];
-          const uint32_t bx = (w >> (xq & 31)) & 1u;
-          const uint32_t bm1 = x ? (wm1 >> ((x - 1) & 31)) & 1u : 0u;
-          uint32_t f = RB[e] + R16[xq >> 5] + __popc(w & ((1u << (xq & 31)) - 1u));
-          if (x == 65536u) f += bx;
-          F[e] = f;
-          B[e] ^= (x == 65536u ? 0u : bx) ^ bm1;
-        } else {
-          F[e] = 0;
-        }
+      lds_write_words(acc, Pw, lane);
+      wave_lds_sync();
+      if (!exact_batch(s, cid, base, hi, acc, R, lane, X)) {
+        fail_route = true;
+        break;
       }
-    }
-    wave_lds_sync(); // pre16 is dead: the region now holds MC and pos
-    {
-      const uint32_t pn7 = dpp<0x130>(P[0]), fn7 = dpp<0x130>(F[0]); // wave_shl:1
-      uint32_t Cv[8];
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const uint32_t pn = e < 7 ? P[e + 1] : pn7, fn = e < 7 ? F[e + 1] : fn7;
-        const uint32_t c0 = fn - F[e], c1 = (pn - P[e]) - c0;
-        Cv[e] = (c0 & 0xFFFF) | (c1 << 16);
-      }
-      uint4 *mc4 = reinterpret_cast<uint4 *>(MC + 8 * lane);
-#pragma unroll
-      for (int e = 0; e < 8; e += 2) mc4[e >> 1] = make_uint4(Mv[e], Cv[e], Mv[e + 1], Cv[e + 1]);
-#pragma unroll
-      for (int e = 0; e < 8; ++e)
-        if (K[e] != kNoKey) pos[K[e] & 511] = (uint16_t)(Q[e] | (B[e] << 15));
-      // ---- P ^= the batch: complement every elementary interval with odd coverage
-#if RBG_XOR_APPLY_FLAT
-      // one flattened loop over the lane's odd intervals (a queue of up to 8), one dword per trip
-      uint32_t live = 0;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const uint32_t pn = e < 7 ? P[e + 1] : pn7;
-        if (K[e] != kNoKey && (__popc(Mv[e]) & 1) && pn > P[e]) live |= 1u << e; // (ties: zero length)
-      }
-      uint32_t w = 1, wend = 0, ia = 0, ib = 0;
-      while (true) {
-        if (w > wend) {
-          if (!live) break;
-          const int e = __builtin_ctz(live);
-          live &= live - 1;
-          uint32_t a = P[0], pn = P[1];
-#pragma unroll
-          for (int t = 1; t < 8; ++t)
-            if (e == t) {
-              a = P[t];
-              pn = t < 7 ? P[t + 1] : pn7;
-            }
-          ia = a;
-          ib = pn - 1;
-          w = a >> 5;
-          wend = ib >> 5;
-        }
-        atomicXor(&acc[w], dmask(w, ia, ib));
-        ++w;
-      }
-#else
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const uint32_t pn = e < 7 ? P[e + 1] : pn7;
-        if (K[e] != kNoKey && (__popc(Mv[e]) & 1) && pn > P[e]) { // (tie groups: zero-length intervals)
-          const uint32_t a = P[e], b = pn - 1;
-          for (uint32_t w = a >> 5; w <= (b >> 5); ++w) atomicXor(&acc[w], dmask(w, a, b));
-        }
-      }
-#endif
+      lds_read_words(acc, Pw, lane);
+      wave_lds_sync();
+      lds_zero(acc, lane);
+      base += kXB;
     }
     wave_lds_sync();
-
-    // ---- |P_{j-1} ∩ C_j| and |T(P_{j-1}) ∩ T(C_j)| for the lane's 4 runs
-    uint32_t A = 0, match = 0;
-    {
-      const uint4 pv = reinterpret_cast<const uint4 *>(pos)[lane];
-      const uint32_t pw[4] = {pv.x, pv.y, pv.z, pv.w};
-      uint32_t qs[4], qe[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const bool ok = valid && (uint32_t)(4 * h + u) < cur.nr;
-        const uint32_t a = pw[u] & 0xFFFF, b = pw[u] >> 16;
-        qs[u] = ok ? (a & 0x7FFF) : 0;
-        qe[u] = ok ? (b & 0x7FFF) : 0;
-        if (ok) match += (a >> 15) + (b >> 15);
+    if (base >= wbase + 64 && base < hi) {
+      wbase += 64;
+      if (!(RBG_XF_ABLATE & 16)) {
+        W = N;
+        N = xwin_from(s, NN);
+        NN = load_xmeta(s, NNN, wbase + 128 + lane < hi);
+        NNN = cid_at(wbase + 192 + lane);
       }
-      // one flattened loop over the lane's (up to 4) interval ranges, two entries per trip
-      uint32_t cs = qs[0], ce = qe[0], s1 = qs[1], e1 = qe[1], s2 = qs[2], e2 = qe[2], s3 = qs[3], e3 = qe[3];
-      while (true) {
-        if (cs >= ce) {
-          if (s1 >= e1 && s2 >= e2 && s3 >= e3) break;
-          cs = s1;
-          ce = e1;
-          s1 = s2;
-          e1 = e2;
-          s2 = s3;
-          e2 = e3;
-          s3 = e3 = 0;
-          continue;
-        }
-        const bool two = cs + 1 < ce;
-        const uint2 m0 = MC[cs], m1 = MC[two ? cs + 1 : cs];
-        A += (__popc(m0.x & below) & 1) ? (m0.y >> 16) : (m0.y & 0xFFFF);
-        if (two) A += (__popc(m1.x & below) & 1) ? (m1.y >> 16) : (m1.y & 0xFFFF);
-        cs += two ? 2 : 1;
-      }
+      if (!(RBG_XF_ABLATE & 8)) pair_xor(W);
     }
-    wave_lds_sync(); // the next batch rewrites the region
-    A += xor_lane<1>(A, lane);
-    match += xor_lane<1>(match, lane);
-    const bool rep = valid && h == 0;
-    const int dc = rep ? (int)cur.card - 2 * (int)A : 0;
-    const int dr = rep ? (int)cur.nr - (int)match : 0;
-    const int ic = (int)wave_scan_u32((uint32_t)dc, lane), ir = (int)wave_scan_u32((uint32_t)dr, lane);
-    // ---- this step's type map (RunContainer.xor / ArrayContainer.xor / BitmapContainer.xor)
-    uint32_t f = kIdentityMap;
-    if (rep) {
-      const int cjv = c + ic, rjv = r + ir, cprev = cjv - dc;
-      const uint32_t te = cjv == 0 ? 3u : (uint32_t)type_eff(cjv, rjv);
-      const uint32_t ta = cjv == 0 ? 3u : (uint32_t)type_ab(cjv);
-      const uint32_t fa = cprev < kRunArrayThreshold ? te : ta;
-      f = fa | (ta << 2) | (te << 4) | (2u << 6); // absent -> clone (Run)
-    }
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const uint32_t y = (uint32_t)__builtin_amdgcn_ds_bpermute(((lane + d) & 63) << 2, (int)f);
-      f = compose(lane + d < 64 ? y : kIdentityMap, f);
-    }
-    const uint32_t G = readlane(f, 0);
-    state = (int)((G >> (2 * state)) & 3u);
-    c += (int)readlane((uint32_t)ic, 63);
-    r += (int)readlane((uint32_t)ir, 63);
   }
   if (fail_route) {
     if (lane == 0) route[q] = 1;
@@ -439,22 +615,21 @@ __global__ __launch_bounds__(256) void k_wide_runs_xor(SetView s, const uint32_t
   }
   // ---- result
   uint8_t *dst = out + (uint64_t)q * kBitmapBytes;
-  const int ty = state == 3 ? (int)kEmpty : state;
+  const int ty = X.state == 3 ? (int)kEmpty : X.state;
+  int c = X.c, r = X.r;
   if (ty != (int)kEmpty) {
-    uint64_t w[kW];
-    lds_read_words(acc, w, lane);
-    wave_lds_sync();
     // the chain's metrics must describe the accumulated set; a mismatch (never expected) sends the
     // key to the generic kernel instead of emitting a container sized from wrong metrics
     int cc, rr;
-    metrics(w, lane, true, cc, rr);
+    metrics(Pw, lane, true, cc, rr);
+    if (!X.rvalid) r = rr;
     if (cc != c || rr != r) {
       if (lane == 0) route[q] = 1;
       return;
     }
-    emit_container(ty, w, c, r, dst, acc, lane);
+    emit_container(ty, Pw, c, r, dst, acc, lane);
   }
-  const uint32_t inb_sum = wave_sum_u32(inb);
+  const uint32_t inb_sum = wave_sum_u32(X.inb);
   if (lane == 0) {
     route[q] = 0;
     wo.type[q] = (uint8_t)ty;
@@ -472,7 +647,10 @@ void launch_wide_runs_xor(const SetView &s, const uint32_t *cid, const uint64_t 
                           uint32_t nk, uint8_t *out, const WideOut &wo, uint8_t *route, uint64_t *stats,
                           hipStream_t st) {
   if (!nk) return;
-  k_wide_runs_xor<<<(nk + 3) / 4, 256, 0, st>>>(s, cid, seg, klist, nk, out, wo, route, stats);
+  // RBGPU_XOR_NO_FASTFWD=1: exact batches only (an A/B switch for the parity tests)
+  const char *e = getenv("RBGPU_XOR_NO_FASTFWD");
+  const int fastfwd = !(e && e[0] == '1');
+  k_wide_runs_xor<<<(nk + 3) / 4, 256, 0, st>>>(s, cid, seg, klist, nk, out, wo, route, stats, fastfwd);
 }
 
 } // namespace rbg

@@ -228,6 +228,13 @@ class DeviceSet:
         L.check(L.lib().rbgpu_set_summaries(self.h, first, count, arr))
         return [{k: int(getattr(arr[i], k)) for k, _ in L.RbBitmapSummary._fields_} for i in range(count)]
 
+    def type_stats(self) -> dict:
+        """Container mix (rbgpu_set_type_stats): counts and serialized payload bytes per type."""
+        out = np.zeros(6, np.uint64)
+        L.check(L.lib().rbgpu_set_type_stats(self.h, out.ctypes.data_as(L._U64P)))
+        return {"array": int(out[0]), "bitmap": int(out[1]), "run": int(out[2]),
+                "array_bytes": int(out[3]), "bitmap_bytes": int(out[4]), "run_bytes": int(out[5])}
+
     def key_bytes(self) -> np.ndarray:
         """Algorithmic bytes per high key (rbgpu_set_key_bytes), shape [65536]."""
         out = np.zeros(65536, np.uint64)

@@ -311,3 +311,55 @@ def test_batched_xor_long_chains(ctx, oracle):
         assert ctx.wide(rb.FAST_XOR, s, members).serialize()[0] == want
     finally:
         del os.environ["RBGPU_NO_RUN_FASTPATH"]
+
+
+def _runs_container(rng, nruns, lo, hi, maxlen):
+    """Sorted values of <= nruns random runs of length 4..maxlen inside [lo, hi) (overlaps merge; >= 4
+    values per run keeps runOptimize's choice a Run container)."""
+    v = []
+    for _ in range(nruns):
+        s0 = int(rng.integers(lo, hi - 4))
+        v.append(np.arange(s0, min(s0 + int(rng.integers(4, maxlen + 1)), hi)))
+    return np.unique(np.concatenate(v))
+
+
+def test_xor_fastforward_threshold_regimes(ctx, oracle):
+    """naive_xor's fast-forward (wide_xor.hip) skips per-step metrics only where no step can cross a
+    type threshold; chains built to hover at each threshold must still give the oracle's bytes, and the
+    same bytes with the fast-forward off (RBGPU_XOR_NO_FASTFWD=1):
+      key 0  config-4 shape (shared core + random runs): long AB stretches (Bitmap), Run stretches early;
+      key 1  values in [0, 8192): c hovers around 4096 (Array <-> Bitmap at every few steps);
+      key 2  tiny runs in [0, 64): c near 32 (the |A| < 32 EFF rule of Array ^ Run);
+      key 3  many 4-6 value runs in [0, 12000): r around 2047 and 2r ~ c (Run <-> Bitmap by EFF);
+      key 4  repeated members: the chain empties (key removed, next member cloned as a Run)."""
+    import os
+
+    import roaringbitmap_amd as rb
+    rng = np.random.default_rng(44)
+    nb = 260
+    per = [[] for _ in range(nb)]
+    prev = None
+    for b in range(nb):
+        parts = [np.unique(np.concatenate([np.arange(7000, 8024), _runs_container(rng, 7, 0, 65536, 256)])),
+                 _runs_container(rng, int(rng.integers(1, 9)), 0, 8192, 400),
+                 _runs_container(rng, int(rng.integers(1, 4)), 0, 64, 10),
+                 _runs_container(rng, 8, 0, 12000, 6)]
+        if prev is not None and b % 5 == 1:
+            parts.append(prev)
+        else:
+            prev = _runs_container(rng, 6, 30000, 36000, 300)
+            parts.append(prev)
+        per[b] = np.concatenate([(p.astype(np.uint32) % 65536) | np.uint32(k << 16) for k, p in enumerate(parts)])
+    s = ctx.upload_values(per, run_optimize=True)
+    h = s.download()
+    assert set(h.type.tolist()) == {rb.RUN} and int(h.nruns.max()) <= 8  # all members take the Run path
+    refs = [oracle.RefBitmap.deserialize(x) for x in s.serialize()]
+    for n in (nb, 200, 129, 64, 65):
+        members = np.arange(n, dtype=np.uint32)
+        want = oracle.wide(oracle.FAST_XOR, [refs[m] for m in members]).serialize()
+        assert ctx.wide(rb.FAST_XOR, s, members).serialize()[0] == want, n
+        os.environ["RBGPU_XOR_NO_FASTFWD"] = "1"
+        try:
+            assert ctx.wide(rb.FAST_XOR, s, members).serialize()[0] == want, n
+        finally:
+            del os.environ["RBGPU_XOR_NO_FASTFWD"]

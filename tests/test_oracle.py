@@ -140,3 +140,20 @@ def test_bsi_known_answers(oracle):
     assert q(R.BSI_EQ, 0, s=zero) == [0, 1] and q(R.BSI_EQ, 1, s=zero) == [2]
     eq = R.bsi_build(list(range(1, 100)), [1 if x <= 50 else x for x in range(1, 100)])
     assert len(q(R.BSI_EQ, 1, s=eq)) == 50
+
+
+@pytest.mark.parametrize("sem", ["FAST_OR", "FAST_AND", "WORKSHY_AND", "FAST_XOR", "PAR_OR", "PAR_XOR"])
+def test_key_parallel_restatement_matches(oracle, sem):
+    """rbref_wide_mt (the all-cores CPU baseline) gives the single-threaded oracle's bytes for every
+    key-independent semantics, on real data and on mixed synthetic bitmaps."""
+    from datasets import synthetic_bitmaps
+    R = oracle
+    sets = [[R.RefBitmap.of(v) for v in load_realdata("census1881_srt")[:60]],
+            [R.RefBitmap.of(v) for v in synthetic_bitmaps(40, seed=4, max_keys=6, key_space=6)]]
+    for bms in sets:
+        for r in bms[::2]:
+            r.run_optimize()
+        for n in (3, 11, len(bms)):
+            want = R.wide(getattr(R, sem), bms[:n]).serialize()
+            for threads in (1, 4):
+                assert R.wide_mt(getattr(R, sem), bms[:n], threads).serialize() == want, (sem, n, threads)
