@@ -1,17 +1,25 @@
 #!/usr/bin/env python3
 """Benchmark of the MI355X RoaringBitmap set-algebra path (BASELINE.json metric).
 
-Default workload (N=1): SURVEY §8d config 2 — batched pairwise AND of 1M (filter,
-posting-list) bitmap pairs with mixed Array/Bitmap/Run containers, generated on the device
-(SplitMix64, seed 42 + rank).  One "step" = one rbgpu_pairwise(AND) call over every pair,
-inputs already resident in HBM, results materialized in HBM (RoaringFormatSpec payloads).
+Headline (N=1): SURVEY §8d config 2 — batched pairwise AND of 1M (filter, posting-list) bitmap
+pairs with mixed Array/Bitmap/Run containers, generated on the device (SplitMix64, seed 42 + rank).
+One "step" = one rbgpu_pairwise(AND) call over every pair, inputs already resident in HBM, results
+materialized in HBM (RoaringFormatSpec payloads).
 
-Multi-GPU (torchrun, one process per GPU): pairs are independent, so each rank owns its own
-1M pairs (weak scaling, no data-path collective); barrier + max-over-ranks timing.
+Secondary lines (same JSON object, key "secondary"): config 2 at the same scale for OR / XOR /
+ANDNOT; config 1 (census1881, 4 ops); config 5 (BSI RANGE, 64 x 100M); config 3 (FastAggregation.or
+of 1024 dense bitmaps); config 4 (FastAggregation.and / .xor of 4096 run-heavy bitmaps).  Each
+carries `roofline` (its dominant kernel's algorithmic bytes / HIP-event duration on the library
+stream, against 8 TB/s, plus the PMC-measured HBM traffic of the same launch from
+profiles/<round>/traffic.json) and a `cpu_baseline` with 1-thread and all-core values.
 
-Output: one JSON line on rank 0 with `roofline` (dominant kernel k_pairwise: algorithmic bytes
-per launch / HIP-event duration on the library stream, against 8 TB/s HBM) and `cpu_baseline`
-(the oracle — C++ restatement of RoaringBitmap.and — on a bounded sample, host threads).
+Multi-GPU (torchrun, one process per GPU):
+  * pairwise (configs 2): pairs are independent, each rank owns its own 1M pairs (weak scaling);
+    per step one all_reduce of the result cardinality (ShardedPairwise's exchange);
+  * wide (configs 3, 4) and BSI (config 5): rank r owns a high-key range of the one global dataset
+    (strong scaling), per step an all_gather of the shard summaries (global cardinality and
+    serialized size: ShardedWide / ShardedBsi);
+barrier + max-over-ranks timing; value = all ranks' input bytes / that time.
 """
 from __future__ import annotations
 
@@ -28,9 +36,38 @@ sys.path.insert(0, ROOT)
 
 METRIC = "input GB/s (HBM roofline %) for batched and/or/xor + wide-OR, 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+OPS = ["AND", "OR", "XOR", "ANDNOT"]
 
 
-TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r01", "traffic.json")
+def _traffic_json():
+    for rnd in ("r02", "r01"):
+        p = os.path.join(ROOT, "profiles", rnd, "traffic.json")
+        if os.path.exists(p):
+            return p
+    return None
+
+
+TRAFFIC_JSON = _traffic_json()
+
+
+def _traffic_groups(pmc_name):
+    if TRAFFIC_JSON is None:
+        return None
+    try:
+        with open(TRAFFIC_JSON) as f:
+            return json.load(f)["kernels"].get(pmc_name) or None
+    except (OSError, ValueError, KeyError):
+        return None
+
+
+def pmc_traffic(pmc_name: str, with_count: bool = False):
+    """HBM bytes per launch of `pmc_name` from the committed rocprofv3 PMC summary of this same bench
+    command (scripts/traffic.py: FETCH_SIZE x2 for gfx950 16-B/lane reads + WRITE_SIZE, separate
+    passes); the dominant (largest) dispatch group is the headline launch.  None if not profiled."""
+    g = _traffic_groups(pmc_name)
+    if not g:
+        return None
+    return (int(g[0]["traffic_bytes"]), int(g[0]["dispatches"])) if with_count else int(g[0]["traffic_bytes"])
 
 
 def pair_traffic(op, main_name):
@@ -49,21 +86,70 @@ def pair_traffic(op, main_name):
     return x[0] if x else None
 
 
-def pmc_traffic(pmc_name: str, with_count: bool = False):
-    """HBM bytes per launch of `pmc_name` from the committed rocprofv3 PMC summary of this same bench
-    command (scripts/traffic.py: FETCH_SIZE x2 for gfx950 16-B/lane reads + WRITE_SIZE, separate
-    passes); the dominant (largest) dispatch group is the headline launch.  None if not profiled."""
+def traffic_source():
+    return os.path.relpath(TRAFFIC_JSON, ROOT) + " (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes)" \
+        if TRAFFIC_JSON else None
+
+
+# ------------------------------------------------------------------------------- host cores
+def host_cores() -> dict:
+    """CPUs this process may run on (affinity mask) and the cgroup CPU quota, beside the machine's
+    count: the all-core CPU baseline runs one thread per schedulable CPU."""
+    machine = os.cpu_count() or 1
     try:
-        with open(TRAFFIC_JSON) as f:
-            groups = json.load(f)["kernels"].get(pmc_name)
-        if not groups:
-            return None
-        return (int(groups[0]["traffic_bytes"]), int(groups[0]["dispatches"])) if with_count else \
-            int(groups[0]["traffic_bytes"])
-    except (OSError, ValueError, KeyError):
-        return None
+        sched = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        sched = machine
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, p = f.read().split()[:2]
+            if q != "max":
+                quota = float(q) / float(p)
+    except (OSError, ValueError):
+        pass
+    return {"machine_cpus": machine, "schedulable_cpus": sched, "cgroup_cpu_quota": quota}
 
 
+HOST = host_cores()
+ALL_CORES = HOST["schedulable_cpus"]
+# thread counts the all-core baselines try: every schedulable CPU, and the cgroup's CPU share when
+# it is smaller (more threads than the quota only time-share it); the best is `value`
+THREAD_COUNTS = sorted({ALL_CORES} | ({max(1, int(HOST["cgroup_cpu_quota"]))}
+                                      if HOST["cgroup_cpu_quota"] and HOST["cgroup_cpu_quota"] < ALL_CORES else set()))
+
+
+def time_loop(fn, seconds: float):
+    """Passes per second of fn, looping for at least `seconds` (at least one pass)."""
+    passes, t0 = 0, time.perf_counter()
+    while True:
+        fn()
+        passes += 1
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            return passes / el
+
+
+def multi_rate(fn_threads, seconds: float):
+    """{threads: passes/s} of fn_threads(threads) for 1 and THREAD_COUNTS, `seconds` split evenly."""
+    counts = [1] + [t for t in THREAD_COUNTS if t > 1]
+    return {t: time_loop(lambda: fn_threads(t), seconds / len(counts)) for t in counts}
+
+
+def baseline_entry(bytes_per_pass, rates: dict, kind, sample, extra=None):
+    """`value` = the best thread count's rate (the CPU at its best on this workload), with every
+    measured count beside it."""
+    best = max(rates, key=lambda t: rates[t])
+    out = {"value": round(bytes_per_pass * rates[best] / 1e9, 3), "unit": "GB/s", "cores": best, "kind": kind,
+           "value_1thread": round(bytes_per_pass * rates[1] / 1e9, 3),
+           "by_threads": {str(t): round(bytes_per_pass * r / 1e9, 3) for t, r in rates.items()},
+           "host": HOST, "sample": sample}
+    if extra:
+        out.update(extra)
+    return out
+
+
+# ------------------------------------------------------------------------------- args / dist
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
@@ -72,16 +158,17 @@ def parse():
     p.add_argument("--pairs", type=int, default=1_000_000, help="pairs per GPU (config 2)")
     p.add_argument("--workload", default="pairwise_and",
                    choices=["pairwise_and", "pairwise_or", "pairwise_xor", "pairwise_andnot", "wide_or",
-                            "wide_and_runs", "wide_xor_runs"])
+                            "wide_and_runs", "wide_xor_runs", "bsi_range"])
     p.add_argument("--wide-bitmaps", type=int, default=0, help="bitmaps of a wide workload (0: the config's)")
-    p.add_argument("--secondary", default="wide_or", choices=["none", "wide_or", "wide_and_runs", "wide_xor_runs"],
-                   help="key-range-sharded wide workload reported beside the headline (strong scaling)")
-    p.add_argument("--cpu-seconds", type=float, default=10.0)
-    p.add_argument("--census", type=int, default=1, help="also report config 1 (census1881) at N=1")
-    p.add_argument("--bsi", type=int, default=1, help="also report config 5 (BSI RANGE, 64 x 100M) at N=1")
+    p.add_argument("--secondary", default="all",
+                   help="comma list of secondary lines: pairwise_ops,census,bsi_range,wide_or,wide_and_runs,"
+                        "wide_xor_runs; 'all' or 'none'")
+    p.add_argument("--cpu-seconds", type=float, default=10.0, help="headline CPU baseline budget")
     p.add_argument("--no-cpu-baseline", action="store_true")
     return p.parse_args()
 
+
+SECONDARY_ALL = ["pairwise_ops", "census", "bsi_range", "wide_or", "wide_and_runs", "wide_xor_runs"]
 
 # Rehearsal knobs (not used by the driver): RBGPU_DIST_BACKEND=gloo keeps the collectives on the
 # host, RBGPU_SAME_DEVICE=1 puts every rank on device 0 — together they exercise the N>1 path on a
@@ -94,175 +181,144 @@ def coll_device(local: int = 0):
     return torch.device("cuda", local) if BACKEND == "nccl" else torch.device("cpu")
 
 
-def dist_setup(args):
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if os.environ.get("RBGPU_SAME_DEVICE") == "1":
-        local = 0
-    dist = None
-    if world > 1:
+class Dist:
+    def __init__(self):
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        if os.environ.get("RBGPU_SAME_DEVICE") == "1":
+            self.local = 0
+        self.td = None
+        if self.world > 1:
+            import torch
+            import torch.distributed as td
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            if BACKEND == "nccl":
+                torch.cuda.set_device(self.local)
+            td.init_process_group(BACKEND, rank=self.rank, world_size=self.world)
+            self.td = td
+
+    @property
+    def device(self):
+        return coll_device(self.local) if self.td is not None else None
+
+    def barrier(self):
+        if self.td is not None:
+            self.td.barrier()
+
+    def reduce(self, values, op="sum"):
+        if self.td is None:
+            return list(values)
         import torch
-        import torch.distributed as td
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        if BACKEND == "nccl":
-            torch.cuda.set_device(local)
-        td.init_process_group(BACKEND, rank=rank, world_size=world)
-        dist = td
-    return world, rank, local, dist
+        t = torch.tensor(list(values), dtype=torch.float64, device=self.device)
+        self.td.all_reduce(t, op=self.td.ReduceOp.MAX if op == "max" else self.td.ReduceOp.SUM)
+        return t.cpu().tolist()
+
+    def close(self):
+        if self.td is not None:
+            self.td.destroy_process_group()
 
 
-def barrier_max(dist, value: float) -> float:
-    if dist is None:
-        return value
-    import torch
-    t = torch.tensor([value], dtype=torch.float64, device=coll_device(torch.cuda.current_device()
-                                                                       if BACKEND == "nccl" else 0))
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    return float(t.item())
-
-
-def allreduce_sum(dist, value: float) -> float:
-    if dist is None:
-        return value
-    import torch
-    t = torch.tensor([value], dtype=torch.float64, device=coll_device(torch.cuda.current_device()
-                                                                       if BACKEND == "nccl" else 0))
-    dist.all_reduce(t, op=dist.ReduceOp.SUM)
-    return float(t.item())
-
-
-def barrier(dist):
-    if dist is not None:
-        dist.barrier()
-
-
-def cpu_baseline(ctx, rb, a, b, op, seconds: float):
-    """Oracle (C++ restatement of RoaringBitmap.and etc.) on a bounded sample, host threads."""
-    from oracle import rbref as R
-    n_total = len(a)
-    sample = min(n_total, 20000)
-    ra = [R.RefBitmap.deserialize(x) for x in a.serialize(0, sample)]
-    rbb = [R.RefBitmap.deserialize(x) for x in b.serialize(0, sample)]
-    # algorithmic input bytes of the sample, counted exactly like the device run
-    tmp = ctx.pairwise(op, a, b, np.arange(sample, dtype=np.uint32), np.arange(sample, dtype=np.uint32))
-    sample_bytes = ctx.stats()["input_bytes"]
-    tmp.close()
-    threads = min(16, os.cpu_count() or 1)
-    res = {}
-    for th in (1, threads):
-        passes, t0 = 0, time.perf_counter()
-        while True:
-            R.pairwise_batch(op, ra, rbb, threads=th)
-            passes += 1
-            el = time.perf_counter() - t0
-            if el >= seconds / 2:
-                break
-        res[th] = passes * sample_bytes / el / 1e9
-    return {
-        "value": round(res[threads], 3), "unit": "GB/s", "cores": threads, "kind": "port",
-        "value_1thread": round(res[1], 3),
-        "sample": f"first {sample} of the {n_total} generated pairs, looped for ~{seconds / 2:.0f}s per thread count; "
-                  f"oracle/rbref.cpp RoaringBitmap.{['and', 'or', 'xor', 'andNot'][op]} (C++ restatement, -O3)",
-    }
-
-
-WIDE_WORKLOADS = {
-    # name: (generator workload, semantics, default bitmaps, description)
-    "wide_or": ("WL_WIDE_DENSE", "FAST_OR", 1024,
-                "config3: FastAggregation.or of {n} dense bitmaps over the full 2^32 universe"),
-    "wide_and_runs": ("WL_WIDE_RUNS", "FAST_AND", 4096,
-                      "config4: FastAggregation.and (workShyAnd) of {n} run-heavy bitmaps x 65536 keys"),
-    "wide_xor_runs": ("WL_WIDE_RUNS", "FAST_XOR", 4096,
-                      "config4: FastAggregation.xor (naive_xor) of {n} run-heavy bitmaps x 65536 keys"),
-}
-
-
-def run_wide(args, name, world, rank, local, dist, ctx, rb, nbitmaps, steps, warmup):
-    """Key-range-sharded wide aggregation: rank r generates and aggregates keys [lo_r, hi_r) of the
-    one global dataset (strong scaling: total work fixed), then the RCCL exchange of the shard
-    summaries (roaringbitmap_amd.sharding).  The synthetic data is uniform over keys, so equal key
-    ranges are byte-balanced; partition_keys() does the same from rbgpu_set_key_bytes for real data."""
-    from roaringbitmap_amd.sharding import ShardedWide
-    wl, sem_name, _, desc = WIDE_WORKLOADS[name]
-    lo, hi = (65536 * rank) // world, (65536 * (rank + 1)) // world
-    a = ctx.generate_keys(getattr(rb, wl), nbitmaps, lo, hi, seed=42)
-    sem = getattr(rb, sem_name)
-    sw = ShardedWide(dist, rank, world, device=coll_device(local)) if dist is not None else None
-
-    def step():
-        if sw is None:
-            return ctx.wide(sem, a, key_range=(lo, hi)), None
-        res = sw.aggregate(ctx, sem, a, (lo, hi))
-        return res.local, res
-
-    ctx.synchronize()
+def timed(D, ctx, steps, warmup, step):
+    """W untimed steps, then K timed ones between barrier + device sync on both sides; returns
+    (max-over-ranks elapsed, per-step stats of this rank)."""
     for _ in range(warmup):
-        r, _ = step()
-        r.close()
-    kernel_ms, kernel_bytes, in_bytes, out_bytes = [], [], 0, 0
-    barrier(dist)
+        step()
     ctx.synchronize()
+    D.barrier()
+    ctx.synchronize()
+    sts = []
     t0 = time.perf_counter()
     for _ in range(steps):
-        r, res = step()
-        st = ctx.stats()
-        kernel_ms.append(st["main_kernel_ms"])
-        kernel_bytes.append(st["main_kernel_bytes"])
-        in_bytes += st["input_bytes"]
-        out_bytes += st["output_bytes"]
-        r.close()
+        sts.append(step())
     ctx.synchronize()
-    barrier(dist)
-    elapsed = barrier_max(dist, time.perf_counter() - t0)
-    total_in = allreduce_sum(dist, float(in_bytes))
-    k_ms = barrier_max(dist, float(np.mean(kernel_ms)))
-    k_bytes = float(np.mean(kernel_bytes))
-    out = {
-        "workload": desc.format(n=nbitmaps),
-        "value": round(total_in / elapsed / 1e9, 3), "unit": "GB/s", "n_gpus": world, "steps": steps,
-        "ms_per_step": round(elapsed / steps * 1e3, 4), "scaling": "strong",
-        "input_bytes_per_step": int(total_in // steps),
-        "key_range_rank0": [lo, hi],
-        "parallelism": f"key-range shards x{world}; RCCL all_gather of shard summaries (cardinality, "
-                       f"containers, Run containers, payload bytes) per step" if world > 1 else "single GPU",
-        "roofline": {"bound": "hbm", "kernel": st["main_kernel"], "traffic": pmc_traffic(
-                         "rbg::k_wide_reduce<%d>" % getattr(rb, sem_name)) if world == 1 else None,
-                     "achieved": round(k_bytes / (k_ms * 1e-3) / 1e9, 2),
-                     "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(k_bytes / (k_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                     "kernel_ms_max_over_ranks": round(k_ms, 4), "algorithmic_bytes_per_launch_rank0": int(k_bytes)},
-    }
-    if res is not None:
-        out["result_cardinality"] = res.cardinality
-        out["result_serialized_bytes"] = res.serialized_size
-    a.close()
+    D.barrier()
+    el = D.reduce([time.perf_counter() - t0], "max")[0]
+    return el, sts
+
+
+def roofline(main_name, k_ms, k_bytes, traffic, D, extra=None):
+    k_ms_max = D.reduce([k_ms], "max")[0]
+    achieved = k_bytes / (k_ms_max * 1e-3) / 1e9 if k_ms_max > 0 else 0.0
+    out = {"bound": "hbm", "kernel": main_name, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
+           "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+           "traffic": traffic if D.world == 1 else None, "traffic_source": traffic_source(),
+           "kernel_ms": round(k_ms_max, 4), "algorithmic_bytes_per_launch": int(k_bytes)}
+    if extra:
+        out.update(extra)
     return out
 
 
-def wide_cpu_baseline(ctx, rb, name, seconds: float):
-    """The oracle's FastAggregation (C++ restatement) on keys [0, 64) of the same dataset, 1 thread."""
+# ------------------------------------------------------------------------------- config 2
+def pairwise_line(D, ctx, rb, a, b, op, steps, warmup, npairs):
+    """Config 2 for one op: every rank runs its own npairs pairs (weak scaling); per step the
+    ShardedPairwise exchange (all_reduce of result cardinality / containers / bytes) at N > 1."""
+    from roaringbitmap_amd.sharding import ShardedPairwise
+    sp = ShardedPairwise(D.td, D.rank, D.world, D.device) if D.td is not None else None
+
+    def step():
+        r = ctx.pairwise(op, a, b)
+        st = ctx.stats()
+        glob = None
+        if sp is not None:
+            glob = sp.finish(None, (0, npairs), st["result_cardinality"], st["result_containers"],
+                             st["output_bytes"])
+        r.close()
+        return st, glob
+
+    el, sts = timed(D, ctx, steps, warmup, step)
+    in_b, out_b = sum(s["input_bytes"] for s, _ in sts), sum(s["output_bytes"] for s, _ in sts)
+    tot_in, tot_out = D.reduce([float(in_b), float(out_b)])
+    last, glob = sts[-1]
+    per_kernel = {}
+    for s, _ in sts:
+        for k in s["kernels"]:
+            agg = per_kernel.setdefault(k["name"], {"ms": 0.0, "bytes": 0, "items": 0})
+            agg["ms"] += k["ms"] / steps
+            agg["bytes"] += k["bytes"] // steps
+            agg["items"] += k["items"] // steps
+    k_ms = float(np.mean([s["main_kernel_ms"] for s, _ in sts]))
+    k_bytes = float(np.mean([s["main_kernel_bytes"] for s, _ in sts]))
+    card = glob.cardinality if glob is not None else int(last["result_cardinality"])
+    rl = roofline(last["main_kernel"], k_ms, k_bytes, pair_traffic(op, last["main_kernel"]), D, {
+        "kernels": {n: {"ms": round(v["ms"], 4), "bytes": v["bytes"], "items": v["items"],
+                        "GB/s": round(v["bytes"] / max(v["ms"], 1e-9) / 1e6, 1)} for n, v in per_kernel.items()}})
+    return {
+        "workload": f"config2: batched pairwise {OPS[op]} of {npairs} (filter, posting-list) pairs per GPU, "
+                    f"mixed Array/Bitmap/Run, 2^18 universe",
+        "value": round(tot_in / el / 1e9, 3), "unit": "GB/s", "n_gpus": D.world, "steps": steps,
+        "ms_per_step": round(el / steps * 1e3, 4), "scaling": "weak",
+        "input_bytes_per_step_per_gpu": in_b // steps, "output_bytes_per_step_per_gpu": out_b // steps,
+        "roofline_pct_whole_step": round(100.0 * (tot_in + tot_out) / el / 1e9 / (HBM_PEAK_GBS * D.world), 2),
+        "result_cardinality_all_ranks": card, "result_containers_rank0": int(last["result_containers"]),
+        "parallelism": (f"pair shards x{D.world}: each rank owns its own {npairs} pairs (no data-path collective); "
+                        "per step one all_reduce of (result cardinality, containers, bytes)") if D.world > 1
+        else "single GPU",
+        "roofline": rl,
+    }
+
+
+def pairwise_cpu_baseline(ctx, a, b, op, seconds: float, sample: int = 50000):
+    """Oracle (C++ restatement of RoaringBitmap.and/or/xor/andNot) on a bounded sample of the same
+    pairs: 1 thread, then one thread per schedulable host CPU (pair-parallel)."""
     from oracle import rbref as R
-    wl, sem_name, n, _ = WIDE_WORKLOADS[name]
-    a = ctx.generate_keys(getattr(rb, wl), n, 0, 64, seed=42)
-    refs = [R.RefBitmap.deserialize(x) for x in a.serialize()]
-    r = ctx.wide(getattr(rb, sem_name), a)
-    sample_bytes = ctx.stats()["input_bytes"]
-    r.close()
-    a.close()
-    sem = getattr(R, sem_name)
-    passes, t0 = 0, time.perf_counter()
-    while True:
-        R.wide(sem, refs)
-        passes += 1
-        if time.perf_counter() - t0 >= seconds:
-            break
-    el = time.perf_counter() - t0
-    return {"value": round(passes * sample_bytes / el / 1e9, 3), "unit": "GB/s", "cores": 1, "kind": "port",
-            "sample": f"keys [0, 64) of the {n} generated bitmaps ({sample_bytes} algorithmic input bytes), "
-                      f"oracle/rbref.cpp {sem_name} looped for ~{seconds:.0f}s"}
+    n_total = len(a)
+    sample = min(n_total, sample)
+    ra = [R.RefBitmap.deserialize(x) for x in a.serialize(0, sample)]
+    rbb = [R.RefBitmap.deserialize(x) for x in b.serialize(0, sample)]
+    idx = np.arange(sample, dtype=np.uint32)
+    tmp = ctx.pairwise(op, a, b, idx, idx)
+    sample_bytes = ctx.stats()["input_bytes"]  # algorithmic input bytes, counted like the device run
+    tmp.close()
+    rates = multi_rate(lambda th: R.pairwise_batch(op, ra, rbb, threads=th), seconds)
+    return baseline_entry(sample_bytes, rates, "port",
+                          f"first {sample} of the {n_total} generated pairs ({sample_bytes} algorithmic input "
+                          f"bytes), looped ~{seconds / len(rates):.1f}s per thread count; oracle/rbref.cpp "
+                          f"RoaringBitmap.{['and', 'or', 'xor', 'andNot'][op]} (C++ restatement, -O3), pairs split "
+                          "over the threads")
 
 
+# ------------------------------------------------------------------------------- config 1
 CENSUS_EXPECTED = {"AND": 23, "OR": 2007691, "XOR": 2007668, "ANDNOT": 1003836}  # RealDataBenchmark*Test.java
 
 
@@ -278,7 +334,7 @@ def load_census(name="census1881"):
     return out
 
 
-def run_census(args, ctx, rb):
+def run_census(args, ctx, rb, steps=50, warmup=5):
     """Config 1: RealDataBenchmark{And,Or,Xor,AndNot} on census1881 — 199 consecutive pairs (k, k+1)
     of the 200 bitmaps (bitmapOf), one batched call per op; a step is the four ops."""
     vals = load_census()
@@ -286,228 +342,297 @@ def run_census(args, ctx, rb):
     n = len(vals) - 1
     ai = np.arange(n, dtype=np.uint32)
     bi = ai + 1
-    ops = {"AND": rb.AND, "OR": rb.OR, "XOR": rb.XOR, "ANDNOT": rb.ANDNOT}
+    ops = {k: getattr(rb, k) for k in OPS}
     cards = {k: int(ctx.pairwise(op, s, s, ai, bi).cardinalities().sum()) for k, op in ops.items()}
-    for _ in range(args.warmup):
+    for _ in range(warmup):
         for op in ops.values():
             ctx.pairwise(op, s, s, ai, bi).close()
     ctx.synchronize()
     in_bytes = 0
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for _ in range(steps):
         for op in ops.values():
             ctx.pairwise(op, s, s, ai, bi).close()
             in_bytes += ctx.stats()["input_bytes"]
     ctx.synchronize()
     el = time.perf_counter() - t0
     out = {"workload": "config1: census1881 RealDataBenchmark and/or/xor/andNot, 199 consecutive pairs per op",
-           "value": round(in_bytes / el / 1e9, 3), "unit": "GB/s", "ms_per_step": round(el / args.steps * 1e3, 4),
-           "us_per_op_sweep": round(el / args.steps / 4 * 1e6, 1), "cardinality_sums": cards,
+           "value": round(in_bytes / el / 1e9, 3), "unit": "GB/s", "steps": steps,
+           "ms_per_step": round(el / steps * 1e3, 4),
+           "us_per_op_sweep": round(el / steps / 4 * 1e6, 1), "cardinality_sums": cards,
            "golden_ok": cards == CENSUS_EXPECTED}
     if not args.no_cpu_baseline:
         from oracle import rbref as R
         refs = [R.RefBitmap.deserialize(x) for x in s.serialize()]
         a_r, b_r = refs[:-1], refs[1:]
-        passes, t0 = 0, time.perf_counter()
-        while time.perf_counter() - t0 < 2.0:
+
+        def sweep(th):
             for op in ops.values():
-                R.pairwise_batch(op, a_r, b_r, threads=1)
-            passes += 1
-        el = time.perf_counter() - t0
-        out["cpu_baseline"] = {"value": round(passes * in_bytes / args.steps / el / 1e9, 3), "unit": "GB/s",
-                               "cores": 1, "kind": "port", "us_per_op_sweep": round(el / passes / 4 * 1e6, 1),
-                               "sample": "the whole config (199 pairs x 4 ops), oracle/rbref.cpp, 1 thread"}
+                R.pairwise_batch(op, a_r, b_r, threads=th)
+        rates = multi_rate(sweep, 3.0)
+        out["cpu_baseline"] = baseline_entry(in_bytes / steps, rates, "port",
+                                             "the whole config (199 pairs x 4 ops), oracle/rbref.cpp",
+                                             {"us_per_op_sweep_1thread": round(1e6 / rates[1] / 4, 1),
+                                              "us_per_op_sweep_best": round(1e6 / max(rates.values()) / 4, 1)})
     s.close()
     return out
 
 
-def run_bsi(args, ctx, rb, nslices=64, nrows=100_000_000, steps=5, warmup=2):
+# ------------------------------------------------------------------------------- config 5
+BSI_NSLICES, BSI_NROWS = 64, 100_000_000
+BSI_LO, BSI_HI = 0x3A00_0000_0000_0000, 0xB100_0000_0000_0000  # a mid-range window: no min/max shortcut
+
+
+def run_bsi(args, D, ctx, rb, steps=5, warmup=2):
     """Config 5: Roaring64BitmapSliceIndex.compare(RANGE, lo, hi, null) over 64 slices x 100M rows
-    (runOptimize'd BSI, random value bits) — one fused pass per high key for each O'Neil chain."""
-    d = ctx.generate_bsi(nslices, nrows, seed=42)
-    lo, hi = 0x3A00_0000_0000_0000, 0xB100_0000_0000_0000  # a mid-range window: no min/max shortcut
-    vmin, vmax = 0, (1 << nslices) - 1
-    for _ in range(warmup):
-        ctx.bsi_compare(rb.BSI_RANGE, d, lo, hi, vmin, vmax).close()
-    ctx.synchronize()
-    in_bytes, k_ms, k_bytes = 0, [], []
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        r = ctx.bsi_compare(rb.BSI_RANGE, d, lo, hi, vmin, vmax)
+    (runOptimize'd BSI, random value bits) — one fused pass per high key for both O'Neil chains.
+    At N > 1 rank r holds and answers its high-key range (ShardedBsi; strong scaling)."""
+    from roaringbitmap_amd.sharding import ShardedBsi
+    nkeys = (BSI_NROWS + 65535) // 65536
+    lo_k, hi_k = (nkeys * D.rank) // D.world, (nkeys * (D.rank + 1)) // D.world
+    if D.rank == D.world - 1:
+        hi_k = 65536
+    kr = (lo_k, hi_k)
+    d = ctx.generate_bsi(BSI_NSLICES, BSI_NROWS, seed=42, key_range=kr if D.world > 1 else None)
+    vmin, vmax = 0, (1 << BSI_NSLICES) - 1
+    sb = ShardedBsi(D.td, D.rank, D.world, D.device) if D.td is not None else None
+
+    def step():
+        r = ctx.bsi_compare(rb.BSI_RANGE, d, BSI_LO, BSI_HI, vmin, vmax, key_range=kr)
         st = ctx.stats()
-        in_bytes += st["input_bytes"]
-        k_ms.append(st["main_kernel_ms"])
-        k_bytes.append(st["main_kernel_bytes"])
-        card = None
-        if _ == steps - 1:
-            card = int(r.cardinalities()[0])
+        card = sb.finish(r, kr, r.summaries()[0]).cardinality if sb is not None else None
         r.close()
-    ctx.synchronize()
-    el = time.perf_counter() - t0
-    km, kb = float(np.mean(k_ms)), float(np.mean(k_bytes))
-    out = {"workload": f"config5: BSI compare RANGE over {nslices} slices x {nrows} rows (2 O'Neil chains + AND, "
-                       "fused into one pass per key)",
-           "value": round(in_bytes / el / 1e9, 3), "unit": "GB/s", "ms_per_step": round(el / steps * 1e3, 4),
-           "result_cardinality": card,
-           "roofline": {"bound": "hbm", "kernel": st["main_kernel"],
-                        "traffic": pmc_traffic("rbg::k_bsi_range"),
-                        "note": "the fused kernel reads every slice container once for both comparators "
-                                "(GE and LE); algorithmic bytes count that one read",
-                        "achieved": round(kb / (km * 1e-3) / 1e9, 2),
-                        "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(kb / (km * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                        "kernel_ms": round(km, 4), "algorithmic_bytes_per_launch": int(kb)}}
-    if not args.no_cpu_baseline:
-        from oracle import rbref as R
-        small = ctx.generate_bsi(nslices, 4 * 65536, seed=42)  # the first 4 keys of the same shape
-        refs = [R.RefBitmap.deserialize(x) for x in small.serialize()]
-        r = ctx.bsi_compare(rb.BSI_RANGE, small, lo, hi, vmin, vmax)
-        sb = ctx.stats()["input_bytes"]
-        r.close()
-        small.close()
-        passes, t0 = 0, time.perf_counter()
-        while time.perf_counter() - t0 < 3.0:
-            R.bsi_compare(refs[:-1], refs[-1], R.BSI_RANGE, lo, hi, None, vmin, vmax)
-            passes += 1
-        el = time.perf_counter() - t0
-        out["cpu_baseline"] = {"value": round(passes * sb / el / 1e9, 3), "unit": "GB/s", "cores": 1, "kind": "port",
-                               "sample": f"the same query on 4 x 65536 rows ({sb} algorithmic input bytes), "
-                                         "oracle/rbref.py BSI restatement over rbref.cpp static ops, 1 thread"}
+        return st, card
+
+    el, sts = timed(D, ctx, steps, warmup, step)
+    in_b = sum(s["input_bytes"] for s, _ in sts)
+    tot_in = D.reduce([float(in_b)])[0]
+    last = sts[-1][0]
+    km = float(np.mean([s["main_kernel_ms"] for s, _ in sts]))
+    kb = float(np.mean([s["main_kernel_bytes"] for s, _ in sts]))
+    card = sts[-1][1] if sb is not None else int(last["result_cardinality"])
+    ts = d.type_stats()
+    out = {"workload": f"config5: BSI compare RANGE over {BSI_NSLICES} slices x {BSI_NROWS} rows (2 O'Neil chains "
+                       "+ AND, fused into one pass per key)",
+           "value": round(tot_in / el / 1e9, 3), "unit": "GB/s", "n_gpus": D.world, "steps": steps,
+           "ms_per_step": round(el / steps * 1e3, 4), "scaling": "strong",
+           "result_cardinality": card, "containers_rank0": ts,
+           "parallelism": (f"high-key range shards x{D.world} (rbgpu_bsi_compare_keys), per step all_gather of "
+                           "shard summaries") if D.world > 1 else "single GPU",
+           "key_range_rank0": list(kr),
+           "roofline": roofline(last["main_kernel"], km, kb, pmc_traffic("rbg::k_bsi_range"), D, {
+               "note": "the fused kernel reads every slice container once for both comparators (GE and LE); "
+                       "algorithmic bytes count that one read"})}
     d.close()
+    if not args.no_cpu_baseline and D.world == 1:
+        out["cpu_baseline"] = bsi_cpu_baseline(ctx, rb)
     return out
 
 
+def bsi_cpu_baseline(ctx, rb, seconds=4.0):
+    """The oracle's compare (rbref.py O'Neil restatement over rbref.cpp static ops) on the first
+    high keys of the same index (2 per host CPU, at least 64): 1 thread, then key-parallel over all
+    host CPUs (a pool of per-key compares, the split BitSliceIndexBase.java:99-166 uses; the C ops
+    release the GIL)."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    from oracle import rbref as R
+    nkeys = min(max(64, 2 * ALL_CORES), (BSI_NROWS + 65535) // 65536)
+    vmin, vmax = 0, (1 << BSI_NSLICES) - 1
+    per_key = []
+    for k in range(nkeys):
+        s = ctx.generate_bsi(BSI_NSLICES, BSI_NROWS, seed=42, key_range=(k, k + 1))
+        refs = [R.RefBitmap.deserialize(x) for x in s.serialize()]
+        s.close()
+        per_key.append((refs[:-1], refs[-1]))
+    s = ctx.generate_bsi(BSI_NSLICES, BSI_NROWS, seed=42, key_range=(0, nkeys))
+    ctx.bsi_compare(rb.BSI_RANGE, s, BSI_LO, BSI_HI, vmin, vmax).close()
+    sb = ctx.stats()["input_bytes"]
+    s.close()
+    run_key = lambda sl_eb: R.bsi_compare(sl_eb[0], sl_eb[1], R.BSI_RANGE, BSI_LO, BSI_HI, None, vmin, vmax)  # noqa
+
+    def one():
+        for x in per_key:
+            run_key(x)
+    def pool(th):
+        if th == 1:
+            return one()
+        with ThreadPoolExecutor(min(th, nkeys)) as ex:
+            list(ex.map(run_key, per_key))
+    rates = multi_rate(pool, seconds)
+    return baseline_entry(sb, rates, "port",
+                          f"the same query on the first {nkeys} high keys ({nkeys} x 65536 rows, {sb} algorithmic "
+                          "input bytes); oracle/rbref.py BSI restatement over rbref.cpp static ops")
+
+
+# ------------------------------------------------------------------------------- configs 3 / 4
+WIDE_WORKLOADS = {
+    # name: (generator workload, semantics, default bitmaps, PMC kernel, CPU sample keys, description)
+    "wide_or": ("WL_WIDE_DENSE", "FAST_OR", 1024, "rbg::k_wide_reduce<0>", 1024,
+                "config3: FastAggregation.or of {n} dense bitmaps over the full 2^32 universe"),
+    "wide_and_runs": ("WL_WIDE_RUNS", "FAST_AND", 4096, "rbg::k_wide_runs_and", 256,
+                      "config4: FastAggregation.and (workShyAnd) of {n} run-heavy bitmaps x 65536 keys"),
+    "wide_xor_runs": ("WL_WIDE_RUNS", "FAST_XOR", 4096, "rbg::k_wide_runs_xor", 256,
+                      "config4: FastAggregation.xor (naive_xor) of {n} run-heavy bitmaps x 65536 keys"),
+}
+# the all-core CPU baseline of each wide semantic: ParallelAggregation where the reference has one,
+# else the same per-key semantic key-parallel (oracle rbref_wide_mt)
+WIDE_PARALLEL = {"FAST_OR": "PAR_OR", "FAST_XOR": "PAR_XOR", "FAST_AND": "FAST_AND"}
+
+
+def run_wide(args, name, D, ctx, rb, nbitmaps, steps, warmup, a=None):
+    """Key-range-sharded wide aggregation: rank r generates and aggregates keys [lo_r, hi_r) of the
+    one global dataset (strong scaling: total work fixed), then the RCCL exchange of the shard
+    summaries (roaringbitmap_amd.sharding).  The synthetic data is uniform over keys, so equal key
+    ranges are byte-balanced; partition_keys() does the same from rbgpu_set_key_bytes for real data."""
+    from roaringbitmap_amd.sharding import ShardedWide
+    wl, sem_name, _, pmc_name, _, desc = WIDE_WORKLOADS[name]
+    lo, hi = (65536 * D.rank) // D.world, (65536 * (D.rank + 1)) // D.world
+    own = a is None
+    if own:
+        a = ctx.generate_keys(getattr(rb, wl), nbitmaps, lo, hi, seed=42)
+    sem = getattr(rb, sem_name)
+    sw = ShardedWide(D.td, D.rank, D.world, device=D.device) if D.td is not None else None
+
+    def step():
+        if sw is None:
+            r = ctx.wide(sem, a, key_range=(lo, hi))
+            st, res = ctx.stats(), None
+        else:
+            res = sw.aggregate(ctx, sem, a, (lo, hi))
+            r = res.local
+            st = ctx.stats()
+        r.close()
+        return st, res
+
+    el, sts = timed(D, ctx, steps, warmup, step)
+    in_b = sum(s["input_bytes"] for s, _ in sts)
+    total_in = D.reduce([float(in_b)])[0]
+    last, res = sts[-1]
+    k_ms = float(np.mean([s["main_kernel_ms"] for s, _ in sts]))
+    k_bytes = float(np.mean([s["main_kernel_bytes"] for s, _ in sts]))
+    out = {
+        "workload": desc.format(n=nbitmaps),
+        "value": round(total_in / el / 1e9, 3), "unit": "GB/s", "n_gpus": D.world, "steps": steps,
+        "ms_per_step": round(el / steps * 1e3, 4), "scaling": "strong",
+        "input_bytes_per_step": int(total_in // steps),
+        "key_range_rank0": [lo, hi],
+        "containers_rank0": a.type_stats(),
+        "parallelism": f"key-range shards x{D.world}; RCCL all_gather of shard summaries (cardinality, "
+                       f"containers, Run containers, payload bytes) per step" if D.world > 1 else "single GPU",
+        "roofline": roofline(last["main_kernel"], k_ms, k_bytes, pmc_traffic(pmc_name), D),
+    }
+    out["result_cardinality"] = res.cardinality if res is not None else int(last["result_cardinality"])
+    if res is not None:
+        out["result_serialized_bytes"] = res.serialized_size
+    if own:
+        a.close()
+    return out
+
+
+def wide_cpu_baseline(ctx, rb, name, seconds: float):
+    """The oracle's FastAggregation (C++ restatement) on the first K high keys of the same dataset:
+    1 thread with the FastAggregation semantic, then all host CPUs with ParallelAggregation's
+    key-parallel restatement (ParallelAggregation.java:161-223; rbref_wide_mt)."""
+    from oracle import rbref as R
+    wl, sem_name, n, _, nkeys, _ = WIDE_WORKLOADS[name]
+    a = ctx.generate_keys(getattr(rb, wl), n, 0, nkeys, seed=42)
+    refs = [R.RefBitmap.deserialize(x) for x in a.serialize()]
+    r = ctx.wide(getattr(rb, sem_name), a)
+    sample_bytes = ctx.stats()["input_bytes"]
+    r.close()
+    a.close()
+    sem, par = getattr(R, sem_name), getattr(R, WIDE_PARALLEL[sem_name])
+    rates = multi_rate(lambda th: R.wide(sem, refs) if th == 1 else R.wide_mt(par, refs, th), seconds)
+    return baseline_entry(sample_bytes, rates, "port",
+                          f"keys [0, {nkeys}) of the {n} generated bitmaps ({sample_bytes} algorithmic input bytes); "
+                          f"1 thread: oracle/rbref.cpp {sem_name}; more threads: {WIDE_PARALLEL[sem_name]} "
+                          f"key-parallel restatement (rbref_wide_mt); ~{seconds / len(rates):.1f}s each")
+
+
+# ------------------------------------------------------------------------------- main
 def main():
     args = parse()
-    world, rank, local, dist = dist_setup(args)
+    D = Dist()
     import roaringbitmap_amd as rb
-    ctx = rb.Context(local)
-    seed = 42 + rank
+    ctx = rb.Context(D.local)
+    seed = 42 + D.rank
+    sec = SECONDARY_ALL if args.secondary == "all" else \
+        ([] if args.secondary == "none" else [s for s in args.secondary.split(",") if s])
+    line = {"metric": METRIC, "higher_is_better": True, "vs_baseline": None, "dtype": "u64",
+            "n_gpus": D.world, "steps": args.steps, "warmup": args.warmup,
+            "data": "synthetic (device SplitMix64 generator, runOptimize'd containers; SURVEY §8d)"}
+    secondary = {}
 
-    if args.workload in WIDE_WORKLOADS:
-        nb = args.wide_bitmaps or WIDE_WORKLOADS[args.workload][2]
-        w = run_wide(args, args.workload, world, rank, local, dist, ctx, rb, nb, args.steps, args.warmup)
-        if rank == 0:
-            line = {"metric": METRIC, "value": w["value"], "unit": "GB/s", "n_gpus": world, "steps": args.steps,
-                    "warmup": args.warmup, "ms_per_step": w["ms_per_step"], "higher_is_better": True,
-                    "scaling": "strong", "vs_baseline": None, "dtype": "u64",
-                    "data": "synthetic (device SplitMix64 generator keyed by (bitmap, key); SURVEY §8d)",
-                    "config": {k: v for k, v in w.items() if k not in ("value", "roofline", "ms_per_step")},
-                    "roofline": w["roofline"]}
-            if world == 1 and not args.no_cpu_baseline:
-                line["cpu_baseline"] = wide_cpu_baseline(ctx, rb, args.workload, args.cpu_seconds / 2)
+    if args.workload in WIDE_WORKLOADS or args.workload == "bsi_range":
+        if args.workload == "bsi_range":
+            w = run_bsi(args, D, ctx, rb, args.steps, args.warmup)
+        else:
+            nb = args.wide_bitmaps or WIDE_WORKLOADS[args.workload][2]
+            w = run_wide(args, args.workload, D, ctx, rb, nb, args.steps, args.warmup)
+            if D.world == 1 and not args.no_cpu_baseline:
+                w["cpu_baseline"] = wide_cpu_baseline(ctx, rb, args.workload, args.cpu_seconds / 2)
+        line.update({"value": w["value"], "unit": "GB/s", "ms_per_step": w["ms_per_step"], "scaling": "strong",
+                     "config": {k: v for k, v in w.items() if k not in ("value", "roofline", "ms_per_step",
+                                                                        "cpu_baseline", "unit", "steps", "n_gpus")},
+                     "roofline": w["roofline"]})
+        if "cpu_baseline" in w:
+            line["cpu_baseline"] = w["cpu_baseline"]
+        if D.rank == 0:
             print(json.dumps(line), flush=True)
-        if dist is not None:
-            dist.destroy_process_group()
+        D.close()
         return
 
     op = {"pairwise_and": rb.AND, "pairwise_or": rb.OR, "pairwise_xor": rb.XOR, "pairwise_andnot": rb.ANDNOT}[
         args.workload]
     a, b = ctx.generate(rb.WL_FILTER_POSTING, args.pairs, seed=seed)
-    run = lambda: ctx.pairwise(op, a, b)  # noqa: E731
-    workload = (f"config2: batched pairwise {['AND', 'OR', 'XOR', 'ANDNOT'][op]} of {args.pairs} "
-                f"(filter, posting-list) pairs per GPU, mixed Array/Bitmap/Run, 2^18 universe")
-    units = args.pairs
-    unit_name = "pairs"
     ctx.synchronize()
+    h = pairwise_line(D, ctx, rb, a, b, op, args.steps, args.warmup, args.pairs)
+    line.update({"value": h["value"], "unit": "GB/s", "ms_per_step": h["ms_per_step"], "scaling": "weak",
+                 "config": {"workload": h["workload"], "units_per_gpu": args.pairs, "unit": "pairs",
+                            "input_bytes_per_step_per_gpu": h["input_bytes_per_step_per_gpu"],
+                            "output_bytes_per_step_per_gpu": h["output_bytes_per_step_per_gpu"],
+                            "roofline_pct_whole_step": h["roofline_pct_whole_step"],
+                            "result_cardinality_all_ranks": h["result_cardinality_all_ranks"],
+                            "containers_a_rank0": a.type_stats(), "containers_b_rank0": b.type_stats(),
+                            "parallelism": h["parallelism"]},
+                 "roofline": h["roofline"]})
+    if D.world == 1 and not args.no_cpu_baseline:
+        line["cpu_baseline"] = pairwise_cpu_baseline(ctx, a, b, op, args.cpu_seconds)
+    if "pairwise_ops" in sec:
+        for o in range(4):
+            if o == op:
+                continue
+            w = pairwise_line(D, ctx, rb, a, b, o, max(3, args.steps // 2), 1, args.pairs)
+            if D.world == 1 and not args.no_cpu_baseline:
+                w["cpu_baseline"] = pairwise_cpu_baseline(ctx, a, b, o, 4.0, sample=20000)
+            secondary["pairwise_" + OPS[o].lower()] = w
+    a.close()
+    b.close()
+    if "census" in sec and D.world == 1:
+        secondary["census1881"] = run_census(args, ctx, rb)
+    if "bsi_range" in sec:
+        secondary["bsi_range"] = run_bsi(args, D, ctx, rb)
+    def wide_secondary(name, data=None):
+        w = run_wide(args, name, D, ctx, rb, WIDE_WORKLOADS[name][2], 3, 1, a=data)
+        if D.world == 1 and not args.no_cpu_baseline:
+            w["cpu_baseline"] = wide_cpu_baseline(ctx, rb, name, 4.0)
+        secondary[name] = w
 
-    for _ in range(args.warmup):
-        r = run()
-        r.close()
-    ctx.synchronize()
-
-    kernel_ms, kernel_bytes, in_bytes, out_bytes = [], [], 0, 0
-    per_kernel = {}
-    barrier(dist)
-    ctx.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        r = run()
-        st = ctx.stats()
-        kernel_ms.append(st["main_kernel_ms"])
-        kernel_bytes.append(st["main_kernel_bytes"])
-        for k in st["kernels"]:
-            agg = per_kernel.setdefault(k["name"], {"ms": 0.0, "bytes": 0, "items": 0})
-            agg["ms"] += k["ms"] / args.steps
-            agg["bytes"] += k["bytes"] // args.steps
-            agg["items"] += k["items"] // args.steps
-        in_bytes += st["input_bytes"]
-        out_bytes += st["output_bytes"]
-        r.close()
-    ctx.synchronize()
-    barrier(dist)
-    elapsed = time.perf_counter() - t0
-    elapsed = barrier_max(dist, elapsed)
-    total_in = allreduce_sum(dist, float(in_bytes))
-    total_out = allreduce_sum(dist, float(out_bytes))  # every rank joins every collective
-    main_name = st["main_kernel"]
-
-    if rank == 0:
-        ms_per_step = elapsed / args.steps * 1e3
-        value = total_in / elapsed / 1e9
-        per_launch = float(np.mean(kernel_bytes))
-        k_ms = float(np.mean(kernel_ms))
-        achieved = per_launch / (k_ms * 1e-3) / 1e9
-        line = {
-            "metric": METRIC,
-            "value": round(value, 3),
-            "unit": "GB/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(ms_per_step, 4),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "u64",
-            "data": "synthetic (device SplitMix64 generator, runOptimize'd containers; SURVEY §8d)",
-            "config": {
-                "workload": workload,
-                "units_per_gpu": units,
-                "unit": unit_name,
-                "input_bytes_per_step_per_gpu": in_bytes // args.steps,
-                "output_bytes_per_step_per_gpu": out_bytes // args.steps,
-                "roofline_pct_whole_step": round(100.0 * (total_in + total_out) / elapsed / 1e9 / (HBM_PEAK_GBS * world),
-                                                 2),
-                "parallelism": f"key-range/pair sharding x{world} (replicas, no data-path collective)",
-            },
-            "roofline": {
-                "bound": "hbm",
-                "kernel": main_name,
-                "achieved": round(achieved, 2),
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": pair_traffic(op, main_name),
-                "traffic_source": "profiles/r01/traffic.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes)",
-                "kernel_ms": round(k_ms, 4),
-                "algorithmic_bytes_per_launch": int(per_launch),
-                "kernels": {n: {"ms": round(v["ms"], 4), "bytes": v["bytes"], "items": v["items"],
-                                "GB/s": round(v["bytes"] / max(v["ms"], 1e-9) / 1e6, 1)}
-                            for n, v in per_kernel.items()},
-            },
-        }
-        if world == 1 and not args.no_cpu_baseline:
-            line["cpu_baseline"] = cpu_baseline(ctx, rb, a, b, op, args.cpu_seconds)
-    if args.secondary != "none" or (world == 1 and (args.census or args.bsi)):
-        a.close()
-        b.close()
-    if world == 1 and args.census:
-        c1 = run_census(args, ctx, rb)
-        if rank == 0:
-            line.setdefault("secondary", {})["census1881"] = c1
-    if world == 1 and args.bsi:
-        line.setdefault("secondary", {})["bsi_range"] = run_bsi(args, ctx, rb)
-    if args.secondary != "none":
-        w = run_wide(args, args.secondary, world, rank, local, dist, ctx, rb,
-                     WIDE_WORKLOADS[args.secondary][2], max(3, args.steps // 3), 1)
-        if rank == 0:
-            if world == 1 and not args.no_cpu_baseline:
-                w["cpu_baseline"] = wide_cpu_baseline(ctx, rb, args.secondary, args.cpu_seconds / 2)
-            line.setdefault("secondary", {})[args.secondary] = w
-    if rank == 0:
+    if "wide_or" in sec:
+        wide_secondary("wide_or")
+    c4 = [n for n in ("wide_and_runs", "wide_xor_runs") if n in sec]
+    if c4:  # config 4 AND and XOR read the same dataset: generate this rank's key range once
+        lo, hi = (65536 * D.rank) // D.world, (65536 * (D.rank + 1)) // D.world
+        data = ctx.generate_keys(rb.WL_WIDE_RUNS, WIDE_WORKLOADS["wide_and_runs"][2], lo, hi, seed=42)
+        for name in c4:
+            wide_secondary(name, data)
+        data.close()
+    if secondary:
+        line["secondary"] = secondary
+    if D.rank == 0:
         print(json.dumps(line), flush=True)
-    if dist is not None:
-        dist.destroy_process_group()
+    D.close()
 
 
 if __name__ == "__main__":

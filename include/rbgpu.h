@@ -190,6 +190,14 @@ enum rb_bsi_op { RB_BSI_EQ = 0, RB_BSI_NEQ = 1, RB_BSI_LE = 2, RB_BSI_LT = 3, RB
  * one-bitmap set, byte-identical to the reference's Roaring(64)Bitmap containers. */
 int rbgpu_bsi_compare(rbgpu_ctx *ctx, const rbgpu_set *bsi, int op, uint64_t start_or_value, uint64_t end,
                       uint64_t min_value, uint64_t max_value, const rbgpu_set *found, rbgpu_set **out);
+/* The high keys [key_lo, key_hi) of rbgpu_bsi_compare's answer: a rank that owns that key range of
+ * the index (rbgpu_generate_bsi_keys, or any bsi set whose other keys it ignores) computes exactly
+ * those containers of the result.  The compare is key-local (each 2^16-row chunk is independent),
+ * so the disjoint shards of a partition concatenate, in key order, to the whole answer
+ * (key-range sharding, no data-path collective). */
+int rbgpu_bsi_compare_keys(rbgpu_ctx *ctx, const rbgpu_set *bsi, int op, uint64_t start_or_value, uint64_t end,
+                           uint64_t min_value, uint64_t max_value, const rbgpu_set *found, uint32_t key_lo,
+                           uint32_t key_hi, rbgpu_set **out);
 /* RoaringBitmap.clone of bitmaps [first, first+count) into a new set (device copy). */
 int rbgpu_set_extract(const rbgpu_set *set, uint32_t first, uint32_t count, rbgpu_set **out);
 
@@ -209,6 +217,9 @@ int rbgpu_generate_keys(rbgpu_ctx *ctx, int workload, uint32_t n, uint64_t seed,
 /* a runOptimize'd BSI over rows [0, nrows) with nslices random value bits per
  * row (every slice container Bernoulli(1/2)), i.e. nslices + 1 bitmaps (slices, then ebM). */
 int rbgpu_generate_bsi(rbgpu_ctx *ctx, uint32_t nslices, uint64_t nrows, uint64_t seed, rbgpu_set **out);
+/* The containers of rbgpu_generate_bsi's index with high keys in [key_lo, key_hi) (a rank's shard). */
+int rbgpu_generate_bsi_keys(rbgpu_ctx *ctx, uint32_t nslices, uint64_t nrows, uint64_t seed, uint32_t key_lo,
+                            uint32_t key_hi, rbgpu_set **out);
 /* Generates a (and b for RB_WL_FILTER_POSTING; *b may be NULL otherwise).  n = pairs or
  * bitmaps.  Every container goes through runOptimize semantics, as
  * RoaringBitmapWriter(runCompress=true) does (ContainerAppender.java:130-137). */

@@ -91,6 +91,10 @@ SIGNATURES = {
     "rbgpu_set_summaries": (C.c_int, [_P, C.c_uint32, C.c_uint32, C.POINTER(RbBitmapSummary)]),
     "rbgpu_bsi_compare": (C.c_int, [_P, _P, C.c_int, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64, _P,
                                     C.POINTER(_P)]),
+    "rbgpu_bsi_compare_keys": (C.c_int, [_P, _P, C.c_int, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64, _P,
+                                         C.c_uint32, C.c_uint32, C.POINTER(_P)]),
+    "rbgpu_generate_bsi_keys": (C.c_int, [_P, C.c_uint32, C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint32,
+                                          C.POINTER(_P)]),
     "rbgpu_set_extract": (C.c_int, [_P, C.c_uint32, C.c_uint32, C.POINTER(_P)]),
     "rbgpu_generate_bsi": (C.c_int, [_P, C.c_uint32, C.c_uint64, C.c_uint64, C.POINTER(_P)]),
     "rbgpu_generate_keys": (C.c_int, [_P, C.c_int, C.c_uint32, C.c_uint64, C.c_uint32, C.c_uint32, C.POINTER(_P)]),

@@ -227,6 +227,29 @@ int check_ctx(rbgpu_ctx *ctx) {
 } // namespace
 
 namespace rbg {
+// Only the min/max shortcut answers of a key-range BSI shard come here (a copy of ebM or foundSet,
+// restricted); the containers stay bytes-identical.
+int set_key_subset(const rbgpu_set *s, uint32_t key_lo, uint32_t key_hi, rbgpu_set **out) {
+  HostSoA h;
+  int rc = download_host(s, 0, 1, h);
+  if (rc) return rc;
+  HostSoA r;
+  r.nb = 1;
+  r.begin.assign(2, 0);
+  for (uint64_t i = 0; i < h.nc(); ++i) {
+    if (h.key[i] < key_lo || h.key[i] >= key_hi) continue;
+    const uint64_t bytes = payload_bytes(h.type[i], h.card[i], h.nruns[i]);
+    r.key.push_back(h.key[i]);
+    r.type.push_back(h.type[i]);
+    r.card.push_back(h.card[i]);
+    r.nruns.push_back(h.nruns[i]);
+    r.off.push_back(r.payload.size());
+    r.payload.insert(r.payload.end(), h.payload.begin() + h.off[i], h.payload.begin() + h.off[i] + round16(bytes));
+  }
+  r.begin[1] = r.key.size();
+  return upload_host(s->ctx, r, out);
+}
+
 void stats_begin(rbgpu_ctx *ctx) {
   (void)hipMemsetAsync(ctx->d_stats, 0, kStatWords * kStripes * sizeof(uint64_t), ctx->stream);
   (void)hipEventRecord(ctx->ev[0], ctx->stream);
@@ -917,8 +940,9 @@ int rbgpu_wide_cardinality(rbgpu_ctx *ctx, int op, const rbgpu_set *in, const ui
 }
 
 // ---------------------------------------------------------------- bit-sliced index
-int rbgpu_bsi_compare(rbgpu_ctx *ctx, const rbgpu_set *bsi, int op, uint64_t start_or_value, uint64_t end,
-                      uint64_t min_value, uint64_t max_value, const rbgpu_set *found, rbgpu_set **out) {
+int rbgpu_bsi_compare_keys(rbgpu_ctx *ctx, const rbgpu_set *bsi, int op, uint64_t start_or_value, uint64_t end,
+                           uint64_t min_value, uint64_t max_value, const rbgpu_set *found, uint32_t key_lo,
+                           uint32_t key_hi, rbgpu_set **out) {
   if (!out) return fail(RB_EINVAL, "null out");
   *out = nullptr;
   int rc = check_ctx(ctx);
@@ -927,9 +951,15 @@ int rbgpu_bsi_compare(rbgpu_ctx *ctx, const rbgpu_set *bsi, int op, uint64_t sta
   if (bsi->nb < 1 || bsi->nb > 65) return fail(RB_EINVAL, "a bsi set holds 0..64 slices and the existence bitmap");
   if (found && (found->ctx != ctx || found->nb != 1)) return fail(RB_EINVAL, "foundSet must be a one-bitmap set");
   if (op < RB_BSI_EQ || op > RB_BSI_RANGE) return fail(RB_EINVAL, "not support operation!");
+  if (key_lo > key_hi || key_hi > 65536) return fail(RB_EINVAL, "bad key range [%u, %u)", key_lo, key_hi);
   rc = ensure_h_begin(bsi);
   if (rc) return rc;
-  return bsi_compare(ctx, bsi, op, start_or_value, end, min_value, max_value, found, out);
+  return bsi_compare(ctx, bsi, op, start_or_value, end, min_value, max_value, found, key_lo, key_hi, out);
+}
+
+int rbgpu_bsi_compare(rbgpu_ctx *ctx, const rbgpu_set *bsi, int op, uint64_t start_or_value, uint64_t end,
+                      uint64_t min_value, uint64_t max_value, const rbgpu_set *found, rbgpu_set **out) {
+  return rbgpu_bsi_compare_keys(ctx, bsi, op, start_or_value, end, min_value, max_value, found, 0, 65536, out);
 }
 
 int rbgpu_set_extract(const rbgpu_set *s, uint32_t first, uint32_t count, rbgpu_set **out) {
@@ -947,7 +977,16 @@ int rbgpu_generate_bsi(rbgpu_ctx *ctx, uint32_t nslices, uint64_t nrows, uint64_
   if (rc) return rc;
   if (!out) return fail(RB_EINVAL, "null out");
   *out = nullptr;
-  return generate_bsi(ctx, nslices, nrows, seed, out);
+  return generate_bsi(ctx, nslices, nrows, seed, 0, 65536, out);
+}
+
+int rbgpu_generate_bsi_keys(rbgpu_ctx *ctx, uint32_t nslices, uint64_t nrows, uint64_t seed, uint32_t key_lo,
+                            uint32_t key_hi, rbgpu_set **out) {
+  int rc = check_ctx(ctx);
+  if (rc) return rc;
+  if (!out) return fail(RB_EINVAL, "null out");
+  *out = nullptr;
+  return generate_bsi(ctx, nslices, nrows, seed, key_lo, key_hi, out);
 }
 
 // ---------------------------------------------------------------- generator

@@ -30,9 +30,11 @@ __global__ __launch_bounds__(256) void k_bsi_index(SetView s, uint32_t first, in
   for (uint64_t c = lo + (uint64_t)blockIdx.x * 256 + threadIdx.x; c < hi; c += (uint64_t)gridDim.x * 256)
     table[(uint64_t)row * 65536 + s.key[c]] = (int32_t)c;
 }
-__global__ __launch_bounds__(256) void k_bsi_active(const int32_t *frow, uint64_t *active) {
+// keys of F (ebM or foundSet) inside the shard's [key_lo, key_hi)
+__global__ __launch_bounds__(256) void k_bsi_active(const int32_t *frow, uint32_t key_lo, uint32_t key_hi,
+                                                    uint64_t *active) {
   const uint32_t k = blockIdx.x * 256 + threadIdx.x;
-  if (k < 65536) active[k] = frow[k] >= 0;
+  if (k < 65536) active[k] = frow[k] >= 0 && k >= key_lo && k < key_hi;
 }
 __global__ __launch_bounds__(256) void k_bsi_list(const uint64_t *active, const uint64_t *pos, uint32_t *klist) {
   const uint32_t k = blockIdx.x * 256 + threadIdx.x;
@@ -553,11 +555,20 @@ static int min_max_shortcut(int op, uint64_t a, uint64_t b, uint64_t mn, uint64_
 }
 
 int bsi_compare(rbgpu_ctx *ctx, const rbgpu_set *bsi, int op, uint64_t start, uint64_t end, uint64_t vmin,
-                uint64_t vmax, const rbgpu_set *found, rbgpu_set **out) {
+                uint64_t vmax, const rbgpu_set *found, uint32_t key_lo, uint32_t key_hi, rbgpu_set **out) {
   const uint32_t nbits = bsi->nb - 1;
   hipStream_t st = ctx->stream;
   stats_begin(ctx);
   const int sc = min_max_shortcut(op, start, end, vmin, vmax);
+  if (sc >= 0 && (key_lo > 0 || key_hi < 65536)) {
+    // a key-range shard of the shortcut's answer: the whole-range answer, restricted
+    rbgpu_set *whole = nullptr;
+    int rc = bsi_compare(ctx, bsi, op, start, end, vmin, vmax, found, 0, 65536, &whole);
+    if (rc) return rc;
+    rc = set_key_subset(whole, key_lo, key_hi, out);
+    rbgpu_set_free(whole);
+    return rc;
+  }
   if (sc >= 0) {
     // all = foundSet == null ? ebM.clone() : and(ebM, foundSet); empty = new bitmap
     if (sc == 0) {
@@ -596,7 +607,8 @@ int bsi_compare(rbgpu_ctx *ctx, const rbgpu_set *bsi, int op, uint64_t start, ui
   HIPCHK(hipMemsetAsync(d_table, 0xFF, (uint64_t)rows * 65536 * 4, st));
   k_bsi_index<<<dim3(64, nbits + 1), 256, 0, st>>>(bsi->view(), 0, d_table);
   if (found) k_bsi_index<<<dim3(64, 1), 256, 0, st>>>(found->view(), 0, d_table + (uint64_t)(nbits + 1) * 65536);
-  k_bsi_active<<<256, 256, 0, st>>>(d_table + (uint64_t)(found ? nbits + 1 : nbits) * 65536, d_active);
+  k_bsi_active<<<256, 256, 0, st>>>(d_table + (uint64_t)(found ? nbits + 1 : nbits) * 65536, key_lo, key_hi,
+                                    d_active);
   scan_exclusive(d_active, d_pos, 65536, d_tmp, st);
   k_bsi_list<<<256, 256, 0, st>>>(d_active, d_pos, d_klist);
   HIPCHK(hipMemcpyAsync(ctx->h_pinned, d_pos + 65536, 8, hipMemcpyDeviceToHost, st));

@@ -343,12 +343,16 @@ void set_mix(const int *m) {
   for (int i = 0; i < 4; ++i) g_mix[i] = m[i];
 }
 
-int generate_bsi(rbgpu_ctx *ctx, uint32_t nslices, uint64_t nrows, uint64_t seed, rbgpu_set **out) {
+// Containers are a function of (seed, slice, key) alone, so a key-range shard holds exactly the
+// whole index's containers for its keys.
+int generate_bsi(rbgpu_ctx *ctx, uint32_t nslices, uint64_t nrows, uint64_t seed, uint32_t key_lo, uint32_t key_hi,
+                 rbgpu_set **out) {
   if (nslices > 64 || nrows > (1ull << 32)) return fail(RB_EINVAL, "bsi: at most 64 slices over 2^32 rows");
+  if (key_lo > key_hi || key_hi > 65536) return fail(RB_EINVAL, "bad key range [%u, %u)", key_lo, key_hi);
   GenStructure g;
-  const uint64_t nkeys = (nrows + 65535) / 65536;
+  const uint64_t nkeys = std::min<uint64_t>((nrows + 65535) / 65536, key_hi);
   for (uint32_t b = 0; b <= nslices; ++b) { // slices 0..nslices-1, then the existence bitmap
-    for (uint64_t k = 0; k < nkeys; ++k) {
+    for (uint64_t k = key_lo; k < nkeys; ++k) {
       const uint32_t limit = (uint32_t)std::min<uint64_t>(65536, nrows - k * 65536);
       g.add((uint16_t)k, b < nslices ? kGenHalfLimit : kGenFullLimit, limit, ((uint64_t)b << 16) | k);
     }

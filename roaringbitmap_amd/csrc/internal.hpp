@@ -154,9 +154,12 @@ int wide_run(rbgpu_ctx *ctx, int sem, const rbgpu_set *in, const std::vector<uin
              uint32_t key_hi, rbgpu_set **out);
 int compact_keyed(rbgpu_ctx *ctx, const uint32_t *d_klist, uint32_t nk, const WideOut &wo, rbgpu_set *res,
                   uint64_t *nres_out);
-// bsi.hip: op = BitmapSliceIndex.Operation ordinal (EQ, NEQ, LE, LT, GE, GT, RANGE)
+// bsi.hip: op = BitmapSliceIndex.Operation ordinal (EQ, NEQ, LE, LT, GE, GT, RANGE); only the high keys in
+// [key_lo, key_hi) are computed (a key-range shard of the answer)
 int bsi_compare(rbgpu_ctx *ctx, const rbgpu_set *bsi, int op, uint64_t start, uint64_t end, uint64_t vmin,
-                uint64_t vmax, const rbgpu_set *found, rbgpu_set **out);
+                uint64_t vmax, const rbgpu_set *found, uint32_t key_lo, uint32_t key_hi, rbgpu_set **out);
+// api.hip: the containers of bitmap 0 of `s` with keys in [key_lo, key_hi), as a new one-bitmap set
+int set_key_subset(const rbgpu_set *s, uint32_t key_lo, uint32_t key_hi, rbgpu_set **out);
 // codec.hip: RoaringFormatSpec on the device.  d_in is readable up to in_lim; d_in_off[n + 1] (device).
 int deserialize_device(rbgpu_ctx *ctx, const uint8_t *d_in, uint64_t in_lim, const uint64_t *d_in_off, uint32_t n,
                        rbgpu_set **out);
@@ -164,7 +167,8 @@ int deserialize_device(rbgpu_ctx *ctx, const uint8_t *d_in, uint64_t in_lim, con
 int serialize_device(const rbgpu_set *s, uint32_t first, uint32_t count, uint8_t *dst, uint64_t cap,
                      uint64_t *offsets, bool host_dst);
 void set_mix(const int *m);
-int generate_bsi(rbgpu_ctx *ctx, uint32_t nslices, uint64_t nrows, uint64_t seed, rbgpu_set **out);
+int generate_bsi(rbgpu_ctx *ctx, uint32_t nslices, uint64_t nrows, uint64_t seed, uint32_t key_lo, uint32_t key_hi,
+                 rbgpu_set **out);
 // generate.hip
 int generate_sets(rbgpu_ctx *ctx, int workload, uint32_t n, uint64_t seed, uint32_t key_lo, uint32_t key_hi,
                   rbgpu_set **a, rbgpu_set **b);

@@ -428,7 +428,9 @@ constexpr uint64_t kQueueChunk = RBG_QUEUE_CHUNK;
 #endif
 constexpr uint32_t kQueueStripes = RBG_QUEUE_STRIPES;
 constexpr uint32_t kQueueStride = 16; // counters 128 B apart
-static_assert(kQueueStripes >= 1 && kQueueStripes <= 32, "the API reserves 32 counters (4 KiB)");
+// the API reserves 32 counters (4 KiB): 16 for the light tasks' queue, 16 for the heavy tasks'
+static_assert(kQueueStripes >= 1 && kQueueStripes <= 16, "two queues of at most 16 counters");
+constexpr uint32_t kHeavyQueueOffset = 16 * kQueueStride;
 // Next chunk [s, e) of the wave's current sub-range, moving to the following sub-ranges as they run
 // dry; s = n when every sub-range is exhausted.  One vector atomic by lane 0 per try, broadcast.
 struct Chunk {
@@ -925,20 +927,24 @@ static void launch_op_concurrent(bool card_only, const uint8_t *pa, const uint8_
                                  uint64_t nl, const TaskRec *heavy, uint64_t nh, uint8_t *out, const TaskMeta &tm,
                                  hipStream_t st, hipStream_t side, hipEvent_t light_done, hipEvent_t ev_h0,
                                  hipEvent_t ev_h1, unsigned long long *queue) {
+  // Light and heavy tasks each come from a shared queue (both zeroed by the caller before the side
+  // stream's wait).  Whichever kernel drains first hands its CUs to the other kind: the side stream
+  // runs heavy then light, the library stream light then heavy, and a second launch of a kind
+  // takes whatever tasks of that kind are left (AND: the light tasks dominate; OR / XOR: the heavy).
+  unsigned long long *hq = queue ? queue + kHeavyQueueOffset : nullptr;
   // heavy first: its blocks need the larger register slot
   (void)hipEventRecord(ev_h0, side);
-  if (card_only) launch_tasks<OP, true, kRoleHeavy>(pa, pb, heavy, nh, out, tm, side, RBG_CONC_HEAVY_PER_CU);
-  else launch_tasks<OP, false, kRoleHeavy>(pa, pb, heavy, nh, out, tm, side, RBG_CONC_HEAVY_PER_CU);
+  if (card_only) launch_tasks<OP, true, kRoleHeavy>(pa, pb, heavy, nh, out, tm, side, RBG_CONC_HEAVY_PER_CU, hq);
+  else launch_tasks<OP, false, kRoleHeavy>(pa, pb, heavy, nh, out, tm, side, RBG_CONC_HEAVY_PER_CU, hq);
   (void)hipEventRecord(ev_h1, side);
-  // light tasks from a shared queue (zeroed by the caller before the side stream's wait): one launch
-  // beside the heavy kernel, a second one on the side stream once the heavy kernel is done (its
-  // waves take whatever tasks are left)
   if (card_only) launch_tasks<OP, true, kRoleLight>(pa, pb, light, nl, out, tm, st, RBG_CONC_LIGHT_PER_CU, queue);
   else launch_tasks<OP, false, kRoleLight>(pa, pb, light, nl, out, tm, st, RBG_CONC_LIGHT_PER_CU, queue);
   (void)hipEventRecord(light_done, st);
   if (queue) {
     if (card_only) launch_tasks<OP, true, kRoleLight>(pa, pb, light, nl, out, tm, side, RBG_CONC_LIGHT_PER_CU, queue);
     else launch_tasks<OP, false, kRoleLight>(pa, pb, light, nl, out, tm, side, RBG_CONC_LIGHT_PER_CU, queue);
+    if (card_only) launch_tasks<OP, true, kRoleHeavy>(pa, pb, heavy, nh, out, tm, st, RBG_CONC_HEAVY_PER_CU, hq);
+    else launch_tasks<OP, false, kRoleHeavy>(pa, pb, heavy, nh, out, tm, st, RBG_CONC_HEAVY_PER_CU, hq);
   }
 }
 void launch_pairwise_concurrent(int op, bool card_only, const uint8_t *pa, const uint8_t *pb, const TaskRec *light,

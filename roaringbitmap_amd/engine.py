@@ -393,17 +393,25 @@ class Context:
         return DeviceSet(self, out.value)
 
     def bsi_compare(self, op: int, bsi: DeviceSet, start: int, end: int, min_value: int, max_value: int,
-                    found: Optional[DeviceSet] = None) -> DeviceSet:
-        """Roaring64BitmapSliceIndex.compare over a device BSI (slices then ebM), rbgpu_bsi_compare."""
+                    found: Optional[DeviceSet] = None, key_range=None) -> DeviceSet:
+        """Roaring64BitmapSliceIndex.compare over a device BSI (slices then ebM), rbgpu_bsi_compare;
+        key_range=(lo, hi) computes only that key-range shard of the answer (rbgpu_bsi_compare_keys)."""
         out = C.c_void_p()
-        L.check(L.lib().rbgpu_bsi_compare(self.h, bsi.h, op, start & (2**64 - 1), end & (2**64 - 1),
-                                          min_value & (2**64 - 1), max_value & (2**64 - 1),
-                                          found.h if found is not None else None, C.byref(out)))
+        lo, hi = key_range if key_range is not None else (0, 65536)
+        L.check(L.lib().rbgpu_bsi_compare_keys(self.h, bsi.h, op, start & (2**64 - 1), end & (2**64 - 1),
+                                               min_value & (2**64 - 1), max_value & (2**64 - 1),
+                                               found.h if found is not None else None, int(lo), int(hi),
+                                               C.byref(out)))
         return DeviceSet(self, out.value)
 
-    def generate_bsi(self, nslices: int, nrows: int, seed: int = 42) -> DeviceSet:
+    def generate_bsi(self, nslices: int, nrows: int, seed: int = 42, key_range=None) -> DeviceSet:
+        """The synthetic BSI of SURVEY §8d config 5, or its [lo, hi) key-range shard."""
         a = C.c_void_p()
-        L.check(L.lib().rbgpu_generate_bsi(self.h, nslices, nrows, seed, C.byref(a)))
+        if key_range is None:
+            L.check(L.lib().rbgpu_generate_bsi(self.h, nslices, nrows, seed, C.byref(a)))
+        else:
+            L.check(L.lib().rbgpu_generate_bsi_keys(self.h, nslices, nrows, seed, int(key_range[0]),
+                                                    int(key_range[1]), C.byref(a)))
         return DeviceSet(self, a.value)
 
     def extract(self, s: DeviceSet, first: int, count: int = 1) -> DeviceSet:

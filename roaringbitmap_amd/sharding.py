@@ -31,28 +31,48 @@ SERIAL_COOKIE = 12347                  # RoaringArray.java:42
 NO_OFFSET_THRESHOLD = 4                # RoaringArray.java:44
 
 
-def partition_keys(key_bytes: np.ndarray, nparts: int) -> List[Tuple[int, int]]:
-    """Contiguous [lo, hi) ranges covering [0, 65536) with near-equal byte totals.
+def _balanced_ranges(weights: np.ndarray, nparts: int) -> List[Tuple[int, int]]:
+    """Contiguous [lo, hi) ranges covering [0, len(weights)) with near-equal weight totals.
 
-    Range r ends at the first key where the running byte total reaches r/nparts of the whole, so
-    every range holds at most one key's bytes more than its share.  Ranges may be empty when a few
-    keys hold all the bytes."""
-    kb = np.asarray(key_bytes, dtype=np.float64)
-    if kb.shape != (65536,):
-        raise ValueError("key_bytes must have 65536 entries")
+    Range r ends at the first item where the running total reaches r/nparts of the whole, so every
+    range holds at most one item's weight more than its share.  Ranges may be empty when a few items
+    hold all the weight."""
+    w = np.asarray(weights, dtype=np.float64)
+    n = len(w)
     if nparts < 1:
         raise ValueError("nparts must be >= 1")
-    csum = np.cumsum(kb)
+    csum = np.cumsum(w) if n else np.zeros(1)
     total = csum[-1]
     bounds = [0]
     for r in range(1, nparts):
         if total <= 0:
-            b = (65536 * r) // nparts
+            b = (n * r) // nparts
         else:
             b = int(np.searchsorted(csum, total * r / nparts, side="left")) + 1
-        bounds.append(min(max(b, bounds[-1]), 65536))
-    bounds.append(65536)
+        bounds.append(min(max(b, bounds[-1]), n))
+    bounds.append(n)
     return [(bounds[i], bounds[i + 1]) for i in range(nparts)]
+
+
+def partition_keys(key_bytes: np.ndarray, nparts: int) -> List[Tuple[int, int]]:
+    """Contiguous [lo, hi) high-key ranges covering [0, 65536) with near-equal byte totals."""
+    kb = np.asarray(key_bytes)
+    if kb.shape != (65536,):
+        raise ValueError("key_bytes must have 65536 entries")
+    return _balanced_ranges(kb, nparts)
+
+
+def pair_bytes(a_bytes: np.ndarray, b_bytes: np.ndarray, a_idx: np.ndarray, b_idx: np.ndarray) -> np.ndarray:
+    """Input payload bytes of each pair of a batch (the work a pair costs the HBM-bound kernels):
+    a_bytes / b_bytes are per-bitmap payload bytes of the two sets (DeviceSet.summaries())."""
+    return np.asarray(a_bytes, np.uint64)[np.asarray(a_idx, np.int64)] + \
+        np.asarray(b_bytes, np.uint64)[np.asarray(b_idx, np.int64)]
+
+
+def partition_pairs(bytes_per_pair: np.ndarray, nparts: int) -> List[Tuple[int, int]]:
+    """Contiguous [lo, hi) ranges of one caller batch with near-equal input bytes: a rank computes
+    its range of the pairs (results stay in batch order across ranks)."""
+    return _balanced_ranges(bytes_per_pair, nparts)
 
 
 def _payload_size(t: int, c: int, r: int) -> int:
@@ -161,3 +181,79 @@ class ShardedWide:
         if self.rank != dst:
             return None
         return serialize_parts(parts)
+
+
+class ShardedBsi(ShardedWide):
+    """Key-range-sharded Roaring64BitmapSliceIndex.compare.
+
+    The O'Neil comparison is key-local: every 2^16-row chunk (high key) of the answer depends only
+    on the slices' and ebM's containers of that key, the way the reference already splits the work
+    (BitSliceIndexBase.java:99-166 partitions the foundSet by high key for its thread pool).  Rank r
+    holds the slices and ebM of its key range (rbgpu_generate_bsi_keys, or any BSI set: keys outside
+    the range are ignored) and computes that range of the answer (rbgpu_bsi_compare_keys); the
+    exchange is ShardedWide's: an all_gather of the shard summaries (global cardinality = the
+    reference's getCardinality of the answer, serialized size) and, on request, the gather of the
+    shards to one rank."""
+
+    def compare(self, ctx, op: int, bsi, start: int, end: int, min_value: int, max_value: int,
+                key_range: Tuple[int, int], found=None) -> ShardResult:
+        local = ctx.bsi_compare(op, bsi, start, end, min_value, max_value, found, key_range=key_range)
+        return self.finish(local, key_range, local.summaries()[0])
+
+
+@dataclass
+class PairShardResult:
+    """One rank's share of a pair-sharded batch plus the global facts about the results."""
+    local: object                 # DeviceSet of this rank's results (pairs [lo, hi) in order), or HostSoA
+    pair_range: Tuple[int, int]
+    cardinality: int              # sum of every result's cardinality over all ranks
+    n_containers: int
+    payload_bytes: int
+
+
+class ShardedPairwise:
+    """One caller batch of (a[i], b[i]) pairs split across ranks by input bytes (partition_pairs).
+
+    Pairs are independent (RoaringBitmap.and/or/xor/andNot of two bitmaps), so the data path has no
+    collective; the exchange is one all_reduce of (result cardinality, containers, payload bytes) —
+    the batch's total cardinality, which the reference's callers get by summing
+    getCardinality / andCardinality — and, on request, the gather of the serialized results to one
+    rank in batch order."""
+
+    def __init__(self, dist, rank: int, world: int, device=None):
+        self.dist, self.rank, self.world = dist, rank, world
+        self.device = device
+
+    def split(self, bytes_per_pair: np.ndarray) -> Tuple[int, int]:
+        return partition_pairs(bytes_per_pair, self.world)[self.rank]
+
+    def finish(self, local, pair_range: Tuple[int, int], cardinality: int, n_containers: int,
+               payload_bytes: int) -> PairShardResult:
+        import torch
+        t = torch.tensor([cardinality, n_containers, payload_bytes], dtype=torch.int64, device=self.device)
+        self.dist.all_reduce(t)
+        g = t.cpu().tolist()
+        return PairShardResult(local, pair_range, int(g[0]), int(g[1]), int(g[2]))
+
+    def run(self, ctx, op: int, a, b, a_idx: np.ndarray, b_idx: np.ndarray, bytes_per_pair=None) -> PairShardResult:
+        """This rank's pairs of the batch on its MI355X (rbgpu_pairwise) + the exchange."""
+        if bytes_per_pair is None:
+            pa = np.array([s["payload_bytes"] for s in a.summaries()], np.uint64)
+            pb = pa if b is a else np.array([s["payload_bytes"] for s in b.summaries()], np.uint64)
+            bytes_per_pair = pair_bytes(pa, pb, a_idx, b_idx)
+        lo, hi = self.split(bytes_per_pair)
+        ai = np.ascontiguousarray(a_idx[lo:hi], np.uint32)
+        bi = np.ascontiguousarray(b_idx[lo:hi], np.uint32)
+        local = ctx.pairwise(op, a, b, ai, bi)
+        st = ctx.stats()
+        return self.finish(local, (lo, hi), st["result_cardinality"], st["result_containers"],
+                           st["output_bytes"])
+
+    def gather_serialized(self, res: PairShardResult, dst: int = 0) -> Optional[List[bytes]]:
+        """Every result's RoaringFormatSpec bytes, in batch order, on rank `dst` (None elsewhere)."""
+        mine = res.local.serialize() if hasattr(res.local, "serialize") else list(res.local)
+        parts: Optional[List[List[bytes]]] = [None] * self.world if self.rank == dst else None
+        self.dist.gather_object(mine, parts, dst=dst)
+        if self.rank != dst:
+            return None
+        return [x for p in parts for x in p]

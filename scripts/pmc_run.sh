@@ -12,7 +12,7 @@ i=0
 for set in "$@"; do
   i=$((i+1))
   echo "=== pass $i: $set"
-  timeout -s KILL 100 rocprofv3 --pmc $set --output-format csv -d "$out/p$i" -o run -- $cmd > "$out/p$i.log" 2>&1
+  timeout -s KILL "${PMC_TIMEOUT:-100}" rocprofv3 --pmc $set --output-format csv -d "$out/p$i" -o run -- $cmd > "$out/p$i.log" 2>&1
   rc=$?
   echo "exit=$rc"
   if [ $rc -ne 0 ]; then tail -5 "$out/p$i.log"; exit $rc; fi

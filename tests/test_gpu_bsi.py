@@ -84,3 +84,40 @@ def test_generated_bsi_sample(ctx, oracle):
         got = ctx.bsi_compare(op, d, lo, hi, 0, (1 << 24) - 1).serialize()[0]
         want = oracle.bsi_compare(sl, ebm, op, lo, hi, None, 0, (1 << 24) - 1).serialize()
         assert got == want, name
+
+
+def test_bsi_key_range_shards(ctx, oracle):
+    """rbgpu_bsi_compare_keys / rbgpu_generate_bsi_keys: the key-range shards of the
+    answer, computed from the whole index and from per-shard generated indexes, reassemble
+    (serialize_parts) to the whole answer's bytes — O'Neil path and min/max shortcut, with foundSet."""
+    import roaringbitmap_amd as rb
+    from roaringbitmap_amd.sharding import serialize_parts
+    nrows, nbits = 5 * 65536 + 77, 20
+    d = ctx.generate_bsi(nbits, nrows, seed=9)
+    fvals = np.arange(0, nrows, 3, dtype=np.uint32)
+    found = ctx.upload_values([fvals])
+    parts = [(0, 2), (2, 3), (3, 65536)]
+    shards = [ctx.generate_bsi(nbits, nrows, seed=9, key_range=kr) for kr in parts]
+    whole = d.download()
+    for s, (klo, khi) in zip(shards, parts):  # a generated shard holds exactly the index's containers
+        h = s.download()
+        for b in range(nbits + 1):
+            sel = [i for i in range(int(whole.begin[b]), int(whole.begin[b + 1])) if klo <= whole.key[i] < khi]
+            assert list(h.key[int(h.begin[b]):int(h.begin[b + 1])]) == [int(whole.key[i]) for i in sel]
+            for j, i in zip(range(int(h.begin[b]), int(h.begin[b + 1])), sel):
+                assert bytes(h.container_payload(j)) == bytes(whole.container_payload(i))
+    vmax = (1 << nbits) - 1
+    for name, lo, hi in (("RANGE", 1 << 17, 5 << 17), ("GE", 4321, 0), ("NEQ", 7, 0), ("LE", vmax, 0),
+                         ("GT", 1 << 30, 0)):  # LE vmax / GT above max: the min/max shortcut
+        op = getattr(rb, "BSI_" + name)
+        for f in (None, found):
+            want = ctx.bsi_compare(op, d, lo, hi, 0, vmax, f).serialize()[0]
+            for src in ("whole", "shards"):
+                hs = []
+                for i, kr in enumerate(parts):
+                    r = ctx.bsi_compare(op, d if src == "whole" else shards[i], lo, hi, 0, vmax, f, key_range=kr)
+                    assert len(r) == 1
+                    hs.append(r.download())
+                assert serialize_parts(hs) == want, (name, src, f is not None)
+    with pytest.raises(rb.InvalidArgument):
+        ctx.bsi_compare(rb.BSI_GE, d, 3, 0, 0, vmax, key_range=(5, 70000))

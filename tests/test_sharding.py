@@ -12,7 +12,8 @@ import torch.multiprocessing as mp
 from datasets import fixture_bytes, load_realdata, synthetic_bitmaps
 from roaringbitmap_amd import _lib as L
 from roaringbitmap_amd.engine import HostSoA, host_summary, soa_from_serialized
-from roaringbitmap_amd.sharding import ShardedWide, header_size, partition_keys, serialize_parts
+from roaringbitmap_amd.sharding import (ShardedWide, header_size, pair_bytes, partition_keys, partition_pairs,
+                                        serialize_parts)
 
 SEMS = {"FAST_OR": L.FAST_OR, "WORKSHY_AND": L.WORKSHY_AND, "FAST_XOR": L.FAST_XOR, "PAR_OR": L.PAR_OR,
         "PAR_XOR": L.PAR_XOR}
@@ -116,16 +117,140 @@ def _rank_main(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def test_gloo_two_rank_sharded_wide():
+def _spawn(target, world=2):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_rank_main, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=target, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
     out = q.get(timeout=240)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    for name, ok in out.items():
+    return out
+
+
+def test_gloo_two_rank_sharded_wide():
+    for name, ok in _spawn(_rank_main).items():
+        assert all(ok), (name, ok)
+
+
+def test_partition_pairs_balanced():
+    rng = np.random.default_rng(9)
+    pb = rng.integers(0, 20000, 3001).astype(np.uint64)
+    for n in (1, 2, 3, 8):
+        parts = partition_pairs(pb, n)
+        assert parts[0][0] == 0 and parts[-1][1] == len(pb)
+        assert all(parts[i][1] == parts[i + 1][0] for i in range(n - 1))
+        for lo, hi in parts:
+            assert int(pb[lo:hi].sum()) <= pb.sum() / n + int(pb.max())
+    assert partition_pairs(np.zeros(0, np.uint64), 3) == [(0, 0)] * 3
+    assert list(pair_bytes(np.array([5, 7]), np.array([1, 2, 3]), np.array([1, 0]), np.array([2, 2]))) == [10, 8]
+
+
+def _restrict(R, r, lo, hi):
+    """The containers of oracle bitmap r with high keys in [lo, hi) (bitmapOf-built, as r is)."""
+    v = r.to_array()
+    k = v >> 16
+    return R.RefBitmap.of(v[(k >= lo) & (k < hi)])
+
+
+def _bsi_case(R, seed=4):
+    """A BSI over ~6 high keys of rows (bitmapOf-built slices, BitmapSliceIndex.setValue order)."""
+    rng = np.random.default_rng(seed)
+    cols = np.unique(rng.integers(0, 6 * 65536, 40000)).astype(np.uint64)
+    vals = rng.integers(0, 1 << 20, len(cols)).astype(np.uint64)
+    slices, ebm, vmin, vmax = R.bsi_build(cols, vals)
+    found = R.RefBitmap.of(cols[rng.random(len(cols)) < 0.6].astype(np.uint32))
+    return slices, ebm, vmin, vmax, found
+
+
+BSI_QUERIES = [  # (op, start, end, with foundSet)
+    ("RANGE", 1 << 18, 3 << 18, False), ("GE", 12345, 0, True), ("LT", 99999, 0, False), ("EQ", None, 0, False),
+    ("NEQ", None, 0, True), ("GT", 0, 0, False),  # GT 0 with min 0: the O'Neil path
+    ("LE", 1 << 40, 0, True),  # LE above max: the min/max shortcut (all of ebM AND foundSet)
+]
+
+
+def _rank_bsi(rank, world, port, q):
+    import torch.distributed as dist
+
+    from oracle import rbref as R
+    from roaringbitmap_amd.sharding import ShardedBsi
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        slices, ebm, vmin, vmax, found = _bsi_case(R)
+        kb = np.zeros(65536, np.uint64)
+        h = soa_from_serialized([ebm.serialize()])
+        np.add.at(kb, h.key.astype(np.int64), 1)
+        lo, hi = partition_keys(kb, world)[rank]
+        # this rank's shard of the index: slices + ebM (+ foundSet) restricted to its key range
+        s_sl = [_restrict(R, s, lo, hi) for s in slices]
+        s_eb, s_fd = _restrict(R, ebm, lo, hi), _restrict(R, found, lo, hi)
+        sw = ShardedBsi(dist, rank, world)
+        out = {}
+        for name, start, end, use_found in BSI_QUERIES:
+            op_ = getattr(R, "BSI_" + name)
+            if start is None:  # EQ the minimum value, NEQ 0
+                start = 0 if name == "NEQ" else int(vmin)
+            local = R.bsi_compare(s_sl, s_eb, op_, start, end, s_fd if use_found else None, vmin, vmax)
+            hl = soa_from_serialized([local.serialize()])
+            res = sw.finish(hl, (lo, hi), host_summary(hl))
+            data = sw.gather_serialized(res)
+            if rank == 0:
+                want = R.bsi_compare(slices, ebm, op_, start, end, found if use_found else None, vmin, vmax)
+                out[name] = (data == want.serialize(), res.cardinality == want.cardinality(),
+                             res.serialized_size == len(want.serialize()))
+        if rank == 0:
+            q.put(out)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_two_rank_sharded_bsi():
+    for name, ok in _spawn(_rank_bsi).items():
+        assert all(ok), (name, ok)
+
+
+def _rank_pairs(rank, world, port, q):
+    import torch.distributed as dist
+
+    from oracle import rbref as R
+    from roaringbitmap_amd.sharding import ShardedPairwise
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        vals = load_realdata("census1881_srt")[:60] + synthetic_bitmaps(20, seed=8, max_keys=6, key_space=16)
+        bms = [R.RefBitmap.of(v) for v in vals]
+        for r in bms[1::4]:
+            r.run_optimize()
+        sizes = np.array([len(r.serialize()) for r in bms], np.uint64)
+        rng = np.random.default_rng(1)
+        ai = rng.integers(0, len(bms), 150).astype(np.uint32)
+        bi = rng.integers(0, len(bms), 150).astype(np.uint32)
+        sp = ShardedPairwise(dist, rank, world)
+        lo, hi = sp.split(pair_bytes(sizes, sizes, ai, bi))
+        out = {}
+        for name, opc in (("AND", L.AND), ("OR", L.OR), ("XOR", L.XOR), ("ANDNOT", L.ANDNOT)):
+            local = [R.op(opc, bms[a], bms[b]) for a, b in zip(ai[lo:hi], bi[lo:hi])]
+            res = sp.finish([r.serialize() for r in local], (lo, hi), sum(r.cardinality() for r in local),
+                            sum(len(r.containers()) for r in local), 0)
+            got = sp.gather_serialized(res)
+            if rank == 0:
+                want = [R.op(opc, bms[a], bms[b]) for a, b in zip(ai, bi)]
+                out[name] = (got == [w.serialize() for w in want],
+                             res.cardinality == sum(w.cardinality() for w in want),
+                             res.n_containers == sum(len(w.containers()) for w in want))
+        if rank == 0:
+            q.put(out)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_two_rank_sharded_pairwise():
+    for name, ok in _spawn(_rank_pairs).items():
         assert all(ok), (name, ok)
