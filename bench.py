@@ -360,7 +360,8 @@ def run_census(args, ctx, rb, steps=50, warmup=5):
            "value": round(in_bytes / el / 1e9, 3), "unit": "GB/s", "steps": steps,
            "ms_per_step": round(el / steps * 1e3, 4),
            "us_per_op_sweep": round(el / steps / 4 * 1e6, 1), "cardinality_sums": cards,
-           "golden_ok": cards == CENSUS_EXPECTED}
+           "golden_ok": cards == CENSUS_EXPECTED, "kernel": ctx.stats()["main_kernel"],
+           "call_ms_device": round(ctx.stats()["total_ms"], 4)}
     if not args.no_cpu_baseline:
         from oracle import rbref as R
         refs = [R.RefBitmap.deserialize(x) for x in s.serialize()]

@@ -226,6 +226,62 @@ int rbgpu_generate_bsi_keys(rbgpu_ctx *ctx, uint32_t nslices, uint64_t nrows, ui
 int rbgpu_generate(rbgpu_ctx *ctx, int workload, uint32_t n, uint64_t seed, rbgpu_set **a,
                    rbgpu_set **b);
 
+/* ---- multi-GPU: one process (or host thread) per GPU, RCCL over xGMI ------------------------
+ * The reference scales one JVM over a ForkJoin pool (ParallelAggregation.java:161-195, keys
+ * grouped and reduced in parallel).  Here each GPU owns a high-key range of the data (the key
+ * partition is exact: every key's result depends only on that key's containers) and the exchange
+ * happens inside the library on the communicator: an all-gather of the shard summaries and, on
+ * request, the gather of the shards' serialized bytes to one rank, assembled there on the device
+ * into the RoaringFormatSpec bytes of the whole result (RoaringArray.serialize, RoaringArray.java:
+ * 851-940).  RCCL is opened at rbgpu_comm_init (dlopen of librccl.so.1: the library itself has no
+ * link-time dependency on it). */
+typedef struct rbgpu_comm rbgpu_comm;
+enum { RB_COMM_ID_BYTES = 128 };
+/* A communicator id (ncclGetUniqueId): made on one rank and handed to the others by the caller
+ * over any channel (the JVM's own transport, torch.distributed, an environment variable). */
+int rbgpu_comm_unique_id(uint8_t id[RB_COMM_ID_BYTES]);
+/* Joins the communicator of `nranks` ranks as `rank` on ctx's GPU (collective: every rank calls it). */
+int rbgpu_comm_init(rbgpu_ctx *ctx, const uint8_t id[RB_COMM_ID_BYTES], int nranks, int rank, rbgpu_comm **out);
+void rbgpu_comm_destroy(rbgpu_comm *comm);
+
+/* The whole result of a key-range-sharded aggregation, as every rank sees it after the exchange. */
+typedef struct rb_shard_summary {
+  uint64_t cardinality;       /* RoaringBitmap.getCardinality of the whole result */
+  uint64_t n_containers;
+  uint64_t n_run_containers;
+  uint64_t payload_bytes;     /* container payload bytes of the whole result (Run counts included) */
+  uint64_t serialized_size;   /* RoaringBitmap.serializedSizeInBytes of the whole result */
+  uint64_t payload_offset;    /* where this rank's first container payload starts in those bytes */
+  uint64_t container_offset;  /* this rank's first container index in the whole result */
+  uint64_t local_serialized;  /* serializedSizeInBytes of this rank's shard alone */
+} rb_shard_summary;
+/* The exchange for a one-bitmap shard `local` (keys of every rank disjoint and increasing with rank):
+ * an all-gather of (cardinality, containers, Run containers, payload bytes, shard bytes) over the
+ * communicator.  Collective. */
+int rbgpu_shard_summarize(rbgpu_comm *comm, const rbgpu_set *local, rb_shard_summary *out);
+/* rbgpu_wide_keys over [key_lo, key_hi) on this rank's GPU + rbgpu_shard_summarize.  Collective. */
+int rbgpu_wide_sharded(rbgpu_comm *comm, int sem, const rbgpu_set *in, const uint32_t *members, uint32_t n,
+                       uint32_t key_lo, uint32_t key_hi, rbgpu_set **local, rb_shard_summary *summary);
+/* rbgpu_bsi_compare_keys over [key_lo, key_hi) + rbgpu_shard_summarize.  Collective. */
+int rbgpu_bsi_compare_sharded(rbgpu_comm *comm, const rbgpu_set *bsi, int op, uint64_t start_or_value, uint64_t end,
+                              uint64_t min_value, uint64_t max_value, const rbgpu_set *found, uint32_t key_lo,
+                              uint32_t key_hi, rbgpu_set **local, rb_shard_summary *summary);
+/* The serialized bytes of the whole result on rank `root`, written to device memory d_dst (cap >=
+ * summary->serialized_size; ignored on the other ranks): every rank serializes its shard on its
+ * GPU, the shards travel to `root` as one grouped RCCL send/recv, and one kernel there writes the
+ * global header (cookie, Run-container bitmap, key / cardinality-1 pairs, offsets) around the
+ * concatenated payloads.  Collective. */
+int rbgpu_shard_gather_serialized(rbgpu_comm *comm, const rbgpu_set *local, const rb_shard_summary *summary,
+                                  int root, uint8_t *d_dst, uint64_t cap);
+/* Sum of `n` u64 values over the ranks, in place (the pairwise batch's cardinality exchange:
+ * each rank runs its own pairs, the sum of the results' cardinalities is a global fact).  Collective. */
+int rbgpu_comm_allreduce_sum(rbgpu_comm *comm, uint64_t *values, uint32_t n);
+/* The header assembly of rbgpu_shard_gather_serialized on host buffers (the same code the device
+ * kernel runs): parts[r] = the standalone serialized bytes of rank r's shard (keys increasing with
+ * r); writes the whole result's bytes to dst (cap bytes) and their length to *written. */
+int rbgpu_shard_assemble_host(const uint8_t *const *parts, const uint64_t *part_lens, uint32_t nparts,
+                              uint8_t *dst, uint64_t cap, uint64_t *written);
+
 #ifdef __cplusplus
 }
 #endif

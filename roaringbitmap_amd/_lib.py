@@ -59,6 +59,14 @@ class RbStats(C.Structure):
     ]
 
 
+class RbShardSummary(C.Structure):
+    _fields_ = [("cardinality", C.c_uint64), ("n_containers", C.c_uint64), ("n_run_containers", C.c_uint64),
+                ("payload_bytes", C.c_uint64), ("serialized_size", C.c_uint64), ("payload_offset", C.c_uint64),
+                ("container_offset", C.c_uint64), ("local_serialized", C.c_uint64)]
+
+
+COMM_ID_BYTES = 128
+
 # every symbol include/rbgpu.h declares, with its ctypes signature
 _P = C.c_void_p
 _U32P = C.POINTER(C.c_uint32)
@@ -99,6 +107,19 @@ SIGNATURES = {
     "rbgpu_generate_bsi": (C.c_int, [_P, C.c_uint32, C.c_uint64, C.c_uint64, C.POINTER(_P)]),
     "rbgpu_generate_keys": (C.c_int, [_P, C.c_int, C.c_uint32, C.c_uint64, C.c_uint32, C.c_uint32, C.POINTER(_P)]),
     "rbgpu_generate": (C.c_int, [_P, C.c_int, C.c_uint32, C.c_uint64, C.POINTER(_P), C.POINTER(_P)]),
+    "rbgpu_comm_unique_id": (C.c_int, [C.c_void_p]),
+    "rbgpu_comm_init": (C.c_int, [_P, C.c_void_p, C.c_int, C.c_int, C.POINTER(_P)]),
+    "rbgpu_comm_destroy": (None, [_P]),
+    "rbgpu_comm_allreduce_sum": (C.c_int, [_P, _U64P, C.c_uint32]),
+    "rbgpu_shard_summarize": (C.c_int, [_P, _P, C.POINTER(RbShardSummary)]),
+    "rbgpu_wide_sharded": (C.c_int, [_P, C.c_int, _P, _U32P, C.c_uint32, C.c_uint32, C.c_uint32, C.POINTER(_P),
+                                     C.POINTER(RbShardSummary)]),
+    "rbgpu_bsi_compare_sharded": (C.c_int, [_P, _P, C.c_int, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64, _P,
+                                            C.c_uint32, C.c_uint32, C.POINTER(_P), C.POINTER(RbShardSummary)]),
+    "rbgpu_shard_gather_serialized": (C.c_int, [_P, _P, C.POINTER(RbShardSummary), C.c_int, C.c_void_p,
+                                                C.c_uint64]),
+    "rbgpu_shard_assemble_host": (C.c_int, [C.POINTER(C.c_char_p), _U64P, C.c_uint32, C.c_void_p, C.c_uint64,
+                                            _U64P]),
 }
 
 

@@ -116,6 +116,25 @@ int ensure_max_keys(const rbgpu_set *cs) {
   s->max_keys = (int64_t)m;
   return RB_OK;
 }
+int ensure_max_runs(const rbgpu_set *cs) {
+  rbgpu_set *s = const_cast<rbgpu_set *>(cs);
+  if (s->max_runs >= 0) return RB_OK;
+  uint64_t m = 0;
+  if (s->nc) {
+    HIPCHK(hipSetDevice(s->ctx->device));
+    uint64_t *d = nullptr;
+    if (s->ctx->pool.alloc((void **)&d, 8)) return fail(RB_ENOMEM, "max-runs word");
+    HIPCHK(hipMemsetAsync(d, 0, 8, s->ctx->stream));
+    launch_max_runs(s->type, s->nruns, s->nc, d, s->ctx->stream);
+    HIPCHK(hipMemcpyAsync(s->ctx->h_pinned + 7, d, 8, hipMemcpyDeviceToHost, s->ctx->stream));
+    HIPCHK(hipStreamSynchronize(s->ctx->stream));
+    LAUNCHCHK();
+    s->ctx->pool.release(d);
+    m = s->ctx->h_pinned[7];
+  }
+  s->max_runs = (int64_t)m;
+  return RB_OK;
+}
 } // namespace rbg
 
 namespace {
@@ -654,6 +673,107 @@ static uint32_t pairwise_seg_keys(const rbgpu_set *a, const rbgpu_set *b, uint64
   while (seg > 8 && est / seg < 131072.0) seg >>= 1;
   return seg;
 }
+// Small batches (kernels.hpp: <= kSmallPairs pairs of <= kSmallPairKeys keys, <= kSmallSlots merged
+// keys, no Run container over 8 KiB to copy): two launches and one host read-back.  Returns 1 when
+// the batch does not qualify (the general pipeline runs), else an rbgpu status.
+static int pairwise_small(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu_set *b, const uint32_t *a_idx,
+                          const uint32_t *b_idx, uint32_t np, rbgpu_set **out, uint64_t *card_out) {
+  const char *dis = getenv("RBGPU_NO_SMALL_PAIRS"); // parity tests run both paths
+  if ((dis && dis[0] == '1') || np == 0 || np > kSmallPairs) return 1;
+  int rc = ensure_h_begin(a);
+  if (!rc) rc = ensure_h_begin(b);
+  if (rc) return rc;
+  // staging blob (host pinned and device): slot[np + 1] (u64), then a_idx[np], b_idx[np] (u32)
+  const size_t nslot = 8 * (np + 1ull), nidx = 4ull * np * ((a_idx != nullptr) + (b_idx != nullptr));
+  const size_t blob = nslot + nidx;
+  if (blob > ctx->h_stage_cap) {
+    if (ctx->h_stage) (void)hipHostFree(ctx->h_stage);
+    ctx->h_stage = nullptr;
+    ctx->h_stage_cap = 0;
+    if (hipHostMalloc((void **)&ctx->h_stage, blob) != hipSuccess) return fail(RB_ENOMEM, "pinned staging");
+    ctx->h_stage_cap = blob;
+  }
+  uint64_t *slot = reinterpret_cast<uint64_t *>(ctx->h_stage), acc = 0;
+  uint32_t max_keys = 0;
+  for (uint32_t p = 0; p < np; ++p) {
+    const uint32_t ai = a_idx ? a_idx[p] : p, bi = b_idx ? b_idx[p] : p;
+    const uint64_t nk = (a->h_begin[ai + 1] - a->h_begin[ai]) + (b->h_begin[bi + 1] - b->h_begin[bi]);
+    if (nk > kSmallPairKeys) return 1;
+    max_keys = std::max(max_keys, (uint32_t)nk);
+    slot[p] = acc;
+    acc += nk;
+    if (acc > kSmallSlots) return 1;
+  }
+  slot[np] = acc;
+  rc = ensure_max_runs(a);
+  if (!rc) rc = ensure_max_runs(b);
+  if (rc) return rc;
+  if (a->max_runs > 2048 || b->max_runs > 2048) return 1; // a copy would not fit its 8 KiB slot
+  const uint64_t E = acc;
+  uint8_t *hp = ctx->h_stage + nslot;
+  if (a_idx) std::memcpy(hp, a_idx, 4ull * np), hp += 4ull * np;
+  if (b_idx) std::memcpy(hp, b_idx, 4ull * np);
+
+  hipStream_t st = ctx->stream;
+  const bool card_only = out == nullptr;
+  const uint64_t E1 = std::max<uint64_t>(E, 1);
+  const size_t need = aligned256(blob) + aligned256(8ull * np) + aligned256(4 * E1) + aligned256(2 * E1) +
+                      aligned256(E1) + aligned256(4 * E1) + aligned256(2 * E1) + aligned256(8) + 256;
+  if (ctx->ws_pairs.reserve(need, st) != hipSuccess) return fail(RB_ENOMEM, "pair workspace");
+  Workspace &W = ctx->ws_pairs;
+  uint8_t *d_blob = W.take<uint8_t>(blob);
+  SmallPairArgs sa{};
+  sa.A = a->view();
+  sa.B = b->view();
+  sa.slot = reinterpret_cast<const uint64_t *>(d_blob);
+  const uint32_t *d_idx = reinterpret_cast<const uint32_t *>(d_blob + nslot);
+  sa.aidx = a_idx ? d_idx : nullptr;
+  sa.bidx = b_idx ? d_idx + (a_idx ? np : 0) : nullptr;
+  sa.np = np;
+  sa.pcard = card_out ? W.take<uint64_t>(np) : nullptr;
+  uint32_t *xpos = W.take<uint32_t>(E1);
+  sa.skey = W.take<uint16_t>(E1);
+  sa.stype = W.take<uint8_t>(E1);
+  sa.scard = W.take<uint32_t>(E1);
+  sa.snruns = W.take<uint16_t>(E1);
+  uint64_t *d_total = W.take<uint64_t>(1);
+  HIPCHK(hipMemcpyAsync(d_blob, ctx->h_stage, blob, hipMemcpyHostToDevice, st));
+
+  rbgpu_set *res = nullptr;
+  if (!card_only) {
+    res = new rbgpu_set;
+    rc = set_alloc(ctx, res, np, E, E * kBitmapBytes);
+    if (rc) {
+      delete res;
+      return rc;
+    }
+    sa.arena = res->payload;
+  }
+  stats_begin(ctx);
+  HIPCHK(hipEventRecord(ctx->ev[1], st));
+  launch_pair_small(op, card_only, sa, max_keys, ctx->d_stats, st);
+  HIPCHK(hipEventRecord(ctx->ev[2], st));
+  OutView ov{};
+  if (res) ov = OutView{res->key, res->type, res->card, res->nruns, res->off};
+  launch_pair_small_compact(sa, ov, res ? res->begin : nullptr, xpos, d_total, st);
+  HIPCHK(hipEventRecord(ctx->ev[3], st));
+  HIPCHK(hipMemcpyAsync(ctx->h_pinned + 5, d_total, 8, hipMemcpyDeviceToHost, st));
+  if (card_out) HIPCHK(hipMemcpyAsync(card_out, sa.pcard, 8ull * np, hipMemcpyDeviceToHost, st));
+  const KernelSpan spans[2] = {{"k_pair_small", 6, 1, E}, {"k_pair_small_compact", -1, -1, E}};
+  rc = stats_end(ctx, E, 0, spans, 2);
+  if (rc) {
+    if (res) rbgpu_set_free(res);
+    return rc;
+  }
+  const uint64_t nres = ctx->h_pinned[5];
+  ctx->last.result_containers = nres;
+  if (res) {
+    res->nc = nres;
+    *out = res;
+  }
+  return RB_OK;
+}
+
 // probe: 0 = the product path; 1 / 2 = measurement probes (rbgpu_internal_probe) in place of the
 // task kernel — results are not produced.
 static int pairwise_impl(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu_set *b, const uint32_t *a_idx,
@@ -670,6 +790,10 @@ static int pairwise_impl(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu
     if (a_idx[i] >= a->nb) return fail(RB_EINVAL, "a_idx[%u] out of range", i);
   for (uint32_t i = 0; b_idx && i < npairs; ++i)
     if (b_idx[i] >= b->nb) return fail(RB_EINVAL, "b_idx[%u] out of range", i);
+  if (!probe) {
+    rc = pairwise_small(ctx, op, a, b, a_idx, b_idx, npairs, out, card_out);
+    if (rc != 1) return rc;
+  }
   const bool card_only = out == nullptr;
   hipStream_t st = ctx->stream;
   const uint64_t np = npairs;

@@ -126,6 +126,7 @@ struct rbgpu_set {
   uint8_t *payload = nullptr;
   std::vector<uint64_t> h_begin; // host copy of the CSR, downloaded on demand
   int64_t max_keys = -1;          // most containers in one bitmap (cached on first pairwise use)
+  int64_t max_runs = -1;          // most runs in one Run container (cached on first small-batch use)
   rbg::SetView view() const { return rbg::SetView{begin, key, type, card, nruns, off, payload}; }
 };
 
@@ -135,6 +136,7 @@ void ctx_unref(rbgpu_ctx *ctx);
 void set_release(rbgpu_set *s);
 int ensure_h_begin(const rbgpu_set *s);
 int ensure_max_keys(const rbgpu_set *s);
+int ensure_max_runs(const rbgpu_set *s);
 // call accounting: zero the byte counters + record the start event / read everything back
 void stats_begin(rbgpu_ctx *ctx);
 // Compute-phase kernels k = 0..n-1 ran between events ev[1+k] and ev[2+k]; their algorithmic

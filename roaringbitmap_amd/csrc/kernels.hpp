@@ -50,6 +50,7 @@ void launch_seg_count(const PairArgs &a, uint64_t *nseg, hipStream_t st);
 void launch_seg_fill(const PairArgs &a, const uint64_t *seg_begin, uint32_t *seg_pair, hipStream_t st);
 void launch_seg_identity(uint64_t np, uint64_t *seg_begin, uint32_t *seg_pair, hipStream_t st);
 void launch_max_span(const uint64_t *begin, uint32_t nb, uint64_t *out, hipStream_t st);
+void launch_max_runs(const uint8_t *type, const uint16_t *nruns, uint64_t n, uint64_t *out, hipStream_t st);
 void launch_pair_rbegin(const uint64_t *seg_begin, uint32_t npairs, const uint64_t *rseg, uint64_t *rbegin,
                         hipStream_t st);
 // per segment from here on
@@ -75,6 +76,29 @@ void launch_compact_count(const uint64_t *task_begin, uint64_t nseg, const uint8
 void launch_compact_write(const uint64_t *task_begin, uint64_t nseg, const TaskMeta &tm, const uint64_t *rbegin,
                           const OutView &out, const uint32_t *seg_pair, uint64_t *pair_card, uint64_t *stats,
                           hipStream_t st);
+
+// small batches (<= kSmallPairs pairs, <= kSmallPairKeys keys per pair, <= kSmallSlots merged keys in
+// all): one kernel per call computes every pair into one 8 KiB slot per merged key, one single-block
+// kernel compacts the slots into the result CSR
+constexpr uint32_t kSmallPairs = 4096, kSmallPairKeys = 4096, kSmallSlots = 32768;
+struct SmallPairArgs {
+  SetView A, B;
+  const uint32_t *aidx, *bidx; // may be null (identity)
+  const uint64_t *slot;        // [np + 1] first slot of pair p (prefix of its key counts)
+  uint32_t np;
+  uint8_t *arena;              // slot t's payload at t * 8 KiB (null for cardinality only)
+  uint16_t *skey;              // per slot
+  uint8_t *stype;
+  uint32_t *scard;
+  uint16_t *snruns;
+  uint64_t *pcard;             // [np] result cardinality per pair, or null
+};
+// max_keys: the most keys of one pair (na + nb), sizes the blocks per pair
+void launch_pair_small(int op, bool card_only, const SmallPairArgs &a, uint32_t max_keys, uint64_t *stats,
+                       hipStream_t st);
+// out.key null: only *total and rbegin; rbegin may be null
+void launch_pair_small_compact(const SmallPairArgs &a, const OutView &out, uint64_t *rbegin, uint32_t *xpos,
+                               uint64_t *total, hipStream_t st);
 
 // ---- wide.hip: per-key reduction outputs (one 8 KiB slot per active key q)
 struct WideOut {

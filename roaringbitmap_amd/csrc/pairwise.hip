@@ -116,6 +116,21 @@ __global__ __launch_bounds__(kPairThreads) void k_max_span(const uint64_t *begin
   if ((threadIdx.x & 63) == 0 && m) atomicMax((unsigned long long *)out, (unsigned long long)m);
 }
 
+// largest run count of the Run containers, atomicMax into *out (zeroed)
+__global__ __launch_bounds__(kPairThreads) void k_max_runs(const uint8_t *type, const uint16_t *nruns, uint64_t n,
+                                                          uint64_t *out) {
+  uint32_t m = 0;
+  for (uint64_t i = (uint64_t)blockIdx.x * kPairThreads + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kPairThreads)
+    if (type[i] == kRun) m = max(m, (uint32_t)nruns[i]);
+  m = wave_max_u32(m);
+  if ((threadIdx.x & 63) == 0 && m) atomicMax((unsigned long long *)out, (unsigned long long)m);
+}
+void launch_max_runs(const uint8_t *type, const uint16_t *nruns, uint64_t n, uint64_t *out, hipStream_t st) {
+  if (!n) return;
+  const unsigned blocks = (unsigned)std::min<uint64_t>((n + kPairThreads - 1) / kPairThreads, 1024);
+  k_max_runs<<<blocks, kPairThreads, 0, st>>>(type, nruns, n, out);
+}
+
 // inb[0]: key bytes, inb[1]: light-task input bytes, inb[2]: heavy-task input bytes
 template <bool EMIT>
 __device__ __forceinline__ void pair_walk(const PairArgs &a, uint64_t sg, PairCounts &n, uint64_t (&inb)[3],
@@ -979,6 +994,239 @@ void launch_compact_write(const uint64_t *task_begin, uint64_t nseg, const TaskM
   if (!nseg) return;
   k_compact_write<<<blocks_for(nseg, kPairThreads), kPairThreads, 0, st>>>(task_begin, nseg, tm, rbegin, out,
                                                                            seg_pair, pair_card, stats);
+}
+
+// ---------------------------------------------------------------- small batches: two launches
+// A call of a few thousand pairs (config 1: 199 census pairs) is bound by launch and host-sync
+// latency, not by bytes: the general pipeline's ~15 launches and two host read-backs cost ~150 us.
+// Here ONE kernel does everything per pair (a block per pair: key alignment in LDS, then its 4 waves
+// take the merged keys — unmatched copies and every matched pair through the register path, so the
+// result types are the register path's, which the general pipeline also uses) into one 8 KiB slot
+// per merged key, and one single-block kernel compacts the slots into the result CSR.
+__device__ __forceinline__ uint32_t lower_bound_u16(const uint16_t *k, uint32_t n, uint32_t x) {
+  uint32_t lo = 0, hi = n;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (k[mid] < x) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+// exclusive block-wide prefix of v (blockDim.x a multiple of 64, <= 1024); *total = the sum
+__device__ __forceinline__ uint32_t block_xscan(uint32_t v, uint32_t *wtot, uint32_t &total) {
+  const int lane = lane_id(), w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const uint32_t inc = wave_scan_u32(v, lane);
+  if (lane == 63) wtot[w] = inc;
+  __syncthreads();
+  uint32_t before = 0;
+  total = 0;
+  for (int i = 0; i < nw; ++i) {
+    const uint32_t t = wtot[i];
+    if (i < w) before += t;
+    total += t;
+  }
+  __syncthreads();
+  return before + inc - v;
+}
+
+template <int OP, bool CARD_ONLY>
+__global__ __launch_bounds__(256) void k_pair_small(SmallPairArgs a, uint64_t *stats) {
+  __shared__ uint16_t K[kSmallPairKeys];  // A's keys, then B's
+  __shared__ uint32_t ent[kSmallPairKeys]; // merged key: A index | B index << 16 (0xFFFF: absent)
+  __shared__ uint16_t mpref[kSmallPairKeys + 1]; // matched keys among A[0, i)
+  __shared__ uint32_t wtot[4];
+  __shared__ __attribute__((aligned(16))) uint32_t lds[4][2048];
+  const int lane = lane_id(), wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  // blockIdx.y of gridDim.y blocks of pair blockIdx.x: each aligns the keys (cheap) and takes every
+  // gridDim.y-th group of 4 merged keys, so a pair's keys spread over 4 * gridDim.y waves
+  const uint32_t p = blockIdx.x, sub = blockIdx.y, nsub = gridDim.y;
+  const uint32_t ai = a.aidx ? a.aidx[p] : p, bi = a.bidx ? a.bidx[p] : p;
+  const uint64_t i0 = a.A.begin[ai], j0 = a.B.begin[bi];
+  const uint32_t na = (uint32_t)(a.A.begin[ai + 1] - i0), nb = (uint32_t)(a.B.begin[bi + 1] - j0);
+  for (uint32_t t = threadIdx.x; t < na; t += 256) K[t] = a.A.key[i0 + t];
+  for (uint32_t t = threadIdx.x; t < nb; t += 256) K[na + t] = a.B.key[j0 + t];
+  __syncthreads();
+  const uint16_t *KA = K, *KB = K + na;
+  // ---- merged key order (RoaringBitmap.and/or/xor/andNot key loops, RoaringBitmap.java:377-473,
+  //      860-902, 1071-1118): A[i] lands at i + #B below it - #matches below it
+  const uint32_t per = (na + 255) >> 8, lo = min(threadIdx.x * per, na), hi = min(lo + per, na);
+  uint32_t cnt = 0;
+  for (uint32_t i = lo; i < hi; ++i) {
+    const uint32_t lb = lower_bound_u16(KB, nb, KA[i]);
+    cnt += lb < nb && KB[lb] == KA[i];
+  }
+  uint32_t matches;
+  uint32_t base = block_xscan(cnt, wtot, matches);
+  for (uint32_t i = lo; i < hi; ++i) {
+    const uint32_t lb = lower_bound_u16(KB, nb, KA[i]);
+    const bool m = lb < nb && KB[lb] == KA[i];
+    mpref[i] = (uint16_t)base;
+    ent[i + lb - base] = i | ((m ? lb : 0xFFFFu) << 16);
+    base += m;
+  }
+  if (threadIdx.x == 0) mpref[na] = (uint16_t)matches;
+  __syncthreads();
+  for (uint32_t j = threadIdx.x; j < nb; j += 256) {
+    const uint32_t la = lower_bound_u16(KA, na, KB[j]);
+    if (la < na && KA[la] == KB[j]) continue;
+    ent[j + la - mpref[la]] = 0xFFFFu | (j << 16);
+  }
+  __syncthreads();
+  const uint32_t nu = na + nb - matches;
+  // ---- one wave per merged key
+  uint32_t *s = lds[wv];
+  const uint64_t slot0 = a.slot[p];
+  const uint64_t keyb = sub == 0 && wv == 0 && lane == 0 ? 2ull * (na + nb) : 0ull;
+  uint64_t inb = keyb, outb = 0, csum = 0;
+  for (uint32_t e = 4 * sub + wv; e < nu; e += 4 * nsub) {
+    const uint32_t en = ent[e], ia = en & 0xFFFF, ib = en >> 16;
+    const bool has_a = ia != 0xFFFFu, has_b = ib != 0xFFFFu;
+    const uint64_t slot = slot0 + e;
+    uint8_t *dst = a.arena + slot * kBitmapBytes;
+    int ty = kEmpty, c = 0, nr = 0;
+    if (has_a && has_b) {
+      const uint64_t xa = i0 + ia, xb = j0 + ib;
+      const int ta = a.A.type[xa], tb = a.B.type[xb];
+      const uint32_t ca = a.A.card[xa], cb = a.B.card[xb], ra = a.A.nruns[xa], rb = a.B.nruns[xb];
+      const uint8_t *pa = a.A.payload + a.A.off[xa], *pb = a.B.payload + a.B.off[xb];
+      const uint32_t ba = (uint32_t)payload_bytes(ta, ca, ra), bb = (uint32_t)payload_bytes(tb, cb, rb);
+      if (lane == 0) inb += alg_bytes(ta, ca, ra) + alg_bytes(tb, cb, rb) + 32;
+      uint64_t w[kW];
+      uint4 q[8];
+      if (ta == kBitmap) {
+        load_bitmap(pa, w, lane);
+      } else {
+        if (ba > (uint32_t)kBitmapBytes) stage_big_runs(pa, ra, s, lane);
+        else {
+          load_chunks(q, pa, ba, lane);
+          stage_from_chunks(ta, q, ca, ra, s, lane);
+        }
+        lds_read_words(s, w, lane);
+        wave_lds_sync();
+      }
+      if (tb == kBitmap) {
+        load_chunks(q, pb, kBitmapBytes, lane);
+      } else {
+        if (bb > (uint32_t)kBitmapBytes) stage_big_runs(pb, rb, s, lane);
+        else {
+          load_chunks(q, pb, bb, lane);
+          stage_from_chunks(tb, q, cb, rb, s, lane);
+        }
+        const uint4 *s4 = reinterpret_cast<const uint4 *>(s);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) q[k] = s4[k * 64 + lane];
+        wave_lds_sync();
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        word_op<OP>(w[2 * k], pack2(q[k].x, q[k].y));
+        word_op<OP>(w[2 * k + 1], pack2(q[k].z, q[k].w));
+      }
+      const bool eff = eff_rule<OP>(ta, tb, ca, cb);
+      int r;
+      metrics(w, lane, eff && !CARD_ONLY, c, r);
+      if (OP != RB_OR && c == 0) ty = kEmpty;
+      else if (eff) ty = type_eff(c, r);
+      else if (OP == RB_OR && (ta == kBitmap || tb == kBitmap)) {
+        ty = type_lr(c);
+        if (ty == kRun) r = 1; // LR's Run is the full container: one run
+      } else ty = type_ab(c);
+      if (CARD_ONLY) ty = c ? kArray : kEmpty;
+      else if (ty != kEmpty) emit_container(ty, w, c, r, dst, s, lane);
+      nr = ty == kRun ? r : 0;
+    } else if (has_a ? keeps_a_only(OP) : keeps_b_only(OP)) {
+      // unmatched key: RoaringArray.appendCopy (RoaringArray.java:184-205)
+      const SetView &S = has_a ? a.A : a.B;
+      const uint64_t x = has_a ? i0 + ia : j0 + ib;
+      ty = S.type[x];
+      c = (int)S.card[x];
+      nr = S.nruns[x];
+      if (lane == 0) inb += alg_bytes(ty, (uint32_t)c, (uint32_t)nr) + 16;
+      if (!CARD_ONLY) copy_payload(S.payload + S.off[x], dst, payload_bytes(ty, (uint32_t)c, (uint32_t)nr), lane);
+      if (CARD_ONLY) ty = kArray;
+    }
+    if (lane == 0) {
+      a.skey[slot] = has_a ? KA[ia] : KB[ib];
+      a.stype[slot] = (uint8_t)ty;
+      a.scard[slot] = (uint32_t)c;
+      a.snruns[slot] = (uint16_t)nr;
+      if (ty != kEmpty) {
+        csum += (uint64_t)c;
+        if (!CARD_ONLY) outb += alg_bytes(ty, (uint32_t)c, (uint32_t)nr) + 16;
+      }
+    }
+  }
+  // slots past the merged keys hold nothing
+  if (sub == 0)
+    for (uint64_t t = slot0 + nu + threadIdx.x; t < a.slot[p + 1]; t += 256) a.stype[t] = kEmpty;
+  // stats words: 0 total input (with key arrays), 6 container input, 1 output, 7 result cardinality
+  stat_add(stats, 0, inb);
+  stat_add(stats, 6, inb - keyb);
+  stat_add(stats, 1, outb);
+  stat_add(stats, 7, csum);
+}
+
+// One block: drop the empty slots, write the result SoA and CSR (slot s's payload stays at s * 8 KiB).
+__global__ __launch_bounds__(1024) void k_pair_small_compact(SmallPairArgs a, OutView out, uint64_t *rbegin,
+                                                              uint32_t *xpos, uint64_t *total) {
+  __shared__ uint32_t wtot[16];
+  const uint64_t E = a.slot[a.np];
+  const uint32_t per = (uint32_t)((E + 1023) >> 10);
+  const uint64_t lo = min<uint64_t>((uint64_t)threadIdx.x * per, E), hi = min<uint64_t>(lo + per, E);
+  uint32_t cnt = 0;
+  for (uint64_t t = lo; t < hi; ++t) cnt += a.stype[t] != kEmpty;
+  uint32_t tot;
+  uint32_t r = block_xscan(cnt, wtot, tot);
+  for (uint64_t t = lo; t < hi; ++t) {
+    xpos[t] = r;
+    if (a.stype[t] == kEmpty) continue;
+    if (out.key) {
+      out.key[r] = a.skey[t];
+      out.type[r] = a.stype[t];
+      out.card[r] = a.scard[t];
+      out.nruns[r] = a.snruns[t];
+      out.off[r] = t * kBitmapBytes;
+    }
+    ++r;
+  }
+  __syncthreads();
+  if (rbegin)
+    for (uint32_t p = threadIdx.x; p <= a.np; p += 1024) {
+      const uint64_t t = a.slot[p];
+      rbegin[p] = t < E ? xpos[t] : tot;
+    }
+  if (a.pcard) // per-pair result cardinality (RoaringBitmap.andCardinality etc.)
+    for (uint32_t p = threadIdx.x; p < a.np; p += 1024) {
+      uint64_t c = 0;
+      for (uint64_t t = a.slot[p]; t < a.slot[p + 1]; ++t)
+        if (a.stype[t] != kEmpty) c += a.scard[t];
+      a.pcard[p] = c;
+    }
+  if (threadIdx.x == 0) *total = tot;
+}
+
+template <int OP>
+static void launch_small_op(bool card_only, const SmallPairArgs &a, unsigned nsub, uint64_t *stats, hipStream_t st) {
+  const dim3 grid(a.np, nsub);
+  if (card_only) k_pair_small<OP, true><<<grid, 256, 0, st>>>(a, stats);
+  else k_pair_small<OP, false><<<grid, 256, 0, st>>>(a, stats);
+}
+void launch_pair_small(int op, bool card_only, const SmallPairArgs &a, uint32_t max_keys, uint64_t *stats,
+                       hipStream_t st) {
+  if (!a.np) return;
+  // enough blocks per pair that a wave takes ~2 merged keys, while the grid stays a few waves per CU
+  unsigned nsub = (max_keys + 7) / 8;
+  nsub = std::max(1u, std::min(nsub, std::max(1u, 4096u / a.np)));
+  switch (op) {
+  case RB_AND: launch_small_op<RB_AND>(card_only, a, nsub, stats, st); break;
+  case RB_OR: launch_small_op<RB_OR>(card_only, a, nsub, stats, st); break;
+  case RB_XOR: launch_small_op<RB_XOR>(card_only, a, nsub, stats, st); break;
+  default: launch_small_op<RB_ANDNOT>(card_only, a, nsub, stats, st); break;
+  }
+}
+void launch_pair_small_compact(const SmallPairArgs &a, const OutView &out, uint64_t *rbegin, uint32_t *xpos,
+                               uint64_t *total, hipStream_t st) {
+  k_pair_small_compact<<<1, 1024, 0, st>>>(a, out, rbegin, xpos, total);
 }
 
 } // namespace rbg

@@ -427,6 +427,88 @@ class Context:
         return int(out.value)
 
 
+def _summary(s: L.RbShardSummary) -> dict:
+    return {k: int(getattr(s, k)) for k, _ in L.RbShardSummary._fields_}
+
+
+class Comm:
+    """The library's RCCL communicator (rbgpu_comm): one rank per GPU; the shard exchange of the
+    key-range-sharded aggregations runs inside librbgpu (include/rbgpu.h, multi-GPU section)."""
+
+    @staticmethod
+    def unique_id() -> bytes:
+        buf = C.create_string_buffer(L.COMM_ID_BYTES)
+        L.check(L.lib().rbgpu_comm_unique_id(buf))
+        return buf.raw
+
+    def __init__(self, ctx: "Context", uid: bytes, nranks: int, rank: int):
+        if len(uid) != L.COMM_ID_BYTES:
+            raise ValueError("communicator id must be 128 bytes")
+        h = C.c_void_p()
+        L.check(L.lib().rbgpu_comm_init(ctx.h, C.create_string_buffer(uid, L.COMM_ID_BYTES), nranks, rank,
+                                        C.byref(h)))
+        self.h, self.ctx, self.nranks, self.rank = h, ctx, nranks, rank
+
+    def close(self):
+        if self.h and self.h.value:
+            L.lib().rbgpu_comm_destroy(self.h)
+            self.h = None
+
+    def allreduce_sum(self, values) -> np.ndarray:
+        v = np.ascontiguousarray(np.asarray(values, dtype=np.uint64)).copy()
+        L.check(L.lib().rbgpu_comm_allreduce_sum(self.h, v.ctypes.data_as(L._U64P), len(v)))
+        return v
+
+    def summarize(self, local: DeviceSet) -> dict:
+        s = L.RbShardSummary()
+        L.check(L.lib().rbgpu_shard_summarize(self.h, local.h, C.byref(s)))
+        return _summary(s)
+
+    def wide_sharded(self, sem: int, s: DeviceSet, key_range, members=None):
+        mi, mp = _idx(members)
+        n = len(mi) if mi is not None else len(s)
+        out, summ = C.c_void_p(), L.RbShardSummary()
+        L.check(L.lib().rbgpu_wide_sharded(self.h, sem, s.h, mp, n, int(key_range[0]), int(key_range[1]),
+                                           C.byref(out), C.byref(summ)))
+        return DeviceSet(self.ctx, out.value), _summary(summ)
+
+    def bsi_compare_sharded(self, op: int, bsi: DeviceSet, start: int, end: int, min_value: int, max_value: int,
+                            key_range, found: Optional[DeviceSet] = None):
+        out, summ = C.c_void_p(), L.RbShardSummary()
+        m = 2**64 - 1
+        L.check(L.lib().rbgpu_bsi_compare_sharded(self.h, bsi.h, op, start & m, end & m, min_value & m, max_value & m,
+                                                  found.h if found is not None else None, int(key_range[0]),
+                                                  int(key_range[1]), C.byref(out), C.byref(summ)))
+        return DeviceSet(self.ctx, out.value), _summary(summ)
+
+    def gather_serialized(self, local: DeviceSet, summary: dict, root: int = 0) -> Optional[bytes]:
+        """The whole result's RoaringFormatSpec bytes on `root` (None elsewhere), assembled on the
+        root's GPU (rbgpu_shard_gather_serialized); the device buffer is a torch uint8 tensor."""
+        import torch
+        s = L.RbShardSummary(**summary)
+        n = int(summary["serialized_size"]) if self.rank == root else 0
+        buf = torch.empty(max(n, 16), dtype=torch.uint8, device=torch.device("cuda", self.ctx.device))
+        L.check(L.lib().rbgpu_shard_gather_serialized(self.h, local.h, C.byref(s), root, C.c_void_p(buf.data_ptr()),
+                                                      buf.numel()))
+        if self.rank != root:
+            return None
+        return bytes(buf[:n].cpu().numpy().tobytes())
+
+
+def assemble_host(parts: Sequence[bytes]) -> bytes:
+    """rbgpu_shard_assemble_host: the whole bitmap's bytes from its key-ordered shards' bytes (the
+    header assembly the device gather runs, on the CPU)."""
+    n = len(parts)
+    arr = (C.c_char_p * max(n, 1))(*parts)
+    lens = np.array([len(p) for p in parts] or [0], np.uint64)
+    written = C.c_uint64()
+    L.lib().rbgpu_shard_assemble_host(arr, lens.ctypes.data_as(L._U64P), n, None, 0, C.byref(written))
+    out = C.create_string_buffer(max(int(written.value), 1))
+    L.check(L.lib().rbgpu_shard_assemble_host(arr, lens.ctypes.data_as(L._U64P), n, out, int(written.value),
+                                              C.byref(written)))
+    return out.raw[:int(written.value)]
+
+
 _default: Optional[Context] = None
 
 

@@ -1,5 +1,7 @@
 """Parity of the MI355X pairwise path (librbgpu k_pairwise) with the oracle: identical
-RoaringFormatSpec bytes for every result, identical cardinalities."""
+RoaringFormatSpec bytes for every result, identical cardinalities.  Every test runs twice: batches of
+<= 4096 pairs through the two-launch small-batch path (k_pair_small), and with RBGPU_NO_SMALL_PAIRS=1
+through the general pipeline (merge-path segments, light / heavy task kernels)."""
 import numpy as np
 import pytest
 
@@ -8,6 +10,12 @@ from datasets import (DATASETS, EXPECTED, fixture_bytes, load_realdata, ornot_fu
 
 pytestmark = pytest.mark.gpu
 OPS = {"AND": 0, "OR": 1, "XOR": 2, "ANDNOT": 3}
+
+
+@pytest.fixture(autouse=True, params=["small", "general"])
+def pair_path(request, monkeypatch):
+    monkeypatch.setenv("RBGPU_NO_SMALL_PAIRS", "1" if request.param == "general" else "0")
+    return request.param
 
 
 def _ref_list(oracle, blobs):

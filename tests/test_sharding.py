@@ -11,7 +11,7 @@ import torch.multiprocessing as mp
 
 from datasets import fixture_bytes, load_realdata, synthetic_bitmaps
 from roaringbitmap_amd import _lib as L
-from roaringbitmap_amd.engine import HostSoA, host_summary, soa_from_serialized
+from roaringbitmap_amd.engine import HostSoA, assemble_host, host_summary, soa_from_serialized
 from roaringbitmap_amd.sharding import (ShardedWide, header_size, pair_bytes, partition_keys, partition_pairs,
                                         serialize_parts)
 
@@ -48,7 +48,25 @@ def test_writer_matches_reference_fixtures():
     # testdata/bitmapwithruns.bin / bitmapwithoutruns.bin (TestAdversarialInputs.java:32-48)
     for name in ("bitmapwithruns.bin", "bitmapwithoutruns.bin"):
         data = fixture_bytes(name)
-        assert serialize_parts([soa_from_serialized([data])]) == data
+        h = soa_from_serialized([data])
+        assert serialize_parts([h]) == data
+        # split at every container boundary region, including shards of < 4 containers with Runs
+        # (no offset table: the assembly walks their payloads) and empty shards
+        nk = len(h.key)
+        for cuts in ([0, nk], [0, 1, nk], [0, 2, 3, nk], [0, 0, nk // 2, nk, nk], [0, nk - 3, nk - 1, nk]):
+            parts = [_subset(h, int(h.key[a]) if a < nk else 65536, int(h.key[b]) if b < nk else 65536)
+                     for a, b in zip(cuts[:-1], cuts[1:])]
+            assert assemble_host([serialize_parts([p]) for p in parts]) == data, cuts
+
+
+def test_assemble_host_edges():
+    empty = serialize_parts([HostSoA(np.zeros(2, np.uint64), np.zeros(0, np.uint16), np.zeros(0, np.uint8),
+                                     np.zeros(0, np.uint32), np.zeros(0, np.uint16), np.zeros(0, np.uint64),
+                                     np.zeros(16, np.uint8))])
+    assert assemble_host([empty, empty]) == empty
+    assert assemble_host([]) == empty
+    with pytest.raises(L.FormatError):
+        assemble_host([b"\x01\x02\x03\x04\x05\x06\x07\x08"])
 
 
 @pytest.mark.parametrize("run_optimize", [False, True])
@@ -65,6 +83,9 @@ def test_split_and_reassemble(oracle, run_optimize):
             np.add.at(kb, h.key.astype(np.int64), 1)
             parts = [_subset(h, lo, hi) for lo, hi in partition_keys(kb, n)]
             assert serialize_parts(parts) == data
+            # the library's gather assembly (rbgpu_shard_assemble_host, the code the root GPU runs)
+            # from each shard's standalone bytes
+            assert assemble_host([serialize_parts([p]) for p in parts]) == data
             s = host_summary(h)
             assert len(data) == header_size(s["n_containers"], s["n_run_containers"] > 0) + s["payload_bytes"]
 
