@@ -96,6 +96,7 @@ typedef struct rb_stats {
   uint64_t kernel_bytes[4];
   uint64_t kernel_items[4];
   uint64_t result_cardinality; /* Σ cardinality of every result bitmap of the call */
+  double call_us;              /* host wall time of the call, entry to return (pairwise calls) */
 } rb_stats;
 
 /* ---- context ---------------------------------------------------------------------- */

@@ -56,6 +56,7 @@ class RbStats(C.Structure):
         ("kernel_bytes", C.c_uint64 * 4),
         ("kernel_items", C.c_uint64 * 4),
         ("result_cardinality", C.c_uint64),
+        ("call_us", C.c_double),
     ]
 
 

@@ -1,6 +1,7 @@
 // api.hip — the C ABI of librbgpu (include/rbgpu.h): contexts, device-resident sets,
 // pairwise / wide set algebra orchestration, serialization, synthetic generation.
 #include <algorithm>
+#include <chrono>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -74,6 +75,7 @@ void ctx_unref(rbgpu_ctx *ctx) {
   (void)hipHostFree(ctx->h_pinned);
   (void)hipHostFree(ctx->h_stats);
   if (ctx->h_stage) (void)hipHostFree(ctx->h_stage);
+  if (ctx->h_small) (void)hipHostFree(ctx->h_small);
   ctx->pool.clear();
   ctx->ws_pairs.destroy();
   ctx->ws_tasks.destroy();
@@ -269,19 +271,26 @@ int set_key_subset(const rbgpu_set *s, uint32_t key_lo, uint32_t key_hi, rbgpu_s
   return upload_host(s->ctx, r, out);
 }
 
-void stats_begin(rbgpu_ctx *ctx) {
-  (void)hipMemsetAsync(ctx->d_stats, 0, kStatWords * kStripes * sizeof(uint64_t), ctx->stream);
+void stats_begin(rbgpu_ctx *ctx, bool zero) {
+  if (zero) (void)hipMemsetAsync(ctx->d_stats, 0, kStatWords * kStripes * sizeof(uint64_t), ctx->stream);
   (void)hipEventRecord(ctx->ev[0], ctx->stream);
 }
-int stats_end(rbgpu_ctx *ctx, uint64_t tasks, uint64_t result_containers, const KernelSpan *k, int n) {
+int stats_end(rbgpu_ctx *ctx, uint64_t tasks, uint64_t result_containers, const KernelSpan *k, int n,
+              const uint64_t *d_src) {
   HIPCHK(hipEventRecord(ctx->ev[5], ctx->stream));
-  HIPCHK(hipMemcpyAsync(ctx->h_stats, ctx->d_stats, kStatWords * kStripes * sizeof(uint64_t), hipMemcpyDeviceToHost,
-                        ctx->stream));
+  HIPCHK(hipMemcpyAsync(ctx->h_stats, d_src ? d_src : ctx->d_stats, kStatWords * kStripes * sizeof(uint64_t),
+                        hipMemcpyDeviceToHost, ctx->stream));
   HIPCHK(hipStreamSynchronize(ctx->stream));
   LAUNCHCHK();
-  uint64_t w[kStatWords] = {};
-  for (int i = 0; i < kStatWords; ++i)
+  uint64_t *w = ctx->words;
+  for (int i = 0; i < kStatWords; ++i) {
+    w[i] = 0;
     for (int j = 0; j < kStripes; ++j) w[i] += ctx->h_stats[i * kStripes + j];
+  }
+  return stats_fill(ctx, tasks, result_containers, k, n);
+}
+int stats_fill(rbgpu_ctx *ctx, uint64_t tasks, uint64_t result_containers, const KernelSpan *k, int n) {
+  const uint64_t *w = ctx->words;
   rb_stats &s = ctx->last;
   s = rb_stats{};
   s.tasks = tasks;
@@ -683,17 +692,26 @@ static int pairwise_small(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgp
   int rc = ensure_h_begin(a);
   if (!rc) rc = ensure_h_begin(b);
   if (rc) return rc;
-  // staging blob (host pinned and device): slot[np + 1] (u64), then a_idx[np], b_idx[np] (u32)
-  const size_t nslot = 8 * (np + 1ull), nidx = 4ull * np * ((a_idx != nullptr) + (b_idx != nullptr));
-  const size_t blob = nslot + nidx;
-  if (blob > ctx->h_stage_cap) {
-    if (ctx->h_stage) (void)hipHostFree(ctx->h_stage);
-    ctx->h_stage = nullptr;
-    ctx->h_stage_cap = 0;
-    if (hipHostMalloc((void **)&ctx->h_stage, blob) != hipSuccess) return fail(RB_ENOMEM, "pinned staging");
-    ctx->h_stage_cap = blob;
+  // host memory the kernels read / write in place (no copy engine on the call's path): 8 result
+  // words, slot[np + 1] (u64), then a_idx[np], b_idx[np] (u32)
+  const size_t nout = 64, nslot = 8 * (np + 1ull), nidx = 4ull * np * ((a_idx != nullptr) + (b_idx != nullptr));
+  const size_t blob = nout + nslot + nidx;
+  if (blob > ctx->h_small_cap) {
+    if (ctx->h_small) (void)hipHostFree(ctx->h_small);
+    ctx->h_small = ctx->d_small = nullptr;
+    ctx->h_small_cap = 0;
+    const size_t cap = std::max<size_t>(blob, 64 * 1024);
+    if (hipHostMalloc((void **)&ctx->h_small, cap, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
+      return fail(RB_ENOMEM, "host-visible staging");
+    if (hipHostGetDevicePointer((void **)&ctx->d_small, ctx->h_small, 0) != hipSuccess) {
+      (void)hipHostFree(ctx->h_small);
+      ctx->h_small = nullptr;
+      return fail(RB_EDEVICE, "host-visible staging has no device address");
+    }
+    ctx->h_small_cap = cap;
   }
-  uint64_t *slot = reinterpret_cast<uint64_t *>(ctx->h_stage), acc = 0;
+  uint64_t *hout = reinterpret_cast<uint64_t *>(ctx->h_small);
+  uint64_t *slot = reinterpret_cast<uint64_t *>(ctx->h_small + nout), acc = 0;
   uint32_t max_keys = 0;
   for (uint32_t p = 0; p < np; ++p) {
     const uint32_t ai = a_idx ? a_idx[p] : p, bi = b_idx ? b_idx[p] : p;
@@ -710,34 +728,35 @@ static int pairwise_small(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgp
   if (rc) return rc;
   if (a->max_runs > 2048 || b->max_runs > 2048) return 1; // a copy would not fit its 8 KiB slot
   const uint64_t E = acc;
-  uint8_t *hp = ctx->h_stage + nslot;
+  uint8_t *hp = ctx->h_small + nout + nslot;
   if (a_idx) std::memcpy(hp, a_idx, 4ull * np), hp += 4ull * np;
   if (b_idx) std::memcpy(hp, b_idx, 4ull * np);
 
   hipStream_t st = ctx->stream;
   const bool card_only = out == nullptr;
   const uint64_t E1 = std::max<uint64_t>(E, 1);
-  const size_t need = aligned256(blob) + aligned256(8ull * np) + aligned256(4 * E1) + aligned256(2 * E1) +
-                      aligned256(E1) + aligned256(4 * E1) + aligned256(2 * E1) + aligned256(8) + 256;
+  const uint32_t nblocks = np * small_pair_blocks(np, max_keys);
+  const size_t need = aligned256(8ull * np) + aligned256(4 * E1) + aligned256(2 * E1) + aligned256(E1 + 32) +
+                      aligned256(4 * E1) + aligned256(2 * E1) + aligned256(32ull * nblocks) +
+                      aligned256(8ull * (np + 1)) + 256;
   if (ctx->ws_pairs.reserve(need, st) != hipSuccess) return fail(RB_ENOMEM, "pair workspace");
   Workspace &W = ctx->ws_pairs;
-  uint8_t *d_blob = W.take<uint8_t>(blob);
   SmallPairArgs sa{};
   sa.A = a->view();
   sa.B = b->view();
-  sa.slot = reinterpret_cast<const uint64_t *>(d_blob);
-  const uint32_t *d_idx = reinterpret_cast<const uint32_t *>(d_blob + nslot);
+  sa.slot = reinterpret_cast<const uint64_t *>(ctx->d_small + nout);
+  const uint32_t *d_idx = reinterpret_cast<const uint32_t *>(ctx->d_small + nout + nslot);
   sa.aidx = a_idx ? d_idx : nullptr;
   sa.bidx = b_idx ? d_idx + (a_idx ? np : 0) : nullptr;
   sa.np = np;
   sa.pcard = card_out ? W.take<uint64_t>(np) : nullptr;
   uint32_t *xpos = W.take<uint32_t>(E1);
   sa.skey = W.take<uint16_t>(E1);
-  sa.stype = W.take<uint8_t>(E1);
+  sa.stype = W.take<uint8_t>(E1 + 32); // + 32: the compaction reads type bytes 8 at a time
   sa.scard = W.take<uint32_t>(E1);
   sa.snruns = W.take<uint16_t>(E1);
-  uint64_t *d_total = W.take<uint64_t>(1);
-  HIPCHK(hipMemcpyAsync(d_blob, ctx->h_stage, blob, hipMemcpyHostToDevice, st));
+  sa.bstat = W.take<uint64_t>(4ull * nblocks);
+  sa.dslot = W.take<uint64_t>(np + 1ull);
 
   rbgpu_set *res = nullptr;
   if (!card_only) {
@@ -749,23 +768,35 @@ static int pairwise_small(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgp
     }
     sa.arena = res->payload;
   }
-  stats_begin(ctx);
+  stats_begin(ctx, false);
   HIPCHK(hipEventRecord(ctx->ev[1], st));
-  launch_pair_small(op, card_only, sa, max_keys, ctx->d_stats, st);
+  launch_pair_small(op, card_only, sa, max_keys, st);
   HIPCHK(hipEventRecord(ctx->ev[2], st));
   OutView ov{};
   if (res) ov = OutView{res->key, res->type, res->card, res->nruns, res->off};
-  launch_pair_small_compact(sa, ov, res ? res->begin : nullptr, xpos, d_total, st);
+  launch_pair_small_compact(sa, (uint32_t)E, nblocks, ov, res ? res->begin : nullptr, xpos,
+                            reinterpret_cast<uint64_t *>(ctx->d_small), st);
   HIPCHK(hipEventRecord(ctx->ev[3], st));
-  HIPCHK(hipMemcpyAsync(ctx->h_pinned + 5, d_total, 8, hipMemcpyDeviceToHost, st));
   if (card_out) HIPCHK(hipMemcpyAsync(card_out, sa.pcard, 8ull * np, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipEventRecord(ctx->ev[5], st));
+  if (hipStreamSynchronize(st) != hipSuccess || hipGetLastError() != hipSuccess) {
+    if (res) rbgpu_set_free(res);
+    return fail(RB_EDEVICE, "small-batch pairwise kernels failed");
+  }
+  // the result words, written by the compaction kernel straight into host memory
+  uint64_t *w = ctx->words;
+  for (int i = 0; i < kStatWords; ++i) w[i] = 0;
+  w[0] = hout[1];           // input bytes with key arrays
+  w[6] = hout[1] - hout[2]; // container input bytes
+  w[1] = hout[3];           // output bytes
+  w[7] = hout[4];           // result cardinality
+  const uint64_t nres = hout[0];
   const KernelSpan spans[2] = {{"k_pair_small", 6, 1, E}, {"k_pair_small_compact", -1, -1, E}};
-  rc = stats_end(ctx, E, 0, spans, 2);
+  rc = stats_fill(ctx, E, nres, spans, 2);
   if (rc) {
     if (res) rbgpu_set_free(res);
     return rc;
   }
-  const uint64_t nres = ctx->h_pinned[5];
   ctx->last.result_containers = nres;
   if (res) {
     res->nc = nres;
@@ -993,17 +1024,27 @@ static int pairwise_impl(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu
   return RB_OK;
 }
 
+static double us_since(std::chrono::steady_clock::time_point t0) {
+  return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+}
+
 int rbgpu_pairwise(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu_set *b, const uint32_t *a_idx,
                    const uint32_t *b_idx, uint32_t npairs, rbgpu_set **out) {
+  const auto t0 = std::chrono::steady_clock::now();
   if (!out) return fail(RB_EINVAL, "null out");
   *out = nullptr;
-  return pairwise_impl(ctx, op, a, b, a_idx, b_idx, npairs, out, nullptr);
+  const int rc = pairwise_impl(ctx, op, a, b, a_idx, b_idx, npairs, out, nullptr);
+  if (!rc) ctx->last.call_us = us_since(t0);
+  return rc;
 }
 
 int rbgpu_pairwise_cardinality(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu_set *b, const uint32_t *a_idx,
                                const uint32_t *b_idx, uint32_t npairs, uint64_t *out) {
+  const auto t0 = std::chrono::steady_clock::now();
   if (!out && npairs) return fail(RB_EINVAL, "null out");
-  return pairwise_impl(ctx, op, a, b, a_idx, b_idx, npairs, nullptr, out);
+  const int rc = pairwise_impl(ctx, op, a, b, a_idx, b_idx, npairs, nullptr, out);
+  if (!rc) ctx->last.call_us = us_since(t0);
+  return rc;
 }
 
 // Measurement hook (not part of rbgpu.h): runs the pairwise setup, then a read-only probe kernel

@@ -48,7 +48,9 @@ __host__ __device__ inline uint32_t desc_type(uint32_t d) { return d & 3; }
 __host__ __device__ inline uint32_t desc_card(uint32_t d) { return d >> 2; }
 
 // Striped accounting counters (stats word w, stripe s): d_stats[w * kStripes + s].
-constexpr int kStatWords = 8, kStripes = 64;
+// Word 8 is a per-call result word (the small-batch path's result container count), read back
+// with the counters so the call needs one device-to-host copy.
+constexpr int kStatWords = 9, kStripes = 64;
 
 __host__ __device__ inline uint64_t payload_bytes(int type, uint32_t card, uint32_t nruns) {
   return type == kBitmap ? (uint64_t)kBitmapBytes : type == kArray ? 2ull * card : 4ull * nruns;

@@ -108,7 +108,12 @@ struct rbgpu_ctx {
   uint64_t *h_stats = nullptr;  // [kStatWords * kStripes]
   uint8_t *h_stage = nullptr;   // pinned staging for small host->device arguments (pair indices)
   size_t h_stage_cap = 0;
+  // host memory the GPU reads and writes directly (pinned, mapped, coherent): the small-batch
+  // pairwise call's arguments and result words, so that call needs no copy engine
+  uint8_t *h_small = nullptr, *d_small = nullptr;
+  size_t h_small_cap = 0;
   rb_stats last{};
+  uint64_t words[rbg::kStatWords] = {}; // the last call's counters, summed over stripes
   int refs = 1;                 // the handle + one per live set; destroyed at zero
   bool closed = false;
 };
@@ -138,7 +143,8 @@ int ensure_h_begin(const rbgpu_set *s);
 int ensure_max_keys(const rbgpu_set *s);
 int ensure_max_runs(const rbgpu_set *s);
 // call accounting: zero the byte counters + record the start event / read everything back
-void stats_begin(rbgpu_ctx *ctx);
+// zero = false: the caller's counters come zeroed some other way (the small-batch path's H2D copy)
+void stats_begin(rbgpu_ctx *ctx, bool zero = true);
 // Compute-phase kernels k = 0..n-1 ran between events ev[1+k] and ev[2+k]; their algorithmic
 // bytes are d_stats[in_word[k]] + d_stats[out_word[k]] (-1: none).
 // A span may name its own events (e0, e1) and two more byte words (in2, out2: a concurrent pair).
@@ -149,7 +155,11 @@ struct KernelSpan {
   hipEvent_t e0 = nullptr, e1 = nullptr;
   int in2 = -1, out2 = -1;
 };
-int stats_end(rbgpu_ctx *ctx, uint64_t tasks, uint64_t result_containers, const KernelSpan *k, int n);
+// d_src: the counters (default ctx->d_stats)
+int stats_end(rbgpu_ctx *ctx, uint64_t tasks, uint64_t result_containers, const KernelSpan *k, int n,
+              const uint64_t *d_src = nullptr);
+// stats_end's second half: ctx->words already hold the call's counters and the stream is idle
+int stats_fill(rbgpu_ctx *ctx, uint64_t tasks, uint64_t result_containers, const KernelSpan *k, int n);
 // wide.hip
 // keys outside [key_lo, key_hi) produce no result containers (key-range shard of the aggregation)
 int wide_run(rbgpu_ctx *ctx, int sem, const rbgpu_set *in, const std::vector<uint32_t> &members, uint32_t key_lo,

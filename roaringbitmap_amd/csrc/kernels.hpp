@@ -92,13 +92,16 @@ struct SmallPairArgs {
   uint32_t *scard;
   uint16_t *snruns;
   uint64_t *pcard;             // [np] result cardinality per pair, or null
+  uint64_t *bstat;             // [4 * blocks] per block: input bytes, key-array bytes, output bytes, cardinality
+  uint64_t *dslot;             // [np + 1] device copy of slot (written by the first kernel)
 };
-// max_keys: the most keys of one pair (na + nb), sizes the blocks per pair
-void launch_pair_small(int op, bool card_only, const SmallPairArgs &a, uint32_t max_keys, uint64_t *stats,
-                       hipStream_t st);
-// out.key null: only *total and rbegin; rbegin may be null
-void launch_pair_small_compact(const SmallPairArgs &a, const OutView &out, uint64_t *rbegin, uint32_t *xpos,
-                               uint64_t *total, hipStream_t st);
+// blocks per pair for a batch whose largest pair has max_keys keys (na + nb)
+unsigned small_pair_blocks(uint32_t np, uint32_t max_keys);
+void launch_pair_small(int op, bool card_only, const SmallPairArgs &a, uint32_t max_keys, hipStream_t st);
+// out.key null: only the words and rbegin; rbegin may be null.  hout (host-visible): [0] result
+// containers, [1..4] the summed block counters
+void launch_pair_small_compact(const SmallPairArgs &a, uint32_t E, uint32_t nblocks, const OutView &out,
+                               uint64_t *rbegin, uint32_t *xpos, uint64_t *hout, hipStream_t st);
 
 // ---- wide.hip: per-key reduction outputs (one 8 KiB slot per active key q)
 struct WideOut {

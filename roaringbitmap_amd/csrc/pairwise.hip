@@ -1029,27 +1029,36 @@ __device__ __forceinline__ uint32_t block_xscan(uint32_t v, uint32_t *wtot, uint
   return before + inc - v;
 }
 
+// Dynamic LDS of k_pair_small: per wave an 8 KiB scratch, then the merged-key list, the keys and the
+// match prefix, each sized by the batch's largest na + nb (kmax).
+constexpr int kSmallLdsMax = 160 * 1024;
+// (All LDS of the kernel is in the dynamic region, whose base stays 16-B aligned — the 8 KiB scratch
+// takes 16-B accesses.)
+__host__ __device__ inline uint32_t small_lds_bytes(uint32_t waves, uint32_t kmax) {
+  return waves * 8192u + 64u + 4u * kmax + 2u * kmax + 2u * (kmax + 1) + 16u;
+}
 template <int OP, bool CARD_ONLY>
-__global__ __launch_bounds__(256) void k_pair_small(SmallPairArgs a, uint64_t *stats) {
-  __shared__ uint16_t K[kSmallPairKeys];  // A's keys, then B's
-  __shared__ uint32_t ent[kSmallPairKeys]; // merged key: A index | B index << 16 (0xFFFF: absent)
-  __shared__ uint16_t mpref[kSmallPairKeys + 1]; // matched keys among A[0, i)
-  __shared__ uint32_t wtot[4];
-  __shared__ __attribute__((aligned(16))) uint32_t lds[4][2048];
+__global__ __launch_bounds__(256) void k_pair_small(SmallPairArgs a, uint32_t kmax) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t dyn_lds[];
+  const uint32_t nw = blockDim.x >> 6;
+  uint32_t *wtot = reinterpret_cast<uint32_t *>(dyn_lds + nw * 8192u); // [16] block-scan wave totals
+  uint32_t *ent = wtot + 16; // merged key: A index | B index << 16
+  uint16_t *K = reinterpret_cast<uint16_t *>(ent + kmax);             // A's keys, then B's
+  uint16_t *mpref = K + kmax;                                          // matched keys among A[0, i)
   const int lane = lane_id(), wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  // blockIdx.y of gridDim.y blocks of pair blockIdx.x: each aligns the keys (cheap) and takes every
-  // gridDim.y-th group of 4 merged keys, so a pair's keys spread over 4 * gridDim.y waves
-  const uint32_t p = blockIdx.x, sub = blockIdx.y, nsub = gridDim.y;
+  // gridDim.y blocks per pair (blockIdx.x): each aligns the keys (cheap, in LDS) and its waves take
+  // the merged keys e = nw * blockIdx.y + wv, + nw * gridDim.y, ...
+  const uint32_t p = blockIdx.x, nt = blockDim.x, sub = blockIdx.y, nsub = gridDim.y;
   const uint32_t ai = a.aidx ? a.aidx[p] : p, bi = a.bidx ? a.bidx[p] : p;
   const uint64_t i0 = a.A.begin[ai], j0 = a.B.begin[bi];
   const uint32_t na = (uint32_t)(a.A.begin[ai + 1] - i0), nb = (uint32_t)(a.B.begin[bi + 1] - j0);
-  for (uint32_t t = threadIdx.x; t < na; t += 256) K[t] = a.A.key[i0 + t];
-  for (uint32_t t = threadIdx.x; t < nb; t += 256) K[na + t] = a.B.key[j0 + t];
+  for (uint32_t t = threadIdx.x; t < na; t += nt) K[t] = a.A.key[i0 + t];
+  for (uint32_t t = threadIdx.x; t < nb; t += nt) K[na + t] = a.B.key[j0 + t];
   __syncthreads();
   const uint16_t *KA = K, *KB = K + na;
   // ---- merged key order (RoaringBitmap.and/or/xor/andNot key loops, RoaringBitmap.java:377-473,
   //      860-902, 1071-1118): A[i] lands at i + #B below it - #matches below it
-  const uint32_t per = (na + 255) >> 8, lo = min(threadIdx.x * per, na), hi = min(lo + per, na);
+  const uint32_t per = (na + nt - 1) / nt, lo = min(threadIdx.x * per, na), hi = min(lo + per, na);
   uint32_t cnt = 0;
   for (uint32_t i = lo; i < hi; ++i) {
     const uint32_t lb = lower_bound_u16(KB, nb, KA[i]);
@@ -1066,7 +1075,7 @@ __global__ __launch_bounds__(256) void k_pair_small(SmallPairArgs a, uint64_t *s
   }
   if (threadIdx.x == 0) mpref[na] = (uint16_t)matches;
   __syncthreads();
-  for (uint32_t j = threadIdx.x; j < nb; j += 256) {
+  for (uint32_t j = threadIdx.x; j < nb; j += nt) {
     const uint32_t la = lower_bound_u16(KA, na, KB[j]);
     if (la < na && KA[la] == KB[j]) continue;
     ent[j + la - mpref[la]] = 0xFFFFu | (j << 16);
@@ -1074,11 +1083,15 @@ __global__ __launch_bounds__(256) void k_pair_small(SmallPairArgs a, uint64_t *s
   __syncthreads();
   const uint32_t nu = na + nb - matches;
   // ---- one wave per merged key
-  uint32_t *s = lds[wv];
-  const uint64_t slot0 = a.slot[p];
+  uint32_t *s = reinterpret_cast<uint32_t *>(dyn_lds) + wv * 2048;
+  const uint64_t slot0 = a.slot[p], slot1 = a.slot[p + 1];
+  if (sub == 0 && threadIdx.x == 0) { // a device copy of the slot table for the compaction kernel
+    a.dslot[p] = slot0;
+    if (p + 1 == a.np) a.dslot[p + 1] = slot1;
+  }
   const uint64_t keyb = sub == 0 && wv == 0 && lane == 0 ? 2ull * (na + nb) : 0ull;
   uint64_t inb = keyb, outb = 0, csum = 0;
-  for (uint32_t e = 4 * sub + wv; e < nu; e += 4 * nsub) {
+  for (uint32_t e = nw * sub + wv; e < nu; e += nw * nsub) {
     const uint32_t en = ent[e], ia = en & 0xFFFF, ib = en >> 16;
     const bool has_a = ia != 0xFFFFu, has_b = ib != 0xFFFFu;
     const uint64_t slot = slot0 + e;
@@ -1158,75 +1171,128 @@ __global__ __launch_bounds__(256) void k_pair_small(SmallPairArgs a, uint64_t *s
   }
   // slots past the merged keys hold nothing
   if (sub == 0)
-    for (uint64_t t = slot0 + nu + threadIdx.x; t < a.slot[p + 1]; t += 256) a.stype[t] = kEmpty;
-  // stats words: 0 total input (with key arrays), 6 container input, 1 output, 7 result cardinality
-  stat_add(stats, 0, inb);
-  stat_add(stats, 6, inb - keyb);
-  stat_add(stats, 1, outb);
-  stat_add(stats, 7, csum);
+    for (uint64_t t = slot0 + nu + threadIdx.x; t < slot1; t += nt) a.stype[t] = kEmpty;
+  // the block's counters (input with key arrays, key arrays, output, result cardinality) into its
+  // own record: no atomics and no zeroing before the call; the compaction kernel adds them up
+  uint64_t v[4] = {inb, keyb, outb, csum};
+  __syncthreads(); // wtot is reused below
+  uint64_t *red = reinterpret_cast<uint64_t *>(dyn_lds); // every wave is past its scratch use
+  for (int k = 0; k < 4; ++k) {
+    const uint64_t x = wave_sum_u64(v[k]);
+    if (lane == 0) red[4 * wv + k] = x;
+  }
+  __syncthreads();
+  if (threadIdx.x < 4) {
+    uint64_t x = 0;
+    for (uint32_t w = 0; w < nw; ++w) x += red[4 * w + threadIdx.x];
+    a.bstat[4 * ((uint64_t)p * nsub + sub) + threadIdx.x] = x;
+  }
 }
 
-// One block: drop the empty slots, write the result SoA and CSR (slot s's payload stays at s * 8 KiB).
-__global__ __launch_bounds__(1024) void k_pair_small_compact(SmallPairArgs a, OutView out, uint64_t *rbegin,
-                                                              uint32_t *xpos, uint64_t *total) {
+// One block: drop the empty slots, write the result SoA and CSR (slot s's payload stays at s * 8 KiB),
+// add up the blocks' counters and write the call's result words to host-visible memory.
+__global__ __launch_bounds__(1024) void k_pair_small_compact(SmallPairArgs a, uint32_t E, uint32_t nblocks,
+                                                              OutView out, uint64_t *rbegin, uint32_t *xpos,
+                                                              uint64_t *hout) {
   __shared__ uint32_t wtot[16];
-  const uint64_t E = a.slot[a.np];
-  const uint32_t per = (uint32_t)((E + 1023) >> 10);
-  const uint64_t lo = min<uint64_t>((uint64_t)threadIdx.x * per, E), hi = min<uint64_t>(lo + per, E);
+  __shared__ uint64_t red[16][4];
+  // a thread's slots [lo, hi): a multiple of 8 (E <= kSmallSlots = 32 * 1024), their type bytes in
+  // <= 4 independent 8-B loads
+  const uint32_t per = (((E + 1023) >> 10) + 7) & ~7u;
+  const uint32_t lo = min(threadIdx.x * per, E), hi = min(lo + per, E);
+  uint64_t tw[4] = {0, 0, 0, 0};
+#pragma unroll
+  for (int g = 0; g < 4; ++g)
+    if (8u * g < per && lo + 8u * g < hi) tw[g] = *reinterpret_cast<const uint64_t *>(a.stype + lo + 8u * g);
+  auto type_at = [&](uint32_t t) { // selects, not a dynamically indexed (scratch) array
+    const uint32_t g = (t - lo) >> 3;
+    const uint64_t x = g == 0 ? tw[0] : g == 1 ? tw[1] : g == 2 ? tw[2] : tw[3];
+    return (uint32_t)((x >> (8 * ((t - lo) & 7))) & 0xFF);
+  };
   uint32_t cnt = 0;
-  for (uint64_t t = lo; t < hi; ++t) cnt += a.stype[t] != kEmpty;
+  for (uint32_t t = lo; t < hi; ++t) cnt += type_at(t) != (uint32_t)kEmpty;
   uint32_t tot;
   uint32_t r = block_xscan(cnt, wtot, tot);
-  for (uint64_t t = lo; t < hi; ++t) {
+  for (uint32_t t = lo; t < hi; ++t) {
     xpos[t] = r;
-    if (a.stype[t] == kEmpty) continue;
+    const uint32_t ty = type_at(t);
+    if (ty == (uint32_t)kEmpty) continue;
     if (out.key) {
       out.key[r] = a.skey[t];
-      out.type[r] = a.stype[t];
+      out.type[r] = (uint8_t)ty;
       out.card[r] = a.scard[t];
       out.nruns[r] = a.snruns[t];
-      out.off[r] = t * kBitmapBytes;
+      out.off[r] = (uint64_t)t * kBitmapBytes;
     }
     ++r;
   }
   __syncthreads();
   if (rbegin)
     for (uint32_t p = threadIdx.x; p <= a.np; p += 1024) {
-      const uint64_t t = a.slot[p];
+      const uint64_t t = a.dslot[p];
       rbegin[p] = t < E ? xpos[t] : tot;
     }
   if (a.pcard) // per-pair result cardinality (RoaringBitmap.andCardinality etc.)
     for (uint32_t p = threadIdx.x; p < a.np; p += 1024) {
       uint64_t c = 0;
-      for (uint64_t t = a.slot[p]; t < a.slot[p + 1]; ++t)
+      for (uint64_t t = a.dslot[p]; t < a.dslot[p + 1]; ++t)
         if (a.stype[t] != kEmpty) c += a.scard[t];
       a.pcard[p] = c;
     }
-  if (threadIdx.x == 0) *total = tot;
+  uint64_t v[4] = {0, 0, 0, 0};
+  for (uint32_t b = threadIdx.x; b < nblocks; b += 1024)
+    for (int k = 0; k < 4; ++k) v[k] += a.bstat[4ull * b + k];
+  const int lane = lane_id(), wv = threadIdx.x >> 6;
+  for (int k = 0; k < 4; ++k) {
+    const uint64_t x = wave_sum_u64(v[k]);
+    if (lane == 0) red[wv][k] = x;
+  }
+  __syncthreads();
+  if (threadIdx.x < 4) {
+    uint64_t x = 0;
+    for (int w = 0; w < 16; ++w) x += red[w][threadIdx.x];
+    hout[1 + threadIdx.x] = x;
+  }
+  if (threadIdx.x == 0) hout[0] = tot;
 }
 
 template <int OP>
-static void launch_small_op(bool card_only, const SmallPairArgs &a, unsigned nsub, uint64_t *stats, hipStream_t st) {
+static void launch_small_op(bool card_only, const SmallPairArgs &a, unsigned waves, unsigned nsub, uint32_t kmax,
+                            hipStream_t st) {
+  static bool attr = false; // allow the whole 160 KiB of a CU to one block
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_pair_small<OP, true>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, kSmallLdsMax);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_pair_small<OP, false>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, kSmallLdsMax);
+    attr = true;
+  }
+  const uint32_t lds = small_lds_bytes(waves, kmax);
   const dim3 grid(a.np, nsub);
-  if (card_only) k_pair_small<OP, true><<<grid, 256, 0, st>>>(a, stats);
-  else k_pair_small<OP, false><<<grid, 256, 0, st>>>(a, stats);
+  if (card_only) k_pair_small<OP, true><<<grid, 64 * waves, lds, st>>>(a, kmax);
+  else k_pair_small<OP, false><<<grid, 64 * waves, lds, st>>>(a, kmax);
 }
-void launch_pair_small(int op, bool card_only, const SmallPairArgs &a, uint32_t max_keys, uint64_t *stats,
-                       hipStream_t st) {
+unsigned small_pair_blocks(uint32_t np, uint32_t max_keys) {
+  // The call is latency-bound (a wave's merged keys run one after the other): 4 waves per block and
+  // enough blocks per pair that a wave takes ~1 merged key (measured on census: 10 blocks per pair
+  // 28-51 us, 2 blocks per pair — one resident round — 41-77 us: the per-key latency dominates)
+  const unsigned nsub = std::max(1u, std::min((max_keys + 3) / 4, std::max(1u, 2048u / std::max(np, 1u))));
+  return nsub;
+}
+void launch_pair_small(int op, bool card_only, const SmallPairArgs &a, uint32_t max_keys, hipStream_t st) {
   if (!a.np) return;
-  // enough blocks per pair that a wave takes ~2 merged keys, while the grid stays a few waves per CU
-  unsigned nsub = (max_keys + 7) / 8;
-  nsub = std::max(1u, std::min(nsub, std::max(1u, 4096u / a.np)));
+  const uint32_t kmax = std::max(1u, max_keys);
+  const unsigned waves = 4, nsub = small_pair_blocks(a.np, max_keys);
   switch (op) {
-  case RB_AND: launch_small_op<RB_AND>(card_only, a, nsub, stats, st); break;
-  case RB_OR: launch_small_op<RB_OR>(card_only, a, nsub, stats, st); break;
-  case RB_XOR: launch_small_op<RB_XOR>(card_only, a, nsub, stats, st); break;
-  default: launch_small_op<RB_ANDNOT>(card_only, a, nsub, stats, st); break;
+  case RB_AND: launch_small_op<RB_AND>(card_only, a, waves, nsub, kmax, st); break;
+  case RB_OR: launch_small_op<RB_OR>(card_only, a, waves, nsub, kmax, st); break;
+  case RB_XOR: launch_small_op<RB_XOR>(card_only, a, waves, nsub, kmax, st); break;
+  default: launch_small_op<RB_ANDNOT>(card_only, a, waves, nsub, kmax, st); break;
   }
 }
-void launch_pair_small_compact(const SmallPairArgs &a, const OutView &out, uint64_t *rbegin, uint32_t *xpos,
-                               uint64_t *total, hipStream_t st) {
-  k_pair_small_compact<<<1, 1024, 0, st>>>(a, out, rbegin, xpos, total);
+void launch_pair_small_compact(const SmallPairArgs &a, uint32_t E, uint32_t nblocks, const OutView &out,
+                               uint64_t *rbegin, uint32_t *xpos, uint64_t *hout, hipStream_t st) {
+  k_pair_small_compact<<<1, 1024, 0, st>>>(a, E, nblocks, out, rbegin, xpos, hout);
 }
 
 } // namespace rbg
