@@ -55,9 +55,14 @@ def _traffic_groups(pmc_name):
         return None
     try:
         with open(TRAFFIC_JSON) as f:
-            return json.load(f)["kernels"].get(pmc_name) or None
+            kernels = json.load(f)["kernels"]
     except (OSError, ValueError, KeyError):
         return None
+    if pmc_name in kernels:
+        return kernels[pmc_name] or None
+    # a template instance of the named kernel (e.g. rbg::k_wide_runs_and<16>)
+    hits = [g for k, g in kernels.items() if k.startswith(pmc_name + "<")]
+    return hits[0] if len(hits) == 1 else None
 
 
 def pmc_traffic(pmc_name: str, with_count: bool = False):

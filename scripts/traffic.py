@@ -1,7 +1,7 @@
 """HBM traffic per launch from rocprofv3 PMC passes (MI355X_MICROARCH.md, HBM section):
 FETCH_SIZE and WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE reports half of the bytes of 16-B-per-lane
-streaming reads, so it is doubled (every payload load in librbgpu is a 16-B-per-lane buffer/global
-load); WRITE_SIZE is taken as is.  Writes profiles/<round>/traffic.json keyed by kernel name.
+streaming reads, so it is doubled for the kernels that read that way (STREAM16); WRITE_SIZE is taken
+as is.  Writes profiles/<round>/traffic.json keyed by kernel name.
 
 usage: python scripts/traffic.py <pmc dir with p*/run_counter_collection.csv> <out.json> "<command>"
 """
@@ -12,6 +12,10 @@ import json
 import sys
 
 root, out, cmd = sys.argv[1], sys.argv[2], sys.argv[3]
+# kernels whose payload reads are 16-B-per-lane streaming loads (the calibrated case: FETCH_SIZE x2);
+# every other kernel's FETCH_SIZE is reported raw (a lower bound: its access widths are uncalibrated,
+# MI355X_MICROARCH.md HBM section), with the x2 figure beside it as the upper bound
+STREAM16 = ("k_pair_tasks", "k_wide_reduce", "k_bsi_range", "k_bsi_chain", "k_pair_small<")
 vals = collections.defaultdict(lambda: collections.defaultdict(list))
 for f in sorted(glob.glob(f"{root}/p*/run_counter_collection.csv")):
     for row in csv.DictReader(open(f)):
@@ -22,14 +26,19 @@ res = {}
 for (name, grid), c in vals.items():
     if "FETCH_SIZE" not in c or "WRITE_SIZE" not in c:
         continue
-    fetch = 2.0 * 1024 * sum(c["FETCH_SIZE"]) / len(c["FETCH_SIZE"])
+    raw = 1024.0 * sum(c["FETCH_SIZE"]) / len(c["FETCH_SIZE"])
+    calibrated = any(k in name for k in STREAM16)
+    fetch = 2.0 * raw if calibrated else raw
     write = 1024.0 * sum(c["WRITE_SIZE"]) / len(c["WRITE_SIZE"])
     g = {"grid": grid, "fetch_bytes": int(fetch), "write_bytes": int(write), "traffic_bytes": int(fetch + write),
-         "dispatches": len(c["FETCH_SIZE"])}
+         "dispatches": len(c["FETCH_SIZE"]),
+         "fetch_correction": "x2 (16-B/lane streaming reads)" if calibrated else "raw (uncalibrated widths: lower bound)",
+         "traffic_bytes_x2": int(2.0 * raw + write)}
     res.setdefault(name, []).append(g)
 for name in res:
     res[name].sort(key=lambda g: -g["traffic_bytes"])
-json.dump({"command": cmd, "correction": "FETCH_SIZE x2 (gfx950 16-B/lane reads), KiB->B", "kernels": res},
+json.dump({"command": cmd, "correction": "FETCH_SIZE KiB->B; x2 for the 16-B/lane streaming kernels only "
+                                         "(per-group fetch_correction)", "kernels": res},
           open(out, "w"), indent=1, sort_keys=True)
 for name, gs in res.items():
     print(name, gs[0])
