@@ -81,12 +81,13 @@ def pair_traffic(op, main_name):
     lt = pmc_traffic(f"rbg::k_pair_tasks<{op}, false, 0>", True)
     hv = pmc_traffic(f"rbg::k_pair_tasks<{op}, false, 1>", True)
     if "||" in main_name:
-        # the concurrent phase launches the light kernel twice (beside the heavy kernel, then on the
-        # side stream after it; one task queue): its bytes per phase = all light dispatches' bytes
-        # over the number of phases (= heavy dispatches)
+        # the concurrent phase launches each kernel twice (light beside heavy, then each kind again
+        # once the other has drained; one task queue per kind), so a phase's bytes are all dispatches'
+        # bytes over half the light dispatch count
         if lt is None or hv is None:
             return None
-        return int(lt[0] * lt[1] / max(hv[1], 1)) + hv[0]
+        phases = max(lt[1] // 2, 1)
+        return int((lt[0] * lt[1] + hv[0] * hv[1]) / phases)
     x = lt if "light" in main_name else hv
     return x[0] if x else None
 

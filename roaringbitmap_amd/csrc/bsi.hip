@@ -101,7 +101,7 @@ __global__ __launch_bounds__(256, 2) void k_bsi_chain(SetView bsi, SetView fnd, 
   __shared__ __attribute__((aligned(16))) uint32_t lds[4][2][2048];
   const int lane = lane_id();
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint32_t q = blockIdx.x * 4 + wv;
+  const uint32_t q = xcd_swizzle(blockIdx.x, gridDim.x) * 4 + wv;
   if (q >= nk) return;
   uint32_t *sS = lds[wv][0], *sX = lds[wv][1];
   const uint32_t key = klist[q];
@@ -349,7 +349,7 @@ __global__ __launch_bounds__(128, 2) void k_bsi_range(SetView bsi, SetView fnd, 
   __shared__ __attribute__((aligned(16))) uint32_t lds[2][3][2048];
   const int lane = lane_id();
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint32_t q = blockIdx.x * 2 + wv;
+  const uint32_t q = xcd_swizzle(blockIdx.x, gridDim.x) * 2 + wv;
   if (q >= nk) return;
   uint32_t *sS = lds[wv][0], *sG = lds[wv][1], *sL = lds[wv][2];
   const uint32_t key = klist[q];
@@ -472,7 +472,7 @@ __global__ __launch_bounds__(256) void k_bsi_and(const uint8_t *__restrict__ ga,
   __shared__ __attribute__((aligned(16))) uint32_t lds[4][2048];
   const int lane = lane_id();
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint32_t q = blockIdx.x * 4 + wv;
+  const uint32_t q = xcd_swizzle(blockIdx.x, gridDim.x) * 4 + wv;
   if (q >= nk) return;
   uint32_t *s = lds[wv];
   const int ta = wa.type[q], tb = wb.type[q];

@@ -61,6 +61,23 @@ __device__ __forceinline__ void stat_add(uint64_t *stats, int word, uint64_t v) 
   }
 }
 
+// exclusive block-wide prefix of v (blockDim.x a multiple of 64, <= 1024); *total = the sum
+__device__ __forceinline__ uint32_t block_xscan(uint32_t v, uint32_t *wtot, uint32_t &total) {
+  const int lane = lane_id(), w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const uint32_t inc = wave_scan_u32(v, lane);
+  if (lane == 63) wtot[w] = inc;
+  __syncthreads();
+  uint32_t before = 0;
+  total = 0;
+  for (int i = 0; i < nw; ++i) {
+    const uint32_t t = wtot[i];
+    if (i < w) before += t;
+    total += t;
+  }
+  __syncthreads();
+  return before + inc - v;
+}
+
 // ---------------------------------------------------------------- key alignment by merge path
 // A pair is cut into segments of <= a.seg_keys merged keys (merge path over the two sorted key lists,
 // A first on equal keys), one thread per segment, so a pair of large bitmaps aligns its keys in
@@ -132,9 +149,13 @@ void launch_max_runs(const uint8_t *type, const uint16_t *nruns, uint64_t n, uin
 }
 
 // inb[0]: key bytes, inb[1]: light-task input bytes, inb[2]: heavy-task input bytes
+// sl / sh (EMIT): when non-null, the records go to this block's LDS stage instead (light record x at
+// sl[x - l0], heavy at sh[x - h0]) and the block stores them contiguously afterwards
 template <bool EMIT>
 __device__ __forceinline__ void pair_walk(const PairArgs &a, uint64_t sg, PairCounts &n, uint64_t (&inb)[3],
-                                          const PairBases &base, TaskRec *light, TaskRec *heavy, TaskMeta tm) {
+                                          const PairBases &base, TaskRec *light, TaskRec *heavy, TaskMeta tm,
+                                          TaskRec *sl = nullptr, TaskRec *sh = nullptr, uint64_t l0 = 0,
+                                          uint64_t h0 = 0, uint64_t t0 = 0) {
   const uint32_t p = a.seg_pair[sg];
   uint64_t i0, na, j0, nb;
   pair_ranges(a, p, i0, na, j0, nb);
@@ -163,11 +184,19 @@ __device__ __forceinline__ void pair_walk(const PairArgs &a, uint64_t sg, PairCo
       r.db = ib >= 0 ? ((uint32_t)tb | (a.B.card[ib] << 2)) : kAbsent;
       r.ra = ia >= 0 ? a.A.nruns[ia] : 0;
       r.rb = ib >= 0 ? a.B.nruns[ib] : 0;
-      if (lt) light[base.light + n.light] = r;
-      else heavy[base.heavy + n.heavy] = r;
-      tm.key[t] = key;
-      tm.cat[t] = lt ? 0 : 1;
-      tm.out[t] = r.out;
+      if (lt) {
+        const uint64_t x = base.light + n.light;
+        if (sl) sl[x - l0] = r;
+        else light[x] = r;
+      } else {
+        const uint64_t x = base.heavy + n.heavy;
+        if (sh) sh[x - h0] = r;
+        else heavy[x] = r;
+      }
+      // staged: tm holds the block's LDS arrays, indexed from the block's first task t0
+      tm.key[t - t0] = key;
+      tm.cat[t - t0] = lt ? 0 : 1;
+      tm.out[t - t0] = r.out;
     }
     ++n.task;
     if (lt) ++n.light;
@@ -230,15 +259,49 @@ __global__ __launch_bounds__(kPairThreads) void k_pair_count(PairArgs a, PairCou
   stat_add(stats, 6, inb[1] + inb[2]);
 }
 
+// A block's segments own contiguous ranges of the light and of the heavy record arrays (the scans
+// run in segment order), so its records are staged in LDS and stored as contiguous 8-B-per-lane
+// runs: a thread's own records are 40-B structs at scattered positions, which the store path
+// replays line by line (k_pair_emit measured 189 us per 1M pairs, issue-stall bound).
+constexpr uint32_t kEmitStage = 640; // records (25 KiB); a block with more stores directly
 __global__ __launch_bounds__(kPairThreads) void k_pair_emit(PairArgs a, PairCountArrays scans, uint64_t small_base,
                                                             TaskRec *light, TaskRec *heavy, TaskMeta tm) {
-  const uint64_t p = (uint64_t)blockIdx.x * kPairThreads + threadIdx.x; // segment
-  if (p >= a.nseg) return;
-  PairCounts n{};
-  PairBases b{scans.task[p], scans.light[p], scans.task[p] - scans.light[p], scans.big[p],
-              small_base + scans.small[p]};
-  uint64_t inb[3] = {0, 0, 0};
-  pair_walk<true>(a, p, n, inb, b, light, heavy, tm);
+  __shared__ __attribute__((aligned(16))) TaskRec stage[kEmitStage];
+  __shared__ uint64_t s_out[kEmitStage];
+  __shared__ uint16_t s_key[kEmitStage];
+  __shared__ uint8_t s_cat[kEmitStage];
+  const uint64_t b0 = (uint64_t)blockIdx.x * kPairThreads, be = min(b0 + kPairThreads, a.nseg);
+  const uint64_t p = b0 + threadIdx.x; // segment
+  const uint64_t L0 = scans.light[b0], L1 = scans.light[be], T0 = scans.task[b0], T1 = scans.task[be];
+  const uint64_t H0 = T0 - L0, nl = L1 - L0, nh = (T1 - L1) - H0, nt = T1 - T0;
+  const bool staged = nt <= kEmitStage; // block-uniform
+  if (p < a.nseg) {
+    PairCounts n{};
+    PairBases b{scans.task[p], scans.light[p], scans.task[p] - scans.light[p], scans.big[p],
+                small_base + scans.small[p]};
+    uint64_t inb[3] = {0, 0, 0};
+    if (staged) {
+      TaskMeta sm = tm;
+      sm.key = s_key;
+      sm.cat = s_cat;
+      sm.out = s_out;
+      pair_walk<true>(a, p, n, inb, b, light, heavy, sm, stage, stage + nl, L0, H0, T0);
+    } else {
+      pair_walk<true>(a, p, n, inb, b, light, heavy, tm);
+    }
+  }
+  if (!staged) return;
+  __syncthreads();
+  static_assert(sizeof(TaskRec) == 40, "TaskRec is 5 u64 words");
+  const uint64_t *s64 = reinterpret_cast<const uint64_t *>(stage);
+  uint64_t *l64 = reinterpret_cast<uint64_t *>(light + L0), *h64 = reinterpret_cast<uint64_t *>(heavy + H0);
+  for (uint64_t w = threadIdx.x; w < 5 * nl; w += kPairThreads) l64[w] = s64[w];
+  for (uint64_t w = threadIdx.x; w < 5 * nh; w += kPairThreads) h64[w] = s64[5 * nl + w];
+  for (uint64_t t = threadIdx.x; t < nt; t += kPairThreads) {
+    tm.key[T0 + t] = s_key[t];
+    tm.cat[T0 + t] = s_cat[t];
+    tm.out[T0 + t] = s_out[t];
+  }
 }
 
 // ---------------------------------------------------------------- the per-task kernels
@@ -808,7 +871,35 @@ __global__ __launch_bounds__(kPairThreads) void k_compact_write(const uint64_t *
                                                                 uint64_t *stats) {
   const uint64_t p = (uint64_t)blockIdx.x * kPairThreads + threadIdx.x;
   uint64_t outb[2] = {0, 0}, card_sum = 0;
-  if (p < npairs) {
+  if (!pair_card && out.key) {
+    // A block's segments own the contiguous task range [T0, T1) and result range from rbegin[b0]:
+    // one thread per task, ranked by a block scan, so loads and stores are coalesced (a thread
+    // walking its own segment's tasks is latency-bound).
+    __shared__ uint32_t wtot[4];
+    const uint64_t b0 = (uint64_t)blockIdx.x * kPairThreads, be = min(b0 + kPairThreads, npairs);
+    const uint64_t T0 = tb[b0], T1 = tb[be];
+    uint64_t R = rbegin[b0];
+    for (uint64_t base = T0; base < T1; base += kPairThreads) {
+      const uint64_t t = base + threadIdx.x;
+      const uint8_t ty = t < T1 ? tm.type[t] : (uint8_t)kEmpty;
+      const bool keep = ty != kEmpty;
+      uint32_t tot;
+      const uint32_t rank = block_xscan(keep ? 1u : 0u, wtot, tot);
+      if (keep) {
+        const uint64_t r = R + rank;
+        const uint32_t c = tm.card[t];
+        const uint16_t nr = tm.nruns[t];
+        out.key[r] = tm.key[t];
+        out.type[r] = ty;
+        out.card[r] = c;
+        out.nruns[r] = nr;
+        out.off[r] = tm.out[t];
+        outb[tm.cat[t] ? 1 : 0] += alg_bytes(ty, c, nr) + 16;
+        card_sum += c;
+      }
+      R += tot;
+    }
+  } else if (p < npairs) {
     uint64_t r = rbegin ? rbegin[p] : 0, card = 0;
     for (uint64_t t = tb[p]; t < tb[p + 1]; ++t) {
       const uint8_t ty = tm.type[t];
@@ -1011,22 +1102,6 @@ __device__ __forceinline__ uint32_t lower_bound_u16(const uint16_t *k, uint32_t 
     else hi = mid;
   }
   return lo;
-}
-// exclusive block-wide prefix of v (blockDim.x a multiple of 64, <= 1024); *total = the sum
-__device__ __forceinline__ uint32_t block_xscan(uint32_t v, uint32_t *wtot, uint32_t &total) {
-  const int lane = lane_id(), w = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  const uint32_t inc = wave_scan_u32(v, lane);
-  if (lane == 63) wtot[w] = inc;
-  __syncthreads();
-  uint32_t before = 0;
-  total = 0;
-  for (int i = 0; i < nw; ++i) {
-    const uint32_t t = wtot[i];
-    if (i < w) before += t;
-    total += t;
-  }
-  __syncthreads();
-  return before + inc - v;
 }
 
 // Dynamic LDS of k_pair_small: per wave an 8 KiB scratch, then the merged-key list, the keys and the

@@ -26,6 +26,16 @@ __device__ __forceinline__ void wave_lds_sync() {
 
 __device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & 63); }
 
+// XCD-aware block order (cdna_hip_programming.md §5 T1): blocks b, b+8, b+16, ... share an XCD's L2,
+// so they get consecutive logical indices — neighbouring keys of a wide aggregation then read the
+// same metadata lines (type / card / run-count / offset arrays are member-major: key k and k+1 of a
+// member are adjacent) from one L2 instead of eight.  A bijection on [0, nwg) for any nwg; a pure
+// speed choice (placement is not guaranteed).
+__device__ __forceinline__ uint32_t xcd_swizzle(uint32_t orig, uint32_t nwg) {
+  const uint32_t q = nwg / 8, r = nwg % 8, xcd = orig % 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
+}
+
 // ---- wave collectives on DPP (VALU lane crossbar: no LDS round trip, no bpermute chain).
 // dpp_ctrl: row_shr:n = 0x110+n, wave_shl:1 = 0x130, wave_shr:1 = 0x138, row_bcast:15 = 0x142,
 // row_bcast:31 = 0x143.  Lanes without a source (or in rows masked off) read 0.

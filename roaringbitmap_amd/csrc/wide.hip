@@ -300,7 +300,7 @@ __global__ __launch_bounds__(256) void k_wide_reduce(SetView s, const uint32_t *
   __shared__ __attribute__((aligned(16))) uint32_t lds_all[4][2048];
   const int lane = lane_id();
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint32_t q = blockIdx.x * 4 + wv;
+  const uint32_t q = xcd_swizzle(blockIdx.x, gridDim.x) * 4 + wv;
   if (q >= nk) return;
   if (route && route[q] == 0) return; // done by the Run-list fast path (wide_runs.hip)
   uint32_t *lds = lds_all[wv];

@@ -78,7 +78,7 @@ __global__ __launch_bounds__(256) void k_wide_runs(SetView s, const uint32_t *__
   __shared__ __attribute__((aligned(16))) uint32_t lds_all[4][2048];
   const int lane = lane_id();
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint32_t q = blockIdx.x * 4 + wv;
+  const uint32_t q = xcd_swizzle(blockIdx.x, gridDim.x) * 4 + wv;
   if (q >= nk) return;
   uint32_t *acc = lds_all[wv];
   const uint32_t key = klist[q];
@@ -269,7 +269,7 @@ __global__ __launch_bounds__(256) void k_wide_runs_and(SetView s, const uint32_t
   __shared__ __attribute__((aligned(16))) uint32_t lds_all[4][2 * kAndCap * 64];
   const int lane = lane_id();
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint32_t q0 = (blockIdx.x * 4 + wv) * KB;
+  const uint32_t q0 = (xcd_swizzle(blockIdx.x, gridDim.x) * 4 + wv) * KB;
   if (q0 >= nk) return;
   uint32_t *L = lds_all[wv];
   const int kk = lane % KB, g = lane / KB;

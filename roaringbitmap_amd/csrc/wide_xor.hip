@@ -486,7 +486,7 @@ __global__ __launch_bounds__(256, 3) void k_wide_runs_xor(SetView s, const uint3
   __shared__ __attribute__((aligned(16))) uint32_t reg_all[4][kXRegion];
   const int lane = lane_id();
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint32_t q = blockIdx.x * 4 + wv;
+  const uint32_t q = xcd_swizzle(blockIdx.x, gridDim.x) * 4 + wv;
   if (q >= nk) return;
   // acc: the accumulator P during exact batches, the (zeroed) toggle image of fast-forwards; P itself
   // lives in registers between batches (the 65536-bit register layout of wave.hpp)

@@ -5,5 +5,5 @@ mkdir -p gpurun_out/ab
 while [ $# -ge 2 ]; do
   tag=$1; lib=$2; shift 2
   if [ "$lib" = default ]; then unset RBGPU_LIB; else export RBGPU_LIB=$lib; fi
-  timeout -k 10 200 python -u bench.py --secondary none --census 0 --bsi 0 --no-cpu-baseline > gpurun_out/ab/$tag.json 2> gpurun_out/ab/$tag.err || exit 1
+  timeout -k 10 200 python -u bench.py --secondary none --no-cpu-baseline > gpurun_out/ab/$tag.json 2> gpurun_out/ab/$tag.err || exit 1
 done
