@@ -63,7 +63,15 @@ enum rb_wide_sem {
   RB_FAST_XOR = 4,     /* FastAggregation.xor == naive_xor                   FastAggregation.java:576-582,772 */
   RB_PAR_OR = 5,       /* ParallelAggregation.or                             ParallelAggregation.java:161-175 */
   RB_PAR_XOR = 6,      /* ParallelAggregation.xor                            ParallelAggregation.java:182-195 */
-  RB_NAIVE_AND_ITER = 7 /* FastAggregation.and(Iterator) == naive_and(Iterator) FastAggregation.java:26,304 */
+  RB_NAIVE_AND_ITER = 7, /* FastAggregation.and(Iterator) == naive_and(Iterator) FastAggregation.java:26,304 */
+  /* Global-order semantics: which containers meet, and in which order, follows a priority queue over
+   * all the members (java.util.PriorityQueue ties included), so the order is computed on the host from
+   * the members' keys and cardinalities and the per-key work runs on the device. */
+  RB_HORIZONTAL_OR = 8,  /* FastAggregation.horizontal_or(List / varargs)     FastAggregation.java:124-231 */
+  RB_HORIZONTAL_XOR = 9, /* FastAggregation.horizontal_xor                    FastAggregation.java:243-289 */
+  RB_PQ_XOR = 11         /* FastAggregation.priorityqueue_xor: the two smallest bitmaps (getLongSizeInBytes)
+                            replaced by their RoaringBitmap.xor, on the device, until one is left
+                            FastAggregation.java:732-752 (whole result only: no key range) */
 };
 
 /* Host-side SoA description of a batch of bitmaps (used for upload and download). */
@@ -141,6 +149,7 @@ typedef struct rb_bitmap_summary {
   uint64_t n_containers;
   uint64_t n_run_containers;
   uint64_t payload_bytes; /* serialized container payloads (Run: 2 + 4 * nruns), no header */
+  uint64_t size_in_bytes; /* RoaringBitmap.getLongSizeInBytes (RoaringBitmap.java:2212-2219) */
 } rb_bitmap_summary;
 int rbgpu_set_summaries(const rbgpu_set *set, uint32_t first, uint32_t count, rb_bitmap_summary *out);
 /* Container mix of the whole set, what insights/BitmapAnalyser reports (insights/BitmapAnalyser.java:

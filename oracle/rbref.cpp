@@ -1071,6 +1071,244 @@ BM *wide_par(const BM *const *bs, size_t n, bool is_xor) {
   return out;
 }
 
+// ---- java.util.PriorityQueue (the OpenJDK binary heap the reference's horizontal_* / priorityqueue_*
+// rely on, ties included): offer = append + siftUp, poll = root out, last element sifted down from
+// the root; cmp(a, b) is compareTo / Comparator.compare (< 0, 0, > 0).
+template <class T, class Cmp> struct JavaPQ {
+  std::vector<T> q;
+  Cmp cmp;
+  explicit JavaPQ(Cmp c) : cmp(c) {}
+  bool empty() const { return q.empty(); }
+  size_t size() const { return q.size(); }
+  const T &peek() const { return q[0]; }
+  void offer(const T &x) { // PriorityQueue.siftUpComparable / siftUpUsingComparator
+    size_t k = q.size();
+    q.push_back(x);
+    while (k > 0) {
+      const size_t parent = (k - 1) >> 1;
+      if (cmp(x, q[parent]) >= 0) break;
+      q[k] = q[parent];
+      k = parent;
+    }
+    q[k] = x;
+  }
+  T poll() { // PriorityQueue.poll + siftDownComparable / siftDownUsingComparator
+    T result = q[0];
+    T x = q.back();
+    q.pop_back();
+    const size_t n = q.size();
+    if (n > 0) {
+      size_t k = 0;
+      const size_t half = n >> 1;
+      while (k < half) {
+        size_t child = 2 * k + 1;
+        const size_t right = child + 1;
+        if (right < n && cmp(q[child], q[right]) > 0) child = right;
+        if (cmp(x, q[child]) <= 0) break;
+        q[k] = q[child];
+        k = child;
+      }
+      q[k] = x;
+    }
+    return result;
+  }
+};
+
+// Container.lazyOR (Container.java:751-774): the non-in-place dispatch — Array with Bitmap and Run
+// with Bitmap go to BitmapContainer.lazyor (a lazy Bitmap), Run with Run to RunContainer.or.
+Cont c_lazy_or(const Cont &x, const Cont &y) {
+  auto lazy_bitmap = [](const Cont &b, const Cont &o) { // BitmapContainer.lazyor (:887-918): clone, OR, card -1
+    Cont r = b;
+    r.card = -1;
+    if (o.t == kA) {
+      for (uint16_t v : o.v) r.w[v >> 6] |= 1ull << (v & 63);
+    } else if (o.t == kB) {
+      for (int i = 0; i < kWords; ++i) r.w[i] |= o.w[i];
+    } else {
+      for (int i = 0; i < o.nruns(); ++i) word_range(r.w, o.rs(i), o.rs(i) + o.rl(i) + 1, 0);
+    }
+    return r;
+  };
+  if (x.t == kA) {
+    if (y.t == kA) return c_lazy_ior(x, y);   // ArrayContainer.lazyor (:1449-1464)
+    if (y.t == kB) return lazy_bitmap(y, x);  // ((BitmapContainer) x).lazyor(this)
+    return run_lazy_or_array(y, x);           // ((RunContainer) x).lazyor(this) -> lazyorToRun
+  }
+  if (x.t == kR) {
+    if (y.t == kA) return run_lazy_or_array(x, y);
+    if (y.t == kB) return lazy_bitmap(y, x);
+    return run_or_run(x, y);
+  }
+  return lazy_bitmap(x, y);
+}
+
+// FastAggregation.horizontal_or / horizontal_xor (FastAggregation.java:124-289): a priority queue of
+// ContainerPointers (RoaringArray.getContainerPointer, RoaringArray.java:688-746: ordered by key, then
+// by cardinality descending); per key the first two polled containers are combined (lazyOR / xor), the
+// rest of the key's pointers in poll order folded in place (lazyIOR / ixor); the OR is repaired, the
+// XOR is appended as is (an empty result included).
+struct CPtr {
+  const BM *b;
+  size_t k;
+  bool valid() const { return k < b->size(); }
+  int key() const { return b->keys[k]; }
+  int card() const { return cardinality(b->vals[k]); }
+  const Cont &c() const { return b->vals[k]; }
+};
+BM *wide_horizontal(const BM *const *bs, size_t n, bool is_xor) {
+  BM *ans = new BM;
+  if (n == 0) return ans;
+  auto cmp = [](const CPtr &x, const CPtr &y) { return x.key() != y.key() ? x.key() - y.key() : y.card() - x.card(); };
+  JavaPQ<CPtr, decltype(cmp)> pq(cmp);
+  for (size_t k = 0; k < n; ++k) {
+    CPtr x{bs[k], 0};
+    if (x.valid()) pq.offer(x);
+  }
+  while (!pq.empty()) {
+    CPtr x1 = pq.poll();
+    if (pq.empty() || pq.peek().key() != x1.key()) {
+      ans->keys.push_back((uint16_t)x1.key());
+      ans->vals.push_back(x1.c());
+      ++x1.k;
+      if (x1.valid()) pq.offer(x1);
+      continue;
+    }
+    CPtr x2 = pq.poll();
+    Cont newc = is_xor ? c_xor(x1.c(), x2.c()) : c_lazy_or(x1.c(), x2.c());
+    while (!pq.empty() && pq.peek().key() == x1.key()) {
+      CPtr x = pq.poll();
+      newc = is_xor ? c_ixor(newc, x.c()) : c_lazy_ior(newc, x.c());
+      ++x.k;
+      if (x.valid()) pq.offer(x);
+      else if (pq.empty()) break;
+    }
+    if (!is_xor) newc = repair(std::move(newc));
+    ans->keys.push_back((uint16_t)x1.key());
+    ans->vals.push_back(std::move(newc));
+    ++x1.k;
+    if (x1.valid()) pq.offer(x1);
+    ++x2.k;
+    if (x2.valid()) pq.offer(x2);
+  }
+  return ans;
+}
+
+// RoaringBitmap.getLongSizeInBytes (RoaringBitmap.java:2212-2219) with the containers' getSizeInBytes:
+// Array 2c + 4 (ArrayContainer.java:450), Bitmap 8192 (BitmapContainer.java:507), Run 4r + 4
+// (RunContainer.java:1043) — a lazy Bitmap counts 8192 too.
+int64_t bm_size_in_bytes(const BM &b) {
+  int64_t s = 8;
+  for (const Cont &c : b.vals) s += 2 + (c.t == kA ? 2 * (int64_t)c.card + 4 : c.t == kB ? 8192 : 4 * (int64_t)c.nruns() + 4);
+  return s;
+}
+// RoaringBitmap.lazyor(x1, x2) static (RoaringBitmap.java:724-767): matched keys lazyOR, others cloned
+BM bm_lazyor_static(const BM &a, const BM &b) {
+  BM out;
+  size_t i = 0, j = 0;
+  while (i < a.size() && j < b.size()) {
+    if (a.keys[i] == b.keys[j]) {
+      out.keys.push_back(a.keys[i]);
+      out.vals.push_back(c_lazy_or(a.vals[i], b.vals[j]));
+      ++i;
+      ++j;
+    } else if (a.keys[i] < b.keys[j]) {
+      out.keys.push_back(a.keys[i]);
+      out.vals.push_back(a.vals[i++]);
+    } else {
+      out.keys.push_back(b.keys[j]);
+      out.vals.push_back(b.vals[j++]);
+    }
+  }
+  for (; i < a.size(); ++i) { out.keys.push_back(a.keys[i]); out.vals.push_back(a.vals[i]); }
+  for (; j < b.size(); ++j) { out.keys.push_back(b.keys[j]); out.vals.push_back(b.vals[j]); }
+  return out;
+}
+// this.lazyor(x2) in place (RoaringBitmap.java:2357-2402): matched keys lazyIOR, x2's other keys cloned
+// in; lazyorfromlazyinputs(x1, x2) (:769-830): matched keys lazyIOR with a Bitmap (lazy or not) put
+// first, the others taken over.  On value-semantics containers both are the same merge apart from
+// that swap.
+BM bm_lazyor_inplace(const BM &a, const BM &b, bool bitmap_first) {
+  BM out;
+  size_t i = 0, j = 0;
+  while (i < a.size() && j < b.size()) {
+    if (a.keys[i] == b.keys[j]) {
+      const Cont *c1 = &a.vals[i], *c2 = &b.vals[j];
+      if (bitmap_first && c2->t == kB && c1->t != kB) std::swap(c1, c2);
+      out.keys.push_back(a.keys[i]);
+      out.vals.push_back(c_lazy_ior(*c1, *c2));
+      ++i;
+      ++j;
+    } else if (a.keys[i] < b.keys[j]) {
+      out.keys.push_back(a.keys[i]);
+      out.vals.push_back(a.vals[i++]);
+    } else {
+      out.keys.push_back(b.keys[j]);
+      out.vals.push_back(b.vals[j++]);
+    }
+  }
+  for (; i < a.size(); ++i) { out.keys.push_back(a.keys[i]); out.vals.push_back(a.vals[i]); }
+  for (; j < b.size(); ++j) { out.keys.push_back(b.keys[j]); out.vals.push_back(b.vals[j]); }
+  return out;
+}
+// FastAggregation.priorityqueue_or(RoaringBitmap...) (FastAggregation.java:675-721): the bitmaps by
+// size in a priority queue of indices; the two smallest are lazily OR'd (which side is reused
+// depends on which operands are temporaries), the result re-queued with its new size; the survivor
+// is repaired.
+BM *wide_pq_or(const BM *const *bs, size_t n) {
+  if (n == 0) return new BM;
+  std::vector<BM> buffer(n);
+  for (size_t k = 0; k < n; ++k) buffer[k] = *bs[k];
+  std::vector<int64_t> sizes(n);
+  std::vector<char> istmp(n, 0);
+  for (size_t k = 0; k < n; ++k) sizes[k] = bm_size_in_bytes(buffer[k]);
+  auto cmp = [&](int a, int b) { return (int)(sizes[a] - sizes[b]); };
+  JavaPQ<int, decltype(cmp)> pq(cmp);
+  for (size_t k = 0; k < n; ++k) pq.offer((int)k);
+  while (pq.size() > 1) {
+    const int x1 = pq.poll(), x2 = pq.poll();
+    if (istmp[x2] && istmp[x1]) {
+      buffer[x1] = bm_lazyor_inplace(buffer[x1], buffer[x2], true);
+      sizes[x1] = bm_size_in_bytes(buffer[x1]);
+      istmp[x1] = 1;
+      pq.offer(x1);
+    } else if (istmp[x2]) {
+      buffer[x2] = bm_lazyor_inplace(buffer[x2], buffer[x1], false);
+      sizes[x2] = bm_size_in_bytes(buffer[x2]);
+      pq.offer(x2);
+    } else if (istmp[x1]) {
+      buffer[x1] = bm_lazyor_inplace(buffer[x1], buffer[x2], false);
+      sizes[x1] = bm_size_in_bytes(buffer[x1]);
+      pq.offer(x1);
+    } else {
+      buffer[x1] = bm_lazyor_static(buffer[x1], buffer[x2]);
+      sizes[x1] = bm_size_in_bytes(buffer[x1]);
+      istmp[x1] = 1;
+      pq.offer(x1);
+    }
+  }
+  BM *ans = new BM(std::move(buffer[pq.poll()]));
+  for (Cont &c : ans->vals) c = repair(std::move(c)); // RoaringBitmap.repairAfterLazy (:2752-2757)
+  return ans;
+}
+// FastAggregation.priorityqueue_xor (FastAggregation.java:732-752): the two smallest bitmaps (by
+// getLongSizeInBytes) replaced by their RoaringBitmap.xor until one is left
+BM *wide_pq_xor(const BM *const *bs, size_t n) {
+  if (n == 0) return new BM;
+  std::vector<BM> pool;
+  pool.reserve(2 * n);
+  for (size_t k = 0; k < n; ++k) pool.push_back(*bs[k]);
+  auto cmp = [&](int a, int b) { return (int)(bm_size_in_bytes(pool[a]) - bm_size_in_bytes(pool[b])); };
+  JavaPQ<int, decltype(cmp)> pq(cmp);
+  for (size_t k = 0; k < n; ++k) pq.offer((int)k); // Collections.addAll: add() in array order
+  while (pq.size() > 1) {
+    const int x1 = pq.poll(), x2 = pq.poll();
+    std::unique_ptr<BM> r(bm_or_xor(pool[x1], pool[x2], true));
+    pool.push_back(std::move(*r));
+    pq.offer((int)pool.size() - 1);
+  }
+  return new BM(pool[pq.poll()]);
+}
+
 // ---- key-parallel restatements (the CPU baseline on all host cores).  Every wide semantics is
 // per-key independent with the key's containers in member order, so each key's result is the
 // single-threaded one; ParallelAggregation itself is key-parallel on the ForkJoin pool
@@ -1430,13 +1668,18 @@ rbref_bitmap *rbref_wide(int sem, const rbref_bitmap *const *bs, size_t n) {
   case RBREF_PAR_OR: return wide_par(bs, n, false);
   case RBREF_PAR_XOR: return wide_par(bs, n, true);
   case RBREF_NAIVE_AND_ITER: return wide_naive_and_iter(bs, n);
+  case RBREF_HORIZONTAL_OR: return wide_horizontal(bs, n, false);
+  case RBREF_HORIZONTAL_XOR: return wide_horizontal(bs, n, true);
+  case RBREF_PQ_OR: return wide_pq_or(bs, n);
+  case RBREF_PQ_XOR: return wide_pq_xor(bs, n);
   default: return nullptr;
   }
 }
 
 rbref_bitmap *rbref_wide_mt(int sem, const rbref_bitmap *const *bs, size_t n, int threads) {
   if (sem == RBREF_FAST_AND) sem = n > 10 ? RBREF_WORKSHY_AND : RBREF_NAIVE_AND;
-  if (sem == RBREF_NAIVE_AND || sem == RBREF_NAIVE_AND_ITER) return rbref_wide(sem, bs, n);
+  // global-order semantics (the queue's tie order spans keys): single-threaded
+  if (sem == RBREF_NAIVE_AND || sem == RBREF_NAIVE_AND_ITER || sem >= RBREF_HORIZONTAL_OR) return rbref_wide(sem, bs, n);
   if (n == 0) return new BM;
   return wide_key_parallel(sem, bs, n, threads);
 }

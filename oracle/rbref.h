@@ -40,7 +40,11 @@ enum {
   RBREF_FAST_XOR = 4,     /* FastAggregation.xor == naive_xor          FastAggregation.java:772 */
   RBREF_PAR_OR = 5,       /* ParallelAggregation.or                    ParallelAggregation.java:161 */
   RBREF_PAR_XOR = 6,      /* ParallelAggregation.xor                   ParallelAggregation.java:182 */
-  RBREF_NAIVE_AND_ITER = 7 /* FastAggregation.and(Iterator)            FastAggregation.java:26,304 */
+  RBREF_NAIVE_AND_ITER = 7, /* FastAggregation.and(Iterator)           FastAggregation.java:26,304 */
+  RBREF_HORIZONTAL_OR = 8,  /* FastAggregation.horizontal_or           FastAggregation.java:124-231 */
+  RBREF_HORIZONTAL_XOR = 9, /* FastAggregation.horizontal_xor          FastAggregation.java:243-289 */
+  RBREF_PQ_OR = 10,         /* FastAggregation.priorityqueue_or        FastAggregation.java:615-721 */
+  RBREF_PQ_XOR = 11         /* FastAggregation.priorityqueue_xor       FastAggregation.java:732-752 */
 };
 
 /* container type tags (RoaringFormatSpec order used by the device SoA) */

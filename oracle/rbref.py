@@ -14,7 +14,8 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 _LIB_PATH = os.path.join(_HERE, "librbref.so")
 
 AND, OR, XOR, ANDNOT = 0, 1, 2, 3
-FAST_OR, FAST_AND, WORKSHY_AND, NAIVE_AND, FAST_XOR, PAR_OR, PAR_XOR, NAIVE_AND_ITER = range(8)
+(FAST_OR, FAST_AND, WORKSHY_AND, NAIVE_AND, FAST_XOR, PAR_OR, PAR_XOR, NAIVE_AND_ITER, HORIZONTAL_OR, HORIZONTAL_XOR,
+ PQ_OR, PQ_XOR) = range(12)
 ARRAY, BITMAP, RUN = 0, 1, 2
 
 

@@ -586,11 +586,14 @@ int rbgpu_set_summaries(const rbgpu_set *s, uint32_t first, uint32_t count, rb_b
   for (uint32_t b = 0; b < count; ++b) {
     rb_bitmap_summary &o = out[b];
     o = rb_bitmap_summary{};
+    o.size_in_bytes = 8;
     for (uint64_t i = s->h_begin[first + b] - lo; i < s->h_begin[first + b + 1] - lo; ++i) {
       o.cardinality += card[i];
       o.n_containers += 1;
       o.n_run_containers += type[i] == RB_RUN;
       o.payload_bytes += type[i] == RB_BITMAP ? 8192ull : type[i] == RB_ARRAY ? 2ull * card[i] : 2 + 4ull * nruns[i];
+      // 2 key bytes + Container.getSizeInBytes: Array 2c + 4, Bitmap 8192, Run 4r + 4
+      o.size_in_bytes += 2 + (type[i] == RB_BITMAP ? 8192ull : type[i] == RB_ARRAY ? 2ull * card[i] + 4 : 4ull * nruns[i] + 4);
     }
   }
   return RB_OK;
@@ -1064,6 +1067,72 @@ void rbgpu_internal_set_mix(int fa, int fab, int pa, int pab) {
 }
 
 // ---------------------------------------------------------------- wide
+// FastAggregation.priorityqueue_xor (FastAggregation.java:732-752): a queue of bitmaps ordered by
+// getLongSizeInBytes (java.util.PriorityQueue, Collections.addAll order); the two smallest are
+// replaced by their RoaringBitmap.xor — one pairwise call on the device — until one is left.
+static int empty_result(rbgpu_ctx *ctx, rbgpu_set **out) {
+  rbgpu_set *e = new rbgpu_set;
+  int rc = set_alloc(ctx, e, 1, 0, 16);
+  if (rc) {
+    delete e;
+    return rc;
+  }
+  const uint64_t hb[2] = {0, 0};
+  HIPCHK(hipMemcpy(e->begin, hb, 16, hipMemcpyHostToDevice));
+  e->h_begin = {0, 0};
+  *out = e;
+  return RB_OK;
+}
+static int pq_xor(rbgpu_ctx *ctx, const rbgpu_set *in, const std::vector<uint32_t> &mem, rbgpu_set **out) {
+  const size_t n = mem.size();
+  if (n == 0) return empty_result(ctx, out);
+  std::vector<rb_bitmap_summary> summ(in->nb);
+  int rc = rbgpu_set_summaries(in, 0, in->nb, summ.data());
+  if (rc) return rc;
+  struct Node {
+    const rbgpu_set *s;
+    uint32_t idx;
+    int64_t size;
+    rbgpu_set *owned;
+  };
+  std::vector<Node> nodes;
+  nodes.reserve(2 * n);
+  for (uint32_t m : mem) nodes.push_back(Node{in, m, (int64_t)summ[m].size_in_bytes, nullptr});
+  auto cmp = [&](uint32_t a, uint32_t b) { return (int)(nodes[a].size - nodes[b].size); };
+  JavaHeap<uint32_t, decltype(cmp)> pq(cmp);
+  for (uint32_t k = 0; k < n; ++k) pq.offer(k);
+  auto cleanup = [&]() {
+    for (Node &x : nodes)
+      if (x.owned) rbgpu_set_free(x.owned), x.owned = nullptr;
+  };
+  while (pq.size() > 1) {
+    const uint32_t x1 = pq.poll(), x2 = pq.poll();
+    const uint32_t i1 = nodes[x1].idx, i2 = nodes[x2].idx;
+    rbgpu_set *r = nullptr;
+    rc = rbgpu_pairwise(ctx, RB_XOR, nodes[x1].s, nodes[x2].s, &i1, &i2, 1, &r);
+    rb_bitmap_summary rs{};
+    if (!rc) rc = rbgpu_set_summaries(r, 0, 1, &rs);
+    if (rc) {
+      if (r) rbgpu_set_free(r);
+      cleanup();
+      return rc;
+    }
+    for (uint32_t x : {x1, x2}) // the operands are not referenced again
+      if (nodes[x].owned) rbgpu_set_free(nodes[x].owned), nodes[x].owned = nullptr;
+    nodes.push_back(Node{r, 0, (int64_t)rs.size_in_bytes, r});
+    pq.offer((uint32_t)nodes.size() - 1);
+  }
+  Node &last = nodes[pq.poll()];
+  if (last.owned) {
+    *out = last.owned;
+    last.owned = nullptr;
+    cleanup();
+    return RB_OK;
+  }
+  cleanup();
+  return rbgpu_set_extract(last.s, last.idx, 1, out); // one member: the reference returns it as is
+}
+
 int rbgpu_wide(rbgpu_ctx *ctx, int sem, const rbgpu_set *in, const uint32_t *members, uint32_t n, rbgpu_set **out) {
   return rbgpu_wide_keys(ctx, sem, in, members, n, 0, 65536, out);
 }
@@ -1076,7 +1145,7 @@ int rbgpu_wide_keys(rbgpu_ctx *ctx, int sem, const rbgpu_set *in, const uint32_t
   int rc = check_ctx(ctx);
   if (rc) return rc;
   if (!in || in->ctx != ctx) return fail(RB_EINVAL, "bad input set");
-  if (sem < RB_FAST_OR || sem > RB_NAIVE_AND_ITER) return fail(RB_EINVAL, "bad semantics %d", sem);
+  if (sem < RB_FAST_OR || sem > RB_PQ_XOR || sem == 10) return fail(RB_EINVAL, "bad semantics %d", sem);
   rc = ensure_h_begin(in);
   if (rc) return rc;
   std::vector<uint32_t> mem;
@@ -1088,6 +1157,10 @@ int rbgpu_wide_keys(rbgpu_ctx *ctx, int sem, const rbgpu_set *in, const uint32_t
     if (n > in->nb) return fail(RB_EINVAL, "n exceeds the set");
     mem.resize(n);
     for (uint32_t i = 0; i < n; ++i) mem[i] = i;
+  }
+  if (sem == RB_PQ_XOR) {
+    if (key_lo != 0 || key_hi != 65536) return fail(RB_EINVAL, "priorityqueue_xor has no key-range shards");
+    return pq_xor(ctx, in, mem, out);
   }
   return wide_run(ctx, sem, in, mem, key_lo, key_hi, out);
 }

@@ -93,6 +93,48 @@ struct Workspace {
 };
 inline size_t aligned256(size_t b) { return (b + 255) & ~size_t(255); }
 
+// java.util.PriorityQueue's binary heap (OpenJDK: offer = append + siftUp, poll = the last element
+// sifted down from the root), so elements that compare equal come out in the reference's order.
+// cmp(a, b) < 0 / 0 / > 0 like compareTo.  Used by the global-order aggregations
+// (FastAggregation.horizontal_* and priorityqueue_*), whose order the host computes.
+template <class T, class Cmp> struct JavaHeap {
+  std::vector<T> q;
+  Cmp cmp;
+  explicit JavaHeap(Cmp c) : cmp(c) {}
+  bool empty() const { return q.empty(); }
+  size_t size() const { return q.size(); }
+  const T &peek() const { return q[0]; }
+  void offer(const T &x) {
+    size_t k = q.size();
+    q.push_back(x);
+    while (k > 0) {
+      const size_t parent = (k - 1) >> 1;
+      if (cmp(x, q[parent]) >= 0) break;
+      q[k] = q[parent];
+      k = parent;
+    }
+    q[k] = x;
+  }
+  T poll() {
+    T result = q[0];
+    T x = q.back();
+    q.pop_back();
+    const size_t n = q.size();
+    if (n > 0) {
+      size_t k = 0;
+      while (k < (n >> 1)) {
+        size_t child = 2 * k + 1;
+        if (child + 1 < n && cmp(q[child], q[child + 1]) > 0) ++child;
+        if (cmp(x, q[child]) <= 0) break;
+        q[k] = q[child];
+        k = child;
+      }
+      q[k] = x;
+    }
+    return result;
+  }
+};
+
 } // namespace rbg
 
 struct rbgpu_ctx {

@@ -312,7 +312,16 @@ __global__ __launch_bounds__(256) void k_wide_reduce(SetView s, const uint32_t *
   uint64_t inb = 0;
   int ty = kEmpty, c = 0, r = 0;
 
-  if ((SEM == RB_FAST_OR || SEM == RB_PAR_OR) && m == 1) {
+  if ((SEM == RB_HORIZONTAL_OR || SEM == RB_HORIZONTAL_XOR) && m == 1) {
+    // horizontal_*: a key held by one bitmap is appended as a clone, unrepaired
+    // (FastAggregation.java:139-145, 258-264)
+    const CRef a = cref(s, cid[lo]);
+    inb = alg_bytes_w(a.type, a.card, a.nruns) + 16;
+    copy_payload(a.p, dst, payload_bytes(a.type, a.card, a.nruns), lane);
+    ty = a.type;
+    c = (int)a.card;
+    r = (int)a.nruns;
+  } else if ((SEM == RB_FAST_OR || SEM == RB_PAR_OR) && m == 1) {
     // a key seen once: clone, then repairAfterLazy (A, B unchanged; Run -> toEfficientContainer)
     const CRef a = cref(s, cid[lo]);
     inb = alg_bytes_w(a.type, a.card, a.nruns) + 16;
@@ -367,7 +376,7 @@ __global__ __launch_bounds__(256) void k_wide_reduce(SetView s, const uint32_t *
     }
     ty = c ? t : kEmpty;
     if (ty != kEmpty) emit_container(ty, acc, c, r, dst, lds, lane);
-  } else if (SEM == RB_FAST_XOR || SEM == RB_PAR_XOR) {
+  } else if (SEM == RB_FAST_XOR || SEM == RB_PAR_XOR || SEM == RB_HORIZONTAL_XOR) {
     // naive_xor: in-place xor() per bitmap — absent key -> clone; empty -> key removed
     //   (RoaringBitmap.xor(x2) :3296-3348).  ParallelAggregation.xor: clone + ixor fold with no
     //   removal (ParallelAggregation.java:189-195); an empty Run accumulator returns the other
@@ -392,20 +401,40 @@ __global__ __launch_bounds__(256) void k_wide_reduce(SetView s, const uint32_t *
       const uint32_t cc = (uint32_t)c;
       fold<RB_XOR>(acc, x);
       metrics(acc, lane, true, c, r);
-      if (SEM == RB_PAR_XOR && ct == kRun && cc == 0 && b.type != kBitmap) t = b.type;
+      if ((SEM == RB_PAR_XOR || SEM == RB_HORIZONTAL_XOR) && ct == kRun && cc == 0 && b.type != kBitmap) t = b.type;
       else t = type_xor_step(ct, b.type, cc, b.card, c, r);
       if (SEM == RB_FAST_XOR && c == 0) present = false;
     }
-    ty = present && c > 0 ? t : kEmpty;
+    // horizontal_xor appends the key's result even when it is empty (FastAggregation.java:278)
+    ty = SEM == RB_HORIZONTAL_XOR ? t : present && c > 0 ? t : kEmpty;
     if (ty != kEmpty) emit_container(ty, acc, c, r, dst, lds, lane);
-  } else { // RB_PAR_OR with 2..15 containers: clone + lazyIOR chain + repairAfterLazy
+  } else { // RB_PAR_OR with 2..15 containers: clone + lazyIOR chain + repairAfterLazy; RB_HORIZONTAL_OR:
+           // lazyOR of the first two, then the same lazyIOR chain + repairAfterLazy
     const CRef a = cref(s, cid[lo]);
     inb = alg_bytes_w(a.type, a.card, a.nruns) + 16;
     load_container(a.type, a.p, a.card, a.nruns, lds, acc, lane);
     int st = a.type == kArray ? kStA : a.type == kBitmap ? kStBValid : kStRun;
     c = (int)a.card;
     r = (int)a.nruns;
-    for (uint64_t i = lo + 1; i < hi; ++i) {
+    uint64_t i0 = lo + 1;
+    if (SEM == RB_HORIZONTAL_OR) {
+      // Container.lazyOR (Container.java:751-774) of the first two polled containers
+      const CRef b = cref(s, cid[lo + 1]);
+      inb += alg_bytes_w(b.type, b.card, b.nruns) + 16;
+      uint64_t x[kW];
+      load_container(b.type, b.p, b.card, b.nruns, lds, x, lane);
+      fold<RB_OR>(acc, x);
+      metrics(acc, lane, true, c, r);
+      if (a.type == kBitmap || b.type == kBitmap) st = kStBLazy;                  // BitmapContainer.lazyor
+      else if (a.type == kArray && b.type == kArray)
+        st = a.card + b.card > 1024u ? kStBLazy : kStA;                            // ArrayContainer.lazyor :1449
+      else if (a.type == kRun && b.type == kRun) {                                 // RunContainer.or -> EFF
+        const int e = type_eff(c, r);
+        st = c == kSpan ? kStRun : e == kRun ? kStRun : e == kBitmap ? kStBValid : kStA;
+      } else st = c == kSpan ? kStRun : (r > kMaxArray ? kStBLazy : kStRun);       // RunContainer.lazyorToRun
+      i0 = lo + 2;
+    }
+    for (uint64_t i = i0; i < hi; ++i) {
       const CRef b = cref(s, cid[i]);
       inb += alg_bytes_w(b.type, b.card, b.nruns) + 16;
       const bool acc_full = st == kStRun && c == kSpan;
@@ -515,6 +544,67 @@ static void launch_reduce(const SetView &s, const uint32_t *cid, const uint64_t 
   k_wide_reduce<SEM><<<nblk(nk, 4), 256, 0, st>>>(s, cid, seg, klist, nk, out, wo, route, stats);
 }
 
+// FastAggregation.horizontal_or / horizontal_xor's container order (FastAggregation.java:124-289): a
+// ContainerPointer per member in a java.util.PriorityQueue ordered by key, then by cardinality
+// descending (RoaringArray.java:708-713); per key the poll order is the fold order.  The tie order
+// depends on the whole queue's history, so the host replays the queue over the members' keys and
+// cardinalities (6 bytes per container read back) and the device folds each key in that order.
+static int horizontal_order(const rbgpu_set *in, const std::vector<uint32_t> &mem, std::vector<uint32_t> &cid,
+                            std::vector<uint64_t> &seg) {
+  const uint64_t nc = in->nc;
+  std::vector<uint16_t> K(nc);
+  std::vector<uint32_t> C(nc);
+  if (nc) {
+    HIPCHK(hipMemcpyAsync(K.data(), in->key, nc * 2, hipMemcpyDeviceToHost, in->ctx->stream));
+    HIPCHK(hipMemcpyAsync(C.data(), in->card, nc * 4, hipMemcpyDeviceToHost, in->ctx->stream));
+    HIPCHK(hipStreamSynchronize(in->ctx->stream));
+  }
+  struct P {
+    uint32_t m;  // member
+    uint64_t k;  // container index in the set
+  };
+  std::vector<uint64_t> end(mem.size());
+  for (size_t i = 0; i < mem.size(); ++i) end[i] = in->h_begin[mem[i] + 1];
+  auto cmp = [&](const P &a, const P &b) {
+    return K[a.k] != K[b.k] ? (int)K[a.k] - (int)K[b.k] : (int)C[b.k] - (int)C[a.k];
+  };
+  JavaHeap<P, decltype(cmp)> pq(cmp);
+  for (size_t i = 0; i < mem.size(); ++i) {
+    const P x{(uint32_t)i, in->h_begin[mem[i]]};
+    if (x.k < end[i]) pq.offer(x);
+  }
+  cid.clear();
+  seg.assign(65537, 0);
+  int cur = -1;
+  auto advance = [&](P x) { // ContainerPointer.advance + re-queue while it points at a container
+    ++x.k;
+    if (x.k < end[x.m]) pq.offer(x);
+    return x.k < end[x.m];
+  };
+  while (!pq.empty()) {
+    const P x1 = pq.poll();
+    const int key = K[x1.k];
+    for (int k = cur + 1; k <= key; ++k) seg[k] = cid.size();
+    cur = key;
+    cid.push_back((uint32_t)x1.k);
+    if (pq.empty() || K[pq.peek().k] != key) {
+      advance(x1);
+      continue;
+    }
+    const P x2 = pq.poll();
+    cid.push_back((uint32_t)x2.k);
+    while (!pq.empty() && K[pq.peek().k] == key) {
+      const P x = pq.poll();
+      cid.push_back((uint32_t)x.k);
+      if (!advance(x) && pq.empty()) break;
+    }
+    advance(x1);
+    advance(x2);
+  }
+  for (int k = cur + 1; k <= 65536; ++k) seg[k] = cid.size();
+  return RB_OK;
+}
+
 int wide_run(rbgpu_ctx *ctx, int sem, const rbgpu_set *in, const std::vector<uint32_t> &members_in,
              uint32_t key_lo, uint32_t key_hi, rbgpu_set **out) {
   hipStream_t st = ctx->stream;
@@ -576,7 +666,19 @@ int wide_run(rbgpu_ctx *ctx, int sem, const rbgpu_set *in, const std::vector<uin
   static const bool no_dense = getenv("RBGPU_NO_DENSE_GROUPING") != nullptr;
   bool dense = M && nkr && !no_dense;
   for (uint32_t i = 0; dense && i < M; ++i) dense = in->h_begin[members[i] + 1] - in->h_begin[members[i]] == 65536;
-  if (dense) {
+  std::vector<uint32_t> h_cid;
+  std::vector<uint64_t> h_seg;
+  if (sem == RB_HORIZONTAL_OR || sem == RB_HORIZONTAL_XOR) {
+    // the queue order of FastAggregation.horizontal_* over every member key (ties included), then the
+    // per-key containers in that order; keys outside the shard are left to k_wide_select
+    int rc = horizontal_order(in, members, h_cid, h_seg);
+    if (rc) {
+      release();
+      return rc;
+    }
+    if (!h_cid.empty()) HIPCHK(hipMemcpyAsync(d_cid2, h_cid.data(), 4 * h_cid.size(), hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(d_seg, h_seg.data(), 8 * 65537ull, hipMemcpyHostToDevice, st));
+  } else if (dense) {
     k_group_dense<<<(unsigned)std::min<uint64_t>(nblk((uint64_t)krange * M, 256), 65536), 256, 0, st>>>(
         sv.begin, d_mem, M, key_lo, key_hi, d_seg, d_cid2);
   } else {
@@ -637,6 +739,8 @@ int wide_run(rbgpu_ctx *ctx, int sem, const rbgpu_set *in, const std::vector<uin
     case RB_NAIVE_AND_ITER: launch_reduce<RB_NAIVE_AND_ITER>(sv, d_cid2, d_seg, d_klist, nk, res->payload, wo, ctx->d_stats, st); break;
     case RB_FAST_XOR: launch_reduce<RB_FAST_XOR>(sv, d_cid2, d_seg, d_klist, nk, res->payload, wo, ctx->d_stats, st, rt); break;
     case RB_PAR_OR: launch_reduce<RB_PAR_OR>(sv, d_cid2, d_seg, d_klist, nk, res->payload, wo, ctx->d_stats, st); break;
+    case RB_HORIZONTAL_OR: launch_reduce<RB_HORIZONTAL_OR>(sv, d_cid2, d_seg, d_klist, nk, res->payload, wo, ctx->d_stats, st); break;
+    case RB_HORIZONTAL_XOR: launch_reduce<RB_HORIZONTAL_XOR>(sv, d_cid2, d_seg, d_klist, nk, res->payload, wo, ctx->d_stats, st); break;
     default: launch_reduce<RB_PAR_XOR>(sv, d_cid2, d_seg, d_klist, nk, res->payload, wo, ctx->d_stats, st); break;
     }
   }
@@ -655,7 +759,9 @@ int wide_run(rbgpu_ctx *ctx, int sem, const rbgpu_set *in, const std::vector<uin
                      : sem == RB_WORKSHY_AND ? (fp ? "k_wide_runs_and+k_wide_reduce<WORKSHY_AND>" : "k_wide_reduce<WORKSHY_AND>")
                      : sem == RB_FAST_XOR ? (fp ? "k_wide_runs_xor+k_wide_reduce<FAST_XOR>" : "k_wide_reduce<FAST_XOR>")
                      : sem == RB_PAR_OR ? "k_wide_reduce<PAR_OR>"
-                     : sem == RB_PAR_XOR ? "k_wide_reduce<PAR_XOR>" : "k_wide_reduce<NAIVE_AND>";
+                     : sem == RB_PAR_XOR ? "k_wide_reduce<PAR_XOR>"
+                     : sem == RB_HORIZONTAL_OR ? "k_wide_reduce<HORIZONTAL_OR>"
+                     : sem == RB_HORIZONTAL_XOR ? "k_wide_reduce<HORIZONTAL_XOR>" : "k_wide_reduce<NAIVE_AND>";
   const KernelSpan spans[1] = {{name, 0, 1, nk}};
   // ev[2] -> ev[3]: nothing; stats_end reads ev[1]..ev[2] for kernel 0
   rc = stats_end(ctx, N, nres, spans, 1);

@@ -180,6 +180,20 @@ class FastAggregation:
         return _wide(L.FAST_XOR, bitmaps)
 
     @staticmethod
+    def horizontal_or(*bitmaps) -> RoaringBitmap:
+        """horizontal_or(List / varargs) (FastAggregation.java:124-231); the Iterator overload
+        (:110-112) is naive_or."""
+        return _wide(L.HORIZONTAL_OR, bitmaps)
+
+    @staticmethod
+    def horizontal_xor(*bitmaps) -> RoaringBitmap:
+        return _wide(L.HORIZONTAL_XOR, bitmaps)
+
+    @staticmethod
+    def priorityqueue_xor(*bitmaps) -> RoaringBitmap:
+        return _wide(L.PQ_XOR, bitmaps)
+
+    @staticmethod
     def andCardinality(*bitmaps) -> int:
         bms = _flatten(bitmaps)
         if not bms:

@@ -5,7 +5,9 @@ import pytest
 from datasets import DATASETS, EXPECTED, load_realdata, synthetic_bitmaps
 
 pytestmark = pytest.mark.gpu
-SEMS = ["FAST_OR", "FAST_AND", "WORKSHY_AND", "NAIVE_AND", "FAST_XOR", "PAR_OR", "PAR_XOR", "NAIVE_AND_ITER"]
+SEMS = ["FAST_OR", "FAST_AND", "WORKSHY_AND", "NAIVE_AND", "FAST_XOR", "PAR_OR", "PAR_XOR", "NAIVE_AND_ITER",
+        "HORIZONTAL_OR", "HORIZONTAL_XOR", "PQ_XOR"]
+SHARDABLE = [x for x in SEMS if x != "PQ_XOR"]  # priorityqueue_xor: whole results only
 
 
 def _check(ctx, oracle, s, refs, sem_name, members):
@@ -91,8 +93,9 @@ def test_key_range_shards_reassemble(ctx, oracle):
     refs = [oracle.RefBitmap.deserialize(b) for b in s.serialize()]
     for n in (8, 11, 17):
         members = np.arange(n, dtype=np.uint32)
-        for sem in SEMS:
-            want = oracle.wide(getattr(oracle, sem), [refs[m] for m in members]).serialize()
+        for sem in SHARDABLE:
+            want_bm = oracle.wide(getattr(oracle, sem), [refs[m] for m in members])
+            want = want_bm.serialize()
             mem, sem_shard = members, getattr(rb, sem)
             if sem == "NAIVE_AND" or (sem == "FAST_AND" and n <= 10):
                 sizes = [len(refs[m].containers()) for m in members]
@@ -104,7 +107,7 @@ def test_key_range_shards_reassemble(ctx, oracle):
                 got = serialize_parts([sh.download() for sh in shards])
                 assert got == want, (sem, n, parts)
                 summ = [sh.summaries()[0] for sh in shards]
-                assert sum(x["cardinality"] for x in summ) == oracle.RefBitmap.deserialize(want).cardinality()
+                assert sum(x["cardinality"] for x in summ) == want_bm.cardinality()
 
 
 def test_generated_key_shards_equal_full_dataset(ctx):
@@ -363,3 +366,34 @@ def test_xor_fastforward_threshold_regimes(ctx, oracle):
             assert ctx.wide(rb.FAST_XOR, s, members).serialize()[0] == want, n
         finally:
             del os.environ["RBGPU_XOR_NO_FASTFWD"]
+
+
+def test_queue_order_ties(ctx, oracle):
+    """horizontal_or / horizontal_xor / priorityqueue_xor where many containers of a key tie on
+    cardinality (the java.util.PriorityQueue's tie order then picks which types meet first) and
+    bitmaps tie on getLongSizeInBytes."""
+    rng = np.random.default_rng(17)
+    bms = []
+    for i in range(26):
+        parts = []
+        for k in range(4):
+            c = [100, 100, 3000, 5000][k]
+            if (i + k) % 3 == 0:  # a run of c values
+                a = int(rng.integers(0, 65536 - c))
+                v = np.arange(a, a + c)
+            else:  # c scattered values
+                v = rng.choice(65536, size=c, replace=False)
+            parts.append(np.sort(v).astype(np.uint32) | np.uint32(k << 16))
+        bms.append(np.concatenate(parts))
+    import roaringbitmap_amd as rb
+    for ro in (False, True):
+        s = ctx.upload_values(bms, run_optimize=ro)
+        refs = [oracle.RefBitmap.deserialize(b) for b in s.serialize()]
+        for n in (2, 3, 7, 26):
+            members = np.arange(n, dtype=np.uint32)
+            for sem in ("HORIZONTAL_OR", "HORIZONTAL_XOR", "PQ_XOR"):
+                _check(ctx, oracle, s, refs, sem, members)
+        members = np.array([3, 3, 5, 5, 5, 9], np.uint32)  # duplicates: empty xor containers kept
+        for sem in ("HORIZONTAL_XOR", "PQ_XOR", "HORIZONTAL_OR"):
+            _check(ctx, oracle, s, refs, sem, members)
+    assert ctx.wide(rb.PQ_XOR, s, np.zeros(0, np.uint32)).n_containers == 0

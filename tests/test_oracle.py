@@ -157,3 +157,48 @@ def test_key_parallel_restatement_matches(oracle, sem):
             want = R.wide(getattr(R, sem), bms[:n]).serialize()
             for threads in (1, 4):
                 assert R.wide_mt(getattr(R, sem), bms[:n], threads).serialize() == want, (sem, n, threads)
+
+
+def test_horizontal_and_priorityqueue_known_answers(oracle):
+    """TestFastAggregation.java:22-69 (horizontal_or, horizontal_or2, priorityqueue_or,
+    priorityqueue_or2): the union of {0,1,2}, {0,5,6}, {1<<16, 2<<16}; TestRoaringBitmap.java:3190-3320:
+    horizontal_* / priorityqueue_* equal RoaringBitmap.or / xor (content)."""
+    R = oracle
+    rb1, rb2, rb3 = R.RefBitmap.of([0, 1, 2]), R.RefBitmap.of([0, 5, 6]), R.RefBitmap.of([1 << 16, 2 << 16])
+    for sem in (R.HORIZONTAL_OR, R.PQ_OR):
+        assert list(R.wide(sem, [rb1, rb2, rb3]).to_array()) == [0, 1, 2, 5, 6, 1 << 16, 2 << 16]
+    rng = np.random.default_rng(7)
+    for trial in range(6):
+        bms = []
+        for i in range(int(rng.integers(1, 30))):
+            v = np.unique(rng.integers(0, 6 * 65536, int(rng.integers(1, 20000)))).astype(np.uint32)
+            if i % 4 == 0:
+                a = int(rng.integers(0, 6 * 65536 - 70000))
+                v = np.union1d(v, np.arange(a, a + 70000, dtype=np.uint32))
+            b = R.RefBitmap.of(v)
+            if (i + trial) % 3 == 0:
+                b.run_optimize()
+            bms.append(b)
+        u = R.wide(R.FAST_OR, bms).to_array()
+        x = R.wide(R.FAST_XOR, bms).to_array()
+        for sem in (R.HORIZONTAL_OR, R.PQ_OR):
+            assert np.array_equal(R.wide(sem, bms).to_array(), u)
+        for sem in (R.HORIZONTAL_XOR, R.PQ_XOR):
+            assert np.array_equal(R.wide(sem, bms).to_array(), x)
+
+
+def test_java_priority_queue_tie_order(oracle):
+    """horizontal_or of bitmaps whose key-0 containers tie on cardinality: the result is the union
+    whatever the order, and its container type follows the restated java.util.PriorityQueue order
+    (deterministic: the same inputs in the same order give the same bytes)."""
+    R = oracle
+    bms = []
+    for i in range(9):
+        v = np.arange(100 * i, 100 * i + 50, dtype=np.uint32) if i % 2 else np.arange(0, 5000, 100, dtype=np.uint32)
+        b = R.RefBitmap.of(v)
+        if i % 3 == 0:
+            b.run_optimize()
+        bms.append(b)
+    a = R.wide(R.HORIZONTAL_OR, bms).serialize()
+    assert a == R.wide(R.HORIZONTAL_OR, bms).serialize()
+    assert np.array_equal(R.RefBitmap.deserialize(a).to_array(), R.wide(R.FAST_OR, bms).to_array())
