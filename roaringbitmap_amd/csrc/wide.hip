@@ -100,7 +100,7 @@ __global__ __launch_bounds__(256) void k_group_count(GroupArgs a, uint32_t *Hc) 
   for (int u = 0; u < (int)kGrpMembers; ++u)
     if (kk[u] != ~0u) atomicAdd(&cnt[kk[u]], 1u);
   __syncthreads();
-  if (threadIdx.x < nk) Hc[(uint64_t)mb * 65536 + k0 + threadIdx.x] = cnt[threadIdx.x];
+  if (threadIdx.x < nk) Hc[(uint64_t)mb * (a.key_hi - a.key_lo) + (k0 - a.key_lo) + threadIdx.x] = cnt[threadIdx.x];
 }
 __global__ __launch_bounds__(256) void k_group_totals(const uint32_t *Hc, uint32_t nmb, uint32_t key_lo,
                                                       uint32_t key_hi, uint64_t *tot) {
@@ -108,7 +108,7 @@ __global__ __launch_bounds__(256) void k_group_totals(const uint32_t *Hc, uint32
   if (k > 65536) return;
   uint64_t s = 0;
   if (k >= key_lo && k < key_hi)
-    for (uint32_t b = 0; b < nmb; ++b) s += Hc[(uint64_t)b * 65536 + k];
+    for (uint32_t b = 0; b < nmb; ++b) s += Hc[(uint64_t)b * (key_hi - key_lo) + (k - key_lo)];
   tot[k] = s;
 }
 __global__ __launch_bounds__(256) void k_group_base(const uint32_t *Hc, uint64_t *H, uint32_t nmb, uint32_t key_lo,
@@ -117,8 +117,9 @@ __global__ __launch_bounds__(256) void k_group_base(const uint32_t *Hc, uint64_t
   if (k >= key_hi) return;
   uint64_t run = seg[k];
   for (uint32_t b = 0; b < nmb; ++b) {
-    H[(uint64_t)b * 65536 + k] = run;
-    run += Hc[(uint64_t)b * 65536 + k];
+    const uint64_t x = (uint64_t)b * (key_hi - key_lo) + (k - key_lo);
+    H[x] = run;
+    run += Hc[x];
   }
 }
 // Per tile: a 64-bit presence mask per key (bit u = member u of the block holds the key) gives every
@@ -149,7 +150,7 @@ __global__ __launch_bounds__(256) void k_group_scatter(GroupArgs a, const uint64
   const uint32_t mb = blockIdx.y, j = blockIdx.x, t = threadIdx.x;
   const uint32_t k0 = a.key_lo + j * a.KR, nk = min(a.KR, a.key_hi - k0);
   mask[t] = 0;
-  gbase[t] = t < nk ? H[(uint64_t)mb * 65536 + k0 + t] : 0;
+  gbase[t] = t < nk ? H[(uint64_t)mb * (a.key_hi - a.key_lo) + (k0 - a.key_lo) + t] : 0;
   if (t < a.MB && mb * a.MB + t < a.M) mbase[t] = a.bnd[(uint64_t)(mb * a.MB + t) * (a.nkr + 1) + j];
   uint32_t kk[kGrpMembers], ci[kGrpMembers];
   tile_load(a, mb, j, k0, kk, ci);
@@ -649,8 +650,8 @@ int wide_run(rbgpu_ctx *ctx, int sem, const rbgpu_set *in, const std::vector<uin
   const uint64_t tmpw = std::max<uint64_t>(scan_tmp_words(65537), 1);
   if (pool.alloc((void **)&d_mem, std::max<uint32_t>(M, 1) * 4ull) ||
       pool.alloc((void **)&d_bnd, std::max<uint64_t>((uint64_t)M * (nkr + 1), 1) * 8) ||
-      pool.alloc((void **)&d_Hc, std::max<uint32_t>(nmb, 1) * 65536ull * 4) ||
-      pool.alloc((void **)&d_H, std::max<uint32_t>(nmb, 1) * 65536ull * 8) || pool.alloc((void **)&d_cid2, N1 * 4) ||
+      pool.alloc((void **)&d_Hc, std::max<uint64_t>((uint64_t)nmb * krange, 1) * 4) ||
+      pool.alloc((void **)&d_H, std::max<uint64_t>((uint64_t)nmb * krange, 1) * 8) || pool.alloc((void **)&d_cid2, N1 * 4) ||
       pool.alloc((void **)&d_tot, 65537 * 8ull) || pool.alloc((void **)&d_seg, 65537 * 8ull) ||
       pool.alloc((void **)&d_active, 65537 * 8ull) || pool.alloc((void **)&d_apos, 65537 * 8ull) ||
       pool.alloc((void **)&d_klist, 65536 * 4ull) || pool.alloc((void **)&d_tmp, tmpw * 8))
