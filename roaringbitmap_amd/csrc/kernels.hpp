@@ -112,11 +112,22 @@ struct WideOut {
 
 // ---- wide_runs.hip: Run-list fast path for naive_or / workShyAnd / naive_xor keys whose containers
 // are all Runs with <= 8 runs; route[q] = 0 where done, 1 where the generic kernel must run
+// naive_xor's key-major member records (wide_xor.hip): workspace `rec` of n entries (one per grouped
+// container); dense = every member holds every key (k_group_dense's layout over mem[0..M), keys
+// [key_lo, key_hi)), else the records are gathered through the container ids
+struct XorRecords {
+  uint64_t *rec;
+  uint64_t n;
+  bool dense;
+  const uint32_t *mem;
+  uint32_t M, key_lo, key_hi;
+};
 void launch_wide_runs_xor(const SetView &s, const uint32_t *cid, const uint64_t *seg, const uint32_t *klist,
                           uint32_t nk, uint8_t *out, const WideOut &wo, uint8_t *route, uint64_t *stats,
-                          hipStream_t st);
+                          const XorRecords &xr, hipStream_t st);
 bool launch_wide_runs(int sem, const SetView &s, const uint32_t *cid, const uint64_t *seg, const uint32_t *klist,
-                      uint32_t nk, uint8_t *out, const WideOut &wo, uint8_t *route, uint64_t *stats, hipStream_t st);
+                      uint32_t nk, uint8_t *out, const WideOut &wo, uint8_t *route, uint64_t *stats,
+                      const XorRecords &xr, hipStream_t st);
 
 // ---- setops.hip
 void launch_bitmap_cards(const SetView &s, uint32_t nbitmaps, uint64_t *out, hipStream_t st);

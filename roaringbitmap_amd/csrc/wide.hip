@@ -645,7 +645,7 @@ int wide_run(rbgpu_ctx *ctx, int sem, const rbgpu_set *in, const std::vector<uin
   const uint32_t nmb = (M + MB - 1) / MB, nkr = (krange + KR - 1) / KR;
   uint32_t *d_mem = nullptr, *d_cid2 = nullptr, *d_klist = nullptr, *d_Hc = nullptr;
   uint64_t *d_bnd = nullptr, *d_H = nullptr, *d_tot = nullptr, *d_seg = nullptr, *d_active = nullptr,
-           *d_apos = nullptr, *d_tmp = nullptr;
+           *d_apos = nullptr, *d_tmp = nullptr, *d_rec = nullptr;
   const uint64_t N1 = std::max<uint64_t>(N, 1);
   const uint64_t tmpw = std::max<uint64_t>(scan_tmp_words(65537), 1);
   if (pool.alloc((void **)&d_mem, std::max<uint32_t>(M, 1) * 4ull) ||
@@ -658,8 +658,8 @@ int wide_run(rbgpu_ctx *ctx, int sem, const rbgpu_set *in, const std::vector<uin
     return fail(RB_ENOMEM, "wide workspace (%llu containers)", (unsigned long long)N);
   auto release = [&]() {
     for (void *p : {(void *)d_mem, (void *)d_bnd, (void *)d_Hc, (void *)d_H, (void *)d_cid2, (void *)d_tot,
-                    (void *)d_seg, (void *)d_active, (void *)d_apos, (void *)d_klist, (void *)d_tmp})
-      pool.release(p);
+                    (void *)d_seg, (void *)d_active, (void *)d_apos, (void *)d_klist, (void *)d_tmp, (void *)d_rec})
+      if (p) pool.release(p);
   };
   if (M) HIPCHK(hipMemcpyAsync(d_mem, members.data(), M * 4ull, hipMemcpyHostToDevice, st));
   const SetView sv = in->view();
@@ -726,12 +726,20 @@ int wide_run(rbgpu_ctx *ctx, int sem, const rbgpu_set *in, const std::vector<uin
   bool fast_ok = !getenv("RBGPU_NO_RUN_FASTPATH"); // parity tests run both paths
   if (pool.alloc((void **)&d_route, nk1)) d_route = nullptr;
   HIPCHK(hipEventRecord(ctx->ev[1], st));
+  // naive_xor's fast path reads key-major member records (wide_xor.hip); byte offsets fit 40 bits
+  XorRecords xr{nullptr, N, dense, d_mem, M, key_lo, key_hi};
   if (nk) {
     // Run-heavy keys first (all Run containers with <= 8 runs): route[q] = 0 when done there
     const bool fast = sem == RB_FAST_OR || sem == RB_WORKSHY_AND || sem == RB_FAST_XOR;
     if (fast && !d_route) fast_ok = false;
-    if (fast && fast_ok)
-      launch_wide_runs(sem, sv, d_cid2, d_seg, d_klist, nk, res->payload, wo, d_route, ctx->d_stats, st);
+    if (fast && fast_ok && sem == RB_FAST_XOR) {
+      if (in->payload_bytes >= (1ull << 40) || pool.alloc((void **)&d_rec, std::max<uint64_t>(N, 1) * 8))
+        fast_ok = false; // the generic kernel takes every key
+      xr.rec = d_rec;
+    }
+    if (fast && fast_ok && !launch_wide_runs(sem, sv, d_cid2, d_seg, d_klist, nk, res->payload, wo, d_route,
+                                             ctx->d_stats, xr, st))
+      fast_ok = false;
     const uint8_t *rt = fast && fast_ok ? d_route : nullptr;
     switch (sem) {
     case RB_FAST_OR: launch_reduce<RB_FAST_OR>(sv, d_cid2, d_seg, d_klist, nk, res->payload, wo, ctx->d_stats, st, rt); break;

@@ -447,7 +447,8 @@ __global__ __launch_bounds__(256) void k_wide_runs_and(SetView s, const uint32_t
 #endif
 
 bool launch_wide_runs(int sem, const SetView &s, const uint32_t *cid, const uint64_t *seg, const uint32_t *klist,
-                      uint32_t nk, uint8_t *out, const WideOut &wo, uint8_t *route, uint64_t *stats, hipStream_t st) {
+                      uint32_t nk, uint8_t *out, const WideOut &wo, uint8_t *route, uint64_t *stats,
+                      const XorRecords &xr, hipStream_t st) {
   const unsigned g = (nk + 3) / 4;
   switch (sem) {
   case RB_FAST_OR: k_wide_runs<RB_FAST_OR><<<g, 256, 0, st>>>(s, cid, seg, klist, nk, out, wo, route, stats); return true;
@@ -458,7 +459,8 @@ bool launch_wide_runs(int sem, const SetView &s, const uint32_t *cid, const uint
   }
   case RB_FAST_XOR:
 #if RBG_XOR_BATCHED
-    launch_wide_runs_xor(s, cid, seg, klist, nk, out, wo, route, stats, st);
+    if (!xr.rec) return false;
+    launch_wide_runs_xor(s, cid, seg, klist, nk, out, wo, route, stats, xr, st);
 #else
     k_wide_runs<RB_FAST_XOR><<<g, 256, 0, st>>>(s, cid, seg, klist, nk, out, wo, route, stats);
 #endif

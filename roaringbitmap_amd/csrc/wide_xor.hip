@@ -143,11 +143,71 @@ __device__ __forceinline__ uint32_t compose(uint32_t later, uint32_t earlier) {
   return out;
 }
 
+// Key-major member records.  The SoA metadata is member-major (container m * 65536 + k for dense
+// members), so a wave walking one key's members reads type / card / nruns / off as four lines per
+// member, ~5 L2 requests per container with the payload: the kernel was L2-request-bound (PMC:
+// TCC_BUSY 91 % of the kernel, 1.36G TCC requests per launch, 77 % hits) with its VALU at ~60 %.
+// A pre-pass packs each (key, member) into 8 B in key order — payload byte offset (40 bits), card (17),
+// min(nruns, 15) (4), type (2) — transposing 64 x 64 tiles through LDS so both its reads (along keys)
+// and its writes (along members) are coalesced; the kernel then reads one coalesced record per member.
+__host__ __device__ inline uint64_t pack_rec(uint32_t typ, uint32_t card, uint32_t nr, uint64_t off) {
+  return off | ((uint64_t)card << 40) | ((uint64_t)(nr < 15u ? nr : 15u) << 57) | ((uint64_t)(typ & 3u) << 61);
+}
+__device__ __forceinline__ uint32_t rec_type(uint64_t r) { return (uint32_t)(r >> 61) & 3u; }
+__device__ __forceinline__ uint32_t rec_card(uint64_t r) { return (uint32_t)(r >> 40) & 0x1FFFFu; }
+__device__ __forceinline__ uint32_t rec_nruns(uint64_t r) { return (uint32_t)(r >> 57) & 15u; }
+__device__ __forceinline__ uint64_t rec_off(uint64_t r) { return r & ((1ull << 40) - 1); }
+
+} // namespace
+
+// Dense members (container of key k in member mem[i] = begin[mem[i]] + k; k_group_dense's layout:
+// position (k - key_lo) * M + i): one 64-key x 64-member tile per block.
+__global__ __launch_bounds__(256) void k_xor_records_dense(SetView s, const uint32_t *__restrict__ mem, uint32_t M,
+                                                           uint32_t key_lo, uint32_t key_hi, uint64_t *__restrict__ rec) {
+  __shared__ uint64_t tile[64][65]; // [member][key], padded against bank conflicts on the column reads
+  const uint32_t k0 = key_lo + blockIdx.x * 64, m0 = blockIdx.y * 64;
+  const uint32_t t = threadIdx.x, kx = t & 63, ry = t >> 6;
+  // reads along keys: the 16 rows' container bases first, then all 64 metadata loads in flight at once
+  uint64_t rb[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) rb[j] = s.begin[mem[min(m0 + ry + 4 * j, M - 1)]];
+  const uint32_t k = min(k0 + kx, key_hi - 1);
+  uint32_t ty[16], cd[16], nr[16];
+  uint64_t of[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const uint64_t c = rb[j] + k;
+    ty[j] = s.type[c];
+    cd[j] = s.card[c];
+    nr[j] = s.nruns[c];
+    of[j] = s.off[c];
+  }
+#pragma unroll
+  for (int j = 0; j < 16; ++j) tile[ry + 4 * j][kx] = pack_rec(ty[j], cd[j], nr[j], of[j]);
+  __syncthreads();
+  for (uint32_t r = ry; r < 64; r += 4) { // writes along members
+    const uint32_t kw = k0 + r, i = m0 + kx;
+    if (i < M && kw < key_hi) rec[(uint64_t)(kw - key_lo) * M + i] = tile[kx][r];
+  }
+}
+// Any other grouping: a gather through the container ids (the grouped count, seg[65536], can be less
+// than the members' containers when the call is a key-range shard).
+__global__ __launch_bounds__(256) void k_xor_records_gather(SetView s, const uint32_t *__restrict__ cid,
+                                                            const uint64_t *__restrict__ seg, uint64_t *__restrict__ rec) {
+  const uint64_t n = seg[65536];
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
+    const uint32_t c = cid[i];
+    rec[i] = pack_rec(s.type[c], s.card[c], s.nruns[c], s.off[c]);
+  }
+}
+
+namespace {
+
 struct XBatch {
   uint32_t card, nr, typ;
   uint4 r; // runs 4h .. 4h+3 of the lane's container
 };
-__device__ __forceinline__ XBatch load_xbatch(const SetView &s, const uint32_t *cid, uint64_t i, uint64_t hi,
+__device__ __forceinline__ XBatch load_xbatch(const SetView &s, const uint64_t *rec, uint64_t i, uint64_t hi,
                                               int h) {
   XBatch b;
   b.card = 0;
@@ -155,12 +215,12 @@ __device__ __forceinline__ XBatch load_xbatch(const SetView &s, const uint32_t *
   b.typ = kRun;
   b.r = make_uint4(0, 0, 0, 0);
   if (i < hi) {
-    const uint32_t c = cid[i];
-    b.typ = s.type[c];
-    b.card = s.card[c];
-    b.nr = s.nruns[c];
+    const uint64_t r = rec[i];
+    b.typ = rec_type(r);
+    b.card = rec_card(r);
+    b.nr = rec_nruns(r);
     if (b.typ == kRun && b.nr <= 8 && b.nr > (uint32_t)(4 * h))
-      b.r = reinterpret_cast<const uint4 *>(s.payload + s.off[c])[h];
+      b.r = reinterpret_cast<const uint4 *>(s.payload + rec_off(r))[h];
   }
   return b;
 }
@@ -184,14 +244,14 @@ struct XState {
 // One exact batch of <= 32 containers starting at `base` (the accumulator P is the LDS bitmap `acc`):
 // every step's (c_j, r_j) from the sorted run boundaries, the type maps composed, P updated.  Returns
 // false when a container of the batch does not qualify (the key goes to the generic kernel).
-__device__ __forceinline__ bool exact_batch(const SetView &s, const uint32_t *cid, uint64_t base, uint64_t hi,
+__device__ __forceinline__ bool exact_batch(const SetView &s, const uint64_t *rec, uint64_t base, uint64_t hi,
                                             uint32_t *acc, uint32_t *R, int lane, XState &X) {
   uint16_t *R16 = reinterpret_cast<uint16_t *>(R);
   uint16_t *pos = R16 + 2048;                       // [512] sorted position | tie/boundary bit 15
   uint2 *MC = reinterpret_cast<uint2 *>(R);         // [512] (coverage mask, c0 | c1 << 16)
   const int cj = lane >> 1, h = lane & 1;
   const uint32_t below = (1u << cj) - 1u;
-  const XBatch cur = load_xbatch(s, cid, base + cj, hi, h);
+  const XBatch cur = load_xbatch(s, rec, base + cj, hi, h);
   const bool valid = base + (uint64_t)cj < hi;
   const bool bad = valid && (cur.typ != kRun || cur.nr > 8u || cur.card >= (uint32_t)kSpan);
   if (__ballot(bad)) return false;
@@ -412,9 +472,9 @@ struct XWin { // one container per lane: the fast-forward window
   uint4 r0, r1;
   uint32_t pairx; // even lanes: |C_lane ⊕ C_lane+1| (set by pair_xor)
 };
-// A window's loads form a chain (container id -> metadata -> run list), so they are software-pipelined
-// over four windows: the id of window w+3, the metadata of w+2 and the runs of w+1 are in flight while
-// window w is processed, and every load issued at an advance only uses values loaded a window earlier.
+// A window's loads form a chain (record -> run list), so they are software-pipelined over three windows:
+// the records of window w+2 and the runs of w+1 are in flight while window w is processed, and every
+// load issued at an advance only uses values loaded a window earlier.
 struct XMeta {
   uint32_t typ, card, nr;
   uint64_t off;
@@ -422,17 +482,12 @@ struct XMeta {
 // The loads are unconditional (addresses clamped to valid memory, results selected afterwards): a load
 // under a branch makes the waitcnt pass assume the worst at the merge and wait for every load in flight,
 // which would expose the whole chain's latency at every window.
-__device__ __forceinline__ XMeta load_xmeta(const SetView &s, uint32_t c, bool valid) {
+__device__ __forceinline__ XMeta xmeta_of(uint64_t r, bool valid) {
   XMeta m;
-  m.typ = s.type[c];
-  m.card = s.card[c];
-  m.nr = s.nruns[c];
-  m.off = s.off[c];
-  if (!valid) {
-    m.typ = kRun;
-    m.card = m.nr = 0u;
-    m.off = 0ull;
-  }
+  m.typ = valid ? rec_type(r) : (uint32_t)kRun;
+  m.card = valid ? rec_card(r) : 0u;
+  m.nr = valid ? rec_nruns(r) : 0u;
+  m.off = valid ? rec_off(r) : 0ull;
   return m;
 }
 __device__ __forceinline__ XWin xwin_from(const SetView &s, const XMeta &m) {
@@ -475,8 +530,27 @@ __device__ __forceinline__ void pair_xor(XWin &w) {
 #ifndef RBG_XOR_MIN_FAST
 #define RBG_XOR_MIN_FAST 8 // shortest stretch worth a fast-forward (an exact batch costs ~32 stretches' steps)
 #endif
+// Union stretches.  The pair bounds above limit an AB stretch to about one window when the members'
+// XOR can reach the accumulator's size (config 4: |C ⊕ C'| ~ 900 per pair, ~29k per window against
+// c ~ 32k), so every window paid a toggle -> word conversion and a re-measure (~600 of ~1100 VALU per
+// window, ISA count).  A second, bound-free proof covers whole windows at once: every member of a
+// stretch lies inside U, the union of its runs, so each intermediate X_j ⊆ U and
+//   c_j = |P ⊕ X_j| >= |P \ U| >= |P \ U'|      for any U' ⊇ U,
+// with U' = U rounded out to 64-bit words (a 1024-bit touched-word mask in LDS, one or two atomic ORs
+// per run).  While |P \ U'| >= 32 every step of an AB-typed accumulator is AB(c_j) (c_j >= 32, never
+// empty), so the windows' toggles accumulate in the toggle image with no conversion at all; the stretch
+// closes (one conversion, one re-measure of c) when the next window would push |P \ U'| below 32.
+#ifndef RBG_XOR_UNION
+#define RBG_XOR_UNION 1
+#endif
+#ifndef RBG_XOR_TRACE
+#define RBG_XOR_TRACE 0 // 1: per-key stretch counts of three keys (printf; study builds only)
+#endif
+#ifndef RBG_XOR_UNION_MIN_C
+#define RBG_XOR_UNION_MIN_C 1024 // try a union stretch only above this c (a heuristic: results do not depend on it)
+#endif
 
-__global__ __launch_bounds__(256, 3) void k_wide_runs_xor(SetView s, const uint32_t *__restrict__ cid,
+__global__ __launch_bounds__(256, 3) void k_wide_runs_xor(SetView s, const uint64_t *__restrict__ rec,
                                                           const uint64_t *__restrict__ seg,
                                                           const uint32_t *__restrict__ klist, uint32_t nk,
                                                           uint8_t *__restrict__ out, WideOut wo,
@@ -494,7 +568,7 @@ __global__ __launch_bounds__(256, 3) void k_wide_runs_xor(SetView s, const uint3
   uint32_t *R = reg_all[wv];
   const uint32_t key = klist[q];
   const uint64_t lo = seg[key], hi = seg[key + 1];
-  if (hi <= lo || s.type[cid[lo]] != kRun) { // (no member) / first container not a Run: the generic kernel
+  if (hi <= lo || rec_type(rec[lo]) != (uint32_t)kRun) { // (no member) / first container not a Run: the generic kernel
     if (lane == 0) route[q] = 1;
     return;
   }
@@ -506,18 +580,49 @@ __global__ __launch_bounds__(256, 3) void k_wide_runs_xor(SetView s, const uint3
   XState X{3, 0, 0, 0u, 1};
   bool fail_route = false;
   uint64_t wbase = lo;
-  auto cid_at = [&](uint64_t i) { // unconditional load (see load_xmeta); hi > lo here
-    const uint32_t c = cid[i < hi ? i : hi - 1];
-    return i < hi ? c : 0u;
+  auto rec_at = [&](uint64_t i) { // unconditional load (clamped address, selected later); hi > lo here
+    return rec[i < hi ? i : hi - 1];
   };
-  const uint32_t c0 = cid_at(lo + lane), c1 = cid_at(lo + 64 + lane), c2 = cid_at(lo + 128 + lane);
-  const XMeta m0 = load_xmeta(s, c0, lo + lane < hi), m1 = load_xmeta(s, c1, lo + 64 + lane < hi);
-  XWin W = xwin_from(s, m0);                                 // window w
-  XWin N = xwin_from(s, m1);                                 // w+1: runs in flight
-  XMeta NN = load_xmeta(s, c2, lo + 128 + lane < hi);        // w+2: metadata in flight
-  uint32_t NNN = cid_at(lo + 192 + lane);                    // w+3: id in flight
+  const uint64_t r0 = rec_at(lo + lane), r1 = rec_at(lo + 64 + lane);
+  XWin W = xwin_from(s, xmeta_of(r0, lo + lane < hi));       // window w
+  XWin N = xwin_from(s, xmeta_of(r1, lo + 64 + lane < hi));  // w+1: runs in flight
+  uint64_t NN = rec_at(lo + 128 + lane);                     // w+2: record in flight
   pair_xor(W);
   uint64_t base = lo;
+  // union stretch state: windows whose toggles are pending in acc (P = Pw, X describe the accumulator
+  // before them) and their touched-word mask M (in R, which only exact batches use otherwise)
+  uint32_t *M = R;                                      // [32] touched 64-bit words (1024 bits)
+  uint8_t *pcT = reinterpret_cast<uint8_t *>(R + 32);   // [1024] popcount of each word of P
+  int upend = 0;
+  bool urun = false; // flavour of the pending stretch: Run (every step stays a Run) or AB
+  int usum = 0;      // Run flavour: Σ nruns of the pending windows (r_j <= X.r + usum)
+  bool wpx = true;   // W.pairx is current
+#if RBG_XOR_TRACE
+  int tr_u = 0, tr_f = 0, tr_rej = 0, tr_p = 0, tr_pb = 0, tr_e = 0;
+#define RBG_TR(x) x
+#else
+#define RBG_TR(x)
+#endif
+  // the pending windows' XOR into P and (c, r) re-measured: the state is AB(c) (AB flavour) or Run
+  auto flush_union = [&]() {
+    wave_lds_sync();
+    uint64_t t[kW];
+    lds_read_words(acc, t, lane);
+    wave_lds_sync();
+    lds_zero(acc, lane);
+    toggles_to_words(t, lane);
+#pragma unroll
+    for (int j = 0; j < kW; ++j) Pw[j] ^= t[j];
+    int cc = X.c, rr = X.r;
+    metrics(Pw, lane, urun, cc, rr);
+    X.c = cc;
+    X.r = rr;
+    X.rvalid = urun;
+    X.state = urun ? (int)kRun : type_ab(cc);
+    upend = 0;
+    wave_lds_sync();
+  };
+  static_assert(kXRegion >= 32 + 256, "M and pcT fit the exact batches' region");
   while (base < hi) {
     const uint32_t posw = __builtin_amdgcn_readfirstlane((uint32_t)(base - wbase)); // < 64
     const bool inwin = (uint32_t)lane >= posw && wbase + (uint64_t)lane < hi;
@@ -525,8 +630,100 @@ __global__ __launch_bounds__(256, 3) void k_wide_runs_xor(SetView s, const uint3
       fail_route = true;
       break;
     }
-    // ---- the longest stretch from posw that provably crosses no threshold (see above)
     const uint32_t wlen = (uint32_t)min<uint64_t>(64, hi - wbase); // containers in the window
+    // window's Σ nruns (the Run flavour's r bound); a Run stretch needs 2 + 4 r_j <= min(8192, 2 c_j + 2)
+    const int wnr = RBG_XOR_UNION && fastfwd && posw == 0 && (upend ? urun : X.state == kRun)
+                        ? (int)wave_sum_u32((uint32_t)lane < wlen ? W.nr : 0u) : 0;
+    const bool ab_in = X.state == kBitmap || (X.state == kArray && X.c >= RBG_XOR_UNION_MIN_C);
+    const bool run_in = X.state == kRun && X.rvalid && X.c >= RBG_XOR_UNION_MIN_C &&
+                        X.r + wnr <= 2047 && X.c >= 4 * (X.r + wnr); // |P \ U'| ~ c / 2 after a window
+    if (RBG_XOR_UNION && fastfwd && posw == 0 && (upend || ab_in || run_in)) {
+      // ---- union stretch: mark the window's words, then |P \ U'| decides (see RBG_XOR_UNION)
+      const bool mem = (uint32_t)lane < wlen;
+      if (!upend) { // a new stretch: clear U', and the per-word popcounts of P for |P \ U'|
+        urun = !ab_in;
+        usum = 0;
+        if (lane < 32) M[lane] = 0u;
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+          reinterpret_cast<uint16_t *>(pcT)[64 * k + lane] =
+              (uint16_t)(__popcll(Pw[2 * k]) | (__popcll(Pw[2 * k + 1]) << 8));
+        wave_lds_sync();
+      }
+      if (mem) {
+        const uint32_t rw[8] = {W.r0.x, W.r0.y, W.r0.z, W.r0.w, W.r1.x, W.r1.y, W.r1.z, W.r1.w};
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          if ((uint32_t)u < W.nr) {
+            const uint32_t st = rw[u] & 0xFFFF, en = st + (rw[u] >> 16);
+            const uint32_t w0 = st >> 6, w1 = en >> 6, d0 = w0 >> 5, d1 = w1 >> 5;
+            const uint32_t mlo = 0xFFFFFFFFu << (w0 & 31), mhi = 0xFFFFFFFFu >> (31 - (w1 & 31));
+            atomicOr(&M[d0], d0 == d1 ? (mlo & mhi) : mlo);
+            if (d1 != d0) {
+              atomicOr(&M[d1], mhi);
+              for (uint32_t d = d0 + 1; d < d1; ++d) atomicOr(&M[d], 0xFFFFFFFFu); // runs over 2048 values
+            }
+          }
+        }
+      }
+      wave_lds_sync();
+      // |P \ U'|: lane l sums the popcounts of words 16 l .. 16 l + 15 not in U'
+      uint32_t ls = 0;
+      {
+        const uint4 pcv = reinterpret_cast<const uint4 *>(pcT)[lane];
+        const uint32_t tv = (M[lane >> 1] >> (16 * (lane & 1))) & 0xFFFFu;
+        const uint32_t p4[4] = {pcv.x, pcv.y, pcv.z, pcv.w};
+#pragma unroll
+        for (int qd = 0; qd < 4; ++qd) {
+          const uint32_t nib = (tv >> (4 * qd)) & 15u;
+          const uint32_t bm = ((nib * 0x00204081u) & 0x01010101u) * 0xFFu; // touched words' bytes
+          const uint32_t v = p4[qd] & ~bm;
+          ls += (v & 0x00FF00FFu) + ((v >> 8) & 0x00FF00FFu);
+        }
+        ls = (ls & 0xFFFFu) + (ls >> 16);
+      }
+      const int L = (int)wave_sum_u32(ls);
+      const int rub = X.r + usum + wnr; // >= every r_j of the stretch (Run flavour)
+      if (urun ? (2 + 4 * rub <= min(kBitmapBytes, 2 * L + 2)) : L >= kRunArrayThreshold) {
+        usum += wnr;
+        if (mem) {
+          const uint32_t rw[8] = {W.r0.x, W.r0.y, W.r0.z, W.r0.w, W.r1.x, W.r1.y, W.r1.z, W.r1.w};
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            if ((uint32_t)u < W.nr) {
+              const uint32_t st = rw[u] & 0xFFFF, e1 = st + (rw[u] >> 16) + 1;
+              atomicXor(&acc[st >> 5], 1u << (st & 31));
+              if (e1 < (uint32_t)kSpan) atomicXor(&acc[e1 >> 5], 1u << (e1 & 31));
+            }
+          }
+          X.inb += 4u * W.nr + 2u + 16u;
+        }
+        ++upend;
+        RBG_TR(++tr_u);
+        base += wlen;
+        wave_lds_sync();
+        if (base < hi) {
+          wbase += 64;
+          W = N;
+          N = xwin_from(s, xmeta_of(NN, wbase + 64 + lane < hi));
+          NN = rec_at(wbase + 128 + lane);
+          wpx = false;
+        }
+        continue;
+      }
+      // this window would let U' cover too much of P: close the stretch before it, and take the
+      // window again (a fresh stretch, or the per-window rules)
+      RBG_TR(++tr_rej);
+      if (upend) {
+        RBG_TR(++tr_f);
+        flush_union();
+      }
+    }
+    if (!wpx) { // the window's pair bounds, computed only where the per-window rules need them
+      pair_xor(W);
+      wpx = true;
+    }
+    // ---- the longest stretch from posw that provably crosses no threshold (see above)
     const int nr_first = (int)readlane(W.nr, (int)posw), card_first = (int)readlane(W.card, (int)posw);
     const uint32_t first_even = posw + (posw & 1u);
     const uint32_t pair_in = dpp<0x138>(W.pairx); // wave_shr:1 — the pair (lane-1, lane) on its odd lane
@@ -579,6 +776,7 @@ __global__ __launch_bounds__(256, 3) void k_wide_runs_xor(SetView s, const uint3
       X.rvalid = mode == 2;
       X.state = mode == 1 ? type_ab(cc) : kRun;
       base += B;
+      RBG_TR(++tr_p; tr_pb += B);
     } else {
       if (!X.rvalid) {
         int cc, rr;
@@ -588,7 +786,7 @@ __global__ __launch_bounds__(256, 3) void k_wide_runs_xor(SetView s, const uint3
       }
       lds_write_words(acc, Pw, lane);
       wave_lds_sync();
-      if (!exact_batch(s, cid, base, hi, acc, R, lane, X)) {
+      if (!exact_batch(s, rec, base, hi, acc, R, lane, X)) {
         fail_route = true;
         break;
       }
@@ -596,23 +794,32 @@ __global__ __launch_bounds__(256, 3) void k_wide_runs_xor(SetView s, const uint3
       wave_lds_sync();
       lds_zero(acc, lane);
       base += kXB;
+      RBG_TR(++tr_e);
     }
     wave_lds_sync();
     if (base >= wbase + 64 && base < hi) {
       wbase += 64;
       if (!(RBG_XF_ABLATE & 16)) {
         W = N;
-        N = xwin_from(s, NN);
-        NN = load_xmeta(s, NNN, wbase + 128 + lane < hi);
-        NNN = cid_at(wbase + 192 + lane);
+        N = xwin_from(s, xmeta_of(NN, wbase + 64 + lane < hi));
+        NN = rec_at(wbase + 128 + lane);
       }
-      if (!(RBG_XF_ABLATE & 8)) pair_xor(W);
+      wpx = false;
     }
   }
   if (fail_route) {
     if (lane == 0) route[q] = 1;
     return;
   }
+  if (upend) {
+    RBG_TR(++tr_f);
+    flush_union();
+  }
+#if RBG_XOR_TRACE
+  if (lane == 0 && (q == 1000 || q == 30000 || q == 65000))
+    printf("xor trace key %u: union windows %d flushes %d refused %d | per-window stretches %d (members %d) | exact %d | c %d state %d\n",
+           q, tr_u, tr_f, tr_rej, tr_p, tr_pb, tr_e, X.c, X.state);
+#endif
   // ---- result
   uint8_t *dst = out + (uint64_t)q * kBitmapBytes;
   const int ty = X.state == 3 ? (int)kEmpty : X.state;
@@ -645,12 +852,19 @@ __global__ __launch_bounds__(256, 3) void k_wide_runs_xor(SetView s, const uint3
 
 void launch_wide_runs_xor(const SetView &s, const uint32_t *cid, const uint64_t *seg, const uint32_t *klist,
                           uint32_t nk, uint8_t *out, const WideOut &wo, uint8_t *route, uint64_t *stats,
-                          hipStream_t st) {
+                          const XorRecords &xr, hipStream_t st) {
   if (!nk) return;
   // RBGPU_XOR_NO_FASTFWD=1: exact batches only (an A/B switch for the parity tests)
   const char *e = getenv("RBGPU_XOR_NO_FASTFWD");
   const int fastfwd = !(e && e[0] == '1');
-  k_wide_runs_xor<<<(nk + 3) / 4, 256, 0, st>>>(s, cid, seg, klist, nk, out, wo, route, stats, fastfwd);
+  if (xr.dense) {
+    const uint32_t krange = xr.key_hi - xr.key_lo;
+    k_xor_records_dense<<<dim3((krange + 63) / 64, (xr.M + 63) / 64), 256, 0, st>>>(s, xr.mem, xr.M, xr.key_lo,
+                                                                                  xr.key_hi, xr.rec);
+  } else if (xr.n) {
+    k_xor_records_gather<<<(unsigned)std::min<uint64_t>((xr.n + 255) / 256, 65536), 256, 0, st>>>(s, cid, seg, xr.rec);
+  }
+  k_wide_runs_xor<<<(nk + 3) / 4, 256, 0, st>>>(s, xr.rec, seg, klist, nk, out, wo, route, stats, fastfwd);
 }
 
 } // namespace rbg

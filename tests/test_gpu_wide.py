@@ -368,6 +368,47 @@ def test_xor_fastforward_threshold_regimes(ctx, oracle):
             del os.environ["RBGPU_XOR_NO_FASTFWD"]
 
 
+def test_xor_union_stretches(ctx, oracle):
+    """naive_xor union stretches (wide_xor.hip, RBG_XOR_UNION): whole windows of 64 members are
+    XORed without re-measuring while |P \\ U'| >= 32 (U' = the windows' runs rounded out to 64-bit
+    words); chains of 1100 members so stretches span many windows and close on that bound:
+      key 0  config-4 shape: stretches of several windows, closed as U' covers the key;
+      key 1  runs confined to [0, 8192) with c ~ 4096: U' covers P within a window or two (the
+             window is refused, the per-window rules take it);
+      key 2  the same plus a fixed 20-value run at 60000 in member 0 only: |P \\ U'| hovers near 32;
+      key 3  the same with a 40-value run (|P \\ U'| >= 40 holds: one stretch to the end).
+    Bytes must equal the oracle's and those with the fast-forward off."""
+    import os
+
+    import roaringbitmap_amd as rb
+    rng = np.random.default_rng(55)
+    nb = 1100
+    per = []
+    for b in range(nb):
+        p0 = np.unique(np.concatenate([np.arange(20000, 21024), _runs_container(rng, 7, 0, 65536, 256)]))
+        p1 = _runs_container(rng, int(rng.integers(1, 9)), 0, 8192, 400)
+        p2 = _runs_container(rng, int(rng.integers(1, 8)), 0, 8192, 400)
+        p3 = _runs_container(rng, int(rng.integers(1, 8)), 0, 8192, 400)
+        if b == 0:
+            p2 = np.unique(np.concatenate([p2, np.arange(60000, 60020)]))
+            p3 = np.unique(np.concatenate([p3, np.arange(60000, 60040)]))
+        parts = [p0, p1, p2, p3]
+        per.append(np.concatenate([(p.astype(np.uint32) % 65536) | np.uint32(k << 16) for k, p in enumerate(parts)]))
+    s = ctx.upload_values(per, run_optimize=True)
+    h = s.download()
+    assert set(h.type.tolist()) == {rb.RUN} and int(h.nruns.max()) <= 8
+    refs = [oracle.RefBitmap.deserialize(x) for x in s.serialize()]
+    for n in (nb, 700, 321):
+        members = np.arange(n, dtype=np.uint32)
+        want = oracle.wide(oracle.FAST_XOR, [refs[m] for m in members]).serialize()
+        assert ctx.wide(rb.FAST_XOR, s, members).serialize()[0] == want, n
+        os.environ["RBGPU_XOR_NO_FASTFWD"] = "1"
+        try:
+            assert ctx.wide(rb.FAST_XOR, s, members).serialize()[0] == want, n
+        finally:
+            del os.environ["RBGPU_XOR_NO_FASTFWD"]
+
+
 def test_queue_order_ties(ctx, oracle):
     """horizontal_or / horizontal_xor / priorityqueue_xor where many containers of a key tie on
     cardinality (the java.util.PriorityQueue's tie order then picks which types meet first) and
