@@ -356,6 +356,9 @@ __device__ __forceinline__ RecU load_rec(const TaskRec *r) {
 #ifndef RBG_FILTER_TRANSPOSE
 #define RBG_FILTER_TRANSPOSE 1 // probe a row in value order (adjacent lanes, adjacent values)
 #endif
+#ifndef RBG_FILTER_LINEAR
+#define RBG_FILTER_LINEAR 1 // the transposed filter with a linear stage (filter_rows_linear; 0: the ring)
+#endif
 #ifndef RBG_LIGHT_WAVES
 #define RBG_LIGHT_WAVES 4 // waves per SIMD of the copy + filter kernel (128 VGPRs)
 #endif
@@ -686,8 +689,13 @@ __global__ __launch_bounds__(256, ROLE == kRoleHeavy ? RBG_HEAVY_WAVES : RBG_LIG
         (void)nfc;
         (void)none;
         uint4 *tb = tbuf[ROLE == kRoleLight ? wv : 0];
+#if RBG_FILTER_LINEAR
+        c = OP == RB_ANDNOT ? filter_rows_linear<true, !CARD_ONLY>(pq, (int)tc.cp, s, ob, tb, o, lane)
+                            : filter_rows_linear<false, !CARD_ONLY>(pq, (int)tc.cp, s, ob, tb, o, lane);
+#else
         c = OP == RB_ANDNOT ? filter_rows_transposed<true>(pq, (int)tc.cp, s, ob, tb, o, lane)
                             : filter_rows_transposed<false>(pq, (int)tc.cp, s, ob, tb, o, lane);
+#endif
 #else
         c = OP == RB_ANDNOT ? filter_chunks_staged<true>(pq, nfc, (int)tc.cp, s, ob, o, lane, none)
                             : filter_chunks_staged<false>(pq, nfc, (int)tc.cp, s, ob, o, lane, none);

@@ -476,6 +476,73 @@ __device__ __forceinline__ int filter_rows_transposed(const uint4 (&fq)[8], int 
   return (int)tot;
 }
 
+// filter_rows_transposed with a LINEAR stage instead of a ring: after each row's flush the partial
+// block (< 8 kept values) moves to the front, so a kept value's slot is (pending + mbcnt) with no
+// wrap — mbcnt adds the pending count itself — and rejected lanes are masked off instead of writing a
+// dummy slot.  ~8 VALU per 64 probed values instead of ~15 (ISA count).  Pending values stay < 8 + 512.
+template <bool NEGATE, bool STORE>
+__device__ __forceinline__ int filter_rows_linear(const uint4 (&fq)[8], int nf, const uint32_t *s, uint16_t *ob,
+                                                  uint4 *tb, uint16_t *out, int lane) {
+  static_assert(7 + 512 <= kStageRing, "every slot (pending < 8, + < 512 of a row) lies below the dummies");
+  const int iters = (nf + 511) >> 9; // wave-uniform, <= 8
+  uint32_t tot = 0, flushed = 0;     // kept / written out so far (wave-uniform; flushed % 8 == 0)
+  uint4 *out4 = reinterpret_cast<uint4 *>(out);
+  uint4 *ob4 = reinterpret_cast<uint4 *>(ob);
+  const uint16_t *t16 = reinterpret_cast<const uint16_t *>(tb);
+  typedef __attribute__((address_space(3))) const uint32_t lds_u32;
+  lds_u32 *ls = (lds_u32 *)s;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    if (i < iters) {
+#pragma unroll
+      for (int hf = 0; hf < 2; ++hf) {
+        if ((lane >> 5) == hf) tb[lane & 31] = fq[i];
+        wave_lds_sync();
+        const int nh = min(256, nf - 512 * i - 256 * hf); // values of this half (may be <= 0)
+        uint32_t y[4], m[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) y[k] = t16[64 * k + lane];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) { // word y >> 5 of the image: v_bfe + v_lshl_add (the compiler's
+          uint32_t wi;                 // own lowering of the same index takes four VALU)
+          asm("v_bfe_u32 %0, %1, 5, 11" : "=v"(wi) : "v"(y[k]));
+          m[k] = ls[wi];
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          // membership bit (v_bfe reads the offset's low 5 bits), its ballot as an integer compare (no
+          // bool round trip), lanes past the half masked off in scalar registers
+          const uint32_t bit = __builtin_amdgcn_ubfe(m[k], y[k], 1u);
+          uint64_t b = __builtin_amdgcn_uicmp(bit, 0u, NEGATE ? 32 : 33); // ICMP_EQ / ICMP_NE
+          const int lim = nh - 64 * k;
+          if (lim < 64) b &= lim > 0 ? (1ull << lim) - 1ull : 0ull;
+          if (STORE) {
+            // kept lanes take the next slots of the linear stage, the others a per-lane dummy (a lane past
+            // the half may land on the slot after the last kept value: never read as a value)
+            const uint32_t pos =
+                __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, tot - flushed));
+            uint32_t slot;
+            asm("v_cndmask_b32 %0, %1, %2, %3" : "=v"(slot) : "v"((uint32_t)(kStageRing + lane)), "v"(pos), "s"(b));
+            ob[slot] = (uint16_t)y[k];
+          }
+          tot += (uint32_t)__popcll(b);
+        }
+      }
+      if (STORE) {
+        wave_lds_sync(); // the blocks hold other lanes' values
+        const uint32_t pend = tot - flushed, nb = pend >> 3;
+        if ((uint32_t)lane < nb) out4[(flushed >> 3) + lane] = ob4[lane];
+        if (lane == 0 && nb && (pend & 7u)) ob4[0] = ob4[nb]; // the partial block to the front
+        wave_lds_sync();
+        flushed += nb << 3;
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  if (STORE && tot > flushed && lane == 0) out4[flushed >> 3] = ob4[0];
+  return (int)tot;
+}
+
 __device__ __forceinline__ void store_chunks(const uint4 (&q)[8], uint8_t *p, uint32_t bytes, int lane) {
   uint4 *p4 = reinterpret_cast<uint4 *>(p);
   const int n = (int)((bytes + 15) >> 4);
