@@ -356,6 +356,12 @@ __device__ __forceinline__ RecU load_rec(const TaskRec *r) {
 #ifndef RBG_FILTER_TRANSPOSE
 #define RBG_FILTER_TRANSPOSE 1 // probe a row in value order (adjacent lanes, adjacent values)
 #endif
+#ifndef RBG_LIGHT_TIMING
+#define RBG_LIGHT_TIMING 0 // study builds: per-phase s_memtime totals of a few light waves (printf)
+#endif
+#ifndef RBG_LIGHT_ABLATE
+#define RBG_LIGHT_ABLATE 0 // timing study only (wrong results): skip staging X = 1 Bitmap, 2 Array, 4 Run; 8 skip the filter
+#endif
 #ifndef RBG_FILTER_LINEAR
 #define RBG_FILTER_LINEAR 1 // the transposed filter with a linear stage (filter_rows_linear; 0: the ring)
 #endif
@@ -575,6 +581,12 @@ __global__ __launch_bounds__(256, ROLE == kRoleHeavy ? RBG_HEAVY_WAVES : RBG_LIG
   RecU cur = load_rec(recs + g);
   Task tc = decode_task<OP>(cur, pay_a, pay_b);
   uint4 pq[8], qq[8];
+#if RBG_LIGHT_TIMING
+  uint64_t lt_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, lt0 = 0, lt1 = 0, lt2 = 0; // decode, stage B/A/R, copy, filter, iteration, tasks
+#define RBG_LT(x) if (ROLE == kRoleLight) { x; }
+#else
+#define RBG_LT(x)
+#endif
   load_chunks(pq, tc.pp, tc.bigp ? 16u : tc.pbytes, lane);
   if (tc.kind == kCopy || tc.bigq) load_chunks(qq, tc.pp, 16, lane);
   else load_chunks(qq, tc.pq, tc.qbytes, lane);
@@ -589,8 +601,10 @@ __global__ __launch_bounds__(256, ROLE == kRoleHeavy ? RBG_HEAVY_WAVES : RBG_LIG
       }
     }
     const bool has_next = gn < n;
+    RBG_LT(lt0 = __builtin_amdgcn_s_memtime());
     const RecU nx = load_rec(recs + (has_next ? gn : g));
     const Task tn = decode_task<OP>(nx, pay_a, pay_b);
+    RBG_LT(lt1 = __builtin_amdgcn_s_memtime(); lt_acc[0] += lt1 - lt0);
     int ty = kEmpty, c = 0;
     uint32_t nr = 0;
     uint8_t *dst = out + cur.out;
@@ -667,7 +681,7 @@ __global__ __launch_bounds__(256, ROLE == kRoleHeavy ? RBG_HEAVY_WAVES : RBG_LIG
       nr = ty == kRun ? (uint32_t)r : 0u;
     } else if (ROLE != kRoleHeavy) {
       // ---- phase 1: stage X (filter) or store the clone (copy)
-      if (tc.kind == kFilter) {
+      if (tc.kind == kFilter && !(RBG_LIGHT_ABLATE & (tc.tq == kBitmap ? 1 : tc.tq == kArray ? 2 : 4))) {
         if (tc.bigq) stage_big_runs(tc.pq, tc.rq, s, lane); // only a Run payload exceeds 8 KiB
         else stage_from_chunks(tc.tq, qq, tc.cq, tc.rq, s, lane);
       } else if (!CARD_ONLY) {
@@ -678,10 +692,11 @@ __global__ __launch_bounds__(256, ROLE == kRoleHeavy ? RBG_HEAVY_WAVES : RBG_LIG
         const bool real = has_next && tn.kind != kCopy && !tn.bigq;
         load_chunks(qq, real ? tn.pq : tn.pp, real ? tn.qbytes : 16u, lane);
       }
+      RBG_LT(lt2 = __builtin_amdgcn_s_memtime(); lt_acc[tc.kind == kFilter ? 1 + (tc.tq == kBitmap ? 0 : tc.tq == kArray ? 1 : 2) : 4] += lt2 - lt1);
       // ---- phase 2: filter F against the staged X.  (Streaming the next F into pq row by row as
       //      the filter frees it measured 7% slower: loads and the staged stores share vmcnt, so
       //      the loads issued mid-filter serialise the output flushes behind them.)
-      if (tc.kind == kFilter) {
+      if (tc.kind == kFilter && !(RBG_LIGHT_ABLATE & 8)) {
         const int nfc = (int)((tc.cp + 7) >> 3);
         uint16_t *o = CARD_ONLY ? nullptr : reinterpret_cast<uint16_t *>(dst);
         auto none = [](int) {};
@@ -706,6 +721,7 @@ __global__ __launch_bounds__(256, ROLE == kRoleHeavy ? RBG_HEAVY_WAVES : RBG_LIG
         c = (int)tc.cp;
         nr = tc.rp;
       }
+      RBG_LT(lt_acc[5] += __builtin_amdgcn_s_memtime() - lt2);
       load_chunks(pq, tn.pp, tn.bigp ? 16u : tn.pbytes, lane);
     }
     wave_lds_sync(); // the next task restages the same LDS image
@@ -714,6 +730,7 @@ __global__ __launch_bounds__(256, ROLE == kRoleHeavy ? RBG_HEAVY_WAVES : RBG_LIG
       tm.card[cur.t] = (uint32_t)c;
       tm.nruns[cur.t] = (uint16_t)nr;
     }
+    RBG_LT(lt_acc[6] += __builtin_amdgcn_s_memtime() - lt0; ++lt_acc[7]);
     if (!has_next) break;
     if (new_chunk) {
       cend = nend;
@@ -725,6 +742,11 @@ __global__ __launch_bounds__(256, ROLE == kRoleHeavy ? RBG_HEAVY_WAVES : RBG_LIG
     cur = nx;
     tc = tn;
   }
+#if RBG_LIGHT_TIMING
+  if (ROLE == kRoleLight && lane == 0 && wv == 0 && blockIdx.x % 97 == 0)
+    printf("light timing blk %u: decode %lu stageB %lu stageA %lu stageR %lu copy %lu filter %lu iter %lu tasks %lu\n",
+           blockIdx.x, lt_acc[0], lt_acc[1], lt_acc[2], lt_acc[3], lt_acc[4], lt_acc[5], lt_acc[6], lt_acc[7]);
+#endif
 }
 
 // The register path without a software pipeline: ONE WAVE PER TASK, one launch-sized grid (3
