@@ -91,8 +91,9 @@ SIGNATURES = {
     "rbgpu_set_serialize": (C.c_int, [_P, C.c_uint32, C.c_uint32, C.c_void_p, C.c_uint64, _U64P]),
     "rbgpu_set_serialize_device": (C.c_int, [_P, C.c_uint32, C.c_uint32, C.c_void_p, C.c_uint64, _U64P]),
     "rbgpu_set_download": (C.c_int, [_P, C.c_uint32, C.c_uint32, C.POINTER(RbSoa)]),
-    "rbgpu_pairwise": (C.c_int, [_P, C.c_int, _P, _P, _U32P, _U32P, C.c_uint32, C.POINTER(_P)]),
-    "rbgpu_pairwise_cardinality": (C.c_int, [_P, C.c_int, _P, _P, _U32P, _U32P, C.c_uint32, _U64P]),
+    # index arrays as void* (engine passes plain addresses: see engine._idx_addr)
+    "rbgpu_pairwise": (C.c_int, [_P, C.c_int, _P, _P, _P, _P, C.c_uint32, C.POINTER(_P)]),
+    "rbgpu_pairwise_cardinality": (C.c_int, [_P, C.c_int, _P, _P, _P, _P, C.c_uint32, _U64P]),
     "rbgpu_wide": (C.c_int, [_P, C.c_int, _P, _U32P, C.c_uint32, C.POINTER(_P)]),
     "rbgpu_wide_keys": (C.c_int, [_P, C.c_int, _P, _U32P, C.c_uint32, C.c_uint32, C.c_uint32, C.POINTER(_P)]),
     "rbgpu_wide_cardinality": (C.c_int, [_P, C.c_int, _P, _U32P, C.c_uint32, _U64P]),

@@ -685,6 +685,9 @@ static uint32_t pairwise_seg_keys(const rbgpu_set *a, const rbgpu_set *b, uint64
   while (seg > 8 && est / seg < 131072.0) seg >>= 1;
   return seg;
 }
+#ifndef RBG_SMALL_EVENTS
+#define RBG_SMALL_EVENTS 0 // 1: always time the small-batch kernels with events
+#endif
 // Small batches (kernels.hpp: <= kSmallPairs pairs of <= kSmallPairKeys keys, <= kSmallSlots merged
 // keys, no Run container over 8 KiB to copy): two launches and one host read-back.  Returns 1 when
 // the batch does not qualify (the general pipeline runs), else an rbgpu status.
@@ -697,8 +700,15 @@ static int pairwise_small(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgp
   if (rc) return rc;
   // host memory the kernels read / write in place (no copy engine on the call's path): 8 result
   // words, slot[np + 1] (u64), then a_idx[np], b_idx[np] (u32)
+  // blocks per pair (small_pair_nsub), at most ~16K blocks in all
+  const uint32_t cap = std::max<uint32_t>(1, std::min<uint32_t>(2048, 16384 / np));
+  uint64_t nblocks64 = 0;
+  for (uint32_t p = 0; p < np; ++p) {
+    const uint32_t ai = a_idx ? a_idx[p] : p, bi = b_idx ? b_idx[p] : p;
+    nblocks64 += small_pair_nsub((a->h_begin[ai + 1] - a->h_begin[ai]) + (b->h_begin[bi + 1] - b->h_begin[bi]), cap);
+  }
   const size_t nout = 64, nslot = 8 * (np + 1ull), nidx = 4ull * np * ((a_idx != nullptr) + (b_idx != nullptr));
-  const size_t blob = nout + nslot + nidx;
+  const size_t blob = nout + nslot + nidx + 4 * nblocks64;
   if (blob > ctx->h_small_cap) {
     if (ctx->h_small) (void)hipHostFree(ctx->h_small);
     ctx->h_small = ctx->d_small = nullptr;
@@ -733,12 +743,15 @@ static int pairwise_small(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgp
   const uint64_t E = acc;
   uint8_t *hp = ctx->h_small + nout + nslot;
   if (a_idx) std::memcpy(hp, a_idx, 4ull * np), hp += 4ull * np;
-  if (b_idx) std::memcpy(hp, b_idx, 4ull * np);
+  if (b_idx) std::memcpy(hp, b_idx, 4ull * np), hp += 4ull * np;
+  uint32_t *blk = reinterpret_cast<uint32_t *>(hp);
+  const uint32_t nblocks = (uint32_t)nblocks64;
+  for (uint32_t p = 0, k = 0; p < np; ++p)
+    for (uint32_t j = 0, nj = small_pair_nsub(slot[p + 1] - slot[p], cap); j < nj; ++j) blk[k++] = p | (j << 12);
 
   hipStream_t st = ctx->stream;
   const bool card_only = out == nullptr;
   const uint64_t E1 = std::max<uint64_t>(E, 1);
-  const uint32_t nblocks = np * small_pair_blocks(np, max_keys);
   const size_t need = aligned256(8ull * np) + aligned256(4 * E1) + aligned256(2 * E1) + aligned256(E1 + 32) +
                       aligned256(4 * E1) + aligned256(2 * E1) + aligned256(32ull * nblocks) +
                       aligned256(8ull * (np + 1)) + 256;
@@ -752,6 +765,8 @@ static int pairwise_small(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgp
   sa.aidx = a_idx ? d_idx : nullptr;
   sa.bidx = b_idx ? d_idx + (a_idx ? np : 0) : nullptr;
   sa.np = np;
+  sa.blk = reinterpret_cast<const uint32_t *>(ctx->d_small + (reinterpret_cast<uint8_t *>(blk) - ctx->h_small));
+  sa.cap = cap;
   sa.pcard = card_out ? W.take<uint64_t>(np) : nullptr;
   uint32_t *xpos = W.take<uint32_t>(E1);
   sa.skey = W.take<uint16_t>(E1);
@@ -771,15 +786,22 @@ static int pairwise_small(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgp
     }
     sa.arena = res->payload;
   }
+  // per-kernel events only when asked for (RBGPU_SMALL_KERNEL_TIMES=1, the bench's breakdown): the call
+  // is a few tens of microseconds and each timed marker sits between its launches
+  const char *kt = getenv("RBGPU_SMALL_KERNEL_TIMES");
+  const bool ktimes = RBG_SMALL_EVENTS || (kt && kt[0] == '1');
   stats_begin(ctx, false);
-  HIPCHK(hipEventRecord(ctx->ev[1], st));
-  launch_pair_small(op, card_only, sa, max_keys, st);
-  HIPCHK(hipEventRecord(ctx->ev[2], st));
-  OutView ov{};
-  if (res) ov = OutView{res->key, res->type, res->card, res->nruns, res->off};
-  launch_pair_small_compact(sa, (uint32_t)E, nblocks, ov, res ? res->begin : nullptr, xpos,
-                            reinterpret_cast<uint64_t *>(ctx->d_small), st);
-  HIPCHK(hipEventRecord(ctx->ev[3], st));
+  if (ktimes) HIPCHK(hipEventRecord(ctx->ev[1], st));
+  sa.E = (uint32_t)E;
+  sa.nblocks = nblocks;
+  sa.xpos = xpos;
+  sa.rbegin = res ? res->begin : nullptr;
+  if (res) sa.out = OutView{res->key, res->type, res->card, res->nruns, res->off};
+  sa.hout = reinterpret_cast<uint64_t *>(ctx->d_small);
+  launch_pair_small(op, card_only, sa, max_keys, nblocks, st);
+  if (ktimes) HIPCHK(hipEventRecord(ctx->ev[2], st));
+  launch_pair_small_compact(sa, st);
+  if (ktimes) HIPCHK(hipEventRecord(ctx->ev[3], st));
   if (card_out) HIPCHK(hipMemcpyAsync(card_out, sa.pcard, 8ull * np, hipMemcpyDeviceToHost, st));
   HIPCHK(hipEventRecord(ctx->ev[5], st));
   if (hipStreamSynchronize(st) != hipSuccess || hipGetLastError() != hipSuccess) {
@@ -795,7 +817,7 @@ static int pairwise_small(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgp
   w[7] = hout[4];           // result cardinality
   const uint64_t nres = hout[0];
   const KernelSpan spans[2] = {{"k_pair_small", 6, 1, E}, {"k_pair_small_compact", -1, -1, E}};
-  rc = stats_fill(ctx, E, nres, spans, 2);
+  rc = stats_fill(ctx, E, nres, spans, ktimes ? 2 : 0);
   if (rc) {
     if (res) rbgpu_set_free(res);
     return rc;

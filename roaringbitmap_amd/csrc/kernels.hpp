@@ -94,14 +94,23 @@ struct SmallPairArgs {
   uint64_t *pcard;             // [np] result cardinality per pair, or null
   uint64_t *bstat;             // [4 * blocks] per block: input bytes, key-array bytes, output bytes, cardinality
   uint64_t *dslot;             // [np + 1] device copy of slot (written by the first kernel)
+  const uint32_t *blk;         // [blocks] pair | block-within-pair << 12 (host-visible)
+  uint32_t cap;                // most blocks per pair
+  // the compaction kernel's: E slots, nblocks blocks, slot -> result position scratch (used above
+  // kSmallXposLds slots), result SoA (key null: cardinality only), result CSR or null, host-visible
+  // words: [0] result containers, [1..4] the summed counters
+  uint32_t E, nblocks;
+  uint32_t *xpos;
+  uint64_t *rbegin, *hout;
+  OutView out;
 };
-// blocks per pair for a batch whose largest pair has max_keys keys (na + nb)
-unsigned small_pair_blocks(uint32_t np, uint32_t max_keys);
-void launch_pair_small(int op, bool card_only, const SmallPairArgs &a, uint32_t max_keys, hipStream_t st);
-// out.key null: only the words and rbegin; rbegin may be null.  hout (host-visible): [0] result
-// containers, [1..4] the summed block counters
-void launch_pair_small_compact(const SmallPairArgs &a, uint32_t E, uint32_t nblocks, const OutView &out,
-                               uint64_t *rbegin, uint32_t *xpos, uint64_t *hout, hipStream_t st);
+// blocks of one pair with nk keys (na + nb): a wave per merged key, 4 waves per block, at most `cap`
+__host__ __device__ inline uint32_t small_pair_nsub(uint64_t nk, uint32_t cap) {
+  const uint64_t b = (nk + 3) / 4;
+  return (uint32_t)(b < 1 ? 1 : b > cap ? cap : b);
+}
+void launch_pair_small(int op, bool card_only, const SmallPairArgs &a, uint32_t max_keys, uint32_t nblocks, hipStream_t st);
+void launch_pair_small_compact(const SmallPairArgs &a, hipStream_t st);
 
 // ---- wide.hip: per-key reduction outputs (one 8 KiB slot per active key q)
 struct WideOut {

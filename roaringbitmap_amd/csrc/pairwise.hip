@@ -1134,6 +1134,94 @@ __device__ __forceinline__ uint32_t lower_bound_u16(const uint16_t *k, uint32_t 
   return lo;
 }
 
+// The compaction kernel (one block of 1024 threads after k_pair_small): drop the empty slots, write
+// the result SoA and CSR (slot t's payload stays at t * 8 KiB), add up the blocks' counters and write
+// the call's result words to host-visible memory.  Latency-bound (a chain of dependent global round
+// trips), so every independent load — type bytes, block counters, slot table — is issued up front, and
+// the slot -> result position map stays in LDS (E <= kSmallXposLds) for the CSR.  (Running it in the
+// last block of k_pair_small instead needs an agent-scope release per block — an L2 write-back on a
+// multi-XCD part: 104 vs 29 us measured.)
+constexpr uint32_t kSmallXposLds = 16384;
+__global__ __launch_bounds__(1024) void k_pair_small_compact(SmallPairArgs a) {
+  extern __shared__ uint32_t xl[]; // [E] when E <= kSmallXposLds
+  __shared__ uint32_t wtot[16];
+  __shared__ uint64_t red[16 * 4];
+  const uint32_t nt = blockDim.x, E = a.E;
+  const bool lds_x = E <= kSmallXposLds;
+  uint32_t *xpos = lds_x ? xl : a.xpos;
+  const OutView &out = a.out;
+  // independent loads first: the first tile's type bytes, the block counters, the slot table
+  const uint32_t lo0 = 8 * threadIdx.x;
+  uint64_t tw = lo0 < E ? *reinterpret_cast<const uint64_t *>(a.stype + lo0) : ~0ull;
+  uint64_t v[4] = {0, 0, 0, 0};
+  for (uint32_t b = threadIdx.x; b < a.nblocks; b += nt)
+    for (int k = 0; k < 4; ++k) v[k] += a.bstat[4ull * b + k];
+  uint64_t ds[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const uint32_t p = threadIdx.x + k * nt;
+    ds[k] = p <= a.np ? a.dslot[p] : 0;
+  }
+  uint32_t base = 0; // results of the tiles before
+  for (uint32_t t0 = 0; t0 < E; t0 += 8 * nt) {
+    const uint32_t lo = t0 + lo0;
+    if (t0) tw = lo < E ? *reinterpret_cast<const uint64_t *>(a.stype + lo) : ~0ull;
+    uint32_t cnt = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) cnt += lo + k < E && ((tw >> (8 * k)) & 0xFF) != (uint64_t)kEmpty;
+    uint32_t tot;
+    uint32_t r = base + block_xscan(cnt, wtot, tot);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const uint32_t t = lo + k;
+      if (t >= E) break;
+      xpos[t] = r;
+      const uint32_t ty = (uint32_t)((tw >> (8 * k)) & 0xFF);
+      if (ty == (uint32_t)kEmpty) continue;
+      if (out.key) {
+        out.key[r] = a.skey[t];
+        out.type[r] = (uint8_t)ty;
+        out.card[r] = a.scard[t];
+        out.nruns[r] = a.snruns[t];
+        out.off[r] = (uint64_t)t * kBitmapBytes;
+      }
+      ++r;
+    }
+    base += tot;
+  }
+  __syncthreads();
+  if (a.rbegin) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t p = threadIdx.x + k * nt;
+      if (p <= a.np) a.rbegin[p] = ds[k] < E ? xpos[ds[k]] : base;
+    }
+    for (uint32_t p = threadIdx.x + 4 * nt; p <= a.np; p += nt) { // (np <= kSmallPairs = 4 * 1024)
+      const uint64_t t = a.dslot[p];
+      a.rbegin[p] = t < E ? xpos[t] : base;
+    }
+  }
+  if (a.pcard) // per-pair result cardinality (RoaringBitmap.andCardinality etc.)
+    for (uint32_t p = threadIdx.x; p < a.np; p += nt) {
+      uint64_t c = 0;
+      for (uint64_t t = a.dslot[p]; t < a.dslot[p + 1]; ++t)
+        if (a.stype[t] != kEmpty) c += a.scard[t];
+      a.pcard[p] = c;
+    }
+  const int lane = lane_id(), wv = threadIdx.x >> 6;
+  for (int k = 0; k < 4; ++k) {
+    const uint64_t x = wave_sum_u64(v[k]);
+    if (lane == 0) red[4 * wv + k] = x;
+  }
+  __syncthreads();
+  if (threadIdx.x < 4) {
+    uint64_t x = 0;
+    for (uint32_t w = 0; w < (nt >> 6); ++w) x += red[4 * w + threadIdx.x];
+    a.hout[1 + threadIdx.x] = x;
+  }
+  if (threadIdx.x == 0) a.hout[0] = base;
+}
+
 // Dynamic LDS of k_pair_small: per wave an 8 KiB scratch, then the merged-key list, the keys and the
 // match prefix, each sized by the batch's largest na + nb (kmax).
 constexpr int kSmallLdsMax = 160 * 1024;
@@ -1142,8 +1230,11 @@ constexpr int kSmallLdsMax = 160 * 1024;
 __host__ __device__ inline uint32_t small_lds_bytes(uint32_t waves, uint32_t kmax) {
   return waves * 8192u + 64u + 4u * kmax + 2u * kmax + 2u * (kmax + 1) + 16u;
 }
+#ifndef RBG_SMALL_WAVES
+#define RBG_SMALL_WAVES 2 // waves per SIMD of the small-batch kernel (the register path takes ~235 VGPRs; 3 and 4 spill)
+#endif
 template <int OP, bool CARD_ONLY>
-__global__ __launch_bounds__(256) void k_pair_small(SmallPairArgs a, uint32_t kmax) {
+__global__ __launch_bounds__(256, RBG_SMALL_WAVES) void k_pair_small(SmallPairArgs a, uint32_t kmax) {
   extern __shared__ __attribute__((aligned(16))) uint8_t dyn_lds[];
   const uint32_t nw = blockDim.x >> 6;
   uint32_t *wtot = reinterpret_cast<uint32_t *>(dyn_lds + nw * 8192u); // [16] block-scan wave totals
@@ -1151,9 +1242,9 @@ __global__ __launch_bounds__(256) void k_pair_small(SmallPairArgs a, uint32_t km
   uint16_t *K = reinterpret_cast<uint16_t *>(ent + kmax);             // A's keys, then B's
   uint16_t *mpref = K + kmax;                                          // matched keys among A[0, i)
   const int lane = lane_id(), wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  // gridDim.y blocks per pair (blockIdx.x): each aligns the keys (cheap, in LDS) and its waves take
-  // the merged keys e = nw * blockIdx.y + wv, + nw * gridDim.y, ...
-  const uint32_t p = blockIdx.x, nt = blockDim.x, sub = blockIdx.y, nsub = gridDim.y;
+  // small_pair_nsub blocks per pair (the host's block table names each block's pair and rank): each
+  // aligns the keys (cheap, in LDS) and its waves take the merged keys e = nw * sub + wv, + nw * nsub, ...
+  const uint32_t bk = a.blk[blockIdx.x], p = bk & 0xFFFu, sub = bk >> 12, nt = blockDim.x;
   const uint32_t ai = a.aidx ? a.aidx[p] : p, bi = a.bidx ? a.bidx[p] : p;
   const uint64_t i0 = a.A.begin[ai], j0 = a.B.begin[bi];
   const uint32_t na = (uint32_t)(a.A.begin[ai + 1] - i0), nb = (uint32_t)(a.B.begin[bi + 1] - j0);
@@ -1190,6 +1281,7 @@ __global__ __launch_bounds__(256) void k_pair_small(SmallPairArgs a, uint32_t km
   // ---- one wave per merged key
   uint32_t *s = reinterpret_cast<uint32_t *>(dyn_lds) + wv * 2048;
   const uint64_t slot0 = a.slot[p], slot1 = a.slot[p + 1];
+  const uint32_t nsub = small_pair_nsub(slot1 - slot0, a.cap);
   if (sub == 0 && threadIdx.x == 0) { // a device copy of the slot table for the compaction kernel
     a.dslot[p] = slot0;
     if (p + 1 == a.np) a.dslot[p + 1] = slot1;
@@ -1290,79 +1382,12 @@ __global__ __launch_bounds__(256) void k_pair_small(SmallPairArgs a, uint32_t km
   if (threadIdx.x < 4) {
     uint64_t x = 0;
     for (uint32_t w = 0; w < nw; ++w) x += red[4 * w + threadIdx.x];
-    a.bstat[4 * ((uint64_t)p * nsub + sub) + threadIdx.x] = x;
+    a.bstat[4 * (uint64_t)blockIdx.x + threadIdx.x] = x;
   }
-}
-
-// One block: drop the empty slots, write the result SoA and CSR (slot s's payload stays at s * 8 KiB),
-// add up the blocks' counters and write the call's result words to host-visible memory.
-__global__ __launch_bounds__(1024) void k_pair_small_compact(SmallPairArgs a, uint32_t E, uint32_t nblocks,
-                                                              OutView out, uint64_t *rbegin, uint32_t *xpos,
-                                                              uint64_t *hout) {
-  __shared__ uint32_t wtot[16];
-  __shared__ uint64_t red[16][4];
-  // a thread's slots [lo, hi): a multiple of 8 (E <= kSmallSlots = 32 * 1024), their type bytes in
-  // <= 4 independent 8-B loads
-  const uint32_t per = (((E + 1023) >> 10) + 7) & ~7u;
-  const uint32_t lo = min(threadIdx.x * per, E), hi = min(lo + per, E);
-  uint64_t tw[4] = {0, 0, 0, 0};
-#pragma unroll
-  for (int g = 0; g < 4; ++g)
-    if (8u * g < per && lo + 8u * g < hi) tw[g] = *reinterpret_cast<const uint64_t *>(a.stype + lo + 8u * g);
-  auto type_at = [&](uint32_t t) { // selects, not a dynamically indexed (scratch) array
-    const uint32_t g = (t - lo) >> 3;
-    const uint64_t x = g == 0 ? tw[0] : g == 1 ? tw[1] : g == 2 ? tw[2] : tw[3];
-    return (uint32_t)((x >> (8 * ((t - lo) & 7))) & 0xFF);
-  };
-  uint32_t cnt = 0;
-  for (uint32_t t = lo; t < hi; ++t) cnt += type_at(t) != (uint32_t)kEmpty;
-  uint32_t tot;
-  uint32_t r = block_xscan(cnt, wtot, tot);
-  for (uint32_t t = lo; t < hi; ++t) {
-    xpos[t] = r;
-    const uint32_t ty = type_at(t);
-    if (ty == (uint32_t)kEmpty) continue;
-    if (out.key) {
-      out.key[r] = a.skey[t];
-      out.type[r] = (uint8_t)ty;
-      out.card[r] = a.scard[t];
-      out.nruns[r] = a.snruns[t];
-      out.off[r] = (uint64_t)t * kBitmapBytes;
-    }
-    ++r;
-  }
-  __syncthreads();
-  if (rbegin)
-    for (uint32_t p = threadIdx.x; p <= a.np; p += 1024) {
-      const uint64_t t = a.dslot[p];
-      rbegin[p] = t < E ? xpos[t] : tot;
-    }
-  if (a.pcard) // per-pair result cardinality (RoaringBitmap.andCardinality etc.)
-    for (uint32_t p = threadIdx.x; p < a.np; p += 1024) {
-      uint64_t c = 0;
-      for (uint64_t t = a.dslot[p]; t < a.dslot[p + 1]; ++t)
-        if (a.stype[t] != kEmpty) c += a.scard[t];
-      a.pcard[p] = c;
-    }
-  uint64_t v[4] = {0, 0, 0, 0};
-  for (uint32_t b = threadIdx.x; b < nblocks; b += 1024)
-    for (int k = 0; k < 4; ++k) v[k] += a.bstat[4ull * b + k];
-  const int lane = lane_id(), wv = threadIdx.x >> 6;
-  for (int k = 0; k < 4; ++k) {
-    const uint64_t x = wave_sum_u64(v[k]);
-    if (lane == 0) red[wv][k] = x;
-  }
-  __syncthreads();
-  if (threadIdx.x < 4) {
-    uint64_t x = 0;
-    for (int w = 0; w < 16; ++w) x += red[w][threadIdx.x];
-    hout[1 + threadIdx.x] = x;
-  }
-  if (threadIdx.x == 0) hout[0] = tot;
 }
 
 template <int OP>
-static void launch_small_op(bool card_only, const SmallPairArgs &a, unsigned waves, unsigned nsub, uint32_t kmax,
+static void launch_small_op(bool card_only, const SmallPairArgs &a, unsigned waves, unsigned nblocks, uint32_t kmax,
                             hipStream_t st) {
   static bool attr = false; // allow the whole 160 KiB of a CU to one block
   if (!attr) {
@@ -1373,31 +1398,33 @@ static void launch_small_op(bool card_only, const SmallPairArgs &a, unsigned wav
     attr = true;
   }
   const uint32_t lds = small_lds_bytes(waves, kmax);
-  const dim3 grid(a.np, nsub);
-  if (card_only) k_pair_small<OP, true><<<grid, 64 * waves, lds, st>>>(a, kmax);
-  else k_pair_small<OP, false><<<grid, 64 * waves, lds, st>>>(a, kmax);
+  if (card_only) k_pair_small<OP, true><<<nblocks, 64 * waves, lds, st>>>(a, kmax);
+  else k_pair_small<OP, false><<<nblocks, 64 * waves, lds, st>>>(a, kmax);
 }
-unsigned small_pair_blocks(uint32_t np, uint32_t max_keys) {
-  // The call is latency-bound (a wave's merged keys run one after the other): 4 waves per block and
-  // enough blocks per pair that a wave takes ~1 merged key (measured on census: 10 blocks per pair
-  // 28-51 us, 2 blocks per pair — one resident round — 41-77 us: the per-key latency dominates)
-  const unsigned nsub = std::max(1u, std::min((max_keys + 3) / 4, std::max(1u, 2048u / std::max(np, 1u))));
-  return nsub;
+// The call is latency-bound (a wave's merged keys run one after the other): 4 waves per block and
+// enough blocks per pair that each wave takes ~1 merged key — sized per pair (small_pair_nsub), so a
+// batch of small pairs with one large pair launches no idle blocks for the small ones (census: a
+// uniform 10 blocks per pair left ~60 % of the waves without a key after the alignment).
+void launch_pair_small_compact(const SmallPairArgs &a, hipStream_t st) {
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_pair_small_compact),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 4 * kSmallXposLds);
+    attr = true;
+  }
+  k_pair_small_compact<<<1, 1024, a.E <= kSmallXposLds ? 4 * a.E : 0, st>>>(a);
 }
-void launch_pair_small(int op, bool card_only, const SmallPairArgs &a, uint32_t max_keys, hipStream_t st) {
+void launch_pair_small(int op, bool card_only, const SmallPairArgs &a, uint32_t max_keys, uint32_t nblocks,
+                       hipStream_t st) {
   if (!a.np) return;
   const uint32_t kmax = std::max(1u, max_keys);
-  const unsigned waves = 4, nsub = small_pair_blocks(a.np, max_keys);
+  const unsigned waves = 4;
   switch (op) {
-  case RB_AND: launch_small_op<RB_AND>(card_only, a, waves, nsub, kmax, st); break;
-  case RB_OR: launch_small_op<RB_OR>(card_only, a, waves, nsub, kmax, st); break;
-  case RB_XOR: launch_small_op<RB_XOR>(card_only, a, waves, nsub, kmax, st); break;
-  default: launch_small_op<RB_ANDNOT>(card_only, a, waves, nsub, kmax, st); break;
+  case RB_AND: launch_small_op<RB_AND>(card_only, a, waves, nblocks, kmax, st); break;
+  case RB_OR: launch_small_op<RB_OR>(card_only, a, waves, nblocks, kmax, st); break;
+  case RB_XOR: launch_small_op<RB_XOR>(card_only, a, waves, nblocks, kmax, st); break;
+  default: launch_small_op<RB_ANDNOT>(card_only, a, waves, nblocks, kmax, st); break;
   }
-}
-void launch_pair_small_compact(const SmallPairArgs &a, uint32_t E, uint32_t nblocks, const OutView &out,
-                               uint64_t *rbegin, uint32_t *xpos, uint64_t *hout, hipStream_t st) {
-  k_pair_small_compact<<<1, 1024, 0, st>>>(a, E, nblocks, out, rbegin, xpos, hout);
 }
 
 } // namespace rbg

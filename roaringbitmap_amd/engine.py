@@ -286,6 +286,16 @@ def _idx(arr):
     return a, a.ctypes.data_as(L._U32P)
 
 
+def _idx_addr(arr):
+    """(array, address) of a u32 index array — the address as a plain int for void* parameters (the
+    ctypes pointer object costs ~2 us per call; small-batch calls take tens of microseconds)."""
+    if arr is None:
+        return None, None
+    a = arr if (type(arr) is np.ndarray and arr.dtype == np.uint32 and arr.flags.c_contiguous) else \
+        np.ascontiguousarray(arr, dtype=np.uint32)
+    return a, a.__array_interface__["data"][0]
+
+
 class Context:
     """One MI355X: a HIP stream, workspaces and an allocation cache (rbgpu_ctx*)."""
 
@@ -363,8 +373,8 @@ class Context:
 
     # ---- algebra
     def pairwise(self, op: int, a: DeviceSet, b: DeviceSet, a_idx=None, b_idx=None, npairs=None) -> DeviceSet:
-        ai, ap = _idx(a_idx)
-        bi, bp = _idx(b_idx)
+        ai, ap = _idx_addr(a_idx)
+        bi, bp = _idx_addr(b_idx)
         n = npairs if npairs is not None else (len(ai) if ai is not None else min(len(a), len(b)))
         out = C.c_void_p()
         L.check(L.lib().rbgpu_pairwise(self.h, op, a.h, b.h, ap, bp, n, C.byref(out)))
@@ -372,8 +382,8 @@ class Context:
 
     def pairwise_cardinality(self, op: int, a: DeviceSet, b: DeviceSet, a_idx=None, b_idx=None,
                              npairs=None) -> np.ndarray:
-        ai, ap = _idx(a_idx)
-        bi, bp = _idx(b_idx)
+        ai, ap = _idx_addr(a_idx)
+        bi, bp = _idx_addr(b_idx)
         n = npairs if npairs is not None else (len(ai) if ai is not None else min(len(a), len(b)))
         out = np.zeros(max(n, 1), np.uint64)
         L.check(L.lib().rbgpu_pairwise_cardinality(self.h, op, a.h, b.h, ap, bp, n, out.ctypes.data_as(L._U64P)))

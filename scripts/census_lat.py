@@ -36,8 +36,10 @@ def main():
             r = ctx.pairwise(op, s, s, ai, bi)
             t.append(time.perf_counter() - t0)
             r.close()
+        st = ctx.stats()
         res[name] = {"median_us": round(1e6 * float(np.median(t)), 1), "min_us": round(1e6 * min(t), 1),
-                     "gpu_total_us": round(1e3 * ctx.stats()["total_ms"], 1)}
+                     "gpu_total_us": round(1e3 * st["total_ms"], 1),
+                     "kernels_us": {k["name"]: round(1e3 * k["ms"], 1) for k in st["kernels"]}}
     print(json.dumps(res))
 
 
