@@ -356,6 +356,12 @@ __device__ __forceinline__ RecU load_rec(const TaskRec *r) {
 #ifndef RBG_FILTER_TRANSPOSE
 #define RBG_FILTER_TRANSPOSE 1 // probe a row in value order (adjacent lanes, adjacent values)
 #endif
+#ifndef RBG_REC_AHEAD
+#define RBG_REC_AHEAD 0 // 1: task records loaded one task further ahead (measured neutral to slower: 4.06-4.17 vs 3.98-4.06 ms)
+#endif
+#ifndef RBG_EARLY_NEXT_P
+#define RBG_EARLY_NEXT_P 0 // 1: filter tasks load the next P once F's last row is in the transpose buffer (measured slower: task phase 4.17 vs 4.01 ms)
+#endif
 #ifndef RBG_LIGHT_TIMING
 #define RBG_LIGHT_TIMING 0 // study builds: per-phase s_memtime totals of a few light waves (printf)
 #endif
@@ -590,6 +596,8 @@ __global__ __launch_bounds__(256, ROLE == kRoleHeavy ? RBG_HEAVY_WAVES : RBG_LIG
   load_chunks(pq, tc.pp, tc.bigp ? 16u : tc.pbytes, lane);
   if (tc.kind == kCopy || tc.bigq) load_chunks(qq, tc.pp, 16, lane);
   else load_chunks(qq, tc.pq, tc.qbytes, lane);
+  RecU nn{};
+  bool nn_ok = false;
   while (true) {
     uint64_t gn = g + stride;
     bool new_chunk = false;
@@ -602,7 +610,21 @@ __global__ __launch_bounds__(256, ROLE == kRoleHeavy ? RBG_HEAVY_WAVES : RBG_LIG
     }
     const bool has_next = gn < n;
     RBG_LT(lt0 = __builtin_amdgcn_s_memtime());
-    const RecU nx = load_rec(recs + (has_next ? gn : g));
+    const RecU nx = RBG_REC_AHEAD && nn_ok ? nn : load_rec(recs + (has_next ? gn : g));
+    if (RBG_REC_AHEAD) { // the record after next, where its index is already known, an iteration ahead
+      uint64_t gnn = n;
+      if (has_next) {
+        if (queue) {
+          const uint64_t ce = new_chunk ? nend : cend; // end of gn's chunk
+          if (gn + 1 < ce) gnn = gn + 1;
+          else if (!new_chunk) gnn = nxt; // gn ends the current chunk: the claimed chunk follows
+        } else {
+          gnn = gn + stride;
+        }
+      }
+      nn_ok = gnn < n;
+      if (nn_ok) nn = load_rec(recs + gnn);
+    }
     const Task tn = decode_task<OP>(nx, pay_a, pay_b);
     RBG_LT(lt1 = __builtin_amdgcn_s_memtime(); lt_acc[0] += lt1 - lt0);
     int ty = kEmpty, c = 0;
@@ -705,8 +727,11 @@ __global__ __launch_bounds__(256, ROLE == kRoleHeavy ? RBG_HEAVY_WAVES : RBG_LIG
         (void)none;
         uint4 *tb = tbuf[ROLE == kRoleLight ? wv : 0];
 #if RBG_FILTER_LINEAR
-        c = OP == RB_ANDNOT ? filter_rows_linear<true, !CARD_ONLY>(pq, (int)tc.cp, s, ob, tb, o, lane)
-                            : filter_rows_linear<false, !CARD_ONLY>(pq, (int)tc.cp, s, ob, tb, o, lane);
+        auto next_f = [&]() { // the next task's P into the registers F has left
+          if (RBG_EARLY_NEXT_P) load_chunks(pq, tn.pp, tn.bigp ? 16u : tn.pbytes, lane);
+        };
+        c = OP == RB_ANDNOT ? filter_rows_linear<true, !CARD_ONLY>(pq, (int)tc.cp, s, ob, tb, o, lane, next_f)
+                            : filter_rows_linear<false, !CARD_ONLY>(pq, (int)tc.cp, s, ob, tb, o, lane, next_f);
 #else
         c = OP == RB_ANDNOT ? filter_rows_transposed<true>(pq, (int)tc.cp, s, ob, tb, o, lane)
                             : filter_rows_transposed<false>(pq, (int)tc.cp, s, ob, tb, o, lane);
@@ -722,7 +747,8 @@ __global__ __launch_bounds__(256, ROLE == kRoleHeavy ? RBG_HEAVY_WAVES : RBG_LIG
         nr = tc.rp;
       }
       RBG_LT(lt_acc[5] += __builtin_amdgcn_s_memtime() - lt2);
-      load_chunks(pq, tn.pp, tn.bigp ? 16u : tn.pbytes, lane);
+      if (!(RBG_EARLY_NEXT_P && RBG_FILTER_LINEAR && tc.kind == kFilter && !(RBG_LIGHT_ABLATE & 8)))
+        load_chunks(pq, tn.pp, tn.bigp ? 16u : tn.pbytes, lane);
     }
     wave_lds_sync(); // the next task restages the same LDS image
     if (lane == 0) {

@@ -480,9 +480,11 @@ __device__ __forceinline__ int filter_rows_transposed(const uint4 (&fq)[8], int 
 // block (< 8 kept values) moves to the front, so a kept value's slot is (pending + mbcnt) with no
 // wrap — mbcnt adds the pending count itself — and rejected lanes are masked off instead of writing a
 // dummy slot.  ~8 VALU per 64 probed values instead of ~15 (ISA count).  Pending values stay < 8 + 512.
-template <bool NEGATE, bool STORE>
+// `next()` runs once the last row of F is in the transpose buffer — F's registers are free from
+// there, so the caller's prefetch of the next task's F overlaps the last row's probes and flush.
+template <bool NEGATE, bool STORE, class Next>
 __device__ __forceinline__ int filter_rows_linear(const uint4 (&fq)[8], int nf, const uint32_t *s, uint16_t *ob,
-                                                  uint4 *tb, uint16_t *out, int lane) {
+                                                  uint4 *tb, uint16_t *out, int lane, const Next &next) {
   static_assert(7 + 512 <= kStageRing, "every slot (pending < 8, + < 512 of a row) lies below the dummies");
   const int iters = (nf + 511) >> 9; // wave-uniform, <= 8
   uint32_t tot = 0, flushed = 0;     // kept / written out so far (wave-uniform; flushed % 8 == 0)
@@ -498,6 +500,7 @@ __device__ __forceinline__ int filter_rows_linear(const uint4 (&fq)[8], int nf, 
       for (int hf = 0; hf < 2; ++hf) {
         if ((lane >> 5) == hf) tb[lane & 31] = fq[i];
         wave_lds_sync();
+        if (hf == 1 && i == iters - 1) next();
         const int nh = min(256, nf - 512 * i - 256 * hf); // values of this half (may be <= 0)
         uint32_t y[4], m[4];
 #pragma unroll
