@@ -68,7 +68,11 @@ def _traffic_groups(pmc_name):
 def pmc_traffic(pmc_name: str, with_count: bool = False):
     """HBM bytes per launch of `pmc_name` from the committed rocprofv3 PMC summary of this same bench
     command (scripts/traffic.py: FETCH_SIZE x2 for gfx950 16-B/lane reads + WRITE_SIZE, separate
-    passes); the dominant (largest) dispatch group is the headline launch.  None if not profiled."""
+    passes); the dominant (largest) dispatch group is the headline launch.  None if not profiled.
+    "a+b": the kernels of one timed span (e.g. naive_xor's record pre-pass and its kernel), summed."""
+    if "+" in pmc_name and not with_count:
+        parts = [pmc_traffic(x) for x in pmc_name.split("+")]
+        return None if any(x is None for x in parts) else sum(parts)
     g = _traffic_groups(pmc_name)
     if not g:
         return None
@@ -498,7 +502,7 @@ WIDE_WORKLOADS = {
                 "config3: FastAggregation.or of {n} dense bitmaps over the full 2^32 universe"),
     "wide_and_runs": ("WL_WIDE_RUNS", "FAST_AND", 4096, "rbg::k_wide_runs_and", 256,
                       "config4: FastAggregation.and (workShyAnd) of {n} run-heavy bitmaps x 65536 keys"),
-    "wide_xor_runs": ("WL_WIDE_RUNS", "FAST_XOR", 4096, "rbg::k_wide_runs_xor", 256,
+    "wide_xor_runs": ("WL_WIDE_RUNS", "FAST_XOR", 4096, "rbg::k_xor_records_dense+rbg::k_wide_runs_xor", 256,
                       "config4: FastAggregation.xor (naive_xor) of {n} run-heavy bitmaps x 65536 keys"),
 }
 # the all-core CPU baseline of each wide semantic: ParallelAggregation where the reference has one,
