@@ -69,6 +69,10 @@ enum rb_wide_sem {
    * the members' keys and cardinalities and the per-key work runs on the device. */
   RB_HORIZONTAL_OR = 8,  /* FastAggregation.horizontal_or(List / varargs)     FastAggregation.java:124-231 */
   RB_HORIZONTAL_XOR = 9, /* FastAggregation.horizontal_xor                    FastAggregation.java:243-289 */
+  RB_PQ_OR = 10,         /* FastAggregation.priorityqueue_or: the two smallest bitmaps (getLongSizeInBytes)
+                            lazily OR'd on the device (lazyor / in-place lazyor / lazyorfromlazyinputs by
+                            which operands are temporaries), re-queued, the survivor repaired
+                            FastAggregation.java:675-721 (whole result only: no key range) */
   RB_PQ_XOR = 11         /* FastAggregation.priorityqueue_xor: the two smallest bitmaps (getLongSizeInBytes)
                             replaced by their RoaringBitmap.xor, on the device, until one is left
                             FastAggregation.java:732-752 (whole result only: no key range) */

@@ -12,13 +12,13 @@ from .engine import Context, DeviceSet, HostSoA, default_context, soa_from_value
 from .roaring import FastAggregation, ParallelAggregation, RoaringBitmap
 from .bsi import Operation, Roaring64BitmapSliceIndex, RoaringBitmapSliceIndex
 from ._lib import BSI_EQ, BSI_GE, BSI_GT, BSI_LE, BSI_LT, BSI_NEQ, BSI_RANGE
-from ._lib import HORIZONTAL_OR, HORIZONTAL_XOR, PQ_XOR
+from ._lib import HORIZONTAL_OR, HORIZONTAL_XOR, PQ_OR, PQ_XOR
 from .engine import Comm
 
 __all__ = [
     "AND", "OR", "XOR", "ANDNOT", "ARRAY", "BITMAP", "RUN",
     "FAST_OR", "FAST_AND", "WORKSHY_AND", "NAIVE_AND", "FAST_XOR", "PAR_OR", "PAR_XOR", "NAIVE_AND_ITER",
-    "HORIZONTAL_OR", "HORIZONTAL_XOR", "PQ_XOR", "Comm",
+    "HORIZONTAL_OR", "HORIZONTAL_XOR", "PQ_OR", "PQ_XOR", "Comm",
     "WL_FILTER_POSTING", "WL_WIDE_DENSE", "WL_WIDE_MIXED", "WL_WIDE_RUNS",
     "Context", "DeviceSet", "HostSoA", "default_context", "soa_from_values",
     "RoaringBitmap", "FastAggregation", "ParallelAggregation",

@@ -16,7 +16,7 @@ RB_OK, RB_EFORMAT, RB_EINVAL, RB_ENOMEM, RB_EDEVICE = 0, -1, -2, -3, -4
 AND, OR, XOR, ANDNOT = 0, 1, 2, 3
 ARRAY, BITMAP, RUN = 0, 1, 2
 FAST_OR, FAST_AND, WORKSHY_AND, NAIVE_AND, FAST_XOR, PAR_OR, PAR_XOR, NAIVE_AND_ITER = range(8)
-HORIZONTAL_OR, HORIZONTAL_XOR, PQ_XOR = 8, 9, 11  # global-order semantics (rbgpu.h rb_wide_sem)
+HORIZONTAL_OR, HORIZONTAL_XOR, PQ_OR, PQ_XOR = 8, 9, 10, 11  # global-order semantics (rbgpu.h rb_wide_sem)
 WL_FILTER_POSTING, WL_WIDE_DENSE, WL_WIDE_MIXED, WL_WIDE_RUNS = range(4)
 BSI_EQ, BSI_NEQ, BSI_LE, BSI_LT, BSI_GE, BSI_GT, BSI_RANGE = range(7)  # BitmapSliceIndex.Operation
 

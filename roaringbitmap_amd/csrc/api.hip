@@ -798,7 +798,8 @@ static int pairwise_small(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgp
   sa.rbegin = res ? res->begin : nullptr;
   if (res) sa.out = OutView{res->key, res->type, res->card, res->nruns, res->off};
   sa.hout = reinterpret_cast<uint64_t *>(ctx->d_small);
-  launch_pair_small(op, card_only, sa, max_keys, nblocks, st);
+  sa.lazy = is_lazy_op(op) ? op : 0;
+  launch_pair_small(is_lazy_op(op) ? (int)RB_OR : op, card_only, sa, max_keys, nblocks, st);
   if (ktimes) HIPCHK(hipEventRecord(ctx->ev[2], st));
   launch_pair_small_compact(sa, st);
   if (ktimes) HIPCHK(hipEventRecord(ctx->ev[3], st));
@@ -837,7 +838,7 @@ static int pairwise_impl(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu
                          int probe = 0) {
   int rc = check_ctx(ctx);
   if (rc) return rc;
-  if (op < RB_AND || op > RB_ANDNOT) return fail(RB_EINVAL, "bad op %d", op);
+  if ((op < RB_AND || op > RB_ANDNOT) && !is_lazy_op(op)) return fail(RB_EINVAL, "bad op %d", op);
   if (!a || !b) return fail(RB_EINVAL, "null set");
   if (a->ctx != ctx || b->ctx != ctx) return fail(RB_EINVAL, "sets belong to another context");
   if (!a_idx && npairs > a->nb) return fail(RB_EINVAL, "npairs exceeds bitmaps of a");
@@ -851,6 +852,7 @@ static int pairwise_impl(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu
     if (rc != 1) return rc;
   }
   const bool card_only = out == nullptr;
+  const int kop = is_lazy_op(op) ? (int)RB_OR : op; // the kernels' op (lazy roles run as OR, TaskMeta::lazy)
   hipStream_t st = ctx->stream;
   const uint64_t np = npairs;
   // ---- per pair: indices, merge-path segment counts and their scan, pair cardinalities
@@ -961,7 +963,8 @@ static int pairwise_impl(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu
   Workspace &T = ctx->ws_tasks;
   TaskRec *light = T.take<TaskRec>(std::max<uint64_t>(nlight, 1));
   TaskRec *heavy = T.take<TaskRec>(std::max<uint64_t>(nheavy, 1));
-  TaskMeta tm;
+  TaskMeta tm{};
+  tm.lazy = is_lazy_op(op) ? op : 0;
   tm.key = T.take<uint16_t>(nt1);
   tm.nruns = T.take<uint16_t>(nt1);
   tm.type = T.take<uint8_t>(nt1);
@@ -1009,13 +1012,13 @@ static int pairwise_impl(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu
   }
   if (conc) {
     HIPCHK(hipStreamWaitEvent(ctx->side, ctx->ev[1], 0));
-    launch_pairwise_concurrent(op, card_only, a->payload, b->payload, light, nlight, heavy, nheavy,
+    launch_pairwise_concurrent(kop, card_only, a->payload, b->payload, light, nlight, heavy, nheavy,
                                res ? res->payload : nullptr, tm, st, ctx->side, ctx->ev[2], ctx->ev_side[0],
                                ctx->ev_side[1], static_light ? nullptr : queue);
     HIPCHK(hipEventRecord(ctx->ev_side[2], ctx->side));
     HIPCHK(hipStreamWaitEvent(st, ctx->ev_side[2], 0));
   } else {
-    launch_pairwise(op, card_only, a->payload, b->payload, light, nlight, heavy, nheavy, res ? res->payload : nullptr,
+    launch_pairwise(kop, card_only, a->payload, b->payload, light, nlight, heavy, nheavy, res ? res->payload : nullptr,
                     tm, st, ctx->ev[2]);
   }
   HIPCHK(hipEventRecord(ctx->ev[3], st));
@@ -1155,6 +1158,66 @@ static int pq_xor(rbgpu_ctx *ctx, const rbgpu_set *in, const std::vector<uint32_
   return rbgpu_set_extract(last.s, last.idx, 1, out); // one member: the reference returns it as is
 }
 
+// FastAggregation.priorityqueue_or(RoaringBitmap...) (FastAggregation.java:675-721; oracle wide_pq_or):
+// the bitmaps in a java.util.PriorityQueue by getLongSizeInBytes; the two smallest are lazily OR'd —
+// RoaringBitmap.lazyor (static) when neither is a temporary, this.lazyor(other) on the temporary one,
+// lazyorfromlazyinputs when both are — the result re-queued with its size; the survivor is repaired
+// (repairAfterLazy).  Each step is one device pairwise call in a lazy role (pairwise.hip
+// lazy_or_type); its size comes back from the result's summary.  The repair is one more call, the
+// survivor with itself in the kLazyRepair role (a lazy Bitmap -> LR, an exact one kept, Run -> EFF).
+static int pq_or(rbgpu_ctx *ctx, const rbgpu_set *in, const std::vector<uint32_t> &mem, rbgpu_set **out) {
+  const size_t n = mem.size();
+  if (n == 0) return empty_result(ctx, out);
+  std::vector<rb_bitmap_summary> summ(in->nb);
+  int rc = rbgpu_set_summaries(in, 0, in->nb, summ.data());
+  if (rc) return rc;
+  struct Node {
+    const rbgpu_set *s;
+    uint32_t idx;
+    int64_t size;
+    rbgpu_set *owned;
+    bool tmp; // a temporary of the queue (istmp)
+  };
+  std::vector<Node> nodes;
+  nodes.reserve(2 * n);
+  for (uint32_t m : mem) nodes.push_back(Node{in, m, (int64_t)summ[m].size_in_bytes, nullptr, false});
+  auto cmp = [&](uint32_t a, uint32_t b) { return (int)(nodes[a].size - nodes[b].size); };
+  JavaHeap<uint32_t, decltype(cmp)> pq(cmp);
+  for (uint32_t k = 0; k < n; ++k) pq.offer(k);
+  auto cleanup = [&]() {
+    for (Node &x : nodes)
+      if (x.owned) rbgpu_set_free(x.owned), x.owned = nullptr;
+  };
+  while (pq.size() > 1) {
+    const uint32_t x1 = pq.poll(), x2 = pq.poll();
+    // target (left operand) and role, FastAggregation.java:690-716
+    uint32_t t = x1, o = x2;
+    int role = kLazyStatic;
+    if (nodes[x1].tmp && nodes[x2].tmp) role = kLazyIorBf;
+    else if (nodes[x2].tmp) t = x2, o = x1, role = kLazyIor;
+    else if (nodes[x1].tmp) role = kLazyIor;
+    const uint32_t it = nodes[t].idx, io = nodes[o].idx;
+    rbgpu_set *r = nullptr;
+    rc = pairwise_impl(ctx, role, nodes[t].s, nodes[o].s, &it, &io, 1, &r, nullptr);
+    rb_bitmap_summary rs{};
+    if (!rc) rc = rbgpu_set_summaries(r, 0, 1, &rs);
+    if (rc) {
+      if (r) rbgpu_set_free(r);
+      cleanup();
+      return rc;
+    }
+    for (uint32_t x : {x1, x2}) // the operands are not referenced again
+      if (nodes[x].owned) rbgpu_set_free(nodes[x].owned), nodes[x].owned = nullptr;
+    nodes.push_back(Node{r, 0, (int64_t)rs.size_in_bytes, r, true});
+    pq.offer((uint32_t)nodes.size() - 1);
+  }
+  const Node last = nodes[pq.poll()];
+  const uint32_t il = last.idx;
+  rc = pairwise_impl(ctx, kLazyRepair, last.s, last.s, &il, &il, 1, out, nullptr); // repairAfterLazy
+  cleanup();
+  return rc;
+}
+
 int rbgpu_wide(rbgpu_ctx *ctx, int sem, const rbgpu_set *in, const uint32_t *members, uint32_t n, rbgpu_set **out) {
   return rbgpu_wide_keys(ctx, sem, in, members, n, 0, 65536, out);
 }
@@ -1167,7 +1230,7 @@ int rbgpu_wide_keys(rbgpu_ctx *ctx, int sem, const rbgpu_set *in, const uint32_t
   int rc = check_ctx(ctx);
   if (rc) return rc;
   if (!in || in->ctx != ctx) return fail(RB_EINVAL, "bad input set");
-  if (sem < RB_FAST_OR || sem > RB_PQ_XOR || sem == 10) return fail(RB_EINVAL, "bad semantics %d", sem);
+  if (sem < RB_FAST_OR || sem > RB_PQ_XOR) return fail(RB_EINVAL, "bad semantics %d", sem);
   rc = ensure_h_begin(in);
   if (rc) return rc;
   std::vector<uint32_t> mem;
@@ -1180,9 +1243,9 @@ int rbgpu_wide_keys(rbgpu_ctx *ctx, int sem, const rbgpu_set *in, const uint32_t
     mem.resize(n);
     for (uint32_t i = 0; i < n; ++i) mem[i] = i;
   }
-  if (sem == RB_PQ_XOR) {
-    if (key_lo != 0 || key_hi != 65536) return fail(RB_EINVAL, "priorityqueue_xor has no key-range shards");
-    return pq_xor(ctx, in, mem, out);
+  if (sem == RB_PQ_XOR || sem == RB_PQ_OR) {
+    if (key_lo != 0 || key_hi != 65536) return fail(RB_EINVAL, "priorityqueue_or/xor have no key-range shards");
+    return sem == RB_PQ_XOR ? pq_xor(ctx, in, mem, out) : pq_or(ctx, in, mem, out);
   }
   return wide_run(ctx, sem, in, mem, key_lo, key_hi, out);
 }

@@ -52,8 +52,22 @@ __host__ __device__ inline uint32_t desc_card(uint32_t d) { return d >> 2; }
 // with the counters so the call needs one device-to-host copy.
 constexpr int kStatWords = 9, kStripes = 64;
 
+// FastAggregation.priorityqueue_or's intermediate bitmaps (api.hip pq_or) carry two marks in the card
+// word of their containers, never seen outside that call: a lazy Bitmap (the reference's cardinality
+// -1 after a lazy OR) and a Run kept as 8 KiB of bitmap words (a lazily merged Run of 2048..4096 runs,
+// RunContainer.lazyorToRun, whose run list would not fit an 8 KiB slot).
+constexpr uint32_t kLazyCard = 1u << 28;
+constexpr uint32_t kRunAsBitmap = 1u << 29;
+constexpr uint32_t kCardMarks = kLazyCard | kRunAsBitmap;
+// internal pairwise ops of priorityqueue_or (Container.lazyOR / lazyIOR roles, run as the OR kernels;
+// kLazyRepair: a bitmap with itself, each container through its repairAfterLazy)
+enum { kLazyStatic = 16, kLazyIor = 17, kLazyIorBf = 18, kLazyRepair = 19 };
+__host__ __device__ inline bool is_lazy_op(int op) { return op >= kLazyStatic && op <= kLazyRepair; }
+__host__ __device__ inline bool bitmap_payload(int type, uint32_t card) {
+  return type == kBitmap || (type == kRun && (card & kRunAsBitmap));
+}
 __host__ __device__ inline uint64_t payload_bytes(int type, uint32_t card, uint32_t nruns) {
-  return type == kBitmap ? (uint64_t)kBitmapBytes : type == kArray ? 2ull * card : 4ull * nruns;
+  return bitmap_payload(type, card) ? (uint64_t)kBitmapBytes : type == kArray ? 2ull * card : 4ull * nruns;
 }
 __host__ __device__ inline uint64_t round16(uint64_t x) { return (x + 15) & ~15ull; }
 

@@ -32,6 +32,7 @@ struct TaskMeta {
   uint16_t *nruns;
   uint8_t *cat;    // 0 light, 1 heavy
   uint64_t *out;   // output slot offset
+  int lazy;        // 0, or the priorityqueue_or role (kLazyStatic / kLazyIor / kLazyIorBf) of an OR call
 };
 struct PairCounts {
   uint64_t task, light, heavy, big, small;
@@ -94,6 +95,7 @@ struct SmallPairArgs {
   uint64_t *pcard;             // [np] result cardinality per pair, or null
   uint64_t *bstat;             // [4 * blocks] per block: input bytes, key-array bytes, output bytes, cardinality
   uint64_t *dslot;             // [np + 1] device copy of slot (written by the first kernel)
+  int lazy;                    // 0, or the priorityqueue_or role of an OR call (TaskMeta::lazy)
   const uint32_t *blk;         // [blocks] pair | block-within-pair << 12 (host-visible)
   uint32_t cap;                // most blocks per pair
   // the compaction kernel's: E slots, nblocks blocks, slot -> result position scratch (used above

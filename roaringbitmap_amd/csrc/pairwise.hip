@@ -22,7 +22,7 @@ namespace rbg {
 constexpr int kPairThreads = 256;
 
 __device__ __forceinline__ bool keeps_a_only(int op) { return op != RB_AND; }
-__device__ __forceinline__ bool keeps_b_only(int op) { return op == RB_OR || op == RB_XOR; }
+__device__ __forceinline__ bool keeps_b_only(int op) { return op == RB_OR || op == RB_XOR || is_lazy_op(op); }
 
 // algorithmic payload bytes: Bitmap 8192, Array 2c, Run 4r+2
 __device__ __forceinline__ uint64_t alg_bytes(int t, uint32_t c, uint32_t r) {
@@ -33,6 +33,11 @@ __device__ __forceinline__ uint64_t alg_bytes(int t, uint32_t c, uint32_t r) {
 // 2*cmax bytes when cmax <= 4096 (Array 2c; a Run is only chosen when 4r+2 <= 2c+2), and in
 // one 8 KiB slot otherwise.
 __device__ __forceinline__ void matched_bound(int op, uint32_t ca, uint32_t cb, bool &big, uint64_t &bytes) {
+  if (is_lazy_op(op)) { // lazy results (a lazy Bitmap of two small Arrays, a Run of any run count) take 8 KiB
+    big = true;
+    bytes = 0;
+    return;
+  }
   uint32_t cmax = op == RB_AND ? min(ca, cb) : op == RB_ANDNOT ? ca : ca + cb;
   big = 2ull * cmax >= (uint64_t)kBitmapBytes;
   bytes = big ? 0 : round16(2ull * cmax);
@@ -422,6 +427,66 @@ template <int OP> __device__ __forceinline__ bool eff_rule(int ta, int tb, uint3
            (ta == kRun && tb == kArray && cb < (uint32_t)kRunArrayThreshold);
   return (ta == kRun && tb == kRun) || (ta == kRun && tb == kArray && cb < (uint32_t)kRunArrayThreshold);
 }
+// FastAggregation.priorityqueue_or's lazy OR of x (P, the in-place target) and y (Q) for their union
+// (c, r): the result type of Container.lazyOR (kLazyStatic, RoaringBitmap.lazyor static) or lazyIOR
+// (kLazyIor: this.lazyor(x2); kLazyIorBf: lazyorfromlazyinputs, a Bitmap y goes first) — oracle
+// c_lazy_or / c_lazy_ior (ArrayContainer.lazyor :1449-1464, RunContainer.lazyorToRun :1769-1813,
+// BitmapContainer.lazyor / ilazyor :657-685, 887-918, BitmapContainer.or(Array), RunContainer.or(Bitmap),
+// RunContainer.ior(Run)).  cw = the card word to store (kLazyCard: a lazy Bitmap; | kRunAsBitmap: a Run
+// of more than 2047 runs kept as bitmap words), bits = the payload is emitted as bitmap words.
+__device__ __forceinline__ int lazy_or_type(int mode, int tx, int ty, uint32_t cx, uint32_t cy, int c, int r,
+                                            uint32_t &cw, bool &bits) {
+  bits = false;
+  cw = (uint32_t)c;
+  if (mode == kLazyRepair) { // x == y: repairAfterLazy (BitmapContainer :1214-1224 repairs only a lazy
+                             // Bitmap — cardinality -1; RunContainer :2073 toEfficientContainer)
+    if (tx == kRun) return type_eff(c, r);
+    if (tx != kBitmap) return kArray;
+    const int t = (cx & kLazyCard) ? type_lr(c) : (int)kBitmap;
+    bits = t == kBitmap;
+    return t;
+  }
+  if (mode == kLazyIorBf && ty == kBitmap && tx != kBitmap) { // the Bitmap becomes the target
+    const int t = tx;
+    tx = ty;
+    ty = t;
+    const uint32_t u = cx;
+    cx = cy;
+    cy = u;
+  }
+  const bool full = c == kSpan, ylazy = ty == kBitmap && (cy & kLazyCard);
+  const bool xfull = tx == kRun && (cx & ~kCardMarks) == (uint32_t)kSpan;
+  enum { kLazyB, kExactB, kA, kR, kEff } k;
+  if (tx == kArray && ty == kArray) {
+    k = (cx & ~kCardMarks) + (cy & ~kCardMarks) > 1024u ? kLazyB : kA; // ARRAY_LAZY_LOWERBOUND
+  } else if (mode == kLazyStatic) {
+    if (tx == kBitmap || ty == kBitmap) k = kLazyB;
+    else if (tx == kRun && ty == kRun) k = full ? kR : kEff;                 // run_or_run
+    else k = full ? kR : r > kMaxArray ? kLazyB : kR;                        // lazyorToRun
+  } else if (tx == kArray) {
+    if (ty == kBitmap) k = ylazy ? kLazyB : full ? kR : kExactB;             // y.or(x): full -> Run
+    else k = full ? kR : r > kMaxArray ? kLazyB : kR;                        // y.lazyor(x) -> lazyorToRun
+  } else if (tx == kRun) {
+    if (xfull) k = kR;                                                       // returns a full this
+    else if (ty == kArray) k = full ? kR : r > kMaxArray ? kLazyB : kR;      // ilazyorToRun
+    else if (ty == kBitmap) k = full ? kR : kExactB;                         // or(Bitmap)
+    else k = kEff;                                                           // ior(Run)
+  } else {
+    k = kLazyB;                                                              // Bitmap.ilazyor
+  }
+  switch (k) {
+  case kLazyB: bits = true; cw = kLazyCard; return kBitmap;
+  case kExactB: bits = true; return kBitmap;
+  case kA: return kArray;
+  case kEff: return type_eff(c, r);
+  default:
+    if (r > 2047) { // 4r + 2 > 8 KiB: kept as bitmap words (the size stays the reference's 4r + 4)
+      bits = true;
+      cw = (uint32_t)c | kRunAsBitmap;
+    }
+    return kRun;
+  }
+}
 template <int OP> __device__ __forceinline__ void word_op(uint64_t &a, uint64_t b) {
   if (OP == RB_AND) a &= b;
   else if (OP == RB_OR) a |= b;
@@ -628,7 +693,7 @@ __global__ __launch_bounds__(256, ROLE == kRoleHeavy ? RBG_HEAVY_WAVES : RBG_LIG
     const Task tn = decode_task<OP>(nx, pay_a, pay_b);
     RBG_LT(lt1 = __builtin_amdgcn_s_memtime(); lt_acc[0] += lt1 - lt0);
     int ty = kEmpty, c = 0;
-    uint32_t nr = 0;
+    uint32_t nr = 0, cw = 0xFFFFFFFFu; // cw: the card word to store when it is not c (lazy marks)
     uint8_t *dst = out + cur.out;
     bool done = false;
     if (ROLE == kRoleHeavy && RBG_RUN_INTERVALS && OP == RB_AND && tc.tp == kRun && tc.tq == kRun && !tc.bigp &&
@@ -650,7 +715,7 @@ __global__ __launch_bounds__(256, ROLE == kRoleHeavy ? RBG_HEAVY_WAVES : RBG_LIG
       // ---- the result as a register bitmap: P = A, Q = B (never swapped: ANDNOT and the type
       //      rules are ordered)
       uint64_t w[kW];
-      if (tc.tp == kBitmap) {
+      if (bitmap_payload(tc.tp, tc.cp)) {
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
           w[2 * k] = pack2(pq[k].x, pq[k].y);
@@ -662,7 +727,7 @@ __global__ __launch_bounds__(256, ROLE == kRoleHeavy ? RBG_HEAVY_WAVES : RBG_LIG
         lds_read_words(s, w, lane);
         wave_lds_sync();
       }
-      if (tc.tq == kBitmap) {
+      if (bitmap_payload(tc.tq, tc.cq)) {
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
           word_op<OP>(w[2 * k], pack2(qq[k].x, qq[k].y));
@@ -689,17 +754,22 @@ __global__ __launch_bounds__(256, ROLE == kRoleHeavy ? RBG_HEAVY_WAVES : RBG_LIG
       }
       load_chunks(pq, tn.pp, tn.bigp ? 16u : tn.pbytes, lane);
       const int ta = tc.tp, tb = tc.tq;
+      const bool lazy = OP == RB_OR && tm.lazy;
       const bool eff = eff_rule<OP>(ta, tb, tc.cp, tc.cq);
       int r;
-      metrics(w, lane, eff && !CARD_ONLY, c, r);
-      if (OP != RB_OR && c == 0) ty = kEmpty;
+      metrics(w, lane, (eff || (lazy && (ta == kRun || tb == kRun))) && !CARD_ONLY, c, r);
+      bool bits = false;
+      if (lazy) {
+        ty = lazy_or_type(tm.lazy, ta, tb, tc.cp, tc.cq, c, r, cw, bits);
+        if (ty == kRun && c == kSpan) r = 1;
+      } else if (OP != RB_OR && c == 0) ty = kEmpty;
       else if (eff) ty = type_eff(c, r);
       else if (OP == RB_OR && (ta == kBitmap || tb == kBitmap)) {
         ty = type_lr(c);
         if (ty == kRun) r = 1; // LR's Run is the full container: one run
       } else ty = type_ab(c);
       if (CARD_ONLY) ty = c ? kArray : kEmpty;
-      else if (ty != kEmpty) emit_container(ty, w, c, r, dst, s, lane);
+      else if (ty != kEmpty) emit_container(bits ? (int)kBitmap : ty, w, c, r, dst, s, lane);
       nr = ty == kRun ? (uint32_t)r : 0u;
     } else if (ROLE != kRoleHeavy) {
       // ---- phase 1: stage X (filter) or store the clone (copy)
@@ -753,7 +823,7 @@ __global__ __launch_bounds__(256, ROLE == kRoleHeavy ? RBG_HEAVY_WAVES : RBG_LIG
     wave_lds_sync(); // the next task restages the same LDS image
     if (lane == 0) {
       tm.type[cur.t] = (uint8_t)ty;
-      tm.card[cur.t] = (uint32_t)c;
+      tm.card[cur.t] = cw != 0xFFFFFFFFu ? cw : (uint32_t)c;
       tm.nruns[cur.t] = (uint16_t)nr;
     }
     RBG_LT(lt_acc[6] += __builtin_amdgcn_s_memtime() - lt0; ++lt_acc[7]);
@@ -1320,6 +1390,7 @@ __global__ __launch_bounds__(256, RBG_SMALL_WAVES) void k_pair_small(SmallPairAr
     const uint64_t slot = slot0 + e;
     uint8_t *dst = a.arena + slot * kBitmapBytes;
     int ty = kEmpty, c = 0, nr = 0;
+    uint32_t cw = 0xFFFFFFFFu; // the card word to store when it is not c (priorityqueue_or's lazy marks)
     if (has_a && has_b) {
       const uint64_t xa = i0 + ia, xb = j0 + ib;
       const int ta = a.A.type[xa], tb = a.B.type[xb];
@@ -1329,7 +1400,7 @@ __global__ __launch_bounds__(256, RBG_SMALL_WAVES) void k_pair_small(SmallPairAr
       if (lane == 0) inb += alg_bytes(ta, ca, ra) + alg_bytes(tb, cb, rb) + 32;
       uint64_t w[kW];
       uint4 q[8];
-      if (ta == kBitmap) {
+      if (bitmap_payload(ta, ca)) {
         load_bitmap(pa, w, lane);
       } else {
         if (ba > (uint32_t)kBitmapBytes) stage_big_runs(pa, ra, s, lane);
@@ -1340,7 +1411,7 @@ __global__ __launch_bounds__(256, RBG_SMALL_WAVES) void k_pair_small(SmallPairAr
         lds_read_words(s, w, lane);
         wave_lds_sync();
       }
-      if (tb == kBitmap) {
+      if (bitmap_payload(tb, cb)) {
         load_chunks(q, pb, kBitmapBytes, lane);
       } else {
         if (bb > (uint32_t)kBitmapBytes) stage_big_runs(pb, rb, s, lane);
@@ -1358,17 +1429,22 @@ __global__ __launch_bounds__(256, RBG_SMALL_WAVES) void k_pair_small(SmallPairAr
         word_op<OP>(w[2 * k], pack2(q[k].x, q[k].y));
         word_op<OP>(w[2 * k + 1], pack2(q[k].z, q[k].w));
       }
+      const bool lazy = OP == RB_OR && a.lazy;
       const bool eff = eff_rule<OP>(ta, tb, ca, cb);
       int r;
-      metrics(w, lane, eff && !CARD_ONLY, c, r);
-      if (OP != RB_OR && c == 0) ty = kEmpty;
+      metrics(w, lane, (eff || (lazy && (ta == kRun || tb == kRun))) && !CARD_ONLY, c, r);
+      bool bits = false;
+      if (lazy) {
+        ty = lazy_or_type(a.lazy, ta, tb, ca, cb, c, r, cw, bits);
+        if (ty == kRun && c == kSpan) r = 1;
+      } else if (OP != RB_OR && c == 0) ty = kEmpty;
       else if (eff) ty = type_eff(c, r);
       else if (OP == RB_OR && (ta == kBitmap || tb == kBitmap)) {
         ty = type_lr(c);
         if (ty == kRun) r = 1; // LR's Run is the full container: one run
       } else ty = type_ab(c);
       if (CARD_ONLY) ty = c ? kArray : kEmpty;
-      else if (ty != kEmpty) emit_container(ty, w, c, r, dst, s, lane);
+      else if (ty != kEmpty) emit_container(bits ? (int)kBitmap : ty, w, c, r, dst, s, lane);
       nr = ty == kRun ? r : 0;
     } else if (has_a ? keeps_a_only(OP) : keeps_b_only(OP)) {
       // unmatched key: RoaringArray.appendCopy (RoaringArray.java:184-205)
@@ -1384,7 +1460,7 @@ __global__ __launch_bounds__(256, RBG_SMALL_WAVES) void k_pair_small(SmallPairAr
     if (lane == 0) {
       a.skey[slot] = has_a ? KA[ia] : KB[ib];
       a.stype[slot] = (uint8_t)ty;
-      a.scard[slot] = (uint32_t)c;
+      a.scard[slot] = cw != 0xFFFFFFFFu ? cw : (uint32_t)c;
       a.snruns[slot] = (uint16_t)nr;
       if (ty != kEmpty) {
         csum += (uint64_t)c;

@@ -190,6 +190,12 @@ class FastAggregation:
         return _wide(L.HORIZONTAL_XOR, bitmaps)
 
     @staticmethod
+    def priorityqueue_or(*bitmaps) -> RoaringBitmap:
+        """priorityqueue_or(RoaringBitmap...) (FastAggregation.java:675-721): lazy ORs of the two
+        smallest bitmaps (getLongSizeInBytes) on the device, the survivor repaired."""
+        return _wide(L.PQ_OR, bitmaps)
+
+    @staticmethod
     def priorityqueue_xor(*bitmaps) -> RoaringBitmap:
         return _wide(L.PQ_XOR, bitmaps)
 

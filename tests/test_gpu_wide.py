@@ -6,8 +6,8 @@ from datasets import DATASETS, EXPECTED, load_realdata, synthetic_bitmaps
 
 pytestmark = pytest.mark.gpu
 SEMS = ["FAST_OR", "FAST_AND", "WORKSHY_AND", "NAIVE_AND", "FAST_XOR", "PAR_OR", "PAR_XOR", "NAIVE_AND_ITER",
-        "HORIZONTAL_OR", "HORIZONTAL_XOR", "PQ_XOR"]
-SHARDABLE = [x for x in SEMS if x != "PQ_XOR"]  # priorityqueue_xor: whole results only
+        "HORIZONTAL_OR", "HORIZONTAL_XOR", "PQ_OR", "PQ_XOR"]
+SHARDABLE = [x for x in SEMS if x not in ("PQ_OR", "PQ_XOR")]  # priorityqueue_or/xor: whole results only
 
 
 def _check(ctx, oracle, s, refs, sem_name, members):
@@ -432,9 +432,50 @@ def test_queue_order_ties(ctx, oracle):
         refs = [oracle.RefBitmap.deserialize(b) for b in s.serialize()]
         for n in (2, 3, 7, 26):
             members = np.arange(n, dtype=np.uint32)
-            for sem in ("HORIZONTAL_OR", "HORIZONTAL_XOR", "PQ_XOR"):
+            for sem in ("HORIZONTAL_OR", "HORIZONTAL_XOR", "PQ_OR", "PQ_XOR"):
                 _check(ctx, oracle, s, refs, sem, members)
         members = np.array([3, 3, 5, 5, 5, 9], np.uint32)  # duplicates: empty xor containers kept
-        for sem in ("HORIZONTAL_XOR", "PQ_XOR", "HORIZONTAL_OR"):
+        for sem in ("HORIZONTAL_XOR", "PQ_XOR", "HORIZONTAL_OR", "PQ_OR"):
             _check(ctx, oracle, s, refs, sem, members)
     assert ctx.wide(rb.PQ_XOR, s, np.zeros(0, np.uint32)).n_containers == 0
+
+
+def test_priorityqueue_or_lazy_roles(ctx, oracle):
+    """FastAggregation.priorityqueue_or on the device (api.hip pq_or, pairwise.hip lazy_or_type): the
+    queue's three lazy roles (static lazyor, in-place lazyor, lazyorfromlazyinputs) meet
+      key 0  a Run of 1500 two-value runs and Arrays in its gaps: lazyorToRun keeps Runs of 2048..4096
+             runs (stored as bitmap words, sized 4r + 4), then more than 4096 -> a lazy Bitmap;
+      key 1  half-density Bitmaps whose union is full, and small Arrays that complete an exact Bitmap
+             (BitmapContainer.or(Array) -> full Run only when the Bitmap is not lazy);
+      key 2  Arrays whose cardinalities sum around ARRAY_LAZY_LOWERBOUND (1024);
+    over random member lists (duplicates allowed) with and without runOptimize."""
+    rng = np.random.default_rng(77)
+    pool = []
+    for b in range(10):
+        parts = []
+        if b % 3 == 0:
+            k0 = np.concatenate([np.arange(4 * i, 4 * i + 2) for i in range(1500)])
+        else:
+            lo = int(rng.integers(0, 1400))
+            k0 = 4 * np.arange(lo, lo + int(rng.integers(200, 1100))) + 3
+        parts.append(k0)
+        if b % 4 == 0:
+            k1 = np.flatnonzero(rng.random(65536) < 0.5)
+        elif b % 4 == 1:
+            k1 = np.setdiff1d(np.arange(65536), np.arange(0, 600))
+        elif b % 4 == 2:
+            s0 = int(rng.integers(0, 2)) * 300
+            k1 = np.arange(s0, s0 + 300)
+        else:
+            k1 = np.flatnonzero(rng.random(65536) >= 0.5)
+        parts.append(k1)
+        parts.append(np.sort(rng.choice(65536, size=int(rng.integers(300, 700)), replace=False)))
+        pool.append(np.concatenate([(np.asarray(p, np.int64) % 65536).astype(np.uint32) | np.uint32(k << 16)
+                                    for k, p in enumerate(parts)]))
+    for ro in (False, True):
+        s = ctx.upload_values(pool, run_optimize=ro)
+        refs = [oracle.RefBitmap.deserialize(x) for x in s.serialize()]
+        for n in (1, 2, 3, 4, 5, 7, 10, 16):
+            for _ in range(3):
+                members = rng.integers(0, len(pool), size=n).astype(np.uint32)
+                _check(ctx, oracle, s, refs, "PQ_OR", members)
