@@ -655,8 +655,10 @@ __global__ __launch_bounds__(256, ROLE == kRoleHeavy ? RBG_HEAVY_WAVES : RBG_LIG
 #if RBG_LIGHT_TIMING
   uint64_t lt_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, lt0 = 0, lt1 = 0, lt2 = 0; // decode, stage B/A/R, copy, filter, iteration, tasks
 #define RBG_LT(x) if (ROLE == kRoleLight) { x; }
+#define RBG_HT(x) if (ROLE == kRoleHeavy) { x; }
 #else
 #define RBG_LT(x)
+#define RBG_HT(x)
 #endif
   load_chunks(pq, tc.pp, tc.bigp ? 16u : tc.pbytes, lane);
   if (tc.kind == kCopy || tc.bigq) load_chunks(qq, tc.pp, 16, lane);
@@ -675,6 +677,7 @@ __global__ __launch_bounds__(256, ROLE == kRoleHeavy ? RBG_HEAVY_WAVES : RBG_LIG
     }
     const bool has_next = gn < n;
     RBG_LT(lt0 = __builtin_amdgcn_s_memtime());
+    RBG_HT(lt0 = __builtin_amdgcn_s_memtime());
     const RecU nx = RBG_REC_AHEAD && nn_ok ? nn : load_rec(recs + (has_next ? gn : g));
     if (RBG_REC_AHEAD) { // the record after next, where its index is already known, an iteration ahead
       uint64_t gnn = n;
@@ -692,6 +695,7 @@ __global__ __launch_bounds__(256, ROLE == kRoleHeavy ? RBG_HEAVY_WAVES : RBG_LIG
     }
     const Task tn = decode_task<OP>(nx, pay_a, pay_b);
     RBG_LT(lt1 = __builtin_amdgcn_s_memtime(); lt_acc[0] += lt1 - lt0);
+    RBG_HT(lt1 = __builtin_amdgcn_s_memtime(); lt_acc[0] += lt1 - lt0);
     int ty = kEmpty, c = 0;
     uint32_t nr = 0, cw = 0xFFFFFFFFu; // cw: the card word to store when it is not c (lazy marks)
     uint8_t *dst = out + cur.out;
@@ -747,6 +751,7 @@ __global__ __launch_bounds__(256, ROLE == kRoleHeavy ? RBG_HEAVY_WAVES : RBG_LIG
       }
       // ---- both next payloads in flight during classification and emission (the fence keeps the
       //      scheduler from hoisting these loads above the consumption of the current ones)
+      RBG_HT(lt2 = __builtin_amdgcn_s_memtime(); lt_acc[1] += lt2 - lt1);
       __builtin_amdgcn_sched_barrier(0);
       {
         const bool real = has_next && !tn.bigq;
@@ -758,6 +763,7 @@ __global__ __launch_bounds__(256, ROLE == kRoleHeavy ? RBG_HEAVY_WAVES : RBG_LIG
       const bool eff = eff_rule<OP>(ta, tb, tc.cp, tc.cq);
       int r;
       metrics(w, lane, (eff || (lazy && (ta == kRun || tb == kRun))) && !CARD_ONLY, c, r);
+      RBG_HT(const uint64_t lt3 = __builtin_amdgcn_s_memtime(); lt_acc[2] += lt3 - lt2; lt2 = lt3);
       bool bits = false;
       if (lazy) {
         ty = lazy_or_type(tm.lazy, ta, tb, tc.cp, tc.cq, c, r, cw, bits);
@@ -771,6 +777,7 @@ __global__ __launch_bounds__(256, ROLE == kRoleHeavy ? RBG_HEAVY_WAVES : RBG_LIG
       if (CARD_ONLY) ty = c ? kArray : kEmpty;
       else if (ty != kEmpty) emit_container(bits ? (int)kBitmap : ty, w, c, r, dst, s, lane);
       nr = ty == kRun ? (uint32_t)r : 0u;
+      RBG_HT(lt_acc[3 + (ty == kBitmap ? 0 : ty == kArray ? 1 : 2)] += __builtin_amdgcn_s_memtime() - lt2);
     } else if (ROLE != kRoleHeavy) {
       // ---- phase 1: stage X (filter) or store the clone (copy)
       if (tc.kind == kFilter && !(RBG_LIGHT_ABLATE & (tc.tq == kBitmap ? 1 : tc.tq == kArray ? 2 : 4))) {
@@ -827,6 +834,7 @@ __global__ __launch_bounds__(256, ROLE == kRoleHeavy ? RBG_HEAVY_WAVES : RBG_LIG
       tm.nruns[cur.t] = (uint16_t)nr;
     }
     RBG_LT(lt_acc[6] += __builtin_amdgcn_s_memtime() - lt0; ++lt_acc[7]);
+    RBG_HT(lt_acc[6] += __builtin_amdgcn_s_memtime() - lt0; ++lt_acc[7]);
     if (!has_next) break;
     if (new_chunk) {
       cend = nend;
@@ -842,6 +850,9 @@ __global__ __launch_bounds__(256, ROLE == kRoleHeavy ? RBG_HEAVY_WAVES : RBG_LIG
   if (ROLE == kRoleLight && lane == 0 && wv == 0 && blockIdx.x % 97 == 0)
     printf("light timing blk %u: decode %lu stageB %lu stageA %lu stageR %lu copy %lu filter %lu iter %lu tasks %lu\n",
            blockIdx.x, lt_acc[0], lt_acc[1], lt_acc[2], lt_acc[3], lt_acc[4], lt_acc[5], lt_acc[6], lt_acc[7]);
+  if (ROLE == kRoleHeavy && lane == 0 && wv == 0 && blockIdx.x % 61 == 0)
+    printf("heavy timing op %d blk %u: decode %lu build %lu metrics %lu emitB %lu emitA %lu emitR %lu iter %lu tasks %lu\n",
+           OP, blockIdx.x, lt_acc[0], lt_acc[1], lt_acc[2], lt_acc[3], lt_acc[4], lt_acc[5], lt_acc[6], lt_acc[7]);
 #endif
 }
 

@@ -757,15 +757,18 @@ __device__ __forceinline__ uint32_t emit_container(int type, const uint64_t (&w)
       const uint32_t open = (uint32_t)(h ? (w[j - 1] >> 63) : ((nb.prev_top_h0 >> k) & 1)) & (uint32_t)(w[j] & 1);
       uint32_t ep = sp - open;
       const uint32_t base = (uint32_t)(128 * k + 2 * lane + h) << 6;
-      uint64_t x = run_starts(w, nb, j);
-      while (x) {
-        S[sp++] = (uint16_t)(base + __builtin_ctzll(x));
-        x &= x - 1;
-      }
-      uint64_t y = run_ends(w, nb, j);
-      while (y) {
-        E[ep++] = (uint16_t)(base + __builtin_ctzll(y));
-        y &= y - 1;
+      // starts and ends of the word in ONE loop: a divergent while runs for the slowest lane, so two
+      // loops cost (max starts) + (max ends) trips, one costs about max(starts, ends)
+      uint64_t x = run_starts(w, nb, j), y = run_ends(w, nb, j);
+      while (x | y) {
+        if (x) {
+          S[sp++] = (uint16_t)(base + __builtin_ctzll(x));
+          x &= x - 1;
+        }
+        if (y) {
+          E[ep++] = (uint16_t)(base + __builtin_ctzll(y));
+          y &= y - 1;
+        }
       }
     }
   }
