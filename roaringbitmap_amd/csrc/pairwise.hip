@@ -361,6 +361,9 @@ __device__ __forceinline__ RecU load_rec(const TaskRec *r) {
 #ifndef RBG_FILTER_TRANSPOSE
 #define RBG_FILTER_TRANSPOSE 1 // probe a row in value order (adjacent lanes, adjacent values)
 #endif
+#ifndef RBG_RUN_REG_PREFIX
+#define RBG_RUN_REG_PREFIX 1 // register path: a Run operand's toggle image read once, prefix-xor in registers
+#endif
 #ifndef RBG_REC_AHEAD
 #define RBG_REC_AHEAD 0 // 1: task records loaded one task further ahead (measured neutral to slower: 4.06-4.17 vs 3.98-4.06 ms)
 #endif
@@ -725,6 +728,11 @@ __global__ __launch_bounds__(256, ROLE == kRoleHeavy ? RBG_HEAVY_WAVES : RBG_LIG
           w[2 * k] = pack2(pq[k].x, pq[k].y);
           w[2 * k + 1] = pack2(pq[k].z, pq[k].w);
         }
+      } else if (RBG_RUN_REG_PREFIX && tc.tp == kRun && !tc.bigp) {
+        stage_run_toggles(pq, tc.rp, s, lane); // toggles -> registers -> prefix-xor in registers
+        lds_read_words(s, w, lane);
+        wave_lds_sync();
+        toggles_to_words(w, lane);
       } else {
         if (tc.bigp) stage_big_runs(tc.pp, tc.rp, s, lane);
         else stage_from_chunks(tc.tp, pq, tc.cp, tc.rp, s, lane);
@@ -737,6 +745,14 @@ __global__ __launch_bounds__(256, ROLE == kRoleHeavy ? RBG_HEAVY_WAVES : RBG_LIG
           word_op<OP>(w[2 * k], pack2(qq[k].x, qq[k].y));
           word_op<OP>(w[2 * k + 1], pack2(qq[k].z, qq[k].w));
         }
+      } else if (RBG_RUN_REG_PREFIX && tc.tq == kRun && !tc.bigq) {
+        stage_run_toggles(qq, tc.rq, s, lane);
+        uint64_t t[kW];
+        lds_read_words(s, t, lane);
+        wave_lds_sync();
+        toggles_to_words(t, lane);
+#pragma unroll
+        for (int j = 0; j < kW; ++j) word_op<OP>(w[j], t[j]);
       } else {
         if (tc.bigq) stage_big_runs(tc.pq, tc.rq, s, lane);
         else stage_from_chunks(tc.tq, qq, tc.cq, tc.rq, s, lane);

@@ -556,6 +556,34 @@ __device__ __forceinline__ void store_chunks(const uint4 (&q)[8], uint8_t *p, ui
   }
 }
 
+// The toggle image of a register-preloaded Run payload (<= 2047 runs) in the wave's LDS scratch: bit
+// start and bit end+1 of every run (see stage_from_chunks); the caller reads it into registers and
+// finishes with toggles_to_words — one LDS pass instead of toggles_to_words_lds's three.
+__device__ __forceinline__ void stage_run_toggles(const uint4 (&q)[8], uint32_t nruns, uint32_t *s, int lane) {
+  lds_zero(s, lane);
+  wave_lds_sync();
+  const int nchunks = (int)((nruns + 3) >> 2);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int c = lane + 64 * i;
+    if (c < nchunks) {
+      const uint32_t r[4] = {q[i].x, q[i].y, q[i].z, q[i].w};
+      uint32_t x[8];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        x[2 * k] = r[k] & 0xFFFF;
+        x[2 * k + 1] = (r[k] & 0xFFFF) + (r[k] >> 16) + 1;
+      }
+      const int nr = min(4, (int)nruns - 4 * c);
+      int n = 2 * nr;
+      const uint32_t last = nr == 4 ? x[7] : nr == 3 ? x[5] : nr == 2 ? x[3] : x[1];
+      if (last >= (uint32_t)kSpan) --n; // only the container's last run can end at 65535
+      or_chunk_values(x, n, s);
+    }
+  }
+  wave_lds_sync();
+}
+
 // Membership image in LDS from a register-preloaded payload (Array <= 4096 values, Run <= 2047
 // runs, Bitmap 8 KiB — i.e. every canonical container whose payload fits 8 KiB).
 __device__ __forceinline__ void stage_from_chunks(int type, const uint4 (&q)[8], uint32_t card, uint32_t nruns,
