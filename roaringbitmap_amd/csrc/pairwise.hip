@@ -364,6 +364,9 @@ __device__ __forceinline__ RecU load_rec(const TaskRec *r) {
 #ifndef RBG_RUN_REG_PREFIX
 #define RBG_RUN_REG_PREFIX 1 // register path: a Run operand's toggle image read once, prefix-xor in registers
 #endif
+#ifndef RBG_LIGHT_RUN_REG
+#define RBG_LIGHT_RUN_REG 0 // 1: light filter computes a Run X's prefix-xor in registers (spills at 128 VGPRs: task phase 4.09-4.16 vs 3.95-4.04 ms)
+#endif
 #ifndef RBG_REC_AHEAD
 #define RBG_REC_AHEAD 0 // 1: task records loaded one task further ahead (measured neutral to slower: 4.06-4.17 vs 3.98-4.06 ms)
 #endif
@@ -798,7 +801,15 @@ __global__ __launch_bounds__(256, ROLE == kRoleHeavy ? RBG_HEAVY_WAVES : RBG_LIG
       // ---- phase 1: stage X (filter) or store the clone (copy)
       if (tc.kind == kFilter && !(RBG_LIGHT_ABLATE & (tc.tq == kBitmap ? 1 : tc.tq == kArray ? 2 : 4))) {
         if (tc.bigq) stage_big_runs(tc.pq, tc.rq, s, lane); // only a Run payload exceeds 8 KiB
-        else stage_from_chunks(tc.tq, qq, tc.cq, tc.rq, s, lane);
+        else if (RBG_LIGHT_RUN_REG && tc.tq == kRun) { // toggles -> registers (X's) -> prefix -> image
+          stage_run_toggles(qq, tc.rq, s, lane);
+          uint64_t t[kW];
+          lds_read_words(s, t, lane);
+          wave_lds_sync();
+          toggles_to_words(t, lane);
+          lds_write_words(s, t, lane);
+          wave_lds_sync();
+        } else stage_from_chunks(tc.tq, qq, tc.cq, tc.rq, s, lane);
       } else if (!CARD_ONLY) {
         if (tc.bigp) copy_payload(tc.pp, dst, tc.pbytes, lane);
         else store_chunks(pq, dst, tc.pbytes, lane);
