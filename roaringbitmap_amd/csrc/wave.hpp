@@ -710,6 +710,9 @@ __device__ __forceinline__ int type_runopt(int c, int r) {
 // ---------------------------------------------------------------- emission
 // Writes the container payload for `type` at `out` (16-B aligned slot); returns payload bytes.
 // `s` is the wave's 8 KiB LDS scratch (free on entry).
+#ifndef RBG_EMIT_ARRAY_PAIRS
+#define RBG_EMIT_ARRAY_PAIRS 0 // 1: two values per trip of the Array emission loop (measured neutral)
+#endif
 __device__ __forceinline__ uint32_t emit_container(int type, const uint64_t (&w)[kW], int card, int runs,
                                                    uint8_t *out, uint32_t *s, int lane) {
   if (type == kBitmap) {
@@ -743,10 +746,24 @@ __device__ __forceinline__ uint32_t emit_container(int type, const uint64_t (&w)
       for (int h = 0; h < 2; ++h) {
         uint64_t x = w[2 * k + h];
         const uint32_t base = (uint32_t)(128 * k + 2 * lane + h) << 6;
+#if RBG_EMIT_ARRAY_PAIRS
+        // two values per trip: a divergent while runs for the lane with the most values of the word
+        while (x) {
+          s16[pos] = (uint16_t)(base + __builtin_ctzll(x));
+          x &= x - 1;
+          if (x) {
+            s16[pos + 1] = (uint16_t)(base + __builtin_ctzll(x));
+            x &= x - 1;
+            ++pos;
+          }
+          ++pos;
+        }
+#else
         while (x) {
           s16[pos++] = (uint16_t)(base + __builtin_ctzll(x));
           x &= x - 1;
         }
+#endif
       }
     }
     wave_lds_sync();
