@@ -1592,7 +1592,7 @@ int rbref_serialize(const rbref_bitmap *b, uint8_t *dst, uint64_t cap) {
   }
   for (const Cont &c : b->vals) {
     if (c.t == kA) {
-      std::memcpy(p, c.v.data(), 2ull * c.card);
+      if (c.card) std::memcpy(p, c.v.data(), 2ull * c.card); // horizontal_xor may hold an empty one
       p += 2ull * c.card;
     } else if (c.t == kB) {
       std::memcpy(p, c.w.data(), 8192);

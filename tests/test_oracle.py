@@ -202,3 +202,21 @@ def test_java_priority_queue_tie_order(oracle):
     a = R.wide(R.HORIZONTAL_OR, bms).serialize()
     assert a == R.wide(R.HORIZONTAL_OR, bms).serialize()
     assert np.array_equal(R.RefBitmap.deserialize(a).to_array(), R.wide(R.FAST_OR, bms).to_array())
+
+
+def test_oracle_sanitizers_clean():
+    """The oracle under AddressSanitizer + UBSan (oracle/san_check.cpp via `make -C oracle san`):
+    random bitmaps of every container type through each pairwise op, every wide semantics and
+    the codec, including truncated / bit-flipped buffers (TestAdversarialInputs.java:18-62); the
+    first sanitizer report aborts the run."""
+    import os
+    import shutil
+    import subprocess
+
+    if shutil.which(os.environ.get("CXX", "g++")) is None:
+        pytest.skip("no host C++ compiler")
+    root = os.path.join(os.path.dirname(__file__), "..", "oracle")
+    subprocess.run(["make", "-s", "-C", root, "san_check"], check=True, timeout=600)
+    r = subprocess.run([os.path.join(root, "san_check"), "25", "7"], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "0 failures" in r.stdout
