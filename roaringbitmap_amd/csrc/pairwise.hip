@@ -382,6 +382,9 @@ __device__ __forceinline__ RecU load_rec(const TaskRec *r) {
 #ifndef RBG_FILTER_LINEAR
 #define RBG_FILTER_LINEAR 1 // the transposed filter with a linear stage (filter_rows_linear; 0: the ring)
 #endif
+#ifndef RBG_FILTER_WORDS
+#define RBG_FILTER_WORDS 0 // 1: light filter with F loaded in word order, no LDS transpose (correct; slower: light 4.05-4.17 vs 3.94-3.97 ms, stride-2 probes double the bank conflicts)
+#endif
 #ifndef RBG_LIGHT_WAVES
 #define RBG_LIGHT_WAVES 4 // waves per SIMD of the copy + filter kernel (128 VGPRs)
 #endif
@@ -666,7 +669,12 @@ __global__ __launch_bounds__(256, ROLE == kRoleHeavy ? RBG_HEAVY_WAVES : RBG_LIG
 #define RBG_LT(x)
 #define RBG_HT(x)
 #endif
-  load_chunks(pq, tc.pp, tc.bigp ? 16u : tc.pbytes, lane);
+  // P of a light filter task in word order (filter_words_linear), every other P in 16-B chunks
+  auto load_p = [&](const Task &t) {
+    if (ROLE == kRoleLight && RBG_FILTER_WORDS && t.kind == kFilter) load_words(pq, t.pp, t.pbytes, lane);
+    else load_chunks(pq, t.pp, t.bigp ? 16u : t.pbytes, lane);
+  };
+  load_p(tc);
   if (tc.kind == kCopy || tc.bigq) load_chunks(qq, tc.pp, 16, lane);
   else load_chunks(qq, tc.pq, tc.qbytes, lane);
   RecU nn{};
@@ -826,7 +834,12 @@ __global__ __launch_bounds__(256, ROLE == kRoleHeavy ? RBG_HEAVY_WAVES : RBG_LIG
         const int nfc = (int)((tc.cp + 7) >> 3);
         uint16_t *o = CARD_ONLY ? nullptr : reinterpret_cast<uint16_t *>(dst);
         auto none = [](int) {};
-#if RBG_FILTER_TRANSPOSE
+#if RBG_FILTER_WORDS
+        (void)nfc;
+        (void)none;
+        c = OP == RB_ANDNOT ? filter_words_linear<true, !CARD_ONLY>(pq, (int)tc.cp, s, ob, o, lane)
+                            : filter_words_linear<false, !CARD_ONLY>(pq, (int)tc.cp, s, ob, o, lane);
+#elif RBG_FILTER_TRANSPOSE
         (void)nfc;
         (void)none;
         uint4 *tb = tbuf[ROLE == kRoleLight ? wv : 0];
@@ -851,8 +864,8 @@ __global__ __launch_bounds__(256, ROLE == kRoleHeavy ? RBG_HEAVY_WAVES : RBG_LIG
         nr = tc.rp;
       }
       RBG_LT(lt_acc[5] += __builtin_amdgcn_s_memtime() - lt2);
-      if (!(RBG_EARLY_NEXT_P && RBG_FILTER_LINEAR && tc.kind == kFilter && !(RBG_LIGHT_ABLATE & 8)))
-        load_chunks(pq, tn.pp, tn.bigp ? 16u : tn.pbytes, lane);
+      if (!(RBG_EARLY_NEXT_P && RBG_FILTER_LINEAR && !RBG_FILTER_WORDS && tc.kind == kFilter && !(RBG_LIGHT_ABLATE & 8)))
+        load_p(tn);
     }
     wave_lds_sync(); // the next task restages the same LDS image
     if (lane == 0) {

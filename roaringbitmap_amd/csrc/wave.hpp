@@ -546,6 +546,83 @@ __device__ __forceinline__ int filter_rows_linear(const uint4 (&fq)[8], int nf, 
   return (int)tot;
 }
 
+// ---- F in word order: register word j (component j & 3 of q[j >> 2]) holds payload u32 word
+// 64 j + lane, i.e. values 2(64 j + lane) and +1, so adjacent lanes hold adjacent values without the
+// LDS transpose of filter_rows_linear.  Only the words of the payload are loaded (wave-uniform guards).
+__device__ __forceinline__ uint32_t &qword(uint4 &v, int k) { return k == 0 ? v.x : k == 1 ? v.y : k == 2 ? v.z : v.w; }
+__device__ __forceinline__ uint32_t qword(const uint4 &v, int k) { return k == 0 ? v.x : k == 1 ? v.y : k == 2 ? v.z : v.w; }
+__device__ __forceinline__ void load_words(uint4 (&q)[8], const uint8_t *p, uint32_t bytes, int lane) {
+  const __amdgpu_buffer_rsrc_t rs = chunk_rsrc(p, bytes);
+#pragma unroll
+  for (int j = 0; j < 32; ++j)
+    if ((uint32_t)(256 * j) < bytes) qword(q[j >> 2], j & 3) = __builtin_amdgcn_raw_buffer_load_b32(rs, (64 * j + lane) * 4, 0, 0);
+}
+
+// filter_rows_linear over F in word order: per register word the lane's two values are probed (two
+// probe instructions cover 128 consecutive values), ranked with two ballots (the low value first),
+// and written to the same linear stage and 16-B block flush.
+template <bool NEGATE, bool STORE>
+__device__ __forceinline__ int filter_words_linear(const uint4 (&fq)[8], int nf, const uint32_t *s, uint16_t *ob,
+                                                   uint16_t *out, int lane) {
+  static_assert(7 + 512 <= kStageRing, "every slot (pending < 8, + < 512 of a row) lies below the dummies");
+  const int iters = (nf + 511) >> 9; // wave-uniform, <= 8
+  uint32_t tot = 0, flushed = 0;
+  uint4 *out4 = reinterpret_cast<uint4 *>(out);
+  uint4 *ob4 = reinterpret_cast<uint4 *>(ob);
+  typedef __attribute__((address_space(3))) const uint32_t lds_u32;
+  lds_u32 *ls = (lds_u32 *)s;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    if (i < iters) {
+      uint32_t m[8];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) { // all 8 probes of the row in flight
+        const uint32_t x = qword(fq[i], k);
+        uint32_t wl, wh;
+        asm("v_bfe_u32 %0, %1, 5, 11" : "=v"(wl) : "v"(x));
+        asm("v_bfe_u32 %0, %1, 21, 11" : "=v"(wh) : "v"(x));
+        m[2 * k] = ls[wl];
+        m[2 * k + 1] = ls[wh];
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint32_t x = qword(fq[i], k);
+        const uint32_t bl = __builtin_amdgcn_ubfe(m[2 * k], x, 1u), bh = __builtin_amdgcn_ubfe(m[2 * k + 1], x >> 16, 1u);
+        uint64_t b0 = __builtin_amdgcn_uicmp(bl, 0u, NEGATE ? 32 : 33);
+        uint64_t b1 = __builtin_amdgcn_uicmp(bh, 0u, NEGATE ? 32 : 33);
+        const int lim = nf - 128 * (4 * i + k); // values left from this word's first
+        if (lim < 128) { // lane l holds values 2l, 2l+1 of the 128
+          const int l0 = (lim + 1) >> 1, l1 = lim >> 1;
+          b0 &= l0 > 0 ? (l0 >= 64 ? ~0ull : (1ull << l0) - 1ull) : 0ull;
+          b1 &= l1 > 0 ? (1ull << l1) - 1ull : 0ull;
+        }
+        if (STORE) {
+          const uint32_t p0 = __builtin_amdgcn_mbcnt_hi((uint32_t)(b0 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b0, tot - flushed));
+          const uint32_t p1 = __builtin_amdgcn_mbcnt_hi((uint32_t)(b1 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b1, p0));
+          uint32_t s0, s1; // the high value after the low one when both are kept
+          asm("v_cndmask_b32 %0, %1, %2, %3" : "=v"(s0) : "v"((uint32_t)(kStageRing + lane)), "v"(p1), "s"(b0));
+          const uint32_t ph = p1 + (uint32_t)((b0 >> lane) & 1);
+          asm("v_cndmask_b32 %0, %1, %2, %3" : "=v"(s1) : "v"((uint32_t)(kStageRing + lane)), "v"(ph), "s"(b1));
+          ob[s0] = (uint16_t)x;
+          ob[s1] = (uint16_t)(x >> 16);
+        }
+        tot += (uint32_t)__popcll(b0) + (uint32_t)__popcll(b1);
+      }
+      if (STORE) {
+        wave_lds_sync(); // the blocks hold other lanes' values
+        const uint32_t pend = tot - flushed, nb = pend >> 3;
+        if ((uint32_t)lane < nb) out4[(flushed >> 3) + lane] = ob4[lane];
+        if (lane == 0 && nb && (pend & 7u)) ob4[0] = ob4[nb]; // the partial block to the front
+        wave_lds_sync();
+        flushed += nb << 3;
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  if (STORE && tot > flushed && lane == 0) out4[flushed >> 3] = ob4[0];
+  return (int)tot;
+}
+
 __device__ __forceinline__ void store_chunks(const uint4 (&q)[8], uint8_t *p, uint32_t bytes, int lane) {
   uint4 *p4 = reinterpret_cast<uint4 *>(p);
   const int n = (int)((bytes + 15) >> 4);
