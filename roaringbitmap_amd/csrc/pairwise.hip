@@ -385,6 +385,9 @@ __device__ __forceinline__ RecU load_rec(const TaskRec *r) {
 #ifndef RBG_FILTER_WORDS
 #define RBG_FILTER_WORDS 0 // 1: light filter with F loaded in word order, no LDS transpose (correct; slower: light 4.05-4.17 vs 3.94-3.97 ms, stride-2 probes double the bank conflicts)
 #endif
+#ifndef RBG_HEAVY_COMBINE
+#define RBG_HEAVY_COMBINE 0 // 1: register path OR / XOR stages A|A, A^A, R^R as one LDS image (one zero + one read; correct, measured neutral)
+#endif
 #ifndef RBG_LIGHT_WAVES
 #define RBG_LIGHT_WAVES 4 // waves per SIMD of the copy + filter kernel (128 VGPRs)
 #endif
@@ -733,7 +736,24 @@ __global__ __launch_bounds__(256, ROLE == kRoleHeavy ? RBG_HEAVY_WAVES : RBG_LIG
       // ---- the result as a register bitmap: P = A, Q = B (never swapped: ANDNOT and the type
       //      rules are ordered)
       uint64_t w[kW];
-      if (bitmap_payload(tc.tp, tc.cp)) {
+      const bool comb = RBG_HEAVY_COMBINE && (OP == RB_OR || OP == RB_XOR) && !tc.bigp && !tc.bigq &&
+                        !bitmap_payload(tc.tp, tc.cp) && !bitmap_payload(tc.tq, tc.cq) &&
+                        ((tc.tp == kArray && tc.tq == kArray) || (OP == RB_XOR && tc.tp == kRun && tc.tq == kRun));
+      if (comb) { // both operands into one image: P | Q, P ^ Q, or the toggles of P ^ Q
+        lds_zero(s, lane);
+        wave_lds_sync();
+        if (tc.tp == kArray) {
+          scatter_array_chunks<false>(pq, tc.cp, s, lane);
+          scatter_array_chunks<OP == RB_XOR>(qq, tc.cq, s, lane);
+        } else {
+          scatter_run_toggles<false>(pq, tc.rp, s, lane);
+          scatter_run_toggles<true>(qq, tc.rq, s, lane);
+        }
+        wave_lds_sync();
+        lds_read_words(s, w, lane);
+        wave_lds_sync();
+        if (tc.tp == kRun) toggles_to_words(w, lane);
+      } else if (bitmap_payload(tc.tp, tc.cp)) {
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
           w[2 * k] = pack2(pq[k].x, pq[k].y);
@@ -750,7 +770,8 @@ __global__ __launch_bounds__(256, ROLE == kRoleHeavy ? RBG_HEAVY_WAVES : RBG_LIG
         lds_read_words(s, w, lane);
         wave_lds_sync();
       }
-      if (bitmap_payload(tc.tq, tc.cq)) {
+      if (comb) {
+      } else if (bitmap_payload(tc.tq, tc.cq)) {
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
           word_op<OP>(w[2 * k], pack2(qq[k].x, qq[k].y));

@@ -126,6 +126,7 @@ __device__ __forceinline__ void lds_write_words(uint32_t *s, const uint64_t (&w)
 // last value and 0 elsewhere (an OR of 0 changes nothing).  No value-dependent branch: the earlier
 // form branched per value on "new word?", which cost ~16 SALU exec-mask instructions per value.
 // Values past n OR 0 into the word of the last live value.
+template <bool XOR = false> // XOR: ds_xor instead of ds_or (a second operand into the same image)
 __device__ __forceinline__ void or_chunk_values(const uint32_t (&x)[8], int n, uint32_t *s) {
   uint32_t acc = 0, prev = x[0] >> 5;
   const uint32_t lastw = x[n - 1 < 7 ? n - 1 : 7] >> 5;
@@ -135,8 +136,10 @@ __device__ __forceinline__ void or_chunk_values(const uint32_t (&x)[8], int n, u
     const uint32_t wi = live ? x[i] >> 5 : lastw;
     acc = (wi == prev ? acc : 0u) | (live ? 1u << (x[i] & 31) : 0u);
     prev = wi;
-    const bool last = i == 7 || i + 1 >= n || (x[i + 1] >> 5) != wi;
-    atomicOr(&s[wi], last ? acc : 0u);
+    // past n the last group's mask would be re-emitted: harmless for ds_or, not for ds_xor
+    const bool last = live && (i == 7 || i + 1 >= n || (x[i + 1] >> 5) != wi);
+    if (XOR) atomicXor(&s[wi], last ? acc : 0u);
+    else atomicOr(&s[wi], last ? acc : 0u);
   }
 }
 
@@ -659,6 +662,46 @@ __device__ __forceinline__ void stage_run_toggles(const uint4 (&q)[8], uint32_t 
     }
   }
   wave_lds_sync();
+}
+
+// Two operands into ONE LDS image for the register path's OR / XOR (the caller zeroes it first):
+// an Array's values (ds_or, or ds_xor for the second operand of an XOR: an Array's own values are
+// distinct bits, so the image becomes P | Q or P ^ Q), or a Run's toggles (the second Run's by
+// ds_xor: toggle images are linear under xor, so the prefix-xor of the sum is P ^ Q).
+template <bool XOR>
+__device__ __forceinline__ void scatter_array_chunks(const uint4 (&q)[8], uint32_t card, uint32_t *s, int lane) {
+  const int nchunks = (int)((card + 7) >> 3);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int c = lane + 64 * i;
+    if (c < nchunks) {
+      const uint32_t x[8] = {q[i].x & 0xFFFF, q[i].x >> 16, q[i].y & 0xFFFF, q[i].y >> 16,
+                             q[i].z & 0xFFFF, q[i].z >> 16, q[i].w & 0xFFFF, q[i].w >> 16};
+      or_chunk_values<XOR>(x, min(8, (int)card - 8 * c), s);
+    }
+  }
+}
+template <bool XOR>
+__device__ __forceinline__ void scatter_run_toggles(const uint4 (&q)[8], uint32_t nruns, uint32_t *s, int lane) {
+  const int nchunks = (int)((nruns + 3) >> 2);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int c = lane + 64 * i;
+    if (c < nchunks) {
+      const uint32_t r[4] = {q[i].x, q[i].y, q[i].z, q[i].w};
+      uint32_t x[8];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        x[2 * k] = r[k] & 0xFFFF;
+        x[2 * k + 1] = (r[k] & 0xFFFF) + (r[k] >> 16) + 1;
+      }
+      const int nr = min(4, (int)nruns - 4 * c);
+      int n = 2 * nr;
+      const uint32_t last = nr == 4 ? x[7] : nr == 3 ? x[5] : nr == 2 ? x[3] : x[1];
+      if (last >= (uint32_t)kSpan) --n; // only the container's last run can end at 65535
+      or_chunk_values<XOR>(x, n, s);
+    }
+  }
 }
 
 // Membership image in LDS from a register-preloaded payload (Array <= 4096 values, Run <= 2047
