@@ -162,6 +162,13 @@ int rbgpu_set_type_stats(const rbgpu_set *set, uint64_t *out /* [6] */);
 /* Algorithmic bytes (payload + 16 B metadata) per high key over every container of the set:
  * out[65536].  Feeds the byte-balanced key-range partition of a sharded wide aggregation. */
 int rbgpu_set_key_bytes(const rbgpu_set *set, uint64_t *out);
+/* Containers of each member (members NULL = bitmaps 0..n-1) with high key in [key_lo, key_hi) ->
+ * out[n].  Summed over the ranks of a key-range partition it is each bitmap's
+ * highLowContainer.size(), the order FastAggregation.naive_and(varargs) starts from
+ * (FastAggregation.java:328-346): rbgpu_wide_sharded and ShardedWide use it so every shard starts
+ * from the globally smallest member. */
+int rbgpu_set_range_counts(const rbgpu_set *set, const uint32_t *members, uint32_t n, uint32_t key_lo,
+                           uint32_t key_hi, uint64_t *out);
 /* Download bitmaps [first, first+count) as host SoA.  Call once with soa->key == NULL to get
  * n_containers / payload_bytes, allocate, call again to fill. */
 int rbgpu_set_download(const rbgpu_set *set, uint32_t first, uint32_t count, rb_soa *soa);
@@ -184,7 +191,8 @@ int rbgpu_wide(rbgpu_ctx *ctx, int sem, const rbgpu_set *in, const uint32_t *mem
  * Every key is independent and keeps its member order, so the shards of a partition of
  * [0, 65536), concatenated in key order, are exactly rbgpu_wide's result.  For
  * RB_NAIVE_AND the smallest member is chosen within the shard's containers; a sharded caller
- * passes the globally ordered member list with RB_NAIVE_AND_ITER instead. */
+ * passes the globally ordered member list with RB_NAIVE_AND_ITER instead (rbgpu_wide_sharded and
+ * ShardedWide.aggregate do, from the all-reduced rbgpu_set_range_counts). */
 int rbgpu_wide_keys(rbgpu_ctx *ctx, int sem, const rbgpu_set *in, const uint32_t *members, uint32_t n,
                     uint32_t key_lo, uint32_t key_hi, rbgpu_set **out);
 /* FastAggregation.andCardinality / orCardinality — FastAggregation.java:71-101 */
@@ -273,7 +281,11 @@ typedef struct rb_shard_summary {
  * an all-gather of (cardinality, containers, Run containers, payload bytes, shard bytes) over the
  * communicator.  Collective. */
 int rbgpu_shard_summarize(rbgpu_comm *comm, const rbgpu_set *local, rb_shard_summary *out);
-/* rbgpu_wide_keys over [key_lo, key_hi) on this rank's GPU + rbgpu_shard_summarize.  Collective. */
+/* rbgpu_wide_keys over [key_lo, key_hi) on this rank's GPU + rbgpu_shard_summarize.  Collective.
+ * RB_NAIVE_AND (and RB_FAST_AND over <= 10 members, which is naive_and) first all-reduces the
+ * members' rbgpu_set_range_counts so every shard folds from the globally smallest bitmap, as the
+ * unsharded call does.  RB_PQ_OR / RB_PQ_XOR are refused (their merge order follows whole-bitmap
+ * sizes of intermediate results). */
 int rbgpu_wide_sharded(rbgpu_comm *comm, int sem, const rbgpu_set *in, const uint32_t *members, uint32_t n,
                        uint32_t key_lo, uint32_t key_hi, rbgpu_set **local, rb_shard_summary *summary);
 /* rbgpu_bsi_compare_keys over [key_lo, key_hi) + rbgpu_shard_summarize.  Collective. */

@@ -98,6 +98,7 @@ SIGNATURES = {
     "rbgpu_wide_keys": (C.c_int, [_P, C.c_int, _P, _U32P, C.c_uint32, C.c_uint32, C.c_uint32, C.POINTER(_P)]),
     "rbgpu_wide_cardinality": (C.c_int, [_P, C.c_int, _P, _U32P, C.c_uint32, _U64P]),
     "rbgpu_set_key_bytes": (C.c_int, [_P, _U64P]),
+    "rbgpu_set_range_counts": (C.c_int, [_P, _U32P, C.c_uint32, C.c_uint32, C.c_uint32, _U64P]),
     "rbgpu_set_type_stats": (C.c_int, [_P, _U64P]),
     "rbgpu_set_summaries": (C.c_int, [_P, C.c_uint32, C.c_uint32, C.POINTER(RbBitmapSummary)]),
     "rbgpu_bsi_compare": (C.c_int, [_P, _P, C.c_int, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64, _P,

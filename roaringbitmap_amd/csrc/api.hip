@@ -622,6 +622,53 @@ int rbgpu_set_type_stats(const rbgpu_set *s, uint64_t *out) {
   return RB_OK;
 }
 
+// containers of each member with high key in [lo, hi): two binary searches over its sorted keys
+__global__ void k_range_counts(const uint64_t *begin, const uint16_t *key, const uint32_t *members, uint32_t n,
+                               uint32_t lo, uint32_t hi, uint64_t *out) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t m = members ? members[i] : i;
+  const uint64_t b = begin[m], e = begin[m + 1];
+  auto lower = [&](uint32_t k) {
+    uint64_t l = b, h = e;
+    while (l < h) {
+      const uint64_t mid = (l + h) >> 1;
+      if (key[mid] < k) l = mid + 1;
+      else h = mid;
+    }
+    return l;
+  };
+  out[i] = lower(hi) - lower(lo);
+}
+
+int rbgpu_set_range_counts(const rbgpu_set *s, const uint32_t *members, uint32_t n, uint32_t key_lo, uint32_t key_hi,
+                           uint64_t *out) {
+  if (!s || (n && !out)) return fail(RB_EINVAL, "null argument");
+  if (key_lo > key_hi || key_hi > 65536u) return fail(RB_EINVAL, "key range [%u, %u) outside [0, 65536]", key_lo, key_hi);
+  if (!members && n != s->nb) return fail(RB_EINVAL, "without a member list n must be the bitmap count");
+  for (uint32_t i = 0; members && i < n; ++i)
+    if (members[i] >= s->nb) return fail(RB_EINVAL, "member %u out of range", members[i]);
+  int rc = check_ctx(s->ctx);
+  if (rc) return rc;
+  if (!n) return RB_OK;
+  HIPCHK(hipSetDevice(s->ctx->device));
+  uint32_t *d_m = nullptr;
+  uint64_t *d_out = nullptr;
+  if ((members && s->ctx->pool.alloc((void **)&d_m, 4ull * n)) || s->ctx->pool.alloc((void **)&d_out, 8ull * n)) {
+    if (d_m) s->ctx->pool.release(d_m);
+    return fail(RB_ENOMEM, "range counts");
+  }
+  hipStream_t st = s->ctx->stream;
+  if (members) HIPCHK(hipMemcpyAsync(d_m, members, 4ull * n, hipMemcpyHostToDevice, st));
+  k_range_counts<<<(n + 255) / 256, 256, 0, st>>>(s->begin, s->key, d_m, n, key_lo, key_hi, d_out);
+  HIPCHK(hipMemcpyAsync(out, d_out, 8ull * n, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  LAUNCHCHK();
+  if (d_m) s->ctx->pool.release(d_m);
+  s->ctx->pool.release(d_out);
+  return RB_OK;
+}
+
 int rbgpu_set_key_bytes(const rbgpu_set *s, uint64_t *out) {
   if (!s || !out) return fail(RB_EINVAL, "null argument");
   int rc = check_ctx(s->ctx);

@@ -366,7 +366,38 @@ int rbgpu_shard_summarize(rbgpu_comm *c, const rbgpu_set *local, rb_shard_summar
 int rbgpu_wide_sharded(rbgpu_comm *c, int sem, const rbgpu_set *in, const uint32_t *members, uint32_t n,
                        uint32_t key_lo, uint32_t key_hi, rbgpu_set **local, rb_shard_summary *summary) {
   if (!c || !local || !summary) return fail(RB_EINVAL, "null argument");
-  int rc = rbgpu_wide_keys(c->ctx, sem, in, members, n, key_lo, key_hi, local);
+  if (!in) return fail(RB_EINVAL, "null input set");
+  int rc;
+  std::vector<uint32_t> ord;
+  if (sem == RB_NAIVE_AND || (sem == RB_FAST_AND && n <= 10)) {
+    // naive_and(varargs) starts from the bitmap with the fewest containers (first on ties) and skips
+    // it by identity (FastAggregation.java:328-346): its container counts are global, so they are the
+    // ranks' key-range counts summed; then every shard folds the same order (naive_and(Iterator))
+    std::vector<uint32_t> mem(n);
+    for (uint32_t i = 0; i < n; ++i) mem[i] = members ? members[i] : i;
+    std::vector<uint64_t> cnt(n);
+    rc = rbgpu_set_range_counts(in, mem.data(), n, key_lo, key_hi, cnt.data());
+    if (rc) return rc;
+    if (n) {
+      uint64_t *d = nullptr;
+      if (c->ctx->pool.alloc((void **)&d, 8ull * n)) return fail(RB_ENOMEM, "member counts");
+      hipStream_t st = c->ctx->stream;
+      HIPCHK(hipMemcpyAsync(d, cnt.data(), 8ull * n, hipMemcpyHostToDevice, st));
+      NCCLCHK(c->r, c->r->all_reduce(d, d, n, ncclUint64, ncclSum, c->nc, st));
+      HIPCHK(hipMemcpyAsync(cnt.data(), d, 8ull * n, hipMemcpyDeviceToHost, st));
+      HIPCHK(hipStreamSynchronize(st));
+      c->ctx->pool.release(d);
+      uint32_t sm = 0;
+      for (uint32_t i = 1; i < n; ++i)
+        if (cnt[i] < cnt[sm]) sm = i;
+      ord.push_back(mem[sm]);
+      for (uint32_t m : mem)
+        if (m != mem[sm]) ord.push_back(m);
+    }
+    rc = rbgpu_wide_keys(c->ctx, RB_NAIVE_AND_ITER, in, ord.data(), (uint32_t)ord.size(), key_lo, key_hi, local);
+  } else {
+    rc = rbgpu_wide_keys(c->ctx, sem, in, members, n, key_lo, key_hi, local);
+  }
   if (rc) return rc;
   rc = rbgpu_shard_summarize(c, *local, summary);
   if (rc) {

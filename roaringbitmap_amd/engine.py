@@ -10,7 +10,7 @@ from __future__ import annotations
 
 import ctypes as C
 from dataclasses import dataclass, field
-from typing import List, Optional, Sequence
+from typing import List, Optional, Sequence, Tuple
 
 import numpy as np
 
@@ -239,6 +239,15 @@ class DeviceSet:
         """Algorithmic bytes per high key (rbgpu_set_key_bytes), shape [65536]."""
         out = np.zeros(65536, np.uint64)
         L.check(L.lib().rbgpu_set_key_bytes(self.h, out.ctypes.data_as(L._U64P)))
+        return out
+
+    def range_counts(self, members=None, key_range: Tuple[int, int] = (0, 65536)) -> np.ndarray:
+        """Containers of each member with high key in key_range (rbgpu_set_range_counts)."""
+        m = None if members is None else np.ascontiguousarray(members, dtype=np.uint32)
+        n = len(self) if m is None else len(m)
+        out = np.zeros(n, np.uint64)
+        L.check(L.lib().rbgpu_set_range_counts(self.h, None if m is None else m.ctypes.data_as(L._U32P), n,
+                                               int(key_range[0]), int(key_range[1]), out.ctypes.data_as(L._U64P)))
         return out
 
     def serialize(self, first: int = 0, count: Optional[int] = None) -> List[bytes]:

@@ -141,6 +141,37 @@ class ShardResult:
     payload_offset: int           # where this rank's first container payload starts in those bytes
 
 
+def _gather_blobs(dist, rank: int, world: int, device, blobs: Sequence[bytes], dst: int) -> Optional[List[List[bytes]]]:
+    """Every rank's byte strings on rank `dst` (None elsewhere), as tensors: an all_gather of the
+    (count, bytes) sizes, then two tensor gathers (the lengths, the concatenated bytes), each padded
+    to the largest rank's — no pickling."""
+    import torch
+    lens = np.array([len(b) for b in blobs], np.int64)
+    sz = torch.tensor([len(blobs), int(lens.sum())], dtype=torch.int64, device=device)
+    szs = [torch.zeros_like(sz) for _ in range(world)]
+    dist.all_gather(szs, sz)
+    g = torch.stack(szs).cpu().numpy()
+    maxn, maxb = max(int(g[:, 0].max()), 1), max(int(g[:, 1].max()), 1)
+    tl = torch.zeros(maxn, dtype=torch.int64, device=device)
+    tl[:len(blobs)] = torch.from_numpy(lens).to(device)
+    tb = torch.zeros(maxb, dtype=torch.uint8, device=device)
+    if int(lens.sum()):
+        tb[:int(lens.sum())] = torch.frombuffer(bytearray(b"".join(blobs)), dtype=torch.uint8).to(device)
+    gl = [torch.empty_like(tl) for _ in range(world)] if rank == dst else None
+    gb = [torch.empty_like(tb) for _ in range(world)] if rank == dst else None
+    dist.gather(tl, gl, dst=dst)
+    dist.gather(tb, gb, dst=dst)
+    if rank != dst:
+        return None
+    out = []
+    for r in range(world):
+        ln = gl[r].cpu().numpy()[:int(g[r, 0])]
+        data = gb[r].cpu().numpy().tobytes()
+        offs = np.concatenate([[0], np.cumsum(ln)])
+        out.append([data[int(offs[i]):int(offs[i + 1])] for i in range(len(ln))])
+    return out
+
+
 class ShardedWide:
     """Key-range-sharded FastAggregation / ParallelAggregation over torch.distributed.
 
@@ -169,18 +200,39 @@ class ShardedWide:
         return ShardResult(local, key_range, int(g[:, 0].sum()), n, int(g[:, 2].sum()), int(g[:, 3].sum()),
                            hdr + int(g[:, 3].sum()), hdr + before)
 
+    def naive_and_order(self, counts: Sequence[int], members: Sequence[int]) -> List[int]:
+        """FastAggregation.naive_and(varargs)'s fold order (FastAggregation.java:328-346): the bitmap
+        with the fewest containers (first on ties), then the others in order, skipping it by
+        identity.  Container counts are global, so this rank's key-range counts are summed over the
+        ranks (an all_reduce) — every shard then folds the same order as the unsharded call."""
+        import torch
+        t = torch.tensor([int(c) for c in counts], dtype=torch.int64, device=self.device)
+        self.dist.all_reduce(t)
+        tot = t.cpu().numpy()
+        if len(members) == 0:
+            return []
+        sm = members[int(np.argmin(tot))]  # argmin: the first minimal one
+        return [sm] + [m for m in members if m != sm]
+
     def aggregate(self, ctx, sem: int, dset, key_range: Tuple[int, int], members=None) -> ShardResult:
-        local = ctx.wide(sem, dset, members, key_range=key_range)
+        mem = list(range(len(dset))) if members is None else [int(m) for m in members]
+        if sem == L.NAIVE_AND or (sem == L.FAST_AND and len(mem) <= 10):
+            order = self.naive_and_order(dset.range_counts(mem, key_range), mem)
+            local = ctx.wide(L.NAIVE_AND_ITER, dset, order, key_range=key_range)
+        else:
+            local = ctx.wide(sem, dset, members, key_range=key_range)
         return self.finish(local, key_range, local.summaries()[0])
 
     def gather_serialized(self, res: ShardResult, dst: int = 0) -> Optional[bytes]:
-        """Global RoaringFormatSpec bytes on rank `dst` (None elsewhere)."""
-        h = res.local if isinstance(res.local, HostSoA) else res.local.download()
-        parts: List[Optional[HostSoA]] = [None] * self.world if self.rank == dst else None
-        self.dist.gather_object(h, parts, dst=dst)
-        if self.rank != dst:
+        """Global RoaringFormatSpec bytes on rank `dst` (None elsewhere): each shard serialized on its
+        rank, the bytes gathered as tensors, the header of the concatenation assembled by the
+        library (rbgpu_shard_assemble_host)."""
+        from .engine import assemble_host
+        mine = serialize_parts([res.local]) if isinstance(res.local, HostSoA) else res.local.serialize()[0]
+        parts = _gather_blobs(self.dist, self.rank, self.world, self.device, [mine], dst)
+        if parts is None:
             return None
-        return serialize_parts(parts)
+        return assemble_host([p[0] for p in parts])
 
 
 class ShardedBsi(ShardedWide):
@@ -252,8 +304,7 @@ class ShardedPairwise:
     def gather_serialized(self, res: PairShardResult, dst: int = 0) -> Optional[List[bytes]]:
         """Every result's RoaringFormatSpec bytes, in batch order, on rank `dst` (None elsewhere)."""
         mine = res.local.serialize() if hasattr(res.local, "serialize") else list(res.local)
-        parts: Optional[List[List[bytes]]] = [None] * self.world if self.rank == dst else None
-        self.dist.gather_object(mine, parts, dst=dst)
-        if self.rank != dst:
+        parts = _gather_blobs(self.dist, self.rank, self.world, self.device, mine, dst)
+        if parts is None:
             return None
         return [x for p in parts for x in p]

@@ -23,7 +23,7 @@ def test_comm_wide_sharded_gather(ctx, oracle, comm):
     import roaringbitmap_amd as rb
     vals = load_realdata("census1881_srt")[:40] + synthetic_bitmaps(30, seed=3, max_keys=12, key_space=40)
     s = ctx.upload_values(vals, run_optimize=True)
-    for sem in (rb.FAST_OR, rb.FAST_XOR, rb.WORKSHY_AND, rb.PAR_OR):
+    for sem in (rb.FAST_OR, rb.FAST_XOR, rb.WORKSHY_AND, rb.PAR_OR, rb.NAIVE_AND):
         want = ctx.wide(sem, s)
         want_bytes = want.serialize()[0]
         local, summ = comm.wide_sharded(sem, s, (0, 65536))
@@ -31,6 +31,8 @@ def test_comm_wide_sharded_gather(ctx, oracle, comm):
         assert summ["cardinality"] == int(want.cardinalities()[0])
         assert summ["container_offset"] == 0 and summ["local_serialized"] == len(want_bytes)
         assert comm.gather_serialized(local, summ) == want_bytes
+        if sem == rb.NAIVE_AND:  # its fold order needs a whole partition of the keys (the counts' sum)
+            continue
         # a sub-range shard at world size 1 is the whole result of that key range
         local2, summ2 = comm.wide_sharded(sem, s, (3, 17))
         part = ctx.wide(sem, s, key_range=(3, 17)).serialize()[0]

@@ -103,6 +103,9 @@ def test_key_range_shards_reassemble(ctx, oracle):
                 mem = np.array([members[first]] + [m for i, m in enumerate(members) if i != first], np.uint32)
                 sem_shard = rb.NAIVE_AND_ITER
             for parts in (3, 5):
+                if sem == "NAIVE_AND":  # the ranks' range counts sum to the container counts
+                    cnt = sum(s.range_counts(members, r) for r in partition_keys(kb, parts))
+                    assert cnt.tolist() == [len(refs[m].containers()) for m in members]
                 shards = [ctx.wide(sem_shard, s, mem, key_range=r) for r in partition_keys(kb, parts)]
                 got = serialize_parts([sh.download() for sh in shards])
                 assert got == want, (sem, n, parts)

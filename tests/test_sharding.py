@@ -16,7 +16,8 @@ from roaringbitmap_amd.sharding import (ShardedWide, header_size, pair_bytes, pa
                                         serialize_parts)
 
 SEMS = {"FAST_OR": L.FAST_OR, "WORKSHY_AND": L.WORKSHY_AND, "FAST_XOR": L.FAST_XOR, "PAR_OR": L.PAR_OR,
-        "PAR_XOR": L.PAR_XOR}
+        "PAR_XOR": L.PAR_XOR, "NAIVE_AND": L.NAIVE_AND, "HORIZONTAL_OR": L.HORIZONTAL_OR,
+        "HORIZONTAL_XOR": L.HORIZONTAL_XOR}
 
 
 def _subset(h: HostSoA, lo: int, hi: int) -> HostSoA:
@@ -125,7 +126,11 @@ def _rank_main(rank, world, port, q):
                 if i % 3 == 0:
                     sub.run_optimize()
                 shard_in.append(sub)
-            local = soa_from_serialized([R.wide(sem, shard_in).serialize()])
+            if name == "NAIVE_AND":  # the fold order from the all-reduced range counts
+                order = sw.naive_and_order([len(x.containers()) for x in shard_in], list(range(len(shard_in))))
+                local = soa_from_serialized([R.wide(R.NAIVE_AND_ITER, [shard_in[i] for i in order]).serialize()])
+            else:
+                local = soa_from_serialized([R.wide(sem, shard_in).serialize()])
             res = sw.finish(local, (lo, hi), host_summary(local))
             data = sw.gather_serialized(res)
             if rank == 0:
