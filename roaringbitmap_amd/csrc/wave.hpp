@@ -485,6 +485,9 @@ __device__ __forceinline__ int filter_rows_transposed(const uint4 (&fq)[8], int 
 // dummy slot.  ~8 VALU per 64 probed values instead of ~15 (ISA count).  Pending values stay < 8 + 512.
 // `next()` runs once the last row of F is in the transpose buffer — F's registers are free from
 // there, so the caller's prefetch of the next task's F overlaps the last row's probes and flush.
+#ifndef RBG_SKIP_EMPTY_HALF
+#define RBG_SKIP_EMPTY_HALF 1 // filter_rows_linear: a last row with <= 256 values skips its empty second half
+#endif
 template <bool NEGATE, bool STORE, class Next>
 __device__ __forceinline__ int filter_rows_linear(const uint4 (&fq)[8], int nf, const uint32_t *s, uint16_t *ob,
                                                   uint4 *tb, uint16_t *out, int lane, const Next &next) {
@@ -501,6 +504,10 @@ __device__ __forceinline__ int filter_rows_linear(const uint4 (&fq)[8], int nf, 
     if (i < iters) {
 #pragma unroll
       for (int hf = 0; hf < 2; ++hf) {
+        if (RBG_SKIP_EMPTY_HALF && hf == 1 && nf - 512 * i <= 256) { // the row's values all lie in its first half
+          if (i == iters - 1) next();
+          continue;
+        }
         if ((lane >> 5) == hf) tb[lane & 31] = fq[i];
         wave_lds_sync();
         if (hf == 1 && i == iters - 1) next();
