@@ -388,6 +388,10 @@ __device__ __forceinline__ RecU load_rec(const TaskRec *r) {
 #ifndef RBG_HEAVY_COMBINE
 #define RBG_HEAVY_COMBINE 0 // 1: register path OR / XOR stages A|A, A^A, R^R as one LDS image (one zero + one read; correct, measured neutral)
 #endif
+#ifndef RBG_LOAD_USED_ROWS
+#define RBG_LOAD_USED_ROWS 0 // payload rows past a task's bytes not loaded (load_chunks_used): 0 never, 1 both task kernels (light much slower), 2 the register path only (neutral)
+#endif
+#define RBG_LOAD load_rows<ROLE>
 #ifndef RBG_LIGHT_WAVES
 #define RBG_LIGHT_WAVES 4 // waves per SIMD of the copy + filter kernel (128 VGPRs)
 #endif
@@ -623,6 +627,32 @@ __device__ __forceinline__ Chunk claim_chunk(unsigned long long *queue, uint64_t
   return Chunk{n, n};
 }
 
+// claim_chunk split in two so the atomic's return is waited for an iteration later, after the next
+// task's payload loads: waited for right after issue (claim_chunk), its vmcnt(0) also drains those
+// prefetches.  Issued only while a sub-range is left to try (the same condition as claim_chunk's).
+#ifndef RBG_CLAIM_EARLY
+#define RBG_CLAIM_EARLY 1
+#endif
+__device__ __forceinline__ unsigned long long claim_issue(unsigned long long *queue, uint32_t k, uint32_t tried, int lane) {
+  unsigned long long v = 0;
+  if (tried < kQueueStripes && lane == 0)
+    v = __hip_atomic_fetch_add(queue + k * kQueueStride, (unsigned long long)kQueueChunk, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+  return v;
+}
+__device__ __forceinline__ Chunk claim_finish(unsigned long long v, unsigned long long *queue, uint64_t n, uint32_t &k,
+                                              uint32_t &tried, int lane) {
+  if (tried < kQueueStripes) {
+    const uint64_t lo = n * k / kQueueStripes, hi = n * (k + 1) / kQueueStripes;
+    const uint64_t st = lo + pack2(__builtin_amdgcn_readfirstlane((uint32_t)v),
+                                   __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)));
+    if (st < hi) return Chunk{st, min(st + kQueueChunk, hi)};
+    k = (k + 1) % kQueueStripes;
+    ++tried;
+  }
+  return claim_chunk(queue, n, k, tried, lane); // the following sub-ranges, synchronously
+}
+
 // The task kernel, ONE WAVE PER TASK, persistent waves striding over one record list with a
 // one-task software pipeline: the next task's record and both payloads are in flight while the
 // current one computes.  Loads sit at fixed points of the loop body (a task with fewer payloads
@@ -632,6 +662,12 @@ __device__ __forceinline__ Chunk claim_chunk(unsigned long long *queue, uint64_t
 //   ROLE kRoleHeavy (register path): build the 65536-bit result in registers from P and Q, load
 //                   both next payloads, then classify and emit.
 enum { kRoleLight = 0, kRoleHeavy = 1 };
+// Guarded loads keep fully out-of-range rows off the texture data path; in the light kernel they
+// cost more than they save (A/B: light 4.73-4.82 vs 3.96-3.97 ms with them).
+template <int ROLE> __device__ __forceinline__ void load_rows(uint4 (&q)[8], const uint8_t *p, uint32_t bytes, int lane) {
+  if (RBG_LOAD_USED_ROWS == 1 || (RBG_LOAD_USED_ROWS == 2 && ROLE == kRoleHeavy)) load_chunks_used(q, p, bytes, lane);
+  else load_chunks(q, p, bytes, lane);
+}
 template <int OP, bool CARD_ONLY, int ROLE>
 __global__ __launch_bounds__(256, ROLE == kRoleHeavy ? RBG_HEAVY_WAVES : RBG_LIGHT_WAVES) void k_pair_tasks(
     const uint8_t *__restrict__ pay_a, const uint8_t *__restrict__ pay_b, const TaskRec *__restrict__ recs,
@@ -675,11 +711,11 @@ __global__ __launch_bounds__(256, ROLE == kRoleHeavy ? RBG_HEAVY_WAVES : RBG_LIG
   // P of a light filter task in word order (filter_words_linear), every other P in 16-B chunks
   auto load_p = [&](const Task &t) {
     if (ROLE == kRoleLight && RBG_FILTER_WORDS && t.kind == kFilter) load_words(pq, t.pp, t.pbytes, lane);
-    else load_chunks(pq, t.pp, t.bigp ? 16u : t.pbytes, lane);
+    else RBG_LOAD(pq, t.pp, t.bigp ? 16u : t.pbytes, lane);
   };
   load_p(tc);
-  if (tc.kind == kCopy || tc.bigq) load_chunks(qq, tc.pp, 16, lane);
-  else load_chunks(qq, tc.pq, tc.qbytes, lane);
+  if (tc.kind == kCopy || tc.bigq) RBG_LOAD(qq, tc.pp, 16, lane);
+  else RBG_LOAD(qq, tc.pq, tc.qbytes, lane);
   RecU nn{};
   bool nn_ok = false;
   while (true) {
@@ -693,6 +729,8 @@ __global__ __launch_bounds__(256, ROLE == kRoleHeavy ? RBG_HEAVY_WAVES : RBG_LIG
       }
     }
     const bool has_next = gn < n;
+    unsigned long long claim_v = 0;
+    if (RBG_CLAIM_EARLY && new_chunk) claim_v = claim_issue(queue, qk, qtried, lane);
     RBG_LT(lt0 = __builtin_amdgcn_s_memtime());
     RBG_HT(lt0 = __builtin_amdgcn_s_memtime());
     const RecU nx = RBG_REC_AHEAD && nn_ok ? nn : load_rec(recs + (has_next ? gn : g));
@@ -727,9 +765,9 @@ __global__ __launch_bounds__(256, ROLE == kRoleHeavy ? RBG_HEAVY_WAVES : RBG_LIG
         __builtin_amdgcn_sched_barrier(0);
         {
           const bool real = has_next && !tn.bigq;
-          load_chunks(qq, real ? tn.pq : tn.pp, real ? tn.qbytes : 16u, lane);
+          RBG_LOAD(qq, real ? tn.pq : tn.pp, real ? tn.qbytes : 16u, lane);
         }
-        load_chunks(pq, tn.pp, tn.bigp ? 16u : tn.pbytes, lane);
+        RBG_LOAD(pq, tn.pp, tn.bigp ? 16u : tn.pbytes, lane);
       }
     }
     if (ROLE == kRoleHeavy && !done) {
@@ -803,9 +841,9 @@ __global__ __launch_bounds__(256, ROLE == kRoleHeavy ? RBG_HEAVY_WAVES : RBG_LIG
       __builtin_amdgcn_sched_barrier(0);
       {
         const bool real = has_next && !tn.bigq;
-        load_chunks(qq, real ? tn.pq : tn.pp, real ? tn.qbytes : 16u, lane);
+        RBG_LOAD(qq, real ? tn.pq : tn.pp, real ? tn.qbytes : 16u, lane);
       }
-      load_chunks(pq, tn.pp, tn.bigp ? 16u : tn.pbytes, lane);
+      RBG_LOAD(pq, tn.pp, tn.bigp ? 16u : tn.pbytes, lane);
       const int ta = tc.tp, tb = tc.tq;
       const bool lazy = OP == RB_OR && tm.lazy;
       const bool eff = eff_rule<OP>(ta, tb, tc.cp, tc.cq);
@@ -845,7 +883,7 @@ __global__ __launch_bounds__(256, ROLE == kRoleHeavy ? RBG_HEAVY_WAVES : RBG_LIG
       }
       {
         const bool real = has_next && tn.kind != kCopy && !tn.bigq;
-        load_chunks(qq, real ? tn.pq : tn.pp, real ? tn.qbytes : 16u, lane);
+        RBG_LOAD(qq, real ? tn.pq : tn.pp, real ? tn.qbytes : 16u, lane);
       }
       RBG_LT(lt2 = __builtin_amdgcn_s_memtime(); lt_acc[tc.kind == kFilter ? 1 + (tc.tq == kBitmap ? 0 : tc.tq == kArray ? 1 : 2) : 4] += lt2 - lt1);
       // ---- phase 2: filter F against the staged X.  (Streaming the next F into pq row by row as
@@ -866,7 +904,7 @@ __global__ __launch_bounds__(256, ROLE == kRoleHeavy ? RBG_HEAVY_WAVES : RBG_LIG
         uint4 *tb = tbuf[ROLE == kRoleLight ? wv : 0];
 #if RBG_FILTER_LINEAR
         auto next_f = [&]() { // the next task's P into the registers F has left
-          if (RBG_EARLY_NEXT_P) load_chunks(pq, tn.pp, tn.bigp ? 16u : tn.pbytes, lane);
+          if (RBG_EARLY_NEXT_P) RBG_LOAD(pq, tn.pp, tn.bigp ? 16u : tn.pbytes, lane);
         };
         c = OP == RB_ANDNOT ? filter_rows_linear<true, !CARD_ONLY>(pq, (int)tc.cp, s, ob, tb, o, lane, next_f)
                             : filter_rows_linear<false, !CARD_ONLY>(pq, (int)tc.cp, s, ob, tb, o, lane, next_f);
@@ -899,7 +937,8 @@ __global__ __launch_bounds__(256, ROLE == kRoleHeavy ? RBG_HEAVY_WAVES : RBG_LIG
     if (!has_next) break;
     if (new_chunk) {
       cend = nend;
-      const Chunk c1 = claim_chunk(queue, n, qk, qtried, lane);
+      const Chunk c1 = RBG_CLAIM_EARLY ? claim_finish(claim_v, queue, n, qk, qtried, lane)
+                                       : claim_chunk(queue, n, qk, qtried, lane);
       nxt = c1.s;
       nend = c1.e;
     }

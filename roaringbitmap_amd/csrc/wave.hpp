@@ -340,6 +340,16 @@ __device__ __forceinline__ void load_chunks(uint4 (&q)[8], const uint8_t *p, uin
 #pragma unroll
   for (int i = 0; i < 8; ++i) q[i] = load_chunk_row(rs, i, lane);
 }
+// load_chunks issuing only the 1 KiB rows the payload reaches (wave-uniform guards): a fully
+// out-of-range row costs no memory request but still a full 64-lane return through the texture
+// data path.  Rows past the payload keep stale registers — every consumer bounds its rows by the
+// payload's count (Array values, runs, F's values, copy bytes).
+__device__ __forceinline__ void load_chunks_used(uint4 (&q)[8], const uint8_t *p, uint32_t bytes, int lane) {
+  const __amdgpu_buffer_rsrc_t rs = chunk_rsrc(p, bytes);
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+    if ((uint32_t)(1024 * i) < bytes) q[i] = load_chunk_row(rs, i, lane);
+}
 
 // Exclusive prefix (over lanes) and wave total of a per-lane count in [0, 16), by bit-sliced ballots
 // and mbcnt: no cross-lane data movement through LDS, no dependency chain of shuffles.
