@@ -631,7 +631,7 @@ __device__ __forceinline__ Chunk claim_chunk(unsigned long long *queue, uint64_t
 // task's payload loads: waited for right after issue (claim_chunk), its vmcnt(0) also drains those
 // prefetches.  Issued only while a sub-range is left to try (the same condition as claim_chunk's).
 #ifndef RBG_CLAIM_EARLY
-#define RBG_CLAIM_EARLY 1
+#define RBG_CLAIM_EARLY 0 // 1: measured neutral with the atomic optimizer (it still consumes the result at once), slower without it (-mllvm -amdgpu-atomic-optimizer-strategy=None: heavy 3.32 vs 3.13 ms, ANDNOT 9.3 vs 8.1 ms)
 #endif
 __device__ __forceinline__ unsigned long long claim_issue(unsigned long long *queue, uint32_t k, uint32_t tried, int lane) {
   unsigned long long v = 0;
@@ -644,8 +644,9 @@ __device__ __forceinline__ Chunk claim_finish(unsigned long long v, unsigned lon
                                               uint32_t &tried, int lane) {
   if (tried < kQueueStripes) {
     const uint64_t lo = n * k / kQueueStripes, hi = n * (k + 1) / kQueueStripes;
-    const uint64_t st = lo + pack2(__builtin_amdgcn_readfirstlane((uint32_t)v),
-                                   __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)));
+    uint32_t vl = (uint32_t)v, vh = (uint32_t)(v >> 32);
+    asm volatile("" : "+v"(vl), "+v"(vh)); // pins the wait here: the readfirstlanes cannot move up to the atomic
+    const uint64_t st = lo + pack2(__builtin_amdgcn_readfirstlane(vl), __builtin_amdgcn_readfirstlane(vh));
     if (st < hi) return Chunk{st, min(st + kQueueChunk, hi)};
     k = (k + 1) % kQueueStripes;
     ++tried;
