@@ -136,8 +136,8 @@ __device__ __forceinline__ void or_chunk_values(const uint32_t (&x)[8], int n, u
     const uint32_t wi = live ? x[i] >> 5 : lastw;
     acc = (wi == prev ? acc : 0u) | (live ? 1u << (x[i] & 31) : 0u);
     prev = wi;
-    // past n the last group's mask would be re-emitted: harmless for ds_or, not for ds_xor
-    const bool last = live && (i == 7 || i + 1 >= n || (x[i + 1] >> 5) != wi);
+    // past n the last group's mask is re-emitted: harmless for ds_or, not for ds_xor
+    const bool last = (!XOR || live) && (i == 7 || i + 1 >= n || (x[i + 1] >> 5) != wi);
     if (XOR) atomicXor(&s[wi], last ? acc : 0u);
     else atomicOr(&s[wi], last ? acc : 0u);
   }
