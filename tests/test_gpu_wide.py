@@ -482,3 +482,25 @@ def test_priorityqueue_or_lazy_roles(ctx, oracle):
             for _ in range(3):
                 members = rng.integers(0, len(pool), size=n).astype(np.uint32)
                 _check(ctx, oracle, s, refs, "PQ_OR", members)
+
+
+def test_range_counts_contract(ctx):
+    """rbgpu_set_range_counts: per-member container counts in a key range (the sharded naive_and's
+    global order), members NULL = every bitmap, and its argument checks."""
+    import pytest
+    import roaringbitmap_amd as rb
+    bms = synthetic_bitmaps(12, seed=41, max_keys=8, key_space=12)
+    s = ctx.upload_values(bms, run_optimize=True)
+    h = s.download()
+    full = np.diff(h.begin.astype(np.int64))
+    assert s.range_counts().tolist() == full.tolist()
+    members = np.array([3, 0, 3, 7], np.uint32)
+    assert s.range_counts(members).tolist() == full[members].tolist()
+    for lo, hi in ((0, 5), (5, 12), (12, 65536), (4, 4)):
+        want = [int(((h.key[h.begin[m]:h.begin[m + 1]] >= lo) & (h.key[h.begin[m]:h.begin[m + 1]] < hi)).sum())
+                for m in members]
+        assert s.range_counts(members, (lo, hi)).tolist() == want
+    with pytest.raises(rb.InvalidArgument):
+        s.range_counts(members, (7, 3))
+    with pytest.raises(rb.InvalidArgument):
+        s.range_counts(np.array([12], np.uint32))
