@@ -60,6 +60,8 @@ void set_release(rbgpu_set *s) {
   p.release(s->nruns);
   p.release(s->off);
   p.release(s->payload);
+  p.release(s->mrec);
+  p.release(s->krec);
   rbgpu_ctx *ctx = s->ctx;
   s->ctx = nullptr;
   ctx_unref(ctx);
@@ -135,6 +137,106 @@ int ensure_max_runs(const rbgpu_set *cs) {
     m = s->ctx->h_pinned[7];
   }
   s->max_runs = (int64_t)m;
+  return RB_OK;
+}
+// Derived metadata (rbgpu_set): built once per set on the set's stream, timed with events so the cost
+// is reported (rbgpu_set_derive_ms), then cached — the set is immutable.
+namespace {
+struct DeriveTimer {
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  rbgpu_set *s;
+  explicit DeriveTimer(rbgpu_set *s_) : s(s_) {
+    if (hipEventCreate(&e0) == hipSuccess && hipEventCreate(&e1) == hipSuccess) (void)hipEventRecord(e0, s->ctx->stream);
+  }
+  ~DeriveTimer() {
+    float ms = 0.f;
+    if (e0 && e1 && hipEventRecord(e1, s->ctx->stream) == hipSuccess && hipEventSynchronize(e1) == hipSuccess &&
+        hipEventElapsedTime(&ms, e0, e1) == hipSuccess)
+      s->derive_ms += ms;
+    if (e0) (void)hipEventDestroy(e0);
+    if (e1) (void)hipEventDestroy(e1);
+  }
+};
+} // namespace
+int ensure_dense(const rbgpu_set *cs) {
+  rbgpu_set *s = const_cast<rbgpu_set *>(cs);
+  if (s->dense_lo != -2) return RB_OK;
+  int rc = ensure_h_begin(s);
+  if (rc) return rc;
+  s->dense_lo = s->dense_hi = -1;
+  if (!s->nb) return RB_OK;
+  const uint64_t cnt = s->h_begin[1] - s->h_begin[0];
+  if (!cnt) return RB_OK;
+  for (uint32_t b = 1; b < s->nb; ++b)
+    if (s->h_begin[b + 1] - s->h_begin[b] != cnt) return RB_OK;
+  HIPCHK(hipSetDevice(s->ctx->device));
+  uint16_t k0 = 0;
+  uint32_t *d = nullptr;
+  if (s->ctx->pool.alloc((void **)&d, 4)) return fail(RB_ENOMEM, "dense-check word");
+  hipStream_t st = s->ctx->stream;
+  HIPCHK(hipMemcpyAsync(&k0, s->key + s->h_begin[0], 2, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  uint32_t bad = 1;
+  if ((uint64_t)k0 + cnt <= 65536) {
+    HIPCHK(hipMemsetAsync(d, 0, 4, st));
+    launch_dense_check(s->view(), s->nb, k0, (uint32_t)cnt, d, st);
+    HIPCHK(hipMemcpyAsync(&bad, d, 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    LAUNCHCHK();
+  }
+  s->ctx->pool.release(d);
+  if (!bad) {
+    s->dense_lo = k0;
+    s->dense_hi = (int64_t)k0 + (int64_t)cnt;
+  }
+  return RB_OK;
+}
+int ensure_mrec(const rbgpu_set *cs) {
+  rbgpu_set *s = const_cast<rbgpu_set *>(cs);
+  if (s->mrec) return RB_OK;
+  if (s->payload_bytes >= kRecMaxPayload) return fail(RB_EINVAL, "packed records hold 40-bit payload offsets");
+  HIPCHK(hipSetDevice(s->ctx->device));
+  uint64_t *m = nullptr;
+  if (s->ctx->pool.alloc((void **)&m, std::max<uint64_t>(s->nc, 1) * 8)) return fail(RB_ENOMEM, "packed records");
+  {
+    DeriveTimer t(s);
+    launch_pack_records(s->view(), s->nc, m, s->ctx->stream);
+  }
+  if (hipGetLastError() != hipSuccess) {
+    s->ctx->pool.release(m);
+    return fail(RB_EDEVICE, "packed-record kernel failed");
+  }
+  s->mrec = m;
+  return RB_OK;
+}
+int ensure_krec(const rbgpu_set *cs) {
+  rbgpu_set *s = const_cast<rbgpu_set *>(cs);
+  if (s->krec) return RB_OK;
+  int rc = ensure_dense(s);
+  if (!rc) rc = ensure_mrec(s);
+  if (rc) return rc;
+  if (s->dense_lo < 0) return fail(RB_EINVAL, "key-major records need a dense set");
+  HIPCHK(hipSetDevice(s->ctx->device));
+  hipStream_t st = s->ctx->stream;
+  uint64_t *k = nullptr, *mb = nullptr;
+  if (s->ctx->pool.alloc((void **)&k, std::max<uint64_t>(s->nc, 1) * 8) || s->ctx->pool.alloc((void **)&mb, s->nb * 8ull)) {
+    s->ctx->pool.release(k);
+    return fail(RB_ENOMEM, "key-major records");
+  }
+  // member bases in set order: container of bitmap b at key x is h_begin[b] + x - dense_lo
+  std::vector<uint64_t> hb(s->nb);
+  for (uint32_t b = 0; b < s->nb; ++b) hb[b] = s->h_begin[b] - (uint64_t)s->dense_lo;
+  {
+    DeriveTimer t(s);
+    if (hipMemcpyAsync(mb, hb.data(), s->nb * 8ull, hipMemcpyHostToDevice, st) == hipSuccess)
+      launch_records_transpose(s->mrec, mb, s->nb, (uint32_t)s->dense_lo, (uint32_t)s->dense_hi, k, st);
+  }
+  s->ctx->pool.release(mb);
+  if (hipGetLastError() != hipSuccess) {
+    s->ctx->pool.release(k);
+    return fail(RB_EDEVICE, "key-major record kernel failed");
+  }
+  s->krec = k;
   return RB_OK;
 }
 } // namespace rbg

@@ -71,4 +71,15 @@ __host__ __device__ inline uint64_t payload_bytes(int type, uint32_t card, uint3
 }
 __host__ __device__ inline uint64_t round16(uint64_t x) { return (x + 15) & ~15ull; }
 
+// Packed 8-B container record (rbgpu_set::mrec / krec): payload byte offset (40 bits), card (17),
+// min(nruns, 15) (4), type (2).  A run count of 15 means ">= 15" (the Run-list fast paths take <= 8).
+__host__ __device__ inline uint64_t pack_rec(uint32_t typ, uint32_t card, uint32_t nr, uint64_t off) {
+  return off | ((uint64_t)card << 40) | ((uint64_t)(nr < 15u ? nr : 15u) << 57) | ((uint64_t)(typ & 3u) << 61);
+}
+__host__ __device__ inline uint32_t rec_type(uint64_t r) { return (uint32_t)(r >> 61) & 3u; }
+__host__ __device__ inline uint32_t rec_card(uint64_t r) { return (uint32_t)(r >> 40) & 0x1FFFFu; }
+__host__ __device__ inline uint32_t rec_nruns(uint64_t r) { return (uint32_t)(r >> 57) & 15u; }
+__host__ __device__ inline uint64_t rec_off(uint64_t r) { return r & ((1ull << 40) - 1); }
+constexpr uint64_t kRecMaxPayload = 1ull << 40;
+
 } // namespace rbg

@@ -174,6 +174,16 @@ struct rbgpu_set {
   std::vector<uint64_t> h_begin; // host copy of the CSR, downloaded on demand
   int64_t max_keys = -1;          // most containers in one bitmap (cached on first pairwise use)
   int64_t max_runs = -1;          // most runs in one Run container (cached on first small-batch use)
+  // Derived metadata, built on first use and kept with the set (sets are immutable, like the
+  // reference's immutable bitmaps: a cached index, never a cached result):
+  //   dense_lo / dense_hi  every bitmap holds exactly the high keys [dense_lo, dense_hi) (-1: no; -2: unknown)
+  //   mrec                 one packed 8-B record per container in set order (pack_rec: payload offset,
+  //                        card, min(nruns, 15), type) — one load instead of four metadata arrays
+  //   krec                 dense sets only: the same records key-major, krec[(k - dense_lo) * nb + b]
+  int64_t dense_lo = -2, dense_hi = -2;
+  uint64_t *mrec = nullptr;
+  uint64_t *krec = nullptr;
+  double derive_ms = 0.0;         // device time spent building mrec / krec (reported, not hidden)
   rbg::SetView view() const { return rbg::SetView{begin, key, type, card, nruns, off, payload}; }
 };
 
@@ -184,6 +194,10 @@ void set_release(rbgpu_set *s);
 int ensure_h_begin(const rbgpu_set *s);
 int ensure_max_keys(const rbgpu_set *s);
 int ensure_max_runs(const rbgpu_set *s);
+// derived metadata of an immutable set (see rbgpu_set): computed once, then cached
+int ensure_dense(const rbgpu_set *s);
+int ensure_mrec(const rbgpu_set *s);
+int ensure_krec(const rbgpu_set *s); // needs a dense set (dense_lo >= 0)
 // call accounting: zero the byte counters + record the start event / read everything back
 // zero = false: the caller's counters come zeroed some other way (the small-batch path's H2D copy)
 void stats_begin(rbgpu_ctx *ctx, bool zero = true);

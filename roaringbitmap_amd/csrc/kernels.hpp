@@ -123,22 +123,47 @@ struct WideOut {
 
 // ---- wide_runs.hip: Run-list fast path for naive_or / workShyAnd / naive_xor keys whose containers
 // are all Runs with <= 8 runs; route[q] = 0 where done, 1 where the generic kernel must run
-// naive_xor's key-major member records (wide_xor.hip): workspace `rec` of n entries (one per grouped
-// container); dense = every member holds every key (k_group_dense's layout over mem[0..M), keys
-// [key_lo, key_hi)), else the records are gathered through the container ids
+// The container ids of the grouped keys.  Grouped by the counting sort: cid[i] for position i of key k's
+// segment [seg[k], seg[k+1]).  Dense members (every member holds every key of [dense_lo, dense_hi) —
+// the config-4 shape): no grouping at all, seg[k] = (k - key_lo) * M and the container of member j at
+// key k is mbase[j] + k, with mbase[j] = begin[mem[j]] - dense_lo (mod 2^64).
+struct CidMap {
+  const uint32_t *cid;   // null: dense
+  const uint64_t *mbase; // [M] (dense)
+};
+// one key's view of a CidMap: operator[] takes the grouped position i of a container of that key
+struct KeyCids {
+  const uint32_t *cid;
+  const uint64_t *mbase;
+  uint64_t lo;  // seg[key]
+  uint32_t key;
+  __device__ __forceinline__ KeyCids(const CidMap &m, uint64_t lo_, uint32_t key_)
+      : cid(m.cid), mbase(m.mbase), lo(lo_), key(key_) {}
+  __device__ __forceinline__ uint32_t operator[](uint64_t i) const {
+    return cid ? cid[i] : (uint32_t)(mbase[i - lo] + key);
+  }
+};
+// naive_xor's key-major member records (wide_xor.hip): `rec` holds one packed record (pack_rec) per
+// grouped container, in grouped order.  kCached: `rec` is the set's krec (dense set, members in set
+// order: nothing to build); kTranspose: dense members in another order, transposed per call from the
+// set's mrec through mbase; kGather: grouped by the counting sort, gathered through the ids.
 struct XorRecords {
+  enum Build { kCached = 0, kTranspose = 1, kGather = 2 };
   uint64_t *rec;
   uint64_t n;
-  bool dense;
-  const uint32_t *mem;
+  Build build;
+  const uint64_t *mrec, *mbase;
   uint32_t M, key_lo, key_hi;
 };
+void launch_records_transpose(const uint64_t *mrec, const uint64_t *mbase, uint32_t M, uint32_t key_lo,
+                              uint32_t key_hi, uint64_t *rec, hipStream_t st);
 void launch_wide_runs_xor(const SetView &s, const uint32_t *cid, const uint64_t *seg, const uint32_t *klist,
                           uint32_t nk, uint8_t *out, const WideOut &wo, uint8_t *route, uint64_t *stats,
                           const XorRecords &xr, hipStream_t st);
-bool launch_wide_runs(int sem, const SetView &s, const uint32_t *cid, const uint64_t *seg, const uint32_t *klist,
-                      uint32_t nk, uint8_t *out, const WideOut &wo, uint8_t *route, uint64_t *stats,
-                      const XorRecords &xr, hipStream_t st);
+// mrec: the set's packed records (workShyAnd's one-load metadata)
+bool launch_wide_runs(int sem, const SetView &s, const uint64_t *mrec, const CidMap &cm, const uint64_t *seg,
+                      const uint32_t *klist, uint32_t nk, uint8_t *out, const WideOut &wo, uint8_t *route,
+                      uint64_t *stats, const XorRecords &xr, hipStream_t st);
 
 // ---- setops.hip
 void launch_bitmap_cards(const SetView &s, uint32_t nbitmaps, uint64_t *out, hipStream_t st);
@@ -146,6 +171,8 @@ void launch_gather(const uint8_t *src, const uint64_t *soff, const uint64_t *byt
                    const uint64_t *doff, uint64_t n, hipStream_t st);
 void launch_layout(const uint64_t *bigflag, const uint64_t *bidx, const uint64_t *soff, uint64_t small_base,
                    uint64_t *off, uint64_t n, hipStream_t st);
+void launch_pack_records(const SetView &s, uint64_t n, uint64_t *mrec, hipStream_t st);
+void launch_dense_check(const SetView &s, uint32_t nb, uint32_t lo, uint32_t cnt, uint32_t *bad, hipStream_t st);
 
 // ---- generate.hip
 struct GenSpec {

@@ -1,4 +1,6 @@
 // setops.hip — small per-set utilities: per-bitmap cardinality, payload gather for downloads.
+#include <algorithm>
+
 #include "kernels.hpp"
 #include "wave.hpp"
 
@@ -43,6 +45,29 @@ void launch_layout(const uint64_t *bigflag, const uint64_t *bidx, const uint64_t
                    uint64_t *off, uint64_t n, hipStream_t st) {
   if (!n) return;
   k_layout<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(bigflag, bidx, soff, small_base, off, n);
+}
+
+// ---- derived metadata of an immutable set (rbgpu_set::mrec / krec / dense_lo)
+// mrec[i] = pack_rec(container i): one streaming pass over the four metadata arrays.
+__global__ __launch_bounds__(256) void k_pack_records(SetView s, uint64_t n, uint64_t *__restrict__ mrec) {
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256)
+    mrec[i] = pack_rec(s.type[i], s.card[i], s.nruns[i], s.off[i]);
+}
+void launch_pack_records(const SetView &s, uint64_t n, uint64_t *mrec, hipStream_t st) {
+  if (!n) return;
+  k_pack_records<<<(unsigned)std::min<uint64_t>((n + 255) / 256, 1u << 16), 256, 0, st>>>(s, n, mrec);
+}
+// bad[0] |= 1 when a bitmap does not hold exactly the keys [lo, lo + cnt): its container count is cnt
+// and, its keys being strictly increasing, its first key lo and its last lo + cnt - 1.
+__global__ __launch_bounds__(256) void k_dense_check(SetView s, uint32_t nb, uint32_t lo, uint32_t cnt, uint32_t *bad) {
+  const uint32_t b = blockIdx.x * 256 + threadIdx.x;
+  if (b >= nb) return;
+  const uint64_t b0 = s.begin[b], b1 = s.begin[b + 1];
+  if (b1 - b0 != cnt || s.key[b0] != lo || s.key[b1 - 1] != lo + cnt - 1) atomicOr(bad, 1u);
+}
+void launch_dense_check(const SetView &s, uint32_t nb, uint32_t lo, uint32_t cnt, uint32_t *bad, hipStream_t st) {
+  if (!nb) return;
+  k_dense_check<<<(nb + 255) / 256, 256, 0, st>>>(s, nb, lo, cnt, bad);
 }
 
 } // namespace rbg

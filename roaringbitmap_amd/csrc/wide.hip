@@ -131,16 +131,15 @@ __global__ __launch_bounds__(256) void k_group_base(const uint32_t *Hc, uint64_t
 #ifndef RBG_GROUP_STAGE
 #define RBG_GROUP_STAGE 0
 #endif
-// Dense members (every member holds all 65536 keys: container index = begin + key) need no sort:
-// key k's containers are begin[mem[i]] + k in member order, seg[k] = (k - key_lo) * M.
+// Dense members (every member holds every key of [dense_lo, dense_hi): container = begin + key -
+// dense_lo) need no sort: key k's containers are mbase[j] + k in member order (CidMap), seg[k] =
+// (k - key_lo) * M.  This kernel writes seg and the per-member bases.
 __global__ __launch_bounds__(256) void k_group_dense(const uint64_t *__restrict__ begin, const uint32_t *__restrict__ mem,
-                                                     uint32_t M, uint32_t key_lo, uint32_t key_hi, uint64_t *seg,
-                                                     uint32_t *cid) {
-  const uint64_t krange = key_hi - key_lo, n = krange * M;
-  for (uint64_t t = (uint64_t)blockIdx.x * 256 + threadIdx.x; t < n; t += (uint64_t)gridDim.x * 256) {
-    const uint64_t kr = t / M, i = t - kr * M;
-    cid[t] = (uint32_t)(begin[mem[i]] + key_lo + kr);
-  }
+                                                     uint32_t M, uint32_t dense_lo, uint32_t key_lo, uint32_t key_hi,
+                                                     uint64_t *seg, uint64_t *mbase) {
+  const uint64_t krange = key_hi - key_lo;
+  for (uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x; j < M; j += (uint64_t)gridDim.x * 256)
+    mbase[j] = begin[mem[j]] - dense_lo;
   for (uint64_t k = (uint64_t)blockIdx.x * 256 + threadIdx.x; k <= 65536; k += (uint64_t)gridDim.x * 256)
     seg[k] = (k < key_lo ? 0 : k >= key_hi ? krange : k - key_lo) * M;
 }
@@ -240,7 +239,7 @@ template <int OP>
 #ifndef RBG_FOLD_PREFETCH
 #define RBG_FOLD_PREFETCH 1 // the next pair's metadata loads issued before the current pair is folded
 #endif
-__device__ __forceinline__ uint64_t fold_all(const SetView &s, const uint32_t *cid, uint64_t lo, uint64_t hi,
+__device__ __forceinline__ uint64_t fold_all(const SetView &s, const KeyCids &cid, uint64_t lo, uint64_t hi,
                                              uint64_t (&acc)[kW], uint32_t *lds, int lane) {
   uint64_t bytes = 0;
   uint64_t i = lo;
@@ -294,7 +293,7 @@ __device__ __forceinline__ int type_xor_step(int ta, int tb, uint32_t ca, uint32
 enum { kStA = 0, kStBValid = 1, kStRun = 2, kStBLazy = 3 };
 
 template <int SEM>
-__global__ __launch_bounds__(256) void k_wide_reduce(SetView s, const uint32_t *__restrict__ cid,
+__global__ __launch_bounds__(256) void k_wide_reduce(SetView s, CidMap cm,
                                                      const uint64_t *__restrict__ seg, const uint32_t *__restrict__ klist,
                                                      uint32_t nk, uint8_t *__restrict__ out, WideOut wo,
                                                      const uint8_t *__restrict__ route, uint64_t *stats) {
@@ -307,6 +306,7 @@ __global__ __launch_bounds__(256) void k_wide_reduce(SetView s, const uint32_t *
   uint32_t *lds = lds_all[wv];
   const uint32_t key = klist[q];
   const uint64_t lo = seg[key], hi = seg[key + 1];
+  const KeyCids cid(cm, lo, key);
   const uint64_t m = hi - lo;
   uint8_t *dst = out + (uint64_t)q * kBitmapBytes;
   uint64_t acc[kW];
@@ -539,10 +539,10 @@ int compact_keyed(rbgpu_ctx *ctx, const uint32_t *d_klist, uint32_t nk, const Wi
 }
 
 template <int SEM>
-static void launch_reduce(const SetView &s, const uint32_t *cid, const uint64_t *seg, const uint32_t *klist,
+static void launch_reduce(const SetView &s, const CidMap &cm, const uint64_t *seg, const uint32_t *klist,
                           uint32_t nk, uint8_t *out, const WideOut &wo, uint64_t *stats, hipStream_t st,
                           const uint8_t *route = nullptr) {
-  k_wide_reduce<SEM><<<nblk(nk, 4), 256, 0, st>>>(s, cid, seg, klist, nk, out, wo, route, stats);
+  k_wide_reduce<SEM><<<nblk(nk, 4), 256, 0, st>>>(s, cm, seg, klist, nk, out, wo, route, stats);
 }
 
 // FastAggregation.horizontal_or / horizontal_xor's container order (FastAggregation.java:124-289): a
@@ -629,6 +629,37 @@ int wide_run(rbgpu_ctx *ctx, int sem, const rbgpu_set *in, const std::vector<uin
   const uint64_t N = mstart[M];
   if (in->nc >= (1ull << 32)) return fail(RB_EINVAL, "wide aggregation supports < 2^32 containers per set");
   const bool and_sem = sem == RB_WORKSHY_AND || sem == RB_NAIVE_AND || sem == RB_NAIVE_AND_ITER;
+  const bool horizontal = sem == RB_HORIZONTAL_OR || sem == RB_HORIZONTAL_XOR;
+  // Dense members (every bitmap of the set holds every key of [dense_lo, dense_hi)): no grouping, the
+  // container ids follow from the member bases (CidMap).  The set's derived metadata is built here, on
+  // its first wide use, before the call's accounting starts (rbgpu_set::derive_ms reports its cost).
+  static const bool no_dense = getenv("RBGPU_NO_DENSE_GROUPING") != nullptr;
+  bool dense = M && !horizontal && !no_dense;
+  if (dense) {
+    int rc = ensure_dense(in);
+    if (rc) return rc;
+    dense = in->dense_lo >= 0 && (uint32_t)std::max<int64_t>(key_lo, in->dense_lo) <
+                                     (uint32_t)std::min<int64_t>(key_hi, in->dense_hi);
+  }
+  if (dense) { // keys outside the set's range hold no container: the call's range is the overlap
+    key_lo = (uint32_t)std::max<int64_t>(key_lo, in->dense_lo);
+    key_hi = (uint32_t)std::min<int64_t>(key_hi, in->dense_hi);
+  }
+  const bool identity = [&] {
+    if (M != in->nb) return false;
+    for (uint32_t i = 0; i < M; ++i)
+      if (members[i] != i) return false;
+    return true;
+  }();
+  const bool fast_sem = sem == RB_FAST_OR || sem == RB_WORKSHY_AND || sem == RB_FAST_XOR;
+  bool fast_ok = fast_sem && !getenv("RBGPU_NO_RUN_FASTPATH"); // parity tests run both paths
+  if (fast_ok && (sem == RB_WORKSHY_AND || sem == RB_FAST_XOR)) {
+    // workShyAnd / naive_xor fast paths read packed records; naive_xor's key-major ones for a dense set
+    // in set order are the set's cached krec
+    if (in->payload_bytes >= kRecMaxPayload || ensure_mrec(in)) fast_ok = false;
+    else if (sem == RB_FAST_XOR && dense && identity && ensure_krec(in)) fast_ok = false;
+  }
+  (void)hipGetLastError();
 
   stats_begin(ctx);
   // ---- group by key (stable; keys in [key_lo, key_hi) only): the tiled counting sort above.
@@ -643,33 +674,34 @@ int wide_run(rbgpu_ctx *ctx, int sem, const rbgpu_set *in, const std::vector<uin
   }
   const uint32_t krange = key_hi > key_lo ? key_hi - key_lo : 0;
   const uint32_t nmb = (M + MB - 1) / MB, nkr = (krange + KR - 1) / KR;
+  const bool sorted = !dense && !horizontal; // the counting sort runs
   uint32_t *d_mem = nullptr, *d_cid2 = nullptr, *d_klist = nullptr, *d_Hc = nullptr;
   uint64_t *d_bnd = nullptr, *d_H = nullptr, *d_tot = nullptr, *d_seg = nullptr, *d_active = nullptr,
-           *d_apos = nullptr, *d_tmp = nullptr, *d_rec = nullptr;
+           *d_apos = nullptr, *d_tmp = nullptr, *d_rec = nullptr, *d_mbase = nullptr;
   const uint64_t N1 = std::max<uint64_t>(N, 1);
   const uint64_t tmpw = std::max<uint64_t>(scan_tmp_words(65537), 1);
+  auto alloc_if = [&](bool need, void **p, uint64_t bytes) { return need ? (bool)pool.alloc(p, bytes) : false; };
   if (pool.alloc((void **)&d_mem, std::max<uint32_t>(M, 1) * 4ull) ||
-      pool.alloc((void **)&d_bnd, std::max<uint64_t>((uint64_t)M * (nkr + 1), 1) * 8) ||
-      pool.alloc((void **)&d_Hc, std::max<uint64_t>((uint64_t)nmb * krange, 1) * 4) ||
-      pool.alloc((void **)&d_H, std::max<uint64_t>((uint64_t)nmb * krange, 1) * 8) || pool.alloc((void **)&d_cid2, N1 * 4) ||
+      alloc_if(sorted, (void **)&d_bnd, std::max<uint64_t>((uint64_t)M * (nkr + 1), 1) * 8) ||
+      alloc_if(sorted, (void **)&d_Hc, std::max<uint64_t>((uint64_t)nmb * krange, 1) * 4) ||
+      alloc_if(sorted, (void **)&d_H, std::max<uint64_t>((uint64_t)nmb * krange, 1) * 8) ||
+      alloc_if(!dense, (void **)&d_cid2, N1 * 4) || alloc_if(dense, (void **)&d_mbase, std::max<uint32_t>(M, 1) * 8ull) ||
       pool.alloc((void **)&d_tot, 65537 * 8ull) || pool.alloc((void **)&d_seg, 65537 * 8ull) ||
       pool.alloc((void **)&d_active, 65537 * 8ull) || pool.alloc((void **)&d_apos, 65537 * 8ull) ||
       pool.alloc((void **)&d_klist, 65536 * 4ull) || pool.alloc((void **)&d_tmp, tmpw * 8))
     return fail(RB_ENOMEM, "wide workspace (%llu containers)", (unsigned long long)N);
   auto release = [&]() {
     for (void *p : {(void *)d_mem, (void *)d_bnd, (void *)d_Hc, (void *)d_H, (void *)d_cid2, (void *)d_tot,
-                    (void *)d_seg, (void *)d_active, (void *)d_apos, (void *)d_klist, (void *)d_tmp, (void *)d_rec})
+                    (void *)d_seg, (void *)d_active, (void *)d_apos, (void *)d_klist, (void *)d_tmp, (void *)d_rec,
+                    (void *)d_mbase})
       if (p) pool.release(p);
   };
   if (M) HIPCHK(hipMemcpyAsync(d_mem, members.data(), M * 4ull, hipMemcpyHostToDevice, st));
   const SetView sv = in->view();
   const GroupArgs ga{sv, d_mem, d_bnd, M, MB, KR, nkr, key_lo, key_hi};
-  static const bool no_dense = getenv("RBGPU_NO_DENSE_GROUPING") != nullptr;
-  bool dense = M && nkr && !no_dense;
-  for (uint32_t i = 0; dense && i < M; ++i) dense = in->h_begin[members[i] + 1] - in->h_begin[members[i]] == 65536;
   std::vector<uint32_t> h_cid;
   std::vector<uint64_t> h_seg;
-  if (sem == RB_HORIZONTAL_OR || sem == RB_HORIZONTAL_XOR) {
+  if (horizontal) {
     // the queue order of FastAggregation.horizontal_* over every member key (ties included), then the
     // per-key containers in that order; keys outside the shard are left to k_wide_select
     int rc = horizontal_order(in, members, h_cid, h_seg);
@@ -680,8 +712,8 @@ int wide_run(rbgpu_ctx *ctx, int sem, const rbgpu_set *in, const std::vector<uin
     if (!h_cid.empty()) HIPCHK(hipMemcpyAsync(d_cid2, h_cid.data(), 4 * h_cid.size(), hipMemcpyHostToDevice, st));
     HIPCHK(hipMemcpyAsync(d_seg, h_seg.data(), 8 * 65537ull, hipMemcpyHostToDevice, st));
   } else if (dense) {
-    k_group_dense<<<(unsigned)std::min<uint64_t>(nblk((uint64_t)krange * M, 256), 65536), 256, 0, st>>>(
-        sv.begin, d_mem, M, key_lo, key_hi, d_seg, d_cid2);
+    k_group_dense<<<nblk(std::max<uint64_t>(M, 65537), 256), 256, 0, st>>>(sv.begin, d_mem, M, (uint32_t)in->dense_lo,
+                                                                           key_lo, key_hi, d_seg, d_mbase);
   } else {
     if (M && nkr) {
       k_group_bounds<<<nblk((uint64_t)M * (nkr + 1), 256), 256, 0, st>>>(ga, d_bnd);
@@ -694,6 +726,7 @@ int wide_run(rbgpu_ctx *ctx, int sem, const rbgpu_set *in, const std::vector<uin
       k_group_scatter<<<dim3(nkr, nmb), 256, 0, st>>>(ga, d_H, d_cid2);
     }
   }
+  const CidMap cm{dense ? nullptr : d_cid2, d_mbase};
   k_wide_select<<<nblk(65536, 256), 256, 0, st>>>(d_seg, and_sem ? (uint64_t)M : 0, key_lo, key_hi, d_active);
   scan_exclusive(d_active, d_apos, 65536, d_tmp, st);
   k_wide_list<<<nblk(65536, 256), 256, 0, st>>>(d_active, d_apos, d_klist);
@@ -723,34 +756,37 @@ int wide_run(rbgpu_ctx *ctx, int sem, const rbgpu_set *in, const std::vector<uin
   }
   WideOut wo{w_type, w_card, w_nruns};
   uint8_t *d_route = nullptr;
-  bool fast_ok = !getenv("RBGPU_NO_RUN_FASTPATH"); // parity tests run both paths
   if (pool.alloc((void **)&d_route, nk1)) d_route = nullptr;
+  if (!d_route) fast_ok = false;
+  // naive_xor's fast path reads key-major member records (wide_xor.hip)
+  XorRecords xr{nullptr, N, XorRecords::kGather, in->mrec, d_mbase, M, key_lo, key_hi};
+  if (nk && fast_ok && sem == RB_FAST_XOR) {
+    if (dense && identity) {
+      xr.rec = in->krec + (uint64_t)(key_lo - in->dense_lo) * in->nb;
+      xr.build = XorRecords::kCached;
+    } else {
+      if (pool.alloc((void **)&d_rec, std::max<uint64_t>(N, 1) * 8)) fast_ok = false;
+      xr.rec = d_rec;
+      xr.build = dense ? XorRecords::kTranspose : XorRecords::kGather;
+    }
+  }
   HIPCHK(hipEventRecord(ctx->ev[1], st));
-  // naive_xor's fast path reads key-major member records (wide_xor.hip); byte offsets fit 40 bits
-  XorRecords xr{nullptr, N, dense, d_mem, M, key_lo, key_hi};
   if (nk) {
     // Run-heavy keys first (all Run containers with <= 8 runs): route[q] = 0 when done there
-    const bool fast = sem == RB_FAST_OR || sem == RB_WORKSHY_AND || sem == RB_FAST_XOR;
-    if (fast && !d_route) fast_ok = false;
-    if (fast && fast_ok && sem == RB_FAST_XOR) {
-      if (in->payload_bytes >= (1ull << 40) || pool.alloc((void **)&d_rec, std::max<uint64_t>(N, 1) * 8))
-        fast_ok = false; // the generic kernel takes every key
-      xr.rec = d_rec;
-    }
-    if (fast && fast_ok && !launch_wide_runs(sem, sv, d_cid2, d_seg, d_klist, nk, res->payload, wo, d_route,
-                                             ctx->d_stats, xr, st))
+    if (fast_ok && !launch_wide_runs(sem, sv, in->mrec, cm, d_seg, d_klist, nk, res->payload, wo, d_route,
+                                     ctx->d_stats, xr, st))
       fast_ok = false;
-    const uint8_t *rt = fast && fast_ok ? d_route : nullptr;
+    const uint8_t *rt = fast_ok ? d_route : nullptr;
     switch (sem) {
-    case RB_FAST_OR: launch_reduce<RB_FAST_OR>(sv, d_cid2, d_seg, d_klist, nk, res->payload, wo, ctx->d_stats, st, rt); break;
-    case RB_WORKSHY_AND: launch_reduce<RB_WORKSHY_AND>(sv, d_cid2, d_seg, d_klist, nk, res->payload, wo, ctx->d_stats, st, rt); break;
-    case RB_NAIVE_AND: launch_reduce<RB_NAIVE_AND>(sv, d_cid2, d_seg, d_klist, nk, res->payload, wo, ctx->d_stats, st); break;
-    case RB_NAIVE_AND_ITER: launch_reduce<RB_NAIVE_AND_ITER>(sv, d_cid2, d_seg, d_klist, nk, res->payload, wo, ctx->d_stats, st); break;
-    case RB_FAST_XOR: launch_reduce<RB_FAST_XOR>(sv, d_cid2, d_seg, d_klist, nk, res->payload, wo, ctx->d_stats, st, rt); break;
-    case RB_PAR_OR: launch_reduce<RB_PAR_OR>(sv, d_cid2, d_seg, d_klist, nk, res->payload, wo, ctx->d_stats, st); break;
-    case RB_HORIZONTAL_OR: launch_reduce<RB_HORIZONTAL_OR>(sv, d_cid2, d_seg, d_klist, nk, res->payload, wo, ctx->d_stats, st); break;
-    case RB_HORIZONTAL_XOR: launch_reduce<RB_HORIZONTAL_XOR>(sv, d_cid2, d_seg, d_klist, nk, res->payload, wo, ctx->d_stats, st); break;
-    default: launch_reduce<RB_PAR_XOR>(sv, d_cid2, d_seg, d_klist, nk, res->payload, wo, ctx->d_stats, st); break;
+    case RB_FAST_OR: launch_reduce<RB_FAST_OR>(sv, cm, d_seg, d_klist, nk, res->payload, wo, ctx->d_stats, st, rt); break;
+    case RB_WORKSHY_AND: launch_reduce<RB_WORKSHY_AND>(sv, cm, d_seg, d_klist, nk, res->payload, wo, ctx->d_stats, st, rt); break;
+    case RB_NAIVE_AND: launch_reduce<RB_NAIVE_AND>(sv, cm, d_seg, d_klist, nk, res->payload, wo, ctx->d_stats, st); break;
+    case RB_NAIVE_AND_ITER: launch_reduce<RB_NAIVE_AND_ITER>(sv, cm, d_seg, d_klist, nk, res->payload, wo, ctx->d_stats, st); break;
+    case RB_FAST_XOR: launch_reduce<RB_FAST_XOR>(sv, cm, d_seg, d_klist, nk, res->payload, wo, ctx->d_stats, st, rt); break;
+    case RB_PAR_OR: launch_reduce<RB_PAR_OR>(sv, cm, d_seg, d_klist, nk, res->payload, wo, ctx->d_stats, st); break;
+    case RB_HORIZONTAL_OR: launch_reduce<RB_HORIZONTAL_OR>(sv, cm, d_seg, d_klist, nk, res->payload, wo, ctx->d_stats, st); break;
+    case RB_HORIZONTAL_XOR: launch_reduce<RB_HORIZONTAL_XOR>(sv, cm, d_seg, d_klist, nk, res->payload, wo, ctx->d_stats, st); break;
+    default: launch_reduce<RB_PAR_XOR>(sv, cm, d_seg, d_klist, nk, res->payload, wo, ctx->d_stats, st); break;
     }
   }
   HIPCHK(hipEventRecord(ctx->ev[2], st));
@@ -763,7 +799,7 @@ int wide_run(rbgpu_ctx *ctx, int sem, const rbgpu_set *in, const std::vector<uin
     return rc;
   }
   // the span covers the Run-list fast path (if any) and the generic kernel for the routed keys
-  const bool fp = fast_ok && d_route;
+  const bool fp = fast_ok;
   const char *name = sem == RB_FAST_OR ? "k_wide_reduce<FAST_OR>"
                      : sem == RB_WORKSHY_AND ? (fp ? "k_wide_runs_and+k_wide_reduce<WORKSHY_AND>" : "k_wide_reduce<WORKSHY_AND>")
                      : sem == RB_FAST_XOR ? (fp ? "k_wide_runs_xor+k_wide_reduce<FAST_XOR>" : "k_wide_reduce<FAST_XOR>")

@@ -37,7 +37,7 @@ struct RunBatch {
   uint32_t card, nr, typ;
   uint4 r0, r1;
 };
-__device__ __forceinline__ RunBatch load_batch(const SetView &s, const uint32_t *cid, uint64_t i, uint64_t hi) {
+__device__ __forceinline__ RunBatch load_batch(const SetView &s, const KeyCids &cid, uint64_t i, uint64_t hi) {
   RunBatch b;
   b.card = 0;
   b.nr = 0;
@@ -71,7 +71,7 @@ __device__ __forceinline__ uint32_t run_word(const RunBatch &b, int t) {
 }
 
 template <int SEM>
-__global__ __launch_bounds__(256) void k_wide_runs(SetView s, const uint32_t *__restrict__ cid,
+__global__ __launch_bounds__(256) void k_wide_runs(SetView s, CidMap cm,
                                                    const uint64_t *__restrict__ seg, const uint32_t *__restrict__ klist,
                                                    uint32_t nk, uint8_t *__restrict__ out, WideOut wo,
                                                    uint8_t *__restrict__ route, uint64_t *stats) {
@@ -83,6 +83,7 @@ __global__ __launch_bounds__(256) void k_wide_runs(SetView s, const uint32_t *__
   uint32_t *acc = lds_all[wv];
   const uint32_t key = klist[q];
   const uint64_t lo = seg[key], hi = seg[key + 1];
+  const KeyCids cid(cm, lo, key);
   if (SEM == RB_FAST_OR && hi - lo < 2) { // a lone container: clone + repairAfterLazy -> generic path
     if (lane == 0) route[q] = 1;
     return;
@@ -261,7 +262,7 @@ __device__ __forceinline__ uint32_t iv_s(uint32_t x) { return x & 0xFFFF; }
 __device__ __forceinline__ uint32_t iv_e(uint32_t x) { return x >> 16; }
 
 template <int KB>
-__global__ __launch_bounds__(256) void k_wide_runs_and(SetView s, const uint32_t *__restrict__ cid,
+__global__ __launch_bounds__(256) void k_wide_runs_and(SetView s, const uint64_t *__restrict__ mrec, CidMap cm,
                                                        const uint64_t *__restrict__ seg, const uint32_t *__restrict__ klist,
                                                        uint32_t nk, uint8_t *__restrict__ out, WideOut wo,
                                                        uint8_t *__restrict__ route, uint64_t *stats) {
@@ -275,11 +276,13 @@ __global__ __launch_bounds__(256) void k_wide_runs_and(SetView s, const uint32_t
   const int kk = lane % KB, g = lane / KB;
   const uint32_t q = q0 + kk;
   uint64_t lo = 0, n = 0;
+  uint32_t key = 0;
   if (q < nk) {
-    const uint32_t key = klist[q];
+    key = klist[q];
     lo = seg[key];
     n = seg[key + 1] - lo;
   }
+  const KeyCids cid(cm, lo, key);
   const uint32_t cnt = n > (uint64_t)g ? (uint32_t)((n - g + G - 1) / G) : 0u; // this lane's members
   const uint32_t tmax = __builtin_amdgcn_readfirstlane(wave_max_u32(cnt));
   // the AND identity: one interval [0, 65535]
@@ -287,13 +290,16 @@ __global__ __launch_bounds__(256) void k_wide_runs_and(SetView s, const uint32_t
   L[and_slot(0, 0, lane)] = 0xFFFF0000u;
   bool bad = false;
   uint64_t inb = 0;
+  // metadata: one packed record per container (the set's mrec) instead of type / nruns / off loads;
+  // dense members skip the id load too (the id is the member's base + key)
   auto ld_cid = [&](uint32_t t) -> uint32_t { return t < cnt ? cid[lo + g + (uint64_t)G * t] : 0u; };
   auto ld_meta = [&](uint32_t t, uint32_t c) -> AndMeta {
     AndMeta m{kRun, 0, 0};
     if (t < cnt) {
-      m.typ = s.type[c];
-      m.nr = s.nruns[c];
-      m.off = s.off[c];
+      const uint64_t r = mrec[c];
+      m.typ = rec_type(r);
+      m.nr = rec_nruns(r);
+      m.off = rec_off(r);
     }
     return m;
   };
@@ -439,31 +445,23 @@ __global__ __launch_bounds__(256) void k_wide_runs_and(SetView s, const uint32_t
   }
 }
 
-#ifndef RBG_XOR_BATCHED
-#define RBG_XOR_BATCHED 1 // naive_xor over Run-heavy keys: batch-parallel metrics (wide_xor.hip)
-#endif
-#ifndef RBG_AND_KEYS
-#define RBG_AND_KEYS 16 // keys per wave of the lane-parallel workShyAnd
-#endif
+constexpr int kAndKeys = 16; // keys per wave of the lane-parallel workShyAnd
 
-bool launch_wide_runs(int sem, const SetView &s, const uint32_t *cid, const uint64_t *seg, const uint32_t *klist,
-                      uint32_t nk, uint8_t *out, const WideOut &wo, uint8_t *route, uint64_t *stats,
-                      const XorRecords &xr, hipStream_t st) {
+bool launch_wide_runs(int sem, const SetView &s, const uint64_t *mrec, const CidMap &cm, const uint64_t *seg,
+                      const uint32_t *klist, uint32_t nk, uint8_t *out, const WideOut &wo, uint8_t *route,
+                      uint64_t *stats, const XorRecords &xr, hipStream_t st) {
   const unsigned g = (nk + 3) / 4;
   switch (sem) {
-  case RB_FAST_OR: k_wide_runs<RB_FAST_OR><<<g, 256, 0, st>>>(s, cid, seg, klist, nk, out, wo, route, stats); return true;
+  case RB_FAST_OR: k_wide_runs<RB_FAST_OR><<<g, 256, 0, st>>>(s, cm, seg, klist, nk, out, wo, route, stats); return true;
   case RB_WORKSHY_AND: {
-    const unsigned waves = (nk + RBG_AND_KEYS - 1) / RBG_AND_KEYS;
-    k_wide_runs_and<RBG_AND_KEYS><<<(waves + 3) / 4, 256, 0, st>>>(s, cid, seg, klist, nk, out, wo, route, stats);
+    if (!mrec) return false;
+    const unsigned waves = (nk + kAndKeys - 1) / kAndKeys;
+    k_wide_runs_and<kAndKeys><<<(waves + 3) / 4, 256, 0, st>>>(s, mrec, cm, seg, klist, nk, out, wo, route, stats);
     return true;
   }
-  case RB_FAST_XOR:
-#if RBG_XOR_BATCHED
+  case RB_FAST_XOR: // batch-parallel metrics over key-major records (wide_xor.hip)
     if (!xr.rec) return false;
-    launch_wide_runs_xor(s, cid, seg, klist, nk, out, wo, route, stats, xr, st);
-#else
-    k_wide_runs<RB_FAST_XOR><<<g, 256, 0, st>>>(s, cid, seg, klist, nk, out, wo, route, stats);
-#endif
+    launch_wide_runs_xor(s, cm.cid, seg, klist, nk, out, wo, route, stats, xr, st);
     return true;
   default: return false;
   }

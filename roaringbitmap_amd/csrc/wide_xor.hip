@@ -143,62 +143,53 @@ __device__ __forceinline__ uint32_t compose(uint32_t later, uint32_t earlier) {
   return out;
 }
 
+} // namespace
+
 // Key-major member records.  The SoA metadata is member-major (container m * 65536 + k for dense
 // members), so a wave walking one key's members reads type / card / nruns / off as four lines per
 // member, ~5 L2 requests per container with the payload: the kernel was L2-request-bound (PMC:
 // TCC_BUSY 91 % of the kernel, 1.36G TCC requests per launch, 77 % hits) with its VALU at ~60 %.
-// A pre-pass packs each (key, member) into 8 B in key order — payload byte offset (40 bits), card (17),
-// min(nruns, 15) (4), type (2) — transposing 64 x 64 tiles through LDS so both its reads (along keys)
-// and its writes (along members) are coalesced; the kernel then reads one coalesced record per member.
-__host__ __device__ inline uint64_t pack_rec(uint32_t typ, uint32_t card, uint32_t nr, uint64_t off) {
-  return off | ((uint64_t)card << 40) | ((uint64_t)(nr < 15u ? nr : 15u) << 57) | ((uint64_t)(typ & 3u) << 61);
-}
-__device__ __forceinline__ uint32_t rec_type(uint64_t r) { return (uint32_t)(r >> 61) & 3u; }
-__device__ __forceinline__ uint32_t rec_card(uint64_t r) { return (uint32_t)(r >> 40) & 0x1FFFFu; }
-__device__ __forceinline__ uint32_t rec_nruns(uint64_t r) { return (uint32_t)(r >> 57) & 15u; }
-__device__ __forceinline__ uint64_t rec_off(uint64_t r) { return r & ((1ull << 40) - 1); }
-
-} // namespace
-
-// Dense members (container of key k in member mem[i] = begin[mem[i]] + k; k_group_dense's layout:
-// position (k - key_lo) * M + i): one 64-key x 64-member tile per block.
-__global__ __launch_bounds__(256) void k_xor_records_dense(SetView s, const uint32_t *__restrict__ mem, uint32_t M,
+// So the kernel reads each (key, member) as one packed 8-B record (pack_rec, common.hpp) in key order.
+// For a dense set read in member order the records are the set's cached krec (built once per set,
+// rbgpu_set); any other member list gets them per call: 64-key x 64-member tiles of the set's packed
+// records (mrec) transposed through LDS, so both the reads (along keys) and the writes (along members)
+// are coalesced.
+__global__ __launch_bounds__(256) void k_records_transpose(const uint64_t *__restrict__ mrec,
+                                                           const uint64_t *__restrict__ mbase, uint32_t M,
                                                            uint32_t key_lo, uint32_t key_hi, uint64_t *__restrict__ rec) {
   __shared__ uint64_t tile[64][65]; // [member][key], padded against bank conflicts on the column reads
   const uint32_t k0 = key_lo + blockIdx.x * 64, m0 = blockIdx.y * 64;
   const uint32_t t = threadIdx.x, kx = t & 63, ry = t >> 6;
-  // reads along keys: the 16 rows' container bases first, then all 64 metadata loads in flight at once
   uint64_t rb[16];
 #pragma unroll
-  for (int j = 0; j < 16; ++j) rb[j] = s.begin[mem[min(m0 + ry + 4 * j, M - 1)]];
+  for (int j = 0; j < 16; ++j) rb[j] = mbase[min(m0 + ry + 4 * j, M - 1)];
   const uint32_t k = min(k0 + kx, key_hi - 1);
-  uint32_t ty[16], cd[16], nr[16];
-  uint64_t of[16];
+  uint64_t v[16];
 #pragma unroll
-  for (int j = 0; j < 16; ++j) {
-    const uint64_t c = rb[j] + k;
-    ty[j] = s.type[c];
-    cd[j] = s.card[c];
-    nr[j] = s.nruns[c];
-    of[j] = s.off[c];
-  }
+  for (int j = 0; j < 16; ++j) v[j] = mrec[rb[j] + k]; // all 16 loads in flight at once
 #pragma unroll
-  for (int j = 0; j < 16; ++j) tile[ry + 4 * j][kx] = pack_rec(ty[j], cd[j], nr[j], of[j]);
+  for (int j = 0; j < 16; ++j) tile[ry + 4 * j][kx] = v[j];
   __syncthreads();
   for (uint32_t r = ry; r < 64; r += 4) { // writes along members
     const uint32_t kw = k0 + r, i = m0 + kx;
     if (i < M && kw < key_hi) rec[(uint64_t)(kw - key_lo) * M + i] = tile[kx][r];
   }
 }
-// Any other grouping: a gather through the container ids (the grouped count, seg[65536], can be less
-// than the members' containers when the call is a key-range shard).
-__global__ __launch_bounds__(256) void k_xor_records_gather(SetView s, const uint32_t *__restrict__ cid,
-                                                            const uint64_t *__restrict__ seg, uint64_t *__restrict__ rec) {
+void launch_records_transpose(const uint64_t *mrec, const uint64_t *mbase, uint32_t M, uint32_t key_lo,
+                              uint32_t key_hi, uint64_t *rec, hipStream_t st) {
+  if (!M || key_hi <= key_lo) return;
+  k_records_transpose<<<dim3((key_hi - key_lo + 63) / 64, (M + 63) / 64), 256, 0, st>>>(mrec, mbase, M, key_lo,
+                                                                                      key_hi, rec);
+}
+
+// Members grouped by the counting sort: a gather of the packed records through the container ids (the
+// grouped count, seg[65536], can be less than the members' containers when the call is a key-range shard).
+__global__ __launch_bounds__(256) void k_records_gather(const uint64_t *__restrict__ mrec,
+                                                        const uint32_t *__restrict__ cid,
+                                                        const uint64_t *__restrict__ seg, uint64_t *__restrict__ rec) {
   const uint64_t n = seg[65536];
-  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
-    const uint32_t c = cid[i];
-    rec[i] = pack_rec(s.type[c], s.card[c], s.nruns[c], s.off[c]);
-  }
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256)
+    rec[i] = mrec[cid[i]];
 }
 
 namespace {
@@ -857,12 +848,11 @@ void launch_wide_runs_xor(const SetView &s, const uint32_t *cid, const uint64_t 
   // RBGPU_XOR_NO_FASTFWD=1: exact batches only (an A/B switch for the parity tests)
   const char *e = getenv("RBGPU_XOR_NO_FASTFWD");
   const int fastfwd = !(e && e[0] == '1');
-  if (xr.dense) {
-    const uint32_t krange = xr.key_hi - xr.key_lo;
-    k_xor_records_dense<<<dim3((krange + 63) / 64, (xr.M + 63) / 64), 256, 0, st>>>(s, xr.mem, xr.M, xr.key_lo,
-                                                                                  xr.key_hi, xr.rec);
-  } else if (xr.n) {
-    k_xor_records_gather<<<(unsigned)std::min<uint64_t>((xr.n + 255) / 256, 65536), 256, 0, st>>>(s, cid, seg, xr.rec);
+  if (xr.build == XorRecords::kTranspose) {
+    launch_records_transpose(xr.mrec, xr.mbase, xr.M, xr.key_lo, xr.key_hi, xr.rec, st);
+  } else if (xr.build == XorRecords::kGather && xr.n) {
+    k_records_gather<<<(unsigned)std::min<uint64_t>((xr.n + 255) / 256, 65536), 256, 0, st>>>(xr.mrec, cid, seg,
+                                                                                           xr.rec);
   }
   k_wide_runs_xor<<<(nk + 3) / 4, 256, 0, st>>>(s, xr.rec, seg, klist, nk, out, wo, route, stats, fastfwd);
 }

@@ -504,3 +504,65 @@ def test_range_counts_contract(ctx):
         s.range_counts(members, (7, 3))
     with pytest.raises(rb.InvalidArgument):
         s.range_counts(np.array([12], np.uint32))
+
+
+def _dense_mixed(rng, n, keys):
+    """n bitmaps that all hold exactly the high keys `keys` (a dense set), mixed container kinds."""
+    from datasets import _container_values
+    kinds = ["single", "tiny", "sparse", "a4095", "b4097", "dense", "full", "runs", "fewruns", "contig"]
+    bms = []
+    for i in range(n):
+        parts = [(_container_values(rng, kinds[(i * 7 + k * 3 + int(rng.integers(0, 3))) % len(kinds)]) |
+                  np.uint32(k << 16)) for k in keys]
+        bms.append(np.concatenate(parts).astype(np.uint32))
+    return bms
+
+
+def test_dense_sets_skip_grouping(ctx, oracle):
+    """A set whose bitmaps all hold exactly the keys [dense_lo, dense_hi) takes the ungrouped path
+    (container ids from the member bases, cached packed / key-major records): every semantics, member
+    orders (set order -> cached krec, permuted / subset / duplicates -> per-call transpose), key-range
+    shards that clip the dense range, and the same bytes with the grouping forced
+    (RBGPU_NO_DENSE_GROUPING=1).  Keys of mixed container types go to the generic kernel with dense ids."""
+    import os
+
+    import roaringbitmap_amd as rb
+    from roaringbitmap_amd.sharding import serialize_parts
+    rng = np.random.default_rng(41)
+    bms = _dense_mixed(rng, 13, range(5, 13))
+    for ro in (False, True):
+        s = ctx.upload_values(bms, run_optimize=ro)
+        refs = [oracle.RefBitmap.deserialize(b) for b in s.serialize()]
+        orders = [np.arange(13, dtype=np.uint32), np.arange(12, -1, -1, dtype=np.uint32),
+                  np.array([3, 1, 4, 1, 5, 9, 2, 6, 5, 3, 5, 8], np.uint32), np.array([7, 2], np.uint32)]
+        for members in orders:
+            for sem in SEMS:
+                _check(ctx, oracle, s, refs, sem, members)
+        members = orders[0]
+        for sem in SHARDABLE:
+            if sem == "NAIVE_AND":
+                continue  # a shard picks its own smallest member (NAIVE_AND_ITER is the sharded form)
+            want = ctx.wide(getattr(rb, sem), s, members).serialize()[0]
+            for ranges in ([(0, 7), (7, 10), (10, 65536)], [(0, 5), (5, 13), (13, 65536)], [(0, 12), (12, 65536)]):
+                shards = [ctx.wide(getattr(rb, sem), s, members, key_range=r) for r in ranges]
+                assert serialize_parts([sh.download() for sh in shards]) == want, (sem, ranges)
+            os.environ["RBGPU_NO_DENSE_GROUPING"] = "1"
+            try:
+                assert ctx.wide(getattr(rb, sem), s, members).serialize()[0] == want, sem
+            finally:
+                del os.environ["RBGPU_NO_DENSE_GROUPING"]
+
+
+def test_dense_run_shard_records(ctx, oracle):
+    """Config-4 shape generated as a key-range shard (dense_lo > 0): workShyAnd through the packed
+    records, naive_xor through the set's cached key-major records (set order) and through per-call
+    transposed records (reversed order), naive_or through dense ids — all equal to the oracle."""
+    import roaringbitmap_amd as rb
+    a = ctx.generate_keys(rb.WL_WIDE_RUNS, 40, 300, 700, seed=5)
+    refs = [oracle.RefBitmap.deserialize(b) for b in a.serialize()]
+    for members in (np.arange(40, dtype=np.uint32), np.arange(39, -1, -1, dtype=np.uint32)):
+        for sem in ("FAST_OR", "FAST_AND", "WORKSHY_AND", "FAST_XOR", "PAR_XOR"):
+            _check(ctx, oracle, a, refs, sem, members)
+        # the cached records are reused call after call
+        for _ in range(2):
+            _check(ctx, oracle, a, refs, "FAST_XOR", members)
