@@ -150,7 +150,11 @@ def baseline_entry(bytes_per_pass, rates: dict, kind, sample, extra=None):
     """`value` = the best thread count's rate (the CPU at its best on this workload), with every
     measured count beside it."""
     best = max(rates, key=lambda t: rates[t])
-    out = {"value": round(bytes_per_pass * rates[best] / 1e9, 3), "unit": "GB/s", "cores": best, "kind": kind,
+    # cores = the CPUs those threads actually had: above the cgroup quota, threads only time-share it
+    quota = HOST["cgroup_cpu_quota"]
+    cores = min(best, max(1, int(quota))) if quota else min(best, ALL_CORES)
+    out = {"value": round(bytes_per_pass * rates[best] / 1e9, 3), "unit": "GB/s", "cores": cores, "threads": best,
+           "kind": kind,
            "value_1thread": round(bytes_per_pass * rates[1] / 1e9, 3),
            "by_threads": {str(t): round(bytes_per_pass * r / 1e9, 3) for t, r in rates.items()},
            "host": HOST, "sample": sample}

@@ -834,9 +834,6 @@ static uint32_t pairwise_seg_keys(const rbgpu_set *a, const rbgpu_set *b, uint64
   while (seg > 8 && est / seg < 131072.0) seg >>= 1;
   return seg;
 }
-#ifndef RBG_SMALL_EVENTS
-#define RBG_SMALL_EVENTS 0 // 1: always time the small-batch kernels with events
-#endif
 // Small batches (kernels.hpp: <= kSmallPairs pairs of <= kSmallPairKeys keys, <= kSmallSlots merged
 // keys, no Run container over 8 KiB to copy): two launches and one host read-back.  Returns 1 when
 // the batch does not qualify (the general pipeline runs), else an rbgpu status.
@@ -938,7 +935,7 @@ static int pairwise_small(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgp
   // per-kernel events only when asked for (RBGPU_SMALL_KERNEL_TIMES=1, the bench's breakdown): the call
   // is a few tens of microseconds and each timed marker sits between its launches
   const char *kt = getenv("RBGPU_SMALL_KERNEL_TIMES");
-  const bool ktimes = RBG_SMALL_EVENTS || (kt && kt[0] == '1');
+  const bool ktimes = kt && kt[0] == '1';
   stats_begin(ctx, false);
   if (ktimes) HIPCHK(hipEventRecord(ctx->ev[1], st));
   sa.E = (uint32_t)E;

@@ -328,30 +328,42 @@ static int gather_u64(rbgpu_comm *c, const uint64_t *mine, int k, std::vector<ui
   return RB_OK;
 }
 
-int rbgpu_shard_summarize(rbgpu_comm *c, const rbgpu_set *local, rb_shard_summary *out) {
-  if (!c || !local || !out) return fail(RB_EINVAL, "null argument");
-  if (local->nb != 1) return fail(RB_EINVAL, "a shard is a one-bitmap set");
-  if (local->ctx != c->ctx) return fail(RB_EINVAL, "the shard belongs to another context");
+// Every rank takes part in each collective even when its own step failed (a rank that returned
+// early would leave the others waiting in the collective): a failure travels as a flag inside the
+// exchange, and every rank then fails together.  Returns the local code, or RB_EDEVICE naming the
+// failure on another rank.
+static int agree(int local_rc, uint64_t failed_ranks) {
+  if (local_rc) return local_rc;
+  if (failed_ranks) return fail(RB_EDEVICE, "%llu other rank(s) failed this collective call", (unsigned long long)failed_ranks);
+  return RB_OK;
+}
+
+// summary exchange; local_rc != 0: this rank's shard could not be built (local may be null), it
+// still takes part in the all-gather and every rank fails together
+static int summarize(rbgpu_comm *c, const rbgpu_set *local, int local_rc, rb_shard_summary *out) {
   rb_bitmap_summary s{};
-  int rc = rbgpu_set_summaries(local, 0, 1, &s);
-  if (rc) return rc;
   uint64_t ser = 0;
-  rc = rbgpu_set_serialized_sizes(local, &ser);
-  if (rc) return rc;
-  const uint64_t mine[5] = {s.cardinality, s.n_containers, s.n_run_containers, s.payload_bytes, ser};
+  if (!local_rc) local_rc = rbgpu_set_summaries(local, 0, 1, &s);
+  if (!local_rc) local_rc = rbgpu_set_serialized_sizes(local, &ser);
+  const uint64_t mine[6] = {s.cardinality, s.n_containers, s.n_run_containers, s.payload_bytes, ser,
+                            local_rc ? 1ull : 0ull};
   std::vector<uint64_t> g;
-  rc = gather_u64(c, mine, 5, g);
+  int rc = gather_u64(c, mine, 6, g);
+  if (rc) return rc;
+  uint64_t failed = 0;
+  for (int r = 0; r < c->nranks; ++r) failed += g[6 * r + 5];
+  rc = agree(local_rc, failed);
   if (rc) return rc;
   rb_shard_summary o{};
   uint64_t before_payload = 0, before_cont = 0;
   for (int r = 0; r < c->nranks; ++r) {
-    o.cardinality += g[5 * r];
-    o.n_containers += g[5 * r + 1];
-    o.n_run_containers += g[5 * r + 2];
-    o.payload_bytes += g[5 * r + 3];
+    o.cardinality += g[6 * r];
+    o.n_containers += g[6 * r + 1];
+    o.n_run_containers += g[6 * r + 2];
+    o.payload_bytes += g[6 * r + 3];
     if (r < c->rank) {
-      before_cont += g[5 * r + 1];
-      before_payload += g[5 * r + 3];
+      before_cont += g[6 * r + 1];
+      before_payload += g[6 * r + 3];
     }
   }
   const uint64_t h = header_bytes(o.n_containers, o.n_run_containers > 0);
@@ -363,11 +375,49 @@ int rbgpu_shard_summarize(rbgpu_comm *c, const rbgpu_set *local, rb_shard_summar
   return RB_OK;
 }
 
+int rbgpu_shard_summarize(rbgpu_comm *c, const rbgpu_set *local, rb_shard_summary *out) {
+  if (!c || !out) return fail(RB_EINVAL, "null argument");
+  int local_rc = RB_OK;
+  if (!local) local_rc = fail(RB_EINVAL, "null argument");
+  else if (local->nb != 1) local_rc = fail(RB_EINVAL, "a shard is a one-bitmap set");
+  else if (local->ctx != c->ctx) local_rc = fail(RB_EINVAL, "the shard belongs to another context");
+  return summarize(c, local, local_rc, out);
+}
+
+// all-reduce of n member counts plus a failure flag: every rank takes part whatever its own step did
+static int reduce_counts(rbgpu_comm *c, std::vector<uint64_t> &cnt, int local_rc) {
+  const uint32_t n = (uint32_t)cnt.size();
+  cnt.push_back(local_rc ? 1 : 0);
+  uint64_t *d = nullptr;
+  rbgpu_ctx *ctx = c->ctx;
+  if (ctx->pool.alloc((void **)&d, 8ull * (n + 1))) return fail(RB_ENOMEM, "member counts");
+  hipStream_t st = ctx->stream;
+  int rc = RB_OK;
+  ncclResult_t e = ncclSuccess;
+  if (hipSetDevice(ctx->device) || hipMemcpyAsync(d, cnt.data(), 8ull * (n + 1), hipMemcpyHostToDevice, st))
+    rc = fail(RB_EDEVICE, "member counts upload");
+  if (!rc && (e = c->r->all_reduce(d, d, n + 1, ncclUint64, ncclSum, c->nc, st)) != ncclSuccess)
+    rc = fail(RB_EDEVICE, "member counts all-reduce: %s", c->r->error_string(e));
+  if (!rc && (hipMemcpyAsync(cnt.data(), d, 8ull * (n + 1), hipMemcpyDeviceToHost, st) || hipStreamSynchronize(st)))
+    rc = fail(RB_EDEVICE, "member counts read-back");
+  (void)hipStreamSynchronize(st);
+  ctx->pool.release(d);
+  if (rc) return rc;
+  const uint64_t failed = cnt[n] - (local_rc ? 1 : 0);
+  cnt.pop_back();
+  return agree(local_rc, failed);
+}
+
 int rbgpu_wide_sharded(rbgpu_comm *c, int sem, const rbgpu_set *in, const uint32_t *members, uint32_t n,
                        uint32_t key_lo, uint32_t key_hi, rbgpu_set **local, rb_shard_summary *summary) {
   if (!c || !local || !summary) return fail(RB_EINVAL, "null argument");
-  if (!in) return fail(RB_EINVAL, "null input set");
-  int rc;
+  *local = nullptr;
+  // priorityqueue_or / _xor merge in the order of intermediate result sizes, which are global: a
+  // key-range shard cannot follow it.  Refused on every rank alike (the arguments agree) before any
+  // collective.
+  if (c->nranks > 1 && (sem == RB_PQ_OR || sem == RB_PQ_XOR))
+    return fail(RB_EINVAL, "priorityqueue_or / priorityqueue_xor cannot be key-range sharded");
+  int rc = in ? RB_OK : fail(RB_EINVAL, "null input set");
   std::vector<uint32_t> ord;
   if (sem == RB_NAIVE_AND || (sem == RB_FAST_AND && n <= 10)) {
     // naive_and(varargs) starts from the bitmap with the fewest containers (first on ties) and skips
@@ -375,18 +425,12 @@ int rbgpu_wide_sharded(rbgpu_comm *c, int sem, const rbgpu_set *in, const uint32
     // ranks' key-range counts summed; then every shard folds the same order (naive_and(Iterator))
     std::vector<uint32_t> mem(n);
     for (uint32_t i = 0; i < n; ++i) mem[i] = members ? members[i] : i;
-    std::vector<uint64_t> cnt(n);
-    rc = rbgpu_set_range_counts(in, mem.data(), n, key_lo, key_hi, cnt.data());
+    std::vector<uint64_t> cnt(n, 0);
+    if (!rc) rc = rbgpu_set_range_counts(in, mem.data(), n, key_lo, key_hi, cnt.data());
+    if (rc) std::fill(cnt.begin(), cnt.end(), 0ull);
+    rc = reduce_counts(c, cnt, rc);
     if (rc) return rc;
     if (n) {
-      uint64_t *d = nullptr;
-      if (c->ctx->pool.alloc((void **)&d, 8ull * n)) return fail(RB_ENOMEM, "member counts");
-      hipStream_t st = c->ctx->stream;
-      HIPCHK(hipMemcpyAsync(d, cnt.data(), 8ull * n, hipMemcpyHostToDevice, st));
-      NCCLCHK(c->r, c->r->all_reduce(d, d, n, ncclUint64, ncclSum, c->nc, st));
-      HIPCHK(hipMemcpyAsync(cnt.data(), d, 8ull * n, hipMemcpyDeviceToHost, st));
-      HIPCHK(hipStreamSynchronize(st));
-      c->ctx->pool.release(d);
       uint32_t sm = 0;
       for (uint32_t i = 1; i < n; ++i)
         if (cnt[i] < cnt[sm]) sm = i;
@@ -395,11 +439,11 @@ int rbgpu_wide_sharded(rbgpu_comm *c, int sem, const rbgpu_set *in, const uint32
         if (m != mem[sm]) ord.push_back(m);
     }
     rc = rbgpu_wide_keys(c->ctx, RB_NAIVE_AND_ITER, in, ord.data(), (uint32_t)ord.size(), key_lo, key_hi, local);
-  } else {
+  } else if (!rc) {
     rc = rbgpu_wide_keys(c->ctx, sem, in, members, n, key_lo, key_hi, local);
   }
-  if (rc) return rc;
-  rc = rbgpu_shard_summarize(c, *local, summary);
+  if (rc) *local = nullptr;
+  rc = summarize(c, *local, rc, summary);
   if (rc) {
     rbgpu_set_free(*local);
     *local = nullptr;
@@ -411,10 +455,11 @@ int rbgpu_bsi_compare_sharded(rbgpu_comm *c, const rbgpu_set *bsi, int op, uint6
                               uint64_t min_value, uint64_t max_value, const rbgpu_set *found, uint32_t key_lo,
                               uint32_t key_hi, rbgpu_set **local, rb_shard_summary *summary) {
   if (!c || !local || !summary) return fail(RB_EINVAL, "null argument");
+  *local = nullptr;
   int rc = rbgpu_bsi_compare_keys(c->ctx, bsi, op, start_or_value, end, min_value, max_value, found, key_lo, key_hi,
                                   local);
-  if (rc) return rc;
-  rc = rbgpu_shard_summarize(c, *local, summary);
+  if (rc) *local = nullptr;
+  rc = summarize(c, *local, rc, summary); // every rank joins the exchange, failed or not
   if (rc) {
     rbgpu_set_free(*local);
     *local = nullptr;
@@ -424,35 +469,59 @@ int rbgpu_bsi_compare_sharded(rbgpu_comm *c, const rbgpu_set *bsi, int op, uint6
 
 int rbgpu_shard_gather_serialized(rbgpu_comm *c, const rbgpu_set *local, const rb_shard_summary *summary, int root,
                                   uint8_t *d_dst, uint64_t cap) {
-  if (!c || !local || !summary) return fail(RB_EINVAL, "null argument");
-  if (root < 0 || root >= c->nranks) return fail(RB_EINVAL, "bad root %d", root);
+  if (!c || !summary) return fail(RB_EINVAL, "null argument");
+  if (root < 0 || root >= c->nranks) return fail(RB_EINVAL, "bad root %d", root); // the same on every rank
   const bool is_root = c->rank == root;
-  if (is_root && (!d_dst || cap < summary->serialized_size))
-    return fail(RB_EINVAL, "destination holds %llu bytes, %llu needed", (unsigned long long)cap,
-                (unsigned long long)summary->serialized_size);
+  // a bad argument on one rank is exchanged with the lengths, so every rank fails together instead of
+  // the others waiting in the send / recv
+  int local_rc = RB_OK;
+  if (!local) local_rc = fail(RB_EINVAL, "null shard");
+  else if (is_root && (!d_dst || cap < summary->serialized_size))
+    local_rc = fail(RB_EINVAL, "destination holds %llu bytes, %llu needed", (unsigned long long)cap,
+                    (unsigned long long)summary->serialized_size);
   rbgpu_ctx *ctx = c->ctx;
   hipStream_t st = ctx->stream;
-  HIPCHK(hipSetDevice(ctx->device));
   // every rank's shard size (the summary's own field, gathered again: callers may pass a summary
-  // from another exchange of the same shards)
-  const uint64_t mine = summary->local_serialized;
-  std::vector<uint64_t> lens;
-  int rc = gather_u64(c, &mine, 1, lens);
+  // from another exchange of the same shards) and failure flag
+  const uint64_t mine[2] = {summary->local_serialized, local_rc ? 1ull : 0ull};
+  std::vector<uint64_t> g;
+  int rc = gather_u64(c, mine, 2, g);
   if (rc) return rc;
-  std::vector<uint64_t> base(c->nranks + 1, 0);
-  for (int r = 0; r < c->nranks; ++r) base[r + 1] = base[r] + lens[r];
+  uint64_t failed = 0;
+  std::vector<uint64_t> lens(c->nranks), base(c->nranks + 1, 0);
+  for (int r = 0; r < c->nranks; ++r) {
+    lens[r] = g[2 * r];
+    failed += g[2 * r + 1];
+    base[r + 1] = base[r] + lens[r];
+  }
+  rc = agree(local_rc, failed - (local_rc ? 1 : 0));
+  if (rc) return rc;
   // this rank's shard, serialized on its GPU
   uint8_t *d_stage = nullptr;
+  Part *d_parts = nullptr;
   const uint64_t stage = is_root ? base[c->nranks] : lens[c->rank];
-  if (ctx->pool.alloc((void **)&d_stage, std::max<uint64_t>(stage, 16))) return fail(RB_ENOMEM, "gather staging");
-  auto done = [&](int code) {
+  if (ctx->pool.alloc((void **)&d_stage, std::max<uint64_t>(stage, 16))) {
+    d_stage = nullptr;
+    local_rc = fail(RB_ENOMEM, "gather staging");
+  }
+  auto done = [&](int code) { // every pooled buffer goes back on every path
     (void)hipStreamSynchronize(st);
-    ctx->pool.release(d_stage);
+    if (d_stage) ctx->pool.release(d_stage);
+    if (d_parts) ctx->pool.release(d_parts);
     return code;
   };
-  uint8_t *mine_at = d_stage + (is_root ? base[c->rank] : 0);
-  uint64_t offs[2] = {0, 0};
-  rc = rbgpu_set_serialize_device(local, 0, 1, mine_at, lens[c->rank], offs);
+  uint8_t *mine_at = d_stage ? d_stage + (is_root ? base[c->rank] : 0) : nullptr;
+  if (!local_rc) {
+    uint64_t offs[2] = {0, 0};
+    local_rc = rbgpu_set_serialize_device(local, 0, 1, mine_at, lens[c->rank], offs);
+  }
+  // agree once more before the point-to-point phase
+  const uint64_t flag = local_rc ? 1 : 0;
+  rc = gather_u64(c, &flag, 1, g);
+  if (rc) return done(rc);
+  failed = 0;
+  for (int r = 0; r < c->nranks; ++r) failed += g[r];
+  rc = agree(local_rc, failed - flag);
   if (rc) return done(rc);
   // one grouped send / recv: the shards travel to the root
   ncclResult_t e = c->r->group_start();
@@ -485,24 +554,28 @@ int rbgpu_shard_gather_serialized(rbgpu_comm *c, const rbgpu_set *local, const r
     p.bytes = d_stage + base[r]; // the kernel reads the device copy
     parts[r] = p;
   }
-  Global g;
-  rc = plan_parts(parts, g);
+  Global gl;
+  rc = plan_parts(parts, gl);
   if (rc) return done(rc);
-  uint64_t total = g.h;
+  uint64_t total = gl.h;
   for (const Part &p : parts) total += p.body;
   if (cap < total)
     return done(fail(RB_EINVAL, "destination holds %llu bytes, %llu needed", (unsigned long long)cap,
                      (unsigned long long)total));
-  Part *d_parts = nullptr;
-  if (ctx->pool.alloc((void **)&d_parts, sizeof(Part) * parts.size())) return done(fail(RB_ENOMEM, "gather plan"));
-  HIPCHK(hipMemcpyAsync(d_parts, parts.data(), sizeof(Part) * parts.size(), hipMemcpyHostToDevice, st));
-  const uint64_t items = assemble_items(g);
-  k_shard_header<<<(unsigned)((items + 255) / 256), 256, 0, st>>>(d_parts, (uint32_t)parts.size(), g, d_dst);
+  if (ctx->pool.alloc((void **)&d_parts, sizeof(Part) * parts.size())) {
+    d_parts = nullptr;
+    return done(fail(RB_ENOMEM, "gather plan"));
+  }
+  if (hipMemcpyAsync(d_parts, parts.data(), sizeof(Part) * parts.size(), hipMemcpyHostToDevice, st))
+    return done(fail(RB_EDEVICE, "gather plan upload"));
+  const uint64_t items = assemble_items(gl);
+  k_shard_header<<<(unsigned)((items + 255) / 256), 256, 0, st>>>(d_parts, (uint32_t)parts.size(), gl, d_dst);
   for (const Part &p : parts)
-    if (p.body) HIPCHK(hipMemcpyAsync(d_dst + g.h + p.bbase, p.bytes + p.lh, p.body, hipMemcpyDeviceToDevice, st));
-  HIPCHK(hipStreamSynchronize(st));
-  LAUNCHCHK();
-  ctx->pool.release(d_parts);
+    if (p.body && hipMemcpyAsync(d_dst + gl.h + p.bbase, p.bytes + p.lh, p.body, hipMemcpyDeviceToDevice, st))
+      return done(fail(RB_EDEVICE, "shard body copy"));
+  if (hipStreamSynchronize(st)) return done(fail(RB_EDEVICE, "shard gather"));
+  const hipError_t le = hipGetLastError();
+  if (le != hipSuccess) return done(fail(RB_EDEVICE, "kernel launch failed: %s", hipGetErrorString(le)));
   return done(RB_OK);
 }
 

@@ -355,48 +355,10 @@ __device__ __forceinline__ RecU load_rec(const TaskRec *r) {
 //           the left; ArrayContainer.and/andNot :184-271, BitmapContainer.and(Array) :162-172,
 //           RunContainer.and(Array) :305-336): P = F, Q = the other operand X, staged in LDS;
 //   kHeavy  everything else: P = A, Q = B as 65536-bit register bitmaps.
-#ifndef RBG_HEAVY_PERSISTENT
-#define RBG_HEAVY_PERSISTENT 1 // 0: the one-launch-sized-grid register path (k_pair_heavy_np)
-#endif
-#ifndef RBG_FILTER_TRANSPOSE
-#define RBG_FILTER_TRANSPOSE 1 // probe a row in value order (adjacent lanes, adjacent values)
-#endif
-#ifndef RBG_RUN_REG_PREFIX
-#define RBG_RUN_REG_PREFIX 1 // register path: a Run operand's toggle image read once, prefix-xor in registers
-#endif
-#ifndef RBG_LIGHT_RUN_REG
-#define RBG_LIGHT_RUN_REG 0 // 1: light filter computes a Run X's prefix-xor in registers (spills at 128 VGPRs: task phase 4.09-4.16 vs 3.95-4.04 ms)
-#endif
-#ifndef RBG_REC_AHEAD
-#define RBG_REC_AHEAD 0 // 1: task records loaded one task further ahead (measured neutral to slower: 4.06-4.17 vs 3.98-4.06 ms)
-#endif
-#ifndef RBG_EARLY_NEXT_P
-#define RBG_EARLY_NEXT_P 0 // 1: filter tasks load the next P once F's last row is in the transpose buffer (measured slower: task phase 4.17 vs 4.01 ms)
-#endif
-#ifndef RBG_LIGHT_TIMING
-#define RBG_LIGHT_TIMING 0 // study builds: per-phase s_memtime totals of a few light waves (printf)
-#endif
-#ifndef RBG_LIGHT_ABLATE
-#define RBG_LIGHT_ABLATE 0 // timing study only (wrong results): skip staging X = 1 Bitmap, 2 Array, 4 Run; 8 skip the filter
-#endif
-#ifndef RBG_FILTER_LINEAR
-#define RBG_FILTER_LINEAR 1 // the transposed filter with a linear stage (filter_rows_linear; 0: the ring)
-#endif
-#ifndef RBG_FILTER_WORDS
-#define RBG_FILTER_WORDS 0 // 1: light filter with F loaded in word order, no LDS transpose (correct; slower: light 4.05-4.17 vs 3.94-3.97 ms, stride-2 probes double the bank conflicts)
-#endif
-#ifndef RBG_HEAVY_COMBINE
-#define RBG_HEAVY_COMBINE 0 // 1: register path OR / XOR stages A|A, A^A, R^R as one LDS image (one zero + one read; correct, measured neutral)
-#endif
-#ifndef RBG_LOAD_USED_ROWS
-#define RBG_LOAD_USED_ROWS 0 // payload rows past a task's bytes not loaded (load_chunks_used): 0 never, 1 both task kernels (light much slower), 2 the register path only (neutral)
-#endif
-#define RBG_LOAD load_rows<ROLE>
-#ifndef RBG_LIGHT_WAVES
-#define RBG_LIGHT_WAVES 4 // waves per SIMD of the copy + filter kernel (128 VGPRs)
-#endif
-#ifndef RBG_HEAVY_WAVES
-#define RBG_HEAVY_WAVES 2 // waves per SIMD the register-path kernel is allocated for (prefetch + bitmap)
+constexpr int kLightWaves = 4; // waves per SIMD of the copy + filter kernel (128 VGPRs)
+constexpr int kHeavyWaves = 2; // waves per SIMD the register-path kernel is allocated for (prefetch + bitmap)
+#ifndef RBG_STUDY
+#define RBG_STUDY 0 // study builds: per-phase s_memtime totals of a few light / heavy waves (printf)
 #endif
 enum { kCopy = 0, kFilter = 1, kHeavy = 2 };
 struct Task {
@@ -589,18 +551,10 @@ __device__ __forceinline__ bool and_runs_intervals(const uint4 (&pq)[8], const u
   wave_lds_sync();
   return true;
 }
-#ifndef RBG_RUN_INTERVALS
-#define RBG_RUN_INTERVALS 1 // Run AND Run by interval intersection (0: always the register bitmap)
-#endif
-
-#ifndef RBG_QUEUE_CHUNK
-#define RBG_QUEUE_CHUNK 8 // light tasks per claim (one counter: 4 -> 6.0 ms steps from atomic contention, 8 -> 4.64, 16 -> 4.59-4.62, 32 -> 4.71-4.78; 8 counters: 8 -> 4.49-4.52)
-#endif
-constexpr uint64_t kQueueChunk = RBG_QUEUE_CHUNK;
-#ifndef RBG_QUEUE_STRIPES
-#define RBG_QUEUE_STRIPES 8 // task sub-ranges with a counter each (a wave moves on when its is empty)
-#endif
-constexpr uint32_t kQueueStripes = RBG_QUEUE_STRIPES;
+// tasks per claim (one counter: 4 -> 6.0 ms steps from atomic contention, 8 -> 4.64, 16 -> 4.59-4.62,
+// 32 -> 4.71-4.78; 8 counters: 8 -> 4.49-4.52)
+constexpr uint64_t kQueueChunk = 8;
+constexpr uint32_t kQueueStripes = 8; // task sub-ranges with a counter each (a wave moves on when its is empty)
 constexpr uint32_t kQueueStride = 16; // counters 128 B apart
 // the API reserves 32 counters (4 KiB): 16 for the light tasks' queue, 16 for the heavy tasks'
 static_assert(kQueueStripes >= 1 && kQueueStripes <= 16, "two queues of at most 16 counters");
@@ -627,33 +581,6 @@ __device__ __forceinline__ Chunk claim_chunk(unsigned long long *queue, uint64_t
   return Chunk{n, n};
 }
 
-// claim_chunk split in two so the atomic's return is waited for an iteration later, after the next
-// task's payload loads: waited for right after issue (claim_chunk), its vmcnt(0) also drains those
-// prefetches.  Issued only while a sub-range is left to try (the same condition as claim_chunk's).
-#ifndef RBG_CLAIM_EARLY
-#define RBG_CLAIM_EARLY 0 // 1: measured neutral with the atomic optimizer (it still consumes the result at once), slower without it (-mllvm -amdgpu-atomic-optimizer-strategy=None: heavy 3.32 vs 3.13 ms, ANDNOT 9.3 vs 8.1 ms)
-#endif
-__device__ __forceinline__ unsigned long long claim_issue(unsigned long long *queue, uint32_t k, uint32_t tried, int lane) {
-  unsigned long long v = 0;
-  if (tried < kQueueStripes && lane == 0)
-    v = __hip_atomic_fetch_add(queue + k * kQueueStride, (unsigned long long)kQueueChunk, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-  return v;
-}
-__device__ __forceinline__ Chunk claim_finish(unsigned long long v, unsigned long long *queue, uint64_t n, uint32_t &k,
-                                              uint32_t &tried, int lane) {
-  if (tried < kQueueStripes) {
-    const uint64_t lo = n * k / kQueueStripes, hi = n * (k + 1) / kQueueStripes;
-    uint32_t vl = (uint32_t)v, vh = (uint32_t)(v >> 32);
-    asm volatile("" : "+v"(vl), "+v"(vh)); // pins the wait here: the readfirstlanes cannot move up to the atomic
-    const uint64_t st = lo + pack2(__builtin_amdgcn_readfirstlane(vl), __builtin_amdgcn_readfirstlane(vh));
-    if (st < hi) return Chunk{st, min(st + kQueueChunk, hi)};
-    k = (k + 1) % kQueueStripes;
-    ++tried;
-  }
-  return claim_chunk(queue, n, k, tried, lane); // the following sub-ranges, synchronously
-}
-
 // The task kernel, ONE WAVE PER TASK, persistent waves striding over one record list with a
 // one-task software pipeline: the next task's record and both payloads are in flight while the
 // current one computes.  Loads sit at fixed points of the loop body (a task with fewer payloads
@@ -663,21 +590,13 @@ __device__ __forceinline__ Chunk claim_finish(unsigned long long v, unsigned lon
 //   ROLE kRoleHeavy (register path): build the 65536-bit result in registers from P and Q, load
 //                   both next payloads, then classify and emit.
 enum { kRoleLight = 0, kRoleHeavy = 1 };
-// Guarded loads keep fully out-of-range rows off the texture data path; in the light kernel they
-// cost more than they save (A/B: light 4.73-4.82 vs 3.96-3.97 ms with them).
-template <int ROLE> __device__ __forceinline__ void load_rows(uint4 (&q)[8], const uint8_t *p, uint32_t bytes, int lane) {
-  if (RBG_LOAD_USED_ROWS == 1 || (RBG_LOAD_USED_ROWS == 2 && ROLE == kRoleHeavy)) load_chunks_used(q, p, bytes, lane);
-  else load_chunks(q, p, bytes, lane);
-}
 template <int OP, bool CARD_ONLY, int ROLE>
-__global__ __launch_bounds__(256, ROLE == kRoleHeavy ? RBG_HEAVY_WAVES : RBG_LIGHT_WAVES) void k_pair_tasks(
+__global__ __launch_bounds__(256, ROLE == kRoleHeavy ? kHeavyWaves : kLightWaves) void k_pair_tasks(
     const uint8_t *__restrict__ pay_a, const uint8_t *__restrict__ pay_b, const TaskRec *__restrict__ recs,
     uint64_t n, uint8_t *__restrict__ out, TaskMeta tm, unsigned long long *queue) {
   __shared__ __attribute__((aligned(16))) uint32_t lds[4][2048];
   __shared__ __attribute__((aligned(16))) uint16_t stage[ROLE == kRoleLight ? 4 : 1][kStageVals];
-#if RBG_FILTER_TRANSPOSE
-  __shared__ uint4 tbuf[ROLE == kRoleLight ? 4 : 1][32]; // per-wave half-row transpose (filter_rows_transposed)
-#endif
+  __shared__ uint4 tbuf[ROLE == kRoleLight ? 4 : 1][32]; // per-wave half-row transpose (filter_rows_linear)
   const int lane = lane_id();
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   // static schedule (queue == nullptr): wave w takes tasks w, w + stride, ...; dynamic: chunks of
@@ -701,7 +620,7 @@ __global__ __launch_bounds__(256, ROLE == kRoleHeavy ? RBG_HEAVY_WAVES : RBG_LIG
   RecU cur = load_rec(recs + g);
   Task tc = decode_task<OP>(cur, pay_a, pay_b);
   uint4 pq[8], qq[8];
-#if RBG_LIGHT_TIMING
+#if RBG_STUDY
   uint64_t lt_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, lt0 = 0, lt1 = 0, lt2 = 0; // decode, stage B/A/R, copy, filter, iteration, tasks
 #define RBG_LT(x) if (ROLE == kRoleLight) { x; }
 #define RBG_HT(x) if (ROLE == kRoleHeavy) { x; }
@@ -709,16 +628,9 @@ __global__ __launch_bounds__(256, ROLE == kRoleHeavy ? RBG_HEAVY_WAVES : RBG_LIG
 #define RBG_LT(x)
 #define RBG_HT(x)
 #endif
-  // P of a light filter task in word order (filter_words_linear), every other P in 16-B chunks
-  auto load_p = [&](const Task &t) {
-    if (ROLE == kRoleLight && RBG_FILTER_WORDS && t.kind == kFilter) load_words(pq, t.pp, t.pbytes, lane);
-    else RBG_LOAD(pq, t.pp, t.bigp ? 16u : t.pbytes, lane);
-  };
-  load_p(tc);
-  if (tc.kind == kCopy || tc.bigq) RBG_LOAD(qq, tc.pp, 16, lane);
-  else RBG_LOAD(qq, tc.pq, tc.qbytes, lane);
-  RecU nn{};
-  bool nn_ok = false;
+  load_chunks(pq, tc.pp, tc.bigp ? 16u : tc.pbytes, lane);
+  if (tc.kind == kCopy || tc.bigq) load_chunks(qq, tc.pp, 16, lane);
+  else load_chunks(qq, tc.pq, tc.qbytes, lane);
   while (true) {
     uint64_t gn = g + stride;
     bool new_chunk = false;
@@ -730,25 +642,9 @@ __global__ __launch_bounds__(256, ROLE == kRoleHeavy ? RBG_HEAVY_WAVES : RBG_LIG
       }
     }
     const bool has_next = gn < n;
-    unsigned long long claim_v = 0;
-    if (RBG_CLAIM_EARLY && new_chunk) claim_v = claim_issue(queue, qk, qtried, lane);
     RBG_LT(lt0 = __builtin_amdgcn_s_memtime());
     RBG_HT(lt0 = __builtin_amdgcn_s_memtime());
-    const RecU nx = RBG_REC_AHEAD && nn_ok ? nn : load_rec(recs + (has_next ? gn : g));
-    if (RBG_REC_AHEAD) { // the record after next, where its index is already known, an iteration ahead
-      uint64_t gnn = n;
-      if (has_next) {
-        if (queue) {
-          const uint64_t ce = new_chunk ? nend : cend; // end of gn's chunk
-          if (gn + 1 < ce) gnn = gn + 1;
-          else if (!new_chunk) gnn = nxt; // gn ends the current chunk: the claimed chunk follows
-        } else {
-          gnn = gn + stride;
-        }
-      }
-      nn_ok = gnn < n;
-      if (nn_ok) nn = load_rec(recs + gnn);
-    }
+    const RecU nx = load_rec(recs + (has_next ? gn : g));
     const Task tn = decode_task<OP>(nx, pay_a, pay_b);
     RBG_LT(lt1 = __builtin_amdgcn_s_memtime(); lt_acc[0] += lt1 - lt0);
     RBG_HT(lt1 = __builtin_amdgcn_s_memtime(); lt_acc[0] += lt1 - lt0);
@@ -756,7 +652,7 @@ __global__ __launch_bounds__(256, ROLE == kRoleHeavy ? RBG_HEAVY_WAVES : RBG_LIG
     uint32_t nr = 0, cw = 0xFFFFFFFFu; // cw: the card word to store when it is not c (lazy marks)
     uint8_t *dst = out + cur.out;
     bool done = false;
-    if (ROLE == kRoleHeavy && RBG_RUN_INTERVALS && OP == RB_AND && tc.tp == kRun && tc.tq == kRun && !tc.bigp &&
+    if (ROLE == kRoleHeavy && OP == RB_AND && tc.tp == kRun && tc.tq == kRun && !tc.bigp &&
         !tc.bigq && ((tc.rp + 3) & ~3u) + tc.rq <= 2048u) {
       int r = 0;
       done = and_runs_intervals<CARD_ONLY>(pq, qq, tc.rp, tc.rq, s, dst, lane, c, r);
@@ -766,39 +662,22 @@ __global__ __launch_bounds__(256, ROLE == kRoleHeavy ? RBG_HEAVY_WAVES : RBG_LIG
         __builtin_amdgcn_sched_barrier(0);
         {
           const bool real = has_next && !tn.bigq;
-          RBG_LOAD(qq, real ? tn.pq : tn.pp, real ? tn.qbytes : 16u, lane);
+          load_chunks(qq, real ? tn.pq : tn.pp, real ? tn.qbytes : 16u, lane);
         }
-        RBG_LOAD(pq, tn.pp, tn.bigp ? 16u : tn.pbytes, lane);
+        load_chunks(pq, tn.pp, tn.bigp ? 16u : tn.pbytes, lane);
       }
     }
     if (ROLE == kRoleHeavy && !done) {
       // ---- the result as a register bitmap: P = A, Q = B (never swapped: ANDNOT and the type
       //      rules are ordered)
       uint64_t w[kW];
-      const bool comb = RBG_HEAVY_COMBINE && (OP == RB_OR || OP == RB_XOR) && !tc.bigp && !tc.bigq &&
-                        !bitmap_payload(tc.tp, tc.cp) && !bitmap_payload(tc.tq, tc.cq) &&
-                        ((tc.tp == kArray && tc.tq == kArray) || (OP == RB_XOR && tc.tp == kRun && tc.tq == kRun));
-      if (comb) { // both operands into one image: P | Q, P ^ Q, or the toggles of P ^ Q
-        lds_zero(s, lane);
-        wave_lds_sync();
-        if (tc.tp == kArray) {
-          scatter_array_chunks<false>(pq, tc.cp, s, lane);
-          scatter_array_chunks<OP == RB_XOR>(qq, tc.cq, s, lane);
-        } else {
-          scatter_run_toggles<false>(pq, tc.rp, s, lane);
-          scatter_run_toggles<true>(qq, tc.rq, s, lane);
-        }
-        wave_lds_sync();
-        lds_read_words(s, w, lane);
-        wave_lds_sync();
-        if (tc.tp == kRun) toggles_to_words(w, lane);
-      } else if (bitmap_payload(tc.tp, tc.cp)) {
+      if (bitmap_payload(tc.tp, tc.cp)) {
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
           w[2 * k] = pack2(pq[k].x, pq[k].y);
           w[2 * k + 1] = pack2(pq[k].z, pq[k].w);
         }
-      } else if (RBG_RUN_REG_PREFIX && tc.tp == kRun && !tc.bigp) {
+      } else if (tc.tp == kRun && !tc.bigp) {
         stage_run_toggles(pq, tc.rp, s, lane); // toggles -> registers -> prefix-xor in registers
         lds_read_words(s, w, lane);
         wave_lds_sync();
@@ -809,14 +688,13 @@ __global__ __launch_bounds__(256, ROLE == kRoleHeavy ? RBG_HEAVY_WAVES : RBG_LIG
         lds_read_words(s, w, lane);
         wave_lds_sync();
       }
-      if (comb) {
-      } else if (bitmap_payload(tc.tq, tc.cq)) {
+      if (bitmap_payload(tc.tq, tc.cq)) {
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
           word_op<OP>(w[2 * k], pack2(qq[k].x, qq[k].y));
           word_op<OP>(w[2 * k + 1], pack2(qq[k].z, qq[k].w));
         }
-      } else if (RBG_RUN_REG_PREFIX && tc.tq == kRun && !tc.bigq) {
+      } else if (tc.tq == kRun && !tc.bigq) {
         stage_run_toggles(qq, tc.rq, s, lane);
         uint64_t t[kW];
         lds_read_words(s, t, lane);
@@ -842,9 +720,9 @@ __global__ __launch_bounds__(256, ROLE == kRoleHeavy ? RBG_HEAVY_WAVES : RBG_LIG
       __builtin_amdgcn_sched_barrier(0);
       {
         const bool real = has_next && !tn.bigq;
-        RBG_LOAD(qq, real ? tn.pq : tn.pp, real ? tn.qbytes : 16u, lane);
+        load_chunks(qq, real ? tn.pq : tn.pp, real ? tn.qbytes : 16u, lane);
       }
-      RBG_LOAD(pq, tn.pp, tn.bigp ? 16u : tn.pbytes, lane);
+      load_chunks(pq, tn.pp, tn.bigp ? 16u : tn.pbytes, lane);
       const int ta = tc.tp, tb = tc.tq;
       const bool lazy = OP == RB_OR && tm.lazy;
       const bool eff = eff_rule<OP>(ta, tb, tc.cp, tc.cq);
@@ -867,56 +745,27 @@ __global__ __launch_bounds__(256, ROLE == kRoleHeavy ? RBG_HEAVY_WAVES : RBG_LIG
       RBG_HT(lt_acc[3 + (ty == kBitmap ? 0 : ty == kArray ? 1 : 2)] += __builtin_amdgcn_s_memtime() - lt2);
     } else if (ROLE != kRoleHeavy) {
       // ---- phase 1: stage X (filter) or store the clone (copy)
-      if (tc.kind == kFilter && !(RBG_LIGHT_ABLATE & (tc.tq == kBitmap ? 1 : tc.tq == kArray ? 2 : 4))) {
+      if (tc.kind == kFilter) {
         if (tc.bigq) stage_big_runs(tc.pq, tc.rq, s, lane); // only a Run payload exceeds 8 KiB
-        else if (RBG_LIGHT_RUN_REG && tc.tq == kRun) { // toggles -> registers (X's) -> prefix -> image
-          stage_run_toggles(qq, tc.rq, s, lane);
-          uint64_t t[kW];
-          lds_read_words(s, t, lane);
-          wave_lds_sync();
-          toggles_to_words(t, lane);
-          lds_write_words(s, t, lane);
-          wave_lds_sync();
-        } else stage_from_chunks(tc.tq, qq, tc.cq, tc.rq, s, lane);
+        else stage_from_chunks(tc.tq, qq, tc.cq, tc.rq, s, lane);
       } else if (!CARD_ONLY) {
         if (tc.bigp) copy_payload(tc.pp, dst, tc.pbytes, lane);
         else store_chunks(pq, dst, tc.pbytes, lane);
       }
       {
         const bool real = has_next && tn.kind != kCopy && !tn.bigq;
-        RBG_LOAD(qq, real ? tn.pq : tn.pp, real ? tn.qbytes : 16u, lane);
+        load_chunks(qq, real ? tn.pq : tn.pp, real ? tn.qbytes : 16u, lane);
       }
       RBG_LT(lt2 = __builtin_amdgcn_s_memtime(); lt_acc[tc.kind == kFilter ? 1 + (tc.tq == kBitmap ? 0 : tc.tq == kArray ? 1 : 2) : 4] += lt2 - lt1);
-      // ---- phase 2: filter F against the staged X.  (Streaming the next F into pq row by row as
-      //      the filter frees it measured 7% slower: loads and the staged stores share vmcnt, so
-      //      the loads issued mid-filter serialise the output flushes behind them.)
-      if (tc.kind == kFilter && !(RBG_LIGHT_ABLATE & 8)) {
-        const int nfc = (int)((tc.cp + 7) >> 3);
+      // ---- phase 2: filter F against the staged X, in value order (adjacent lanes, adjacent values)
+      //      through a linear per-wave stage.  (Streaming the next F into pq row by row as the filter
+      //      frees it measured 7% slower: loads and the staged stores share vmcnt, so the loads issued
+      //      mid-filter serialise the output flushes behind them.)
+      if (tc.kind == kFilter) {
         uint16_t *o = CARD_ONLY ? nullptr : reinterpret_cast<uint16_t *>(dst);
-        auto none = [](int) {};
-#if RBG_FILTER_WORDS
-        (void)nfc;
-        (void)none;
-        c = OP == RB_ANDNOT ? filter_words_linear<true, !CARD_ONLY>(pq, (int)tc.cp, s, ob, o, lane)
-                            : filter_words_linear<false, !CARD_ONLY>(pq, (int)tc.cp, s, ob, o, lane);
-#elif RBG_FILTER_TRANSPOSE
-        (void)nfc;
-        (void)none;
         uint4 *tb = tbuf[ROLE == kRoleLight ? wv : 0];
-#if RBG_FILTER_LINEAR
-        auto next_f = [&]() { // the next task's P into the registers F has left
-          if (RBG_EARLY_NEXT_P) RBG_LOAD(pq, tn.pp, tn.bigp ? 16u : tn.pbytes, lane);
-        };
-        c = OP == RB_ANDNOT ? filter_rows_linear<true, !CARD_ONLY>(pq, (int)tc.cp, s, ob, tb, o, lane, next_f)
-                            : filter_rows_linear<false, !CARD_ONLY>(pq, (int)tc.cp, s, ob, tb, o, lane, next_f);
-#else
-        c = OP == RB_ANDNOT ? filter_rows_transposed<true>(pq, (int)tc.cp, s, ob, tb, o, lane)
-                            : filter_rows_transposed<false>(pq, (int)tc.cp, s, ob, tb, o, lane);
-#endif
-#else
-        c = OP == RB_ANDNOT ? filter_chunks_staged<true>(pq, nfc, (int)tc.cp, s, ob, o, lane, none)
-                            : filter_chunks_staged<false>(pq, nfc, (int)tc.cp, s, ob, o, lane, none);
-#endif
+        c = OP == RB_ANDNOT ? filter_rows_linear<true, !CARD_ONLY>(pq, (int)tc.cp, s, ob, tb, o, lane)
+                            : filter_rows_linear<false, !CARD_ONLY>(pq, (int)tc.cp, s, ob, tb, o, lane);
         ty = c ? kArray : kEmpty;
       } else {
         ty = tc.tp;
@@ -924,8 +773,7 @@ __global__ __launch_bounds__(256, ROLE == kRoleHeavy ? RBG_HEAVY_WAVES : RBG_LIG
         nr = tc.rp;
       }
       RBG_LT(lt_acc[5] += __builtin_amdgcn_s_memtime() - lt2);
-      if (!(RBG_EARLY_NEXT_P && RBG_FILTER_LINEAR && !RBG_FILTER_WORDS && tc.kind == kFilter && !(RBG_LIGHT_ABLATE & 8)))
-        load_p(tn);
+      load_chunks(pq, tn.pp, tn.bigp ? 16u : tn.pbytes, lane);
     }
     wave_lds_sync(); // the next task restages the same LDS image
     if (lane == 0) {
@@ -938,8 +786,7 @@ __global__ __launch_bounds__(256, ROLE == kRoleHeavy ? RBG_HEAVY_WAVES : RBG_LIG
     if (!has_next) break;
     if (new_chunk) {
       cend = nend;
-      const Chunk c1 = RBG_CLAIM_EARLY ? claim_finish(claim_v, queue, n, qk, qtried, lane)
-                                       : claim_chunk(queue, n, qk, qtried, lane);
+      const Chunk c1 = claim_chunk(queue, n, qk, qtried, lane);
       nxt = c1.s;
       nend = c1.e;
     }
@@ -947,7 +794,7 @@ __global__ __launch_bounds__(256, ROLE == kRoleHeavy ? RBG_HEAVY_WAVES : RBG_LIG
     cur = nx;
     tc = tn;
   }
-#if RBG_LIGHT_TIMING
+#if RBG_STUDY
   if (ROLE == kRoleLight && lane == 0 && wv == 0 && blockIdx.x % 97 == 0)
     printf("light timing blk %u: decode %lu stageB %lu stageA %lu stageR %lu copy %lu filter %lu iter %lu tasks %lu\n",
            blockIdx.x, lt_acc[0], lt_acc[1], lt_acc[2], lt_acc[3], lt_acc[4], lt_acc[5], lt_acc[6], lt_acc[7]);
@@ -955,68 +802,6 @@ __global__ __launch_bounds__(256, ROLE == kRoleHeavy ? RBG_HEAVY_WAVES : RBG_LIG
     printf("heavy timing op %d blk %u: decode %lu build %lu metrics %lu emitB %lu emitA %lu emitR %lu iter %lu tasks %lu\n",
            OP, blockIdx.x, lt_acc[0], lt_acc[1], lt_acc[2], lt_acc[3], lt_acc[4], lt_acc[5], lt_acc[6], lt_acc[7]);
 #endif
-}
-
-// The register path without a software pipeline: ONE WAVE PER TASK, one launch-sized grid (3
-// waves per SIMD; the hardware dispatcher supplies the next task).  Both containers as 65536-bit
-// register bitmaps, word op, card + maximal runs, reference type decision, coalesced emission.
-template <int OP, bool CARD_ONLY>
-__global__ __launch_bounds__(256) void k_pair_heavy_np(const uint8_t *__restrict__ pay_a,
-                                                    const uint8_t *__restrict__ pay_b,
-                                                    const TaskRec *__restrict__ recs, uint64_t n,
-                                                    uint8_t *__restrict__ out, TaskMeta tm) {
-  __shared__ __attribute__((aligned(16))) uint32_t lds[4][2048];
-  const int lane = lane_id();
-  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint64_t g = (uint64_t)blockIdx.x * 4 + wv;
-  if (g >= n) return;
-  uint32_t *s = lds[wv];
-  const RecU rc = load_rec(recs + g);
-  const int ta = (int)desc_type(rc.da), tb = (int)desc_type(rc.db);
-  const uint32_t ca = desc_card(rc.da), cb = desc_card(rc.db);
-  uint64_t wa[kW], wb[kW];
-  // issue the coalesced Bitmap loads first so they are in flight during any LDS expansion
-  if (ta == kBitmap) load_bitmap(pay_a + rc.pa, wa, lane);
-  if (tb == kBitmap) load_bitmap(pay_b + rc.pb, wb, lane);
-  if (ta != kBitmap) load_container(ta, pay_a + rc.pa, ca, rc.ra, s, wa, lane);
-  if (tb != kBitmap) load_container(tb, pay_b + rc.pb, cb, rc.rb, s, wb, lane);
-#pragma unroll
-  for (int j = 0; j < kW; ++j) {
-    if (OP == RB_AND) wa[j] &= wb[j];
-    else if (OP == RB_OR) wa[j] |= wb[j];
-    else if (OP == RB_XOR) wa[j] ^= wb[j];
-    else wa[j] &= ~wb[j];
-  }
-  bool eff;
-  if (OP == RB_AND) eff = ta == kRun && tb == kRun;
-  else if (OP == RB_OR) eff = ta != kBitmap && tb != kBitmap && !(ta == kArray && tb == kArray);
-  else if (OP == RB_XOR)
-    eff = (ta == kRun && tb == kRun) || (ta == kArray && tb == kRun && ca < (uint32_t)kRunArrayThreshold) ||
-          (ta == kRun && tb == kArray && cb < (uint32_t)kRunArrayThreshold);
-  else eff = (ta == kRun && tb == kRun) || (ta == kRun && tb == kArray && cb < (uint32_t)kRunArrayThreshold);
-  int c, r;
-  metrics(wa, lane, eff && !CARD_ONLY, c, r);
-  int ty;
-  if (OP != RB_OR && c == 0) ty = kEmpty;
-  else if (eff) ty = type_eff(c, r);
-  else if (OP == RB_OR && (ta == kBitmap || tb == kBitmap)) {
-    ty = type_lr(c);
-    if (ty == kRun) r = 1; // LR's Run is the full container: one run
-  } else ty = type_ab(c);
-  if (CARD_ONLY) {
-    if (lane == 0) {
-      tm.type[rc.t] = c ? (uint8_t)kArray : kEmpty;
-      tm.card[rc.t] = (uint32_t)c;
-      tm.nruns[rc.t] = 0;
-    }
-    return;
-  }
-  if (ty != kEmpty) emit_container(ty, wa, c, r, out + rc.out, s, lane);
-  if (lane == 0) {
-    tm.type[rc.t] = (uint8_t)ty;
-    tm.card[rc.t] = (uint32_t)c;
-    tm.nruns[rc.t] = (uint16_t)(ty == kRun ? r : 0);
-  }
 }
 
 // ---------------------------------------------------------------- measurement probes
@@ -1246,26 +1031,11 @@ static void launch_op(bool card_only, const uint8_t *pa, const uint8_t *pb, cons
   if (card_only) launch_tasks<OP, true, kRoleLight>(pa, pb, light, nl, out, tm, st);
   else launch_tasks<OP, false, kRoleLight>(pa, pb, light, nl, out, tm, st);
   (void)hipEventRecord(mid, st);
-#if RBG_HEAVY_PERSISTENT
   if (card_only) launch_tasks<OP, true, kRoleHeavy>(pa, pb, heavy, nh, out, tm, st);
   else launch_tasks<OP, false, kRoleHeavy>(pa, pb, heavy, nh, out, tm, st);
-#else
-  if (nh) {
-    // one wave per task: at most 2^32 / 64 tasks per launch
-    for (uint64_t t0 = 0; t0 < nh; t0 += (1ull << 26)) {
-      const uint64_t nt = std::min<uint64_t>(nh - t0, 1ull << 26);
-      if (card_only) k_pair_heavy_np<OP, true><<<blocks_for(nt, 4), 256, 0, st>>>(pa, pb, heavy + t0, nt, out, tm);
-      else k_pair_heavy_np<OP, false><<<blocks_for(nt, 4), 256, 0, st>>>(pa, pb, heavy + t0, nt, out, tm);
-    }
-  }
-#endif
 }
-#ifndef RBG_CONC_LIGHT_PER_CU
-#define RBG_CONC_LIGHT_PER_CU 2 // light blocks per CU beside the heavy kernel (2 x 128 VGPRs per SIMD)
-#endif
-#ifndef RBG_CONC_HEAVY_PER_CU
-#define RBG_CONC_HEAVY_PER_CU 1 // heavy blocks per CU (256 VGPRs per SIMD)
-#endif
+constexpr unsigned kConcLightPerCu = 2; // light blocks per CU beside the heavy kernel (2 x 128 VGPRs per SIMD)
+constexpr unsigned kConcHeavyPerCu = 1; // heavy blocks per CU (256 VGPRs per SIMD)
 template <int OP>
 static void launch_op_concurrent(bool card_only, const uint8_t *pa, const uint8_t *pb, const TaskRec *light,
                                  uint64_t nl, const TaskRec *heavy, uint64_t nh, uint8_t *out, const TaskMeta &tm,
@@ -1278,17 +1048,17 @@ static void launch_op_concurrent(bool card_only, const uint8_t *pa, const uint8_
   unsigned long long *hq = queue ? queue + kHeavyQueueOffset : nullptr;
   // heavy first: its blocks need the larger register slot
   (void)hipEventRecord(ev_h0, side);
-  if (card_only) launch_tasks<OP, true, kRoleHeavy>(pa, pb, heavy, nh, out, tm, side, RBG_CONC_HEAVY_PER_CU, hq);
-  else launch_tasks<OP, false, kRoleHeavy>(pa, pb, heavy, nh, out, tm, side, RBG_CONC_HEAVY_PER_CU, hq);
+  if (card_only) launch_tasks<OP, true, kRoleHeavy>(pa, pb, heavy, nh, out, tm, side, kConcHeavyPerCu, hq);
+  else launch_tasks<OP, false, kRoleHeavy>(pa, pb, heavy, nh, out, tm, side, kConcHeavyPerCu, hq);
   (void)hipEventRecord(ev_h1, side);
-  if (card_only) launch_tasks<OP, true, kRoleLight>(pa, pb, light, nl, out, tm, st, RBG_CONC_LIGHT_PER_CU, queue);
-  else launch_tasks<OP, false, kRoleLight>(pa, pb, light, nl, out, tm, st, RBG_CONC_LIGHT_PER_CU, queue);
+  if (card_only) launch_tasks<OP, true, kRoleLight>(pa, pb, light, nl, out, tm, st, kConcLightPerCu, queue);
+  else launch_tasks<OP, false, kRoleLight>(pa, pb, light, nl, out, tm, st, kConcLightPerCu, queue);
   (void)hipEventRecord(light_done, st);
   if (queue) {
-    if (card_only) launch_tasks<OP, true, kRoleLight>(pa, pb, light, nl, out, tm, side, RBG_CONC_LIGHT_PER_CU, queue);
-    else launch_tasks<OP, false, kRoleLight>(pa, pb, light, nl, out, tm, side, RBG_CONC_LIGHT_PER_CU, queue);
-    if (card_only) launch_tasks<OP, true, kRoleHeavy>(pa, pb, heavy, nh, out, tm, st, RBG_CONC_HEAVY_PER_CU, hq);
-    else launch_tasks<OP, false, kRoleHeavy>(pa, pb, heavy, nh, out, tm, st, RBG_CONC_HEAVY_PER_CU, hq);
+    if (card_only) launch_tasks<OP, true, kRoleLight>(pa, pb, light, nl, out, tm, side, kConcLightPerCu, queue);
+    else launch_tasks<OP, false, kRoleLight>(pa, pb, light, nl, out, tm, side, kConcLightPerCu, queue);
+    if (card_only) launch_tasks<OP, true, kRoleHeavy>(pa, pb, heavy, nh, out, tm, st, kConcHeavyPerCu, hq);
+    else launch_tasks<OP, false, kRoleHeavy>(pa, pb, heavy, nh, out, tm, st, kConcHeavyPerCu, hq);
   }
 }
 void launch_pairwise_concurrent(int op, bool card_only, const uint8_t *pa, const uint8_t *pb, const TaskRec *light,
@@ -1438,11 +1208,9 @@ constexpr int kSmallLdsMax = 160 * 1024;
 __host__ __device__ inline uint32_t small_lds_bytes(uint32_t waves, uint32_t kmax) {
   return waves * 8192u + 64u + 4u * kmax + 2u * kmax + 2u * (kmax + 1) + 16u;
 }
-#ifndef RBG_SMALL_WAVES
-#define RBG_SMALL_WAVES 2 // waves per SIMD of the small-batch kernel (the register path takes ~235 VGPRs; 3 and 4 spill)
-#endif
+constexpr int kSmallWaves = 2; // waves per SIMD of the small-batch kernel (the register path takes ~235 VGPRs; 3 and 4 spill)
 template <int OP, bool CARD_ONLY>
-__global__ __launch_bounds__(256, RBG_SMALL_WAVES) void k_pair_small(SmallPairArgs a, uint32_t kmax) {
+__global__ __launch_bounds__(256, kSmallWaves) void k_pair_small(SmallPairArgs a, uint32_t kmax) {
   extern __shared__ __attribute__((aligned(16))) uint8_t dyn_lds[];
   const uint32_t nw = blockDim.x >> 6;
   uint32_t *wtot = reinterpret_cast<uint32_t *>(dyn_lds + nw * 8192u); // [16] block-scan wave totals

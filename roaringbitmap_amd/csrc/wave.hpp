@@ -280,49 +280,6 @@ __device__ __forceinline__ void stage_container(int type, const uint8_t *p, uint
   wave_lds_sync();
 }
 
-// Filter a sorted u16 array F against the LDS membership image `s`: keep the values whose bit
-// equals !NEGATE.  F is preloaded as up to 8 uint4 chunks per lane (chunk c = lane + 64*i holds
-// values 8c..8c+7; nfc chunks, nf values).  Kept values are written in order to `out` (unless
-// null); returns their count (wave-uniform).  This is the whole of A&x, x&A and A\x: the result
-// is a subset of an Array, hence an Array (ArrayContainer.and/andNot, BitmapContainer.and(Array),
-// RunContainer.and(Array): ArrayContainer.java:184-271, BitmapContainer.java:162-172,
-// RunContainer.java:305-336).
-template <bool NEGATE>
-__device__ __forceinline__ int filter_chunks(const uint4 (&fq)[8], int nfc, int nf, const uint32_t *s, uint16_t *out,
-                                             int lane) {
-  const int iters = (nfc + 63) >> 6; // wave-uniform, <= 8
-  uint32_t total = 0;
-  // One chunk row per step, kept values written in the same step: a scan per row keeps only
-  // one row's values live (the scheduling fence stops the compiler from hoisting all 64 LDS
-  // probes of the unrolled loop, which would double the kernel's VGPR footprint).
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    if (i < iters) {
-      const int c = lane + 64 * i;
-      const int n = c < nfc ? min(8, nf - 8 * c) : 0;
-      const uint32_t x[8] = {fq[i].x & 0xFFFF, fq[i].x >> 16, fq[i].y & 0xFFFF, fq[i].y >> 16,
-                             fq[i].z & 0xFFFF, fq[i].z >> 16, fq[i].w & 0xFFFF, fq[i].w >> 16};
-      uint32_t keep = 0;
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const uint32_t m = (s[x[k] >> 5] >> (x[k] & 31)) & 1;
-        if (k < n && (m ^ (NEGATE ? 1u : 0u))) keep |= 1u << k;
-      }
-      const uint32_t cnt = (uint32_t)__popc(keep);
-      const uint32_t incl = wave_scan_u32(cnt, lane);
-      if (out) {
-        uint32_t pos = total + incl - cnt;
-#pragma unroll
-        for (int k = 0; k < 8; ++k)
-          if ((keep >> k) & 1) out[pos++] = (uint16_t)x[k];
-      }
-      total += readlane(incl, 63);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-  }
-  return (int)total;
-}
-
 // ---------------------------------------------------------------- register-preloaded payloads
 // A payload of at most 8 KiB as 8 uint4 per lane: chunk c = lane + 64*i (16 bytes) in q[i].
 // Buffer loads: a 32-bit per-lane offset against a wave-uniform descriptor, and lanes past the
@@ -340,167 +297,31 @@ __device__ __forceinline__ void load_chunks(uint4 (&q)[8], const uint8_t *p, uin
 #pragma unroll
   for (int i = 0; i < 8; ++i) q[i] = load_chunk_row(rs, i, lane);
 }
-// load_chunks issuing only the 1 KiB rows the payload reaches (wave-uniform guards): a fully
-// out-of-range row costs no memory request but still a full 64-lane return through the texture
-// data path.  Rows past the payload keep stale registers — every consumer bounds its rows by the
-// payload's count (Array values, runs, F's values, copy bytes).
-__device__ __forceinline__ void load_chunks_used(uint4 (&q)[8], const uint8_t *p, uint32_t bytes, int lane) {
-  const __amdgpu_buffer_rsrc_t rs = chunk_rsrc(p, bytes);
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-    if ((uint32_t)(1024 * i) < bytes) q[i] = load_chunk_row(rs, i, lane);
-}
-
-// Exclusive prefix (over lanes) and wave total of a per-lane count in [0, 16), by bit-sliced ballots
-// and mbcnt: no cross-lane data movement through LDS, no dependency chain of shuffles.
+// lanes below this one with their bit set in m
 __device__ __forceinline__ uint32_t mbcnt64(uint64_t m) {
   return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
-__device__ __forceinline__ void ballot_scan4(uint32_t cnt, uint32_t &excl, uint32_t &total) {
-  excl = 0;
-  total = 0;
-#pragma unroll
-  for (int b = 0; b < 4; ++b) {
-    const uint64_t m = __ballot((cnt >> b) & 1);
-    excl += mbcnt64(m) << b;
-    total += (uint32_t)__popcll(m) << b;
-  }
-}
-
-// The same filter with coalesced output.  Kept values are ranked into a per-wave LDS ring `ob` of
-// kStageRing u16 (16-B aligned); after each row every complete 16-B block of ranked values is
-// written with one 16-B-per-lane store.  At most 7 + 512 values are pending, so a ring of 576
-// never overwrites a pending value, and a block never straddles the wrap (576 % 8 == 0).  One
-// wave's LDS operations execute in order, so the ranked writes, the block reads and the next
-// row's writes need no drains between them.  The final partial block is written whole: result
-// slots are round16(2 * bound) bytes, so bytes past the last value stay in the slot's padding.
-// Rejected values go to a per-lane dummy slot instead of being branched around.
-constexpr int kStageRing = 576; // >= 7 + 512 pending values, a multiple of 8
-constexpr int kStageVals = kStageRing + 64;   // + one dummy slot per lane
-// `reload(i)` is called once per row i as soon as fq[i] is free — right after the row's values are
-// in registers, or at the start for rows this payload does not have — so the caller can stream the
-// next task's payload into fq row by row instead of after the whole filter.
-template <bool NEGATE, class Reload>
-__device__ __forceinline__ int filter_chunks_staged(uint4 (&fq)[8], int nfc, int nf, const uint32_t *s,
-                                                    uint16_t *ob, uint16_t *out, int lane, const Reload &reload) {
-  const int iters = (nfc + 63) >> 6; // wave-uniform, <= 8
-  uint32_t flushed = 0, tot = 0;     // values written out / ranked so far (wave-uniform)
-  uint4 *out4 = reinterpret_cast<uint4 *>(out);
-  const uint4 *ob4 = reinterpret_cast<const uint4 *>(ob);
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-    if (i >= iters) reload(i);
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    if (i < iters) {
-      const int c = lane + 64 * i;
-      const int n = c < nfc ? min(8, nf - 8 * c) : 0;
-      const uint32_t x[8] = {fq[i].x & 0xFFFF, fq[i].x >> 16, fq[i].y & 0xFFFF, fq[i].y >> 16,
-                             fq[i].z & 0xFFFF, fq[i].z >> 16, fq[i].w & 0xFFFF, fq[i].w >> 16};
-      reload(i);
-      // all 8 probes in flight before the first wait: one LDS round trip per row, not eight
-      uint32_t m[8];
-#pragma unroll
-      for (int k = 0; k < 8; ++k) m[k] = s[x[k] >> 5];
-      __builtin_amdgcn_sched_group_barrier(0x100, 8, 0); // DS reads first
-      __builtin_amdgcn_sched_group_barrier(0x002, 64, 0); // then the VALU work
-      uint32_t keep = 0;
-#pragma unroll
-      for (int k = 0; k < 8; ++k) keep |= (((m[k] >> (x[k] & 31)) & 1) ^ (NEGATE ? 1u : 0u)) << k;
-      keep &= (1u << n) - 1; // n <= 8: lanes past the payload keep nothing
-      uint32_t excl, rowtot;
-      ballot_scan4((uint32_t)__popc(keep), excl, rowtot);
-      if (out) {
-        uint32_t base = tot % kStageRing + excl; // < 640 + 512
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          uint32_t pos = base + (uint32_t)__popc(keep & ((1u << k) - 1));
-          pos = pos >= (uint32_t)kStageRing ? pos - kStageRing : pos;
-          ob[((keep >> k) & 1) ? pos : (uint32_t)(kStageRing + lane)] = (uint16_t)x[k];
-        }
-        const uint32_t full = (tot + rowtot) & ~7u; // values in complete blocks
-        const uint32_t nb = (full - flushed) >> 3, b0 = flushed >> 3;
-        if ((uint32_t)lane < nb) {
-          uint32_t rb = b0 + lane; // ring block
-          rb %= (uint32_t)(kStageRing / 8);
-          out4[b0 + lane] = ob4[rb];
-        }
-        flushed = full;
-      }
-      tot += rowtot;
-    }
-    __builtin_amdgcn_sched_barrier(0);
-  }
-  if (out && tot > flushed && lane == 0) out4[flushed >> 3] = ob4[(flushed >> 3) % (kStageRing / 8)];
-  return (int)tot;
-}
-
-// The staged filter with the row transposed before probing: a row's 512 values arrive as chunks of
-// 8 consecutive values per lane, so in chunk order the 64 lanes of one probe instruction read
-// words ~8 values apart — for a sparse F that is a fixed stride of many words and a 16-way LDS bank
-// conflict (SQ_LDS_BANK_CONFLICT ≈ 13 extra cycles per probe, profiles/r01/v7).  Written once to a
-// per-wave 1 KiB buffer `tb` and read back as value 64k + lane, adjacent lanes probe adjacent
-// values (nearby or shared words).  Kept values are then ranked per k by one ballot, which also
-// keeps them in sorted order for the same ring / 16-B block flush as filter_chunks_staged.
-template <bool NEGATE>
-__device__ __forceinline__ int filter_rows_transposed(const uint4 (&fq)[8], int nf, const uint32_t *s, uint16_t *ob,
-                                                      uint4 *tb, uint16_t *out, int lane) {
-  const int iters = (nf + 511) >> 9; // wave-uniform, <= 8
-  uint32_t flushed = 0, tot = 0;
-  uint4 *out4 = reinterpret_cast<uint4 *>(out);
-  const uint4 *ob4 = reinterpret_cast<const uint4 *>(ob);
-  const uint16_t *t16 = reinterpret_cast<const uint16_t *>(tb);
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    if (i < iters) {
-      // two halves of 256 values (lanes 0-31's chunks, then lanes 32-63's) through a 512-B buffer
-#pragma unroll
-      for (int hf = 0; hf < 2; ++hf) {
-        if ((lane >> 5) == hf) tb[lane & 31] = fq[i];
-        wave_lds_sync(); // other lanes' stores: without the fence the compiler may reuse the last reads
-        const int nh = min(256, nf - 512 * i - 256 * hf); // values of this half (may be <= 0)
-        uint32_t y[4], m[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) y[k] = t16[64 * k + lane];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) m[k] = s[y[k] >> 5];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const bool keep = ((((m[k] >> (y[k] & 31)) & 1) ^ (NEGATE ? 1u : 0u)) != 0) && (64 * k + lane < nh);
-          const uint64_t b = __ballot(keep);
-          if (out) {
-            const uint32_t pos = (tot + mbcnt64(b)) % (uint32_t)kStageRing;
-            ob[keep ? pos : (uint32_t)(kStageRing + lane)] = (uint16_t)y[k];
-          }
-          tot += (uint32_t)__popcll(b);
-        }
-      }
-      if (out) {
-        wave_lds_sync(); // the blocks hold other lanes' ranked values
-        const uint32_t full = tot & ~7u; // values in complete blocks
-        const uint32_t nb = (full - flushed) >> 3, b0 = flushed >> 3;
-        if ((uint32_t)lane < nb) out4[b0 + lane] = ob4[(b0 + lane) % (uint32_t)(kStageRing / 8)];
-        flushed = full;
-      }
-    }
-    __builtin_amdgcn_sched_barrier(0);
-  }
-  if (out && tot > flushed && lane == 0) out4[flushed >> 3] = ob4[(flushed >> 3) % (kStageRing / 8)];
-  return (int)tot;
-}
-
-// filter_rows_transposed with a LINEAR stage instead of a ring: after each row's flush the partial
-// block (< 8 kept values) moves to the front, so a kept value's slot is (pending + mbcnt) with no
-// wrap — mbcnt adds the pending count itself — and rejected lanes are masked off instead of writing a
-// dummy slot.  ~8 VALU per 64 probed values instead of ~15 (ISA count).  Pending values stay < 8 + 512.
-// `next()` runs once the last row of F is in the transpose buffer — F's registers are free from
-// there, so the caller's prefetch of the next task's F overlaps the last row's probes and flush.
-#ifndef RBG_SKIP_EMPTY_HALF
-#define RBG_SKIP_EMPTY_HALF 1 // filter_rows_linear: a last row with <= 256 values skips its empty second half
-#endif
-template <bool NEGATE, bool STORE, class Next>
+// The Array filter (A&x, x&A, A\x: the result is a subset of an Array, hence an Array —
+// ArrayContainer.and/andNot, BitmapContainer.and(Array), RunContainer.and(Array):
+// ArrayContainer.java:184-271, BitmapContainer.java:162-172, RunContainer.java:305-336).  F, a sorted
+// u16 array, is preloaded as up to 8 uint4 chunks per lane (chunk c = lane + 64*i holds values
+// 8c..8c+7); its values whose bit in the LDS membership image `s` equals !NEGATE are kept, in order.
+// Each row of 512 values is transposed through a per-wave buffer `tb` first: in chunk order the 64
+// lanes of one probe read words ~8 values apart, a 16-way LDS bank conflict for a sparse F
+// (SQ_LDS_BANK_CONFLICT ≈ 13 extra cycles per probe, profiles/r01/v7); read back as value 64k + lane,
+// adjacent lanes probe adjacent values.  Kept values are ranked per probe by one ballot into a per-wave
+// linear LDS stage `ob` and written as whole 16-B blocks, one 16-B-per-lane store per row; the final
+// partial block is written whole (result slots are round16(2 * bound) bytes, so bytes past the last
+// value stay in the slot's padding).  Rejected lanes write a per-lane dummy slot.
+constexpr int kStageRing = 576;             // >= 7 + 512 pending values, a multiple of 8
+constexpr int kStageVals = kStageRing + 64; // + one dummy slot per lane
+// The stage is LINEAR: after each row's flush the partial block (< 8 kept values) moves to the front,
+// so a kept value's slot is (pending + mbcnt) with no wrap — mbcnt adds the pending count itself.
+// ~8 VALU per 64 probed values (a ring with modulo took ~15, ISA count).  Pending values stay < 8 + 512.
+// A last row with <= 256 values skips its empty second half.
+template <bool NEGATE, bool STORE>
 __device__ __forceinline__ int filter_rows_linear(const uint4 (&fq)[8], int nf, const uint32_t *s, uint16_t *ob,
-                                                  uint4 *tb, uint16_t *out, int lane, const Next &next) {
+                                                  uint4 *tb, uint16_t *out, int lane) {
   static_assert(7 + 512 <= kStageRing, "every slot (pending < 8, + < 512 of a row) lies below the dummies");
   const int iters = (nf + 511) >> 9; // wave-uniform, <= 8
   uint32_t tot = 0, flushed = 0;     // kept / written out so far (wave-uniform; flushed % 8 == 0)
@@ -514,13 +335,9 @@ __device__ __forceinline__ int filter_rows_linear(const uint4 (&fq)[8], int nf, 
     if (i < iters) {
 #pragma unroll
       for (int hf = 0; hf < 2; ++hf) {
-        if (RBG_SKIP_EMPTY_HALF && hf == 1 && nf - 512 * i <= 256) { // the row's values all lie in its first half
-          if (i == iters - 1) next();
-          continue;
-        }
+        if (hf == 1 && nf - 512 * i <= 256) continue; // the row's values all lie in its first half
         if ((lane >> 5) == hf) tb[lane & 31] = fq[i];
         wave_lds_sync();
-        if (hf == 1 && i == iters - 1) next();
         const int nh = min(256, nf - 512 * i - 256 * hf); // values of this half (may be <= 0)
         uint32_t y[4], m[4];
 #pragma unroll
@@ -550,83 +367,6 @@ __device__ __forceinline__ int filter_rows_linear(const uint4 (&fq)[8], int nf, 
           }
           tot += (uint32_t)__popcll(b);
         }
-      }
-      if (STORE) {
-        wave_lds_sync(); // the blocks hold other lanes' values
-        const uint32_t pend = tot - flushed, nb = pend >> 3;
-        if ((uint32_t)lane < nb) out4[(flushed >> 3) + lane] = ob4[lane];
-        if (lane == 0 && nb && (pend & 7u)) ob4[0] = ob4[nb]; // the partial block to the front
-        wave_lds_sync();
-        flushed += nb << 3;
-      }
-    }
-    __builtin_amdgcn_sched_barrier(0);
-  }
-  if (STORE && tot > flushed && lane == 0) out4[flushed >> 3] = ob4[0];
-  return (int)tot;
-}
-
-// ---- F in word order: register word j (component j & 3 of q[j >> 2]) holds payload u32 word
-// 64 j + lane, i.e. values 2(64 j + lane) and +1, so adjacent lanes hold adjacent values without the
-// LDS transpose of filter_rows_linear.  Only the words of the payload are loaded (wave-uniform guards).
-__device__ __forceinline__ uint32_t &qword(uint4 &v, int k) { return k == 0 ? v.x : k == 1 ? v.y : k == 2 ? v.z : v.w; }
-__device__ __forceinline__ uint32_t qword(const uint4 &v, int k) { return k == 0 ? v.x : k == 1 ? v.y : k == 2 ? v.z : v.w; }
-__device__ __forceinline__ void load_words(uint4 (&q)[8], const uint8_t *p, uint32_t bytes, int lane) {
-  const __amdgpu_buffer_rsrc_t rs = chunk_rsrc(p, bytes);
-#pragma unroll
-  for (int j = 0; j < 32; ++j)
-    if ((uint32_t)(256 * j) < bytes) qword(q[j >> 2], j & 3) = __builtin_amdgcn_raw_buffer_load_b32(rs, (64 * j + lane) * 4, 0, 0);
-}
-
-// filter_rows_linear over F in word order: per register word the lane's two values are probed (two
-// probe instructions cover 128 consecutive values), ranked with two ballots (the low value first),
-// and written to the same linear stage and 16-B block flush.
-template <bool NEGATE, bool STORE>
-__device__ __forceinline__ int filter_words_linear(const uint4 (&fq)[8], int nf, const uint32_t *s, uint16_t *ob,
-                                                   uint16_t *out, int lane) {
-  static_assert(7 + 512 <= kStageRing, "every slot (pending < 8, + < 512 of a row) lies below the dummies");
-  const int iters = (nf + 511) >> 9; // wave-uniform, <= 8
-  uint32_t tot = 0, flushed = 0;
-  uint4 *out4 = reinterpret_cast<uint4 *>(out);
-  uint4 *ob4 = reinterpret_cast<uint4 *>(ob);
-  typedef __attribute__((address_space(3))) const uint32_t lds_u32;
-  lds_u32 *ls = (lds_u32 *)s;
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    if (i < iters) {
-      uint32_t m[8];
-#pragma unroll
-      for (int k = 0; k < 4; ++k) { // all 8 probes of the row in flight
-        const uint32_t x = qword(fq[i], k);
-        uint32_t wl, wh;
-        asm("v_bfe_u32 %0, %1, 5, 11" : "=v"(wl) : "v"(x));
-        asm("v_bfe_u32 %0, %1, 21, 11" : "=v"(wh) : "v"(x));
-        m[2 * k] = ls[wl];
-        m[2 * k + 1] = ls[wh];
-      }
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const uint32_t x = qword(fq[i], k);
-        const uint32_t bl = __builtin_amdgcn_ubfe(m[2 * k], x, 1u), bh = __builtin_amdgcn_ubfe(m[2 * k + 1], x >> 16, 1u);
-        uint64_t b0 = __builtin_amdgcn_uicmp(bl, 0u, NEGATE ? 32 : 33);
-        uint64_t b1 = __builtin_amdgcn_uicmp(bh, 0u, NEGATE ? 32 : 33);
-        const int lim = nf - 128 * (4 * i + k); // values left from this word's first
-        if (lim < 128) { // lane l holds values 2l, 2l+1 of the 128
-          const int l0 = (lim + 1) >> 1, l1 = lim >> 1;
-          b0 &= l0 > 0 ? (l0 >= 64 ? ~0ull : (1ull << l0) - 1ull) : 0ull;
-          b1 &= l1 > 0 ? (1ull << l1) - 1ull : 0ull;
-        }
-        if (STORE) {
-          const uint32_t p0 = __builtin_amdgcn_mbcnt_hi((uint32_t)(b0 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b0, tot - flushed));
-          const uint32_t p1 = __builtin_amdgcn_mbcnt_hi((uint32_t)(b1 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b1, p0));
-          uint32_t s0, s1; // the high value after the low one when both are kept
-          asm("v_cndmask_b32 %0, %1, %2, %3" : "=v"(s0) : "v"((uint32_t)(kStageRing + lane)), "v"(p1), "s"(b0));
-          const uint32_t ph = p1 + (uint32_t)((b0 >> lane) & 1);
-          asm("v_cndmask_b32 %0, %1, %2, %3" : "=v"(s1) : "v"((uint32_t)(kStageRing + lane)), "v"(ph), "s"(b1));
-          ob[s0] = (uint16_t)x;
-          ob[s1] = (uint16_t)(x >> 16);
-        }
-        tot += (uint32_t)__popcll(b0) + (uint32_t)__popcll(b1);
       }
       if (STORE) {
         wave_lds_sync(); // the blocks hold other lanes' values
@@ -679,46 +419,6 @@ __device__ __forceinline__ void stage_run_toggles(const uint4 (&q)[8], uint32_t 
     }
   }
   wave_lds_sync();
-}
-
-// Two operands into ONE LDS image for the register path's OR / XOR (the caller zeroes it first):
-// an Array's values (ds_or, or ds_xor for the second operand of an XOR: an Array's own values are
-// distinct bits, so the image becomes P | Q or P ^ Q), or a Run's toggles (the second Run's by
-// ds_xor: toggle images are linear under xor, so the prefix-xor of the sum is P ^ Q).
-template <bool XOR>
-__device__ __forceinline__ void scatter_array_chunks(const uint4 (&q)[8], uint32_t card, uint32_t *s, int lane) {
-  const int nchunks = (int)((card + 7) >> 3);
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int c = lane + 64 * i;
-    if (c < nchunks) {
-      const uint32_t x[8] = {q[i].x & 0xFFFF, q[i].x >> 16, q[i].y & 0xFFFF, q[i].y >> 16,
-                             q[i].z & 0xFFFF, q[i].z >> 16, q[i].w & 0xFFFF, q[i].w >> 16};
-      or_chunk_values<XOR>(x, min(8, (int)card - 8 * c), s);
-    }
-  }
-}
-template <bool XOR>
-__device__ __forceinline__ void scatter_run_toggles(const uint4 (&q)[8], uint32_t nruns, uint32_t *s, int lane) {
-  const int nchunks = (int)((nruns + 3) >> 2);
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int c = lane + 64 * i;
-    if (c < nchunks) {
-      const uint32_t r[4] = {q[i].x, q[i].y, q[i].z, q[i].w};
-      uint32_t x[8];
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        x[2 * k] = r[k] & 0xFFFF;
-        x[2 * k + 1] = (r[k] & 0xFFFF) + (r[k] >> 16) + 1;
-      }
-      const int nr = min(4, (int)nruns - 4 * c);
-      int n = 2 * nr;
-      const uint32_t last = nr == 4 ? x[7] : nr == 3 ? x[5] : nr == 2 ? x[3] : x[1];
-      if (last >= (uint32_t)kSpan) --n; // only the container's last run can end at 65535
-      or_chunk_values<XOR>(x, n, s);
-    }
-  }
 }
 
 // Membership image in LDS from a register-preloaded payload (Array <= 4096 values, Run <= 2047
@@ -847,9 +547,6 @@ __device__ __forceinline__ int type_runopt(int c, int r) {
 // ---------------------------------------------------------------- emission
 // Writes the container payload for `type` at `out` (16-B aligned slot); returns payload bytes.
 // `s` is the wave's 8 KiB LDS scratch (free on entry).
-#ifndef RBG_EMIT_ARRAY_PAIRS
-#define RBG_EMIT_ARRAY_PAIRS 0 // 1: two values per trip of the Array emission loop (measured neutral)
-#endif
 __device__ __forceinline__ uint32_t emit_container(int type, const uint64_t (&w)[kW], int card, int runs,
                                                    uint8_t *out, uint32_t *s, int lane) {
   if (type == kBitmap) {
@@ -883,24 +580,10 @@ __device__ __forceinline__ uint32_t emit_container(int type, const uint64_t (&w)
       for (int h = 0; h < 2; ++h) {
         uint64_t x = w[2 * k + h];
         const uint32_t base = (uint32_t)(128 * k + 2 * lane + h) << 6;
-#if RBG_EMIT_ARRAY_PAIRS
-        // two values per trip: a divergent while runs for the lane with the most values of the word
-        while (x) {
-          s16[pos] = (uint16_t)(base + __builtin_ctzll(x));
-          x &= x - 1;
-          if (x) {
-            s16[pos + 1] = (uint16_t)(base + __builtin_ctzll(x));
-            x &= x - 1;
-            ++pos;
-          }
-          ++pos;
-        }
-#else
         while (x) {
           s16[pos++] = (uint16_t)(base + __builtin_ctzll(x));
           x &= x - 1;
         }
-#endif
       }
     }
     wave_lds_sync();

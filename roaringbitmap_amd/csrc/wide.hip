@@ -126,11 +126,7 @@ __global__ __launch_bounds__(256) void k_group_base(const uint32_t *Hc, uint64_t
 // container its rank among the key's containers with one LDS atomic and one barrier; the tile's ids
 // are staged in LDS in (key, member) order, then each key's run of <= 64 ids is stored contiguously.
 // The staged entry is (member u << 8 | thread t): container id = first container of member u in the
-// tile + t, so the stage is 32 KiB of u16 (a u32 stage of the ids, RBG_GROUP_STAGE=1, halves the
-// blocks per CU).
-#ifndef RBG_GROUP_STAGE
-#define RBG_GROUP_STAGE 0
-#endif
+// tile + t, so the stage is 32 KiB of u16 (a u32 stage of the ids halves the blocks per CU).
 // Dense members (every member holds every key of [dense_lo, dense_hi): container = begin + key -
 // dense_lo) need no sort: key k's containers are mbase[j] + k in member order (CidMap), seg[k] =
 // (k - key_lo) * M.  This kernel writes seg and the per-member bases.
@@ -159,11 +155,7 @@ __global__ __launch_bounds__(256) void k_group_scatter(GroupArgs a, const uint64
     if (kk[u] != ~0u) atomicOr(&mask[kk[u]], 1ull << u);
   __syncthreads();
   {
-#if RBG_GROUP_STAGE
-  __shared__ uint32_t stage[kGrpMembers * kGrpKeys];
-#else
   __shared__ uint16_t stage[kGrpMembers * kGrpKeys];
-#endif
   __shared__ uint32_t lofs[kGrpKeys + 1], wsum[4];
   const uint32_t lane = t & 63, wv = t >> 6;
   // tile-local offsets of the keys: exclusive scan of the mask popcounts
@@ -180,14 +172,14 @@ __global__ __launch_bounds__(256) void k_group_scatter(GroupArgs a, const uint64
   for (int u = 0; u < (int)kGrpMembers; ++u)
     if (kk[u] != ~0u)
       stage[lofs[kk[u]] + (uint32_t)__popcll(mask[kk[u]] & ((1ull << u) - 1))] =
-          RBG_GROUP_STAGE ? ci[u] : (uint32_t)(u << 8 | t);
+          (uint32_t)(u << 8 | t);
   __syncthreads();
   // one wave per key at a time: the key's ids in member order, one contiguous store
   for (uint32_t k = wv; k < nk; k += 4) {
     const uint32_t o = lofs[k], n = lofs[k + 1] - o;
     if (lane < n) {
       const uint32_t v = stage[o + lane];
-      cid[gbase[k] + lane] = RBG_GROUP_STAGE ? v : (uint32_t)(mbase[v >> 8] + (v & 255));
+      cid[gbase[k] + lane] = (uint32_t)(mbase[v >> 8] + (v & 255));
     }
   }
   }
@@ -236,9 +228,6 @@ template <int OP> __device__ __forceinline__ void fold(uint64_t (&acc)[kW], cons
 // (16 coalesced 1 KiB loads in flight per wave; four per step measured slower: 6.5-7.1 ms config-3
 // steps vs 6.4-6.6).  Returns algorithmic bytes read.
 template <int OP>
-#ifndef RBG_FOLD_PREFETCH
-#define RBG_FOLD_PREFETCH 1 // the next pair's metadata loads issued before the current pair is folded
-#endif
 __device__ __forceinline__ uint64_t fold_all(const SetView &s, const KeyCids &cid, uint64_t lo, uint64_t hi,
                                              uint64_t (&acc)[kW], uint32_t *lds, int lane) {
   uint64_t bytes = 0;
@@ -253,21 +242,14 @@ __device__ __forceinline__ uint64_t fold_all(const SetView &s, const KeyCids &ci
       uint64_t x[kW], y[kW];
       load_bitmap(r0.p, x, lane);
       load_bitmap(r1.p, y, lane);
-#if RBG_FOLD_PREFETCH
       // the next pair's metadata is in flight while this pair's payloads arrive
       const CRef n0 = i + 2 < hi ? cref(s, cid[i + 2]) : r0;
       const CRef n1 = i + 3 < hi ? cref(s, cid[i + 3]) : r0;
-#endif
       fold<OP>(acc, x);
       fold<OP>(acc, y);
       i += 2;
-#if RBG_FOLD_PREFETCH
       r0 = n0;
       r1 = n1;
-#else
-      if (i < hi) r0 = cref(s, cid[i]);
-      if (i + 1 < hi) r1 = cref(s, cid[i + 1]);
-#endif
       continue;
     }
     bytes += alg_bytes_w(r0.type, r0.card, r0.nruns) + 16;

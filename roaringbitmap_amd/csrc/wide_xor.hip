@@ -39,9 +39,6 @@ namespace {
 constexpr int kXB = 32;         // containers per batch (2 lanes per container, 4 runs per lane)
 constexpr int kXRegion = 1280;  // u32 per wave: pre16 (1024) | then MC (1024) + pos (256)
 constexpr uint32_t kNoKey = 0xFFFFFFFFu;
-#ifndef RBG_XOR_APPLY_FLAT
-#define RBG_XOR_APPLY_FLAT 0 // 1: one flattened loop over the odd intervals (measured slower: 42.8 vs 35.8 ms)
-#endif
 
 template <int CTRL> __device__ __forceinline__ uint32_t dpp_mov(uint32_t v) {
   return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xf, 0xf, false);
@@ -514,13 +511,7 @@ __device__ __forceinline__ void pair_xor(XWin &w) {
   const int inter = w.nr ? max(0, min(ea, eb) - max(sa, sb) + 1) : 0;
   w.pairx = w.card + cb - 2u * (uint32_t)inter;
 }
-#ifndef RBG_XF_ABLATE
-#define RBG_XF_ABLATE 0 // timing study only (wrong results): 1 no toggles, 2 no prefix-xor, 4 no re-measure, 8 no pair bound,
-                        // 16 no window loads after the first
-#endif
-#ifndef RBG_XOR_MIN_FAST
-#define RBG_XOR_MIN_FAST 8 // shortest stretch worth a fast-forward (an exact batch costs ~32 stretches' steps)
-#endif
+constexpr int kXorMinFast = 8; // shortest stretch worth a fast-forward (an exact batch costs ~32 stretches' steps)
 // Union stretches.  The pair bounds above limit an AB stretch to about one window when the members'
 // XOR can reach the accumulator's size (config 4: |C ⊕ C'| ~ 900 per pair, ~29k per window against
 // c ~ 32k), so every window paid a toggle -> word conversion and a re-measure (~600 of ~1100 VALU per
@@ -531,14 +522,9 @@ __device__ __forceinline__ void pair_xor(XWin &w) {
 // per run).  While |P \ U'| >= 32 every step of an AB-typed accumulator is AB(c_j) (c_j >= 32, never
 // empty), so the windows' toggles accumulate in the toggle image with no conversion at all; the stretch
 // closes (one conversion, one re-measure of c) when the next window would push |P \ U'| below 32.
-#ifndef RBG_XOR_UNION
-#define RBG_XOR_UNION 1
-#endif
-#ifndef RBG_XOR_TRACE
-#define RBG_XOR_TRACE 0 // 1: per-key stretch counts of three keys (printf; study builds only)
-#endif
-#ifndef RBG_XOR_UNION_MIN_C
-#define RBG_XOR_UNION_MIN_C 1024 // try a union stretch only above this c (a heuristic: results do not depend on it)
+constexpr int kXorUnionMinC = 1024; // try a union stretch only above this c (a heuristic: results do not depend on it)
+#ifndef RBG_STUDY
+#define RBG_STUDY 0 // study builds: per-key stretch counts of three keys (printf)
 #endif
 
 __global__ __launch_bounds__(256, 3) void k_wide_runs_xor(SetView s, const uint64_t *__restrict__ rec,
@@ -588,7 +574,7 @@ __global__ __launch_bounds__(256, 3) void k_wide_runs_xor(SetView s, const uint6
   bool urun = false; // flavour of the pending stretch: Run (every step stays a Run) or AB
   int usum = 0;      // Run flavour: Σ nruns of the pending windows (r_j <= X.r + usum)
   bool wpx = true;   // W.pairx is current
-#if RBG_XOR_TRACE
+#if RBG_STUDY
   int tr_u = 0, tr_f = 0, tr_rej = 0, tr_p = 0, tr_pb = 0, tr_e = 0;
 #define RBG_TR(x) x
 #else
@@ -623,13 +609,13 @@ __global__ __launch_bounds__(256, 3) void k_wide_runs_xor(SetView s, const uint6
     }
     const uint32_t wlen = (uint32_t)min<uint64_t>(64, hi - wbase); // containers in the window
     // window's Σ nruns (the Run flavour's r bound); a Run stretch needs 2 + 4 r_j <= min(8192, 2 c_j + 2)
-    const int wnr = RBG_XOR_UNION && fastfwd && posw == 0 && (upend ? urun : X.state == kRun)
+    const int wnr = fastfwd && posw == 0 && (upend ? urun : X.state == kRun)
                         ? (int)wave_sum_u32((uint32_t)lane < wlen ? W.nr : 0u) : 0;
-    const bool ab_in = X.state == kBitmap || (X.state == kArray && X.c >= RBG_XOR_UNION_MIN_C);
-    const bool run_in = X.state == kRun && X.rvalid && X.c >= RBG_XOR_UNION_MIN_C &&
+    const bool ab_in = X.state == kBitmap || (X.state == kArray && X.c >= kXorUnionMinC);
+    const bool run_in = X.state == kRun && X.rvalid && X.c >= kXorUnionMinC &&
                         X.r + wnr <= 2047 && X.c >= 4 * (X.r + wnr); // |P \ U'| ~ c / 2 after a window
-    if (RBG_XOR_UNION && fastfwd && posw == 0 && (upend || ab_in || run_in)) {
-      // ---- union stretch: mark the window's words, then |P \ U'| decides (see RBG_XOR_UNION)
+    if (fastfwd && posw == 0 && (upend || ab_in || run_in)) {
+      // ---- union stretch: mark the window's words, then |P \ U'| decides (see "Union stretches" above)
       const bool mem = (uint32_t)lane < wlen;
       if (!upend) { // a new stretch: clear U', and the per-word popcounts of P for |P \ U'|
         urun = !ab_in;
@@ -737,8 +723,8 @@ __global__ __launch_bounds__(256, 3) void k_wide_runs_xor(SetView s, const uint6
     const uint64_t okm = __ballot(ok) >> posw;
     // leading members within the bounds (all 64 when posw == 0 and ~okm == 0: ctz of 0 is undefined)
     const uint32_t B = fastfwd ? min(~okm ? (uint32_t)__builtin_ctzll(~okm) : 64u, wlen - posw) : 0u;
-    if (B >= RBG_XOR_MIN_FAST || (B >= 1 && posw + B == wlen)) {
-      if (!(RBG_XF_ABLATE & 1) && (uint32_t)lane >= posw && (uint32_t)lane < posw + B) {
+    if (B >= kXorMinFast || (B >= 1 && posw + B == wlen)) {
+      if ((uint32_t)lane >= posw && (uint32_t)lane < posw + B) {
         const uint32_t rw[8] = {W.r0.x, W.r0.y, W.r0.z, W.r0.w, W.r1.x, W.r1.y, W.r1.z, W.r1.w};
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
@@ -755,13 +741,13 @@ __global__ __launch_bounds__(256, 3) void k_wide_runs_xor(SetView s, const uint6
       lds_read_words(acc, t, lane);
       wave_lds_sync();
       lds_zero(acc, lane);
-      if (!(RBG_XF_ABLATE & 2)) toggles_to_words(t, lane);
+      toggles_to_words(t, lane);
 #pragma unroll
       for (int j = 0; j < kW; ++j) Pw[j] ^= t[j];
       // an AB stretch leaves a Bitmap / Array accumulator whose next rule reads only c (AB), so r is
       // counted again only when a rule can read it (Run stretch, exact batch, the result)
       int cc = X.c, rr = X.r;
-      if (!(RBG_XF_ABLATE & 4)) metrics(Pw, lane, mode == 2, cc, rr);
+      metrics(Pw, lane, mode == 2, cc, rr);
       X.c = cc;
       X.r = rr;
       X.rvalid = mode == 2;
@@ -790,11 +776,9 @@ __global__ __launch_bounds__(256, 3) void k_wide_runs_xor(SetView s, const uint6
     wave_lds_sync();
     if (base >= wbase + 64 && base < hi) {
       wbase += 64;
-      if (!(RBG_XF_ABLATE & 16)) {
-        W = N;
-        N = xwin_from(s, xmeta_of(NN, wbase + 64 + lane < hi));
-        NN = rec_at(wbase + 128 + lane);
-      }
+      W = N;
+      N = xwin_from(s, xmeta_of(NN, wbase + 64 + lane < hi));
+      NN = rec_at(wbase + 128 + lane);
       wpx = false;
     }
   }
@@ -806,7 +790,7 @@ __global__ __launch_bounds__(256, 3) void k_wide_runs_xor(SetView s, const uint6
     RBG_TR(++tr_f);
     flush_union();
   }
-#if RBG_XOR_TRACE
+#if RBG_STUDY
   if (lane == 0 && (q == 1000 || q == 30000 || q == 65000))
     printf("xor trace key %u: union windows %d flushes %d refused %d | per-window stretches %d (members %d) | exact %d | c %d state %d\n",
            q, tr_u, tr_f, tr_rej, tr_p, tr_pb, tr_e, X.c, X.state);

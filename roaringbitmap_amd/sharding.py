@@ -214,7 +214,15 @@ class ShardedWide:
         sm = members[int(np.argmin(tot))]  # argmin: the first minimal one
         return [sm] + [m for m in members if m != sm]
 
+    def check_semantics(self, sem: int) -> None:
+        """priorityqueue_or / _xor merge in the order of intermediate result sizes, which are global:
+        a key-range shard cannot follow it.  Every rank raises alike (the arguments agree), before any
+        collective, as rbgpu_wide_sharded refuses them."""
+        if self.world > 1 and sem in (L.PQ_OR, L.PQ_XOR):
+            raise ValueError("priorityqueue_or / priorityqueue_xor cannot be key-range sharded")
+
     def aggregate(self, ctx, sem: int, dset, key_range: Tuple[int, int], members=None) -> ShardResult:
+        self.check_semantics(sem)
         mem = list(range(len(dset))) if members is None else [int(m) for m in members]
         if sem == L.NAIVE_AND or (sem == L.FAST_AND and len(mem) <= 10):
             order = self.naive_and_order(dset.range_counts(mem, key_range), mem)
@@ -298,8 +306,9 @@ class ShardedPairwise:
         bi = np.ascontiguousarray(b_idx[lo:hi], np.uint32)
         local = ctx.pairwise(op, a, b, ai, bi)
         st = ctx.stats()
+        # output_bytes counts 16 B of metadata per result container beside the payloads
         return self.finish(local, (lo, hi), st["result_cardinality"], st["result_containers"],
-                           st["output_bytes"])
+                           st["output_bytes"] - 16 * st["result_containers"])
 
     def gather_serialized(self, res: PairShardResult, dst: int = 0) -> Optional[List[bytes]]:
         """Every result's RoaringFormatSpec bytes, in batch order, on rank `dst` (None elsewhere)."""

@@ -49,3 +49,40 @@ def test_comm_bsi_sharded_and_allreduce(ctx, oracle, comm):
         assert comm.gather_serialized(local, summ) == want
     v = comm.allreduce_sum([1, 2, 3, 2**40])
     assert list(v) == [1, 2, 3, 2**40]
+
+
+def test_range_counts_partition_sum_gives_whole_order(ctx):
+    """the sharded naive_and fold order comes from the per-range counts summed over the
+    ranks (rbgpu_wide_sharded's all-reduce); over every partition the sums must equal the whole-range
+    counts, so every shard folds the order the unsharded call folds (FastAggregation.java:328-346)."""
+    from roaringbitmap_amd.sharding import partition_keys
+    vals = load_realdata("census1881_srt")[:30] + synthetic_bitmaps(20, seed=11, max_keys=30, key_space=200)
+    s = ctx.upload_values(vals, run_optimize=True)
+    whole = s.range_counts()
+    kb = s.key_bytes()
+    for nparts in (2, 3, 5, 8):
+        parts = partition_keys(kb, nparts)
+        tot = sum(s.range_counts(None, p) for p in parts)
+        assert np.array_equal(tot, whole), nparts
+        mem = list(range(len(s)))
+        sm = int(np.argmin(tot))
+        assert [sm] + [m for m in mem if m != sm] == [int(np.argmin(whole))] + \
+            [m for m in mem if m != int(np.argmin(whole))]
+
+
+def test_comm_errors_are_collective(ctx, comm):
+    """A bad argument on one rank fails the call on that rank without a dangling collective (world 1:
+    the call returns instead of waiting); the communicator stays usable afterwards."""
+    import ctypes as C
+
+    import roaringbitmap_amd as rb
+    from roaringbitmap_amd import _lib as L
+    s = ctx.upload_values(synthetic_bitmaps(6, seed=2, max_keys=5, key_space=10), run_optimize=True)
+    local, summ = comm.wide_sharded(rb.FAST_OR, s, (0, 65536))
+    ss = L.RbShardSummary(**summ)
+    rc = L.lib().rbgpu_shard_gather_serialized(comm.h, local.h, C.byref(ss), 0, None, 0)
+    assert rc == L.RB_EINVAL
+    assert comm.gather_serialized(local, summ) == ctx.wide(rb.FAST_OR, s).serialize()[0]
+    # priorityqueue_or is a whole-result call: allowed at world size 1 over the whole key range
+    pl, ps = comm.wide_sharded(rb.PQ_OR, s, (0, 65536))
+    assert comm.gather_serialized(pl, ps) == ctx.wide(rb.PQ_OR, s).serialize()[0]

@@ -280,3 +280,38 @@ def _rank_pairs(rank, world, port, q):
 def test_gloo_two_rank_sharded_pairwise():
     for name, ok in _spawn(_rank_pairs).items():
         assert all(ok), (name, ok)
+
+
+def _rank_pq_refused(rank, world, port, q):
+    import torch.distributed as dist
+
+    from roaringbitmap_amd.sharding import ShardedWide
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        # every byte on key 65535: partition_keys gives rank 0 the whole range, rank 1 an empty one
+        kb = np.zeros(65536, np.uint64)
+        kb[65535] = 100
+        key_range = partition_keys(kb, world)[rank]
+        sw = ShardedWide(dist, rank, world)
+        raised = {}
+        for sem in (L.PQ_OR, L.PQ_XOR):
+            try:
+                sw.aggregate(None, sem, [object()], key_range)  # refused before touching ctx / dset
+                raised[sem] = False
+            except ValueError:
+                raised[sem] = True
+        dist.barrier()  # both ranks reach here: no rank waits in a collective
+        g = sw._all_gather_i64([int(all(raised.values()))])
+        if rank == 0:
+            q.put({"raised": bool(g[:, 0].all()), "ranges": partition_keys(kb, world)})
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_two_rank_pq_refused_on_every_rank():
+    """priorityqueue_or / _xor are refused alike on every rank (no rank left waiting)."""
+    out = _spawn(_rank_pq_refused)
+    assert out["raised"]
+    assert out["ranges"] == [(0, 65536), (65536, 65536)]
