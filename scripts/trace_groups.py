@@ -22,18 +22,25 @@ for (name, grid), d in sorted(groups.items(), key=lambda kv: -sum(e - s for s, e
     big = [x for x in durs if x >= 0.5 * max(durs)]  # the headline-size dispatches of the group
     print(f"{name:45s} {grid:9d} {len(d):4d} {sum(durs) / len(durs):9.4f} {min(durs):9.4f} {len(big):5d} "
           f"{sum(big) / len(big):10.4f}")
-# union spans of the concurrent light/heavy pair (dispatches that overlap in time)
-lt = sorted(x for (n, g), v in groups.items() if n.endswith("0>") and "k_pair_tasks" in n for x in v)
-hv = sorted(x for (n, g), v in groups.items() if n.endswith("1>") and "k_pair_tasks" in n for x in v)
-spans = []
-for s2, e2 in hv:
-    # the light launch beside the heavy kernel, and the second light launch that starts on the side
-    # stream when the heavy kernel ends (both take tasks from one queue)
-    ph = [(s, e) for s, e in lt if s < e2 + 50_000 and e > s2]
-    if ph:
-        spans.append((max([e2] + [e for _, e in ph]) - min([s2] + [s for s, _ in ph])) / 1e6)
-if spans:
-    big = [x for x in spans if x >= 0.5 * max(spans)]
-    print(f"  headline-size spans: n={len(big)} avg_ms={sum(big) / len(big):.4f}")
-    print(f"concurrent light||heavy union spans: n={len(spans)} avg_ms={sum(spans) / len(spans):.4f} "
-          f"min_ms={min(spans):.4f}")
+# union spans of one call's task phase, per op (the template's first argument: 0 AND, 1 OR, 2 XOR,
+# 3 ANDNOT): every light and heavy dispatch of the op, clustered by overlap (a dispatch that starts
+# within 50 us of the cluster's end joins it), so the two launches of each kind count once per call
+OPS = {"0": "AND", "1": "OR", "2": "XOR", "3": "ANDNOT"}
+for opk, opname in OPS.items():
+    ds = sorted(x for (n, g), v in groups.items() if "k_pair_tasks<" + opk + "," in n for x in v)
+    spans, cur = [], None
+    for st, en in ds:
+        if cur and st <= cur[1] + 50_000:
+            cur[1] = max(cur[1], en)
+        else:
+            if cur:
+                spans.append((cur[1] - cur[0]) / 1e6)
+            cur = [st, en]
+    if cur:
+        spans.append((cur[1] - cur[0]) / 1e6)
+    if not spans:
+        continue
+    big = sorted(x for x in spans if x >= 0.5 * max(spans))
+    med = big[len(big) // 2]
+    print(f"{opname:6s} task-phase union spans (headline-size calls): n={len(big)} median_ms={med:.4f} "
+          f"avg_ms={sum(big) / len(big):.4f} min_ms={min(big):.4f} max_ms={max(big):.4f}")
