@@ -73,9 +73,30 @@ enum rb_wide_sem {
                             lazily OR'd on the device (lazyor / in-place lazyor / lazyorfromlazyinputs by
                             which operands are temporaries), re-queued, the survivor repaired
                             FastAggregation.java:675-721 (whole result only: no key range) */
-  RB_PQ_XOR = 11         /* FastAggregation.priorityqueue_xor: the two smallest bitmaps (getLongSizeInBytes)
+  RB_PQ_XOR = 11,        /* FastAggregation.priorityqueue_xor: the two smallest bitmaps (getLongSizeInBytes)
                             replaced by their RoaringBitmap.xor, on the device, until one is left
                             FastAggregation.java:732-752 (whole result only: no key range) */
+  /* buffer/ front end: BufferFastAggregation over ImmutableRoaringBitmap / MutableRoaringBitmap runs the
+   * same container algebra; these are its entry points whose results differ from FastAggregation's
+   * (paths under buffer/).  The others map onto the values above:
+   *   and(ImmutableRoaringBitmap...), and(long[], Immutable...)     RB_FAST_AND   BufferFastAggregation.java:29-58
+   *   and(Iterator), and(long[], Iterator), and(MutableRoaringBitmap...), workShyAnd,
+   *   workAndMemoryShyAnd                                             RB_WORKSHY_AND          :67-108, 423-675
+   *   naive_and(ImmutableRoaringBitmap...)                            RB_NAIVE_AND            :348-370
+   *   naive_and(Iterator), naive_and(MutableRoaringBitmap...)         RB_NAIVE_AND_ITER       :384-418
+   *   naive_or / or(Immutable... / Iterator), horizontal_or(Iterator) RB_FAST_OR             :675-692, 776-790, 246-249
+   *   naive_xor / xor (every overload)                                RB_FAST_XOR             :728-768, 962-990
+   *   horizontal_or / horizontal_xor(Immutable... / Mutable...)       RB_HORIZONTAL_OR / _XOR :188-244, 259-337
+   */
+  RB_BUFFER_NAIVE_OR = 12,   /* naive_or / or(MutableRoaringBitmap...): answer.lazyor(b) per bitmap, then
+                                repairAfterLazy — per key the lazyIOR chain from a clone of the first
+                                container, for any count (ParallelAggregation.or switches at 16)  :711-717, 797-799 */
+  RB_BUFFER_PQ_OR = 13,      /* priorityqueue_or(ImmutableRoaringBitmap...): the lazy merges of RB_PQ_OR ordered
+                                by serializedSizeInBytes; one bitmap comes back as a copy (no repair)  :810-866 */
+  RB_BUFFER_PQ_OR_ITER = 14, /* priorityqueue_or(Iterator): ordered by ImmutableRoaringBitmap.getLongSizeInBytes
+                                (a lazy Bitmap counts 2 bytes: getCardinality() is -1); one bitmap: a copy  :869-930 */
+  RB_BUFFER_PQ_XOR = 15      /* priorityqueue_xor: RB_PQ_XOR ordered by ImmutableRoaringBitmap.getLongSizeInBytes;
+                                fewer than 2 bitmaps -> RB_EINVAL (IllegalArgumentException)  :933-958 */
 };
 
 /* Host-side SoA description of a batch of bitmaps (used for upload and download). */
@@ -174,17 +195,35 @@ int rbgpu_set_range_counts(const rbgpu_set *set, const uint32_t *members, uint32
 int rbgpu_set_download(const rbgpu_set *set, uint32_t first, uint32_t count, rb_soa *soa);
 
 /* ---- pairwise set algebra (static RoaringBitmap ops) ------------------------------- */
+/* An a_idx / b_idx entry equal to RB_EMPTY_BITMAP stands for an empty bitmap (no containers): op with
+ * it clones the other side's containers (or, xor, andNot with an empty right side) or gives nothing. */
+#define RB_EMPTY_BITMAP 0xFFFFFFFFu
 /* result[i] = op(a[a_idx[i]], b[b_idx[i]]); a_idx / b_idx may be NULL (identity).
  * RoaringBitmap.and/or/xor/andNot — RoaringBitmap.java:377-401, 860-902, 1071-1118, 444-473 */
 int rbgpu_pairwise(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu_set *b,
                    const uint32_t *a_idx, const uint32_t *b_idx, uint32_t npairs, rbgpu_set **out);
+/* In-place x1.op(x2): result[i] = a[a_idx[i]] after a[a_idx[i]].and/or/xor/andNot(b[b_idx[i]]) —
+ * RoaringBitmap.and(x2) :1270-1296, or(x2) :2481-2523, xor(x2) :3296-3348, andNot(x2) :1346-1382.
+ * The container algebra is the static one (Container.iand / iandNot / ixor return the static ops' types)
+ * except x1.or(x2)'s BitmapContainer.ior(ArrayContainer), which keeps a Bitmap even when it fills up
+ * (BitmapContainer.java:749-766; the static or() gives a full Run).  A pair whose operands are the
+ * same bitmap object (a == b and a_idx[i] == b_idx[i]) follows the `x2 == this` branches: and / or
+ * leave x1 as it is, xor / andNot clear it.  Inputs stay unchanged (results are new sets). */
+int rbgpu_pairwise_inplace(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu_set *b,
+                           const uint32_t *a_idx, const uint32_t *b_idx, uint32_t npairs, rbgpu_set **out);
 /* RoaringBitmap.andCardinality/orCardinality/xorCardinality/andNotCardinality
  * — RoaringBitmap.java:413-434, 916-920, 931-933, 944-985 */
 int rbgpu_pairwise_cardinality(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu_set *b,
                                const uint32_t *a_idx, const uint32_t *b_idx, uint32_t npairs,
                                uint64_t *out /* [npairs] */);
 
-/* ---- wide aggregation over members[0..n) of `in` (NULL = all bitmaps, in order) ------ */
+/* ---- wide aggregation over members[0..n) of `in` (NULL = all bitmaps, in order) ------
+ * A repeated member index is the same bitmap object (naive_and skips its smallest member by identity,
+ * FastAggregation.java:337-341).  The long[] aggregation-buffer overloads (FastAggregation.and(long[],
+ * RoaringBitmap...) :51-63, workAndMemoryShyAnd :477-514) take no buffer here: the caller checks the
+ * reference's "buffer should have at least 1024 elements" IllegalArgumentException (more than 10
+ * bitmaps for and(long[], ...), always for workAndMemoryShyAnd) and zero-fills it; the results are
+ * RB_FAST_AND / RB_WORKSHY_AND.  priorityqueue_or(Iterator) (:615-664) is RB_PQ_OR. */
 int rbgpu_wide(rbgpu_ctx *ctx, int sem, const rbgpu_set *in, const uint32_t *members, uint32_t n,
                rbgpu_set **out);
 /* The same aggregation restricted to high keys in [key_lo, key_hi): one key-range shard of it.
@@ -220,6 +259,12 @@ int rbgpu_bsi_compare(rbgpu_ctx *ctx, const rbgpu_set *bsi, int op, uint64_t sta
 int rbgpu_bsi_compare_keys(rbgpu_ctx *ctx, const rbgpu_set *bsi, int op, uint64_t start_or_value, uint64_t end,
                            uint64_t min_value, uint64_t max_value, const rbgpu_set *found, uint32_t key_lo,
                            uint32_t key_hi, rbgpu_set **out);
+/* RoaringBitmap.runOptimize (RoaringBitmap.java:2764-2775) of every bitmap of `in` into a new set:
+ * each Array / Bitmap container becomes a Run when that is strictly smaller, each Run goes through
+ * toEfficientContainer (ArrayContainer.java:1085-1099, BitmapContainer.java:1227-1246,
+ * RunContainer.java:2326-2335).  any_run[n_bitmaps] (may be NULL) receives runOptimize's return value
+ * per bitmap (1 when the bitmap holds a Run container afterwards). */
+int rbgpu_set_run_optimize(const rbgpu_set *in, rbgpu_set **out, uint8_t *any_run);
 /* RoaringBitmap.clone of bitmaps [first, first+count) into a new set (device copy). */
 int rbgpu_set_extract(const rbgpu_set *set, uint32_t first, uint32_t count, rbgpu_set **out);
 
@@ -247,6 +292,47 @@ int rbgpu_generate_bsi_keys(rbgpu_ctx *ctx, uint32_t nslices, uint64_t nrows, ui
  * RoaringBitmapWriter(runCompress=true) does (ContainerAppender.java:130-137). */
 int rbgpu_generate(rbgpu_ctx *ctx, int workload, uint32_t n, uint64_t seed, rbgpu_set **a,
                    rbgpu_set **b);
+
+/* ---- 64-bit bitmaps (longlong/): Roaring64NavigableMap and Roaring64Bitmap ----------------------
+ * A 64-bit bitmap is a list of buckets (high 32 bits, 32-bit RoaringBitmap of the low halves) in
+ * ascending unsigned order: Roaring64NavigableMap's highToBitmap (default unsigned comparator) and
+ * Roaring64Bitmap's 48-bit ART keys grouped by their high 32 bits.  Bytes cross the boundary in the
+ * RoaringFormatSpec 64-bit extension ("portable": u64 bucket count, then per bucket u32 high and the
+ * 32-bit RoaringBitmap), Roaring64NavigableMap.serializePortable / deserializePortable
+ * (longlong/Roaring64NavigableMap.java:1254-1261).  The bucket algebra is the 32-bit engine's: one
+ * batched pairwise call per batch of 64-bit pairs. */
+typedef struct rbgpu_set64 rbgpu_set64;
+enum rb64_flavor {
+  RB64_BITMAP = 0,   /* Roaring64Bitmap: static and/or/xor/andNot(x1, x2) (longlong/Roaring64Bitmap.java:345-390,
+                        421-460, 497-517, 630-650) and in place x1.op(x2) (:319-343, 392-419, 468-495, 599-628):
+                        per 48-bit key the container op (in place: iand / ior / ixor / iandNot), an empty and /
+                        andNot result removed, an empty xor result KEPT (the reference stores it unchecked) */
+  RB64_NAVIGABLE = 1 /* Roaring64NavigableMap in place x1.and/or/xor/andNot(x2) (longlong/Roaring64NavigableMap.java:
+                        773-977): per bucket the 32-bit RoaringBitmap's in-place op; a bucket left empty stays */
+};
+/* n 64-bit bitmaps from portable bytes (RB_EFORMAT: truncated / bad bucket; RB_EINVAL: bucket highs
+ * not strictly increasing — the reference's TreeMap would reorder them). */
+int rbgpu_set64_from_portable(rbgpu_ctx *ctx, const uint8_t *const *bufs, const uint64_t *lens, uint32_t n,
+                              rbgpu_set64 **out);
+/* n 64-bit bitmaps from a 32-bit set of their buckets: bitmap i is buckets [begin[i], begin[i+1]) of
+ * `buckets` with highs[begin[i]..] (begin[n] == bitmaps of `buckets`); the buckets are copied. */
+int rbgpu_set64_from_buckets(const rbgpu_set *buckets, const uint32_t *highs, const uint64_t *begin, uint32_t n,
+                             rbgpu_set64 **out);
+void rbgpu_set64_free(rbgpu_set64 *set);
+uint32_t rbgpu_set64_bitmap_count(const rbgpu_set64 *set);
+/* bucket highs of bitmap i (up to cap of them into highs, may be NULL); *count = its bucket count */
+int rbgpu_set64_buckets(const rbgpu_set64 *set, uint32_t i, uint32_t *highs, uint64_t cap, uint64_t *count);
+/* getLongCardinality per bitmap */
+int rbgpu_set64_cardinalities(const rbgpu_set64 *set, uint64_t *out);
+/* portable serialized size per bitmap, and the bytes of bitmaps [first, first+count) back to back */
+int rbgpu_set64_portable_sizes(const rbgpu_set64 *set, uint64_t *out);
+int rbgpu_set64_serialize_portable(const rbgpu_set64 *set, uint32_t first, uint32_t count, uint8_t *dst,
+                                   uint64_t cap, uint64_t *offsets);
+/* result[i] = op(a[a_idx[i]], b[b_idx[i]]) with flavor's rules; inplace != 0: the state of a[a_idx[i]]
+ * after a[a_idx[i]].op(b[b_idx[i]]) (same set and index on both sides: the `x2 == this` branches).
+ * RB64_NAVIGABLE needs inplace (the class has no static and/or/xor/andNot). */
+int rbgpu_pairwise64(rbgpu_ctx *ctx, int flavor, int op, int inplace, const rbgpu_set64 *a, const rbgpu_set64 *b,
+                     const uint32_t *a_idx, const uint32_t *b_idx, uint32_t npairs, rbgpu_set64 **out);
 
 /* ---- multi-GPU: one process (or host thread) per GPU, RCCL over xGMI ------------------------
  * The reference scales one JVM over a ForkJoin pool (ParallelAggregation.java:161-195, keys

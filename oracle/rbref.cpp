@@ -841,6 +841,24 @@ BM *bm_or_xor(const BM &a, const BM &b, bool is_xor) {
   for (; j < b.size(); ++j) { out->keys.push_back(b.keys[j]); out->vals.push_back(b.vals[j]); }
   return out;
 }
+// Roaring64Bitmap.xor (longlong/Roaring64Bitmap.java:421-460 static, :392-419 in place) stores each
+// matched key's xor result without an isEmpty check: an empty container stays under its key.
+BM *bm_xor_keep_empty(const BM &a, const BM &b) {
+  BM *out = new BM;
+  size_t i = 0, j = 0;
+  while (i < a.size() && j < b.size()) {
+    if (a.keys[i] == b.keys[j]) {
+      out->keys.push_back(a.keys[i]); out->vals.push_back(c_xor(a.vals[i], b.vals[j])); ++i; ++j;
+    } else if (a.keys[i] < b.keys[j]) {
+      out->keys.push_back(a.keys[i]); out->vals.push_back(a.vals[i]); ++i;
+    } else {
+      out->keys.push_back(b.keys[j]); out->vals.push_back(b.vals[j]); ++j;
+    }
+  }
+  for (; i < a.size(); ++i) { out->keys.push_back(a.keys[i]); out->vals.push_back(a.vals[i]); }
+  for (; j < b.size(); ++j) { out->keys.push_back(b.keys[j]); out->vals.push_back(b.vals[j]); }
+  return out;
+}
 // RoaringBitmap.andNot(x1, x2) (:444-473)
 BM *bm_andnot(const BM &a, const BM &b) {
   BM *out = new BM;
@@ -1309,6 +1327,105 @@ BM *wide_pq_xor(const BM *const *bs, size_t n) {
   return new BM(pool[pq.poll()]);
 }
 
+// ---- buffer/ (BufferFastAggregation over Immutable/MutableRoaringBitmap): the same container
+// algebra (the Mappeable* containers restate the Container rules), three entry points that differ.
+// ImmutableRoaringBitmap.getLongSizeInBytes (buffer/ImmutableRoaringBitmap.java:1508-1521) with
+// BufferUtil.getSizeInBytesFromCardinalityEtc (buffer/BufferUtil.java:512-524): 4, then per container
+// 4 + (Run: 2 + 4r; else getCardinality() > 4096 ? 8192 : 2 * getCardinality()).  A lazy Bitmap's
+// getCardinality() is -1 (MappeableBitmapContainer.java:540-542), so it counts 4 - 2 bytes.
+int64_t bm_size_immutable(const BM &b) {
+  int64_t s = 4;
+  for (const Cont &c : b.vals) {
+    const int64_t card = c.t == kB && c.card < 0 ? -1 : (int64_t)cardinality(c);
+    s += 4 + (c.t == kR ? 2 + 4 * (int64_t)c.nruns() : card > kMaxArray ? 8192 : 2 * card);
+  }
+  return s;
+}
+// ImmutableRoaringBitmap.serializedSizeInBytes = MutableRoaringArray.serializedSizeInBytes
+// (buffer/MutableRoaringArray.java:756-764): headerSize + getArraySizeInBytes per container (a Bitmap
+// 8192 whether lazy or not, MappeableBitmapContainer.java:533-535).
+int64_t bm_serialized_size_lazy(const BM &b) {
+  const uint64_t n = b.size();
+  bool hr = false;
+  int64_t s = 0;
+  for (const Cont &c : b.vals) {
+    hr |= c.t == kR;
+    s += c.t == kA ? 2 * (int64_t)c.card : c.t == kB ? 8192 : 2 + 4 * (int64_t)c.nruns();
+  }
+  return s + (int64_t)(hr ? (n < 4 ? 4 + (n + 7) / 8 + 4 * n : 4 + (n + 7) / 8 + 8 * n) : 8 + 8 * n);
+}
+// BufferFastAggregation.naive_or(MutableRoaringBitmap...) / or(MutableRoaringBitmap...)
+// (buffer/BufferFastAggregation.java:711-717, 797-799): an empty answer, answer.lazyor(b) per bitmap
+// (MutableRoaringBitmap.lazyor, buffer/MutableRoaringBitmap.java:1309-1352: matched keys lazyIOR, new
+// keys cloned in), then repairAfterLazy.  Per key: a clone of the first container, the lazyIOR chain
+// over the rest — ParallelAggregation.or's short chain without its 16-container switch.
+BM *wide_buffer_naive_or(const BM *const *bs, size_t n) {
+  BM acc;
+  for (size_t k = 0; k < n; ++k) acc = bm_lazyor_inplace(acc, *bs[k], false);
+  BM *out = new BM(std::move(acc));
+  for (Cont &c : out->vals) c = repair(std::move(c));
+  return out;
+}
+// BufferFastAggregation.priorityqueue_or (buffer/BufferFastAggregation.java:810-866 varargs,
+// :869-930 Iterator): FastAggregation.priorityqueue_or's lazy merges ordered by another size — the
+// varargs form by serializedSizeInBytes (an int), the Iterator form by ImmutableRoaringBitmap.
+// getLongSizeInBytes — and a single bitmap comes back as a copy (toMutableRoaringBitmap, no repair).
+template <class Size> BM *wide_pq_or_sized(const BM *const *bs, size_t n, Size size, bool single_copy) {
+  if (n == 0) return new BM;
+  if (n == 1 && single_copy) return new BM(*bs[0]);
+  std::vector<BM> buffer(n);
+  for (size_t k = 0; k < n; ++k) buffer[k] = *bs[k];
+  std::vector<int64_t> sizes(n);
+  std::vector<char> istmp(n, 0);
+  for (size_t k = 0; k < n; ++k) sizes[k] = size(buffer[k]);
+  auto cmp = [&](int a, int b) { return (int)(sizes[a] - sizes[b]); };
+  JavaPQ<int, decltype(cmp)> pq(cmp);
+  for (size_t k = 0; k < n; ++k) pq.offer((int)k);
+  while (pq.size() > 1) {
+    const int x1 = pq.poll(), x2 = pq.poll();
+    if (istmp[x1] && istmp[x2]) {        // MutableRoaringBitmap.lazyorfromlazyinputs (:522-570)
+      buffer[x1] = bm_lazyor_inplace(buffer[x1], buffer[x2], true);
+      sizes[x1] = size(buffer[x1]);
+      pq.offer(x1);
+    } else if (istmp[x2]) {              // ((MutableRoaringBitmap) x2).lazyor(x1)
+      buffer[x2] = bm_lazyor_inplace(buffer[x2], buffer[x1], false);
+      sizes[x2] = size(buffer[x2]);
+      pq.offer(x2);
+    } else if (istmp[x1]) {
+      buffer[x1] = bm_lazyor_inplace(buffer[x1], buffer[x2], false);
+      sizes[x1] = size(buffer[x1]);
+      pq.offer(x1);
+    } else {                             // ImmutableRoaringBitmap.lazyor (static)
+      buffer[x1] = bm_lazyor_static(buffer[x1], buffer[x2]);
+      sizes[x1] = size(buffer[x1]);
+      istmp[x1] = 1;
+      pq.offer(x1);
+    }
+  }
+  BM *ans = new BM(std::move(buffer[pq.poll()]));
+  for (Cont &c : ans->vals) c = repair(std::move(c)); // MutableRoaringBitmap.repairAfterLazy
+  return ans;
+}
+// BufferFastAggregation.priorityqueue_xor (buffer/BufferFastAggregation.java:933-958): fewer than 2
+// bitmaps throw IllegalArgumentException (nullptr here); the queue orders by ImmutableRoaringBitmap.
+// getLongSizeInBytes.
+BM *wide_buffer_pq_xor(const BM *const *bs, size_t n) {
+  if (n < 2) return nullptr;
+  std::vector<BM> pool;
+  pool.reserve(2 * n);
+  for (size_t k = 0; k < n; ++k) pool.push_back(*bs[k]);
+  auto cmp = [&](int a, int b) { return (int)(bm_size_immutable(pool[a]) - bm_size_immutable(pool[b])); };
+  JavaPQ<int, decltype(cmp)> pq(cmp);
+  for (size_t k = 0; k < n; ++k) pq.offer((int)k); // Collections.addAll
+  while (pq.size() > 1) {
+    const int x1 = pq.poll(), x2 = pq.poll();
+    std::unique_ptr<BM> r(bm_or_xor(pool[x1], pool[x2], true));
+    pool.push_back(std::move(*r));
+    pq.offer((int)pool.size() - 1);
+  }
+  return new BM(pool[pq.poll()]);
+}
+
 // ---- key-parallel restatements (the CPU baseline on all host cores).  Every wide semantics is
 // per-key independent with the key's containers in member order, so each key's result is the
 // single-threaded one; ParallelAggregation itself is key-parallel on the ForkJoin pool
@@ -1647,6 +1764,10 @@ int64_t rbref_op_cardinality(int op, const rbref_bitmap *a, const rbref_bitmap *
   }
 }
 
+rbref_bitmap *rbref_xor_keep_empty(const rbref_bitmap *a, const rbref_bitmap *b) {
+  return bm_xor_keep_empty(*a, *b); // c_ixor == c_xor: the static and in-place forms agree
+}
+
 int rbref_op_inplace(int op, rbref_bitmap *a, const rbref_bitmap *b) {
   switch (op) {
   case RBREF_AND: bm_iand(*a, *b); break;
@@ -1672,6 +1793,10 @@ rbref_bitmap *rbref_wide(int sem, const rbref_bitmap *const *bs, size_t n) {
   case RBREF_HORIZONTAL_XOR: return wide_horizontal(bs, n, true);
   case RBREF_PQ_OR: return wide_pq_or(bs, n);
   case RBREF_PQ_XOR: return wide_pq_xor(bs, n);
+  case RBREF_BUFFER_NAIVE_OR: return wide_buffer_naive_or(bs, n);
+  case RBREF_BUFFER_PQ_OR: return wide_pq_or_sized(bs, n, bm_serialized_size_lazy, true);
+  case RBREF_BUFFER_PQ_OR_ITER: return wide_pq_or_sized(bs, n, bm_size_immutable, true);
+  case RBREF_BUFFER_PQ_XOR: return wide_buffer_pq_xor(bs, n);
   default: return nullptr;
   }
 }

@@ -44,7 +44,12 @@ enum {
   RBREF_HORIZONTAL_OR = 8,  /* FastAggregation.horizontal_or           FastAggregation.java:124-231 */
   RBREF_HORIZONTAL_XOR = 9, /* FastAggregation.horizontal_xor          FastAggregation.java:243-289 */
   RBREF_PQ_OR = 10,         /* FastAggregation.priorityqueue_or        FastAggregation.java:615-721 */
-  RBREF_PQ_XOR = 11         /* FastAggregation.priorityqueue_xor       FastAggregation.java:732-752 */
+  RBREF_PQ_XOR = 11,        /* FastAggregation.priorityqueue_xor       FastAggregation.java:732-752 */
+  /* buffer/BufferFastAggregation entry points whose results differ from FastAggregation's */
+  RBREF_BUFFER_NAIVE_OR = 12,   /* naive_or / or(MutableRoaringBitmap...)  buffer/BufferFastAggregation.java:711-717 */
+  RBREF_BUFFER_PQ_OR = 13,      /* priorityqueue_or(ImmutableRoaringBitmap...)                       :810-866 */
+  RBREF_BUFFER_PQ_OR_ITER = 14, /* priorityqueue_or(Iterator)                                        :869-930 */
+  RBREF_BUFFER_PQ_XOR = 15      /* priorityqueue_xor (< 2 bitmaps: IllegalArgumentException -> NULL) :933-958 */
 };
 
 /* container type tags (RoaringFormatSpec order used by the device SoA) */
@@ -83,10 +88,14 @@ int rbref_from_soa(uint32_t n, const uint16_t *keys, const uint8_t *types, const
 rbref_bitmap *rbref_op(int op, const rbref_bitmap *a, const rbref_bitmap *b);
 /* RoaringBitmap.andCardinality/orCardinality/xorCardinality/andNotCardinality */
 int64_t rbref_op_cardinality(int op, const rbref_bitmap *a, const rbref_bitmap *b);
+/* Roaring64Bitmap.xor's per-key rule (longlong/Roaring64Bitmap.java:392-460): matched keys xor'd, the
+ * result kept even when empty; unmatched keys cloned */
+rbref_bitmap *rbref_xor_keep_empty(const rbref_bitmap *a, const rbref_bitmap *b);
 /* in-place RoaringBitmap.and/or/xor/andNot(x2) — RoaringBitmap.java:1272,2481,3296,1346 */
 int rbref_op_inplace(int op, rbref_bitmap *a, const rbref_bitmap *b);
 
-/* wide aggregation over bitmaps[0..n) (pointer identity matters for naive_and) */
+/* wide aggregation over bitmaps[0..n) (pointer identity matters for naive_and); NULL when the
+ * reference throws (BUFFER_PQ_XOR below 2 bitmaps) */
 rbref_bitmap *rbref_wide(int sem, const rbref_bitmap *const *bitmaps, size_t n);
 /* The same aggregation computed key-parallel on `threads` host threads (every semantics is per-key
  * independent; ParallelAggregation.or/xor are the reference's own key-parallel entry points,

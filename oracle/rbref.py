@@ -15,7 +15,7 @@ _LIB_PATH = os.path.join(_HERE, "librbref.so")
 
 AND, OR, XOR, ANDNOT = 0, 1, 2, 3
 (FAST_OR, FAST_AND, WORKSHY_AND, NAIVE_AND, FAST_XOR, PAR_OR, PAR_XOR, NAIVE_AND_ITER, HORIZONTAL_OR, HORIZONTAL_XOR,
- PQ_OR, PQ_XOR) = range(12)
+ PQ_OR, PQ_XOR, BUFFER_NAIVE_OR, BUFFER_PQ_OR, BUFFER_PQ_OR_ITER, BUFFER_PQ_XOR) = range(16)
 ARRAY, BITMAP, RUN = 0, 1, 2
 
 
@@ -48,6 +48,7 @@ def _load():
         "rbref_op": (P, [C.c_int, P, P]),
         "rbref_op_cardinality": (C.c_int64, [C.c_int, P, P]),
         "rbref_op_inplace": (C.c_int, [C.c_int, P, P]),
+        "rbref_xor_keep_empty": (P, [P, P]),
         "rbref_wide": (P, [C.c_int, C.POINTER(P), C.c_size_t]),
         "rbref_wide_cardinality": (C.c_int64, [C.c_int, C.POINTER(P), C.c_size_t]),
         "rbref_wide_mt": (P, [C.c_int, C.POINTER(P), C.c_size_t, C.c_int]),
@@ -143,6 +144,10 @@ def op_cardinality(opcode: int, a: RefBitmap, b: RefBitmap) -> int:
     return int(lib().rbref_op_cardinality(opcode, a.h, b.h))
 
 
+def xor_keep_empty(a: RefBitmap, b: RefBitmap) -> RefBitmap:
+    return RefBitmap(lib().rbref_xor_keep_empty(a.h, b.h))
+
+
 def op_inplace(opcode: int, a: RefBitmap, b: RefBitmap) -> None:
     assert lib().rbref_op_inplace(opcode, a.h, b.h) == 0
 
@@ -153,7 +158,10 @@ def _handles(bitmaps):
 
 
 def wide(sem: int, bitmaps) -> RefBitmap:
-    return RefBitmap(lib().rbref_wide(sem, _handles(bitmaps), len(bitmaps)))
+    h = lib().rbref_wide(sem, _handles(bitmaps), len(bitmaps))
+    if not h:  # the reference throws IllegalArgumentException (BufferFastAggregation.priorityqueue_xor)
+        raise ValueError("Expecting at least 2 bitmaps")
+    return RefBitmap(h)
 
 
 def wide_mt(sem: int, bitmaps, threads: int) -> RefBitmap:

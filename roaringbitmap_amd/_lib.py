@@ -17,6 +17,11 @@ AND, OR, XOR, ANDNOT = 0, 1, 2, 3
 ARRAY, BITMAP, RUN = 0, 1, 2
 FAST_OR, FAST_AND, WORKSHY_AND, NAIVE_AND, FAST_XOR, PAR_OR, PAR_XOR, NAIVE_AND_ITER = range(8)
 HORIZONTAL_OR, HORIZONTAL_XOR, PQ_OR, PQ_XOR = 8, 9, 10, 11  # global-order semantics (rbgpu.h rb_wide_sem)
+# buffer/ (BufferFastAggregation) entry points whose results differ from FastAggregation's
+BUFFER_NAIVE_OR, BUFFER_PQ_OR, BUFFER_PQ_OR_ITER, BUFFER_PQ_XOR = 12, 13, 14, 15
+PQ_SEMS = (PQ_OR, PQ_XOR, BUFFER_PQ_OR, BUFFER_PQ_OR_ITER, BUFFER_PQ_XOR)  # whole results only
+RB64_BITMAP, RB64_NAVIGABLE = 0, 1  # rbgpu.h rb64_flavor: Roaring64Bitmap / Roaring64NavigableMap
+EMPTY_BITMAP = 0xFFFFFFFF           # RB_EMPTY_BITMAP pair index
 WL_FILTER_POSTING, WL_WIDE_DENSE, WL_WIDE_MIXED, WL_WIDE_RUNS = range(4)
 BSI_EQ, BSI_NEQ, BSI_LE, BSI_LT, BSI_GE, BSI_GT, BSI_RANGE = range(7)  # BitmapSliceIndex.Operation
 
@@ -94,6 +99,17 @@ SIGNATURES = {
     # index arrays as void* (engine passes plain addresses: see engine._idx_addr)
     "rbgpu_pairwise": (C.c_int, [_P, C.c_int, _P, _P, _P, _P, C.c_uint32, C.POINTER(_P)]),
     "rbgpu_pairwise_cardinality": (C.c_int, [_P, C.c_int, _P, _P, _P, _P, C.c_uint32, _U64P]),
+    "rbgpu_pairwise_inplace": (C.c_int, [_P, C.c_int, _P, _P, _P, _P, C.c_uint32, C.POINTER(_P)]),
+    "rbgpu_set_run_optimize": (C.c_int, [_P, C.POINTER(_P), C.c_void_p]),
+    "rbgpu_set64_from_portable": (C.c_int, [_P, C.POINTER(C.c_char_p), _U64P, C.c_uint32, C.POINTER(_P)]),
+    "rbgpu_set64_from_buckets": (C.c_int, [_P, _U32P, _U64P, C.c_uint32, C.POINTER(_P)]),
+    "rbgpu_set64_free": (None, [_P]),
+    "rbgpu_set64_bitmap_count": (C.c_uint32, [_P]),
+    "rbgpu_set64_buckets": (C.c_int, [_P, C.c_uint32, _U32P, C.c_uint64, _U64P]),
+    "rbgpu_set64_cardinalities": (C.c_int, [_P, _U64P]),
+    "rbgpu_set64_portable_sizes": (C.c_int, [_P, _U64P]),
+    "rbgpu_set64_serialize_portable": (C.c_int, [_P, C.c_uint32, C.c_uint32, C.c_void_p, C.c_uint64, _U64P]),
+    "rbgpu_pairwise64": (C.c_int, [_P, C.c_int, C.c_int, C.c_int, _P, _P, _P, _P, C.c_uint32, C.POINTER(_P)]),
     "rbgpu_wide": (C.c_int, [_P, C.c_int, _P, _U32P, C.c_uint32, C.POINTER(_P)]),
     "rbgpu_wide_keys": (C.c_int, [_P, C.c_int, _P, _U32P, C.c_uint32, C.c_uint32, C.c_uint32, C.POINTER(_P)]),
     "rbgpu_wide_cardinality": (C.c_int, [_P, C.c_int, _P, _U32P, C.c_uint32, _U64P]),

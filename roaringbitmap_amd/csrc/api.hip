@@ -837,8 +837,13 @@ static uint32_t pairwise_seg_keys(const rbgpu_set *a, const rbgpu_set *b, uint64
 // Small batches (kernels.hpp: <= kSmallPairs pairs of <= kSmallPairKeys keys, <= kSmallSlots merged
 // keys, no Run container over 8 KiB to copy): two launches and one host read-back.  Returns 1 when
 // the batch does not qualify (the general pipeline runs), else an rbgpu status.
+// containers of bitmap i (RB_EMPTY_BITMAP: none)
+static inline uint64_t bm_conts(const rbgpu_set *s, uint32_t i) {
+  return i == kEmptyBitmap ? 0 : s->h_begin[i + 1] - s->h_begin[i];
+}
 static int pairwise_small(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu_set *b, const uint32_t *a_idx,
-                          const uint32_t *b_idx, uint32_t np, rbgpu_set **out, uint64_t *card_out) {
+                          const uint32_t *b_idx, uint32_t np, rbgpu_set **out, uint64_t *card_out, bool inplace,
+                          bool keep_empty) {
   const char *dis = getenv("RBGPU_NO_SMALL_PAIRS"); // parity tests run both paths
   if ((dis && dis[0] == '1') || np == 0 || np > kSmallPairs) return 1;
   int rc = ensure_h_begin(a);
@@ -851,7 +856,7 @@ static int pairwise_small(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgp
   uint64_t nblocks64 = 0;
   for (uint32_t p = 0; p < np; ++p) {
     const uint32_t ai = a_idx ? a_idx[p] : p, bi = b_idx ? b_idx[p] : p;
-    nblocks64 += small_pair_nsub((a->h_begin[ai + 1] - a->h_begin[ai]) + (b->h_begin[bi + 1] - b->h_begin[bi]), cap);
+    nblocks64 += small_pair_nsub(bm_conts(a, ai) + bm_conts(b, bi), cap);
   }
   const size_t nout = 64, nslot = 8 * (np + 1ull), nidx = 4ull * np * ((a_idx != nullptr) + (b_idx != nullptr));
   const size_t blob = nout + nslot + nidx + 4 * nblocks64;
@@ -874,7 +879,7 @@ static int pairwise_small(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgp
   uint32_t max_keys = 0;
   for (uint32_t p = 0; p < np; ++p) {
     const uint32_t ai = a_idx ? a_idx[p] : p, bi = b_idx ? b_idx[p] : p;
-    const uint64_t nk = (a->h_begin[ai + 1] - a->h_begin[ai]) + (b->h_begin[bi + 1] - b->h_begin[bi]);
+    const uint64_t nk = bm_conts(a, ai) + bm_conts(b, bi);
     if (nk > kSmallPairKeys) return 1;
     max_keys = std::max(max_keys, (uint32_t)nk);
     slot[p] = acc;
@@ -945,6 +950,9 @@ static int pairwise_small(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgp
   if (res) sa.out = OutView{res->key, res->type, res->card, res->nruns, res->off};
   sa.hout = reinterpret_cast<uint64_t *>(ctx->d_small);
   sa.lazy = is_lazy_op(op) ? op : 0;
+  sa.inplace = inplace;
+  sa.same = a == b;
+  sa.keep_empty = keep_empty;
   launch_pair_small(is_lazy_op(op) ? (int)RB_OR : op, card_only, sa, max_keys, nblocks, st);
   if (ktimes) HIPCHK(hipEventRecord(ctx->ev[2], st));
   launch_pair_small_compact(sa, st);
@@ -981,7 +989,7 @@ static int pairwise_small(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgp
 // task kernel — results are not produced.
 static int pairwise_impl(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu_set *b, const uint32_t *a_idx,
                          const uint32_t *b_idx, uint32_t npairs, rbgpu_set **out, uint64_t *card_out,
-                         int probe = 0) {
+                         int probe = 0, bool inplace = false, bool keep_empty = false) {
   int rc = check_ctx(ctx);
   if (rc) return rc;
   if ((op < RB_AND || op > RB_ANDNOT) && !is_lazy_op(op)) return fail(RB_EINVAL, "bad op %d", op);
@@ -990,11 +998,11 @@ static int pairwise_impl(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu
   if (!a_idx && npairs > a->nb) return fail(RB_EINVAL, "npairs exceeds bitmaps of a");
   if (!b_idx && npairs > b->nb) return fail(RB_EINVAL, "npairs exceeds bitmaps of b");
   for (uint32_t i = 0; a_idx && i < npairs; ++i)
-    if (a_idx[i] >= a->nb) return fail(RB_EINVAL, "a_idx[%u] out of range", i);
+    if (a_idx[i] >= a->nb && a_idx[i] != kEmptyBitmap) return fail(RB_EINVAL, "a_idx[%u] out of range", i);
   for (uint32_t i = 0; b_idx && i < npairs; ++i)
-    if (b_idx[i] >= b->nb) return fail(RB_EINVAL, "b_idx[%u] out of range", i);
+    if (b_idx[i] >= b->nb && b_idx[i] != kEmptyBitmap) return fail(RB_EINVAL, "b_idx[%u] out of range", i);
   if (!probe) {
-    rc = pairwise_small(ctx, op, a, b, a_idx, b_idx, npairs, out, card_out);
+    rc = pairwise_small(ctx, op, a, b, a_idx, b_idx, npairs, out, card_out, inplace, keep_empty);
     if (rc != 1) return rc;
   }
   const bool card_only = out == nullptr;
@@ -1042,7 +1050,7 @@ static int pairwise_impl(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu
       uint64_t *sb = reinterpret_cast<uint64_t *>(h), acc = 0;
       for (uint64_t p = 0; p < np; ++p) { // k_seg_count's formula
         const uint32_t ai = a_idx ? a_idx[p] : (uint32_t)p, bi = b_idx ? b_idx[p] : (uint32_t)p;
-        const uint64_t nk = (a->h_begin[ai + 1] - a->h_begin[ai]) + (b->h_begin[bi + 1] - b->h_begin[bi]);
+        const uint64_t nk = bm_conts(a, ai) + bm_conts(b, bi);
         sb[p] = acc;
         acc += (nk + seg_keys - 1) / seg_keys + (nk == 0);
       }
@@ -1053,7 +1061,7 @@ static int pairwise_impl(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu
   if (card_out && np) HIPCHK(hipMemsetAsync(pcard, 0, np * 8, st));
 
   stats_begin(ctx);
-  PairArgs pa{op, a->view(), b->view(), d_aidx, d_bidx, npairs, seg_begin, nullptr, 0, seg_keys};
+  PairArgs pa{op, a->view(), b->view(), d_aidx, d_bidx, npairs, seg_begin, nullptr, 0, seg_keys, inplace, a == b};
   uint64_t *const tot = ctx->h_pinned;
   uint64_t ns = 0;
   // one segment per pair when no pair can exceed seg_keys merged keys (config 2: <= 8 keys per
@@ -1111,6 +1119,8 @@ static int pairwise_impl(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu
   TaskRec *heavy = T.take<TaskRec>(std::max<uint64_t>(nheavy, 1));
   TaskMeta tm{};
   tm.lazy = is_lazy_op(op) ? op : 0;
+  tm.inplace = inplace;
+  tm.keep_empty = keep_empty;
   tm.key = T.take<uint16_t>(nt1);
   tm.nruns = T.take<uint16_t>(nt1);
   tm.type = T.take<uint8_t>(nt1);
@@ -1221,6 +1231,70 @@ int rbgpu_pairwise_cardinality(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const
   return rc;
 }
 
+} // extern "C"
+namespace rbg {
+int pairwise_call(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu_set *b, const uint32_t *a_idx,
+                  const uint32_t *b_idx, uint32_t npairs, rbgpu_set **out, bool inplace, bool keep_empty) {
+  *out = nullptr;
+  return pairwise_impl(ctx, op, a, b, a_idx, b_idx, npairs, out, nullptr, 0, inplace, keep_empty);
+}
+} // namespace rbg
+extern "C" {
+
+int rbgpu_set_run_optimize(const rbgpu_set *in, rbgpu_set **out, uint8_t *any_run) {
+  if (!in || !out) return fail(RB_EINVAL, "null argument");
+  *out = nullptr;
+  rbgpu_ctx *ctx = in->ctx;
+  int rc = check_ctx(ctx);
+  if (rc) return rc;
+  hipStream_t st = ctx->stream;
+  rbgpu_set *res = new rbgpu_set;
+  rc = set_alloc(ctx, res, in->nb, in->nc, in->payload_bytes);
+  if (rc) {
+    delete res;
+    return rc;
+  }
+  uint8_t *d_any = nullptr;
+  if (any_run && in->nb && ctx->pool.alloc((void **)&d_any, in->nb)) {
+    rbgpu_set_free(res);
+    return fail(RB_ENOMEM, "runOptimize flags");
+  }
+  const uint64_t n = in->nc;
+  auto copy = [&](void *d, const void *s, uint64_t b) { return b ? hipMemcpyAsync(d, s, b, hipMemcpyDeviceToDevice, st) : hipSuccess; };
+  if (copy(res->begin, in->begin, 8ull * (in->nb + 1)) || copy(res->key, in->key, 2 * n) ||
+      copy(res->card, in->card, 4 * n) || copy(res->off, in->off, 8 * n)) {
+    ctx->pool.release(d_any);
+    rbgpu_set_free(res);
+    return fail(RB_EDEVICE, "runOptimize metadata copy");
+  }
+  stats_begin(ctx);
+  HIPCHK(hipEventRecord(ctx->ev[1], st));
+  launch_run_optimize(in->view(), n, res->type, res->nruns, res->payload, in->nb, d_any, st);
+  HIPCHK(hipEventRecord(ctx->ev[2], st));
+  if (d_any) HIPCHK(hipMemcpyAsync(any_run, d_any, in->nb, hipMemcpyDeviceToHost, st));
+  const KernelSpan spans[1] = {{"k_run_optimize", 0, 1, n}};
+  rc = stats_end(ctx, n, n, spans, 1);
+  ctx->pool.release(d_any);
+  if (rc) {
+    rbgpu_set_free(res);
+    return rc;
+  }
+  res->h_begin = in->h_begin;
+  *out = res;
+  return RB_OK;
+}
+
+int rbgpu_pairwise_inplace(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu_set *b, const uint32_t *a_idx,
+                           const uint32_t *b_idx, uint32_t npairs, rbgpu_set **out) {
+  const auto t0 = std::chrono::steady_clock::now();
+  if (!out) return fail(RB_EINVAL, "null out");
+  *out = nullptr;
+  if (op < RB_AND || op > RB_ANDNOT) return fail(RB_EINVAL, "bad op %d", op);
+  const int rc = pairwise_impl(ctx, op, a, b, a_idx, b_idx, npairs, out, nullptr, 0, true);
+  if (!rc) ctx->last.call_us = us_since(t0);
+  return rc;
+}
+
 // Measurement hook (not part of rbgpu.h): runs the pairwise setup, then a read-only probe kernel
 // in place of the task kernel (mode 1: the task kernel's payload loads; 2: a streaming read of
 // a's arena).  The probe's time is in rbgpu_get_stats().main_kernel_ms.
@@ -1254,11 +1328,61 @@ static int empty_result(rbgpu_ctx *ctx, rbgpu_set **out) {
   *out = e;
   return RB_OK;
 }
-static int pq_xor(rbgpu_ctx *ctx, const rbgpu_set *in, const std::vector<uint32_t> &mem, rbgpu_set **out) {
+// The size a priority queue orders bitmaps by, per bitmap of s (one metadata read-back):
+//   kSizeLong       RoaringBitmap.getLongSizeInBytes (RoaringBitmap.java:2212-2219): 8 + per container
+//                   2 + getSizeInBytes (Array 2c + 4, Bitmap 8192 lazy or not, Run 4r + 4);
+//   kSizeImmutable  ImmutableRoaringBitmap.getLongSizeInBytes (buffer/ImmutableRoaringBitmap.java:1508-1521):
+//                   4 + per container 4 + (Run 2 + 4r; else getCardinality() > 4096 ? 8192 : 2 getCardinality()),
+//                   a lazy Bitmap's getCardinality() being -1 (MappeableBitmapContainer.java:540-542);
+//   kSizeSerialized ImmutableRoaringBitmap.serializedSizeInBytes (buffer/MutableRoaringArray.java:756-764).
+// Intermediate results of priorityqueue_or carry the lazy marks in their card words (common.hpp).
+enum { kSizeLong = 0, kSizeImmutable = 1, kSizeSerialized = 2 };
+static int pq_sizes(const rbgpu_set *s, int kind, std::vector<int64_t> &out) {
+  int rc = ensure_h_begin(s);
+  if (rc) return rc;
+  const uint64_t n = s->nc;
+  std::vector<uint8_t> type(n);
+  std::vector<uint16_t> nruns(n);
+  std::vector<uint32_t> card(n);
+  if (n) {
+    HIPCHK(hipMemcpyAsync(type.data(), s->type, n, hipMemcpyDeviceToHost, s->ctx->stream));
+    HIPCHK(hipMemcpyAsync(nruns.data(), s->nruns, n * 2, hipMemcpyDeviceToHost, s->ctx->stream));
+    HIPCHK(hipMemcpyAsync(card.data(), s->card, n * 4, hipMemcpyDeviceToHost, s->ctx->stream));
+    HIPCHK(hipStreamSynchronize(s->ctx->stream));
+  }
+  out.assign(s->nb, 0);
+  for (uint32_t b = 0; b < s->nb; ++b) {
+    const uint64_t lo = s->h_begin[b], hi = s->h_begin[b + 1], k = hi - lo;
+    int64_t v = kind == kSizeLong ? 8 : kind == kSizeImmutable ? 4 : 0;
+    bool hasrun = false;
+    for (uint64_t i = lo; i < hi; ++i) {
+      const int64_t r = nruns[i], c = card[i] & ~kCardMarks;
+      const bool lazy = type[i] == RB_BITMAP && (card[i] & kLazyCard);
+      hasrun |= type[i] == RB_RUN;
+      if (kind == kSizeLong)
+        v += 2 + (type[i] == RB_BITMAP ? 8192 : type[i] == RB_ARRAY ? 2 * c + 4 : 4 * r + 4);
+      else if (kind == kSizeImmutable)
+        v += 4 + (type[i] == RB_RUN ? 2 + 4 * r : lazy ? -2 : c > kMaxArray ? 8192 : 2 * c);
+      else
+        v += type[i] == RB_BITMAP ? 8192 : type[i] == RB_ARRAY ? 2 * c : 2 + 4 * r;
+    }
+    if (kind == kSizeSerialized)
+      v += (int64_t)(hasrun ? (k < 4 ? 4 + (k + 7) / 8 + 4 * k : 4 + (k + 7) / 8 + 8 * k) : 8 + 8 * k);
+    out[b] = v;
+  }
+  return RB_OK;
+}
+
+// buffered: BufferFastAggregation.priorityqueue_xor (buffer/BufferFastAggregation.java:933-958) — fewer
+// than 2 bitmaps throw, the queue orders by ImmutableRoaringBitmap.getLongSizeInBytes.
+static int pq_xor(rbgpu_ctx *ctx, const rbgpu_set *in, const std::vector<uint32_t> &mem, rbgpu_set **out,
+                  bool buffered) {
   const size_t n = mem.size();
+  if (buffered && n < 2) return fail(RB_EINVAL, "Expecting at least 2 bitmaps");
   if (n == 0) return empty_result(ctx, out);
-  std::vector<rb_bitmap_summary> summ(in->nb);
-  int rc = rbgpu_set_summaries(in, 0, in->nb, summ.data());
+  const int kind = buffered ? kSizeImmutable : kSizeLong;
+  std::vector<int64_t> sz;
+  int rc = pq_sizes(in, kind, sz);
   if (rc) return rc;
   struct Node {
     const rbgpu_set *s;
@@ -1268,7 +1392,7 @@ static int pq_xor(rbgpu_ctx *ctx, const rbgpu_set *in, const std::vector<uint32_
   };
   std::vector<Node> nodes;
   nodes.reserve(2 * n);
-  for (uint32_t m : mem) nodes.push_back(Node{in, m, (int64_t)summ[m].size_in_bytes, nullptr});
+  for (uint32_t m : mem) nodes.push_back(Node{in, m, sz[m], nullptr});
   auto cmp = [&](uint32_t a, uint32_t b) { return (int)(nodes[a].size - nodes[b].size); };
   JavaHeap<uint32_t, decltype(cmp)> pq(cmp);
   for (uint32_t k = 0; k < n; ++k) pq.offer(k);
@@ -1281,8 +1405,8 @@ static int pq_xor(rbgpu_ctx *ctx, const rbgpu_set *in, const std::vector<uint32_
     const uint32_t i1 = nodes[x1].idx, i2 = nodes[x2].idx;
     rbgpu_set *r = nullptr;
     rc = rbgpu_pairwise(ctx, RB_XOR, nodes[x1].s, nodes[x2].s, &i1, &i2, 1, &r);
-    rb_bitmap_summary rs{};
-    if (!rc) rc = rbgpu_set_summaries(r, 0, 1, &rs);
+    std::vector<int64_t> rs;
+    if (!rc) rc = pq_sizes(r, kind, rs);
     if (rc) {
       if (r) rbgpu_set_free(r);
       cleanup();
@@ -1290,7 +1414,7 @@ static int pq_xor(rbgpu_ctx *ctx, const rbgpu_set *in, const std::vector<uint32_
     }
     for (uint32_t x : {x1, x2}) // the operands are not referenced again
       if (nodes[x].owned) rbgpu_set_free(nodes[x].owned), nodes[x].owned = nullptr;
-    nodes.push_back(Node{r, 0, (int64_t)rs.size_in_bytes, r});
+    nodes.push_back(Node{r, 0, rs[0], r});
     pq.offer((uint32_t)nodes.size() - 1);
   }
   Node &last = nodes[pq.poll()];
@@ -1311,11 +1435,16 @@ static int pq_xor(rbgpu_ctx *ctx, const rbgpu_set *in, const std::vector<uint32_
 // (repairAfterLazy).  Each step is one device pairwise call in a lazy role (pairwise.hip
 // lazy_or_type); its size comes back from the result's summary.  The repair is one more call, the
 // survivor with itself in the kLazyRepair role (a lazy Bitmap -> LR, an exact one kept, Run -> EFF).
-static int pq_or(rbgpu_ctx *ctx, const rbgpu_set *in, const std::vector<uint32_t> &mem, rbgpu_set **out) {
+// BufferFastAggregation.priorityqueue_or (buffer/BufferFastAggregation.java:810-930) runs the same merges
+// ordered by serializedSizeInBytes (varargs, kind kSizeSerialized) or ImmutableRoaringBitmap.
+// getLongSizeInBytes (Iterator, kSizeImmutable), and returns a lone bitmap as a copy, unrepaired.
+static int pq_or(rbgpu_ctx *ctx, const rbgpu_set *in, const std::vector<uint32_t> &mem, rbgpu_set **out,
+                 int kind) {
   const size_t n = mem.size();
   if (n == 0) return empty_result(ctx, out);
-  std::vector<rb_bitmap_summary> summ(in->nb);
-  int rc = rbgpu_set_summaries(in, 0, in->nb, summ.data());
+  if (n == 1 && kind != kSizeLong) return rbgpu_set_extract(in, mem[0], 1, out); // toMutableRoaringBitmap
+  std::vector<int64_t> sz;
+  int rc = pq_sizes(in, kind, sz);
   if (rc) return rc;
   struct Node {
     const rbgpu_set *s;
@@ -1326,7 +1455,7 @@ static int pq_or(rbgpu_ctx *ctx, const rbgpu_set *in, const std::vector<uint32_t
   };
   std::vector<Node> nodes;
   nodes.reserve(2 * n);
-  for (uint32_t m : mem) nodes.push_back(Node{in, m, (int64_t)summ[m].size_in_bytes, nullptr, false});
+  for (uint32_t m : mem) nodes.push_back(Node{in, m, sz[m], nullptr, false});
   auto cmp = [&](uint32_t a, uint32_t b) { return (int)(nodes[a].size - nodes[b].size); };
   JavaHeap<uint32_t, decltype(cmp)> pq(cmp);
   for (uint32_t k = 0; k < n; ++k) pq.offer(k);
@@ -1345,8 +1474,8 @@ static int pq_or(rbgpu_ctx *ctx, const rbgpu_set *in, const std::vector<uint32_t
     const uint32_t it = nodes[t].idx, io = nodes[o].idx;
     rbgpu_set *r = nullptr;
     rc = pairwise_impl(ctx, role, nodes[t].s, nodes[o].s, &it, &io, 1, &r, nullptr);
-    rb_bitmap_summary rs{};
-    if (!rc) rc = rbgpu_set_summaries(r, 0, 1, &rs);
+    std::vector<int64_t> rs;
+    if (!rc) rc = pq_sizes(r, kind, rs);
     if (rc) {
       if (r) rbgpu_set_free(r);
       cleanup();
@@ -1354,7 +1483,7 @@ static int pq_or(rbgpu_ctx *ctx, const rbgpu_set *in, const std::vector<uint32_t
     }
     for (uint32_t x : {x1, x2}) // the operands are not referenced again
       if (nodes[x].owned) rbgpu_set_free(nodes[x].owned), nodes[x].owned = nullptr;
-    nodes.push_back(Node{r, 0, (int64_t)rs.size_in_bytes, r, true});
+    nodes.push_back(Node{r, 0, rs[0], r, true});
     pq.offer((uint32_t)nodes.size() - 1);
   }
   const Node last = nodes[pq.poll()];
@@ -1376,7 +1505,7 @@ int rbgpu_wide_keys(rbgpu_ctx *ctx, int sem, const rbgpu_set *in, const uint32_t
   int rc = check_ctx(ctx);
   if (rc) return rc;
   if (!in || in->ctx != ctx) return fail(RB_EINVAL, "bad input set");
-  if (sem < RB_FAST_OR || sem > RB_PQ_XOR) return fail(RB_EINVAL, "bad semantics %d", sem);
+  if (sem < RB_FAST_OR || sem > RB_BUFFER_PQ_XOR) return fail(RB_EINVAL, "bad semantics %d", sem);
   rc = ensure_h_begin(in);
   if (rc) return rc;
   std::vector<uint32_t> mem;
@@ -1389,9 +1518,15 @@ int rbgpu_wide_keys(rbgpu_ctx *ctx, int sem, const rbgpu_set *in, const uint32_t
     mem.resize(n);
     for (uint32_t i = 0; i < n; ++i) mem[i] = i;
   }
-  if (sem == RB_PQ_XOR || sem == RB_PQ_OR) {
+  if (sem == RB_PQ_XOR || sem == RB_PQ_OR || sem >= RB_BUFFER_PQ_OR) {
     if (key_lo != 0 || key_hi != 65536) return fail(RB_EINVAL, "priorityqueue_or/xor have no key-range shards");
-    return sem == RB_PQ_XOR ? pq_xor(ctx, in, mem, out) : pq_or(ctx, in, mem, out);
+    switch (sem) {
+    case RB_PQ_XOR: return pq_xor(ctx, in, mem, out, false);
+    case RB_BUFFER_PQ_XOR: return pq_xor(ctx, in, mem, out, true);
+    case RB_PQ_OR: return pq_or(ctx, in, mem, out, kSizeLong);
+    case RB_BUFFER_PQ_OR: return pq_or(ctx, in, mem, out, kSizeSerialized);
+    default: return pq_or(ctx, in, mem, out, kSizeImmutable);
+    }
   }
   return wide_run(ctx, sem, in, mem, key_lo, key_hi, out);
 }

@@ -415,7 +415,7 @@ int rbgpu_wide_sharded(rbgpu_comm *c, int sem, const rbgpu_set *in, const uint32
   // priorityqueue_or / _xor merge in the order of intermediate result sizes, which are global: a
   // key-range shard cannot follow it.  Refused on every rank alike (the arguments agree) before any
   // collective.
-  if (c->nranks > 1 && (sem == RB_PQ_OR || sem == RB_PQ_XOR))
+  if (c->nranks > 1 && (sem == RB_PQ_OR || sem == RB_PQ_XOR || sem >= RB_BUFFER_PQ_OR))
     return fail(RB_EINVAL, "priorityqueue_or / priorityqueue_xor cannot be key-range sharded");
   int rc = in ? RB_OK : fail(RB_EINVAL, "null input set");
   std::vector<uint32_t> ord;

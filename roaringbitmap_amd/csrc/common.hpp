@@ -44,6 +44,7 @@ struct TaskRec {
   uint16_t ra, rb; // run counts
 };
 constexpr uint32_t kAbsent = 3;
+constexpr uint32_t kEmptyBitmap = 0xFFFFFFFFu; // RB_EMPTY_BITMAP: a pair index naming an empty bitmap
 __host__ __device__ inline uint32_t desc_type(uint32_t d) { return d & 3; }
 __host__ __device__ inline uint32_t desc_card(uint32_t d) { return d >> 2; }
 

@@ -189,6 +189,10 @@ struct rbgpu_set {
 
 namespace rbg {
 int set_alloc(rbgpu_ctx *ctx, rbgpu_set *s, uint32_t nb, uint64_t nc, uint64_t payload);
+// the pairwise pipeline with its flags (api.hip): x1.op(x2) in place (PairArgs::inplace), XOR results
+// kept when empty (TaskMeta::keep_empty); a_idx / b_idx may hold kEmptyBitmap
+int pairwise_call(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu_set *b, const uint32_t *a_idx,
+                  const uint32_t *b_idx, uint32_t npairs, rbgpu_set **out, bool inplace, bool keep_empty);
 void ctx_unref(rbgpu_ctx *ctx);
 void set_release(rbgpu_set *s);
 int ensure_h_begin(const rbgpu_set *s);

@@ -23,6 +23,10 @@ struct PairArgs {
   const uint32_t *seg_pair;  // [nseg] pair of each segment
   uint64_t nseg;
   uint32_t seg_keys; // merged keys per segment (a power of two in [8, 256])
+  // in-place x1.op(x2) (RoaringBitmap.and/or/xor/andNot(x2)): `same` = A and B are one set, so a pair
+  // with equal indices is one bitmap with itself — x.and(x) / x.or(x) leave x as it is, x.xor(x) /
+  // x.andNot(x) clear it (RoaringBitmap.java:1271, 1347-1350, 2482, 3297-3300)
+  int inplace, same;
 };
 // per task result metadata (workspace, indexed like tasks)
 struct TaskMeta {
@@ -33,6 +37,8 @@ struct TaskMeta {
   uint8_t *cat;    // 0 light, 1 heavy
   uint64_t *out;   // output slot offset
   int lazy;        // 0, or the priorityqueue_or role (kLazyStatic / kLazyIor / kLazyIorBf) of an OR call
+  int inplace;     // x1.or(x2) in place: BitmapContainer.ior(ArrayContainer) keeps a Bitmap even when full
+  int keep_empty;  // XOR results are kept when empty (Roaring64Bitmap.xor: Roaring64Bitmap.java:392-460)
 };
 struct PairCounts {
   uint64_t task, light, heavy, big, small;
@@ -96,6 +102,8 @@ struct SmallPairArgs {
   uint64_t *bstat;             // [4 * blocks] per block: input bytes, key-array bytes, output bytes, cardinality
   uint64_t *dslot;             // [np + 1] device copy of slot (written by the first kernel)
   int lazy;                    // 0, or the priorityqueue_or role of an OR call (TaskMeta::lazy)
+  int inplace, same;           // in-place x1.op(x2) (PairArgs::inplace / same)
+  int keep_empty;              // TaskMeta::keep_empty
   const uint32_t *blk;         // [blocks] pair | block-within-pair << 12 (host-visible)
   uint32_t cap;                // most blocks per pair
   // the compaction kernel's: E slots, nblocks blocks, slot -> result position scratch (used above
@@ -173,6 +181,10 @@ void launch_layout(const uint64_t *bigflag, const uint64_t *bidx, const uint64_t
                    uint64_t *off, uint64_t n, hipStream_t st);
 void launch_pack_records(const SetView &s, uint64_t n, uint64_t *mrec, hipStream_t st);
 void launch_dense_check(const SetView &s, uint32_t nb, uint32_t lo, uint32_t cnt, uint32_t *bad, hipStream_t st);
+// RoaringBitmap.runOptimize of every container of s into type / nruns / payload (same offsets); any_run[nb]
+// (may be null): per bitmap, whether it holds a Run container afterwards
+void launch_run_optimize(const SetView &s, uint64_t n, uint8_t *type, uint16_t *nruns, uint8_t *payload,
+                         uint32_t nb, uint8_t *any_run, hipStream_t st);
 
 // ---- generate.hip
 struct GenSpec {

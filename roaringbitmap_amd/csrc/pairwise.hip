@@ -91,12 +91,13 @@ __device__ __forceinline__ uint32_t block_xscan(uint32_t v, uint32_t *wtot, uint
 // shorter segments when a batch has few keys (pairwise_seg_keys) to keep enough threads walking.
 
 __device__ __forceinline__ void pair_ranges(const PairArgs &a, uint32_t p, uint64_t &i0, uint64_t &na, uint64_t &j0,
-                                            uint64_t &nb) {
+                                            uint64_t &nb, bool *ident = nullptr) {
   const uint32_t ai = a.aidx ? a.aidx[p] : p, bi = a.bidx ? a.bidx[p] : p;
-  i0 = a.A.begin[ai];
-  na = a.A.begin[ai + 1] - i0;
-  j0 = a.B.begin[bi];
-  nb = a.B.begin[bi + 1] - j0;
+  if (ident) *ident = a.inplace && a.same && ai == bi && ai != kEmptyBitmap; // x1.op(x1) in place
+  i0 = ai == kEmptyBitmap ? 0 : a.A.begin[ai];
+  na = ai == kEmptyBitmap ? 0 : a.A.begin[ai + 1] - i0;
+  j0 = bi == kEmptyBitmap ? 0 : a.B.begin[bi];
+  nb = bi == kEmptyBitmap ? 0 : a.B.begin[bi + 1] - j0;
 }
 // position after d merged keys -> (i, j) offsets into A and B
 __device__ __forceinline__ void merge_split(const uint16_t *ka, uint64_t na, const uint16_t *kb, uint64_t nb,
@@ -163,7 +164,8 @@ __device__ __forceinline__ void pair_walk(const PairArgs &a, uint64_t sg, PairCo
                                           uint64_t h0 = 0, uint64_t t0 = 0) {
   const uint32_t p = a.seg_pair[sg];
   uint64_t i0, na, j0, nb;
-  pair_ranges(a, p, i0, na, j0, nb);
+  bool ident;
+  pair_ranges(a, p, i0, na, j0, nb, &ident);
   const uint64_t d0 = (sg - a.seg_begin[p]) * a.seg_keys, d1 = d0 + a.seg_keys < na + nb ? d0 + a.seg_keys : na + nb;
   uint64_t si0, sj0, si1, sj1;
   merge_split(a.A.key + i0, na, a.B.key + j0, nb, d0, si0, sj0);
@@ -214,8 +216,13 @@ __device__ __forceinline__ void pair_walk(const PairArgs &a, uint64_t sg, PairCo
   while (i < i1 && j < j1) {
     uint16_t ka = a.A.key[i], kb = a.B.key[j];
     if (ka == kb) {
-      matched_bound(a.op, a.A.card[i], a.B.card[j], big, bytes);
-      slot((int64_t)i, (int64_t)j, ka, big, bytes);
+      if (!ident) {
+        matched_bound(a.op, a.A.card[i], a.B.card[j], big, bytes);
+        slot((int64_t)i, (int64_t)j, ka, big, bytes);
+      } else if (a.op == RB_AND || a.op == RB_OR) { // x.and(x) / x.or(x): x unchanged (its own containers)
+        copy_bound(a.A, i, big, bytes);
+        slot((int64_t)i, -1, ka, big, bytes);
+      } // x.xor(x) / x.andNot(x): cleared
       ++i;
       ++j;
     } else if (ka < kb) {
@@ -733,9 +740,11 @@ __global__ __launch_bounds__(256, ROLE == kRoleHeavy ? kHeavyWaves : kLightWaves
       if (lazy) {
         ty = lazy_or_type(tm.lazy, ta, tb, tc.cp, tc.cq, c, r, cw, bits);
         if (ty == kRun && c == kSpan) r = 1;
-      } else if (OP != RB_OR && c == 0) ty = kEmpty;
+      } else if (OP != RB_OR && c == 0 && !(OP == RB_XOR && tm.keep_empty)) ty = kEmpty;
       else if (eff) ty = type_eff(c, r);
-      else if (OP == RB_OR && (ta == kBitmap || tb == kBitmap)) {
+      else if (OP == RB_OR && tm.inplace && ta == kBitmap && tb == kArray) {
+        ty = kBitmap; // BitmapContainer.ior(ArrayContainer) returns this, full or not (BitmapContainer.java:749-766)
+      } else if (OP == RB_OR && (ta == kBitmap || tb == kBitmap)) {
         ty = type_lr(c);
         if (ty == kRun) r = 1; // LR's Run is the full container: one run
       } else ty = type_ab(c);
@@ -1222,8 +1231,10 @@ __global__ __launch_bounds__(256, kSmallWaves) void k_pair_small(SmallPairArgs a
   // aligns the keys (cheap, in LDS) and its waves take the merged keys e = nw * sub + wv, + nw * nsub, ...
   const uint32_t bk = a.blk[blockIdx.x], p = bk & 0xFFFu, sub = bk >> 12, nt = blockDim.x;
   const uint32_t ai = a.aidx ? a.aidx[p] : p, bi = a.bidx ? a.bidx[p] : p;
-  const uint64_t i0 = a.A.begin[ai], j0 = a.B.begin[bi];
-  const uint32_t na = (uint32_t)(a.A.begin[ai + 1] - i0), nb = (uint32_t)(a.B.begin[bi + 1] - j0);
+  const bool ident = a.inplace && a.same && ai == bi && ai != kEmptyBitmap; // x1.op(x1) in place
+  const uint64_t i0 = ai == kEmptyBitmap ? 0 : a.A.begin[ai], j0 = bi == kEmptyBitmap ? 0 : a.B.begin[bi];
+  const uint32_t na = ai == kEmptyBitmap ? 0u : (uint32_t)(a.A.begin[ai + 1] - i0);
+  const uint32_t nb = bi == kEmptyBitmap ? 0u : (uint32_t)(a.B.begin[bi + 1] - j0);
   for (uint32_t t = threadIdx.x; t < na; t += nt) K[t] = a.A.key[i0 + t];
   for (uint32_t t = threadIdx.x; t < nb; t += nt) K[na + t] = a.B.key[j0 + t];
   __syncthreads();
@@ -1271,7 +1282,7 @@ __global__ __launch_bounds__(256, kSmallWaves) void k_pair_small(SmallPairArgs a
     uint8_t *dst = a.arena + slot * kBitmapBytes;
     int ty = kEmpty, c = 0, nr = 0;
     uint32_t cw = 0xFFFFFFFFu; // the card word to store when it is not c (priorityqueue_or's lazy marks)
-    if (has_a && has_b) {
+    if (has_a && has_b && !ident) {
       const uint64_t xa = i0 + ia, xb = j0 + ib;
       const int ta = a.A.type[xa], tb = a.B.type[xb];
       const uint32_t ca = a.A.card[xa], cb = a.B.card[xb], ra = a.A.nruns[xa], rb = a.B.nruns[xb];
@@ -1317,16 +1328,19 @@ __global__ __launch_bounds__(256, kSmallWaves) void k_pair_small(SmallPairArgs a
       if (lazy) {
         ty = lazy_or_type(a.lazy, ta, tb, ca, cb, c, r, cw, bits);
         if (ty == kRun && c == kSpan) r = 1;
-      } else if (OP != RB_OR && c == 0) ty = kEmpty;
+      } else if (OP != RB_OR && c == 0 && !(OP == RB_XOR && a.keep_empty)) ty = kEmpty;
       else if (eff) ty = type_eff(c, r);
-      else if (OP == RB_OR && (ta == kBitmap || tb == kBitmap)) {
+      else if (OP == RB_OR && a.inplace && ta == kBitmap && tb == kArray) {
+        ty = kBitmap; // BitmapContainer.ior(ArrayContainer) returns this, full or not (BitmapContainer.java:749-766)
+      } else if (OP == RB_OR && (ta == kBitmap || tb == kBitmap)) {
         ty = type_lr(c);
         if (ty == kRun) r = 1; // LR's Run is the full container: one run
       } else ty = type_ab(c);
       if (CARD_ONLY) ty = c ? kArray : kEmpty;
       else if (ty != kEmpty) emit_container(bits ? (int)kBitmap : ty, w, c, r, dst, s, lane);
       nr = ty == kRun ? r : 0;
-    } else if (has_a ? keeps_a_only(OP) : keeps_b_only(OP)) {
+    } else if (ident ? (OP == RB_AND || OP == RB_OR) : has_a ? keeps_a_only(OP) : keeps_b_only(OP)) {
+      // x.and(x) / x.or(x) in place leave x's own containers
       // unmatched key: RoaringArray.appendCopy (RoaringArray.java:184-205)
       const SetView &S = has_a ? a.A : a.B;
       const uint64_t x = has_a ? i0 + ia : j0 + ib;

@@ -70,4 +70,48 @@ void launch_dense_check(const SetView &s, uint32_t nb, uint32_t lo, uint32_t cnt
   k_dense_check<<<(nb + 255) / 256, 256, 0, st>>>(s, nb, lo, cnt, bad);
 }
 
+// RoaringBitmap.runOptimize (RoaringBitmap.java:2764-2775): every container through its runOptimize —
+// ArrayContainer / BitmapContainer become a Run when the Run is strictly smaller (ArrayContainer.java:
+// 1085-1099, BitmapContainer.java:1227-1246), a RunContainer goes through toEfficientContainer
+// (RunContainer.java:2326-2335).  One wave per container: the register bitmap gives c and the maximal
+// runs r, the new type follows, the payload is re-emitted.  Every rule picks the smallest encoding, so
+// the new payload never exceeds the old one and keeps its offset (the same arena layout); keys,
+// cardinalities and offsets are copied by the caller.
+__global__ __launch_bounds__(256) void k_run_optimize(SetView s, uint64_t n, uint8_t *__restrict__ type,
+                                                      uint16_t *__restrict__ nruns, uint8_t *__restrict__ payload) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds[4][2048];
+  const int lane = lane_id();
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  for (uint64_t i = (uint64_t)blockIdx.x * 4 + wv; i < n; i += (uint64_t)gridDim.x * 4) {
+    const int t = s.type[i];
+    const uint32_t card = s.card[i], nr = s.nruns[i];
+    uint64_t w[kW];
+    load_container(t, s.payload + s.off[i], card, nr, lds[wv], w, lane);
+    int c, r;
+    metrics(w, lane, true, c, r);
+    const int ty = t == kRun ? type_eff(c, r) : type_runopt(c, r);
+    emit_container(ty, w, c, r, payload + s.off[i], lds[wv], lane);
+    if (lane == 0) {
+      type[i] = (uint8_t)ty;
+      nruns[i] = (uint16_t)(ty == kRun ? r : 0);
+    }
+    wave_lds_sync(); // the next container restages the wave's scratch
+  }
+}
+// out[b] = 1 when bitmap b holds a Run container (runOptimize's return value)
+__global__ __launch_bounds__(256) void k_any_run(const uint64_t *begin, const uint8_t *type, uint32_t nb, uint8_t *out) {
+  const uint64_t b = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= nb) return;
+  const int lane = lane_id();
+  bool any = false;
+  for (uint64_t i = begin[b] + lane; i < begin[b + 1]; i += 64) any |= type[i] == kRun;
+  const uint64_t m = __ballot(any);
+  if (lane == 0) out[b] = m != 0;
+}
+void launch_run_optimize(const SetView &s, uint64_t n, uint8_t *type, uint16_t *nruns, uint8_t *payload,
+                         uint32_t nb, uint8_t *any_run, hipStream_t st) {
+  if (n) k_run_optimize<<<(unsigned)std::min<uint64_t>((n + 3) / 4, 1u << 16), 256, 0, st>>>(s, n, type, nruns, payload);
+  if (nb && any_run) k_any_run<<<(nb + 3) / 4, 256, 0, st>>>(s.begin, type, nb, any_run);
+}
+
 } // namespace rbg

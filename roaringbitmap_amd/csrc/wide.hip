@@ -304,7 +304,7 @@ __global__ __launch_bounds__(256) void k_wide_reduce(SetView s, CidMap cm,
     ty = a.type;
     c = (int)a.card;
     r = (int)a.nruns;
-  } else if ((SEM == RB_FAST_OR || SEM == RB_PAR_OR) && m == 1) {
+  } else if ((SEM == RB_FAST_OR || SEM == RB_PAR_OR || SEM == RB_BUFFER_NAIVE_OR) && m == 1) {
     // a key seen once: clone, then repairAfterLazy (A, B unchanged; Run -> toEfficientContainer)
     const CRef a = cref(s, cid[lo]);
     inb = alg_bytes_w(a.type, a.card, a.nruns) + 16;
@@ -391,8 +391,9 @@ __global__ __launch_bounds__(256) void k_wide_reduce(SetView s, CidMap cm,
     // horizontal_xor appends the key's result even when it is empty (FastAggregation.java:278)
     ty = SEM == RB_HORIZONTAL_XOR ? t : present && c > 0 ? t : kEmpty;
     if (ty != kEmpty) emit_container(ty, acc, c, r, dst, lds, lane);
-  } else { // RB_PAR_OR with 2..15 containers: clone + lazyIOR chain + repairAfterLazy; RB_HORIZONTAL_OR:
-           // lazyOR of the first two, then the same lazyIOR chain + repairAfterLazy
+  } else { // RB_PAR_OR with 2..15 containers and RB_BUFFER_NAIVE_OR with any count (MutableRoaringBitmap.lazyor
+           // per bitmap): clone + lazyIOR chain + repairAfterLazy; RB_HORIZONTAL_OR: lazyOR of the first two,
+           // then the same lazyIOR chain + repairAfterLazy
     const CRef a = cref(s, cid[lo]);
     inb = alg_bytes_w(a.type, a.card, a.nruns) + 16;
     load_container(a.type, a.p, a.card, a.nruns, lds, acc, lane);
@@ -766,6 +767,7 @@ int wide_run(rbgpu_ctx *ctx, int sem, const rbgpu_set *in, const std::vector<uin
     case RB_NAIVE_AND_ITER: launch_reduce<RB_NAIVE_AND_ITER>(sv, cm, d_seg, d_klist, nk, res->payload, wo, ctx->d_stats, st); break;
     case RB_FAST_XOR: launch_reduce<RB_FAST_XOR>(sv, cm, d_seg, d_klist, nk, res->payload, wo, ctx->d_stats, st, rt); break;
     case RB_PAR_OR: launch_reduce<RB_PAR_OR>(sv, cm, d_seg, d_klist, nk, res->payload, wo, ctx->d_stats, st); break;
+    case RB_BUFFER_NAIVE_OR: launch_reduce<RB_BUFFER_NAIVE_OR>(sv, cm, d_seg, d_klist, nk, res->payload, wo, ctx->d_stats, st); break;
     case RB_HORIZONTAL_OR: launch_reduce<RB_HORIZONTAL_OR>(sv, cm, d_seg, d_klist, nk, res->payload, wo, ctx->d_stats, st); break;
     case RB_HORIZONTAL_XOR: launch_reduce<RB_HORIZONTAL_XOR>(sv, cm, d_seg, d_klist, nk, res->payload, wo, ctx->d_stats, st); break;
     default: launch_reduce<RB_PAR_XOR>(sv, cm, d_seg, d_klist, nk, res->payload, wo, ctx->d_stats, st); break;
@@ -786,6 +788,7 @@ int wide_run(rbgpu_ctx *ctx, int sem, const rbgpu_set *in, const std::vector<uin
                      : sem == RB_WORKSHY_AND ? (fp ? "k_wide_runs_and+k_wide_reduce<WORKSHY_AND>" : "k_wide_reduce<WORKSHY_AND>")
                      : sem == RB_FAST_XOR ? (fp ? "k_wide_runs_xor+k_wide_reduce<FAST_XOR>" : "k_wide_reduce<FAST_XOR>")
                      : sem == RB_PAR_OR ? "k_wide_reduce<PAR_OR>"
+                     : sem == RB_BUFFER_NAIVE_OR ? "k_wide_reduce<BUFFER_NAIVE_OR>"
                      : sem == RB_PAR_XOR ? "k_wide_reduce<PAR_XOR>"
                      : sem == RB_HORIZONTAL_OR ? "k_wide_reduce<HORIZONTAL_OR>"
                      : sem == RB_HORIZONTAL_XOR ? "k_wide_reduce<HORIZONTAL_XOR>" : "k_wide_reduce<NAIVE_AND>";

@@ -211,6 +211,14 @@ class DeviceSet:
     def n_containers(self) -> int:
         return int(L.lib().rbgpu_set_container_count(self.h))
 
+    def run_optimize(self):
+        """RoaringBitmap.runOptimize of every bitmap on the device (rbgpu_set_run_optimize): the new set
+        and, per bitmap, runOptimize's return value (it holds a Run container)."""
+        out = C.c_void_p()
+        flags = np.zeros(max(len(self), 1), np.uint8)
+        L.check(L.lib().rbgpu_set_run_optimize(self.h, C.byref(out), flags.ctypes.data))
+        return DeviceSet(self.ctx, out.value), flags[:len(self)].astype(bool)
+
     def cardinalities(self) -> np.ndarray:
         out = np.zeros(len(self), np.uint64)
         L.check(L.lib().rbgpu_set_cardinalities(self.h, out.ctypes.data_as(L._U64P)))
@@ -389,6 +397,56 @@ class Context:
         L.check(L.lib().rbgpu_pairwise(self.h, op, a.h, b.h, ap, bp, n, C.byref(out)))
         return DeviceSet(self, out.value)
 
+    # ---- 64-bit bitmaps (longlong/)
+    def upload_portable64(self, blobs: Sequence[bytes]) -> "DeviceSet64":
+        """Roaring64NavigableMap.deserializePortable per blob (rbgpu_set64_from_portable)."""
+        n = len(blobs)
+        arr = (C.c_char_p * max(n, 1))(*blobs)
+        lens = np.array([len(b) for b in blobs] or [0], np.uint64)
+        out = C.c_void_p()
+        L.check(L.lib().rbgpu_set64_from_portable(self.h, arr, lens.ctypes.data_as(L._U64P), n, C.byref(out)))
+        return DeviceSet64(self, out.value)
+
+    def upload_values64(self, bitmaps: Sequence[np.ndarray]) -> "DeviceSet64":
+        """bitmapOf(long...) per value list: buckets by the high 32 bits (rbgpu_set64_from_buckets)."""
+        lows, highs, begin = [], [], [0]
+        for vals in bitmaps:
+            v = np.unique(np.asarray(vals, dtype=np.uint64))
+            hi = (v >> np.uint64(32)).astype(np.uint32)
+            for h in np.unique(hi):
+                highs.append(int(h))
+                lows.append((v[hi == h] & np.uint64(0xFFFFFFFF)).astype(np.uint32))
+            begin.append(len(highs))
+        bset = self.upload_values(lows) if lows else self.upload_values([])
+        hs = np.array(highs or [0], np.uint32)
+        bg = np.array(begin, np.uint64)
+        out = C.c_void_p()
+        L.check(L.lib().rbgpu_set64_from_buckets(bset.h, hs.ctypes.data_as(L._U32P), bg.ctypes.data_as(L._U64P),
+                                                 len(bitmaps), C.byref(out)))
+        return DeviceSet64(self, out.value)
+
+    def pairwise64(self, flavor: int, op: int, a: "DeviceSet64", b: "DeviceSet64", a_idx=None, b_idx=None,
+                   npairs=None, inplace: bool = False) -> "DeviceSet64":
+        """rbgpu_pairwise64: Roaring64Bitmap (flavor RB64_BITMAP) static or in-place ops,
+        Roaring64NavigableMap (RB64_NAVIGABLE) in-place ops, over a batch of pairs."""
+        ai, ap = _idx_addr(a_idx)
+        bi, bp = _idx_addr(b_idx)
+        n = npairs if npairs is not None else (len(ai) if ai is not None else min(len(a), len(b)))
+        out = C.c_void_p()
+        L.check(L.lib().rbgpu_pairwise64(self.h, flavor, op, 1 if inplace else 0, a.h, b.h, ap, bp, n, C.byref(out)))
+        return DeviceSet64(self, out.value)
+
+    def pairwise_inplace(self, op: int, a: DeviceSet, b: DeviceSet, a_idx=None, b_idx=None,
+                         npairs=None) -> DeviceSet:
+        """result[i] = a[a_idx[i]] after the in-place a[a_idx[i]].op(b[b_idx[i]]) (rbgpu_pairwise_inplace:
+        RoaringBitmap.and/or/xor/andNot(x2)); the inputs stay unchanged."""
+        ai, ap = _idx_addr(a_idx)
+        bi, bp = _idx_addr(b_idx)
+        n = npairs if npairs is not None else (len(ai) if ai is not None else min(len(a), len(b)))
+        out = C.c_void_p()
+        L.check(L.lib().rbgpu_pairwise_inplace(self.h, op, a.h, b.h, ap, bp, n, C.byref(out)))
+        return DeviceSet(self, out.value)
+
     def pairwise_cardinality(self, op: int, a: DeviceSet, b: DeviceSet, a_idx=None, b_idx=None,
                              npairs=None) -> np.ndarray:
         ai, ap = _idx_addr(a_idx)
@@ -512,6 +570,53 @@ class Comm:
         if self.rank != root:
             return None
         return bytes(buf[:n].cpu().numpy().tobytes())
+
+
+class DeviceSet64:
+    """A batch of 64-bit bitmaps (rbgpu_set64*): buckets (high 32 bits, 32-bit bitmap) in HBM."""
+
+    def __init__(self, ctx: "Context", handle: int):
+        self.ctx = ctx
+        self.h = C.c_void_p(handle)
+
+    def close(self):
+        if self.h and self.h.value:
+            L.lib().rbgpu_set64_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __len__(self) -> int:
+        return int(L.lib().rbgpu_set64_bitmap_count(self.h))
+
+    def cardinalities(self) -> np.ndarray:
+        out = np.zeros(max(len(self), 1), np.uint64)
+        L.check(L.lib().rbgpu_set64_cardinalities(self.h, out.ctypes.data_as(L._U64P)))
+        return out[:len(self)]
+
+    def highs(self, i: int) -> np.ndarray:
+        cnt = C.c_uint64()
+        L.check(L.lib().rbgpu_set64_buckets(self.h, i, None, 0, C.byref(cnt)))
+        out = np.zeros(max(cnt.value, 1), np.uint32)
+        L.check(L.lib().rbgpu_set64_buckets(self.h, i, out.ctypes.data_as(L._U32P), cnt.value, C.byref(cnt)))
+        return out[:cnt.value]
+
+    def serialize_portable(self) -> List[bytes]:
+        n = len(self)
+        if n == 0:
+            return []
+        sizes = np.zeros(n, np.uint64)
+        L.check(L.lib().rbgpu_set64_portable_sizes(self.h, sizes.ctypes.data_as(L._U64P)))
+        total = int(sizes.sum())
+        buf = C.create_string_buffer(max(total, 1))
+        offs = np.zeros(n + 1, np.uint64)
+        L.check(L.lib().rbgpu_set64_serialize_portable(self.h, 0, n, buf, total, offs.ctypes.data_as(L._U64P)))
+        raw = buf.raw
+        return [raw[int(offs[i]):int(offs[i + 1])] for i in range(n)]
 
 
 def assemble_host(parts: Sequence[bytes]) -> bytes:

@@ -218,7 +218,7 @@ class ShardedWide:
         """priorityqueue_or / _xor merge in the order of intermediate result sizes, which are global:
         a key-range shard cannot follow it.  Every rank raises alike (the arguments agree), before any
         collective, as rbgpu_wide_sharded refuses them."""
-        if self.world > 1 and sem in (L.PQ_OR, L.PQ_XOR):
+        if self.world > 1 and sem in L.PQ_SEMS:
             raise ValueError("priorityqueue_or / priorityqueue_xor cannot be key-range sharded")
 
     def aggregate(self, ctx, sem: int, dset, key_range: Tuple[int, int], members=None) -> ShardResult:

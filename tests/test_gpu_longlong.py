@@ -1,0 +1,132 @@
+"""The 64-bit front end on the device (rbgpu_set64 / rbgpu_pairwise64): Roaring64NavigableMap and
+Roaring64Bitmap set algebra byte-exact against the oracle's restatement (oracle/rbref64.py), the
+reference's 64-bit portable fixtures, and the Python mirror classes."""
+import numpy as np
+import pytest
+
+from test_oracle64 import FIXTURES64, read
+
+pytestmark = pytest.mark.gpu
+OPS = {"AND": 0, "OR": 1, "XOR": 2, "ANDNOT": 3}
+
+
+def _values64(rng, n_highs=4, dense=False):
+    highs = rng.choice([0, 1, 2, 7, 1 << 20, (1 << 32) - 2, (1 << 32) - 1], size=n_highs, replace=False)
+    parts = []
+    for h in highs:
+        k = int(rng.integers(1, 4))
+        for key in rng.choice(16, size=k, replace=False):
+            base = (int(h) << 32) | (int(key) << 16)
+            kind = int(rng.integers(0, 3))
+            if kind == 0:
+                lows = rng.choice(65536, size=int(rng.integers(1, 3000)), replace=False)
+            elif kind == 1:
+                lows = rng.choice(65536, size=int(rng.integers(5000, 40000)), replace=False)
+            else:
+                s = int(rng.integers(0, 60000))
+                lows = np.arange(s, s + int(rng.integers(1, 5000))) % 65536
+            parts.append(np.uint64(base) + np.asarray(lows, np.uint64))
+    return np.unique(np.concatenate(parts))
+
+
+@pytest.mark.parametrize("name,card,nb,sel", FIXTURES64, ids=[f[0] for f in FIXTURES64])
+def test_portable_fixtures_on_device(ctx, name, card, nb, sel):
+    data = read(name)
+    s = ctx.upload_portable64([data])
+    assert s.serialize_portable() == [data]
+    assert int(s.cardinalities()[0]) == card and len(s.highs(0)) == nb
+
+
+def _pool(ctx, oracle, seed, n=12):
+    from oracle import rbref64 as R64
+    rng = np.random.default_rng(seed)
+    vals = [_values64(rng, n_highs=int(rng.integers(1, 5))) for _ in range(n)]
+    refs = [R64.Ref64.of(v) for v in vals]
+    for r in refs[::3]:  # some buckets runOptimize'd (Run containers in the mix)
+        for _, b in r.buckets:
+            b.run_optimize()
+    s = ctx.upload_portable64([r.to_portable() for r in refs])
+    return s, refs
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_roaring64_ops(ctx, oracle, seed):
+    import roaringbitmap_amd as rb
+    from oracle import rbref64 as R64
+    s, refs = _pool(ctx, oracle, seed)
+    n = len(refs)
+    ai = np.array([i for i in range(n) for j in range(n)], np.uint32)
+    bi = np.array([j for i in range(n) for j in range(n)], np.uint32)  # includes i == j
+    for opname, op in OPS.items():
+        got_s = ctx.pairwise64(rb.RB64_BITMAP, op, s, s, ai, bi).serialize_portable()
+        got_i = ctx.pairwise64(rb.RB64_BITMAP, op, s, s, ai, bi, inplace=True).serialize_portable()
+        got_n = ctx.pairwise64(rb.RB64_NAVIGABLE, op, s, s, ai, bi, inplace=True).serialize_portable()
+        for k in range(len(ai)):
+            i, j = int(ai[k]), int(bi[k])
+            assert got_s[k] == R64.bitmap_op(op, refs[i], refs[j], False).to_portable(), ("static", opname, i, j)
+            assert got_i[k] == R64.bitmap_op(op, refs[i], refs[j], True, same=i == j).to_portable(), \
+                ("in place", opname, i, j)
+            assert got_n[k] == R64.navigable_op(op, refs[i], refs[j], same=i == j).to_portable(), \
+                ("navigable", opname, i, j)
+
+
+def test_roaring64_empty_xor_containers_and_buckets(ctx, oracle):
+    """Roaring64Bitmap.xor keeps an empty container under its key (card - 1 written as 0xFFFF in the
+    bucket's RoaringFormatSpec bytes); Roaring64NavigableMap.xor leaves an empty bucket; both from equal
+    containers, through the register path of the 32-bit engine (one shared Bitmap, one shared Run)."""
+    import roaringbitmap_amd as rb
+    from oracle import rbref64 as R64
+    same = np.concatenate([np.arange(0, 30000, 3, dtype=np.uint64),                       # Bitmap at key 0
+                           (1 << 16) + np.arange(100, 20000, dtype=np.uint64)])          # Run at key 1
+    x = R64.Ref64.of(np.concatenate([same, (5 << 32) + np.arange(10, dtype=np.uint64)]))
+    y = R64.Ref64.of(np.concatenate([same, (6 << 32) + np.arange(10, dtype=np.uint64)]))
+    for r in (x, y):
+        for _, b in r.buckets:
+            b.run_optimize()
+    s = ctx.upload_portable64([x.to_portable(), y.to_portable()])
+    for inplace in (False, True):
+        got = ctx.pairwise64(rb.RB64_BITMAP, rb.XOR, s, s, [0], [1], inplace=inplace).serialize_portable()[0]
+        want = R64.bitmap_op(rb.XOR, x, y, inplace)
+        assert got == want.to_portable()
+        assert [c[2] for c in want.buckets[0][1].containers()] == [0, 0]
+    got = ctx.pairwise64(rb.RB64_NAVIGABLE, rb.XOR, s, s, [0], [1], inplace=True)
+    assert got.serialize_portable()[0] == R64.navigable_op(rb.XOR, x, y).to_portable()
+    assert list(got.highs(0)) == [0, 5, 6]
+
+
+def test_roaring64_large_batch_general_path(ctx, oracle):
+    """More bucket pairs than the small-batch path takes: the general pipeline with RB_EMPTY_BITMAP pairs."""
+    import roaringbitmap_amd as rb
+    from oracle import rbref64 as R64
+    s, refs = _pool(ctx, oracle, 9, n=40)
+    rng = np.random.default_rng(4)
+    ai = rng.integers(0, 40, 3000).astype(np.uint32)
+    bi = rng.integers(0, 40, 3000).astype(np.uint32)
+    for opname, op in OPS.items():
+        got = ctx.pairwise64(rb.RB64_BITMAP, op, s, s, ai, bi).serialize_portable()
+        for k in range(0, 3000, 37):
+            assert got[k] == R64.bitmap_op(op, refs[ai[k]], refs[bi[k]], False).to_portable(), (opname, k)
+
+
+def test_roaring64_python_mirror(ctx, oracle):
+    import roaringbitmap_amd as rb
+    from oracle import rbref64 as R64
+    rng = np.random.default_rng(12)
+    va, vb = _values64(rng), _values64(rng)
+    for cls, flavor in ((rb.Roaring64NavigableMap, "nav"), (rb.Roaring64Bitmap, "art")):
+        a, b = cls.bitmapOf(va), cls.bitmapOf(vb)
+        ra, rb_ = R64.Ref64.of(va), R64.Ref64.of(vb)
+        assert a.getLongCardinality() == len(va)
+        assert np.array_equal(a.toArray(), va)
+        assert a.serializePortable() == ra.to_portable()
+        for opname, op in OPS.items():
+            x = a.clone()
+            getattr(x, {"AND": "and_", "OR": "or_", "XOR": "xor", "ANDNOT": "andNot"}[opname])(b)
+            want = R64.navigable_op(op, ra, rb_) if flavor == "nav" else R64.bitmap_op(op, ra, rb_, True)
+            assert x.serializePortable() == want.to_portable(), (flavor, opname)
+    r = rb.Roaring64Bitmap.and_(rb.Roaring64Bitmap.bitmapOf(va), rb.Roaring64Bitmap.bitmapOf(vb))
+    assert r.serializePortable() == R64.bitmap_op(rb.AND, R64.Ref64.of(va), R64.Ref64.of(vb), False).to_portable()
+    fx = rb.Roaring64NavigableMap.deserializePortable(read("64mapspreadvals.bin"))
+    assert fx.select(90) == (9 << 32) and fx.select(99) == (9 << 32) + 9
+    with pytest.raises(rb.InvalidArgument):  # Roaring64NavigableMap has no static and/or/xor/andNot
+        ctx.pairwise64(rb.RB64_NAVIGABLE, rb.AND, fx._set, fx._set, [0], [0])

@@ -1,8 +1,8 @@
 """The reference's container-type pins (tests/type_pins.py) through the MI355X path: every pin whose
 entry point the device serves (static and/or/xor/andNot, FastAggregation.or, ParallelAggregation.or,
-bitmapOf construction) must give the pinned type and the oracle's bytes.  Pins with non-canonical
-inputs (32768-value ArrayContainers) run with the canonical form of the same sets; in-place ior and
-runOptimize of a Run container have no device entry point and stay oracle-only (test_type_pins.py)."""
+in-place x1.or(x2) (rbgpu_pairwise_inplace), runOptimize (rbgpu_set_run_optimize), bitmapOf
+construction) must give the pinned type and the oracle's bytes.  Pins with non-canonical inputs
+(32768-value ArrayContainers) run with the canonical form of the same sets."""
 import numpy as np
 import pytest
 
@@ -10,7 +10,11 @@ from type_pins import PINS, RUN, RUN_ARG_SETS, TYPE_NAME, ab_type, one_container
 
 pytestmark = pytest.mark.gpu
 OPS = {"AND": 0, "OR": 1, "XOR": 2, "ANDNOT": 3}
-DEVICE_PINS = [p for p in PINS if p.how.split(":")[0] in ("op", "wide", "build")]
+DEVICE_PINS = [p for p in PINS if p.how.split(":")[0] in ("op", "wide", "build", "inplace", "runopt")]
+
+
+def test_every_pin_runs_on_the_device():
+    assert len(DEVICE_PINS) == len(PINS)
 
 
 @pytest.mark.parametrize("pin", DEVICE_PINS, ids=[p.name for p in DEVICE_PINS])
@@ -21,6 +25,18 @@ def test_type_pin_on_device(ctx, oracle, pin):
     if kind == "build":
         out = ctx.upload_values([inputs[0][1]])
         want = oracle.RefBitmap.of(inputs[0][1]).serialize()
+    elif kind == "runopt":
+        s = ctx.upload_soa(one_container_soa(inputs))
+        out, any_run = s.run_optimize()
+        ref = oracle_bitmap(oracle, *inputs[0])
+        assert bool(any_run[0]) == ref.run_optimize(), pin.cite
+        want = ref.serialize()
+    elif kind == "inplace":
+        s = ctx.upload_soa(one_container_soa(inputs))
+        refs = [oracle_bitmap(oracle, t, v) for t, v in inputs]
+        out = ctx.pairwise_inplace(OPS[what], s, s, [0], [1])
+        oracle.op_inplace(OPS[what], refs[0], refs[1])
+        want = refs[0].serialize()
     else:
         s = ctx.upload_soa(one_container_soa(inputs))
         refs = [oracle_bitmap(oracle, t, v) for t, v in inputs]

@@ -6,15 +6,22 @@ from datasets import DATASETS, EXPECTED, load_realdata, synthetic_bitmaps
 
 pytestmark = pytest.mark.gpu
 SEMS = ["FAST_OR", "FAST_AND", "WORKSHY_AND", "NAIVE_AND", "FAST_XOR", "PAR_OR", "PAR_XOR", "NAIVE_AND_ITER",
-        "HORIZONTAL_OR", "HORIZONTAL_XOR", "PQ_OR", "PQ_XOR"]
-SHARDABLE = [x for x in SEMS if x not in ("PQ_OR", "PQ_XOR")]  # priorityqueue_or/xor: whole results only
+        "HORIZONTAL_OR", "HORIZONTAL_XOR", "PQ_OR", "PQ_XOR",
+        "BUFFER_NAIVE_OR", "BUFFER_PQ_OR", "BUFFER_PQ_OR_ITER", "BUFFER_PQ_XOR"]
+PQ = ("PQ_OR", "PQ_XOR", "BUFFER_PQ_OR", "BUFFER_PQ_OR_ITER", "BUFFER_PQ_XOR")
+SHARDABLE = [x for x in SEMS if x not in PQ]  # priorityqueue_or/xor: whole results only
 
 
 def _check(ctx, oracle, s, refs, sem_name, members):
     import roaringbitmap_amd as rb
     sem = getattr(rb, sem_name)
+    try:
+        want = oracle.wide(getattr(oracle, sem_name), [refs[m] for m in members]).serialize()
+    except ValueError:  # BufferFastAggregation.priorityqueue_xor below 2 bitmaps
+        with pytest.raises(rb.InvalidArgument):
+            ctx.wide(sem, s, members)
+        return
     got = ctx.wide(sem, s, members).serialize()[0]
-    want = oracle.wide(getattr(oracle, sem_name), [refs[m] for m in members]).serialize()
     assert got == want, (sem_name, list(members)[:12])
 
 

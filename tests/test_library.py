@@ -9,7 +9,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def _declared_symbols():
     txt = open(os.path.join(ROOT, "include", "rbgpu.h")).read()
-    return sorted(set(re.findall(r"\b(rbgpu_[a-z_]+)\s*\(", txt)))
+    return sorted(set(re.findall(r"\b(rbgpu_[a-z0-9_]+)\s*\(", txt)))
 
 
 def test_header_symbols_exported():

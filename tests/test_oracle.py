@@ -220,3 +220,55 @@ def test_oracle_sanitizers_clean():
     r = subprocess.run([os.path.join(root, "san_check"), "25", "7"], capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "0 failures" in r.stdout
+
+
+def test_buffer_reference_vectors_on_oracle(oracle):
+    """buffer/TestFastAggregation.java:47-100 on the oracle's BufferFastAggregation restatement."""
+    R = oracle
+    a1 = [39173, 39174]
+    a2 = [39173, 39174, 39175, 39176, 39177, 39178, 39179]
+    p1 = [1232, 3324, 123, 43243, 1322, 7897, 8767]
+    d1, d2, d4 = R.RefBitmap.of(p1), R.RefBitmap.of(a2), R.RefBitmap.of([])
+    want3 = sorted(p1 + a2)
+    assert R.wide(R.NAIVE_AND, [R.RefBitmap.of(a1), d2]).to_array().tolist() == a1
+    for sem in (R.BUFFER_PQ_OR, R.BUFFER_PQ_OR_ITER):
+        assert R.wide(sem, [d1, d2]).to_array().tolist() == want3
+        assert R.wide(sem, [d1]).to_array().tolist() == sorted(p1)
+        assert R.wide(sem, [d1, d4]).to_array().tolist() == sorted(p1)
+        assert R.wide(sem, []).cardinality() == 0
+    assert R.wide(R.BUFFER_PQ_XOR, [d1, d2]).to_array().tolist() == want3
+    import pytest as _pytest
+    for bad in ([d1], []):
+        with _pytest.raises(ValueError):
+            R.wide(R.BUFFER_PQ_XOR, bad)
+
+
+def test_buffer_naive_or_chain_has_no_16_switch(oracle):
+    """naive_or(MutableRoaringBitmap...) folds answer.lazyor(b) (buffer/BufferFastAggregation.java:711-717):
+    the lazyIOR chain of ParallelAggregation.or for any count.  Below 16 containers per key both give the
+    same bytes; at 20 Run containers ParallelAggregation.or starts from a lazy Bitmap (LR -> Bitmap) while
+    the chain stays a Run (RunContainer.ior(Run) -> toEfficientContainer)."""
+    R = oracle
+    bms = []
+    for k in range(20):
+        b = R.RefBitmap.of(np.arange(2000 * k, 2000 * k + 501, dtype=np.uint32))
+        b.run_optimize()
+        bms.append(b)
+    for n in (2, 7, 15):
+        assert R.wide(R.BUFFER_NAIVE_OR, bms[:n]).serialize() == R.wide(R.PAR_OR, bms[:n]).serialize()
+    chain, par = R.wide(R.BUFFER_NAIVE_OR, bms), R.wide(R.PAR_OR, bms)
+    assert np.array_equal(chain.to_array(), par.to_array())
+    assert chain.containers()[0][1] == R.RUN and par.containers()[0][1] == R.BITMAP
+    # one bitmap: its containers cloned then repaired (a Run through toEfficientContainer)
+    assert R.wide(R.BUFFER_NAIVE_OR, bms[:1]).serialize() == R.wide(R.PAR_OR, bms[:1]).serialize()
+
+
+def test_buffer_pq_or_single_is_a_copy(oracle):
+    """BufferFastAggregation.priorityqueue_or of one bitmap returns toMutableRoaringBitmap() (no repair),
+    FastAggregation.priorityqueue_or repairs it: an inefficient Run stays a Run only in the buffer form."""
+    R = oracle
+    from type_pins import RUN, oracle_bitmap
+    x = oracle_bitmap(R, RUN, np.arange(0, 6000, 2, dtype=np.uint32))  # 3000 one-value runs
+    assert R.wide(R.BUFFER_PQ_OR, [x]).containers()[0][1] == R.RUN
+    assert R.wide(R.BUFFER_PQ_OR_ITER, [x]).containers()[0][1] == R.RUN
+    assert R.wide(R.PQ_OR, [x]).containers()[0][1] == R.ARRAY

@@ -1,0 +1,62 @@
+"""The 64-bit oracle (oracle/rbref64.py) pinned by the reference's own 64-bit fixtures: the
+RoaringFormatSpec 64-bit extension files of TestRoaring64NavigableMap.testSerialization_* (CRoaring's
+testdata; TestRoaring64NavigableMap.java:1644-1724) — cardinality, bucket count, select() values and the
+byte-identical re-serialization (checkConsistencyWithResource)."""
+import os
+
+import numpy as np
+import pytest
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "testdata")
+MAXU = (1 << 32) - 1
+# (file, cardinality, buckets, {select index: value})  TestRoaring64NavigableMap.java:1644-1724
+FIXTURES64 = [
+    ("64mapempty.bin", 0, 0, {}),
+    ("64map32bitvals.bin", 10, 1, {0: 0, 9: 9}),
+    ("64mapspreadvals.bin", 100, 10, {0: 0, 9: 9, 90: (9 << 32) + 0, 91: (9 << 32) + 1, 99: (9 << 32) + 9}),
+    ("64maphighvals.bin", 121, 11, {0: ((MAXU - 10) << 32) + (MAXU - 10), 10: ((MAXU - 10) << 32) + MAXU,
+                                    110: (MAXU << 32) + (MAXU - 10), 111: (MAXU << 32) + (MAXU - 9),
+                                    120: (MAXU << 32) + MAXU}),
+]
+
+
+def read(name):
+    with open(os.path.join(GOLD, name), "rb") as f:
+        return f.read()
+
+
+@pytest.mark.parametrize("name,card,nb,sel", FIXTURES64, ids=[f[0] for f in FIXTURES64])
+def test_oracle64_fixtures(name, card, nb, sel):
+    from oracle import rbref64 as R64
+    data = read(name)
+    b = R64.Ref64.from_portable(data)
+    assert b.cardinality() == card and len(b.buckets) == nb
+    vals = b.to_array()
+    for j, v in sel.items():
+        assert int(vals[j]) == v
+    assert b.to_portable() == data
+
+
+def test_oracle64_ops_contract():
+    """The per-class rules the device follows: Roaring64Bitmap keeps an empty xor container under its key,
+    Roaring64NavigableMap keeps a bucket whose RoaringBitmap became empty, x.op(x) takes the `x2 == this`
+    branches; content always equals the set algebra."""
+    from oracle import rbref as R
+    from oracle import rbref64 as R64
+    x = R64.Ref64.of([5, 6, (3 << 32) + 7, (3 << 32) + 70000])
+    y = R64.Ref64.of([5, 6, (3 << 32) + 8, (9 << 32) + 1])
+    art = R64.bitmap_op(R.XOR, x, y, inplace=False)
+    assert [h for h, _ in art.buckets] == [0, 3, 9]
+    assert art.buckets[0][1].containers()[0][2] == 0          # the empty container of key 0 is kept
+    nav = R64.navigable_op(R.XOR, x, y)
+    assert [h for h, _ in nav.buckets] == [0, 3, 9] and nav.buckets[0][1].cardinality() == 0
+    assert len(nav.buckets[0][1].containers()) == 0            # RoaringBitmap.xor drops it; the bucket stays
+    for op in (R.AND, R.OR, R.XOR, R.ANDNOT):
+        sx, sy = set(x.to_array().tolist()), set(y.to_array().tolist())
+        want = {R.AND: sx & sy, R.OR: sx | sy, R.XOR: sx ^ sy, R.ANDNOT: sx - sy}[op]
+        for r in (R64.bitmap_op(op, x, y, False), R64.bitmap_op(op, x, y, True), R64.navigable_op(op, x, y)):
+            assert sorted(r.to_array().tolist()) == sorted(want)
+    assert R64.navigable_op(R.AND, x, y).to_array().tolist() == [5, 6]
+    assert [h for h, _ in R64.navigable_op(R.AND, x, y).buckets] == [0, 3]  # bucket 3 stays, empty
+    assert R64.bitmap_op(R.XOR, x, x, True, same=True).buckets == []
+    assert R64.navigable_op(R.OR, x, x, same=True).to_portable() == x.to_portable()
