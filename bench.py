@@ -188,6 +188,12 @@ SECONDARY_ALL = ["pairwise_ops", "census", "bsi_range", "wide_or", "wide_and_run
 # host, RBGPU_SAME_DEVICE=1 puts every rank on device 0 — together they exercise the N>1 path on a
 # one-GPU box.  The production path is one rank per GPU over RCCL ("nccl").
 BACKEND = os.environ.get("RBGPU_DIST_BACKEND", "nccl")
+# At N > 1 the shard exchange runs inside librbgpu on its own RCCL communicator (rbgpu_comm_*, what a Java
+# caller binds), its 128-byte id handed over through torch.distributed's store before any GPU work;
+# torch.distributed keeps only the barrier and the max-over-ranks timing.  RBGPU_BENCH_COMM=torch
+# selects the Python exchange (sharding.py) instead — the rehearsal on one GPU needs it (RCCL refuses
+# two ranks on one device).
+COMM = os.environ.get("RBGPU_BENCH_COMM", "torch" if os.environ.get("RBGPU_SAME_DEVICE") == "1" else "rccl")
 
 
 def coll_device(local: int = 0):
@@ -211,6 +217,33 @@ class Dist:
                 torch.cuda.set_device(self.local)
             td.init_process_group(BACKEND, rank=self.rank, world_size=self.world)
             self.td = td
+        self.comm, self.uid, self.comm_error = None, None, None
+        if self.world == 1 and COMM == "rccl1":  # a one-rank communicator: the C-ABI exchange path at N = 1
+            from roaringbitmap_amd.engine import Comm
+            self.uid = Comm.unique_id()
+        if self.world > 1 and COMM == "rccl":
+            # the communicator id from rank 0 through the rendezvous store (no GPU touched yet)
+            from roaringbitmap_amd.engine import Comm
+            store = self.td.distributed_c10d._get_default_store()
+            if self.rank == 0:
+                store.set("rbgpu_comm_id", Comm.unique_id().hex())
+            self.uid = bytes.fromhex(store.get("rbgpu_comm_id").decode())
+
+    def open_comm(self, ctx):
+        """librbgpu's RCCL communicator on this rank's GPU (rbgpu_comm_init), once the context exists."""
+        if self.uid is not None and self.comm is None:
+            from roaringbitmap_amd.engine import Comm
+            try:
+                self.comm = Comm(ctx, self.uid, self.world, self.rank)
+            except Exception as e:  # the line records it; the torch.distributed exchange takes over
+                self.comm_error = f"{type(e).__name__}: {e}"
+                print(f"[bench] rank {self.rank}: rbgpu_comm_init failed ({self.comm_error}); "
+                      "falling back to the torch.distributed exchange", file=sys.stderr, flush=True)
+            ok = self.reduce([1.0 if self.comm is not None else 0.0], "sum")[0] if self.td is not None else 1.0
+            if self.comm is not None and ok < self.world:  # every rank uses the same path
+                self.comm.close()
+                self.comm = None
+        return self.comm
 
     @property
     def device(self):
@@ -229,6 +262,8 @@ class Dist:
         return t.cpu().tolist()
 
     def close(self):
+        if self.comm is not None:
+            self.comm.close()
         if self.td is not None:
             self.td.destroy_process_group()
 
@@ -267,16 +302,20 @@ def roofline(main_name, k_ms, k_bytes, traffic, D, extra=None):
 def pairwise_line(D, ctx, rb, a, b, op, steps, warmup, npairs):
     """Config 2 for one op: every rank runs its own npairs pairs (weak scaling); per step the
     ShardedPairwise exchange (all_reduce of result cardinality / containers / bytes) at N > 1."""
-    from roaringbitmap_amd.sharding import ShardedPairwise
-    sp = ShardedPairwise(D.td, D.rank, D.world, D.device) if D.td is not None else None
+    from roaringbitmap_amd.sharding import PairShardResult, ShardedPairwise
+    comm = D.comm
+    sp = ShardedPairwise(D.td, D.rank, D.world, D.device) if D.td is not None and comm is None else None
 
     def step():
         r = ctx.pairwise(op, a, b)
         st = ctx.stats()
         glob = None
-        if sp is not None:
-            glob = sp.finish(None, (0, npairs), st["result_cardinality"], st["result_containers"],
-                             st["output_bytes"])
+        payload = st["output_bytes"] - 16 * st["result_containers"]
+        if comm is not None:  # rbgpu_comm_allreduce_sum: the batch's global cardinality / containers / bytes
+            g = comm.allreduce_sum([st["result_cardinality"], st["result_containers"], payload])
+            glob = PairShardResult(None, (0, npairs), int(g[0]), int(g[1]), int(g[2]))
+        elif sp is not None:
+            glob = sp.finish(None, (0, npairs), st["result_cardinality"], st["result_containers"], payload)
         r.close()
         return st, glob
 
@@ -306,8 +345,9 @@ def pairwise_line(D, ctx, rb, a, b, op, steps, warmup, npairs):
         "roofline_pct_whole_step": round(100.0 * (tot_in + tot_out) / el / 1e9 / (HBM_PEAK_GBS * D.world), 2),
         "result_cardinality_all_ranks": card, "result_containers_rank0": int(last["result_containers"]),
         "parallelism": (f"pair shards x{D.world}: each rank owns its own {npairs} pairs (no data-path collective); "
-                        "per step one all_reduce of (result cardinality, containers, bytes)") if D.world > 1
-        else "single GPU",
+                        "per step one all_reduce of (result cardinality, containers, bytes) over "
+                        + ("librbgpu's RCCL communicator (rbgpu_comm_allreduce_sum)" if comm is not None
+                           else "torch.distributed")) if D.world > 1 else "single GPU",
         "roofline": rl,
     }
 
@@ -429,12 +469,17 @@ def run_bsi(args, D, ctx, rb, steps=5, warmup=2):
     kr = (lo_k, hi_k)
     d = ctx.generate_bsi(BSI_NSLICES, BSI_NROWS, seed=42, key_range=kr if D.world > 1 else None)
     vmin, vmax = 0, (1 << BSI_NSLICES) - 1
-    sb = ShardedBsi(D.td, D.rank, D.world, D.device) if D.td is not None else None
+    comm = D.comm
+    sb = ShardedBsi(D.td, D.rank, D.world, D.device) if D.td is not None and comm is None else None
 
     def step():
-        r = ctx.bsi_compare(rb.BSI_RANGE, d, BSI_LO, BSI_HI, vmin, vmax, key_range=kr)
-        st = ctx.stats()
-        card = sb.finish(r, kr, r.summaries()[0]).cardinality if sb is not None else None
+        if comm is not None:  # rbgpu_bsi_compare_sharded: local key range + summary all-gather in librbgpu
+            r, summ = comm.bsi_compare_sharded(rb.BSI_RANGE, d, BSI_LO, BSI_HI, vmin, vmax, kr)
+            st, card = ctx.stats(), summ["cardinality"]
+        else:
+            r = ctx.bsi_compare(rb.BSI_RANGE, d, BSI_LO, BSI_HI, vmin, vmax, key_range=kr)
+            st = ctx.stats()
+            card = sb.finish(r, kr, r.summaries()[0]).cardinality if sb is not None else None
         r.close()
         return st, card
 
@@ -451,8 +496,9 @@ def run_bsi(args, D, ctx, rb, steps=5, warmup=2):
            "value": round(tot_in / el / 1e9, 3), "unit": "GB/s", "n_gpus": D.world, "steps": steps,
            "ms_per_step": round(el / steps * 1e3, 4), "scaling": "strong",
            "result_cardinality": card, "containers_rank0": ts,
-           "parallelism": (f"high-key range shards x{D.world} (rbgpu_bsi_compare_keys), per step all_gather of "
-                           "shard summaries") if D.world > 1 else "single GPU",
+           "parallelism": (f"high-key range shards x{D.world}, per step all_gather of shard summaries over "
+                           + ("librbgpu's RCCL communicator (rbgpu_bsi_compare_sharded)" if comm is not None
+                              else "torch.distributed (ShardedBsi)")) if D.world > 1 else "single GPU",
            "key_range_rank0": list(kr),
            "roofline": roofline(last["main_kernel"], km, kb, pmc_traffic("rbg::k_bsi_range"), D, {
                "note": "the fused kernel reads every slice container once for both comparators (GE and LE); "
@@ -525,11 +571,18 @@ def run_wide(args, name, D, ctx, rb, nbitmaps, steps, warmup, a=None):
     own = a is None
     if own:
         a = ctx.generate_keys(getattr(rb, wl), nbitmaps, lo, hi, seed=42)
+    from roaringbitmap_amd.sharding import ShardResult
     sem = getattr(rb, sem_name)
-    sw = ShardedWide(D.td, D.rank, D.world, device=D.device) if D.td is not None else None
+    comm = D.comm
+    sw = ShardedWide(D.td, D.rank, D.world, device=D.device) if D.td is not None and comm is None else None
 
     def step():
-        if sw is None:
+        if comm is not None:  # rbgpu_wide_sharded: local key range + summary all-gather in librbgpu
+            r, summ = comm.wide_sharded(sem, a, (lo, hi))
+            st = ctx.stats()
+            res = ShardResult(r, (lo, hi), summ["cardinality"], summ["n_containers"], summ["n_run_containers"],
+                              summ["payload_bytes"], summ["serialized_size"], summ["payload_offset"])
+        elif sw is None:
             r = ctx.wide(sem, a, key_range=(lo, hi))
             st, res = ctx.stats(), None
         else:
@@ -552,8 +605,10 @@ def run_wide(args, name, D, ctx, rb, nbitmaps, steps, warmup, a=None):
         "input_bytes_per_step": int(total_in // steps),
         "key_range_rank0": [lo, hi],
         "containers_rank0": a.type_stats(),
-        "parallelism": f"key-range shards x{D.world}; RCCL all_gather of shard summaries (cardinality, "
-                       f"containers, Run containers, payload bytes) per step" if D.world > 1 else "single GPU",
+        "parallelism": (f"key-range shards x{D.world}; per step all_gather of shard summaries (cardinality, "
+                        "containers, Run containers, payload bytes) over "
+                        + ("librbgpu's RCCL communicator (rbgpu_wide_sharded)" if comm is not None
+                           else "torch.distributed (ShardedWide)")) if D.world > 1 else "single GPU",
         "roofline": roofline(last["main_kernel"], k_ms, k_bytes, pmc_traffic(pmc_name), D),
     }
     out["result_cardinality"] = res.cardinality if res is not None else int(last["result_cardinality"])
@@ -590,12 +645,15 @@ def main():
     D = Dist()
     import roaringbitmap_amd as rb
     ctx = rb.Context(D.local)
+    D.open_comm(ctx)
     seed = 42 + D.rank
     sec = SECONDARY_ALL if args.secondary == "all" else \
         ([] if args.secondary == "none" else [s for s in args.secondary.split(",") if s])
     line = {"metric": METRIC, "higher_is_better": True, "vs_baseline": None, "dtype": "u64",
             "n_gpus": D.world, "steps": args.steps, "warmup": args.warmup,
             "data": "synthetic (device SplitMix64 generator, runOptimize'd containers; SURVEY §8d)"}
+    if D.comm_error:
+        line["comm_fallback"] = D.comm_error
     secondary = {}
 
     if args.workload in WIDE_WORKLOADS or args.workload == "bsi_range":
