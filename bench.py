@@ -218,6 +218,7 @@ class Dist:
             td.init_process_group(BACKEND, rank=self.rank, world_size=self.world)
             self.td = td
         self.comm, self.uid, self.comm_error = None, None, None
+        self.last_step_ms = []
         if self.world == 1 and COMM == "rccl1":  # a one-rank communicator: the C-ABI exchange path at N = 1
             from roaringbitmap_amd.engine import Comm
             self.uid = Comm.unique_id()
@@ -278,12 +279,26 @@ def timed(D, ctx, steps, warmup, step):
     ctx.synchronize()
     sts = []
     t0 = time.perf_counter()
+    marks = [t0]
     for _ in range(steps):
         sts.append(step())
+        marks.append(time.perf_counter())
     ctx.synchronize()
     D.barrier()
     el = D.reduce([time.perf_counter() - t0], "max")[0]
+    # per-step wall times of this rank (a step returns once its results are in HBM: the call reads the
+    # result counts back), for the spread a single mean hides
+    D.last_step_ms = [1e3 * (b - a) for a, b in zip(marks, marks[1:])]
     return el, sts
+
+
+def step_spread(D):
+    """min / median / max of the last timed loop's per-step wall times (rank 0's)."""
+    v = sorted(D.last_step_ms)
+    if not v:
+        return None
+    return {"min": round(v[0], 4), "median": round(float(np.median(v)), 4), "max": round(v[-1], 4),
+            "spread_pct": round(100.0 * (v[-1] - v[0]) / float(np.median(v)), 2)}
 
 
 def roofline(main_name, k_ms, k_bytes, traffic, D, extra=None):
@@ -340,7 +355,7 @@ def pairwise_line(D, ctx, rb, a, b, op, steps, warmup, npairs):
         "workload": f"config2: batched pairwise {OPS[op]} of {npairs} (filter, posting-list) pairs per GPU, "
                     f"mixed Array/Bitmap/Run, 2^18 universe",
         "value": round(tot_in / el / 1e9, 3), "unit": "GB/s", "n_gpus": D.world, "steps": steps,
-        "ms_per_step": round(el / steps * 1e3, 4), "scaling": "weak",
+        "ms_per_step": round(el / steps * 1e3, 4), "step_ms": step_spread(D), "scaling": "weak",
         "input_bytes_per_step_per_gpu": in_b // steps, "output_bytes_per_step_per_gpu": out_b // steps,
         "roofline_pct_whole_step": round(100.0 * (tot_in + tot_out) / el / 1e9 / (HBM_PEAK_GBS * D.world), 2),
         "result_cardinality_all_ranks": card, "result_containers_rank0": int(last["result_containers"]),
@@ -494,7 +509,7 @@ def run_bsi(args, D, ctx, rb, steps=5, warmup=2):
     out = {"workload": f"config5: BSI compare RANGE over {BSI_NSLICES} slices x {BSI_NROWS} rows (2 O'Neil chains "
                        "+ AND, fused into one pass per key)",
            "value": round(tot_in / el / 1e9, 3), "unit": "GB/s", "n_gpus": D.world, "steps": steps,
-           "ms_per_step": round(el / steps * 1e3, 4), "scaling": "strong",
+           "ms_per_step": round(el / steps * 1e3, 4), "step_ms": step_spread(D), "scaling": "strong",
            "result_cardinality": card, "containers_rank0": ts,
            "parallelism": (f"high-key range shards x{D.world}, per step all_gather of shard summaries over "
                            + ("librbgpu's RCCL communicator (rbgpu_bsi_compare_sharded)" if comm is not None
@@ -601,7 +616,7 @@ def run_wide(args, name, D, ctx, rb, nbitmaps, steps, warmup, a=None):
     out = {
         "workload": desc.format(n=nbitmaps),
         "value": round(total_in / el / 1e9, 3), "unit": "GB/s", "n_gpus": D.world, "steps": steps,
-        "ms_per_step": round(el / steps * 1e3, 4), "scaling": "strong",
+        "ms_per_step": round(el / steps * 1e3, 4), "step_ms": step_spread(D), "scaling": "strong",
         "input_bytes_per_step": int(total_in // steps),
         "key_range_rank0": [lo, hi],
         "containers_rank0": a.type_stats(),

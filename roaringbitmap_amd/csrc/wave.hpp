@@ -638,10 +638,17 @@ __device__ __forceinline__ uint32_t emit_container(int type, const uint64_t (&w)
     }
   }
   wave_lds_sync();
-  uint32_t *o = reinterpret_cast<uint32_t *>(out);
-  for (int i = lane; i < runs; i += 64) {
-    uint32_t a = S[i], b = E[i];
-    o[i] = a | ((b - a) << 16);
+  // four runs per lane per trip: 8-B reads of S and E, one 16-B store (the slot is 16-B padded and
+  // holds round16(4 runs) bytes: a Run result has 4r <= 2c <= its slot bound; the pad is zeroed)
+  const uint2 *S2 = reinterpret_cast<const uint2 *>(S), *E2 = reinterpret_cast<const uint2 *>(E);
+  uint4 *o4 = reinterpret_cast<uint4 *>(out);
+  for (int i = lane; 4 * i < runs; i += 64) {
+    const uint2 a = S2[i], b = E2[i];
+    const uint32_t s0 = a.x & 0xFFFF, s1 = a.x >> 16, s2 = a.y & 0xFFFF, s3 = a.y >> 16;
+    const uint32_t e0 = b.x & 0xFFFF, e1 = b.x >> 16, e2 = b.y & 0xFFFF, e3 = b.y >> 16;
+    const int n = runs - 4 * i;
+    o4[i] = make_uint4(s0 | ((e0 - s0) << 16), n > 1 ? s1 | ((e1 - s1) << 16) : 0u,
+                       n > 2 ? s2 | ((e2 - s2) << 16) : 0u, n > 3 ? s3 | ((e3 - s3) << 16) : 0u);
   }
   wave_lds_sync();
   return 4u * (uint32_t)runs;

@@ -234,13 +234,21 @@ __global__ __launch_bounds__(256) void k_wide_runs(SetView s, CidMap cm,
 // KB consecutive keys per wave, the containers of one member bitmap for those keys are adjacent in
 // the SoA arrays, so each metadata load touches a few cache lines instead of 64.
 // Per-lane list: <= kAndCap intervals (start | end << 16) in LDS at L[(b*kAndCap + k)*64 + lane],
-// double-buffered (b = 0/1).  Loads run a 3-stage pipeline (cid of step t+2, metadata of t+1,
-// payload of t in flight while step t-1 computes).  A key with another container type, > 8 runs
-// or a list overflow is routed to the generic kernel (route[q] = 1): results are identical.
+// double-buffered (b = 0/1).  Each step's loads form a chain (container id -> packed record -> runs);
+// every link of it spans several steps (kAndDc / kAndDr / kAndDp below), so a step waits only on
+// loads issued two or more steps earlier.  The loads are unconditional — addresses clamped to a valid
+// member, results discarded past the lane's count — because a load under a branch makes the waitcnt
+// pass wait for every load in flight at the merge (r03 PMC: vmcnt(0) at every step, one memory
+// latency per step).  A key with another container type, > 8 runs or a list overflow is routed to the
+// generic kernel (route[q] = 1): results are identical.
 constexpr int kAndCap = 16;
+constexpr int kAndDc = 3; // steps between a container id's load and its record's load
+constexpr int kAndDr = 3; // steps between a record's load and its runs' load
+constexpr int kAndDp = 3; // steps between the runs' load and their use
+constexpr int kAndU = 6;  // steps per unrolled loop trip: a multiple of Dp, Dp + Dr and Dc
+static_assert(kAndU % kAndDp == 0 && kAndU % (kAndDp + kAndDr) == 0 && kAndU % kAndDc == 0, "ring periods");
 struct AndMeta {
   uint32_t typ, nr;
-  uint64_t off;
 };
 struct AndRuns {
   uint4 r0, r1;
@@ -261,7 +269,7 @@ __device__ __forceinline__ int and_slot(int b, int k, int lane) { return (b * kA
 __device__ __forceinline__ uint32_t iv_s(uint32_t x) { return x & 0xFFFF; }
 __device__ __forceinline__ uint32_t iv_e(uint32_t x) { return x >> 16; }
 
-template <int KB>
+template <int KB, bool DENSE>
 __global__ __launch_bounds__(256) void k_wide_runs_and(SetView s, const uint64_t *__restrict__ mrec, CidMap cm,
                                                        const uint64_t *__restrict__ seg, const uint32_t *__restrict__ klist,
                                                        uint32_t nk, uint8_t *__restrict__ out, WideOut wo,
@@ -282,7 +290,6 @@ __global__ __launch_bounds__(256) void k_wide_runs_and(SetView s, const uint64_t
     lo = seg[key];
     n = seg[key + 1] - lo;
   }
-  const KeyCids cid(cm, lo, key);
   const uint32_t cnt = n > (uint64_t)g ? (uint32_t)((n - g + G - 1) / G) : 0u; // this lane's members
   const uint32_t tmax = __builtin_amdgcn_readfirstlane(wave_max_u32(cnt));
   // the AND identity: one interval [0, 65535]
@@ -290,72 +297,92 @@ __global__ __launch_bounds__(256) void k_wide_runs_and(SetView s, const uint64_t
   L[and_slot(0, 0, lane)] = 0xFFFF0000u;
   bool bad = false;
   uint64_t inb = 0;
-  // metadata: one packed record per container (the set's mrec) instead of type / nruns / off loads;
-  // dense members skip the id load too (the id is the member's base + key)
-  auto ld_cid = [&](uint32_t t) -> uint32_t { return t < cnt ? cid[lo + g + (uint64_t)G * t] : 0u; };
-  auto ld_meta = [&](uint32_t t, uint32_t c) -> AndMeta {
-    AndMeta m{kRun, 0, 0};
-    if (t < cnt) {
-      const uint64_t r = mrec[c];
-      m.typ = rec_type(r);
-      m.nr = rec_nruns(r);
-      m.off = rec_off(r);
-    }
-    return m;
-  };
-  auto ld_runs = [&](uint32_t t, const AndMeta &m) -> AndRuns {
-    AndRuns p{make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0)};
-    if (t < cnt && m.typ == kRun && m.nr <= (uint32_t)kMaxRunsFast) {
-      const uint4 *pp = reinterpret_cast<const uint4 *>(s.payload + m.off);
+  if (tmax) {
+    // load positions: step t reads member g + G min(t, cnt - 1) of the key; a lane without members
+    // borrows the first member of the first lane that has one (loads only, never used)
+    const int fl = (int)__builtin_ctzll(__ballot(cnt != 0u));
+    const uint32_t bg = cnt ? (uint32_t)g : readlane((uint32_t)g, fl);
+    const uint32_t bkey = cnt ? key : readlane(key, fl);
+    const uint64_t blo = cnt ? lo : ((uint64_t)readlane((uint32_t)(lo >> 32), fl) << 32 | readlane((uint32_t)lo, fl));
+    const uint32_t blast = cnt ? cnt - 1 : 0u;
+    // metadata: one packed record per container (the set's mrec) instead of type / nruns / off loads;
+    // dense members skip the id load too (the id is the member's base + key)
+    // the id load's raw value: the dense member base gets the key added where the id is used (an add
+    // right behind the load would make the step wait for it)
+    auto ld_cid = [&](uint32_t t) -> uint32_t {
+      const uint64_t m = bg + (uint64_t)G * min(t, blast); // position in the key's member list
+      if constexpr (DENSE) return reinterpret_cast<const uint32_t *>(cm.mbase)[2 * m]; // the low half (ids are u32)
+      else return cm.cid[blo + m];
+    };
+    const uint32_t cadd = DENSE ? bkey : 0u;
+    auto ld_runs = [&](uint64_t r) -> AndRuns { // a non-Run record reads the arena's first 16 B instead
+      const bool runs = rec_type(r) == (uint32_t)kRun && rec_nruns(r) <= (uint32_t)kMaxRunsFast;
+      const uint4 *pp = reinterpret_cast<const uint4 *>(s.payload + (runs ? rec_off(r) : 0ull));
+      AndRuns p;
       p.r0 = pp[0];
-      if (m.nr > 4) p.r1 = pp[1];
-    }
-    return p;
-  };
-  // pipeline prologue: payload(0), meta(1), cid(2) in flight at the top of step 0
-  AndMeta m0 = ld_meta(0, ld_cid(0));
-  uint32_t c1 = ld_cid(1);
-  AndRuns p0 = ld_runs(0, m0);
-  AndMeta m1 = ld_meta(1, c1);
-  uint32_t c2 = ld_cid(2);
-  for (uint32_t t = 0; t < tmax; ++t) {
-    const AndMeta mt = m0;
-    const AndRuns pt = p0;
-    __builtin_amdgcn_sched_barrier(0);
-    p0 = ld_runs(t + 1, m1);
-    m0 = m1;
-    m1 = ld_meta(t + 2, c2);
-    c2 = ld_cid(t + 3);
-    if (t < cnt && !bad) {
-      if (mt.typ != kRun || mt.nr > (uint32_t)kMaxRunsFast) {
-        bad = true;
-      } else {
-        inb += 4ull * mt.nr + 2 + 16;
-        const int nx = cur ^ 1;
-        int i = 0, k = 0;
-        uint32_t x = L[and_slot(cur, 0, lane)];
+      p.r1 = pp[runs && rec_nruns(r) > 4u ? 1 : 0];
+      return p;
+    };
+    // Rings indexed modulo their length, the loop unrolled over kAndU steps so every slot index is a
+    // constant: rotating the rings through register moves would make each step wait for the loads
+    // the moves read.  At the top of step t: P[t % Dp] = runs of t, R[(t + i) % (Dp + Dr)] = record of
+    // t + i (i < Dp + Dr), C[t % Dc] = id of t + Dp + Dr.  (The runs a step reads were requested at the
+    // end of step t - Dp: Dp - 1 whole steps earlier.)
+    AndRuns P[kAndDp];
+    uint64_t R[kAndDp + kAndDr];
+    uint32_t C[kAndDc];
 #pragma unroll
-        for (int u = 0; u < kMaxRunsFast; ++u) {
-          if (u < (int)mt.nr && i < na) {
-            const uint32_t w = and_run(pt, u);
-            const uint32_t rs = w & 0xFFFF, re = rs + (w >> 16);
-            while (i < na && iv_e(x) < rs) x = L[and_slot(cur, ++i, lane)];
-            while (i < na && iv_s(x) <= re) {
-              const uint32_t a = max(iv_s(x), rs), b = min(iv_e(x), re);
-              if (k < kAndCap) L[and_slot(nx, k, lane)] = a | (b << 16);
-              ++k;
-              if (iv_e(x) > re) break;
-              x = L[and_slot(cur, ++i, lane)];
+    for (int i = 0; i < kAndDp + kAndDr; ++i) R[i] = mrec[ld_cid((uint32_t)i) + cadd];
+#pragma unroll
+    for (int i = 0; i < kAndDc; ++i) C[i] = ld_cid((uint32_t)(kAndDp + kAndDr + i));
+#pragma unroll
+    for (int i = 0; i < kAndDp; ++i) P[i] = ld_runs(R[i]);
+    for (uint32_t t0 = 0; t0 < tmax; t0 += kAndU) {
+#pragma unroll
+      for (int j = 0; j < kAndU; ++j) {
+        const uint32_t t = t0 + (uint32_t)j;
+        const uint64_t rt = R[j % (kAndDp + kAndDr)];
+        const AndMeta mt{rec_type(rt), rec_nruns(rt)};
+        const AndRuns &pt = P[j % kAndDp];
+        if (t < cnt && !bad) {
+          if (mt.typ != kRun || mt.nr > (uint32_t)kMaxRunsFast) {
+            bad = true;
+          } else {
+            inb += 4ull * mt.nr + 2 + 16;
+            const int nx = cur ^ 1;
+            int i = 0, k = 0;
+            uint32_t x = L[and_slot(cur, 0, lane)];
+#pragma unroll
+            for (int u = 0; u < kMaxRunsFast; ++u) {
+              if (u < (int)mt.nr && i < na) {
+                const uint32_t w = and_run(pt, u);
+                const uint32_t rs = w & 0xFFFF, re = rs + (w >> 16);
+                while (i < na && iv_e(x) < rs) x = L[and_slot(cur, ++i, lane)];
+                while (i < na && iv_s(x) <= re) {
+                  const uint32_t a = max(iv_s(x), rs), b = min(iv_e(x), re);
+                  if (k < kAndCap) L[and_slot(nx, k, lane)] = a | (b << 16);
+                  ++k;
+                  if (iv_e(x) > re) break;
+                  x = L[and_slot(cur, ++i, lane)];
+                }
+              }
             }
+            if (k > kAndCap) bad = true;
+            na = k;
+            cur = nx;
           }
         }
-        if (k > kAndCap) bad = true;
-        na = k;
-        cur = nx;
+        // the step's loads go out after its compute, into the slots it has just consumed (a slot
+        // refilled while its old value is still read would need a second register and a copy at the
+        // loop's back edge, which waits for the loads)
+        __builtin_amdgcn_sched_barrier(0);
+        P[j % kAndDp] = ld_runs(R[(j + kAndDp) % (kAndDp + kAndDr)]); // record loaded kAndDr steps ago
+        R[j % (kAndDp + kAndDr)] = mrec[C[j % kAndDc] + cadd];        // id loaded kAndDc steps ago
+        C[j % kAndDc] = ld_cid(t + (uint32_t)(kAndDp + kAndDr + kAndDc));
       }
+      // every lane's list empty (or routed): the remaining containers change nothing
+      if (!__ballot(t0 + kAndU < cnt && !bad && na > 0)) break;
     }
-    // every lane's list empty (or routed): the remaining containers change nothing
-    if ((t & 15) == 15 && !__ballot(t + 1 < cnt && !bad && na > 0)) break;
   }
   // ---- intersect the G lists of each key pairwise
 #pragma unroll
@@ -456,7 +483,10 @@ bool launch_wide_runs(int sem, const SetView &s, const uint64_t *mrec, const Cid
   case RB_WORKSHY_AND: {
     if (!mrec) return false;
     const unsigned waves = (nk + kAndKeys - 1) / kAndKeys;
-    k_wide_runs_and<kAndKeys><<<(waves + 3) / 4, 256, 0, st>>>(s, mrec, cm, seg, klist, nk, out, wo, route, stats);
+    if (cm.cid)
+      k_wide_runs_and<kAndKeys, false><<<(waves + 3) / 4, 256, 0, st>>>(s, mrec, cm, seg, klist, nk, out, wo, route, stats);
+    else
+      k_wide_runs_and<kAndKeys, true><<<(waves + 3) / 4, 256, 0, st>>>(s, mrec, cm, seg, klist, nk, out, wo, route, stats);
     return true;
   }
   case RB_FAST_XOR: // batch-parallel metrics over key-major records (wide_xor.hip)

@@ -462,7 +462,19 @@ struct XWin { // one container per lane: the fast-forward window
 };
 // A window's loads form a chain (record -> run list), so they are software-pipelined over three windows:
 // the records of window w+2 and the runs of w+1 are in flight while window w is processed, and every
-// load issued at an advance only uses values loaded a window earlier.
+// load issued at an advance only uses values loaded a window earlier.  The runs of w+1 go straight to
+// LDS (global_load_lds, 2 KiB in the exact batches' region, `kNextRuns`): as VGPR loads, the window
+// rotation (W = N) made the compiler load into temporaries and copy them right away, which waited for
+// the loads just issued — every window paid the full memory latency (r03 ISA).
+constexpr int kNextRuns = 768; // u32 offset in the wave's region of the next window's runs (r0 x 64 | r1 x 64)
+constexpr int kMCopies = 8, kMStride = 33; // touched-word mask copies (lane & 7), strided over distinct banks
+constexpr int kPcT = 272;                  // u32 offset of pcT (16-B aligned, after the mask copies)
+static_assert(kMCopies * kMStride <= kPcT && kPcT + 256 <= kNextRuns && kNextRuns + 512 <= kXRegion,
+              "mask copies, pcT and the next runs inside the region");
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) void gbl_void_t;
+constexpr int kWaitVm0 = 0x0F70;   // s_waitcnt vmcnt(0)
+constexpr int kWaitLgkm0 = 0xC07F; // s_waitcnt lgkmcnt(0)
 struct XMeta {
   uint32_t typ, card, nr;
   uint64_t off;
@@ -486,11 +498,33 @@ __device__ __forceinline__ XWin xwin_from(const SetView &s, const XMeta &m) {
   const bool runs = m.typ == kRun && m.nr && m.nr <= 8u;
   // a non-Run (or invalid) member reads the arena's first 16 B instead; runs 4..7 exist only if nr > 4
   const uint4 *p = reinterpret_cast<const uint4 *>(s.payload + (runs ? m.off : 0ull));
-  const uint4 a = p[0], b = p[runs && m.nr > 4u ? 1 : 0];
-  const uint4 z = make_uint4(0, 0, 0, 0);
-  w.r0 = runs ? a : z;
-  w.r1 = runs && m.nr > 4u ? b : z;
+  // raw loaded values, no select on them: a select right behind the loads would make the wave wait
+  // for them here, a window early (r03: every window paid the full memory latency).  Only runs u < nr
+  // are ever read, and a lane whose container is not a Run of <= 8 runs routes the key first.
+  w.r0 = p[0];
+  w.r1 = p[runs && m.nr > 4u ? 1 : 0];
   w.pairx = 0;
+  return w;
+}
+// the next window's runs, LDS-DMA into nb (lane-linear: r0 of lane l at nb[4l], r1 at nb[256 + 4l])
+__device__ __forceinline__ void stage_next_runs(const SetView &s, const XMeta &m, uint32_t *nb) {
+  const bool runs = m.typ == kRun && m.nr && m.nr <= 8u;
+  const uint8_t *p = s.payload + (runs ? m.off : 0ull);
+  __builtin_amdgcn_global_load_lds((gbl_void_t *)p, (lds_void_t *)nb, 16, 0, 0);
+  __builtin_amdgcn_global_load_lds((gbl_void_t *)(p + (runs && m.nr > 4u ? 16 : 0)), (lds_void_t *)(nb + 256), 16,
+                                   0, 0);
+}
+// the window staged by stage_next_runs (every load of the previous window waited for first)
+__device__ __forceinline__ XWin take_next(const XMeta &m, const uint32_t *nb, int lane) {
+  __builtin_amdgcn_s_waitcnt(kWaitVm0);
+  XWin w;
+  w.typ = m.typ;
+  w.card = m.card;
+  w.nr = m.nr;
+  w.r0 = reinterpret_cast<const uint4 *>(nb)[lane];
+  w.r1 = reinterpret_cast<const uint4 *>(nb)[64 + lane];
+  w.pairx = 0;
+  __builtin_amdgcn_s_waitcnt(kWaitLgkm0); // read before the next DMA overwrites the slot
   return w;
 }
 // An upper bound of |C_l ⊕ C_l+1| = |C_l| + |C_l+1| - 2 |C_l ∩ C_l+1| for every lane l (meaningful on
@@ -510,6 +544,18 @@ __device__ __forceinline__ void pair_xor(XWin &w) {
   const int sb = (int)(nbest & 0xFFFF), eb = sb + (int)(nbest >> 16);
   const int inter = w.nr ? max(0, min(ea, eb) - max(sa, sb) + 1) : 0;
   w.pairx = w.card + cb - 2u * (uint32_t)inter;
+}
+// the boundary toggles of the lane's runs into the toggle image
+__device__ __forceinline__ void toggle_runs(const XWin &w, uint32_t *acc) {
+  const uint32_t rw[8] = {w.r0.x, w.r0.y, w.r0.z, w.r0.w, w.r1.x, w.r1.y, w.r1.z, w.r1.w};
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    if ((uint32_t)u < w.nr) {
+      const uint32_t st = rw[u] & 0xFFFF, e1 = st + (rw[u] >> 16) + 1;
+      atomicXor(&acc[st >> 5], 1u << (st & 31));
+      if (e1 < (uint32_t)kSpan) atomicXor(&acc[e1 >> 5], 1u << (e1 & 31));
+    }
+  }
 }
 constexpr int kXorMinFast = 8; // shortest stretch worth a fast-forward (an exact batch costs ~32 stretches' steps)
 // Union stretches.  The pair bounds above limit an AB stretch to about one window when the members'
@@ -561,15 +607,19 @@ __global__ __launch_bounds__(256, 3) void k_wide_runs_xor(SetView s, const uint6
     return rec[i < hi ? i : hi - 1];
   };
   const uint64_t r0 = rec_at(lo + lane), r1 = rec_at(lo + 64 + lane);
+  uint32_t *nbuf = R + kNextRuns;
   XWin W = xwin_from(s, xmeta_of(r0, lo + lane < hi));       // window w
-  XWin N = xwin_from(s, xmeta_of(r1, lo + 64 + lane < hi));  // w+1: runs in flight
+  XMeta Nm = xmeta_of(r1, lo + 64 + lane < hi);              // w+1: runs in flight into nbuf
+  stage_next_runs(s, Nm, nbuf);
   uint64_t NN = rec_at(lo + 128 + lane);                     // w+2: record in flight
   pair_xor(W);
   uint64_t base = lo;
   // union stretch state: windows whose toggles are pending in acc (P = Pw, X describe the accumulator
   // before them) and their touched-word mask M (in R, which only exact batches use otherwise)
-  uint32_t *M = R;                                      // [32] touched 64-bit words (1024 bits)
-  uint8_t *pcT = reinterpret_cast<uint8_t *>(R + 32);   // [1024] popcount of each word of P
+  // M: the touched 64-bit words (1024 bits, 32 dwords) in kMCopies copies, lane l marking copy l & 7 —
+  // one copy took every member's core run on one dword, serialising 64 atomics per instruction
+  uint32_t *M = R;
+  uint8_t *pcT = reinterpret_cast<uint8_t *>(R + kPcT); // [1024] popcount of each word of P
   int upend = 0;
   bool urun = false; // flavour of the pending stretch: Run (every step stays a Run) or AB
   int usum = 0;      // Run flavour: Σ nruns of the pending windows (r_j <= X.r + usum)
@@ -577,8 +627,13 @@ __global__ __launch_bounds__(256, 3) void k_wide_runs_xor(SetView s, const uint6
 #if RBG_STUDY
   int tr_u = 0, tr_f = 0, tr_rej = 0, tr_p = 0, tr_pb = 0, tr_e = 0;
 #define RBG_TR(x) x
+  uint64_t tt[6] = {0, 0, 0, 0, 0, 0}, ts = 0; // s_memtime: mark+check, toggles, flush, stretch, exact, advance
+#define RBG_TS() ts = __builtin_amdgcn_s_memtime()
+#define RBG_TA(i) { const uint64_t t_ = __builtin_amdgcn_s_memtime(); tt[i] += t_ - ts; ts = t_; }
 #else
 #define RBG_TR(x)
+#define RBG_TS()
+#define RBG_TA(i)
 #endif
   // the pending windows' XOR into P and (c, r) re-measured: the state is AB(c) (AB flavour) or Run
   auto flush_union = [&]() {
@@ -599,7 +654,6 @@ __global__ __launch_bounds__(256, 3) void k_wide_runs_xor(SetView s, const uint6
     upend = 0;
     wave_lds_sync();
   };
-  static_assert(kXRegion >= 32 + 256, "M and pcT fit the exact batches' region");
   while (base < hi) {
     const uint32_t posw = __builtin_amdgcn_readfirstlane((uint32_t)(base - wbase)); // < 64
     const bool inwin = (uint32_t)lane >= posw && wbase + (uint64_t)lane < hi;
@@ -614,13 +668,15 @@ __global__ __launch_bounds__(256, 3) void k_wide_runs_xor(SetView s, const uint6
     const bool ab_in = X.state == kBitmap || (X.state == kArray && X.c >= kXorUnionMinC);
     const bool run_in = X.state == kRun && X.rvalid && X.c >= kXorUnionMinC &&
                         X.r + wnr <= 2047 && X.c >= 4 * (X.r + wnr); // |P \ U'| ~ c / 2 after a window
+    bool took = false; // the window went into a union stretch
+    RBG_TS();
     if (fastfwd && posw == 0 && (upend || ab_in || run_in)) {
       // ---- union stretch: mark the window's words, then |P \ U'| decides (see "Union stretches" above)
       const bool mem = (uint32_t)lane < wlen;
       if (!upend) { // a new stretch: clear U', and the per-word popcounts of P for |P \ U'|
         urun = !ab_in;
         usum = 0;
-        if (lane < 32) M[lane] = 0u;
+        for (int i = lane; i < kMCopies * kMStride; i += 64) M[i] = 0u;
 #pragma unroll
         for (int k = 0; k < 8; ++k)
           reinterpret_cast<uint16_t *>(pcT)[64 * k + lane] =
@@ -635,10 +691,11 @@ __global__ __launch_bounds__(256, 3) void k_wide_runs_xor(SetView s, const uint6
             const uint32_t st = rw[u] & 0xFFFF, en = st + (rw[u] >> 16);
             const uint32_t w0 = st >> 6, w1 = en >> 6, d0 = w0 >> 5, d1 = w1 >> 5;
             const uint32_t mlo = 0xFFFFFFFFu << (w0 & 31), mhi = 0xFFFFFFFFu >> (31 - (w1 & 31));
-            atomicOr(&M[d0], d0 == d1 ? (mlo & mhi) : mlo);
+            uint32_t *Mc = M + kMStride * (lane & (kMCopies - 1));
+            atomicOr(&Mc[d0], d0 == d1 ? (mlo & mhi) : mlo);
             if (d1 != d0) {
-              atomicOr(&M[d1], mhi);
-              for (uint32_t d = d0 + 1; d < d1; ++d) atomicOr(&M[d], 0xFFFFFFFFu); // runs over 2048 values
+              atomicOr(&Mc[d1], mhi);
+              for (uint32_t d = d0 + 1; d < d1; ++d) atomicOr(&Mc[d], 0xFFFFFFFFu); // runs over 2048 values
             }
           }
         }
@@ -648,7 +705,10 @@ __global__ __launch_bounds__(256, 3) void k_wide_runs_xor(SetView s, const uint6
       uint32_t ls = 0;
       {
         const uint4 pcv = reinterpret_cast<const uint4 *>(pcT)[lane];
-        const uint32_t tv = (M[lane >> 1] >> (16 * (lane & 1))) & 0xFFFFu;
+        uint32_t mv = 0;
+#pragma unroll
+        for (int c = 0; c < kMCopies; ++c) mv |= M[kMStride * c + (lane >> 1)];
+        const uint32_t tv = (mv >> (16 * (lane & 1))) & 0xFFFFu;
         const uint32_t p4[4] = {pcv.x, pcv.y, pcv.z, pcv.w};
 #pragma unroll
         for (int qd = 0; qd < 4; ++qd) {
@@ -660,127 +720,119 @@ __global__ __launch_bounds__(256, 3) void k_wide_runs_xor(SetView s, const uint6
         ls = (ls & 0xFFFFu) + (ls >> 16);
       }
       const int L = (int)wave_sum_u32(ls);
+      RBG_TA(0);
       const int rub = X.r + usum + wnr; // >= every r_j of the stretch (Run flavour)
       if (urun ? (2 + 4 * rub <= min(kBitmapBytes, 2 * L + 2)) : L >= kRunArrayThreshold) {
         usum += wnr;
         if (mem) {
-          const uint32_t rw[8] = {W.r0.x, W.r0.y, W.r0.z, W.r0.w, W.r1.x, W.r1.y, W.r1.z, W.r1.w};
-#pragma unroll
-          for (int u = 0; u < 8; ++u) {
-            if ((uint32_t)u < W.nr) {
-              const uint32_t st = rw[u] & 0xFFFF, e1 = st + (rw[u] >> 16) + 1;
-              atomicXor(&acc[st >> 5], 1u << (st & 31));
-              if (e1 < (uint32_t)kSpan) atomicXor(&acc[e1 >> 5], 1u << (e1 & 31));
-            }
-          }
+          toggle_runs(W, acc);
           X.inb += 4u * W.nr + 2u + 16u;
         }
         ++upend;
         RBG_TR(++tr_u);
+        RBG_TA(1);
         base += wlen;
+        took = true; // on to the one shared window advance below
+      }
+      // this window would let U' cover too much of P: close the stretch before it and take the window
+      // again as the first of a fresh stretch (U' then holds its words alone); a window refused as
+      // the first of a stretch goes to the per-window rules
+      else {
+        RBG_TR(++tr_rej);
+        if (upend) {
+          RBG_TR(++tr_f);
+          flush_union();
+          RBG_TA(2);
+          continue;
+        }
+      }
+    }
+    if (!took) { // the per-window rules: a pair-bounded stretch, or an exact batch
+      if (!wpx) { // the window's pair bounds, computed only where the per-window rules need them
+        pair_xor(W);
+        wpx = true;
+      }
+      // ---- the longest stretch from posw that provably crosses no threshold (see above)
+      const int nr_first = (int)readlane(W.nr, (int)posw), card_first = (int)readlane(W.card, (int)posw);
+      const uint32_t first_even = posw + (posw & 1u);
+      const uint32_t pair_in = dpp<0x138>(W.pairx); // wave_shr:1 — the pair (lane-1, lane) on its odd lane
+      const bool odd_end = inwin && (lane & 1) && (uint32_t)lane >= first_even + 1u;
+      const int S = (int)wave_scan_u32(odd_end ? pair_in : 0u, lane);
+      const bool open_pair = inwin && (uint32_t)lane >= first_even && (((uint32_t)lane - first_even) & 1u) == 0;
+      const int bound = ((posw & 1u) ? card_first : 0) + S + (open_pair ? (int)W.card : 0); // >= |X_j|
+      const int ab_ok_first = X.state == kBitmap || (X.state == kArray && X.c >= kRunArrayThreshold) ||
+                              (X.state == kRun && (X.r - nr_first > 2047 || 2 * (X.r - nr_first) > X.c + card_first));
+      bool ok = false;
+      int mode = 0; // 1: AB stretch, 2: Run stretch
+      if (ab_ok_first) {
+        mode = 1;
+        ok = inwin && X.c - bound >= kRunArrayThreshold;
+      } else if (X.state == kRun) {
+        mode = 2;
+        const int rub = X.r + (int)wave_scan_u32(inwin ? W.nr : 0u, lane), clb = X.c - bound;
+        ok = inwin && clb >= 1 && 2 + 4 * rub <= min(kBitmapBytes, 2 * clb + 2);
+      }
+      const uint64_t okm = __ballot(ok) >> posw;
+      // leading members within the bounds (all 64 when posw == 0 and ~okm == 0: ctz of 0 is undefined)
+      const uint32_t B = fastfwd ? min(~okm ? (uint32_t)__builtin_ctzll(~okm) : 64u, wlen - posw) : 0u;
+      if (B >= kXorMinFast || (B >= 1 && posw + B == wlen)) {
+        if ((uint32_t)lane >= posw && (uint32_t)lane < posw + B) {
+          toggle_runs(W, acc);
+          X.inb += 4u * W.nr + 2u + 16u;
+        }
         wave_lds_sync();
-        if (base < hi) {
-          wbase += 64;
-          W = N;
-          N = xwin_from(s, xmeta_of(NN, wbase + 64 + lane < hi));
-          NN = rec_at(wbase + 128 + lane);
-          wpx = false;
-        }
-        continue;
-      }
-      // this window would let U' cover too much of P: close the stretch before it, and take the
-      // window again (a fresh stretch, or the per-window rules)
-      RBG_TR(++tr_rej);
-      if (upend) {
-        RBG_TR(++tr_f);
-        flush_union();
-      }
-    }
-    if (!wpx) { // the window's pair bounds, computed only where the per-window rules need them
-      pair_xor(W);
-      wpx = true;
-    }
-    // ---- the longest stretch from posw that provably crosses no threshold (see above)
-    const int nr_first = (int)readlane(W.nr, (int)posw), card_first = (int)readlane(W.card, (int)posw);
-    const uint32_t first_even = posw + (posw & 1u);
-    const uint32_t pair_in = dpp<0x138>(W.pairx); // wave_shr:1 — the pair (lane-1, lane) on its odd lane
-    const bool odd_end = inwin && (lane & 1) && (uint32_t)lane >= first_even + 1u;
-    const int S = (int)wave_scan_u32(odd_end ? pair_in : 0u, lane);
-    const bool open_pair = inwin && (uint32_t)lane >= first_even && (((uint32_t)lane - first_even) & 1u) == 0;
-    const int bound = ((posw & 1u) ? card_first : 0) + S + (open_pair ? (int)W.card : 0); // >= |X_j|
-    const int ab_ok_first = X.state == kBitmap || (X.state == kArray && X.c >= kRunArrayThreshold) ||
-                            (X.state == kRun && (X.r - nr_first > 2047 || 2 * (X.r - nr_first) > X.c + card_first));
-    bool ok = false;
-    int mode = 0; // 1: AB stretch, 2: Run stretch
-    if (ab_ok_first) {
-      mode = 1;
-      ok = inwin && X.c - bound >= kRunArrayThreshold;
-    } else if (X.state == kRun) {
-      mode = 2;
-      const int rub = X.r + (int)wave_scan_u32(inwin ? W.nr : 0u, lane), clb = X.c - bound;
-      ok = inwin && clb >= 1 && 2 + 4 * rub <= min(kBitmapBytes, 2 * clb + 2);
-    }
-    const uint64_t okm = __ballot(ok) >> posw;
-    // leading members within the bounds (all 64 when posw == 0 and ~okm == 0: ctz of 0 is undefined)
-    const uint32_t B = fastfwd ? min(~okm ? (uint32_t)__builtin_ctzll(~okm) : 64u, wlen - posw) : 0u;
-    if (B >= kXorMinFast || (B >= 1 && posw + B == wlen)) {
-      if ((uint32_t)lane >= posw && (uint32_t)lane < posw + B) {
-        const uint32_t rw[8] = {W.r0.x, W.r0.y, W.r0.z, W.r0.w, W.r1.x, W.r1.y, W.r1.z, W.r1.w};
+        uint64_t t[kW];
+        lds_read_words(acc, t, lane);
+        wave_lds_sync();
+        lds_zero(acc, lane);
+        toggles_to_words(t, lane);
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          if ((uint32_t)u < W.nr) {
-            const uint32_t st = rw[u] & 0xFFFF, e1 = st + (rw[u] >> 16) + 1;
-            atomicXor(&acc[st >> 5], 1u << (st & 31));
-            if (e1 < (uint32_t)kSpan) atomicXor(&acc[e1 >> 5], 1u << (e1 & 31));
-          }
-        }
-        X.inb += 4u * W.nr + 2u + 16u;
-      }
-      wave_lds_sync();
-      uint64_t t[kW];
-      lds_read_words(acc, t, lane);
-      wave_lds_sync();
-      lds_zero(acc, lane);
-      toggles_to_words(t, lane);
-#pragma unroll
-      for (int j = 0; j < kW; ++j) Pw[j] ^= t[j];
-      // an AB stretch leaves a Bitmap / Array accumulator whose next rule reads only c (AB), so r is
-      // counted again only when a rule can read it (Run stretch, exact batch, the result)
-      int cc = X.c, rr = X.r;
-      metrics(Pw, lane, mode == 2, cc, rr);
-      X.c = cc;
-      X.r = rr;
-      X.rvalid = mode == 2;
-      X.state = mode == 1 ? type_ab(cc) : kRun;
-      base += B;
-      RBG_TR(++tr_p; tr_pb += B);
-    } else {
-      if (!X.rvalid) {
-        int cc, rr;
-        metrics(Pw, lane, true, cc, rr);
+        for (int j = 0; j < kW; ++j) Pw[j] ^= t[j];
+        // an AB stretch leaves a Bitmap / Array accumulator whose next rule reads only c (AB), so r is
+        // counted again only when a rule can read it (Run stretch, exact batch, the result)
+        int cc = X.c, rr = X.r;
+        metrics(Pw, lane, mode == 2, cc, rr);
+        X.c = cc;
         X.r = rr;
-        X.rvalid = 1;
+        X.rvalid = mode == 2;
+        X.state = mode == 1 ? type_ab(cc) : kRun;
+        base += B;
+        RBG_TR(++tr_p; tr_pb += B);
+        RBG_TA(3);
+      } else {
+        if (!X.rvalid) {
+          int cc, rr;
+          metrics(Pw, lane, true, cc, rr);
+          X.r = rr;
+          X.rvalid = 1;
+        }
+        lds_write_words(acc, Pw, lane);
+        __builtin_amdgcn_s_waitcnt(kWaitVm0); // the next window's runs land before the batch reuses R
+        wave_lds_sync();
+        if (!exact_batch(s, rec, base, hi, acc, R, lane, X)) {
+          fail_route = true;
+          break;
+        }
+        lds_read_words(acc, Pw, lane);
+        wave_lds_sync();
+        lds_zero(acc, lane);
+        stage_next_runs(s, Nm, nbuf); // the batch overwrote them: again
+        base += kXB;
+        RBG_TR(++tr_e);
+        RBG_TA(4);
       }
-      lds_write_words(acc, Pw, lane);
-      wave_lds_sync();
-      if (!exact_batch(s, rec, base, hi, acc, R, lane, X)) {
-        fail_route = true;
-        break;
-      }
-      lds_read_words(acc, Pw, lane);
-      wave_lds_sync();
-      lds_zero(acc, lane);
-      base += kXB;
-      RBG_TR(++tr_e);
     }
     wave_lds_sync();
+    RBG_TS();
     if (base >= wbase + 64 && base < hi) {
       wbase += 64;
-      W = N;
-      N = xwin_from(s, xmeta_of(NN, wbase + 64 + lane < hi));
+      W = take_next(Nm, nbuf, lane);
+      Nm = xmeta_of(NN, wbase + 64 + lane < hi);
+      stage_next_runs(s, Nm, nbuf);
       NN = rec_at(wbase + 128 + lane);
       wpx = false;
     }
+    RBG_TA(5);
   }
   if (fail_route) {
     if (lane == 0) route[q] = 1;
@@ -792,8 +844,9 @@ __global__ __launch_bounds__(256, 3) void k_wide_runs_xor(SetView s, const uint6
   }
 #if RBG_STUDY
   if (lane == 0 && (q == 1000 || q == 30000 || q == 65000))
-    printf("xor trace key %u: union windows %d flushes %d refused %d | per-window stretches %d (members %d) | exact %d | c %d state %d\n",
-           q, tr_u, tr_f, tr_rej, tr_p, tr_pb, tr_e, X.c, X.state);
+    printf("xor trace key %u: union windows %d flushes %d refused %d | per-window stretches %d (members %d) | exact %d | c %d state %d"
+           " | cycles mark %lu toggles %lu flush %lu stretch %lu exact %lu advance %lu\n",
+           q, tr_u, tr_f, tr_rej, tr_p, tr_pb, tr_e, X.c, X.state, tt[0], tt[1], tt[2], tt[3], tt[4], tt[5]);
 #endif
   // ---- result
   uint8_t *dst = out + (uint64_t)q * kBitmapBytes;
