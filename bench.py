@@ -323,18 +323,21 @@ def pairwise_line(D, ctx, rb, a, b, op, steps, warmup, npairs):
 
     def step():
         r = ctx.pairwise(op, a, b)
-        st = ctx.stats()
+        st = ctx.stats_raw()  # the struct; converted to a dict after the timed loop
         glob = None
-        payload = st["output_bytes"] - 16 * st["result_containers"]
-        if comm is not None:  # rbgpu_comm_allreduce_sum: the batch's global cardinality / containers / bytes
-            g = comm.allreduce_sum([st["result_cardinality"], st["result_containers"], payload])
-            glob = PairShardResult(None, (0, npairs), int(g[0]), int(g[1]), int(g[2]))
-        elif sp is not None:
-            glob = sp.finish(None, (0, npairs), st["result_cardinality"], st["result_containers"], payload)
+        if comm is not None or sp is not None:
+            payload = st.output_bytes - 16 * st.result_containers
+            if comm is not None:  # rbgpu_comm_allreduce_sum: the batch's global cardinality / containers / bytes
+                g = comm.allreduce_sum([st.result_cardinality, st.result_containers, payload])
+                glob = PairShardResult(None, (0, npairs), int(g[0]), int(g[1]), int(g[2]))
+            else:
+                glob = sp.finish(None, (0, npairs), st.result_cardinality, st.result_containers, payload)
         r.close()
         return st, glob
 
+    from roaringbitmap_amd.engine import stats_dict
     el, sts = timed(D, ctx, steps, warmup, step)
+    sts = [(stats_dict(s), g) for s, g in sts]
     in_b, out_b = sum(s["input_bytes"] for s, _ in sts), sum(s["output_bytes"] for s, _ in sts)
     tot_in, tot_out = D.reduce([float(in_b), float(out_b)])
     last, glob = sts[-1]

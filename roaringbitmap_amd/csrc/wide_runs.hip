@@ -293,8 +293,12 @@ __global__ __launch_bounds__(256) void k_wide_runs_and(SetView s, const uint64_t
   const uint32_t cnt = n > (uint64_t)g ? (uint32_t)((n - g + G - 1) / G) : 0u; // this lane's members
   const uint32_t tmax = __builtin_amdgcn_readfirstlane(wave_max_u32(cnt));
   // the AND identity: one interval [0, 65535]
+  // A list of at most one interval lives in registers (one = [sa, sb] when na == 1): after the first
+  // members a key's intersection is one interval (config 4: the shared core run), and a step against
+  // it is a few min / max per run, with none of the LDS round trips of the list walk.
   int cur = 0, na = 1;
-  L[and_slot(0, 0, lane)] = 0xFFFF0000u;
+  bool one = true;
+  uint32_t sa = 0, sb = 65535;
   bool bad = false;
   uint64_t inb = 0;
   if (tmax) {
@@ -347,6 +351,37 @@ __global__ __launch_bounds__(256) void k_wide_runs_and(SetView s, const uint64_t
         if (t < cnt && !bad) {
           if (mt.typ != kRun || mt.nr > (uint32_t)kMaxRunsFast) {
             bad = true;
+          } else if (one) {
+            inb += 4ull * mt.nr + 2 + 16;
+            if (na) {
+              uint32_t k = 0, ns = 0, ne = 0;
+#pragma unroll
+              for (int u = 0; u < kMaxRunsFast; ++u) {
+                const uint32_t w = and_run(pt, u);
+                const uint32_t a = max(sa, w & 0xFFFF), b = min(sb, (w & 0xFFFF) + (w >> 16));
+                const bool v = u < (int)mt.nr && a <= b;
+                k += v ? 1u : 0u;
+                ns = v ? a : ns;
+                ne = v ? b : ne;
+              }
+              if (k <= 1) {
+                na = (int)k;
+                sa = ns;
+                sb = ne;
+              } else { // the pieces (runs are sorted and disjoint, so are they) to the LDS list
+                const int nx = cur ^ 1;
+                int o = 0;
+#pragma unroll
+                for (int u = 0; u < kMaxRunsFast; ++u) {
+                  const uint32_t w = and_run(pt, u);
+                  const uint32_t a = max(sa, w & 0xFFFF), b = min(sb, (w & 0xFFFF) + (w >> 16));
+                  if (u < (int)mt.nr && a <= b) L[and_slot(nx, o++, lane)] = a | (b << 16);
+                }
+                na = (int)k;
+                cur = nx;
+                one = false;
+              }
+            }
           } else {
             inb += 4ull * mt.nr + 2 + 16;
             const int nx = cur ^ 1;
@@ -370,6 +405,12 @@ __global__ __launch_bounds__(256) void k_wide_runs_and(SetView s, const uint64_t
             if (k > kAndCap) bad = true;
             na = k;
             cur = nx;
+            if (na <= 1 && !bad) { // back to registers
+              const uint32_t x1 = L[and_slot(cur, 0, lane)];
+              sa = na ? iv_s(x1) : 0u;
+              sb = na ? iv_e(x1) : 0u;
+              one = true;
+            }
           }
         }
         // the step's loads go out after its compute, into the slots it has just consumed (a slot
@@ -383,6 +424,10 @@ __global__ __launch_bounds__(256) void k_wide_runs_and(SetView s, const uint64_t
       // every lane's list empty (or routed): the remaining containers change nothing
       if (!__ballot(t0 + kAndU < cnt && !bad && na > 0)) break;
     }
+  }
+  if (one) { // the register list into the LDS list for the tree and the emission
+    cur = 0;
+    if (na) L[and_slot(0, 0, lane)] = sa | (sb << 16);
   }
   // ---- intersect the G lists of each key pairwise
 #pragma unroll

@@ -313,6 +313,16 @@ def _idx_addr(arr):
     return a, a.__array_interface__["data"][0]
 
 
+def stats_dict(s: "L.RbStats") -> dict:
+    """rb_stats as a dict: the scalar fields, main_kernel, and one entry per timed kernel span."""
+    out = {k: getattr(s, k) for k, _ in s._fields_ if not k.startswith("kernel_")}
+    out["main_kernel"] = s.main_kernel.decode()
+    out["kernels"] = [{"name": s.kernel_name[i].value.decode(), "ms": s.kernel_ms[i],
+                       "bytes": int(s.kernel_bytes[i]), "items": int(s.kernel_items[i])}
+                      for i in range(s.n_kernels)]
+    return out
+
+
 class Context:
     """One MI355X: a HIP stream, workspaces and an allocation cache (rbgpu_ctx*)."""
 
@@ -341,14 +351,14 @@ class Context:
         L.check(L.lib().rbgpu_synchronize(self.h))
 
     def stats(self) -> dict:
+        return stats_dict(self.stats_raw())
+
+    def stats_raw(self) -> "L.RbStats":
+        """The last call's rb_stats as the ctypes struct (rbgpu_get_stats), for loops that convert it
+        later (`stats_dict`) rather than build a dict per call."""
         s = L.RbStats()
         L.check(L.lib().rbgpu_get_stats(self.h, C.byref(s)))
-        out = {k: getattr(s, k) for k, _ in s._fields_ if not k.startswith("kernel_")}
-        out["main_kernel"] = s.main_kernel.decode()
-        out["kernels"] = [{"name": s.kernel_name[i].value.decode(), "ms": s.kernel_ms[i],
-                           "bytes": int(s.kernel_bytes[i]), "items": int(s.kernel_items[i])}
-                          for i in range(s.n_kernels)]
-        return out
+        return s
 
     # ---- sets
     def upload_serialized(self, blobs: Sequence[bytes]) -> DeviceSet:
