@@ -40,7 +40,7 @@ OPS = ["AND", "OR", "XOR", "ANDNOT"]
 
 
 def _traffic_json():
-    for rnd in ("r02", "r01"):
+    for rnd in ("r03", "r02", "r01"):
         p = os.path.join(ROOT, "profiles", rnd, "traffic.json")
         if os.path.exists(p):
             return p
@@ -570,7 +570,7 @@ WIDE_WORKLOADS = {
                 "config3: FastAggregation.or of {n} dense bitmaps over the full 2^32 universe"),
     "wide_and_runs": ("WL_WIDE_RUNS", "FAST_AND", 4096, "rbg::k_wide_runs_and", 256,
                       "config4: FastAggregation.and (workShyAnd) of {n} run-heavy bitmaps x 65536 keys"),
-    "wide_xor_runs": ("WL_WIDE_RUNS", "FAST_XOR", 4096, "rbg::k_xor_records_dense+rbg::k_wide_runs_xor", 256,
+    "wide_xor_runs": ("WL_WIDE_RUNS", "FAST_XOR", 4096, "rbg::k_wide_runs_xor", 256,
                       "config4: FastAggregation.xor (naive_xor) of {n} run-heavy bitmaps x 65536 keys"),
 }
 # the all-core CPU baseline of each wide semantic: ParallelAggregation where the reference has one,

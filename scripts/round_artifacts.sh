@@ -10,4 +10,5 @@ scripts/gpu_steps.sh \
   "bench:300:python bench.py > gpurun_out/art/bench.json" \
   "stats:300:rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/art/stats -o run -- python3 bench.py > gpurun_out/art/bench_under_rocprof.json" \
   "pmc_fetch:240:timeout -s KILL 200 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/art/pmc/p1 -o run -- $P" \
-  "pmc_write:240:timeout -s KILL 200 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/art/pmc/p2 -o run -- $P"
+  "pmc_write:240:timeout -s KILL 200 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/art/pmc/p2 -o run -- $P" \
+  "pmc_tcc:240:timeout -s KILL 200 rocprofv3 --pmc TCC_BUSY_avr TCC_REQ_sum TCC_HIT_sum --output-format csv -d gpurun_out/art/pmc/p3 -o run -- $P --secondary none"
