@@ -227,8 +227,16 @@ class Dist:
             from roaringbitmap_amd.engine import Comm
             store = self.td.distributed_c10d._get_default_store()
             if self.rank == 0:
-                store.set("rbgpu_comm_id", Comm.unique_id().hex())
-            self.uid = bytes.fromhex(store.get("rbgpu_comm_id").decode())
+                try:
+                    uid = Comm.unique_id().hex()
+                except Exception as e:  # no RCCL id: every rank takes the torch.distributed exchange
+                    uid = ""
+                    self.comm_error = f"{type(e).__name__}: {e}"
+                    print(f"[bench] rbgpu_comm_unique_id failed ({self.comm_error}); "
+                          "the torch.distributed exchange takes over", file=sys.stderr, flush=True)
+                store.set("rbgpu_comm_id", uid)
+            v = store.get("rbgpu_comm_id").decode()
+            self.uid = bytes.fromhex(v) if v else None
 
     def open_comm(self, ctx):
         """librbgpu's RCCL communicator on this rank's GPU (rbgpu_comm_init), once the context exists."""
