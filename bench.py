@@ -690,8 +690,9 @@ def main():
             w = run_wide(args, args.workload, D, ctx, rb, nb, args.steps, args.warmup)
             if D.world == 1 and not args.no_cpu_baseline:
                 w["cpu_baseline"] = wide_cpu_baseline(ctx, rb, args.workload, args.cpu_seconds / 2)
-        line.update({"value": w["value"], "unit": "GB/s", "ms_per_step": w["ms_per_step"], "scaling": "strong",
-                     "config": {k: v for k, v in w.items() if k not in ("value", "roofline", "ms_per_step",
+        line.update({"value": w["value"], "unit": "GB/s", "ms_per_step": w["ms_per_step"], "step_ms": w["step_ms"],
+                     "scaling": "strong",
+                     "config": {k: v for k, v in w.items() if k not in ("value", "roofline", "ms_per_step", "step_ms",
                                                                         "cpu_baseline", "unit", "steps", "n_gpus")},
                      "roofline": w["roofline"]})
         if "cpu_baseline" in w:
@@ -706,7 +707,8 @@ def main():
     a, b = ctx.generate(rb.WL_FILTER_POSTING, args.pairs, seed=seed)
     ctx.synchronize()
     h = pairwise_line(D, ctx, rb, a, b, op, args.steps, args.warmup, args.pairs)
-    line.update({"value": h["value"], "unit": "GB/s", "ms_per_step": h["ms_per_step"], "scaling": "weak",
+    line.update({"value": h["value"], "unit": "GB/s", "ms_per_step": h["ms_per_step"], "step_ms": h["step_ms"],
+                 "scaling": "weak",
                  "config": {"workload": h["workload"], "units_per_gpu": args.pairs, "unit": "pairs",
                             "input_bytes_per_step_per_gpu": h["input_bytes_per_step_per_gpu"],
                             "output_bytes_per_step_per_gpu": h["output_bytes_per_step_per_gpu"],
