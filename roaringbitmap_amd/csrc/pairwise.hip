@@ -629,6 +629,7 @@ __global__ __launch_bounds__(256, ROLE == kRoleHeavy ? kHeavyWaves : kLightWaves
   uint4 pq[8], qq[8];
 #if RBG_STUDY
   uint64_t lt_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, lt0 = 0, lt1 = 0, lt2 = 0; // decode, stage B/A/R, copy, filter, iteration, tasks
+  uint64_t lt_wait = 0; // heavy: cycles waiting for the task's payload loads (an explicit vmcnt(0) at its start)
 #define RBG_LT(x) if (ROLE == kRoleLight) { x; }
 #define RBG_HT(x) if (ROLE == kRoleHeavy) { x; }
 #else
@@ -677,6 +678,13 @@ __global__ __launch_bounds__(256, ROLE == kRoleHeavy ? kHeavyWaves : kLightWaves
     if (ROLE == kRoleHeavy && !done) {
       // ---- the result as a register bitmap: P = A, Q = B (never swapped: ANDNOT and the type
       //      rules are ordered)
+#if RBG_STUDY
+      {
+        const uint64_t tw0 = __builtin_amdgcn_s_memtime();
+        __builtin_amdgcn_s_waitcnt(0x0F70); // vmcnt(0)
+        lt_wait += __builtin_amdgcn_s_memtime() - tw0;
+      }
+#endif
       uint64_t w[kW];
       if (bitmap_payload(tc.tp, tc.cp)) {
 #pragma unroll
@@ -808,8 +816,8 @@ __global__ __launch_bounds__(256, ROLE == kRoleHeavy ? kHeavyWaves : kLightWaves
     printf("light timing blk %u: decode %lu stageB %lu stageA %lu stageR %lu copy %lu filter %lu iter %lu tasks %lu\n",
            blockIdx.x, lt_acc[0], lt_acc[1], lt_acc[2], lt_acc[3], lt_acc[4], lt_acc[5], lt_acc[6], lt_acc[7]);
   if (ROLE == kRoleHeavy && lane == 0 && wv == 0 && blockIdx.x % 61 == 0)
-    printf("heavy timing op %d blk %u: decode %lu build %lu metrics %lu emitB %lu emitA %lu emitR %lu iter %lu tasks %lu\n",
-           OP, blockIdx.x, lt_acc[0], lt_acc[1], lt_acc[2], lt_acc[3], lt_acc[4], lt_acc[5], lt_acc[6], lt_acc[7]);
+    printf("heavy timing op %d blk %u: decode %lu build %lu (payload wait %lu) metrics %lu emitB %lu emitA %lu emitR %lu iter %lu tasks %lu\n",
+           OP, blockIdx.x, lt_acc[0], lt_acc[1], lt_wait, lt_acc[2], lt_acc[3], lt_acc[4], lt_acc[5], lt_acc[6], lt_acc[7]);
 #endif
 }
 
