@@ -1061,7 +1061,8 @@ static int pairwise_impl(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu
   if (card_out && np) HIPCHK(hipMemsetAsync(pcard, 0, np * 8, st));
 
   stats_begin(ctx);
-  PairArgs pa{op, a->view(), b->view(), d_aidx, d_bidx, npairs, seg_begin, nullptr, 0, seg_keys, inplace, a == b};
+  PairArgs pa{op, a->view(), b->view(), d_aidx, d_bidx, npairs, seg_begin, nullptr, 0, seg_keys, inplace, a == b,
+              a->nc, b->nc};
   uint64_t *const tot = ctx->h_pinned;
   uint64_t ns = 0;
   // one segment per pair when no pair can exceed seg_keys merged keys (config 2: <= 8 keys per

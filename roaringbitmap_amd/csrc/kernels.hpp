@@ -27,6 +27,7 @@ struct PairArgs {
   // with equal indices is one bitmap with itself — x.and(x) / x.or(x) leave x as it is, x.xor(x) /
   // x.andNot(x) clear it (RoaringBitmap.java:1271, 1347-1350, 2482, 3297-3300)
   int inplace, same;
+  uint64_t a_nc, b_nc; // containers in A / B (a short segment's clamped loads need one to exist)
 };
 // per task result metadata (workspace, indexed like tasks)
 struct TaskMeta {
