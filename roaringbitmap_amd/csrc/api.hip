@@ -73,6 +73,7 @@ void ctx_unref(rbgpu_ctx *ctx) {
   if (ctx->side) (void)hipStreamSynchronize(ctx->side);
   for (auto &e : ctx->ev) (void)hipEventDestroy(e);
   for (auto &e : ctx->ev_side) (void)hipEventDestroy(e);
+  (void)hipEventDestroy(ctx->ev_tot);
   (void)hipFree(ctx->d_stats);
   (void)hipHostFree(ctx->h_pinned);
   (void)hipHostFree(ctx->h_stats);
@@ -454,6 +455,7 @@ int rbgpu_open(int device, rbgpu_ctx **out) {
   }
   for (auto &e : c->ev) (void)hipEventCreate(&e);
   for (auto &e : c->ev_side) (void)hipEventCreate(&e);
+  (void)hipEventCreate(&c->ev_tot);
   *out = c;
   return RB_OK;
 }
@@ -987,7 +989,11 @@ static int pairwise_small(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgp
 
 // probe: 0 = the product path; 1 / 2 = measurement probes (rbgpu_internal_probe) in place of the
 // task kernel — results are not produced.
-static int pairwise_impl(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu_set *b, const uint32_t *a_idx,
+static // tasks bound up to which pairwise_impl reserves the task workspace before the totals are read back
+// (58 B per task: 928 MiB at the cap)
+constexpr uint64_t kEarlyEmitTasks = 1ull << 24;
+
+int pairwise_impl(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu_set *b, const uint32_t *a_idx,
                          const uint32_t *b_idx, uint32_t npairs, rbgpu_set **out, uint64_t *card_out,
                          int probe = 0, bool inplace = false, bool keep_empty = false) {
   int rc = check_ctx(ctx);
@@ -1081,54 +1087,84 @@ static int pairwise_impl(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu
     LAUNCHCHK();
     ns = np ? tot[6] : 0;
   }
-  // ---- per segment: counts, scans, result counts / offsets
-  need = aligned256(ns * 4) + 10 * aligned256((ns + 1) * 8) + aligned256(scan_multi_tmp_words(ns + 1, 4) * 8) + 256;
+  // ---- per segment: counts, block totals and their scans, result counts / offsets
+  const uint64_t nblk = pair_blocks(ns);
+  need = aligned256(ns * 4) + 6 * aligned256((ns + 1) * 8) + 10 * aligned256((nblk + 1) * 8) + 4 * 256;
   if (ctx->ws_segs.reserve(need, st) != hipSuccess) return fail(RB_ENOMEM, "segment workspace");
   Workspace &G = ctx->ws_segs;
   uint32_t *seg_pair = G.take<uint32_t>(std::max<uint64_t>(ns, 1));
   PairCountArrays cnt{G.take<uint64_t>(ns + 1), G.take<uint64_t>(ns + 1), G.take<uint64_t>(ns + 1),
                       G.take<uint64_t>(ns + 1)};
-  PairCountArrays scn{G.take<uint64_t>(ns + 1), G.take<uint64_t>(ns + 1), G.take<uint64_t>(ns + 1),
-                      G.take<uint64_t>(ns + 1)};
-  uint64_t *rcnt = G.take<uint64_t>(ns + 1), *rseg = G.take<uint64_t>(ns + 1);
-  uint64_t *tmp = G.take<uint64_t>(std::max<uint64_t>(scan_multi_tmp_words(ns + 1, 4), 1));
+  PairCountArrays bt{G.take<uint64_t>(nblk + 1), G.take<uint64_t>(nblk + 1), G.take<uint64_t>(nblk + 1),
+                     G.take<uint64_t>(nblk + 1)};
+  PairCountArrays bs{G.take<uint64_t>(nblk + 1), G.take<uint64_t>(nblk + 1), G.take<uint64_t>(nblk + 1),
+                     G.take<uint64_t>(nblk + 1)};
+  uint64_t *task_begin = G.take<uint64_t>(ns + 1), *rseg = G.take<uint64_t>(ns + 1);
+  uint64_t *bk = G.take<uint64_t>(nblk + 1), *bks = G.take<uint64_t>(nblk + 1);
   uint64_t *d_tot = G.take<uint64_t>(4);
-  if (ident_segs) launch_seg_identity(np, seg_begin, seg_pair, st);
-  else launch_seg_fill(pa, seg_begin, seg_pair, st);
-  pa.seg_pair = seg_pair;
+  // one segment per pair: no segment maps at all (the kernels take segment p as pair p)
+  if (!ident_segs) launch_seg_fill(pa, seg_begin, seg_pair, st);
+  pa.seg_pair = ident_segs ? nullptr : seg_pair;
   pa.nseg = ns;
-  launch_pair_count(pa, cnt, ctx->d_stats, st);
-  const uint64_t *scan_in[4] = {cnt.task, cnt.light, cnt.big, cnt.small};
-  uint64_t *scan_out[4] = {scn.task, scn.light, scn.big, scn.small};
-  scan_exclusive_multi(scan_in, scan_out, 4, ns, tmp, d_tot, st);
+  launch_pair_count(pa, cnt, bt, ctx->d_stats, st);
+  if (ns) {
+    const uint64_t *scan_in[4] = {bt.task, bt.light, bt.big, bt.small};
+    uint64_t *scan_out[4] = {bs.task, bs.light, bs.big, bs.small};
+    scan_blocks_multi(scan_in, scan_out, 4, nblk, d_tot, st);
+  }
   HIPCHK(hipMemcpyAsync(tot, d_tot, 4 * 8, hipMemcpyDeviceToHost, st));
-  HIPCHK(hipStreamSynchronize(st));
+  // Early emission: with identity pairing every container of A and of B takes at most one task, so
+  // a.nc + b.nc bounds the task count before the totals are on the host.  The task workspace is then
+  // sized by that bound and the emit kernel reads the totals on the device: it runs while the host
+  // waits for the totals, allocates the result and launches the task kernels.  Otherwise the host
+  // reads the totals first (the bound is the segments' key capacity, too loose to reserve).
+  const uint64_t seg_cap = ns * (uint64_t)seg_keys;
+  const uint64_t tbound = !d_aidx && !d_bidx ? std::min<uint64_t>(a->nc + b->nc, seg_cap) : seg_cap;
+  const bool early = !probe && ns && tbound <= kEarlyEmitTasks;
+  TaskMeta tm{};
+  tm.lazy = is_lazy_op(op) ? op : 0;
+  tm.inplace = inplace;
+  tm.keep_empty = keep_empty;
+  TaskRec *light = nullptr;
+  unsigned long long *queue = nullptr;
+  // one record array (the light records, then the heavy ones) and the per-task metadata, for nt tasks
+  auto take_tasks = [&](uint64_t nt) -> int {
+    const uint64_t nt1 = std::max<uint64_t>(nt, 1);
+    const size_t tneed = aligned256(nt1 * sizeof(TaskRec)) + 2 * aligned256(nt1 * 2) + 2 * aligned256(nt1) +
+                         aligned256(nt1 * 4) + aligned256(nt1 * 8) + aligned256(4096) + 256;
+    if (ctx->ws_tasks.reserve(tneed, st) != hipSuccess)
+      return fail(RB_ENOMEM, "task workspace (%llu tasks)", (unsigned long long)nt);
+    Workspace &T = ctx->ws_tasks;
+    light = T.take<TaskRec>(nt1);
+    tm.key = T.take<uint16_t>(nt1);
+    tm.nruns = T.take<uint16_t>(nt1);
+    tm.type = T.take<uint8_t>(nt1);
+    tm.cat = T.take<uint8_t>(nt1);
+    tm.card = T.take<uint32_t>(nt1);
+    tm.out = T.take<uint64_t>(nt1);
+    queue = T.take<unsigned long long>(512); // light-task chunk counters (<= 32, 128 B apart)
+    return RB_OK;
+  };
+  if (early) {
+    if ((rc = take_tasks(tbound))) return rc;
+    HIPCHK(hipEventRecord(ctx->ev_tot, st));
+    launch_pair_emit(pa, cnt, bs, 0, light, nullptr, tm, task_begin, d_tot, tbound, st);
+    HIPCHK(hipEventSynchronize(ctx->ev_tot));
+  } else {
+    HIPCHK(hipStreamSynchronize(st));
+  }
   LAUNCHCHK();
   if (!ns) tot[0] = tot[1] = tot[2] = tot[3] = 0;
   const uint64_t ntasks = tot[0], nlight = tot[1], nheavy = ntasks - nlight, nbig_t = tot[2], small_t = tot[3];
   const uint64_t small_base = nbig_t * kBitmapBytes;
   const uint64_t arena = card_only ? 0 : small_base + small_t;
-
-  const uint64_t nt1 = std::max<uint64_t>(ntasks, 1);
-  size_t tneed = aligned256(std::max<uint64_t>(nlight, 1) * sizeof(TaskRec)) +
-                 aligned256(std::max<uint64_t>(nheavy, 1) * sizeof(TaskRec)) + 2 * aligned256(nt1 * 2) +
-                 2 * aligned256(nt1) + aligned256(nt1 * 4) + aligned256(nt1 * 8) + aligned256(4096) + 256;
-  if (ctx->ws_tasks.reserve(tneed, st) != hipSuccess)
-    return fail(RB_ENOMEM, "task workspace (%llu tasks)", (unsigned long long)ntasks);
-  Workspace &T = ctx->ws_tasks;
-  TaskRec *light = T.take<TaskRec>(std::max<uint64_t>(nlight, 1));
-  TaskRec *heavy = T.take<TaskRec>(std::max<uint64_t>(nheavy, 1));
-  TaskMeta tm{};
-  tm.lazy = is_lazy_op(op) ? op : 0;
-  tm.inplace = inplace;
-  tm.keep_empty = keep_empty;
-  tm.key = T.take<uint16_t>(nt1);
-  tm.nruns = T.take<uint16_t>(nt1);
-  tm.type = T.take<uint8_t>(nt1);
-  tm.cat = T.take<uint8_t>(nt1);
-  tm.card = T.take<uint32_t>(nt1);
-  tm.out = T.take<uint64_t>(nt1);
-  unsigned long long *queue = T.take<unsigned long long>(512); // light-task chunk counters (<= 32, 128 B apart)
+  if (early && ntasks > tbound) { // never expected: the emit dropped the records past the bound
+    (void)hipStreamSynchronize(st);
+    return fail(RB_EDEVICE, "pairwise: %llu tasks exceed the bound %llu", (unsigned long long)ntasks,
+                (unsigned long long)tbound);
+  }
+  if (!early && (rc = take_tasks(ntasks))) return rc;
+  TaskRec *heavy = light + nlight;
 
   rbgpu_set *res = nullptr;
   if (!card_only) {
@@ -1136,6 +1172,7 @@ static int pairwise_impl(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu
     rc = set_alloc(ctx, res, npairs, ntasks, arena);
     if (rc) {
       delete res;
+      (void)hipStreamSynchronize(st); // the early emit may still write the workspace
       return rc;
     }
   }
@@ -1147,7 +1184,7 @@ static int pairwise_impl(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu
   static const bool static_light = getenv("RBGPU_STATIC_LIGHT") != nullptr;
   const bool conc = !probe && !serial && nlight && nheavy && nlight + nheavy >= 65536; // small batches: the
                                                   // cross-stream waits cost more than the overlap
-  launch_pair_emit(pa, scn, small_base, light, heavy, tm, st);
+  if (!early) launch_pair_emit(pa, cnt, bs, small_base, light, heavy, tm, task_begin, nullptr, 0, st);
   // the queue counters are zeroed before ev[1]: the side stream waits on ev[1] before its light launch
   if (conc && !static_light) HIPCHK(hipMemsetAsync(queue, 0, 4096, st));
   HIPCHK(hipEventRecord(ctx->ev[1], st));
@@ -1179,15 +1216,22 @@ static int pairwise_impl(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu
                     tm, st, ctx->ev[2]);
   }
   HIPCHK(hipEventRecord(ctx->ev[3], st));
-  launch_compact_count(scn.task, ns, tm.type, rcnt, st);
-  scan_exclusive(rcnt, rseg, ns, tmp, st);
+  launch_compact_count(task_begin, ns, tm.type, bk, st);
+  // the block totals' scan total is the result container count: stats word 8, read back with the
+  // counters by stats_end
+  if (ns) {
+    const uint64_t *kin[1] = {bk};
+    uint64_t *kout[1] = {bks};
+    scan_blocks_multi(kin, kout, 1, nblk, ctx->d_stats + 8 * kStripes, st);
+  }
   OutView ov{};
   if (res) ov = OutView{res->key, res->type, res->card, res->nruns, res->off};
-  launch_compact_write(scn.task, ns, tm, rseg, ov, seg_pair, card_out ? pcard : nullptr, ctx->d_stats, st);
-  if (res && np) launch_pair_rbegin(seg_begin, npairs, rseg, res->begin, st);
-  else if (res) HIPCHK(hipMemsetAsync(res->begin, 0, 8, st));
-  if (np) HIPCHK(hipMemcpyAsync(ctx->h_pinned + 5, rseg + ns, 8, hipMemcpyDeviceToHost, st));
-  else ctx->h_pinned[5] = 0;
+  // one segment per pair: the compaction writes the result CSR itself; else per segment, mapped below
+  uint64_t *rb_direct = res && ident_segs ? res->begin : nullptr;
+  launch_compact_write(task_begin, ns, tm, bks, ov, pa.seg_pair, card_out ? pcard : nullptr, ctx->d_stats,
+                       res && !ident_segs ? rseg : nullptr, rb_direct, st);
+  if (res && np && !ident_segs) launch_pair_rbegin(seg_begin, npairs, rseg, res->begin, nullptr, st);
+  else if (res && !np) HIPCHK(hipMemsetAsync(res->begin, 0, 8, st));
   if (card_out && np) HIPCHK(hipMemcpyAsync(card_out, pcard, np * 8, hipMemcpyDeviceToHost, st));
   if (conc) {
     // [0] the concurrent task phase (both kernels' bytes over the union of their spans), then each
@@ -1200,7 +1244,7 @@ static int pairwise_impl(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu
     rc = stats_end(ctx, ntasks, 0, spans, 2);
   }
   if (rc) return rc;
-  const uint64_t nres = ctx->h_pinned[5];
+  const uint64_t nres = np ? ctx->words[8] : 0;
   ctx->last.result_containers = nres;
   if (res) {
     res->nc = nres;

@@ -143,6 +143,7 @@ struct rbgpu_ctx {
   hipStream_t side = nullptr; // second stream: the heavy task kernel runs beside the light one
   hipEvent_t ev[6] = {};   // [0] call start, [1..n] around the compute kernels, [5] call end
   hipEvent_t ev_side[3] = {}; // around the kernel on `side`; [2] after the side stream's last launch
+  hipEvent_t ev_tot = {};     // pairwise: after the read-back of the scan totals (the early emit runs past it)
   rbg::DevPool pool;
   rbg::Workspace ws_pairs, ws_tasks, ws_segs; // per pair / per task / per merge-path segment
   uint64_t *d_stats = nullptr;  // [kStatWords * kStripes] striped algorithmic byte counters

@@ -11,6 +11,9 @@ void scan_exclusive(const uint64_t *in, uint64_t *out, uint64_t n, uint64_t *tmp
 // k scans of n words each (k <= 4); totals[i] = out[i][n].  One launch when n fits one block.
 void scan_exclusive_multi(const uint64_t *const *in, uint64_t *const *out, int k, uint64_t n, uint64_t *tmp,
                           uint64_t *totals, hipStream_t st);
+// the same for short arrays (per-block totals, n up to ~1M) in one launch; totals may be null
+void scan_blocks_multi(const uint64_t *const *in, uint64_t *const *out, int k, uint64_t n, uint64_t *totals,
+                       hipStream_t st);
 
 // ---- pairwise.hip
 struct PairArgs {
@@ -20,7 +23,7 @@ struct PairArgs {
   const uint32_t *bidx; // may be null (identity)
   uint32_t npairs;
   const uint64_t *seg_begin; // [npairs + 1] first merge-path segment of each pair
-  const uint32_t *seg_pair;  // [nseg] pair of each segment
+  const uint32_t *seg_pair;  // [nseg] pair of each segment; null: one segment per pair (segment p = pair p)
   uint64_t nseg;
   uint32_t seg_keys; // merged keys per segment (a power of two in [8, 256])
   // in-place x1.op(x2) (RoaringBitmap.and/or/xor/andNot(x2)): `same` = A and B are one set, so a pair
@@ -56,15 +59,23 @@ struct PairCountArrays {
 // merge-path segments of every pair (<= 256 merged keys each): counts, then the segment -> pair map
 void launch_seg_count(const PairArgs &a, uint64_t *nseg, hipStream_t st);
 void launch_seg_fill(const PairArgs &a, const uint64_t *seg_begin, uint32_t *seg_pair, hipStream_t st);
-void launch_seg_identity(uint64_t np, uint64_t *seg_begin, uint32_t *seg_pair, hipStream_t st);
 void launch_max_span(const uint64_t *begin, uint32_t nb, uint64_t *out, hipStream_t st);
 void launch_max_runs(const uint8_t *type, const uint16_t *nruns, uint64_t n, uint64_t *out, hipStream_t st);
+// result CSR per pair (rbegin may be null) and the result container count into *count (may be null)
 void launch_pair_rbegin(const uint64_t *seg_begin, uint32_t npairs, const uint64_t *rseg, uint64_t *rbegin,
-                        hipStream_t st);
+                        uint64_t *count, hipStream_t st);
 // per segment from here on
-void launch_pair_count(const PairArgs &a, const PairCountArrays &c, uint64_t *stats, hipStream_t st);
-void launch_pair_emit(const PairArgs &a, const PairCountArrays &scans, uint64_t small_base, TaskRec *light,
-                      TaskRec *heavy, const TaskMeta &tm, hipStream_t st);
+// per-block layout (segments in blocks of pair_blocks' size): c = each segment's counts, bt = each
+// block's totals; the emit reads the counts and the exclusive scans of the block totals (bs)
+uint64_t pair_blocks(uint64_t nseg);
+void launch_pair_count(const PairArgs &a, const PairCountArrays &c, const PairCountArrays &bt, uint64_t *stats,
+                       hipStream_t st);
+// tot non-null: heavy and small_base come from the device totals (heavy = light + tot[1]) and the
+// workspace holds cap tasks (nothing is written when tot[0] exceeds it)
+// task_begin[p] = segment p's first task ([nseg] = the total), for the compaction
+void launch_pair_emit(const PairArgs &a, const PairCountArrays &cnt, const PairCountArrays &bs, uint64_t small_base,
+                      TaskRec *light, TaskRec *heavy, const TaskMeta &tm, uint64_t *task_begin, const uint64_t *tot,
+                      uint64_t cap, hipStream_t st);
 // light records: copies + subset-of-an-Array filters; heavy records: the register path.  `mid` is
 // recorded between the two persistent launches.
 void launch_pairwise(int op, bool card_only, const uint8_t *pa, const uint8_t *pb, const TaskRec *light,
@@ -79,11 +90,13 @@ void launch_pairwise_concurrent(int op, bool card_only, const uint8_t *pa, const
 // measurement probes (rbgpu_internal_probe): mode 1 = task-order payload reads, 2 = streaming read
 void launch_probe(int op, int mode, const uint8_t *pa, const uint8_t *pb, uint64_t a_bytes, const TaskRec *recs,
                   uint64_t n, uint32_t *sink, unsigned blocks, hipStream_t st);
-void launch_compact_count(const uint64_t *task_begin, uint64_t nseg, const uint8_t *ttype, uint64_t *cnt,
+// bk[block] = the block's kept results; the write takes their exclusive scans (bks) and writes each
+// segment's first result index to rseg and / or rbegin (either may be null)
+void launch_compact_count(const uint64_t *task_begin, uint64_t nseg, const uint8_t *ttype, uint64_t *bk,
                           hipStream_t st);
-void launch_compact_write(const uint64_t *task_begin, uint64_t nseg, const TaskMeta &tm, const uint64_t *rbegin,
+void launch_compact_write(const uint64_t *task_begin, uint64_t nseg, const TaskMeta &tm, const uint64_t *bks,
                           const OutView &out, const uint32_t *seg_pair, uint64_t *pair_card, uint64_t *stats,
-                          hipStream_t st);
+                          uint64_t *rseg, uint64_t *rbegin, hipStream_t st);
 
 // small batches (<= kSmallPairs pairs, <= kSmallPairKeys keys per pair, <= kSmallSlots merged keys in
 // all): one kernel per call computes every pair into one 8 KiB slot per merged key, one single-block

@@ -121,6 +121,26 @@ __device__ __forceinline__ void stat_add_block(uint64_t *stats, const int (&word
     }
 }
 
+// Sums over the block (kPairThreads threads) of N per-thread values; every thread gets all N.
+template <int N>
+__device__ __forceinline__ void block_sums(const uint64_t (&v)[N], uint64_t (&sums)[N]) {
+  __shared__ uint64_t part[kPairThreads / 64][N];
+  const int lane = lane_id(), w = threadIdx.x >> 6;
+#pragma unroll
+  for (int k = 0; k < N; ++k) {
+    const uint64_t s = wave_sum_u64(v[k]);
+    if (lane == 0) part[w][k] = s;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < N; ++k) {
+    uint64_t s = 0;
+    for (int i = 0; i < kPairThreads / 64; ++i) s += part[i][k];
+    sums[k] = s;
+  }
+  __syncthreads();
+}
+
 // exclusive block-wide prefix of v (blockDim.x a multiple of 64, <= 1024); *total = the sum
 __device__ __forceinline__ uint32_t block_xscan(uint32_t v, uint32_t *wtot, uint32_t &total) {
   const int lane = lane_id(), w = threadIdx.x >> 6, nw = blockDim.x >> 6;
@@ -180,11 +200,6 @@ __global__ __launch_bounds__(kPairThreads) void k_seg_fill(PairArgs a, const uin
   for (uint64_t s = seg_begin[p]; s < seg_begin[p + 1]; ++s) seg_pair[s] = p;
 }
 
-__global__ __launch_bounds__(kPairThreads) void k_seg_identity(uint64_t np, uint64_t *seg_begin, uint32_t *seg_pair) {
-  const uint64_t p = (uint64_t)blockIdx.x * kPairThreads + threadIdx.x;
-  if (p <= np) seg_begin[p] = p;
-  if (p < np) seg_pair[p] = (uint32_t)p;
-}
 // largest begin[i+1] - begin[i] (containers of one bitmap), atomicMax into *out (zeroed)
 __global__ __launch_bounds__(kPairThreads) void k_max_span(const uint64_t *begin, uint32_t nb, uint64_t *out) {
   uint64_t m = 0;
@@ -217,11 +232,11 @@ __device__ __forceinline__ void pair_walk(const PairArgs &a, uint64_t sg, PairCo
                                           const PairBases &base, TaskRec *light, TaskRec *heavy, TaskMeta tm,
                                           TaskRec *sl = nullptr, TaskRec *sh = nullptr, uint64_t l0 = 0,
                                           uint64_t h0 = 0, uint64_t t0 = 0) {
-  const uint32_t p = a.seg_pair[sg];
+  const uint32_t p = a.seg_pair ? a.seg_pair[sg] : (uint32_t)sg; // no map: segment sg is pair sg, whole
   uint64_t i0, na, j0, nb;
   bool ident;
   pair_ranges(a, p, i0, na, j0, nb, &ident);
-  const uint64_t d0 = (sg - a.seg_begin[p]) * a.seg_keys, d1 = d0 + a.seg_keys < na + nb ? d0 + a.seg_keys : na + nb;
+  const uint64_t d0 = a.seg_pair ? (sg - a.seg_begin[p]) * a.seg_keys : 0, d1 = d0 + a.seg_keys < na + nb ? d0 + a.seg_keys : na + nb;
   uint64_t si0, sj0, si1, sj1;
   merge_split(a.A.key + i0, na, a.B.key + j0, nb, d0, si0, sj0);
   merge_split(a.A.key + i0, na, a.B.key + j0, nb, d1, si1, sj1);
@@ -360,11 +375,15 @@ __device__ __forceinline__ void pair_walk(const PairArgs &a, uint64_t sg, PairCo
     }
 }
 
-__global__ __launch_bounds__(kPairThreads) void k_pair_count(PairArgs a, PairCountArrays c, uint64_t *stats) {
+// Per-block layout: c holds each segment's counts, bt each block's totals (bt.x[blockIdx]); the
+// block totals alone are scanned (scan_blocks_multi), and k_pair_emit ranks its block's segments
+// itself — the per-segment scan passes over 4 x 8 MB are gone.
+__global__ __launch_bounds__(kPairThreads) void k_pair_count(PairArgs a, PairCountArrays c, PairCountArrays bt,
+                                                             uint64_t *stats) {
   const uint64_t p = (uint64_t)blockIdx.x * kPairThreads + threadIdx.x; // segment
   uint64_t inb[3] = {0, 0, 0};
+  PairCounts n{};
   if (p < a.nseg) {
-    PairCounts n{};
     PairBases b{};
     pair_walk<false>(a, p, n, inb, b, nullptr, nullptr, TaskMeta{});
     c.task[p] = n.task;
@@ -377,6 +396,15 @@ __global__ __launch_bounds__(kPairThreads) void k_pair_count(PairArgs a, PairCou
   const int words[4] = {0, 2, 3, 6};
   const uint64_t vals[4] = {inb[0] + inb[1] + inb[2], inb[1], inb[2], inb[1] + inb[2]};
   stat_add_block(stats, words, vals);
+  const uint64_t cv[4] = {n.task, n.light, n.big, n.small};
+  uint64_t sums[4];
+  block_sums(cv, sums);
+  if (threadIdx.x == 0) {
+    bt.task[blockIdx.x] = sums[0];
+    bt.light[blockIdx.x] = sums[1];
+    bt.big[blockIdx.x] = sums[2];
+    bt.small[blockIdx.x] = sums[3];
+  }
 }
 
 // A block's segments own contiguous ranges of the light and of the heavy record arrays (the scans
@@ -384,21 +412,45 @@ __global__ __launch_bounds__(kPairThreads) void k_pair_count(PairArgs a, PairCou
 // runs: a thread's own records are 40-B structs at scattered positions, which the store path
 // replays line by line (k_pair_emit measured 189 us per 1M pairs, issue-stall bound).
 constexpr uint32_t kEmitStage = 640; // records (25 KiB); a block with more stores directly
-__global__ __launch_bounds__(kPairThreads) void k_pair_emit(PairArgs a, PairCountArrays scans, uint64_t small_base,
-                                                            TaskRec *light, TaskRec *heavy, TaskMeta tm) {
+// tot (when non-null): the scans' totals on the device (tasks, light, big, small) — the heavy records
+// follow the light ones in one array and the small slots follow the big ones, so the launch needs no
+// host read-back of the totals (api.hip launches it before the host has them)
+// cnt: the segments' counts, bs: the exclusive scans of the block totals (bs.x[blockIdx]); every
+// segment's task offset is also stored in task_begin[p] (task_begin[nseg] = the total) for the
+// compaction.
+__global__ __launch_bounds__(kPairThreads) void k_pair_emit(PairArgs a, PairCountArrays cnt, PairCountArrays bs,
+                                                            uint64_t small_base, TaskRec *light, TaskRec *heavy,
+                                                            TaskMeta tm, uint64_t *task_begin, const uint64_t *tot,
+                                                            uint64_t cap) {
+  if (tot) {
+    heavy = light + tot[1];
+    small_base = tot[2] * (uint64_t)kBitmapBytes;
+    if (tot[0] > cap) return; // the workspace holds cap tasks: the host fails the call on the totals
+  }
   __shared__ __attribute__((aligned(16))) TaskRec stage[kEmitStage];
   __shared__ uint64_t s_out[kEmitStage];
   __shared__ uint16_t s_key[kEmitStage];
   __shared__ uint8_t s_cat[kEmitStage];
-  const uint64_t b0 = (uint64_t)blockIdx.x * kPairThreads, be = min(b0 + kPairThreads, a.nseg);
+  __shared__ uint32_t wtot[kPairThreads / 64];
+  const uint64_t b0 = (uint64_t)blockIdx.x * kPairThreads;
   const uint64_t p = b0 + threadIdx.x; // segment
-  const uint64_t L0 = scans.light[b0], L1 = scans.light[be], T0 = scans.task[b0], T1 = scans.task[be];
-  const uint64_t H0 = T0 - L0, nl = L1 - L0, nh = (T1 - L1) - H0, nt = T1 - T0;
+  const bool live = p < a.nseg;
+  // in-block ranks of the segments' counts (a block holds <= 256 x seg_keys tasks and <= 512 MiB of
+  // small slots: 32-bit)
+  const uint32_t ct = live ? (uint32_t)cnt.task[p] : 0u, cl = live ? (uint32_t)cnt.light[p] : 0u;
+  const uint32_t cg = live ? (uint32_t)cnt.big[p] : 0u, cs = live ? (uint32_t)cnt.small[p] : 0u;
+  uint32_t nt32, nl32, ng32, ns32;
+  const uint32_t xt = block_xscan(ct, wtot, nt32), xl = block_xscan(cl, wtot, nl32);
+  const uint32_t xg = block_xscan(cg, wtot, ng32), xs = block_xscan(cs, wtot, ns32);
+  const uint64_t T0 = bs.task[blockIdx.x], L0 = bs.light[blockIdx.x];
+  const uint64_t H0 = T0 - L0, nl = nl32, nh = (uint64_t)nt32 - nl32, nt = nt32;
   const bool staged = nt <= kEmitStage; // block-uniform
-  if (p < a.nseg) {
+  if (live) {
     PairCounts n{};
-    PairBases b{scans.task[p], scans.light[p], scans.task[p] - scans.light[p], scans.big[p],
-                small_base + scans.small[p]};
+    PairBases b{T0 + xt, L0 + xl, (T0 + xt) - (L0 + xl), bs.big[blockIdx.x] + xg,
+                small_base + bs.small[blockIdx.x] + xs};
+    task_begin[p] = b.task;
+    if (p == a.nseg - 1) task_begin[a.nseg] = b.task + ct;
     uint64_t inb[3] = {0, 0, 0};
     if (staged) {
       TaskMeta sm = tm;
@@ -1005,28 +1057,52 @@ void launch_probe(int op, int mode, const uint8_t *pa, const uint8_t *pb, uint64
 // ---------------------------------------------------------------- compaction
 // compaction runs per segment (units u with tasks [tb[u], tb[u+1])); a pair's results are its
 // segments' results in order
-__global__ __launch_bounds__(kPairThreads) void k_compact_count(const uint64_t *tb, uint64_t npairs,
-                                                                const uint8_t *ttype, uint64_t *cnt) {
+// Per-block layout again: k_compact_count leaves each block's kept-result total in bk[blockIdx], the
+// block totals are scanned (scan_blocks_multi, whose total is the call's result container count), and
+// k_compact_write ranks its block's segments and tasks itself.
+__global__ __launch_bounds__(kPairThreads) void k_compact_count(const uint64_t *tb, uint64_t nseg,
+                                                                const uint8_t *ttype, uint64_t *bk) {
   const uint64_t p = (uint64_t)blockIdx.x * kPairThreads + threadIdx.x;
-  if (p >= npairs) return;
   uint64_t n = 0;
-  for (uint64_t t = tb[p]; t < tb[p + 1]; ++t) n += ttype[t] != kEmpty;
-  cnt[p] = n;
+  if (p < nseg)
+    for (uint64_t t = tb[p]; t < tb[p + 1]; ++t) n += ttype[t] != kEmpty;
+  const uint64_t v[1] = {n};
+  uint64_t sum[1];
+  block_sums(v, sum);
+  if (threadIdx.x == 0) bk[blockIdx.x] = sum[0];
 }
-__global__ __launch_bounds__(kPairThreads) void k_compact_write(const uint64_t *tb, uint64_t npairs, TaskMeta tm,
-                                                                const uint64_t *rbegin, OutView out,
+// bks: exclusive scans of the block totals.  rseg (may be null): each segment's first result index,
+// rseg[nseg] = the total (k_pair_rbegin maps them to pairs); rbegin (may be null): the same written
+// as the result CSR directly, when every segment is one pair.
+__global__ __launch_bounds__(kPairThreads) void k_compact_write(const uint64_t *tb, uint64_t nseg, TaskMeta tm,
+                                                                const uint64_t *bks, OutView out,
                                                                 const uint32_t *seg_pair, uint64_t *pair_card,
-                                                                uint64_t *stats) {
-  const uint64_t p = (uint64_t)blockIdx.x * kPairThreads + threadIdx.x;
+                                                                uint64_t *stats, uint64_t *rseg, uint64_t *rbegin) {
+  __shared__ uint32_t wtot[kPairThreads / 64];
+  const uint64_t b0 = (uint64_t)blockIdx.x * kPairThreads, be = min(b0 + kPairThreads, nseg);
+  const uint64_t p = b0 + threadIdx.x;
+  const uint64_t R0 = bks[blockIdx.x];
+  // the segment's kept results and its rank among the block's (<= 256 x seg_keys: 32-bit)
+  uint32_t kept = 0;
+  const uint64_t t0 = p < nseg ? tb[p] : 0, t1 = p < nseg ? tb[p + 1] : 0;
+  for (uint64_t t = t0; t < t1; ++t) kept += tm.type[t] != kEmpty;
+  uint32_t btot;
+  const uint64_t rs = R0 + block_xscan(kept, wtot, btot);
+  if (p < nseg) {
+    if (rseg) rseg[p] = rs;
+    if (rbegin) rbegin[p] = rs;
+    if (p == nseg - 1) {
+      if (rseg) rseg[nseg] = rs + kept;
+      if (rbegin) rbegin[nseg] = rs + kept;
+    }
+  }
   uint64_t outb[2] = {0, 0}, card_sum = 0;
   if (!pair_card && out.key) {
-    // A block's segments own the contiguous task range [T0, T1) and result range from rbegin[b0]:
-    // one thread per task, ranked by a block scan, so loads and stores are coalesced (a thread
-    // walking its own segment's tasks is latency-bound).
-    __shared__ uint32_t wtot[4];
-    const uint64_t b0 = (uint64_t)blockIdx.x * kPairThreads, be = min(b0 + kPairThreads, npairs);
+    // A block's segments own the contiguous task range [T0, T1) and result range from R0: one
+    // thread per task, ranked by a block scan, so loads and stores are coalesced (a thread walking
+    // its own segment's tasks is latency-bound).
     const uint64_t T0 = tb[b0], T1 = tb[be];
-    uint64_t R = rbegin[b0];
+    uint64_t R = R0;
     for (uint64_t base = T0; base < T1; base += kPairThreads) {
       const uint64_t t = base + threadIdx.x;
       const uint8_t ty = t < T1 ? tm.type[t] : (uint8_t)kEmpty;
@@ -1047,9 +1123,9 @@ __global__ __launch_bounds__(kPairThreads) void k_compact_write(const uint64_t *
       }
       R += tot;
     }
-  } else if (p < npairs) {
-    uint64_t r = rbegin ? rbegin[p] : 0, card = 0;
-    for (uint64_t t = tb[p]; t < tb[p + 1]; ++t) {
+  } else if (p < nseg) {
+    uint64_t r = rs, card = 0;
+    for (uint64_t t = t0; t < t1; ++t) {
       const uint8_t ty = tm.type[t];
       if (ty == kEmpty) continue;
       card += tm.card[t];
@@ -1063,7 +1139,7 @@ __global__ __launch_bounds__(kPairThreads) void k_compact_write(const uint64_t *
       }
       ++r;
     }
-    if (pair_card && card) atomicAdd((unsigned long long *)&pair_card[seg_pair[p]], (unsigned long long)card);
+    if (pair_card && card) atomicAdd((unsigned long long *)&pair_card[seg_pair ? seg_pair[p] : p], (unsigned long long)card);
     card_sum = card;
   }
   // stats words: 1 total output, 4 light-task output, 5 heavy-task output, 7 result cardinality
@@ -1075,10 +1151,14 @@ __global__ __launch_bounds__(kPairThreads) void k_compact_write(const uint64_t *
 }
 
 // result CSR per pair from the per-segment result offsets
+// (and the result container count into *count: the stats word the call reads back anyway)
 __global__ __launch_bounds__(kPairThreads) void k_pair_rbegin(const uint64_t *seg_begin, uint32_t npairs,
-                                                              const uint64_t *rseg, uint64_t *rbegin) {
+                                                              const uint64_t *rseg, uint64_t *rbegin, uint64_t *count) {
   const uint32_t p = blockIdx.x * kPairThreads + threadIdx.x;
-  if (p <= npairs) rbegin[p] = rseg[seg_begin[p]];
+  if (p > npairs) return;
+  const uint64_t r = rseg[seg_begin[p]];
+  if (rbegin) rbegin[p] = r;
+  if (p == npairs && count) *count = r;
 }
 
 // ---------------------------------------------------------------- launchers
@@ -1092,26 +1172,27 @@ void launch_seg_fill(const PairArgs &a, const uint64_t *seg_begin, uint32_t *seg
   if (!a.npairs) return;
   k_seg_fill<<<blocks_for(a.npairs, kPairThreads), kPairThreads, 0, st>>>(a, seg_begin, seg_pair);
 }
-void launch_seg_identity(uint64_t np, uint64_t *seg_begin, uint32_t *seg_pair, hipStream_t st) {
-  k_seg_identity<<<blocks_for(np + 1, kPairThreads), kPairThreads, 0, st>>>(np, seg_begin, seg_pair);
-}
 void launch_max_span(const uint64_t *begin, uint32_t nb, uint64_t *out, hipStream_t st) {
   const unsigned blocks = std::min<unsigned>(blocks_for(nb, kPairThreads), 1024);
   k_max_span<<<blocks, kPairThreads, 0, st>>>(begin, nb, out);
 }
 void launch_pair_rbegin(const uint64_t *seg_begin, uint32_t npairs, const uint64_t *rseg, uint64_t *rbegin,
-                        hipStream_t st) {
+                        uint64_t *count, hipStream_t st) {
   k_pair_rbegin<<<blocks_for((uint64_t)npairs + 1, kPairThreads), kPairThreads, 0, st>>>(seg_begin, npairs, rseg,
-                                                                                        rbegin);
+                                                                                        rbegin, count);
 }
-void launch_pair_count(const PairArgs &a, const PairCountArrays &c, uint64_t *stats, hipStream_t st) {
+uint64_t pair_blocks(uint64_t nseg) { return blocks_for(nseg, kPairThreads); }
+void launch_pair_count(const PairArgs &a, const PairCountArrays &c, const PairCountArrays &bt, uint64_t *stats,
+                       hipStream_t st) {
   if (!a.nseg) return;
-  k_pair_count<<<blocks_for(a.nseg, kPairThreads), kPairThreads, 0, st>>>(a, c, stats);
+  k_pair_count<<<blocks_for(a.nseg, kPairThreads), kPairThreads, 0, st>>>(a, c, bt, stats);
 }
-void launch_pair_emit(const PairArgs &a, const PairCountArrays &scans, uint64_t small_base, TaskRec *light,
-                      TaskRec *heavy, const TaskMeta &tm, hipStream_t st) {
+void launch_pair_emit(const PairArgs &a, const PairCountArrays &cnt, const PairCountArrays &bs, uint64_t small_base,
+                      TaskRec *light, TaskRec *heavy, const TaskMeta &tm, uint64_t *task_begin, const uint64_t *tot,
+                      uint64_t cap, hipStream_t st) {
   if (!a.nseg) return;
-  k_pair_emit<<<blocks_for(a.nseg, kPairThreads), kPairThreads, 0, st>>>(a, scans, small_base, light, heavy, tm);
+  k_pair_emit<<<blocks_for(a.nseg, kPairThreads), kPairThreads, 0, st>>>(a, cnt, bs, small_base, light, heavy, tm,
+                                                                          task_begin, tot, cap);
 }
 // Persistent grid: every CU filled to the kernel's occupancy, waves stride over the tasks.
 template <class K> static unsigned persistent_blocks(K kernel, uint64_t tasks) {
@@ -1206,17 +1287,17 @@ void launch_pairwise(int op, bool card_only, const uint8_t *pa, const uint8_t *p
   default: launch_op<RB_ANDNOT>(card_only, pa, pb, light, nl, heavy, nh, out, tm, st, mid); break;
   }
 }
-void launch_compact_count(const uint64_t *task_begin, uint64_t nseg, const uint8_t *ttype, uint64_t *cnt,
+void launch_compact_count(const uint64_t *task_begin, uint64_t nseg, const uint8_t *ttype, uint64_t *bk,
                           hipStream_t st) {
   if (!nseg) return;
-  k_compact_count<<<blocks_for(nseg, kPairThreads), kPairThreads, 0, st>>>(task_begin, nseg, ttype, cnt);
+  k_compact_count<<<blocks_for(nseg, kPairThreads), kPairThreads, 0, st>>>(task_begin, nseg, ttype, bk);
 }
-void launch_compact_write(const uint64_t *task_begin, uint64_t nseg, const TaskMeta &tm, const uint64_t *rbegin,
+void launch_compact_write(const uint64_t *task_begin, uint64_t nseg, const TaskMeta &tm, const uint64_t *bks,
                           const OutView &out, const uint32_t *seg_pair, uint64_t *pair_card, uint64_t *stats,
-                          hipStream_t st) {
+                          uint64_t *rseg, uint64_t *rbegin, hipStream_t st) {
   if (!nseg) return;
-  k_compact_write<<<blocks_for(nseg, kPairThreads), kPairThreads, 0, st>>>(task_begin, nseg, tm, rbegin, out,
-                                                                           seg_pair, pair_card, stats);
+  k_compact_write<<<blocks_for(nseg, kPairThreads), kPairThreads, 0, st>>>(task_begin, nseg, tm, bks, out,
+                                                                           seg_pair, pair_card, stats, rseg, rbegin);
 }
 
 // ---------------------------------------------------------------- small batches: two launches

@@ -152,6 +152,46 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_apply_multi(Multi m, uint
   }
   if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) out[n] = totals[blockIdx.y];
 }
+// k <= 4 short arrays (per-block totals of a per-block layout) in ONE launch: a block per array
+// loops over chunks of 1024 with a carried offset.  out[y][i] = sum(in[y][0..i)), out[y][n] = the
+// sum, and totals[y] = the sum when totals is non-null.
+__global__ __launch_bounds__(kScanThreads) void k_scan_loop_multi(Multi m, uint64_t n, uint64_t *totals) {
+  __shared__ uint64_t sh[4];
+  const uint64_t *in = m.in[blockIdx.y];
+  uint64_t *out = m.out[blockIdx.y];
+  uint64_t carry = 0;
+  for (uint64_t c0 = 0; c0 < n; c0 += (uint64_t)kScanThreads * kScanItems) {
+    const uint64_t base = c0 + threadIdx.x * kScanItems;
+    uint64_t v[kScanItems], s = 0;
+#pragma unroll
+    for (int i = 0; i < kScanItems; ++i) {
+      v[i] = base + i < n ? in[base + i] : 0;
+      s += v[i];
+    }
+    uint64_t total;
+    uint64_t run = block_excl_scan(s, sh, total) + carry;
+#pragma unroll
+    for (int i = 0; i < kScanItems; ++i) {
+      if (base + i < n) out[base + i] = run;
+      run += v[i];
+    }
+    carry += total;
+  }
+  if (threadIdx.x == 0) {
+    out[n] = carry;
+    if (totals) totals[blockIdx.y] = carry;
+  }
+}
+void scan_blocks_multi(const uint64_t *const *in, uint64_t *const *out, int k, uint64_t n, uint64_t *totals,
+                       hipStream_t st) {
+  Multi m{};
+  for (int i = 0; i < k; ++i) {
+    m.in[i] = in[i];
+    m.out[i] = out[i];
+  }
+  k_scan_loop_multi<<<dim3(1, k), kScanThreads, 0, st>>>(m, n, totals);
+}
+
 __global__ void k_gather_totals(Multi m, uint64_t n, uint64_t *totals) { totals[threadIdx.x] = m.out[threadIdx.x][n]; }
 
 void scan_exclusive_multi(const uint64_t *const *in, uint64_t *const *out, int k, uint64_t n, uint64_t *tmp,

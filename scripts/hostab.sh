@@ -1,5 +1,5 @@
 #!/bin/bash
-# Host-phase kernels after a change: the pairwise-path GPU tests on the in-tree library, an interleaved
+# Host-phase kernels after a change: the GPU test suite on the in-tree library, an interleaved
 # A/B of the config-2 bench against abvar/base (the previous tree), and a kernel-trace profile of each
 # library (per-kernel averages of the count / scan / emit / compaction launches).  Every GPU step has
 # its own limit; the first failure ends the call.
@@ -7,9 +7,7 @@ set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out/host
 export HSA_ENABLE_IPC_MODE_LEGACY=0
-timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread \
-  tests/test_gpu_pairwise.py tests/test_gpu_type_pins.py tests/test_gpu_inplace.py tests/test_gpu_longlong.py \
-  tests/test_gpu_roaring_api.py tests/test_gpu_configs.py \
+timeout -k 10 600 python -u -m pytest -x -q -m gpu --timeout 120 --timeout-method thread tests \
   > gpurun_out/host/tests.txt 2>&1 || { tail -30 gpurun_out/host/tests.txt; exit 1; }
 tail -2 gpurun_out/host/tests.txt
 scripts/ab.sh base1 abvar/base/librbgpu.so new1 default base2 abvar/base/librbgpu.so new2 default || exit 1
