@@ -1030,7 +1030,7 @@ int pairwise_impl(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu_set *b
   uint32_t seg_keys = pairwise_seg_keys(a, b, np);
   if (host_segs) { // latency study knob: merge-path segment length of small batches
     static const int sk = getenv("RBGPU_SMALL_SEG_KEYS") ? atoi(getenv("RBGPU_SMALL_SEG_KEYS")) : 0;
-    if (sk > 0) seg_keys = (uint32_t)sk;
+    if (sk > 0) seg_keys = std::min<uint32_t>((uint32_t)sk, kMaxSegKeys);
   }
   if (d_aidx || d_bidx || host_segs) { // through pinned staging: a pageable copy would block the host
     const size_t bytes = np * 4 * ((d_aidx != nullptr) + (d_bidx != nullptr)) + (host_segs ? (np + 1) * 8 : 0);
@@ -1089,12 +1089,11 @@ int pairwise_impl(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu_set *b
   }
   // ---- per segment: counts, block totals and their scans, result counts / offsets
   const uint64_t nblk = pair_blocks(ns);
-  need = aligned256(ns * 4) + 6 * aligned256((ns + 1) * 8) + 10 * aligned256((nblk + 1) * 8) + 4 * 256;
+  need = aligned256(ns * 4) + 3 * aligned256((ns + 1) * 8) + 10 * aligned256((nblk + 1) * 8) + 4 * 256;
   if (ctx->ws_segs.reserve(need, st) != hipSuccess) return fail(RB_ENOMEM, "segment workspace");
   Workspace &G = ctx->ws_segs;
   uint32_t *seg_pair = G.take<uint32_t>(std::max<uint64_t>(ns, 1));
-  PairCountArrays cnt{G.take<uint64_t>(ns + 1), G.take<uint64_t>(ns + 1), G.take<uint64_t>(ns + 1),
-                      G.take<uint64_t>(ns + 1)};
+  uint64_t *cnt = G.take<uint64_t>(ns + 1); // per segment, packed (pack_seg_counts)
   PairCountArrays bt{G.take<uint64_t>(nblk + 1), G.take<uint64_t>(nblk + 1), G.take<uint64_t>(nblk + 1),
                      G.take<uint64_t>(nblk + 1)};
   PairCountArrays bs{G.take<uint64_t>(nblk + 1), G.take<uint64_t>(nblk + 1), G.take<uint64_t>(nblk + 1),
@@ -1118,6 +1117,9 @@ int pairwise_impl(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu_set *b
   // sized by that bound and the emit kernel reads the totals on the device: it runs while the host
   // waits for the totals, allocates the result and launches the task kernels.  Otherwise the host
   // reads the totals first (the bound is the segments' key capacity, too loose to reserve).
+  // light tasks from a shared chunk queue (a second light launch takes over the heavy kernel's CUs
+  // when it finishes) unless RBGPU_STATIC_LIGHT is set
+  static const bool static_light = getenv("RBGPU_STATIC_LIGHT") != nullptr;
   const uint64_t seg_cap = ns * (uint64_t)seg_keys;
   const uint64_t tbound = !d_aidx && !d_bidx ? std::min<uint64_t>(a->nc + b->nc, seg_cap) : seg_cap;
   const bool early = !probe && ns && tbound <= kEarlyEmitTasks;
@@ -1130,25 +1132,23 @@ int pairwise_impl(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu_set *b
   // one record array (the light records, then the heavy ones) and the per-task metadata, for nt tasks
   auto take_tasks = [&](uint64_t nt) -> int {
     const uint64_t nt1 = std::max<uint64_t>(nt, 1);
-    const size_t tneed = aligned256(nt1 * sizeof(TaskRec)) + 2 * aligned256(nt1 * 2) + 2 * aligned256(nt1) +
-                         aligned256(nt1 * 4) + aligned256(nt1 * 8) + aligned256(4096) + 256;
+    const size_t tneed = aligned256(nt1 * sizeof(TaskRec)) + aligned256(nt1) + 2 * aligned256(nt1 * 8) +
+                         aligned256(kQueueWords * 8) + 256;
     if (ctx->ws_tasks.reserve(tneed, st) != hipSuccess)
       return fail(RB_ENOMEM, "task workspace (%llu tasks)", (unsigned long long)nt);
     Workspace &T = ctx->ws_tasks;
     light = T.take<TaskRec>(nt1);
-    tm.key = T.take<uint16_t>(nt1);
-    tm.nruns = T.take<uint16_t>(nt1);
     tm.type = T.take<uint8_t>(nt1);
-    tm.cat = T.take<uint8_t>(nt1);
-    tm.card = T.take<uint32_t>(nt1);
-    tm.out = T.take<uint64_t>(nt1);
-    queue = T.take<unsigned long long>(512); // light-task chunk counters (<= 32, 128 B apart)
+    tm.res = T.take<uint64_t>(nt1);
+    tm.slot = T.take<uint64_t>(nt1);
+    queue = T.take<unsigned long long>(kQueueWords); // light-task chunk counters (<= 32, 128 B apart)
     return RB_OK;
   };
   if (early) {
     if ((rc = take_tasks(tbound))) return rc;
     HIPCHK(hipEventRecord(ctx->ev_tot, st));
-    launch_pair_emit(pa, cnt, bs, 0, light, nullptr, tm, task_begin, d_tot, tbound, st);
+    launch_pair_emit(pa, cnt, bs, 0, light, nullptr, tm, task_begin, d_tot, tbound, static_light ? nullptr : queue,
+                     st);
     HIPCHK(hipEventSynchronize(ctx->ev_tot));
   } else {
     HIPCHK(hipStreamSynchronize(st));
@@ -1158,6 +1158,10 @@ int pairwise_impl(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu_set *b
   const uint64_t ntasks = tot[0], nlight = tot[1], nheavy = ntasks - nlight, nbig_t = tot[2], small_t = tot[3];
   const uint64_t small_base = nbig_t * kBitmapBytes;
   const uint64_t arena = card_only ? 0 : small_base + small_t;
+  if (arena >= kSlotOffsetLimit) { // a task slot holds 40-bit arena offsets
+    (void)hipStreamSynchronize(st);
+    return fail(RB_ENOMEM, "pairwise: result arena of %llu bytes", (unsigned long long)arena);
+  }
   if (early && ntasks > tbound) { // never expected: the emit dropped the records past the bound
     (void)hipStreamSynchronize(st);
     return fail(RB_EDEVICE, "pairwise: %llu tasks exceed the bound %llu", (unsigned long long)ntasks,
@@ -1179,14 +1183,12 @@ int pairwise_impl(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu_set *b
   // the light and heavy task kernels run concurrently (heavy on the side stream, 1 block per CU;
   // light 2 blocks per CU: 2 x 128 + 256 VGPRs per SIMD) unless RBGPU_SERIAL_TASKS is set
   static const bool serial = getenv("RBGPU_SERIAL_TASKS") != nullptr;
-  // light tasks from a shared chunk queue (a second light launch takes over the heavy kernel's CUs
-  // when it finishes) unless RBGPU_STATIC_LIGHT is set
-  static const bool static_light = getenv("RBGPU_STATIC_LIGHT") != nullptr;
   const bool conc = !probe && !serial && nlight && nheavy && nlight + nheavy >= 65536; // small batches: the
                                                   // cross-stream waits cost more than the overlap
-  if (!early) launch_pair_emit(pa, cnt, bs, small_base, light, heavy, tm, task_begin, nullptr, 0, st);
-  // the queue counters are zeroed before ev[1]: the side stream waits on ev[1] before its light launch
-  if (conc && !static_light) HIPCHK(hipMemsetAsync(queue, 0, 4096, st));
+  // the emit zeroes the queue counters before ev[1]: the side stream waits on ev[1] before its light launch
+  if (!early)
+    launch_pair_emit(pa, cnt, bs, small_base, light, heavy, tm, task_begin, nullptr, 0, static_light ? nullptr : queue,
+                     st);
   HIPCHK(hipEventRecord(ctx->ev[1], st));
   if (probe) {
     uint32_t *sink = nullptr;

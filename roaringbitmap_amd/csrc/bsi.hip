@@ -30,15 +30,23 @@ __global__ __launch_bounds__(256) void k_bsi_index(SetView s, uint32_t first, in
   for (uint64_t c = lo + (uint64_t)blockIdx.x * 256 + threadIdx.x; c < hi; c += (uint64_t)gridDim.x * 256)
     table[(uint64_t)row * 65536 + s.key[c]] = (int32_t)c;
 }
-// keys of F (ebM or foundSet) inside the shard's [key_lo, key_hi)
+// keys of F (ebM or foundSet) inside the shard's [key_lo, key_hi), in a per-block layout: k_bsi_active
+// leaves each 256-key block's count in bt, the counts are scanned (bts, bts[256] = nk) and k_bsi_list
+// places the keys
 __global__ __launch_bounds__(256) void k_bsi_active(const int32_t *frow, uint32_t key_lo, uint32_t key_hi,
-                                                    uint64_t *active) {
+                                                    uint64_t *bt) {
+  __shared__ uint32_t wt[4];
   const uint32_t k = blockIdx.x * 256 + threadIdx.x;
-  if (k < 65536) active[k] = frow[k] >= 0 && k >= key_lo && k < key_hi;
+  const uint32_t n = block_flag_count(frow[k] >= 0 && k >= key_lo && k < key_hi, wt);
+  if (threadIdx.x == 0) bt[blockIdx.x] = n;
 }
-__global__ __launch_bounds__(256) void k_bsi_list(const uint64_t *active, const uint64_t *pos, uint32_t *klist) {
+__global__ __launch_bounds__(256) void k_bsi_list(const int32_t *frow, uint32_t key_lo, uint32_t key_hi,
+                                                  const uint64_t *bts, uint32_t *klist) {
+  __shared__ uint32_t wt[4];
   const uint32_t k = blockIdx.x * 256 + threadIdx.x;
-  if (k < 65536 && active[k]) klist[pos[k]] = k;
+  const bool f = frow[k] >= 0 && k >= key_lo && k < key_hi;
+  const uint32_t r = block_flag_rank(f, wt);
+  if (f) klist[bts[blockIdx.x] + r] = k;
 }
 
 // ---- per-key value algebra with the reference's type rules --------------------------------
@@ -607,11 +615,15 @@ int bsi_compare(rbgpu_ctx *ctx, const rbgpu_set *bsi, int op, uint64_t start, ui
   HIPCHK(hipMemsetAsync(d_table, 0xFF, (uint64_t)rows * 65536 * 4, st));
   k_bsi_index<<<dim3(64, nbits + 1), 256, 0, st>>>(bsi->view(), 0, d_table);
   if (found) k_bsi_index<<<dim3(64, 1), 256, 0, st>>>(found->view(), 0, d_table + (uint64_t)(nbits + 1) * 65536);
-  k_bsi_active<<<256, 256, 0, st>>>(d_table + (uint64_t)(found ? nbits + 1 : nbits) * 65536, key_lo, key_hi,
-                                    d_active);
-  scan_exclusive(d_active, d_pos, 65536, d_tmp, st);
-  k_bsi_list<<<256, 256, 0, st>>>(d_active, d_pos, d_klist);
-  HIPCHK(hipMemcpyAsync(ctx->h_pinned, d_pos + 65536, 8, hipMemcpyDeviceToHost, st));
+  {
+    const int32_t *frow = d_table + (uint64_t)(found ? nbits + 1 : nbits) * 65536;
+    k_bsi_active<<<256, 256, 0, st>>>(frow, key_lo, key_hi, d_active);
+    const uint64_t *in1[1] = {d_active};
+    uint64_t *out1[1] = {d_pos};
+    scan_blocks_multi(in1, out1, 1, 256, nullptr, st);
+    k_bsi_list<<<256, 256, 0, st>>>(frow, key_lo, key_hi, d_pos, d_klist);
+  }
+  HIPCHK(hipMemcpyAsync(ctx->h_pinned, d_pos + 256, 8, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
   LAUNCHCHK();
   const uint32_t nk = (uint32_t)ctx->h_pinned[0];
@@ -645,10 +657,10 @@ int bsi_compare(rbgpu_ctx *ctx, const rbgpu_set *bsi, int op, uint64_t start, ui
                                                     ctx->d_stats);
     }
     HIPCHK(hipEventRecord(ctx->ev[2], st));
-    uint64_t nres = 0;
-    rc = compact_keyed(ctx, d_klist, nk, fin.wo, res, &nres);
+    rc = compact_keyed(ctx, d_klist, nk, fin.wo, res);
     const KernelSpan spans[1] = {{fused_range ? "k_bsi_range" : "k_bsi_chain", 0, 1, op == 6 ? 2ull * nk : nk}};
-    if (!rc) rc = stats_end(ctx, nk, nres, spans, 1);
+    if (!rc) rc = stats_end(ctx, nk, 0, spans, 1);
+    if (!rc) keyed_result_count(ctx, res);
   }
   fin.release(ctx, false);
   if (op == 6 && !fused_range) {

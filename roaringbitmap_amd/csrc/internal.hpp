@@ -225,8 +225,8 @@ int stats_fill(rbgpu_ctx *ctx, uint64_t tasks, uint64_t result_containers, const
 // keys outside [key_lo, key_hi) produce no result containers (key-range shard of the aggregation)
 int wide_run(rbgpu_ctx *ctx, int sem, const rbgpu_set *in, const std::vector<uint32_t> &members, uint32_t key_lo,
              uint32_t key_hi, rbgpu_set **out);
-int compact_keyed(rbgpu_ctx *ctx, const uint32_t *d_klist, uint32_t nk, const WideOut &wo, rbgpu_set *res,
-                  uint64_t *nres_out);
+int compact_keyed(rbgpu_ctx *ctx, const uint32_t *d_klist, uint32_t nk, const WideOut &wo, rbgpu_set *res);
+uint64_t keyed_result_count(rbgpu_ctx *ctx, rbgpu_set *res);
 // bsi.hip: op = BitmapSliceIndex.Operation ordinal (EQ, NEQ, LE, LT, GE, GT, RANGE); only the high keys in
 // [key_lo, key_hi) are computed (a key-range shard of the answer)
 int bsi_compare(rbgpu_ctx *ctx, const rbgpu_set *bsi, int op, uint64_t start, uint64_t end, uint64_t vmin,

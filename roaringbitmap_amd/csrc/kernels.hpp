@@ -16,6 +16,7 @@ void scan_blocks_multi(const uint64_t *const *in, uint64_t *const *out, int k, u
                        hipStream_t st);
 
 // ---- pairwise.hip
+constexpr uint32_t kMaxSegKeys = 2048; // merged keys per merge-path segment, at most
 struct PairArgs {
   int op;
   SetView A, B;
@@ -25,7 +26,7 @@ struct PairArgs {
   const uint64_t *seg_begin; // [npairs + 1] first merge-path segment of each pair
   const uint32_t *seg_pair;  // [nseg] pair of each segment; null: one segment per pair (segment p = pair p)
   uint64_t nseg;
-  uint32_t seg_keys; // merged keys per segment (a power of two in [8, 256])
+  uint32_t seg_keys; // merged keys per segment (a power of two in [8, 256]; <= kMaxSegKeys)
   // in-place x1.op(x2) (RoaringBitmap.and/or/xor/andNot(x2)): `same` = A and B are one set, so a pair
   // with equal indices is one bitmap with itself — x.and(x) / x.or(x) leave x as it is, x.xor(x) /
   // x.andNot(x) clear it (RoaringBitmap.java:1271, 1347-1350, 2482, 3297-3300)
@@ -34,16 +35,20 @@ struct PairArgs {
 };
 // per task result metadata (workspace, indexed like tasks)
 struct TaskMeta {
-  uint16_t *key;
-  uint8_t *type;   // kEmpty when dropped
-  uint32_t *card;
-  uint16_t *nruns;
-  uint8_t *cat;    // 0 light, 1 heavy
-  uint64_t *out;   // output slot offset
+  uint8_t *type;   // result type (kEmpty when dropped), written by the task kernels
+  uint64_t *res;   // the result's type | nruns << 8 | card word << 32 (task_res), task kernels
+  uint64_t *slot;  // output slot offset | key << 40 | heavy << 56 (task_slot), k_pair_emit
   int lazy;        // 0, or the priorityqueue_or role (kLazyStatic / kLazyIor / kLazyIorBf) of an OR call
   int inplace;     // x1.or(x2) in place: BitmapContainer.ior(ArrayContainer) keeps a Bitmap even when full
   int keep_empty;  // XOR results are kept when empty (Roaring64Bitmap.xor: Roaring64Bitmap.java:392-460)
 };
+__host__ __device__ inline uint64_t task_res(uint32_t type, uint32_t nruns, uint32_t card) {
+  return (uint64_t)(type & 0xFFu) | ((uint64_t)(nruns & 0xFFFFu) << 8) | ((uint64_t)card << 32);
+}
+__host__ __device__ inline uint64_t task_slot(uint64_t out, uint32_t key, bool heavy) {
+  return out | ((uint64_t)(key & 0xFFFFu) << 40) | ((uint64_t)heavy << 56);
+}
+constexpr uint64_t kSlotOffsetLimit = 1ull << 40; // result arena offsets a task_slot holds
 struct PairCounts {
   uint64_t task, light, heavy, big, small;
 };
@@ -65,17 +70,21 @@ void launch_max_runs(const uint8_t *type, const uint16_t *nruns, uint64_t n, uin
 void launch_pair_rbegin(const uint64_t *seg_begin, uint32_t npairs, const uint64_t *rseg, uint64_t *rbegin,
                         uint64_t *count, hipStream_t st);
 // per segment from here on
-// per-block layout (segments in blocks of pair_blocks' size): c = each segment's counts, bt = each
+// per-block layout (segments in blocks of pair_blocks' size): c = each segment's counts (one packed
+// word), bt = each
 // block's totals; the emit reads the counts and the exclusive scans of the block totals (bs)
 uint64_t pair_blocks(uint64_t nseg);
-void launch_pair_count(const PairArgs &a, const PairCountArrays &c, const PairCountArrays &bt, uint64_t *stats,
+void launch_pair_count(const PairArgs &a, uint64_t *c, const PairCountArrays &bt, uint64_t *stats,
                        hipStream_t st);
 // tot non-null: heavy and small_base come from the device totals (heavy = light + tot[1]) and the
 // workspace holds cap tasks (nothing is written when tot[0] exceeds it)
-// task_begin[p] = segment p's first task ([nseg] = the total), for the compaction
-void launch_pair_emit(const PairArgs &a, const PairCountArrays &cnt, const PairCountArrays &bs, uint64_t small_base,
+// task_begin[p] = segment p's first task ([nseg] = the total), for the compaction; zero_q (may be
+// null): the task kernels' queue counters, zeroed before any record is written
+void launch_pair_emit(const PairArgs &a, const uint64_t *cnt, const PairCountArrays &bs, uint64_t small_base,
                       TaskRec *light, TaskRec *heavy, const TaskMeta &tm, uint64_t *task_begin, const uint64_t *tot,
-                      uint64_t cap, hipStream_t st);
+                      uint64_t cap, unsigned long long *zero_q, hipStream_t st);
+// the task kernels' chunk-queue counters (words; zeroed by the emit when zero_q is given)
+constexpr int kQueueWords = 512;
 // light records: copies + subset-of-an-Array filters; heavy records: the register path.  `mid` is
 // recorded between the two persistent launches.
 void launch_pairwise(int op, bool card_only, const uint8_t *pa, const uint8_t *pb, const TaskRec *light,

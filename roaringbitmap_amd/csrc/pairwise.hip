@@ -274,9 +274,7 @@ __device__ __forceinline__ void pair_walk(const PairArgs &a, uint64_t sg, PairCo
       d[3] = (uint64_t)(uint32_t)t | ((uint64_t)da << 32);
       d[4] = (uint64_t)db | ((uint64_t)rr << 32);
       // staged: tm holds the block's LDS arrays, indexed from the block's first task t0
-      tm.key[t - t0] = key;
-      tm.cat[t - t0] = lt ? 0 : 1;
-      tm.out[t - t0] = out;
+      tm.slot[t - t0] = task_slot(out, key, !lt);
     }
     // branch-free: an `if` between two fields became a select of their addresses, which kept n in scratch
     ++n.task;
@@ -375,10 +373,17 @@ __device__ __forceinline__ void pair_walk(const PairArgs &a, uint64_t sg, PairCo
     }
 }
 
-// Per-block layout: c holds each segment's counts, bt each block's totals (bt.x[blockIdx]); the
+// A segment's four counts in one word: tasks, light tasks and big slots (12 bits each: a segment holds
+// <= kMaxSegKeys + 1 tasks) and small-slot bytes (28 bits: < 8 KiB per small slot).
+static_assert(kMaxSegKeys < 4095 && (uint64_t)(kMaxSegKeys + 1) * kBitmapBytes < (1ull << 28), "segment counts");
+__device__ __forceinline__ uint64_t pack_seg_counts(const PairCounts &n) {
+  return n.task | (n.light << 12) | (n.big << 24) | (n.small << 36);
+}
+
+// Per-block layout: c holds each segment's counts (pack_seg_counts), bt each block's totals (bt.x[blockIdx]); the
 // block totals alone are scanned (scan_blocks_multi), and k_pair_emit ranks its block's segments
 // itself — the per-segment scan passes over 4 x 8 MB are gone.
-__global__ __launch_bounds__(kPairThreads) void k_pair_count(PairArgs a, PairCountArrays c, PairCountArrays bt,
+__global__ __launch_bounds__(kPairThreads) void k_pair_count(PairArgs a, uint64_t *c, PairCountArrays bt,
                                                              uint64_t *stats) {
   const uint64_t p = (uint64_t)blockIdx.x * kPairThreads + threadIdx.x; // segment
   uint64_t inb[3] = {0, 0, 0};
@@ -386,10 +391,7 @@ __global__ __launch_bounds__(kPairThreads) void k_pair_count(PairArgs a, PairCou
   if (p < a.nseg) {
     PairBases b{};
     pair_walk<false>(a, p, n, inb, b, nullptr, nullptr, TaskMeta{});
-    c.task[p] = n.task;
-    c.light[p] = n.light;
-    c.big[p] = n.big;
-    c.small[p] = n.small;
+    c[p] = pack_seg_counts(n);
   }
   // stats words: 0 total input (with key arrays), 2 filter+copy task input, 3 register-path input,
   // 6 all task input (what k_pair_tasks reads)
@@ -418,27 +420,29 @@ constexpr uint32_t kEmitStage = 640; // records (25 KiB); a block with more stor
 // cnt: the segments' counts, bs: the exclusive scans of the block totals (bs.x[blockIdx]); every
 // segment's task offset is also stored in task_begin[p] (task_begin[nseg] = the total) for the
 // compaction.
-__global__ __launch_bounds__(kPairThreads) void k_pair_emit(PairArgs a, PairCountArrays cnt, PairCountArrays bs,
+__global__ __launch_bounds__(kPairThreads) void k_pair_emit(PairArgs a, const uint64_t *cnt, PairCountArrays bs,
                                                             uint64_t small_base, TaskRec *light, TaskRec *heavy,
                                                             TaskMeta tm, uint64_t *task_begin, const uint64_t *tot,
-                                                            uint64_t cap) {
+                                                            uint64_t cap, unsigned long long *zero_q) {
+  // the task kernels' chunk-queue counters (kQueueWords), zeroed here rather than by a memset launch
+  if (zero_q && blockIdx.x == 0)
+    for (int i = threadIdx.x; i < kQueueWords; i += kPairThreads) zero_q[i] = 0ull;
   if (tot) {
     heavy = light + tot[1];
     small_base = tot[2] * (uint64_t)kBitmapBytes;
     if (tot[0] > cap) return; // the workspace holds cap tasks: the host fails the call on the totals
   }
   __shared__ __attribute__((aligned(16))) TaskRec stage[kEmitStage];
-  __shared__ uint64_t s_out[kEmitStage];
-  __shared__ uint16_t s_key[kEmitStage];
-  __shared__ uint8_t s_cat[kEmitStage];
+  __shared__ uint64_t s_slot[kEmitStage];
   __shared__ uint32_t wtot[kPairThreads / 64];
   const uint64_t b0 = (uint64_t)blockIdx.x * kPairThreads;
   const uint64_t p = b0 + threadIdx.x; // segment
   const bool live = p < a.nseg;
   // in-block ranks of the segments' counts (a block holds <= 256 x seg_keys tasks and <= 512 MiB of
   // small slots: 32-bit)
-  const uint32_t ct = live ? (uint32_t)cnt.task[p] : 0u, cl = live ? (uint32_t)cnt.light[p] : 0u;
-  const uint32_t cg = live ? (uint32_t)cnt.big[p] : 0u, cs = live ? (uint32_t)cnt.small[p] : 0u;
+  const uint64_t pc = live ? cnt[p] : 0ull;
+  const uint32_t ct = (uint32_t)(pc & 0xFFFu), cl = (uint32_t)((pc >> 12) & 0xFFFu);
+  const uint32_t cg = (uint32_t)((pc >> 24) & 0xFFFu), cs = (uint32_t)(pc >> 36);
   uint32_t nt32, nl32, ng32, ns32;
   const uint32_t xt = block_xscan(ct, wtot, nt32), xl = block_xscan(cl, wtot, nl32);
   const uint32_t xg = block_xscan(cg, wtot, ng32), xs = block_xscan(cs, wtot, ns32);
@@ -454,9 +458,7 @@ __global__ __launch_bounds__(kPairThreads) void k_pair_emit(PairArgs a, PairCoun
     uint64_t inb[3] = {0, 0, 0};
     if (staged) {
       TaskMeta sm = tm;
-      sm.key = s_key;
-      sm.cat = s_cat;
-      sm.out = s_out;
+      sm.slot = s_slot;
       pair_walk<true>(a, p, n, inb, b, light, heavy, sm, stage, stage + nl, L0, H0, T0);
     } else {
       pair_walk<true>(a, p, n, inb, b, light, heavy, tm);
@@ -470,9 +472,7 @@ __global__ __launch_bounds__(kPairThreads) void k_pair_emit(PairArgs a, PairCoun
   for (uint64_t w = threadIdx.x; w < 5 * nl; w += kPairThreads) l64[w] = s64[w];
   for (uint64_t w = threadIdx.x; w < 5 * nh; w += kPairThreads) h64[w] = s64[5 * nl + w];
   for (uint64_t t = threadIdx.x; t < nt; t += kPairThreads) {
-    tm.key[T0 + t] = s_key[t];
-    tm.cat[T0 + t] = s_cat[t];
-    tm.out[T0 + t] = s_out[t];
+    tm.slot[T0 + t] = s_slot[t];
   }
 }
 
@@ -955,8 +955,7 @@ __global__ __launch_bounds__(256, ROLE == kRoleHeavy ? kHeavyWaves : kLightWaves
     wave_lds_sync(); // the next task restages the same LDS image
     if (lane == 0) {
       tm.type[cur.t] = (uint8_t)ty;
-      tm.card[cur.t] = cw != 0xFFFFFFFFu ? cw : (uint32_t)c;
-      tm.nruns[cur.t] = (uint16_t)nr;
+      tm.res[cur.t] = task_res((uint32_t)ty, nr, cw != 0xFFFFFFFFu ? cw : (uint32_t)c);
     }
     RBG_LT(lt_acc[6] += __builtin_amdgcn_s_memtime() - lt0; ++lt_acc[7]);
     RBG_HT(lt_acc[6] += __builtin_amdgcn_s_memtime() - lt0; ++lt_acc[7]);
@@ -1110,15 +1109,15 @@ __global__ __launch_bounds__(kPairThreads) void k_compact_write(const uint64_t *
       uint32_t tot;
       const uint32_t rank = block_xscan(keep ? 1u : 0u, wtot, tot);
       if (keep) {
-        const uint64_t r = R + rank;
-        const uint32_t c = tm.card[t];
-        const uint16_t nr = tm.nruns[t];
-        out.key[r] = tm.key[t];
+        const uint64_t r = R + rank, rm = tm.res[t], sl = tm.slot[t];
+        const uint32_t c = (uint32_t)(rm >> 32);
+        const uint16_t nr = (uint16_t)(rm >> 8);
+        out.key[r] = (uint16_t)(sl >> 40);
         out.type[r] = ty;
         out.card[r] = c;
         out.nruns[r] = nr;
-        out.off[r] = tm.out[t];
-        outb[tm.cat[t] ? 1 : 0] += alg_bytes(ty, c, nr) + 16;
+        out.off[r] = sl & (kSlotOffsetLimit - 1);
+        outb[(sl >> 56) & 1] += alg_bytes(ty, c, nr) + 16;
         card_sum += c;
       }
       R += tot;
@@ -1128,14 +1127,18 @@ __global__ __launch_bounds__(kPairThreads) void k_compact_write(const uint64_t *
     for (uint64_t t = t0; t < t1; ++t) {
       const uint8_t ty = tm.type[t];
       if (ty == kEmpty) continue;
-      card += tm.card[t];
+      const uint64_t rm = tm.res[t];
+      const uint32_t c = (uint32_t)(rm >> 32);
+      const uint16_t nr = (uint16_t)(rm >> 8);
+      card += c;
       if (out.key) {
-        out.key[r] = tm.key[t];
+        const uint64_t sl = tm.slot[t];
+        out.key[r] = (uint16_t)(sl >> 40);
         out.type[r] = ty;
-        out.card[r] = tm.card[t];
-        out.nruns[r] = tm.nruns[t];
-        out.off[r] = tm.out[t];
-        outb[tm.cat[t] ? 1 : 0] += alg_bytes(ty, tm.card[t], tm.nruns[t]) + 16;
+        out.card[r] = c;
+        out.nruns[r] = nr;
+        out.off[r] = sl & (kSlotOffsetLimit - 1);
+        outb[(sl >> 56) & 1] += alg_bytes(ty, c, nr) + 16;
       }
       ++r;
     }
@@ -1182,17 +1185,17 @@ void launch_pair_rbegin(const uint64_t *seg_begin, uint32_t npairs, const uint64
                                                                                         rbegin, count);
 }
 uint64_t pair_blocks(uint64_t nseg) { return blocks_for(nseg, kPairThreads); }
-void launch_pair_count(const PairArgs &a, const PairCountArrays &c, const PairCountArrays &bt, uint64_t *stats,
+void launch_pair_count(const PairArgs &a, uint64_t *c, const PairCountArrays &bt, uint64_t *stats,
                        hipStream_t st) {
   if (!a.nseg) return;
   k_pair_count<<<blocks_for(a.nseg, kPairThreads), kPairThreads, 0, st>>>(a, c, bt, stats);
 }
-void launch_pair_emit(const PairArgs &a, const PairCountArrays &cnt, const PairCountArrays &bs, uint64_t small_base,
+void launch_pair_emit(const PairArgs &a, const uint64_t *cnt, const PairCountArrays &bs, uint64_t small_base,
                       TaskRec *light, TaskRec *heavy, const TaskMeta &tm, uint64_t *task_begin, const uint64_t *tot,
-                      uint64_t cap, hipStream_t st) {
+                      uint64_t cap, unsigned long long *zero_q, hipStream_t st) {
   if (!a.nseg) return;
   k_pair_emit<<<blocks_for(a.nseg, kPairThreads), kPairThreads, 0, st>>>(a, cnt, bs, small_base, light, heavy, tm,
-                                                                          task_begin, tot, cap);
+                                                                          task_begin, tot, cap, zero_q);
 }
 // Persistent grid: every CU filled to the kernel's occupancy, waves stride over the tasks.
 template <class K> static unsigned persistent_blocks(K kernel, uint64_t tasks) {

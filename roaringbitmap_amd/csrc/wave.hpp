@@ -301,6 +301,23 @@ __device__ __forceinline__ void load_chunks(uint4 (&q)[8], const uint8_t *p, uin
 __device__ __forceinline__ uint32_t mbcnt64(uint64_t m) {
   return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
+// Flags of a 256-thread block: the block's number of set flags (every thread) and a thread's exclusive
+// rank among them — stream compaction of a per-block layout (block totals scanned separately).
+__device__ __forceinline__ uint32_t block_flag_count(bool f, uint32_t *wt) {
+  const uint64_t m = __ballot(f);
+  if ((threadIdx.x & 63) == 0) wt[threadIdx.x >> 6] = (uint32_t)__popcll(m);
+  __syncthreads();
+  return wt[0] + wt[1] + wt[2] + wt[3];
+}
+__device__ __forceinline__ uint32_t block_flag_rank(bool f, uint32_t *wt) {
+  const uint64_t m = __ballot(f);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) wt[w] = (uint32_t)__popcll(m);
+  __syncthreads();
+  uint32_t r = mbcnt64(m);
+  for (int i = 0; i < w; ++i) r += wt[i];
+  return r;
+}
 // The Array filter (A&x, x&A, A\x: the result is a subset of an Array, hence an Array —
 // ArrayContainer.and/andNot, BitmapContainer.and(Array), RunContainer.and(Array):
 // ArrayContainer.java:184-271, BitmapContainer.java:162-172, RunContainer.java:305-336).  F, a sorted

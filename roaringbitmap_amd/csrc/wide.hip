@@ -187,17 +187,25 @@ __global__ __launch_bounds__(256) void k_group_scatter(GroupArgs a, const uint64
 
 // active[k] = 1 when key k (inside the shard's [lo, hi)) produces work: any container, or (AND
 // semantics) one per member
-__global__ __launch_bounds__(256) void k_wide_select(const uint64_t *seg, uint64_t need, uint32_t lo, uint32_t hi,
-                                                     uint64_t *active) {
-  const uint32_t k = blockIdx.x * 256 + threadIdx.x;
-  if (k >= 65536) return;
+// keys that produce work, in a per-block layout: k_wide_select leaves each 256-key block's count in
+// bt, the counts are scanned (scan_blocks_multi: bts, bts[256] = nk) and k_wide_list places the keys
+__device__ __forceinline__ bool wide_active(const uint64_t *seg, uint64_t need, uint32_t lo, uint32_t hi, uint32_t k) {
   const uint64_t m = seg[k + 1] - seg[k];
-  active[k] = (k >= lo && k < hi) && (need ? (m == need) : (m > 0));
+  return (k >= lo && k < hi) && (need ? (m == need) : (m > 0));
 }
-__global__ __launch_bounds__(256) void k_wide_list(const uint64_t *active, const uint64_t *pos, uint32_t *klist) {
+__global__ __launch_bounds__(256) void k_wide_select(const uint64_t *seg, uint64_t need, uint32_t lo, uint32_t hi,
+                                                     uint64_t *bt) {
+  __shared__ uint32_t wt[4];
+  const uint32_t n = block_flag_count(wide_active(seg, need, lo, hi, blockIdx.x * 256 + threadIdx.x), wt);
+  if (threadIdx.x == 0) bt[blockIdx.x] = n;
+}
+__global__ __launch_bounds__(256) void k_wide_list(const uint64_t *seg, uint64_t need, uint32_t lo, uint32_t hi,
+                                                   const uint64_t *bts, uint32_t *klist) {
+  __shared__ uint32_t wt[4];
   const uint32_t k = blockIdx.x * 256 + threadIdx.x;
-  if (k >= 65536) return;
-  if (active[k]) klist[pos[k]] = k;
+  const bool f = wide_active(seg, need, lo, hi, k);
+  const uint32_t r = block_flag_rank(f, wt);
+  if (f) klist[bts[blockIdx.x] + r] = k;
 }
 
 // ---------------------------------------------------------------- per-key folding helpers
@@ -462,20 +470,36 @@ __global__ __launch_bounds__(256) void k_wide_reduce(SetView s, CidMap cm,
   if (ty != kEmpty) stat_add_w(stats, 1, alg_bytes_w(ty, (uint32_t)c, (uint32_t)r) + 16);
 }
 
-__global__ __launch_bounds__(256) void k_wide_keep(const uint8_t *type, uint32_t nk, uint64_t *keep) {
+// Keyed compaction in the per-block layout (as the pairwise compaction): k_wide_keep leaves each
+// block's kept total, one scan_blocks_multi launch scans the block totals (its total, the result
+// container count, goes straight to stats word 8), and k_wide_write ranks its block's results.
+__global__ __launch_bounds__(256) void k_wide_keep(const uint8_t *type, uint32_t nk, uint64_t *bk) {
+  __shared__ uint32_t wt[4];
   const uint32_t q = blockIdx.x * 256 + threadIdx.x;
-  if (q < nk) keep[q] = type[q] != kEmpty;
+  const uint64_t m = __ballot(q < nk && type[q] != kEmpty);
+  if ((threadIdx.x & 63) == 0) wt[threadIdx.x >> 6] = (uint32_t)__popcll(m);
+  __syncthreads();
+  if (threadIdx.x == 0) bk[blockIdx.x] = (uint64_t)wt[0] + wt[1] + wt[2] + wt[3];
 }
+// bks: exclusive scans of the block totals (bks[nblocks] = the total); begin: the result's CSR
 __global__ __launch_bounds__(256) void k_wide_write(const uint32_t *klist, uint32_t nk, WideOut wo,
-                                                    const uint64_t *pos, OutView ov, uint64_t *stats) {
+                                                    const uint64_t *bks, uint32_t nblocks, OutView ov,
+                                                    uint64_t *begin, uint64_t *stats) {
+  __shared__ uint32_t wt[4];
   const uint32_t q = blockIdx.x * 256 + threadIdx.x;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const bool live = q < nk && wo.type[q] != kEmpty;
+  if (blockIdx.x == 0 && threadIdx.x < 2) begin[threadIdx.x] = threadIdx.x ? bks[nblocks] : 0ull;
   // stats word 7: the result's cardinality (RoaringBitmap.getCardinality of the aggregate)
   const uint64_t cs = wave_sum_u64(live ? (uint64_t)wo.card[q] : 0ull);
-  if ((threadIdx.x & 63) == 0 && cs)
+  if (lane == 0 && cs)
     atomicAdd((unsigned long long *)&stats[7 * kStripes + ((q >> 6) & (kStripes - 1))], (unsigned long long)cs);
+  const uint64_t m = __ballot(live);
+  if (lane == 0) wt[w] = (uint32_t)__popcll(m);
+  __syncthreads();
   if (!live) return;
-  const uint64_t r = pos[q];
+  uint64_t r = bks[blockIdx.x] + mbcnt64(m);
+  for (int i = 0; i < w; ++i) r += wt[i];
   ov.key[r] = (uint16_t)klist[q];
   ov.type[r] = wo.type[q];
   ov.card[r] = wo.card[q];
@@ -487,38 +511,42 @@ __global__ __launch_bounds__(256) void k_wide_write(const uint32_t *klist, uint3
 static unsigned nblk(uint64_t n, unsigned per) { return (unsigned)((n + per - 1) / per); }
 
 // Result of a keyed reduction (one 8 KiB slot per active key q, type kEmpty = dropped) -> the
-// one-bitmap result set: drop empties, write key/type/card/nruns/offset, set the CSR.
-int compact_keyed(rbgpu_ctx *ctx, const uint32_t *d_klist, uint32_t nk, const WideOut &wo, rbgpu_set *res,
-                  uint64_t *nres_out) {
+// one-bitmap result set: drop empties, write key/type/card/nruns/offset and the CSR, all on the
+// device with no read-back: the result container count is stats word 8, which stats_end reads
+// (keyed_result_count after it).
+int compact_keyed(rbgpu_ctx *ctx, const uint32_t *d_klist, uint32_t nk, const WideOut &wo, rbgpu_set *res) {
   hipStream_t st = ctx->stream;
-  uint64_t *pin = ctx->h_pinned;
-  if (nk) {
-    uint64_t *keep = nullptr, *pos = nullptr, *tmp2 = nullptr;
-    const uint64_t tw = std::max<uint64_t>(scan_tmp_words(nk), 1);
-    if (ctx->pool.alloc((void **)&keep, (nk + 1) * 8ull) || ctx->pool.alloc((void **)&pos, (nk + 1) * 8ull) ||
-        ctx->pool.alloc((void **)&tmp2, tw * 8))
-      return fail(RB_ENOMEM, "keyed compaction workspace");
-    k_wide_keep<<<nblk(nk, 256), 256, 0, st>>>(wo.type, nk, keep);
-    scan_exclusive(keep, pos, nk, tmp2, st);
-    k_wide_write<<<nblk(nk, 256), 256, 0, st>>>(d_klist, nk, wo, pos,
-                                                OutView{res->key, res->type, res->card, res->nruns, res->off},
-                                                ctx->d_stats);
-    HIPCHK(hipMemcpyAsync(pin + 1, pos + nk, 8, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
-    LAUNCHCHK();
-    ctx->pool.release(keep);
-    ctx->pool.release(pos);
-    ctx->pool.release(tmp2);
-  } else {
-    pin[1] = 0;
+  if (!nk) {
+    HIPCHK(hipMemsetAsync(res->begin, 0, 16, st));
+    return RB_OK;
   }
-  const uint64_t nres = pin[1];
-  const uint64_t hb[2] = {0, nres};
-  HIPCHK(hipMemcpyAsync(res->begin, hb, 16, hipMemcpyHostToDevice, st));
+  const uint32_t nb = nblk(nk, 256);
+  uint64_t *bk = nullptr, *bks = nullptr;
+  if (ctx->pool.alloc((void **)&bk, (nb + 1) * 8ull) || ctx->pool.alloc((void **)&bks, (nb + 1) * 8ull)) {
+    ctx->pool.release(bk);
+    return fail(RB_ENOMEM, "keyed compaction workspace");
+  }
+  k_wide_keep<<<nb, 256, 0, st>>>(wo.type, nk, bk);
+  const uint64_t *in[1] = {bk};
+  uint64_t *outp[1] = {bks};
+  scan_blocks_multi(in, outp, 1, nb, ctx->d_stats + 8 * kStripes, st);
+  k_wide_write<<<nb, 256, 0, st>>>(d_klist, nk, wo, bks, nb,
+                                   OutView{res->key, res->type, res->card, res->nruns, res->off}, res->begin,
+                                   ctx->d_stats);
+  LAUNCHCHK();
+  // pool buffers go back to the pool at once: the pool only hands them out again to later work on
+  // this stream, which runs after these kernels
+  ctx->pool.release(bk);
+  ctx->pool.release(bks);
+  return RB_OK;
+}
+// after stats_end of a call that ran compact_keyed: its result container count, recorded in the stats
+uint64_t keyed_result_count(rbgpu_ctx *ctx, rbgpu_set *res) {
+  const uint64_t nres = ctx->words[8];
+  ctx->last.result_containers = nres;
   res->nc = nres;
   res->h_begin = {0, nres};
-  *nres_out = nres;
-  return RB_OK;
+  return nres;
 }
 
 template <int SEM>
@@ -710,11 +738,16 @@ int wide_run(rbgpu_ctx *ctx, int sem, const rbgpu_set *in, const std::vector<uin
     }
   }
   const CidMap cm{dense ? nullptr : d_cid2, d_mbase};
-  k_wide_select<<<nblk(65536, 256), 256, 0, st>>>(d_seg, and_sem ? (uint64_t)M : 0, key_lo, key_hi, d_active);
-  scan_exclusive(d_active, d_apos, 65536, d_tmp, st);
-  k_wide_list<<<nblk(65536, 256), 256, 0, st>>>(d_active, d_apos, d_klist);
+  {
+    const uint64_t need = and_sem ? (uint64_t)M : 0;
+    k_wide_select<<<256, 256, 0, st>>>(d_seg, need, key_lo, key_hi, d_active);
+    const uint64_t *in1[1] = {d_active};
+    uint64_t *out1[1] = {d_apos};
+    scan_blocks_multi(in1, out1, 1, 256, nullptr, st);
+    k_wide_list<<<256, 256, 0, st>>>(d_seg, need, key_lo, key_hi, d_apos, d_klist);
+  }
   uint64_t *pin = ctx->h_pinned;
-  HIPCHK(hipMemcpyAsync(pin, d_apos + 65536, 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(pin, d_apos + 256, 8, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
   LAUNCHCHK();
   const uint32_t nk = (and_sem && M == 0) ? 0 : (uint32_t)pin[0];
@@ -775,8 +808,7 @@ int wide_run(rbgpu_ctx *ctx, int sem, const rbgpu_set *in, const std::vector<uin
   }
   HIPCHK(hipEventRecord(ctx->ev[2], st));
   // ---- compaction
-  uint64_t nres = 0;
-  rc = compact_keyed(ctx, d_klist, nk, wo, res, &nres);
+  rc = compact_keyed(ctx, d_klist, nk, wo, res);
   if (rc) {
     rbgpu_set_free(res);
     release();
@@ -794,7 +826,8 @@ int wide_run(rbgpu_ctx *ctx, int sem, const rbgpu_set *in, const std::vector<uin
                      : sem == RB_HORIZONTAL_XOR ? "k_wide_reduce<HORIZONTAL_XOR>" : "k_wide_reduce<NAIVE_AND>";
   const KernelSpan spans[1] = {{name, 0, 1, nk}};
   // ev[2] -> ev[3]: nothing; stats_end reads ev[1]..ev[2] for kernel 0
-  rc = stats_end(ctx, N, nres, spans, 1);
+  rc = stats_end(ctx, N, 0, spans, 1);
+  if (!rc) keyed_result_count(ctx, res);
   pool.release(w_type);
   pool.release(w_card);
   pool.release(w_nruns);
@@ -804,8 +837,6 @@ int wide_run(rbgpu_ctx *ctx, int sem, const rbgpu_set *in, const std::vector<uin
     rbgpu_set_free(res);
     return rc;
   }
-  res->nc = nres;
-  res->h_begin = {0, nres};
   *out = res;
   return RB_OK;
 }
