@@ -374,8 +374,13 @@ int set_key_subset(const rbgpu_set *s, uint32_t key_lo, uint32_t key_hi, rbgpu_s
   return upload_host(s->ctx, r, out);
 }
 
+// The counters are zeroed right behind their read-back in stats_end (the memset runs while the host
+// waits anyway), so the next call starts its kernels without one; a call that did not reach
+// stats_end leaves them dirty and the next stats_begin zeroes them.
 void stats_begin(rbgpu_ctx *ctx, bool zero) {
-  if (zero) (void)hipMemsetAsync(ctx->d_stats, 0, kStatWords * kStripes * sizeof(uint64_t), ctx->stream);
+  if (zero && !ctx->stats_clean)
+    (void)hipMemsetAsync(ctx->d_stats, 0, kStatWords * kStripes * sizeof(uint64_t), ctx->stream);
+  ctx->stats_clean = false;
   (void)hipEventRecord(ctx->ev[0], ctx->stream);
 }
 int stats_end(rbgpu_ctx *ctx, uint64_t tasks, uint64_t result_containers, const KernelSpan *k, int n,
@@ -383,8 +388,10 @@ int stats_end(rbgpu_ctx *ctx, uint64_t tasks, uint64_t result_containers, const 
   HIPCHK(hipEventRecord(ctx->ev[5], ctx->stream));
   HIPCHK(hipMemcpyAsync(ctx->h_stats, d_src ? d_src : ctx->d_stats, kStatWords * kStripes * sizeof(uint64_t),
                         hipMemcpyDeviceToHost, ctx->stream));
+  if (!d_src) HIPCHK(hipMemsetAsync(ctx->d_stats, 0, kStatWords * kStripes * sizeof(uint64_t), ctx->stream));
   HIPCHK(hipStreamSynchronize(ctx->stream));
   LAUNCHCHK();
+  if (!d_src) ctx->stats_clean = true;
   uint64_t *w = ctx->words;
   for (int i = 0; i < kStatWords; ++i) {
     w[i] = 0;

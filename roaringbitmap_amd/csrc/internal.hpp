@@ -159,6 +159,7 @@ struct rbgpu_ctx {
   uint64_t words[rbg::kStatWords] = {}; // the last call's counters, summed over stripes
   int refs = 1;                 // the handle + one per live set; destroyed at zero
   bool closed = false;
+  bool stats_clean = false; // d_stats zeroed after the last read-back (stats_begin / stats_end)
 };
 
 struct rbgpu_set {
