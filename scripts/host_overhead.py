@@ -39,8 +39,7 @@ def main():
             dev.append(s.total_ms * 1e-3)
         us = lambda v: round(1e6 * float(np.median(v)), 1)  # noqa: E731
         print({"call_us": us(call), "device_span_us": us(dev), "call_minus_device_us": us(np.subtract(call, dev)),
-               "get_stats_us": us(stats), "set_free_us": us(free), "step_us": us(step),
-               "spin": os.environ.get("RBGPU_SCHEDULE_SPIN", "0")})
+               "get_stats_us": us(stats), "set_free_us": us(free), "step_us": us(step)})
 
 
 if __name__ == "__main__":
