@@ -87,6 +87,11 @@ enum rb_wide_sem {
    *   naive_or / or(Immutable... / Iterator), horizontal_or(Iterator) RB_FAST_OR             :675-692, 776-790, 246-249
    *   naive_xor / xor (every overload)                                RB_FAST_XOR             :728-768, 962-990
    *   horizontal_or / horizontal_xor(Immutable... / Mutable...)       RB_HORIZONTAL_OR / _XOR :188-244, 259-337
+   * and BufferParallelAggregation (buffer/BufferParallelAggregation.java), whose per-key folds are
+   * ParallelAggregation's (clone + lazyIOR below 16 containers, a lazy Bitmap from 16, clone + ixor
+   * with no removal for xor, :194-230):
+   *   BufferParallelAggregation.or(ImmutableRoaringBitmap...)         RB_PAR_OR               :166-180
+   *   BufferParallelAggregation.xor(ImmutableRoaringBitmap...)        RB_PAR_XOR              :187-192
    */
   RB_BUFFER_NAIVE_OR = 12,   /* naive_or / or(MutableRoaringBitmap...): answer.lazyor(b) per bitmap, then
                                 repairAfterLazy — per key the lazyIOR chain from a clone of the first
@@ -322,6 +327,14 @@ void rbgpu_set64_free(rbgpu_set64 *set);
 uint32_t rbgpu_set64_bitmap_count(const rbgpu_set64 *set);
 /* bucket highs of bitmap i (up to cap of them into highs, may be NULL); *count = its bucket count */
 int rbgpu_set64_buckets(const rbgpu_set64 *set, uint32_t i, uint32_t *highs, uint64_t cap, uint64_t *count);
+/* The buckets of 64-bit bitmap i as a new 32-bit set, bitmap k = its k-th bucket (highs from
+ * rbgpu_set64_buckets), containers bytes-identical — empty ones a Roaring64Bitmap keeps included: the
+ * view toArray / select iterate (longlong/Roaring64Bitmap.java:106, 946; Roaring64NavigableMap.java:351,
+ * 1409). */
+int rbgpu_set64_bucket_set(const rbgpu_set64 *set, uint32_t i, rbgpu_set **out);
+/* A copy of 64-bit bitmaps [first, first+count), buckets and all (Roaring64Bitmap.clone,
+ * longlong/Roaring64Bitmap.java:1159; Roaring64NavigableMap's copy is per bucket, :744-803). */
+int rbgpu_set64_extract(const rbgpu_set64 *set, uint32_t first, uint32_t count, rbgpu_set64 **out);
 /* getLongCardinality per bitmap */
 int rbgpu_set64_cardinalities(const rbgpu_set64 *set, uint64_t *out);
 /* portable serialized size per bitmap, and the bytes of bitmaps [first, first+count) back to back */

@@ -9,7 +9,7 @@ from ._lib import (AND, ANDNOT, ARRAY, BITMAP, FAST_AND, FAST_OR, FAST_XOR, NAIV
                    PAR_OR, PAR_XOR, RUN, WL_FILTER_POSTING, WL_WIDE_DENSE, WL_WIDE_MIXED, WL_WIDE_RUNS,
                    WORKSHY_AND, XOR, FormatError, InvalidArgument, RbError)
 from .engine import Context, DeviceSet, HostSoA, default_context, soa_from_values
-from .roaring import (BufferFastAggregation, FastAggregation, ParallelAggregation, Roaring64Bitmap,
+from .roaring import (BufferFastAggregation, BufferParallelAggregation, FastAggregation, ParallelAggregation, Roaring64Bitmap,
                       Roaring64NavigableMap, RoaringBitmap)
 from .bsi import Operation, Roaring64BitmapSliceIndex, RoaringBitmapSliceIndex
 from ._lib import BSI_EQ, BSI_GE, BSI_GT, BSI_LE, BSI_LT, BSI_NEQ, BSI_RANGE
@@ -22,7 +22,7 @@ __all__ = [
     "AND", "OR", "XOR", "ANDNOT", "ARRAY", "BITMAP", "RUN",
     "FAST_OR", "FAST_AND", "WORKSHY_AND", "NAIVE_AND", "FAST_XOR", "PAR_OR", "PAR_XOR", "NAIVE_AND_ITER",
     "HORIZONTAL_OR", "HORIZONTAL_XOR", "PQ_OR", "PQ_XOR", "Comm",
-    "BUFFER_NAIVE_OR", "BUFFER_PQ_OR", "BUFFER_PQ_OR_ITER", "BUFFER_PQ_XOR", "BufferFastAggregation",
+    "BUFFER_NAIVE_OR", "BUFFER_PQ_OR", "BUFFER_PQ_OR_ITER", "BUFFER_PQ_XOR", "BufferFastAggregation", "BufferParallelAggregation",
     "WL_FILTER_POSTING", "WL_WIDE_DENSE", "WL_WIDE_MIXED", "WL_WIDE_RUNS",
     "Context", "DeviceSet", "HostSoA", "default_context", "soa_from_values",
     "RoaringBitmap", "FastAggregation", "ParallelAggregation", "Roaring64Bitmap", "Roaring64NavigableMap",

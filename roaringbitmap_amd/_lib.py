@@ -106,6 +106,8 @@ SIGNATURES = {
     "rbgpu_set64_free": (None, [_P]),
     "rbgpu_set64_bitmap_count": (C.c_uint32, [_P]),
     "rbgpu_set64_buckets": (C.c_int, [_P, C.c_uint32, _U32P, C.c_uint64, _U64P]),
+    "rbgpu_set64_bucket_set": (C.c_int, [_P, C.c_uint32, C.POINTER(_P)]),
+    "rbgpu_set64_extract": (C.c_int, [_P, C.c_uint32, C.c_uint32, C.POINTER(_P)]),
     "rbgpu_set64_cardinalities": (C.c_int, [_P, _U64P]),
     "rbgpu_set64_portable_sizes": (C.c_int, [_P, _U64P]),
     "rbgpu_set64_serialize_portable": (C.c_int, [_P, C.c_uint32, C.c_uint32, C.c_void_p, C.c_uint64, _U64P]),

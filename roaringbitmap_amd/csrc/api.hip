@@ -374,6 +374,32 @@ int set_key_subset(const rbgpu_set *s, uint32_t key_lo, uint32_t key_hi, rbgpu_s
   return upload_host(s->ctx, r, out);
 }
 
+// Bitmaps idx[0..n) of s as a new set, in that order (a device-resident copy through the host; the
+// containers stay bytes-identical, empty ones included).
+int set_gather(const rbgpu_set *s, const uint32_t *idx, uint32_t n, rbgpu_set **out) {
+  for (uint32_t i = 0; i < n; ++i)
+    if (idx[i] >= s->nb) return fail(RB_EINVAL, "bitmap %u out of range", idx[i]);
+  HostSoA h;
+  int rc = s->nb ? download_host(s, 0, s->nb, h) : RB_OK;
+  if (rc) return rc;
+  HostSoA r;
+  r.nb = n;
+  r.begin.assign(1, 0);
+  for (uint32_t k = 0; k < n; ++k) {
+    for (uint64_t i = h.begin[idx[k]]; i < h.begin[idx[k] + 1]; ++i) {
+      const uint64_t bytes = payload_bytes(h.type[i], h.card[i], h.nruns[i]);
+      r.key.push_back(h.key[i]);
+      r.type.push_back(h.type[i]);
+      r.card.push_back(h.card[i]);
+      r.nruns.push_back(h.nruns[i]);
+      r.off.push_back(r.payload.size());
+      r.payload.insert(r.payload.end(), h.payload.begin() + h.off[i], h.payload.begin() + h.off[i] + round16(bytes));
+    }
+    r.begin.push_back(r.key.size());
+  }
+  return upload_host(s->ctx, r, out);
+}
+
 // The counters are zeroed right behind their read-back in stats_end (the memset runs while the host
 // waits anyway), so the next call starts its kernels without one; a call that did not reach
 // stats_end leaves them dirty and the next stats_begin zeroes them.
@@ -1034,11 +1060,7 @@ int pairwise_impl(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu_set *b
   // small batches: the merge-path segment counts come from the host CSR copies (no count kernel,
   // scan and host read-back before the segment phase)
   const bool host_segs = np && np <= 4096 && !ensure_h_begin(a) && !ensure_h_begin(b);
-  uint32_t seg_keys = pairwise_seg_keys(a, b, np);
-  if (host_segs) { // latency study knob: merge-path segment length of small batches
-    static const int sk = getenv("RBGPU_SMALL_SEG_KEYS") ? atoi(getenv("RBGPU_SMALL_SEG_KEYS")) : 0;
-    if (sk > 0) seg_keys = std::min<uint32_t>((uint32_t)sk, kMaxSegKeys);
-  }
+  const uint32_t seg_keys = pairwise_seg_keys(a, b, np);
   if (d_aidx || d_bidx || host_segs) { // through pinned staging: a pageable copy would block the host
     const size_t bytes = np * 4 * ((d_aidx != nullptr) + (d_bidx != nullptr)) + (host_segs ? (np + 1) * 8 : 0);
     if (bytes > ctx->h_stage_cap) {
@@ -1124,9 +1146,8 @@ int pairwise_impl(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu_set *b
   // sized by that bound and the emit kernel reads the totals on the device: it runs while the host
   // waits for the totals, allocates the result and launches the task kernels.  Otherwise the host
   // reads the totals first (the bound is the segments' key capacity, too loose to reserve).
-  // light tasks from a shared chunk queue (a second light launch takes over the heavy kernel's CUs
-  // when it finishes) unless RBGPU_STATIC_LIGHT is set
-  static const bool static_light = getenv("RBGPU_STATIC_LIGHT") != nullptr;
+  // light tasks come from a shared chunk queue (a second light launch takes over the heavy kernel's
+  // CUs when it finishes)
   const uint64_t seg_cap = ns * (uint64_t)seg_keys;
   const uint64_t tbound = !d_aidx && !d_bidx ? std::min<uint64_t>(a->nc + b->nc, seg_cap) : seg_cap;
   const bool early = !probe && ns && tbound <= kEarlyEmitTasks;
@@ -1154,7 +1175,7 @@ int pairwise_impl(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu_set *b
   if (early) {
     if ((rc = take_tasks(tbound))) return rc;
     HIPCHK(hipEventRecord(ctx->ev_tot, st));
-    launch_pair_emit(pa, cnt, bs, 0, light, nullptr, tm, task_begin, d_tot, tbound, static_light ? nullptr : queue,
+    launch_pair_emit(pa, cnt, bs, 0, light, nullptr, tm, task_begin, d_tot, tbound, queue,
                      st);
     HIPCHK(hipEventSynchronize(ctx->ev_tot));
   } else {
@@ -1188,13 +1209,12 @@ int pairwise_impl(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu_set *b
     }
   }
   // the light and heavy task kernels run concurrently (heavy on the side stream, 1 block per CU;
-  // light 2 blocks per CU: 2 x 128 + 256 VGPRs per SIMD) unless RBGPU_SERIAL_TASKS is set
-  static const bool serial = getenv("RBGPU_SERIAL_TASKS") != nullptr;
-  const bool conc = !probe && !serial && nlight && nheavy && nlight + nheavy >= 65536; // small batches: the
+  // light 2 blocks per CU: 2 x 128 + 256 VGPRs per SIMD)
+  const bool conc = !probe && nlight && nheavy && nlight + nheavy >= 65536; // small batches: the
                                                   // cross-stream waits cost more than the overlap
   // the emit zeroes the queue counters before ev[1]: the side stream waits on ev[1] before its light launch
   if (!early)
-    launch_pair_emit(pa, cnt, bs, small_base, light, heavy, tm, task_begin, nullptr, 0, static_light ? nullptr : queue,
+    launch_pair_emit(pa, cnt, bs, small_base, light, heavy, tm, task_begin, nullptr, 0, queue,
                      st);
   HIPCHK(hipEventRecord(ctx->ev[1], st));
   if (probe) {
@@ -1217,7 +1237,7 @@ int pairwise_impl(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu_set *b
     HIPCHK(hipStreamWaitEvent(ctx->side, ctx->ev[1], 0));
     launch_pairwise_concurrent(kop, card_only, a->payload, b->payload, light, nlight, heavy, nheavy,
                                res ? res->payload : nullptr, tm, st, ctx->side, ctx->ev[2], ctx->ev_side[0],
-                               ctx->ev_side[1], static_light ? nullptr : queue);
+                               ctx->ev_side[1], queue);
     HIPCHK(hipEventRecord(ctx->ev_side[2], ctx->side));
     HIPCHK(hipStreamWaitEvent(st, ctx->ev_side[2], 0));
   } else {

@@ -471,42 +471,6 @@ __global__ __launch_bounds__(128, 2) void k_bsi_range(SetView bsi, SetView fnd, 
   }
 }
 
-// RANGE = and(GE(start), LE(end)) (RoaringBitmapSliceIndex.java:492-497) on the two chains' keyed
-// slots: both are indexed by the same key list, so the static AND is one wave per key (AND rule:
-// R&R -> EFF, else AB; empty or one-sided -> dropped).
-__global__ __launch_bounds__(256) void k_bsi_and(const uint8_t *__restrict__ ga, WideOut wa,
-                                                 const uint8_t *__restrict__ gb, WideOut wb, uint32_t nk,
-                                                 uint8_t *__restrict__ out, WideOut wo, uint64_t *stats) {
-  __shared__ __attribute__((aligned(16))) uint32_t lds[4][2048];
-  const int lane = lane_id();
-  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint32_t q = xcd_swizzle(blockIdx.x, gridDim.x) * 4 + wv;
-  if (q >= nk) return;
-  uint32_t *s = lds[wv];
-  const int ta = wa.type[q], tb = wb.type[q];
-  Meta rm{0, 0, 0, 0};
-  uint64_t a[kW];
-  if (ta != kEmpty && tb != kEmpty) {
-    const Meta ma{1, ta, (int)wa.card[q], wa.nruns[q]}, mb{1, tb, (int)wb.card[q], wb.nruns[q]};
-    load_container(ta, ga + (uint64_t)q * kBitmapBytes, (uint32_t)ma.card, (uint32_t)ma.runs, s, a, lane);
-    stage_container(tb, gb + (uint64_t)q * kBitmapBytes, (uint32_t)mb.card, (uint32_t)mb.runs, s, lane);
-#pragma unroll
-    for (int j = 0; j < kW; ++j) a[j] &= lds_word(s, j, lane);
-    wave_lds_sync();
-    rm = classify(a, lane, eff_and(ma, mb), false, false);
-  }
-  const int ty = rm.present ? rm.type : kEmpty;
-  if (rm.present) emit_container(ty, a, rm.card, rm.runs, out + (uint64_t)q * kBitmapBytes, s, lane);
-  if (lane == 0) {
-    wo.type[q] = (uint8_t)ty;
-    wo.card[q] = (uint32_t)(rm.present ? rm.card : 0);
-    wo.nruns[q] = (uint16_t)(ty == kRun ? rm.runs : 0);
-    if (rm.present)
-      atomicAdd((unsigned long long *)&stats[1 * kStripes + (q & (kStripes - 1))],
-                (unsigned long long)(payload_bytes(ty, rm.card, rm.runs) + (ty == kRun ? 2 : 0) + 16));
-  }
-}
-
 // ---------------------------------------------------------------- host side
 static unsigned nblk(uint64_t n, unsigned per) { return (unsigned)((n + per - 1) / per); }
 
@@ -635,38 +599,24 @@ int bsi_compare(rbgpu_ctx *ctx, const rbgpu_set *bsi, int op, uint64_t start, ui
     release();
     return rc;
   }
-  static const bool no_fuse = getenv("RBGPU_BSI_UNFUSED_RANGE") != nullptr;
-  const bool fused_range = op == 6 && !no_fuse;
-  KeyedSlots fin, ge, le;
+  KeyedSlots fin;
   rc = fin.alloc(ctx, nk, false);
-  if (!rc && op == 6 && !fused_range) rc = ge.alloc(ctx, nk, true);
-  if (!rc && op == 6 && !fused_range) rc = le.alloc(ctx, nk, true);
   if (!rc) {
     HIPCHK(hipEventRecord(ctx->ev[1], st));
     if (op != 6) {
       bsi_chain(ctx, bsi, nbits, op, start, found, d_table, d_klist, nk, res->payload, fin.wo);
-    } else if (fused_range) { // RANGE: both chains in one pass, then the keyed static AND in-kernel
-      if (nk)
-        k_bsi_range<<<nblk(nk, 2), 128, 0, st>>>(bsi->view(), found ? found->view() : bsi->view(), found != nullptr,
-                                                 d_table, nbits, start, end, d_klist, nk, res->payload, fin.wo,
-                                                 ctx->d_stats);
-    } else { // RANGE: the two chains, then the keyed static AND
-      bsi_chain(ctx, bsi, nbits, kBsiGE, start, found, d_table, d_klist, nk, ge.payload, ge.wo);
-      bsi_chain(ctx, bsi, nbits, kBsiLE, end, found, d_table, d_klist, nk, le.payload, le.wo);
-      if (nk) k_bsi_and<<<nblk(nk, 4), 256, 0, st>>>(ge.payload, ge.wo, le.payload, le.wo, nk, res->payload, fin.wo,
-                                                    ctx->d_stats);
+    } else if (nk) { // RANGE: both chains in one pass, then the keyed static AND in-kernel
+      k_bsi_range<<<nblk(nk, 2), 128, 0, st>>>(bsi->view(), found ? found->view() : bsi->view(), found != nullptr,
+                                               d_table, nbits, start, end, d_klist, nk, res->payload, fin.wo,
+                                               ctx->d_stats);
     }
     HIPCHK(hipEventRecord(ctx->ev[2], st));
     rc = compact_keyed(ctx, d_klist, nk, fin.wo, res);
-    const KernelSpan spans[1] = {{fused_range ? "k_bsi_range" : "k_bsi_chain", 0, 1, op == 6 ? 2ull * nk : nk}};
+    const KernelSpan spans[1] = {{op == 6 ? "k_bsi_range" : "k_bsi_chain", 0, 1, op == 6 ? 2ull * nk : nk}};
     if (!rc) rc = stats_end(ctx, nk, 0, spans, 1);
     if (!rc) keyed_result_count(ctx, res);
   }
   fin.release(ctx, false);
-  if (op == 6 && !fused_range) {
-    ge.release(ctx, true);
-    le.release(ctx, true);
-  }
   release();
   if (rc) {
     rbgpu_set_free(res);

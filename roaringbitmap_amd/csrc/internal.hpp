@@ -234,6 +234,7 @@ int bsi_compare(rbgpu_ctx *ctx, const rbgpu_set *bsi, int op, uint64_t start, ui
                 uint64_t vmax, const rbgpu_set *found, uint32_t key_lo, uint32_t key_hi, rbgpu_set **out);
 // api.hip: the containers of bitmap 0 of `s` with keys in [key_lo, key_hi), as a new one-bitmap set
 int set_key_subset(const rbgpu_set *s, uint32_t key_lo, uint32_t key_hi, rbgpu_set **out);
+int set_gather(const rbgpu_set *s, const uint32_t *idx, uint32_t n, rbgpu_set **out);
 // codec.hip: RoaringFormatSpec on the device.  d_in is readable up to in_lim; d_in_off[n + 1] (device).
 int deserialize_device(rbgpu_ctx *ctx, const uint8_t *d_in, uint64_t in_lim, const uint64_t *d_in_off, uint32_t n,
                        rbgpu_set **out);

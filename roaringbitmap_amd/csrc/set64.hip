@@ -205,6 +205,40 @@ int rbgpu_set64_buckets(const rbgpu_set64 *s, uint32_t i, uint32_t *highs, uint6
   return RB_OK;
 }
 
+int rbgpu_set64_bucket_set(const rbgpu_set64 *s, uint32_t i, rbgpu_set **out) {
+  if (!s || !out) return fail(RB_EINVAL, "null argument");
+  *out = nullptr;
+  if (i >= s->n()) return fail(RB_EINVAL, "bitmap %u out of range", i);
+  const std::vector<uint32_t> idx(s->idx.begin() + s->begin[i], s->idx.begin() + s->begin[i + 1]);
+  if (idx.empty()) return (*out = empty_set(s->ctx)) ? RB_OK : fail(RB_ENOMEM, "empty set");
+  return set_gather(s->buckets, idx.data(), (uint32_t)idx.size(), out);
+}
+
+int rbgpu_set64_extract(const rbgpu_set64 *s, uint32_t first, uint32_t count, rbgpu_set64 **out) {
+  if (!s || !out) return fail(RB_EINVAL, "null argument");
+  *out = nullptr;
+  if ((uint64_t)first + count > s->n()) return fail(RB_EINVAL, "bitmap range out of bounds");
+  rbgpu_set64 *r = new rbgpu_set64;
+  r->ctx = s->ctx;
+  r->begin.push_back(0);
+  for (uint32_t i = first; i < first + count; ++i) {
+    for (uint64_t k = s->begin[i]; k < s->begin[i + 1]; ++k) {
+      r->high.push_back(s->high[k]);
+      r->idx.push_back((uint32_t)r->idx.size());
+    }
+    r->begin.push_back(r->high.size());
+  }
+  const std::vector<uint32_t> idx(s->idx.begin() + s->begin[first], s->idx.begin() + s->begin[first + count]);
+  const int rc = idx.empty() ? ((r->buckets = empty_set(s->ctx)) ? RB_OK : fail(RB_ENOMEM, "empty set"))
+                             : set_gather(s->buckets, idx.data(), (uint32_t)idx.size(), &r->buckets);
+  if (rc) {
+    delete r;
+    return rc;
+  }
+  *out = r;
+  return RB_OK;
+}
+
 int rbgpu_set64_cardinalities(const rbgpu_set64 *s, uint64_t *out) {
   if (!s || !out) return fail(RB_EINVAL, "null argument");
   std::vector<uint64_t> c(std::max<uint32_t>(s->buckets->nb, 1));

@@ -615,6 +615,28 @@ class DeviceSet64:
         L.check(L.lib().rbgpu_set64_buckets(self.h, i, out.ctypes.data_as(L._U32P), cnt.value, C.byref(cnt)))
         return out[:cnt.value]
 
+    def bucket_set(self, i: int) -> "DeviceSet":
+        """rbgpu_set64_bucket_set: bitmap i's buckets as a 32-bit set (bitmap k = bucket k), empty
+        containers a Roaring64Bitmap keeps included."""
+        out = C.c_void_p()
+        L.check(L.lib().rbgpu_set64_bucket_set(self.h, i, C.byref(out)))
+        return DeviceSet(self.ctx, out.value)
+
+    def extract(self, first: int, count: int) -> "DeviceSet64":
+        """rbgpu_set64_extract: a copy of bitmaps [first, first+count)."""
+        out = C.c_void_p()
+        L.check(L.lib().rbgpu_set64_extract(self.h, first, count, C.byref(out)))
+        return DeviceSet64(self.ctx, out.value)
+
+    def values(self, i: int) -> np.ndarray:
+        """Every value of bitmap i, ascending unsigned: each bucket's low halves under its high."""
+        highs = self.highs(i)
+        if not len(highs):
+            return np.zeros(0, np.uint64)
+        h = self.bucket_set(i).download()
+        return np.concatenate([(np.uint64(hi) << np.uint64(32)) | h.values(k).astype(np.uint64)
+                               for k, hi in enumerate(highs.tolist())])
+
     def serialize_portable(self) -> List[bytes]:
         n = len(self)
         if n == 0:

@@ -14,6 +14,7 @@ MI355X through librbgpu (no CPU fallback).
   FastAggregation.naive_and/workShyAnd/...      FastAggregation.java:328, 356, 477, 541, 576
   ParallelAggregation.or_/xor(*bitmaps)         ParallelAggregation.java:161, 182
   BufferFastAggregation.*                       buffer/BufferFastAggregation.java
+  BufferParallelAggregation.or_/xor             buffer/BufferParallelAggregation.java:166, 187
   serialize / deserialize                       RoaringArray.java:851-940, 276-348
 
 Python reserves `and`/`or`, so those two carry a trailing underscore.  Called on the class with two
@@ -423,6 +424,21 @@ class BufferFastAggregation:
         return _wide(L.BUFFER_PQ_XOR, bitmaps, empty_ok=False)
 
 
+class BufferParallelAggregation:
+    """org.roaringbitmap.buffer.BufferParallelAggregation (buffer/BufferParallelAggregation.java): the
+    per-key folds are ParallelAggregation's (:194-230), so or / xor are RB_PAR_OR / RB_PAR_XOR."""
+
+    @staticmethod
+    def or_(*bitmaps) -> RoaringBitmap:
+        """or(ImmutableRoaringBitmap...) (:166-180)."""
+        return _wide(L.PAR_OR, bitmaps)
+
+    @staticmethod
+    def xor(*bitmaps) -> RoaringBitmap:
+        """xor(ImmutableRoaringBitmap...) (:187-192)."""
+        return _wide(L.PAR_XOR, bitmaps)
+
+
 class _Bitmap64:
     """Shared surface of the two 64-bit classes (one 64-bit bitmap resident in HBM as buckets)."""
 
@@ -449,32 +465,26 @@ class _Bitmap64:
         return int(self._set.cardinalities()[0])
 
     def isEmpty(self) -> bool:
-        return self.getLongCardinality() == 0 and len(self._set.highs(0)) == 0
+        """getLongCardinality() == 0 (Roaring64NavigableMap.java:1148, Roaring64Bitmap.java:837): emptied
+        buckets and kept empty xor containers do not count."""
+        return self.getLongCardinality() == 0
 
     def toArray(self) -> np.ndarray:
-        """Every value, ascending unsigned (the buckets' low halves under their highs)."""
-        import struct
-        from .engine import soa_from_serialized
-        from .sharding import header_size
-        data = self.serializePortable()
-        (n,) = struct.unpack_from("<Q", data, 0)
-        pos, out = 8, []
-        for _ in range(n):
-            (h,) = struct.unpack_from("<I", data, pos)
-            pos += 4
-            soa = soa_from_serialized([data[pos:]])
-            k = len(soa.key)
-            body = sum(8192 if t == L.BITMAP else 2 * int(c) if t == L.ARRAY else 2 + 4 * int(r)
-                       for t, c, r in zip(soa.type.tolist(), soa.card.tolist(), soa.nruns.tolist()))
-            pos += header_size(k, bool((soa.type == L.RUN).any())) + body
-            out.append((np.uint64(h) << np.uint64(32)) | soa.values(0).astype(np.uint64))
-        return np.concatenate(out) if out else np.zeros(0, np.uint64)
+        """Every value, ascending unsigned (Roaring64Bitmap.java:946, Roaring64NavigableMap.java:1409):
+        read from the device buckets, so a kept empty container contributes nothing."""
+        return self._set.values(0)
 
     def select(self, j: int) -> int:
-        return int(self.toArray()[j])
+        """select(j) (Roaring64Bitmap.java:106, Roaring64NavigableMap.java:351): IllegalArgumentException
+        (ValueError) past the cardinality."""
+        v = self.toArray()
+        if not 0 <= j < len(v):
+            raise ValueError(f"select {j} when the cardinality is {len(v)}")
+        return int(v[j])
 
     def clone(self):
-        return type(self).deserializePortable(self.serializePortable())
+        """A device copy (rbgpu_set64_extract), the kept empty containers included."""
+        return type(self)(self._set.extract(0, 1))
 
     def _inplace(self, op: int, x2) -> None:
         b = self._set if x2 is self else x2._set  # x2 == this: the same set and index on both sides

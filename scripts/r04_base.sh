@@ -1,0 +1,8 @@
+#!/bin/bash
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
+mkdir -p gpurun_out/r4base
+export HSA_ENABLE_IPC_MODE_LEGACY=0
+scripts/gpu_steps.sh \
+  "h1:200:python bench.py --secondary none --steps 20 --no-cpu-baseline > gpurun_out/r4base/h1.json" \
+  "h2:200:python bench.py --secondary none --steps 20 --no-cpu-baseline > gpurun_out/r4base/h2.json" \
+  "def:400:python bench.py --no-cpu-baseline > gpurun_out/r4base/default.json"

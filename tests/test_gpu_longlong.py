@@ -130,3 +130,61 @@ def test_roaring64_python_mirror(ctx, oracle):
     assert fx.select(90) == (9 << 32) and fx.select(99) == (9 << 32) + 9
     with pytest.raises(rb.InvalidArgument):  # Roaring64NavigableMap has no static and/or/xor/andNot
         ctx.pairwise64(rb.RB64_NAVIGABLE, rb.AND, fx._set, fx._set, [0], [0])
+
+
+def test_roaring64_kept_empty_container_through_later_ops(ctx, oracle):
+    """A Roaring64Bitmap keeps the empty container an xor leaves (Roaring64Bitmap.java:392-460).  Later
+    in-place and static ops treat it like any other container: an andNot / or / xor against a bitmap
+    without that high (or without that key under it) leaves it untouched or clones it (:319-343, 599-628,
+    630-650), a matched and / andNot drops it, a matched or fills it."""
+    import roaringbitmap_amd as rb
+    from oracle import rbref64 as R64
+    same = np.concatenate([np.arange(0, 30000, 3, dtype=np.uint64),                       # Bitmap at key 0
+                           (1 << 16) + np.arange(100, 200, dtype=np.uint64)])            # Array at key 1
+    x = R64.Ref64.of(np.concatenate([same, (1 << 32) + np.arange(10, dtype=np.uint64)]))
+    y = R64.Ref64.of(same)
+    z_other_high = R64.Ref64.of((9 << 32) + np.arange(5, dtype=np.uint64))
+    z_other_key = R64.Ref64.of((5 << 16) + np.arange(5, dtype=np.uint64))
+    z_matched = R64.Ref64.of(np.arange(0, 90, 3, dtype=np.uint64))
+    s = ctx.upload_portable64([r.to_portable() for r in (x, y, z_other_high, z_other_key, z_matched)])
+    xy = ctx.pairwise64(rb.RB64_BITMAP, rb.XOR, s, s, [0], [1], inplace=True)
+    ref_xy = R64.bitmap_op(rb.XOR, x, y, True)
+    assert xy.serialize_portable()[0] == ref_xy.to_portable()
+    assert [c[2] for c in ref_xy.buckets[0][1].containers()] == [0, 0]  # two kept empty containers
+    pool = [r.to_portable() for r in (ref_xy, z_other_high, z_other_key, z_matched)]
+    s2 = ctx.upload_portable64(pool)
+    refs = [ref_xy, z_other_high, z_other_key, z_matched]
+    for opname, op in OPS.items():
+        for j in (1, 2, 3):
+            for inplace in (False, True):
+                got = ctx.pairwise64(rb.RB64_BITMAP, op, s2, s2, [0], [j], inplace=inplace).serialize_portable()[0]
+                want = R64.bitmap_op(op, refs[0], refs[j], inplace)
+                assert got == want.to_portable(), (opname, j, inplace)
+
+
+def test_roaring64_mirror_after_empty_xor(ctx, oracle):
+    """isEmpty is getLongCardinality() == 0 (Roaring64NavigableMap.java:1148, Roaring64Bitmap.java:837);
+    toArray / select / clone read the device buckets, so the empty containers a Roaring64Bitmap xor keeps
+    (or the empty buckets a Roaring64NavigableMap and leaves) read back correctly."""
+    import roaringbitmap_amd as rb
+    from oracle import rbref64 as R64
+    same = np.concatenate([np.arange(0, 30000, 3, dtype=np.uint64), (1 << 16) + np.arange(100, 200, dtype=np.uint64)])
+    extra = (3 << 32) + np.arange(7, dtype=np.uint64)
+    for cls in (rb.Roaring64Bitmap, rb.Roaring64NavigableMap):
+        x, y = cls.bitmapOf(np.concatenate([same, extra])), cls.bitmapOf(same)
+        x.xor(y)
+        assert not x.isEmpty()
+        assert np.array_equal(x.toArray(), extra)
+        assert x.select(3) == int(extra[3])
+        with pytest.raises(ValueError):
+            x.select(7)
+        c = x.clone()
+        assert c.serializePortable() == x.serializePortable()
+        assert np.array_equal(c.toArray(), extra)
+        x.andNot(cls.bitmapOf(extra))
+        assert x.isEmpty() and x.getLongCardinality() == 0 and len(x.toArray()) == 0
+    nav = rb.Roaring64NavigableMap.bitmapOf([1])
+    nav.and_(rb.Roaring64NavigableMap.bitmapOf([2]))  # the emptied bucket stays in the map
+    assert nav.isEmpty() and len(nav._set.highs(0)) == 1
+    ref = R64.navigable_op(rb.AND, R64.Ref64.of([1]), R64.Ref64.of([2]))
+    assert nav.serializePortable() == ref.to_portable()

@@ -267,3 +267,26 @@ def test_ornot_fuzz_fixture_through_the_device(ctx, oracle):
     assert got.serialize() == [want.serialize()]
     ra = refs[1].to_array()
     assert int(got.cardinalities()[0]) == limit - int((ra < limit).sum())
+
+
+def test_small_batch_kernel_timing_switch(ctx, oracle, pair_path, monkeypatch):
+    """RBGPU_SMALL_KERNEL_TIMES=1 (the bench's per-kernel census breakdown) only adds timing events
+    around the small-batch launches: the same bytes, and both kernels' times in the call's stats."""
+    if pair_path != "small":
+        pytest.skip("small-batch path only")
+    bms = synthetic_bitmaps(40, seed=5)
+    s = ctx.upload_values(bms, run_optimize=True)
+    refs = _ref_list(oracle, s.serialize())
+    a_idx = np.arange(39, dtype=np.uint32)
+    b_idx = a_idx + 1
+    for flag in ("0", "1"):
+        monkeypatch.setenv("RBGPU_SMALL_KERNEL_TIMES", flag)
+        for opname, op in OPS.items():
+            got = ctx.pairwise(op, s, s, a_idx, b_idx).serialize()
+            for k in range(len(a_idx)):
+                assert got[k] == oracle.op(op, refs[k], refs[k + 1]).serialize(), (flag, opname, k)
+            names = [k["name"] for k in ctx.stats()["kernels"]]
+            if flag == "1":
+                assert names[:2] == ["k_pair_small", "k_pair_small_compact"], names
+            else:
+                assert not names, names

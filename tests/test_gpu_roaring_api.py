@@ -131,3 +131,24 @@ def test_buffer_reference_vectors():
     assert B.priorityqueue_xor(d1, d2).toArray().tolist() == want3
     with pytest.raises(ValueError):
         B.priorityqueue_xor(d1)
+
+
+def test_buffer_parallel_aggregation(oracle, census):
+    """BufferParallelAggregation.or / xor (buffer/BufferParallelAggregation.java:166-192) fold each key
+    like ParallelAggregation (clone + lazyIOR below 16 containers, a lazy Bitmap from 16; clone + ixor
+    with no removal): the RB_PAR_OR / RB_PAR_XOR results, on census bitmaps and on a run-optimised mix of
+    Array / Bitmap / Run containers (the lazyIOR chain's states)."""
+    from datasets import synthetic_bitmaps
+    from roaringbitmap_amd import BufferParallelAggregation as BP
+    from roaringbitmap_amd import RoaringBitmap
+    bms, refs = census
+    mixed_vals = synthetic_bitmaps(40, seed=11)
+    mixed = [RoaringBitmap.bitmapOf(v) for v in mixed_vals]
+    for b in mixed[::2]:
+        b.runOptimize()
+    mixed_refs = [oracle.RefBitmap.deserialize(b.serialize()) for b in mixed]
+    for pool, rpool in ((bms, refs), (mixed, mixed_refs)):
+        for lo, n in ((0, 2), (1, 9), (0, 17), (0, len(pool))):
+            sub, rsub = pool[lo:lo + n], rpool[lo:lo + n]
+            assert BP.or_(*sub).serialize() == oracle.wide(oracle.PAR_OR, rsub).serialize(), n
+            assert BP.xor(*sub).serialize() == oracle.wide(oracle.PAR_XOR, rsub).serialize(), n
