@@ -365,6 +365,26 @@ int rbgpu_comm_unique_id(uint8_t id[RB_COMM_ID_BYTES]);
 int rbgpu_comm_init(rbgpu_ctx *ctx, const uint8_t id[RB_COMM_ID_BYTES], int nranks, int rank, rbgpu_comm **out);
 void rbgpu_comm_destroy(rbgpu_comm *comm);
 
+/* A caller-provided host transport (the JVM's own channel, MPI, a torch.distributed group): the same
+ * exchange as the RCCL communicator — summaries, failure agreement, naive_and's global order, the shard
+ * gather and the header assembly — with the shard bytes moving through host memory.  Every callback is
+ * collective in the usual sense (all ranks call it in the same order) except send / recv, which pair
+ * rank -> root.  Return 0 on success.  The callbacks must outlive the communicator. */
+typedef struct rb_host_transport {
+  void *user;
+  int nranks, rank;
+  /* recv[r * bytes .. (r + 1) * bytes) = rank r's `bytes` bytes at send */
+  int (*all_gather)(void *user, const void *send, void *recv, uint64_t bytes);
+  /* element-wise sum of n u64 over the ranks, in place */
+  int (*all_reduce_sum_u64)(void *user, uint64_t *values, uint32_t n);
+  int (*send)(void *user, const void *buf, uint64_t bytes, int peer);
+  int (*recv)(void *user, void *buf, uint64_t bytes, int peer);
+} rb_host_transport;
+/* A communicator over a host transport.  ctx may be NULL: then only the byte-level entry points below
+ * (rbgpu_shard_summarize_serialized, rbgpu_shard_gather_host, rbgpu_comm_naive_and_order,
+ * rbgpu_comm_allreduce_sum) apply; with a ctx every sharded entry point works, over host memory. */
+int rbgpu_comm_init_host(rbgpu_ctx *ctx, const rb_host_transport *t, rbgpu_comm **out);
+
 /* The whole result of a key-range-sharded aggregation, as every rank sees it after the exchange. */
 typedef struct rb_shard_summary {
   uint64_t cardinality;       /* RoaringBitmap.getCardinality of the whole result */
@@ -398,6 +418,19 @@ int rbgpu_bsi_compare_sharded(rbgpu_comm *comm, const rbgpu_set *bsi, int op, ui
  * concatenated payloads.  Collective. */
 int rbgpu_shard_gather_serialized(rbgpu_comm *comm, const rbgpu_set *local, const rb_shard_summary *summary,
                                   int root, uint8_t *d_dst, uint64_t cap);
+/* rbgpu_shard_summarize for a shard given as its standalone serialized bytes (host memory).  Collective. */
+int rbgpu_shard_summarize_serialized(rbgpu_comm *comm, const uint8_t *shard, uint64_t len, rb_shard_summary *out);
+/* rbgpu_shard_gather_serialized for a shard given as host bytes (len == summary->local_serialized);
+ * the root receives the whole result's bytes in host memory dst.  Collective. */
+int rbgpu_shard_gather_host(rbgpu_comm *comm, const uint8_t *shard, uint64_t len, const rb_shard_summary *summary,
+                            int root, uint8_t *dst, uint64_t cap);
+/* naive_and's fold order over a key-range partition (FastAggregation.java:328-346): the members'
+ * per-rank container counts (rbgpu_set_range_counts) are summed over the ranks; order[0] = the member
+ * with the fewest containers (first on ties), then the others in order, that member's other occurrences
+ * skipped by identity (*n_order <= n; RB_NAIVE_AND_ITER folds it).
+ * local_failed != 0: this rank could not count; every rank then fails together.  Collective. */
+int rbgpu_comm_naive_and_order(rbgpu_comm *comm, const uint32_t *members, const uint64_t *local_counts, uint32_t n,
+                               int local_failed, uint32_t *order, uint32_t *n_order);
 /* Sum of `n` u64 values over the ranks, in place (the pairwise batch's cardinality exchange:
  * each rank runs its own pairs, the sum of the results' cardinalities is a global fact).  Collective. */
 int rbgpu_comm_allreduce_sum(rbgpu_comm *comm, uint64_t *values, uint32_t n);

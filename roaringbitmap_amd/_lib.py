@@ -74,6 +74,17 @@ class RbShardSummary(C.Structure):
 
 COMM_ID_BYTES = 128
 
+# rb_host_transport (rbgpu.h): a caller's host channel for the multi-GPU exchange
+HT_ALL_GATHER = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64)
+HT_ALL_REDUCE = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_uint64), C.c_uint32)
+HT_SEND = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_uint64, C.c_int)
+HT_RECV = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_uint64, C.c_int)
+
+
+class RbHostTransport(C.Structure):
+    _fields_ = [("user", C.c_void_p), ("nranks", C.c_int), ("rank", C.c_int), ("all_gather", HT_ALL_GATHER),
+                ("all_reduce_sum_u64", HT_ALL_REDUCE), ("send", HT_SEND), ("recv", HT_RECV)]
+
 # every symbol include/rbgpu.h declares, with its ctypes signature
 _P = C.c_void_p
 _U32P = C.POINTER(C.c_uint32)
@@ -134,6 +145,11 @@ SIGNATURES = {
     "rbgpu_comm_destroy": (None, [_P]),
     "rbgpu_comm_allreduce_sum": (C.c_int, [_P, _U64P, C.c_uint32]),
     "rbgpu_shard_summarize": (C.c_int, [_P, _P, C.POINTER(RbShardSummary)]),
+    "rbgpu_comm_init_host": (C.c_int, [_P, C.POINTER(RbHostTransport), C.POINTER(_P)]),
+    "rbgpu_shard_summarize_serialized": (C.c_int, [_P, C.c_char_p, C.c_uint64, C.POINTER(RbShardSummary)]),
+    "rbgpu_shard_gather_host": (C.c_int, [_P, C.c_char_p, C.c_uint64, C.POINTER(RbShardSummary), C.c_int,
+                                          C.c_void_p, C.c_uint64]),
+    "rbgpu_comm_naive_and_order": (C.c_int, [_P, _U32P, _U64P, C.c_uint32, C.c_int, _U32P, _U32P]),
     "rbgpu_wide_sharded": (C.c_int, [_P, C.c_int, _P, _U32P, C.c_uint32, C.c_uint32, C.c_uint32, C.POINTER(_P),
                                      C.POINTER(RbShardSummary)]),
     "rbgpu_bsi_compare_sharded": (C.c_int, [_P, _P, C.c_int, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64, _P,

@@ -15,6 +15,7 @@
 // RCCL is opened with dlopen at rbgpu_comm_init, so librbgpu has no link-time dependency on it.
 #include <dlfcn.h>
 
+#include <algorithm>
 #include <cstring>
 #include <vector>
 
@@ -234,18 +235,382 @@ int plan_parts(std::vector<Part> &parts, Global &g) {
   return RB_OK;
 }
 
+// ---------------------------------------------------------------- transports
+// The exchange logic below (summaries, failure agreement, the naive_and order, the shard gather and
+// the header assembly) runs over a transport: RCCL on device buffers, or a caller's host transport
+// (rb_host_transport: the JVM's own channel; the CPU tests' gloo group).  Every collective is entered
+// by every rank whatever its own step did: a local failure travels as a flag inside the exchange.
+struct Xport {
+  int nranks = 1, rank = 0;
+  virtual ~Xport() {}
+  virtual bool on_device() const = 0; // exchange buffers (gather staging) live in device memory
+  // all-gather of k u64 per rank -> out[nranks * k] (host values in, host values out)
+  virtual int gather_u64(const uint64_t *mine, uint32_t k, std::vector<uint64_t> &out) = 0;
+  // element-wise sum over the ranks, in place (host values)
+  virtual int reduce_u64(uint64_t *v, uint32_t n) = 0;
+  // shards to the root: rank r's lens[r] bytes land at recv + base[r] on the root (transport memory)
+  virtual int gather_bytes(int root, const uint8_t *mine, const std::vector<uint64_t> &lens,
+                           const std::vector<uint64_t> &base, uint8_t *recv) = 0;
+};
+
+constexpr uint32_t kXbufWords = 1u << 16; // RCCL exchange buffer: every u64 exchange goes through it in chunks
+
+struct RcclXport final : Xport {
+  rbgpu_ctx *ctx = nullptr;
+  const Rccl *r = nullptr;
+  ncclComm_t nc = nullptr;
+  uint64_t *d_buf = nullptr; // kXbufWords * (nranks + 1) u64, allocated once: no allocation inside a collective
+  bool on_device() const override { return true; }
+  int gather_u64(const uint64_t *mine, uint32_t k, std::vector<uint64_t> &out) override {
+    if (k > kXbufWords) return fail(RB_EINVAL, "exchange of %u words", k);
+    hipStream_t st = ctx->stream;
+    uint64_t *send = d_buf, *recv = d_buf + kXbufWords;
+    int rc = hipSetDevice(ctx->device) || hipMemcpyAsync(send, mine, 8ull * k, hipMemcpyHostToDevice, st)
+                 ? fail(RB_EDEVICE, "exchange upload")
+                 : RB_OK;
+    // the collective is entered even when the upload failed: the other ranks are already in it
+    const ncclResult_t e = r->all_gather(send, recv, (size_t)k, ncclUint64, nc, st);
+    if (!rc && e != ncclSuccess) rc = fail(RB_EDEVICE, "ncclAllGather: %s", r->error_string(e));
+    out.assign((size_t)nranks * k, 0);
+    if (!rc && (hipMemcpyAsync(out.data(), recv, 8ull * k * nranks, hipMemcpyDeviceToHost, st) ||
+                hipStreamSynchronize(st)))
+      rc = fail(RB_EDEVICE, "exchange read-back");
+    return rc;
+  }
+  int reduce_u64(uint64_t *v, uint32_t n) override {
+    hipStream_t st = ctx->stream;
+    int rc = hipSetDevice(ctx->device) ? fail(RB_EDEVICE, "hipSetDevice") : RB_OK;
+    for (uint32_t o = 0; o < n; o += kXbufWords) { // fixed chunks: the same count of collectives on every rank
+      const uint32_t m = std::min(kXbufWords, n - o);
+      if (!rc && hipMemcpyAsync(d_buf, v + o, 8ull * m, hipMemcpyHostToDevice, st)) rc = fail(RB_EDEVICE, "reduce upload");
+      const ncclResult_t e = r->all_reduce(d_buf, d_buf, m, ncclUint64, ncclSum, nc, st);
+      if (!rc && e != ncclSuccess) rc = fail(RB_EDEVICE, "ncclAllReduce: %s", r->error_string(e));
+      if (!rc && (hipMemcpyAsync(v + o, d_buf, 8ull * m, hipMemcpyDeviceToHost, st) || hipStreamSynchronize(st)))
+        rc = fail(RB_EDEVICE, "reduce read-back");
+    }
+    return rc;
+  }
+  int gather_bytes(int root, const uint8_t *mine, const std::vector<uint64_t> &lens, const std::vector<uint64_t> &base,
+                   uint8_t *recv) override {
+    hipStream_t st = ctx->stream;
+    ncclResult_t e = r->group_start(); // one grouped send / recv
+    if (e == ncclSuccess) {
+      if (rank == root) {
+        for (int q = 0; q < nranks && e == ncclSuccess; ++q)
+          if (q != root && lens[q]) e = r->recv(recv + base[q], lens[q], ncclUint8, q, nc, st);
+      } else if (lens[rank]) {
+        e = r->send(mine, lens[rank], ncclUint8, root, nc, st);
+      }
+      const ncclResult_t e2 = r->group_end();
+      if (e == ncclSuccess) e = e2;
+    }
+    if (e != ncclSuccess) return fail(RB_EDEVICE, "shard gather: %s", r->error_string(e));
+    return RB_OK;
+  }
+  ~RcclXport() override {
+    if (nc) (void)r->destroy(nc);
+    if (d_buf) (void)hipFree(d_buf);
+  }
+};
+
+struct HostXport final : Xport {
+  rb_host_transport t{};
+  bool on_device() const override { return false; }
+  int gather_u64(const uint64_t *mine, uint32_t k, std::vector<uint64_t> &out) override {
+    out.assign((size_t)nranks * k, 0);
+    if (t.all_gather(t.user, mine, out.data(), 8ull * k)) return fail(RB_EDEVICE, "host transport all_gather failed");
+    return RB_OK;
+  }
+  int reduce_u64(uint64_t *v, uint32_t n) override {
+    if (n && t.all_reduce_sum_u64(t.user, v, n)) return fail(RB_EDEVICE, "host transport all_reduce failed");
+    return RB_OK;
+  }
+  int gather_bytes(int root, const uint8_t *mine, const std::vector<uint64_t> &lens, const std::vector<uint64_t> &base,
+                   uint8_t *recv) override {
+    int rc = RB_OK;
+    if (rank == root) {
+      for (int q = 0; q < nranks; ++q)
+        if (q != root && lens[q] && t.recv(t.user, recv + base[q], lens[q], q) && !rc)
+          rc = fail(RB_EDEVICE, "host transport recv from rank %d failed", q);
+    } else if (lens[rank] && t.send(t.user, mine, lens[rank], root)) {
+      rc = fail(RB_EDEVICE, "host transport send failed");
+    }
+    return rc;
+  }
+};
+
+// ---------------------------------------------------------------- a local shard as the exchange sees it
+// A one-bitmap device set (the product path) or the standalone serialized bytes of one (host memory).
+struct ShardSrc {
+  const rbgpu_set *set = nullptr;
+  const uint8_t *bytes = nullptr;
+  uint64_t len = 0;
+  // (cardinality, containers, Run containers, payload bytes, serialized bytes)
+  int summary(uint64_t (&v)[5]) const {
+    if (set) {
+      rb_bitmap_summary s{};
+      int rc = rbgpu_set_summaries(set, 0, 1, &s);
+      uint64_t ser = 0;
+      if (!rc) rc = rbgpu_set_serialized_sizes(set, &ser);
+      if (rc) return rc;
+      v[0] = s.cardinality, v[1] = s.n_containers, v[2] = s.n_run_containers, v[3] = s.payload_bytes, v[4] = ser;
+      return RB_OK;
+    }
+    Part p{};
+    if (!parse_part(bytes, len, p)) return fail(RB_EFORMAT, "the shard is not a serialized bitmap");
+    uint64_t card = 0, runs = 0;
+    for (uint64_t j = 0; j < p.n; ++j) {
+      const bool run = part_is_run(p, j);
+      runs += run;
+      if (!run) {
+        // card-1 from the header; an empty container (horizontal_xor keeps one, FastAggregation.java:278)
+        // writes 0xFFFF there, so with offsets an Array's card is its payload length / 2
+        uint64_t cj = rd16(p.bytes + p.pre + 4 * j + 2) + 1ull;
+        if (p.has_off) {
+          const uint64_t b0 = part_payload_pos(p, j), b1 = j + 1 < p.n ? part_payload_pos(p, j + 1) : p.body;
+          if (b1 - b0 != 8192) cj = (b1 - b0) / 2;
+        }
+        card += cj;
+      } else { // a Run's cardinality is its run lengths (an empty Run's header says 65536)
+        const uint64_t at = p.lh + part_payload_pos(p, j);
+        if (at + 2 > len) return fail(RB_EFORMAT, "truncated Run container");
+        const uint32_t nr = rd16(bytes + at);
+        if (at + 2 + 4ull * nr > len) return fail(RB_EFORMAT, "truncated Run container");
+        for (uint32_t q = 0; q < nr; ++q) card += rd16(bytes + at + 4 + 4 * q) + 1ull;
+      }
+    }
+    v[0] = card, v[1] = p.n, v[2] = runs, v[3] = p.body, v[4] = len;
+    return RB_OK;
+  }
+  // the standalone serialized bytes into `dst` (device memory when on_device, else host)
+  int serialize(uint8_t *dst, uint64_t cap, bool on_device, hipStream_t st) const {
+    if (set) {
+      uint64_t offs[2] = {0, 0};
+      return on_device ? rbgpu_set_serialize_device(set, 0, 1, dst, cap, offs) : rbgpu_set_serialize(set, 0, 1, dst, cap, offs);
+    }
+    if (cap < len) return fail(RB_EINVAL, "shard staging holds %llu bytes", (unsigned long long)cap);
+    if (!on_device) {
+      if (len) std::memcpy(dst, bytes, len);
+      return RB_OK;
+    }
+    if (len && (hipMemcpyAsync(dst, bytes, len, hipMemcpyHostToDevice, st) || hipStreamSynchronize(st)))
+      return fail(RB_EDEVICE, "shard upload");
+    return RB_OK;
+  }
+};
+
+int agree(int local_rc, uint64_t failed_others) {
+  if (local_rc) return local_rc;
+  if (failed_others) return fail(RB_EDEVICE, "%llu other rank(s) failed this collective call", (unsigned long long)failed_others);
+  return RB_OK;
+}
+
 } // namespace
 } // namespace rbg
 
 using namespace rbg;
 
 struct rbgpu_comm {
-  rbgpu_ctx *ctx = nullptr;
-  ncclComm_t nc = nullptr;
-  const Rccl *r = nullptr;
+  rbgpu_ctx *ctx = nullptr; // null for a host-transport communicator without a device
+  Xport *x = nullptr;
   int nranks = 1, rank = 0;
-  uint64_t *d_buf = nullptr; // small exchange buffer (64 u64 per rank)
 };
+
+namespace {
+
+// summary exchange; local_rc != 0: this rank's shard could not be built (src may be null), it
+// still takes part in the all-gather and every rank fails together
+int summarize(rbgpu_comm *c, const ShardSrc *src, int local_rc, rb_shard_summary *out) {
+  uint64_t v[5] = {0, 0, 0, 0, 0};
+  if (!local_rc) local_rc = src->summary(v);
+  const uint64_t mine[6] = {v[0], v[1], v[2], v[3], v[4], local_rc ? 1ull : 0ull};
+  std::vector<uint64_t> g;
+  int rc = c->x->gather_u64(mine, 6, g);
+  if (rc) return local_rc ? local_rc : rc;
+  uint64_t failed = 0;
+  for (int r = 0; r < c->nranks; ++r) failed += g[6 * r + 5];
+  rc = agree(local_rc, failed - (local_rc ? 1 : 0));
+  if (rc) return rc;
+  rb_shard_summary o{};
+  uint64_t before_payload = 0, before_cont = 0;
+  for (int r = 0; r < c->nranks; ++r) {
+    o.cardinality += g[6 * r];
+    o.n_containers += g[6 * r + 1];
+    o.n_run_containers += g[6 * r + 2];
+    o.payload_bytes += g[6 * r + 3];
+    if (r < c->rank) {
+      before_cont += g[6 * r + 1];
+      before_payload += g[6 * r + 3];
+    }
+  }
+  if (o.n_run_containers && o.n_containers > 65536) return fail(RB_EINVAL, "more than 65536 containers");
+  const uint64_t h = header_bytes(o.n_containers, o.n_run_containers > 0);
+  o.serialized_size = h + o.payload_bytes;
+  o.payload_offset = h + before_payload;
+  o.container_offset = before_cont;
+  o.local_serialized = v[4];
+  *out = o;
+  return RB_OK;
+}
+
+// all-reduce of n member counts plus a failure flag: every rank takes part whatever its own step did;
+// then naive_and's order: the globally smallest member (first on ties) first, the rest in order
+// (FastAggregation.java:328-346)
+int naive_and_order(rbgpu_comm *c, const uint32_t *mem, const uint64_t *counts, uint32_t n, int local_rc,
+                    std::vector<uint32_t> &ord) {
+  std::vector<uint64_t> cnt(n + 1, 0);
+  if (!local_rc && n) std::copy(counts, counts + n, cnt.begin());
+  cnt[n] = local_rc ? 1 : 0;
+  int rc = c->x->reduce_u64(cnt.data(), n + 1);
+  if (rc) return local_rc ? local_rc : rc;
+  rc = agree(local_rc, cnt[n] - (local_rc ? 1 : 0));
+  if (rc) return rc;
+  ord.clear();
+  if (n) {
+    uint32_t sm = 0;
+    for (uint32_t i = 1; i < n; ++i)
+      if (cnt[i] < cnt[sm]) sm = i;
+    ord.push_back(mem[sm]);
+    for (uint32_t i = 0; i < n; ++i)
+      if (mem[i] != mem[sm]) ord.push_back(mem[i]);
+  }
+  return RB_OK;
+}
+
+// The whole result's bytes on the root: shard lengths exchanged (with failure flags), every rank
+// serializes its shard into transport memory, the shards travel to the root, the root assembles the
+// global header around the concatenated payloads (a kernel on a device transport, the same code on the
+// host otherwise) into dst (device memory when dst_device).
+int gather(rbgpu_comm *c, const ShardSrc *src, const rb_shard_summary *summary, int root, uint8_t *dst, uint64_t cap,
+           bool dst_device, int local_rc) {
+  Xport &X = *c->x;
+  const bool is_root = c->rank == root, dev = X.on_device();
+  rbgpu_ctx *ctx = c->ctx;
+  hipStream_t st = ctx ? ctx->stream : nullptr;
+  if (!local_rc && is_root && (!dst || cap < summary->serialized_size))
+    local_rc = fail(RB_EINVAL, "destination holds %llu bytes, %llu needed", (unsigned long long)cap,
+                    (unsigned long long)summary->serialized_size);
+  // every rank's shard size (the summary's own field, gathered again: callers may pass a summary from
+  // another exchange of the same shards) and failure flag
+  const uint64_t mine[2] = {local_rc ? 0 : summary->local_serialized, local_rc ? 1ull : 0ull};
+  std::vector<uint64_t> g;
+  int rc = X.gather_u64(mine, 2, g);
+  if (rc) return local_rc ? local_rc : rc;
+  uint64_t failed = 0;
+  std::vector<uint64_t> lens(c->nranks), base(c->nranks + 1, 0);
+  for (int r = 0; r < c->nranks; ++r) {
+    lens[r] = g[2 * r];
+    failed += g[2 * r + 1];
+    base[r + 1] = base[r] + lens[r];
+  }
+  rc = agree(local_rc, failed - (local_rc ? 1 : 0));
+  if (rc) return rc;
+  // this rank's shard, serialized into transport memory (the root stages every shard)
+  const uint64_t stage = is_root ? base[c->nranks] : lens[c->rank];
+  uint8_t *d_stage = nullptr;
+  std::vector<uint8_t> h_stage;
+  Part *d_parts = nullptr;
+  uint8_t *d_out = nullptr; // device assembly into a host dst
+  if (dev) {
+    if (ctx->pool.alloc((void **)&d_stage, std::max<uint64_t>(stage, 16))) {
+      d_stage = nullptr;
+      local_rc = fail(RB_ENOMEM, "gather staging");
+    }
+  } else {
+    h_stage.assign(std::max<uint64_t>(stage, 16), 0);
+  }
+  uint8_t *stage_p = dev ? d_stage : h_stage.data();
+  auto done = [&](int code) { // every pooled buffer goes back on every path
+    if (st) (void)hipStreamSynchronize(st);
+    for (void *p : {(void *)d_stage, (void *)d_parts, (void *)d_out})
+      if (p) ctx->pool.release(p);
+    return code;
+  };
+  uint8_t *mine_at = stage_p ? stage_p + (is_root ? base[c->rank] : 0) : nullptr;
+  if (!local_rc) local_rc = src->serialize(mine_at, lens[c->rank], dev, st);
+  // agree once more before the point-to-point phase
+  const uint64_t flag = local_rc ? 1 : 0;
+  rc = X.gather_u64(&flag, 1, g);
+  if (rc) return done(local_rc ? local_rc : rc);
+  failed = 0;
+  for (int r = 0; r < c->nranks; ++r) failed += g[r];
+  rc = agree(local_rc, failed - flag);
+  if (rc) return done(rc);
+  rc = X.gather_bytes(root, mine_at, lens, base, stage_p);
+  if (rc || !is_root) return done(rc);
+  // the root reads the shard headers (small) to plan the global header
+  std::vector<Part> parts(c->nranks);
+  std::vector<uint8_t> hdr;
+  for (int r = 0; r < c->nranks; ++r) {
+    const uint8_t *hp = stage_p + base[r];
+    if (dev) { // at most 4 + 8192 + 8 * 65536 header bytes per shard
+      const uint64_t take = std::min<uint64_t>(lens[r], 8 + 8192 + 8ull * 65536);
+      hdr.resize(std::max<uint64_t>(take, 1));
+      if (take && (hipMemcpyAsync(hdr.data(), d_stage + base[r], take, hipMemcpyDeviceToHost, st) ||
+                   hipStreamSynchronize(st)))
+        return done(fail(RB_EDEVICE, "shard header read-back"));
+      hp = hdr.data();
+    }
+    Part p{};
+    if (!parse_part(hp, lens[r], p)) return done(fail(RB_EFORMAT, "shard %d is not a serialized bitmap", r));
+    p.bytes = stage_p + base[r]; // the assembly reads the staged copy
+    parts[r] = p;
+  }
+  Global gl;
+  rc = plan_parts(parts, gl);
+  if (rc) return done(rc);
+  uint64_t total = gl.h;
+  for (const Part &p : parts) total += p.body;
+  if (cap < total)
+    return done(fail(RB_EINVAL, "destination holds %llu bytes, %llu needed", (unsigned long long)cap,
+                     (unsigned long long)total));
+  if (dev) {
+    uint8_t *out = dst;
+    if (!dst_device) {
+      if (ctx->pool.alloc((void **)&d_out, std::max<uint64_t>(total, 16))) {
+        d_out = nullptr;
+        return done(fail(RB_ENOMEM, "assembly buffer"));
+      }
+      out = d_out;
+    }
+    if (ctx->pool.alloc((void **)&d_parts, sizeof(Part) * parts.size())) {
+      d_parts = nullptr;
+      return done(fail(RB_ENOMEM, "gather plan"));
+    }
+    if (hipMemcpyAsync(d_parts, parts.data(), sizeof(Part) * parts.size(), hipMemcpyHostToDevice, st))
+      return done(fail(RB_EDEVICE, "gather plan upload"));
+    const uint64_t items = assemble_items(gl);
+    k_shard_header<<<(unsigned)((items + 255) / 256), 256, 0, st>>>(d_parts, (uint32_t)parts.size(), gl, out);
+    for (const Part &p : parts)
+      if (p.body && hipMemcpyAsync(out + gl.h + p.bbase, p.bytes + p.lh, p.body, hipMemcpyDeviceToDevice, st))
+        return done(fail(RB_EDEVICE, "shard body copy"));
+    if (!dst_device && hipMemcpyAsync(dst, out, total, hipMemcpyDeviceToHost, st))
+      return done(fail(RB_EDEVICE, "assembly read-back"));
+    if (hipStreamSynchronize(st)) return done(fail(RB_EDEVICE, "shard gather"));
+    const hipError_t le = hipGetLastError();
+    if (le != hipSuccess) return done(fail(RB_EDEVICE, "kernel launch failed: %s", hipGetErrorString(le)));
+    return done(RB_OK);
+  }
+  std::vector<uint8_t> h_out;
+  uint8_t *out = dst;
+  if (dst_device) {
+    h_out.resize(std::max<uint64_t>(total, 1));
+    out = h_out.data();
+  }
+  for (uint64_t t = 0; t < assemble_items(gl); ++t) assemble_item(parts.data(), (uint32_t)parts.size(), gl, t, out);
+  for (const Part &p : parts)
+    if (p.body) std::memcpy(out + gl.h + p.bbase, p.bytes + p.lh, p.body);
+  if (dst_device && total &&
+      (hipMemcpyAsync(dst, out, total, hipMemcpyHostToDevice, st) || hipStreamSynchronize(st)))
+    return done(fail(RB_EDEVICE, "assembly upload"));
+  return done(RB_OK);
+}
+
+int need_device(const rbgpu_comm *c) {
+  return c->ctx ? RB_OK : fail(RB_EINVAL, "this communicator has no device context");
+}
+
+} // namespace
 
 extern "C" {
 
@@ -271,141 +636,103 @@ int rbgpu_comm_init(rbgpu_ctx *ctx, const uint8_t id[RB_COMM_ID_BYTES], int nran
   HIPCHK(hipSetDevice(ctx->device));
   ncclUniqueId u;
   std::memcpy(&u, id, RB_COMM_ID_BYTES);
-  rbgpu_comm *c = new rbgpu_comm;
-  c->ctx = ctx;
-  c->r = r;
-  c->nranks = nranks;
-  c->rank = rank;
-  ncclResult_t e = r->init_rank(&c->nc, nranks, u, rank);
+  RcclXport *x = new RcclXport;
+  x->ctx = ctx;
+  x->r = r;
+  x->nranks = nranks;
+  x->rank = rank;
+  const ncclResult_t e = r->init_rank(&x->nc, nranks, u, rank);
   if (e != ncclSuccess) {
-    delete c;
+    x->nc = nullptr;
+    delete x;
     return fail(RB_EDEVICE, "ncclCommInitRank: %s", r->error_string(e));
   }
-  if (hipMalloc((void **)&c->d_buf, 64 * 8 * (size_t)(nranks + 1)) != hipSuccess) {
-    (void)r->destroy(c->nc);
-    delete c;
+  if (hipMalloc((void **)&x->d_buf, 8ull * kXbufWords * (size_t)(nranks + 1)) != hipSuccess) {
+    x->d_buf = nullptr;
+    delete x;
     return fail(RB_ENOMEM, "exchange buffer");
   }
+  rbgpu_comm *c = new rbgpu_comm;
+  c->ctx = ctx;
+  c->x = x;
+  c->nranks = nranks;
+  c->rank = rank;
   ctx->refs++;
+  *out = c;
+  return RB_OK;
+}
+
+int rbgpu_comm_init_host(rbgpu_ctx *ctx, const rb_host_transport *t, rbgpu_comm **out) {
+  if (!t || !out) return fail(RB_EINVAL, "null argument");
+  *out = nullptr;
+  if (!t->all_gather || !t->all_reduce_sum_u64 || !t->send || !t->recv) return fail(RB_EINVAL, "incomplete transport");
+  if (t->nranks < 1 || t->rank < 0 || t->rank >= t->nranks) return fail(RB_EINVAL, "bad rank %d of %d", t->rank, t->nranks);
+  if (ctx) HIPCHK(hipSetDevice(ctx->device));
+  HostXport *x = new HostXport;
+  x->t = *t;
+  x->nranks = t->nranks;
+  x->rank = t->rank;
+  rbgpu_comm *c = new rbgpu_comm;
+  c->ctx = ctx;
+  c->x = x;
+  c->nranks = t->nranks;
+  c->rank = t->rank;
+  if (ctx) ctx->refs++;
   *out = c;
   return RB_OK;
 }
 
 void rbgpu_comm_destroy(rbgpu_comm *c) {
   if (!c) return;
-  (void)hipSetDevice(c->ctx->device);
-  (void)hipStreamSynchronize(c->ctx->stream);
-  if (c->nc) (void)c->r->destroy(c->nc);
-  if (c->d_buf) (void)hipFree(c->d_buf);
+  if (c->ctx) {
+    (void)hipSetDevice(c->ctx->device);
+    (void)hipStreamSynchronize(c->ctx->stream);
+  }
+  delete c->x;
   rbgpu_ctx *ctx = c->ctx;
   delete c;
-  ctx_unref(ctx);
+  if (ctx) ctx_unref(ctx);
 }
 
 int rbgpu_comm_allreduce_sum(rbgpu_comm *c, uint64_t *values, uint32_t n) {
   if (!c || (n && !values)) return fail(RB_EINVAL, "null argument");
-  if (n > 64 * (uint32_t)(c->nranks + 1)) return fail(RB_EINVAL, "at most %d values", 64 * (c->nranks + 1));
   if (!n) return RB_OK;
-  hipStream_t st = c->ctx->stream;
-  HIPCHK(hipSetDevice(c->ctx->device));
-  HIPCHK(hipMemcpyAsync(c->d_buf, values, 8ull * n, hipMemcpyHostToDevice, st));
-  NCCLCHK(c->r, c->r->all_reduce(c->d_buf, c->d_buf, n, ncclUint64, ncclSum, c->nc, st));
-  HIPCHK(hipMemcpyAsync(values, c->d_buf, 8ull * n, hipMemcpyDeviceToHost, st));
-  HIPCHK(hipStreamSynchronize(st));
-  return RB_OK;
-}
-
-// all_gather of k u64 per rank -> out[nranks * k] (host)
-static int gather_u64(rbgpu_comm *c, const uint64_t *mine, int k, std::vector<uint64_t> &out) {
-  hipStream_t st = c->ctx->stream;
-  HIPCHK(hipSetDevice(c->ctx->device));
-  uint64_t *send = c->d_buf, *recv = c->d_buf + 64;
-  HIPCHK(hipMemcpyAsync(send, mine, 8ull * k, hipMemcpyHostToDevice, st));
-  NCCLCHK(c->r, c->r->all_gather(send, recv, (size_t)k, ncclUint64, c->nc, st));
-  out.assign((size_t)c->nranks * k, 0);
-  HIPCHK(hipMemcpyAsync(out.data(), recv, 8ull * k * c->nranks, hipMemcpyDeviceToHost, st));
-  HIPCHK(hipStreamSynchronize(st));
-  return RB_OK;
-}
-
-// Every rank takes part in each collective even when its own step failed (a rank that returned
-// early would leave the others waiting in the collective): a failure travels as a flag inside the
-// exchange, and every rank then fails together.  Returns the local code, or RB_EDEVICE naming the
-// failure on another rank.
-static int agree(int local_rc, uint64_t failed_ranks) {
-  if (local_rc) return local_rc;
-  if (failed_ranks) return fail(RB_EDEVICE, "%llu other rank(s) failed this collective call", (unsigned long long)failed_ranks);
-  return RB_OK;
-}
-
-// summary exchange; local_rc != 0: this rank's shard could not be built (local may be null), it
-// still takes part in the all-gather and every rank fails together
-static int summarize(rbgpu_comm *c, const rbgpu_set *local, int local_rc, rb_shard_summary *out) {
-  rb_bitmap_summary s{};
-  uint64_t ser = 0;
-  if (!local_rc) local_rc = rbgpu_set_summaries(local, 0, 1, &s);
-  if (!local_rc) local_rc = rbgpu_set_serialized_sizes(local, &ser);
-  const uint64_t mine[6] = {s.cardinality, s.n_containers, s.n_run_containers, s.payload_bytes, ser,
-                            local_rc ? 1ull : 0ull};
-  std::vector<uint64_t> g;
-  int rc = gather_u64(c, mine, 6, g);
-  if (rc) return rc;
-  uint64_t failed = 0;
-  for (int r = 0; r < c->nranks; ++r) failed += g[6 * r + 5];
-  rc = agree(local_rc, failed);
-  if (rc) return rc;
-  rb_shard_summary o{};
-  uint64_t before_payload = 0, before_cont = 0;
-  for (int r = 0; r < c->nranks; ++r) {
-    o.cardinality += g[6 * r];
-    o.n_containers += g[6 * r + 1];
-    o.n_run_containers += g[6 * r + 2];
-    o.payload_bytes += g[6 * r + 3];
-    if (r < c->rank) {
-      before_cont += g[6 * r + 1];
-      before_payload += g[6 * r + 3];
-    }
-  }
-  const uint64_t h = header_bytes(o.n_containers, o.n_run_containers > 0);
-  o.serialized_size = h + o.payload_bytes;
-  o.payload_offset = h + before_payload;
-  o.container_offset = before_cont;
-  o.local_serialized = ser;
-  *out = o;
-  return RB_OK;
+  return c->x->reduce_u64(values, n);
 }
 
 int rbgpu_shard_summarize(rbgpu_comm *c, const rbgpu_set *local, rb_shard_summary *out) {
   if (!c || !out) return fail(RB_EINVAL, "null argument");
-  int local_rc = RB_OK;
-  if (!local) local_rc = fail(RB_EINVAL, "null argument");
-  else if (local->nb != 1) local_rc = fail(RB_EINVAL, "a shard is a one-bitmap set");
-  else if (local->ctx != c->ctx) local_rc = fail(RB_EINVAL, "the shard belongs to another context");
-  return summarize(c, local, local_rc, out);
+  int local_rc = need_device(c);
+  if (!local_rc && !local) local_rc = fail(RB_EINVAL, "null argument");
+  else if (!local_rc && local->nb != 1) local_rc = fail(RB_EINVAL, "a shard is a one-bitmap set");
+  else if (!local_rc && local->ctx != c->ctx) local_rc = fail(RB_EINVAL, "the shard belongs to another context");
+  ShardSrc src;
+  src.set = local;
+  return summarize(c, &src, local_rc, out);
 }
 
-// all-reduce of n member counts plus a failure flag: every rank takes part whatever its own step did
-static int reduce_counts(rbgpu_comm *c, std::vector<uint64_t> &cnt, int local_rc) {
-  const uint32_t n = (uint32_t)cnt.size();
-  cnt.push_back(local_rc ? 1 : 0);
-  uint64_t *d = nullptr;
-  rbgpu_ctx *ctx = c->ctx;
-  if (ctx->pool.alloc((void **)&d, 8ull * (n + 1))) return fail(RB_ENOMEM, "member counts");
-  hipStream_t st = ctx->stream;
-  int rc = RB_OK;
-  ncclResult_t e = ncclSuccess;
-  if (hipSetDevice(ctx->device) || hipMemcpyAsync(d, cnt.data(), 8ull * (n + 1), hipMemcpyHostToDevice, st))
-    rc = fail(RB_EDEVICE, "member counts upload");
-  if (!rc && (e = c->r->all_reduce(d, d, n + 1, ncclUint64, ncclSum, c->nc, st)) != ncclSuccess)
-    rc = fail(RB_EDEVICE, "member counts all-reduce: %s", c->r->error_string(e));
-  if (!rc && (hipMemcpyAsync(cnt.data(), d, 8ull * (n + 1), hipMemcpyDeviceToHost, st) || hipStreamSynchronize(st)))
-    rc = fail(RB_EDEVICE, "member counts read-back");
-  (void)hipStreamSynchronize(st);
-  ctx->pool.release(d);
-  if (rc) return rc;
-  const uint64_t failed = cnt[n] - (local_rc ? 1 : 0);
-  cnt.pop_back();
-  return agree(local_rc, failed);
+int rbgpu_shard_summarize_serialized(rbgpu_comm *c, const uint8_t *shard, uint64_t len, rb_shard_summary *out) {
+  if (!c || !out) return fail(RB_EINVAL, "null argument");
+  ShardSrc src;
+  src.bytes = shard;
+  src.len = len;
+  const int local_rc = shard ? RB_OK : fail(RB_EINVAL, "null shard");
+  return summarize(c, &src, local_rc, out);
+}
+
+int rbgpu_comm_naive_and_order(rbgpu_comm *c, const uint32_t *members, const uint64_t *local_counts, uint32_t n,
+                               int local_failed, uint32_t *order, uint32_t *n_order) {
+  if (!c) return fail(RB_EINVAL, "null argument");
+  int local_rc = local_failed ? fail(RB_EINVAL, "this rank's member counts failed") : RB_OK;
+  if (!local_rc && (!n_order || (n && (!local_counts || !order)))) local_rc = fail(RB_EINVAL, "null argument");
+  std::vector<uint32_t> mem(n), ord;
+  for (uint32_t i = 0; i < n; ++i) mem[i] = members ? members[i] : i;
+  const int rc = naive_and_order(c, mem.data(), local_counts, n, local_rc, ord);
+  if (!rc) {
+    std::copy(ord.begin(), ord.end(), order);
+    *n_order = (uint32_t)ord.size();
+  }
+  return rc;
 }
 
 int rbgpu_wide_sharded(rbgpu_comm *c, int sem, const rbgpu_set *in, const uint32_t *members, uint32_t n,
@@ -417,33 +744,26 @@ int rbgpu_wide_sharded(rbgpu_comm *c, int sem, const rbgpu_set *in, const uint32
   // collective.
   if (c->nranks > 1 && (sem == RB_PQ_OR || sem == RB_PQ_XOR || sem >= RB_BUFFER_PQ_OR))
     return fail(RB_EINVAL, "priorityqueue_or / priorityqueue_xor cannot be key-range sharded");
-  int rc = in ? RB_OK : fail(RB_EINVAL, "null input set");
-  std::vector<uint32_t> ord;
+  int rc = need_device(c);
+  if (!rc && !in) rc = fail(RB_EINVAL, "null input set");
   if (sem == RB_NAIVE_AND || (sem == RB_FAST_AND && n <= 10)) {
     // naive_and(varargs) starts from the bitmap with the fewest containers (first on ties) and skips
     // it by identity (FastAggregation.java:328-346): its container counts are global, so they are the
     // ranks' key-range counts summed; then every shard folds the same order (naive_and(Iterator))
-    std::vector<uint32_t> mem(n);
+    std::vector<uint32_t> mem(n), ord;
     for (uint32_t i = 0; i < n; ++i) mem[i] = members ? members[i] : i;
-    std::vector<uint64_t> cnt(n, 0);
+    std::vector<uint64_t> cnt(std::max<uint32_t>(n, 1), 0);
     if (!rc) rc = rbgpu_set_range_counts(in, mem.data(), n, key_lo, key_hi, cnt.data());
-    if (rc) std::fill(cnt.begin(), cnt.end(), 0ull);
-    rc = reduce_counts(c, cnt, rc);
+    rc = naive_and_order(c, mem.data(), cnt.data(), n, rc, ord);
     if (rc) return rc;
-    if (n) {
-      uint32_t sm = 0;
-      for (uint32_t i = 1; i < n; ++i)
-        if (cnt[i] < cnt[sm]) sm = i;
-      ord.push_back(mem[sm]);
-      for (uint32_t m : mem)
-        if (m != mem[sm]) ord.push_back(m);
-    }
     rc = rbgpu_wide_keys(c->ctx, RB_NAIVE_AND_ITER, in, ord.data(), (uint32_t)ord.size(), key_lo, key_hi, local);
   } else if (!rc) {
     rc = rbgpu_wide_keys(c->ctx, sem, in, members, n, key_lo, key_hi, local);
   }
   if (rc) *local = nullptr;
-  rc = summarize(c, *local, rc, summary);
+  ShardSrc src;
+  src.set = *local;
+  rc = summarize(c, &src, rc, summary);
   if (rc) {
     rbgpu_set_free(*local);
     *local = nullptr;
@@ -456,10 +776,14 @@ int rbgpu_bsi_compare_sharded(rbgpu_comm *c, const rbgpu_set *bsi, int op, uint6
                               uint32_t key_hi, rbgpu_set **local, rb_shard_summary *summary) {
   if (!c || !local || !summary) return fail(RB_EINVAL, "null argument");
   *local = nullptr;
-  int rc = rbgpu_bsi_compare_keys(c->ctx, bsi, op, start_or_value, end, min_value, max_value, found, key_lo, key_hi,
-                                  local);
+  int rc = need_device(c);
+  if (!rc)
+    rc = rbgpu_bsi_compare_keys(c->ctx, bsi, op, start_or_value, end, min_value, max_value, found, key_lo, key_hi,
+                                local);
   if (rc) *local = nullptr;
-  rc = summarize(c, *local, rc, summary); // every rank joins the exchange, failed or not
+  ShardSrc src;
+  src.set = *local;
+  rc = summarize(c, &src, rc, summary); // every rank joins the exchange, failed or not
   if (rc) {
     rbgpu_set_free(*local);
     *local = nullptr;
@@ -471,112 +795,27 @@ int rbgpu_shard_gather_serialized(rbgpu_comm *c, const rbgpu_set *local, const r
                                   uint8_t *d_dst, uint64_t cap) {
   if (!c || !summary) return fail(RB_EINVAL, "null argument");
   if (root < 0 || root >= c->nranks) return fail(RB_EINVAL, "bad root %d", root); // the same on every rank
-  const bool is_root = c->rank == root;
   // a bad argument on one rank is exchanged with the lengths, so every rank fails together instead of
   // the others waiting in the send / recv
-  int local_rc = RB_OK;
-  if (!local) local_rc = fail(RB_EINVAL, "null shard");
-  else if (is_root && (!d_dst || cap < summary->serialized_size))
-    local_rc = fail(RB_EINVAL, "destination holds %llu bytes, %llu needed", (unsigned long long)cap,
-                    (unsigned long long)summary->serialized_size);
-  rbgpu_ctx *ctx = c->ctx;
-  hipStream_t st = ctx->stream;
-  // every rank's shard size (the summary's own field, gathered again: callers may pass a summary
-  // from another exchange of the same shards) and failure flag
-  const uint64_t mine[2] = {summary->local_serialized, local_rc ? 1ull : 0ull};
-  std::vector<uint64_t> g;
-  int rc = gather_u64(c, mine, 2, g);
-  if (rc) return rc;
-  uint64_t failed = 0;
-  std::vector<uint64_t> lens(c->nranks), base(c->nranks + 1, 0);
-  for (int r = 0; r < c->nranks; ++r) {
-    lens[r] = g[2 * r];
-    failed += g[2 * r + 1];
-    base[r + 1] = base[r] + lens[r];
-  }
-  rc = agree(local_rc, failed - (local_rc ? 1 : 0));
-  if (rc) return rc;
-  // this rank's shard, serialized on its GPU
-  uint8_t *d_stage = nullptr;
-  Part *d_parts = nullptr;
-  const uint64_t stage = is_root ? base[c->nranks] : lens[c->rank];
-  if (ctx->pool.alloc((void **)&d_stage, std::max<uint64_t>(stage, 16))) {
-    d_stage = nullptr;
-    local_rc = fail(RB_ENOMEM, "gather staging");
-  }
-  auto done = [&](int code) { // every pooled buffer goes back on every path
-    (void)hipStreamSynchronize(st);
-    if (d_stage) ctx->pool.release(d_stage);
-    if (d_parts) ctx->pool.release(d_parts);
-    return code;
-  };
-  uint8_t *mine_at = d_stage ? d_stage + (is_root ? base[c->rank] : 0) : nullptr;
-  if (!local_rc) {
-    uint64_t offs[2] = {0, 0};
-    local_rc = rbgpu_set_serialize_device(local, 0, 1, mine_at, lens[c->rank], offs);
-  }
-  // agree once more before the point-to-point phase
-  const uint64_t flag = local_rc ? 1 : 0;
-  rc = gather_u64(c, &flag, 1, g);
-  if (rc) return done(rc);
-  failed = 0;
-  for (int r = 0; r < c->nranks; ++r) failed += g[r];
-  rc = agree(local_rc, failed - flag);
-  if (rc) return done(rc);
-  // one grouped send / recv: the shards travel to the root
-  ncclResult_t e = c->r->group_start();
-  if (e == ncclSuccess) {
-    if (is_root) {
-      for (int r = 0; r < c->nranks && e == ncclSuccess; ++r)
-        if (r != root && lens[r]) e = c->r->recv(d_stage + base[r], lens[r], ncclUint8, r, c->nc, st);
-    } else if (lens[c->rank]) {
-      e = c->r->send(mine_at, lens[c->rank], ncclUint8, root, c->nc, st);
-    }
-    const ncclResult_t e2 = c->r->group_end();
-    if (e == ncclSuccess) e = e2;
-  }
-  if (e != ncclSuccess) return done(fail(RB_EDEVICE, "shard gather: %s", c->r->error_string(e)));
-  if (!is_root) return done(RB_OK);
-  // the root reads the shard headers (small) to plan the global header
-  std::vector<Part> parts(c->nranks);
-  std::vector<uint8_t> hdr;
-  for (int r = 0; r < c->nranks; ++r) {
-    // at most 4 + 8192 + 8 * 65536 header bytes per shard
-    const uint64_t take = std::min<uint64_t>(lens[r], 8 + 8192 + 8ull * 65536);
-    hdr.resize(take);
-    if (take) {
-      if (hipMemcpyAsync(hdr.data(), d_stage + base[r], take, hipMemcpyDeviceToHost, st) ||
-          hipStreamSynchronize(st))
-        return done(fail(RB_EDEVICE, "shard header read-back"));
-    }
-    Part p{};
-    if (!parse_part(hdr.data(), lens[r], p)) return done(fail(RB_EFORMAT, "shard %d is not a serialized bitmap", r));
-    p.bytes = d_stage + base[r]; // the kernel reads the device copy
-    parts[r] = p;
-  }
-  Global gl;
-  rc = plan_parts(parts, gl);
-  if (rc) return done(rc);
-  uint64_t total = gl.h;
-  for (const Part &p : parts) total += p.body;
-  if (cap < total)
-    return done(fail(RB_EINVAL, "destination holds %llu bytes, %llu needed", (unsigned long long)cap,
-                     (unsigned long long)total));
-  if (ctx->pool.alloc((void **)&d_parts, sizeof(Part) * parts.size())) {
-    d_parts = nullptr;
-    return done(fail(RB_ENOMEM, "gather plan"));
-  }
-  if (hipMemcpyAsync(d_parts, parts.data(), sizeof(Part) * parts.size(), hipMemcpyHostToDevice, st))
-    return done(fail(RB_EDEVICE, "gather plan upload"));
-  const uint64_t items = assemble_items(gl);
-  k_shard_header<<<(unsigned)((items + 255) / 256), 256, 0, st>>>(d_parts, (uint32_t)parts.size(), gl, d_dst);
-  for (const Part &p : parts)
-    if (p.body && hipMemcpyAsync(d_dst + gl.h + p.bbase, p.bytes + p.lh, p.body, hipMemcpyDeviceToDevice, st))
-      return done(fail(RB_EDEVICE, "shard body copy"));
-  if (hipStreamSynchronize(st)) return done(fail(RB_EDEVICE, "shard gather"));
-  const hipError_t le = hipGetLastError();
-  if (le != hipSuccess) return done(fail(RB_EDEVICE, "kernel launch failed: %s", hipGetErrorString(le)));
-  return done(RB_OK);
+  int local_rc = need_device(c);
+  if (!local_rc && !local) local_rc = fail(RB_EINVAL, "null shard");
+  ShardSrc src;
+  src.set = local;
+  return gather(c, &src, summary, root, d_dst, cap, true, local_rc);
+}
+
+int rbgpu_shard_gather_host(rbgpu_comm *c, const uint8_t *shard, uint64_t len, const rb_shard_summary *summary,
+                            int root, uint8_t *dst, uint64_t cap) {
+  if (!c || !summary) return fail(RB_EINVAL, "null argument");
+  if (root < 0 || root >= c->nranks) return fail(RB_EINVAL, "bad root %d", root);
+  int local_rc = shard ? RB_OK : fail(RB_EINVAL, "null shard");
+  if (!local_rc && len != summary->local_serialized)
+    local_rc = fail(RB_EINVAL, "shard of %llu bytes, the summary says %llu", (unsigned long long)len,
+                    (unsigned long long)summary->local_serialized);
+  ShardSrc src;
+  src.bytes = shard;
+  src.len = len;
+  return gather(c, &src, summary, root, dst, cap, false, local_rc);
 }
 
 int rbgpu_shard_assemble_host(const uint8_t *const *bufs, const uint64_t *lens, uint32_t nparts, uint8_t *dst,

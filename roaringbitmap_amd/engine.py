@@ -582,6 +582,108 @@ class Comm:
         return bytes(buf[:n].cpu().numpy().tobytes())
 
 
+class HostTransport:
+    """rb_host_transport over a torch.distributed process group (gloo on the CPU): the library's exchange
+    code (summaries, failure agreement, naive_and's order, the shard gather, the header assembly) runs
+    unchanged over it.  Keep the object alive as long as the communicator."""
+
+    def __init__(self, dist, group=None):
+        import torch
+        self.dist, self.group = dist, group
+        self.rank, self.world = dist.get_rank(group), dist.get_world_size(group)
+
+        def all_gather(_user, send, recv, nbytes):
+            try:
+                n = int(nbytes)
+                mine = torch.frombuffer(bytearray(C.string_at(send, n)), dtype=torch.uint8) if n else \
+                    torch.zeros(0, dtype=torch.uint8)
+                outs = [torch.zeros(n, dtype=torch.uint8) for _ in range(self.world)]
+                dist.all_gather(outs, mine, group=group)
+                if n:
+                    C.memmove(recv, bytes(torch.cat(outs).numpy().tobytes()), n * self.world)
+                return 0
+            except Exception:  # noqa: BLE001 — a failure is reported to the library, not raised through C
+                return 1
+
+        def all_reduce(_user, values, n):
+            try:
+                v = np.ctypeslib.as_array(values, shape=(int(n),))
+                t = torch.from_numpy(v.astype(np.int64))
+                dist.all_reduce(t, group=group)
+                v[:] = t.numpy().astype(np.uint64)
+                return 0
+            except Exception:  # noqa: BLE001
+                return 1
+
+        def send(_user, buf, nbytes, peer):
+            try:
+                dist.send(torch.frombuffer(bytearray(C.string_at(buf, int(nbytes))), dtype=torch.uint8), dst=int(peer),
+                          group=group)
+                return 0
+            except Exception:  # noqa: BLE001
+                return 1
+
+        def recv(_user, buf, nbytes, peer):
+            try:
+                t = torch.zeros(int(nbytes), dtype=torch.uint8)
+                dist.recv(t, src=int(peer), group=group)
+                C.memmove(buf, bytes(t.numpy().tobytes()), int(nbytes))
+                return 0
+            except Exception:  # noqa: BLE001
+                return 1
+
+        self._cb = (L.HT_ALL_GATHER(all_gather), L.HT_ALL_REDUCE(all_reduce), L.HT_SEND(send), L.HT_RECV(recv))
+        self.struct = L.RbHostTransport(None, self.world, self.rank, *self._cb)
+
+
+class HostComm:
+    """A communicator over a HostTransport (rbgpu_comm_init_host).  Without a device context only the
+    byte-level exchange applies: a shard given as its serialized bytes (the CPU tests run the oracle's
+    shards through the library's own exchange code this way)."""
+
+    def __init__(self, transport: HostTransport, ctx: Optional["Context"] = None):
+        h = C.c_void_p()
+        L.check(L.lib().rbgpu_comm_init_host(ctx.h if ctx is not None else None, C.byref(transport.struct),
+                                             C.byref(h)))
+        self.h, self.t, self.ctx = h, transport, ctx
+        self.rank, self.nranks = transport.rank, transport.world
+
+    def close(self):
+        if self.h and self.h.value:
+            L.lib().rbgpu_comm_destroy(self.h)
+            self.h = None
+
+    def allreduce_sum(self, values) -> np.ndarray:
+        v = np.ascontiguousarray(np.asarray(values, dtype=np.uint64)).copy()
+        L.check(L.lib().rbgpu_comm_allreduce_sum(self.h, v.ctypes.data_as(L._U64P), len(v)))
+        return v
+
+    def summarize_serialized(self, shard: Optional[bytes]) -> dict:
+        s = L.RbShardSummary()
+        L.check(L.lib().rbgpu_shard_summarize_serialized(self.h, shard, len(shard) if shard else 0, C.byref(s)))
+        return _summary(s)
+
+    def gather_host(self, shard: Optional[bytes], summary: dict, root: int = 0, cap: Optional[int] = None):
+        """The whole result's bytes on `root` (None elsewhere), through rbgpu_shard_gather_host."""
+        s = L.RbShardSummary(**summary)
+        n = int(summary["serialized_size"]) if self.rank == root else 0
+        cap = n if cap is None else cap
+        buf = C.create_string_buffer(max(cap, 1))
+        L.check(L.lib().rbgpu_shard_gather_host(self.h, shard, len(shard) if shard else 0, C.byref(s), root, buf,
+                                                cap))
+        return buf.raw[:n] if self.rank == root else None
+
+    def naive_and_order(self, members, local_counts, failed: bool = False) -> List[int]:
+        m = np.ascontiguousarray(np.asarray(members, dtype=np.uint32))
+        c = np.ascontiguousarray(np.asarray(local_counts, dtype=np.uint64))
+        out = np.zeros(max(len(m), 1), np.uint32)
+        k = C.c_uint32()
+        L.check(L.lib().rbgpu_comm_naive_and_order(self.h, m.ctypes.data_as(L._U32P), c.ctypes.data_as(L._U64P),
+                                                   len(m), 1 if failed else 0, out.ctypes.data_as(L._U32P),
+                                                   C.byref(k)))
+        return out[:k.value].tolist()
+
+
 class DeviceSet64:
     """A batch of 64-bit bitmaps (rbgpu_set64*): buckets (high 32 bits, 32-bit bitmap) in HBM."""
 

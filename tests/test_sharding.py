@@ -315,3 +315,125 @@ def test_gloo_two_rank_pq_refused_on_every_rank():
     out = _spawn(_rank_pq_refused)
     assert out["raised"]
     assert out["ranges"] == [(0, 65536), (65536, 65536)]
+
+
+# ---- the library's own exchange code (comm.hip) over a host transport: rbgpu_comm_init_host with a gloo
+# group, so the sequencing a multi-GPU run takes through RCCL (summaries, failure agreement, naive_and's
+# global order, the shard gather, the header assembly) runs here with 2 and 3 ranks
+def _rank_host_comm(rank, world, port, q):
+    import torch.distributed as dist
+
+    from oracle import rbref as R
+    from roaringbitmap_amd.engine import HostComm, HostTransport
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    out = {}
+    comm = None
+    try:
+        comm = HostComm(HostTransport(dist))
+        vals = load_realdata("census1881_srt")[:48] + synthetic_bitmaps(24, seed=5, max_keys=10, key_space=40)
+        full = [R.RefBitmap.of(v) for v in vals]
+        for r in full[::3]:
+            r.run_optimize()
+        hs = soa_from_serialized([r.serialize() for r in full])
+        kb = np.zeros(65536, np.uint64)
+        np.add.at(kb, hs.key.astype(np.int64), 1)
+        lo, hi = partition_keys(kb, world)[rank]
+        shard_in = []
+        for i, r in enumerate(full):
+            v = r.to_array()
+            sub = R.RefBitmap.of(v[((v >> 16) >= lo) & ((v >> 16) < hi)])
+            if i % 3 == 0:
+                sub.run_optimize()
+            shard_in.append(sub)
+        members = list(range(len(shard_in)))
+        for name, sem in SEMS.items():
+            if name == "NAIVE_AND":  # the global fold order from the all-reduced range counts, in C
+                order = comm.naive_and_order(members, [len(x.containers()) for x in shard_in])
+                local = R.wide(R.NAIVE_AND_ITER, [shard_in[i] for i in order]).serialize()
+            else:
+                local = R.wide(sem, shard_in).serialize()
+            summ = comm.summarize_serialized(local)
+            data = comm.gather_host(local, summ)
+            if rank == 0:
+                want = R.wide(sem, full)
+                out[name] = (data == want.serialize(), summ["cardinality"] == want.cardinality(),
+                             summ["serialized_size"] == len(want.serialize()))
+        # a Run-marker byte straddling a rank boundary, and shards of < 4 containers with Runs (no
+        # offset table): 20 keys alternating Run / Array, cut at containers 3 and 11 (2 ranks: at 5)
+        one = np.concatenate([(k << 16) + (np.arange(100, 3000) if k % 2 else np.arange(0, 4000, 7))
+                              for k in range(20)]).astype(np.uint32)
+        ref = R.RefBitmap.of(one)
+        ref.run_optimize()
+        cuts = {2: [0, 5, 20], 3: [0, 3, 11, 20]}[world]
+        v = ref.to_array()
+        sub = R.RefBitmap.of(v[((v >> 16) >= cuts[rank]) & ((v >> 16) < cuts[rank + 1])])
+        sub.run_optimize()
+        summ = comm.summarize_serialized(sub.serialize())
+        data = comm.gather_host(sub.serialize(), summ)
+        if rank == 0:
+            out["straddle"] = (data == ref.serialize(), summ["cardinality"] == ref.cardinality(),
+                               summ["n_run_containers"] == 10)
+        # one rank fails its argument checks: every rank fails the call together (no rank hangs)
+        bad = rank == world - 1
+        errs = []
+        try:
+            comm.summarize_serialized(None if bad else sub.serialize())
+        except L.RbError as e:
+            errs.append(type(e).__name__)
+        try:  # the root's destination is too small: it fails, the others are told
+            comm.gather_host(sub.serialize(), summ, root=0, cap=8 if rank == 0 else None)
+        except L.RbError as e:
+            errs.append(type(e).__name__)
+        try:
+            comm.naive_and_order(members, [1] * len(members), failed=bad)
+        except L.RbError as e:
+            errs.append(type(e).__name__)
+        out[f"errors{rank}"] = errs
+        sums = comm.allreduce_sum([rank + 1, 2**40])
+        out[f"sum{rank}"] = list(sums) == [world * (world + 1) // 2, world * 2**40]
+        if rank == 0:
+            for r in range(1, world):  # every rank's error list at the root
+                t = torch_obj_recv(dist, r)
+                out.update(t)
+            q.put(out)
+        else:
+            torch_obj_send(dist, {f"errors{rank}": errs, f"sum{rank}": out[f"sum{rank}"]})
+    finally:
+        if comm is not None:
+            comm.close()
+        dist.destroy_process_group()
+
+
+def torch_obj_send(dist, obj):
+    import json
+
+    import torch
+    b = json.dumps(obj).encode()
+    dist.send(torch.tensor([len(b)], dtype=torch.int64), dst=0)
+    dist.send(torch.frombuffer(bytearray(b), dtype=torch.uint8), dst=0)
+
+
+def torch_obj_recv(dist, src):
+    import json
+
+    import torch
+    n = torch.zeros(1, dtype=torch.int64)
+    dist.recv(n, src=src)
+    t = torch.zeros(int(n[0]), dtype=torch.uint8)
+    dist.recv(t, src=src)
+    return json.loads(bytes(t.numpy().tobytes()).decode())
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_host_transport_exchange_in_c(world):
+    out = _spawn(_rank_host_comm, world=world)
+    for name in SEMS:
+        assert all(out[name]), (name, out[name])
+    assert all(out["straddle"]), out["straddle"]
+    for r in range(world):
+        assert out[f"sum{r}"], r
+        errs = out[f"errors{r}"]
+        # summarize (the last rank's null shard), gather (the root's small destination), naive_and order
+        assert len(errs) == 3, (r, errs)
