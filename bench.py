@@ -347,7 +347,8 @@ def pairwise_line(D, ctx, rb, a, b, op, steps, warmup, npairs):
     el, sts = timed(D, ctx, steps, warmup, step)
     sts = [(stats_dict(s), g) for s, g in sts]
     in_b, out_b = sum(s["input_bytes"] for s, _ in sts), sum(s["output_bytes"] for s, _ in sts)
-    tot_in, tot_out = D.reduce([float(in_b), float(out_b)])
+    ops_n = sum(s["tasks"] for s, _ in sts)
+    tot_in, tot_out, tot_ops = D.reduce([float(in_b), float(out_b), float(ops_n)])
     last, glob = sts[-1]
     per_kernel = {}
     for s, _ in sts:
@@ -367,6 +368,9 @@ def pairwise_line(D, ctx, rb, a, b, op, steps, warmup, npairs):
                     f"mixed Array/Bitmap/Run, 2^18 universe",
         "value": round(tot_in / el / 1e9, 3), "unit": "GB/s", "n_gpus": D.world, "steps": steps,
         "ms_per_step": round(el / steps * 1e3, 4), "step_ms": step_spread(D), "scaling": "weak",
+        "container_ops_per_s": round(tot_ops / el, 1),
+        "container_ops_unit": "container-level ops per step, all ranks: matched container pairs + unmatched "
+                              "containers the op copies (RoaringArray.appendCopy), each producing one result",
         "input_bytes_per_step_per_gpu": in_b // steps, "output_bytes_per_step_per_gpu": out_b // steps,
         "roofline_pct_whole_step": round(100.0 * (tot_in + tot_out) / el / 1e9 / (HBM_PEAK_GBS * D.world), 2),
         "result_cardinality_all_ranks": card, "result_containers_rank0": int(last["result_containers"]),
@@ -425,7 +429,7 @@ def run_census(args, ctx, rb, steps=50, warmup=5):
     ops = {k: getattr(rb, k) for k in OPS}
     cards = {k: int(ctx.pairwise(op, s, s, ai, bi).cardinalities().sum()) for k, op in ops.items()}
     # algorithmic bytes of one sweep (deterministic per op), and the device-side call breakdown
-    step_bytes, calls = 0, {}
+    step_bytes, step_ops, calls = 0, 0, {}
     os.environ["RBGPU_SMALL_KERNEL_TIMES"] = "1"  # per-kernel events for this breakdown only
     for k, op in ops.items():
         lib_us = []
@@ -434,6 +438,7 @@ def run_census(args, ctx, rb, steps=50, warmup=5):
             st = ctx.stats()
             lib_us.append(st["call_us"])
         step_bytes += st["input_bytes"]
+        step_ops += st["tasks"]
         calls[k] = {"device_ms": round(st["total_ms"], 4), "c_call_us_median": round(float(np.median(lib_us)), 1),
                     "kernels": {x["name"]: round(x["ms"], 4) for x in st["kernels"]}}
     del os.environ["RBGPU_SMALL_KERNEL_TIMES"]
@@ -458,6 +463,8 @@ def run_census(args, ctx, rb, steps=50, warmup=5):
            "value": round(in_bytes / el / 1e9, 3), "unit": "GB/s", "steps": steps,
            "ms_per_step": round(el / steps * 1e3, 4),
            "us_per_op_sweep": round(el / steps / 4 * 1e6, 1), "cardinality_sums": cards,
+           "container_ops_per_s": round(step_ops * steps / el, 1),
+           "container_ops_unit": "matched container pairs + copied unmatched containers of the 4 x 199 pairs",
            "golden_ok": cards == CENSUS_EXPECTED, "calls": calls,
            "note": "us_per_op_sweep = wall time of one batched call (199 pairs, one op) through the Python "
                    "binding, results materialized in HBM; device_ms = the call's span on the GPU stream"}
@@ -517,11 +524,17 @@ def run_bsi(args, D, ctx, rb, steps=5, warmup=2):
     kb = float(np.mean([s["main_kernel_bytes"] for s, _ in sts]))
     card = sts[-1][1] if sb is not None else int(last["result_cardinality"])
     ts = d.type_stats()
+    # O'Neil chain steps: per active high key, one per slice and comparator (GE, LE) and the final AND
+    chain_keys = float(np.mean([s["kernels"][0]["items"] for s, _ in sts])) / 2 if last["kernels"] else 0.0
+    tot_ops = D.reduce([chain_keys * (2 * BSI_NSLICES + 1) * steps])[0]
     out = {"workload": f"config5: BSI compare RANGE over {BSI_NSLICES} slices x {BSI_NROWS} rows (2 O'Neil chains "
                        "+ AND, fused into one pass per key)",
            "value": round(tot_in / el / 1e9, 3), "unit": "GB/s", "n_gpus": D.world, "steps": steps,
            "ms_per_step": round(el / steps * 1e3, 4), "step_ms": step_spread(D), "scaling": "strong",
            "result_cardinality": card, "containers_rank0": ts,
+           "container_ops_per_s": round(tot_ops / el, 1),
+           "container_ops_unit": f"container ops of the chains, all ranks: per high key {BSI_NSLICES} slices x 2 "
+                                 "comparators (GE, LE) + the final AND",
            "parallelism": (f"high-key range shards x{D.world}, per step all_gather of shard summaries over "
                            + ("librbgpu's RCCL communicator (rbgpu_bsi_compare_sharded)" if comm is not None
                               else "torch.distributed (ShardedBsi)")) if D.world > 1 else "single GPU",
@@ -620,7 +633,9 @@ def run_wide(args, name, D, ctx, rb, nbitmaps, steps, warmup, a=None):
 
     el, sts = timed(D, ctx, steps, warmup, step)
     in_b = sum(s["input_bytes"] for s, _ in sts)
-    total_in = D.reduce([float(in_b)])[0]
+    ts = a.type_stats()
+    local_conts = sum(int(ts[k]) for k in ("array", "bitmap", "run"))
+    total_in, total_ops = D.reduce([float(in_b), float(local_conts * steps)])
     last, res = sts[-1]
     k_ms = float(np.mean([s["main_kernel_ms"] for s, _ in sts]))
     k_bytes = float(np.mean([s["main_kernel_bytes"] for s, _ in sts]))
@@ -629,14 +644,25 @@ def run_wide(args, name, D, ctx, rb, nbitmaps, steps, warmup, a=None):
         "value": round(total_in / el / 1e9, 3), "unit": "GB/s", "n_gpus": D.world, "steps": steps,
         "ms_per_step": round(el / steps * 1e3, 4), "step_ms": step_spread(D), "scaling": "strong",
         "input_bytes_per_step": int(total_in // steps),
+        "container_ops_per_s": round(total_ops / el, 1),
+        "container_ops_unit": "input containers folded per step, all ranks (each member container enters "
+                              "its key's reduction once)",
         "key_range_rank0": [lo, hi],
-        "containers_rank0": a.type_stats(),
+        "containers_rank0": ts,
         "parallelism": (f"key-range shards x{D.world}; per step all_gather of shard summaries (cardinality, "
                         "containers, Run containers, payload bytes) over "
                         + ("librbgpu's RCCL communicator (rbgpu_wide_sharded)" if comm is not None
                            else "torch.distributed (ShardedWide)")) if D.world > 1 else "single GPU",
         "roofline": roofline(last["main_kernel"], k_ms, k_bytes, pmc_traffic(pmc_name), D),
     }
+    # the per-set metadata the kernels derived on the set's first use (outside the timed steps; a caller
+    # that uploads a fresh set per call pays it once per set)
+    su = a.setup_stats()
+    out["setup"] = {"ms": su["ms"], "bytes": su["bytes"],
+                    "what": "rbgpu_set_setup_stats of this rank's set after the line: dense-layout check, packed "
+                            "8-B container records (k_pack_records) and, for naive_xor, their key-major transpose "
+                            "(k_records_transpose); built once per set before the warmup step, not inside the "
+                            "timed steps"}
     out["result_cardinality"] = res.cardinality if res is not None else int(last["result_cardinality"])
     if res is not None:
         out["result_serialized_bytes"] = res.serialized_size
@@ -713,6 +739,8 @@ def main():
                             "input_bytes_per_step_per_gpu": h["input_bytes_per_step_per_gpu"],
                             "output_bytes_per_step_per_gpu": h["output_bytes_per_step_per_gpu"],
                             "roofline_pct_whole_step": h["roofline_pct_whole_step"],
+                            "container_ops_per_s": h["container_ops_per_s"],
+                            "container_ops_unit": h["container_ops_unit"],
                             "result_cardinality_all_ranks": h["result_cardinality_all_ranks"],
                             "containers_a_rank0": a.type_stats(), "containers_b_rank0": b.type_stats(),
                             "parallelism": h["parallelism"]},
@@ -748,11 +776,28 @@ def main():
         for name in c4:
             wide_secondary(name, data)
         data.close()
+    if D.rank == 0:
+        for name, w in secondary.items():  # one line per secondary workload, before the headline
+            print(json.dumps({"secondary_line": name, **w}), flush=True)
     if secondary:
         line["secondary"] = secondary
+        # the headline line ends with a compact summary, so a tail of the output holds every workload
+        line["secondary_summary"] = {n: secondary_summary(w) for n, w in secondary.items()}
     if D.rank == 0:
         print(json.dumps(line), flush=True)
     D.close()
+
+
+def secondary_summary(w: dict) -> dict:
+    rl = w.get("roofline", {})
+    out = {"ms": w.get("ms_per_step"), "GB/s": w.get("value"), "frac": rl.get("frac"),
+           "whole_pct": w.get("roofline_pct_whole_step"), "cops": w.get("container_ops_per_s")}
+    if "setup" in w:
+        out["setup_ms"] = w["setup"]["ms"]
+    cb = w.get("cpu_baseline")
+    if cb:
+        out["cpu"] = cb.get("value")
+    return {k: v for k, v in out.items() if v is not None}
 
 
 if __name__ == "__main__":

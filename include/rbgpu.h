@@ -272,6 +272,12 @@ int rbgpu_bsi_compare_keys(rbgpu_ctx *ctx, const rbgpu_set *bsi, int op, uint64_
 int rbgpu_set_run_optimize(const rbgpu_set *in, rbgpu_set **out, uint8_t *any_run);
 /* RoaringBitmap.clone of bitmaps [first, first+count) into a new set (device copy). */
 int rbgpu_set_extract(const rbgpu_set *set, uint32_t first, uint32_t count, rbgpu_set **out);
+/* The per-set metadata the wide kernels derive on a set's first use and keep with it (sets are
+ * immutable: a cached index, never a cached result): the dense-layout check, packed 8-B container
+ * records and, for naive_xor, their key-major transpose.  *ms = device time spent building them so far,
+ * *bytes = their algorithmic bytes (metadata read + records written).  A caller that uploads a fresh
+ * set per aggregation pays this once per set on top of the call. */
+int rbgpu_set_setup_stats(const rbgpu_set *set, double *ms, uint64_t *bytes);
 
 /* ---- synthetic inputs for the benchmark (device-side generator, SplitMix64) ---------- */
 enum rb_workload {

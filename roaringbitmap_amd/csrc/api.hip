@@ -186,6 +186,7 @@ int ensure_dense(const rbgpu_set *cs) {
     LAUNCHCHK();
   }
   s->ctx->pool.release(d);
+  s->derive_bytes += 2ull * s->nc; // the keys
   if (!bad) {
     s->dense_lo = k0;
     s->dense_hi = (int64_t)k0 + (int64_t)cnt;
@@ -208,6 +209,7 @@ int ensure_mrec(const rbgpu_set *cs) {
     return fail(RB_EDEVICE, "packed-record kernel failed");
   }
   s->mrec = m;
+  s->derive_bytes += 24ull * s->nc; // 16 B of metadata read, an 8-B record written per container
   return RB_OK;
 }
 int ensure_krec(const rbgpu_set *cs) {
@@ -238,6 +240,7 @@ int ensure_krec(const rbgpu_set *cs) {
     return fail(RB_EDEVICE, "key-major record kernel failed");
   }
   s->krec = k;
+  s->derive_bytes += 16ull * s->nc; // each record read and written once
   return RB_OK;
 }
 } // namespace rbg
@@ -1638,6 +1641,13 @@ int rbgpu_bsi_compare_keys(rbgpu_ctx *ctx, const rbgpu_set *bsi, int op, uint64_
 int rbgpu_bsi_compare(rbgpu_ctx *ctx, const rbgpu_set *bsi, int op, uint64_t start_or_value, uint64_t end,
                       uint64_t min_value, uint64_t max_value, const rbgpu_set *found, rbgpu_set **out) {
   return rbgpu_bsi_compare_keys(ctx, bsi, op, start_or_value, end, min_value, max_value, found, 0, 65536, out);
+}
+
+int rbgpu_set_setup_stats(const rbgpu_set *s, double *ms, uint64_t *bytes) {
+  if (!s || !ms || !bytes) return fail(RB_EINVAL, "null argument");
+  *ms = s->derive_ms;
+  *bytes = s->derive_bytes;
+  return RB_OK;
 }
 
 int rbgpu_set_extract(const rbgpu_set *s, uint32_t first, uint32_t count, rbgpu_set **out) {

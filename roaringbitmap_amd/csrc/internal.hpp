@@ -186,6 +186,7 @@ struct rbgpu_set {
   uint64_t *mrec = nullptr;
   uint64_t *krec = nullptr;
   double derive_ms = 0.0;         // device time spent building mrec / krec (reported, not hidden)
+  uint64_t derive_bytes = 0;      // their algorithmic bytes (metadata read + records written)
   rbg::SetView view() const { return rbg::SetView{begin, key, type, card, nruns, off, payload}; }
 };
 

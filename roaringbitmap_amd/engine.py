@@ -279,6 +279,12 @@ class DeviceSet:
                                                     offs.ctypes.data_as(L._U64P)))
         return offs
 
+    def setup_stats(self) -> dict:
+        """rbgpu_set_setup_stats: device ms and algorithmic bytes of the derived per-set metadata so far."""
+        ms, b = C.c_double(), C.c_uint64()
+        L.check(L.lib().rbgpu_set_setup_stats(self.h, C.byref(ms), C.byref(b)))
+        return {"ms": round(ms.value, 4), "bytes": int(b.value)}
+
     def download(self, first: int = 0, count: Optional[int] = None) -> HostSoA:
         count = len(self) - first if count is None else count
         q = L.RbSoa()
