@@ -347,6 +347,24 @@ int rbgpu_set64_cardinalities(const rbgpu_set64 *set, uint64_t *out);
 int rbgpu_set64_portable_sizes(const rbgpu_set64 *set, uint64_t *out);
 int rbgpu_set64_serialize_portable(const rbgpu_set64 *set, uint32_t first, uint32_t count, uint8_t *dst,
                                    uint64_t cap, uint64_t *offsets);
+/* Roaring64NavigableMap's default ("legacy", SERIALIZATION_MODE_LEGACY) format, serializeLegacy /
+ * deserializeLegacy (longlong/Roaring64NavigableMap.java:1229-1240, 1295-1325): a signedLongs byte, a
+ * big-endian int bucket count, then per bucket a big-endian int high and the RoaringBitmap bytes, in
+ * the map's order (signed ints when signedLongs).  The flag travels with the bitmap; in-place results
+ * keep x1's.  Parity unpinned: the reference holds no legacy fixture. */
+int rbgpu_set64_from_legacy(rbgpu_ctx *ctx, const uint8_t *const *bufs, const uint64_t *lens, uint32_t n,
+                            rbgpu_set64 **out);
+int rbgpu_set64_legacy_sizes(const rbgpu_set64 *set, uint64_t *out);
+int rbgpu_set64_serialize_legacy(const rbgpu_set64 *set, uint32_t first, uint32_t count, uint8_t *dst,
+                                 uint64_t cap, uint64_t *offsets);
+/* new Roaring64NavigableMap(signedLongs) for bitmap i: the order its two serializations write the buckets */
+int rbgpu_set64_set_signed_longs(rbgpu_set64 *set, uint32_t i, int signed_longs);
+int rbgpu_set64_get_signed_longs(const rbgpu_set64 *set, uint32_t i, int *signed_longs);
+/* out[i] = the cardinality of the static op's result, without materialising it:
+ * Roaring64Bitmap.andCardinality(x1, x2) (longlong/Roaring64Bitmap.java:562-592) for RB_AND, and the
+ * same bucket merge for or / xor / andNot (getLongCardinality of Roaring64Bitmap.or/xor/andNot). */
+int rbgpu_pairwise64_cardinality(rbgpu_ctx *ctx, int op, const rbgpu_set64 *a, const rbgpu_set64 *b,
+                                 const uint32_t *a_idx, const uint32_t *b_idx, uint32_t npairs, uint64_t *out);
 /* result[i] = op(a[a_idx[i]], b[b_idx[i]]) with flavor's rules; inplace != 0: the state of a[a_idx[i]]
  * after a[a_idx[i]].op(b[b_idx[i]]) (same set and index on both sides: the `x2 == this` branches).
  * RB64_NAVIGABLE needs inplace (the class has no static and/or/xor/andNot). */

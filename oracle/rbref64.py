@@ -24,12 +24,49 @@ AND, OR, XOR, ANDNOT = R.AND, R.OR, R.XOR, R.ANDNOT
 
 
 class Ref64:
-    """[(high, RefBitmap)] in ascending unsigned high order."""
+    """[(high, RefBitmap)] in ascending unsigned high order; `signed`: Roaring64NavigableMap's signedLongs
+    (its TreeMap then iterates the highs as signed ints, which fixes the serialized bucket order)."""
 
-    __slots__ = ("buckets",)
+    __slots__ = ("buckets", "signed")
 
-    def __init__(self, buckets: List[Tuple[int, "R.RefBitmap"]] = None):
+    def __init__(self, buckets: List[Tuple[int, "R.RefBitmap"]] = None, signed: bool = False):
         self.buckets = list(buckets or [])
+        self.signed = signed
+
+    def _map_order(self):
+        """The buckets in the map's iteration order (Roaring64NavigableMap.highToBitmap.entrySet())."""
+        if not self.signed:
+            return self.buckets
+        return sorted(self.buckets, key=lambda hb: hb[0] - (1 << 32) if hb[0] >= 1 << 31 else hb[0])
+
+    @classmethod
+    def from_legacy(cls, data: bytes) -> "Ref64":
+        """Roaring64NavigableMap.deserializeLegacy (:1295-1325): readBoolean signedLongs, readInt count,
+        then readInt high + RoaringBitmap.deserialize each (DataInput ints are big-endian)."""
+        if len(data) < 5:
+            raise IOError("truncated 64-bit bitmap")
+        signed = data[0] != 0
+        (n,) = struct.unpack_from(">i", data, 1)
+        pos, out = 5, []
+        for _ in range(n):
+            if pos + 4 > len(data):
+                raise IOError("truncated 64-bit bitmap")
+            (h,) = struct.unpack_from(">I", data, pos)
+            pos += 4
+            b = R.RefBitmap.deserialize(data[pos:])
+            pos += len(b.serialize())
+            out.append((h, b))
+        out.sort(key=lambda hb: hb[0])  # kept in unsigned order; `signed` restores the map's order
+        return cls(out, signed)
+
+    def to_legacy(self) -> bytes:
+        """Roaring64NavigableMap.serializeLegacy (:1229-1240): writeBoolean(signedLongs), writeInt(size),
+        then writeInt(high) + the RoaringBitmap's serialize per entry, in the map's order."""
+        parts = [struct.pack(">?i", self.signed, len(self.buckets))]
+        for h, b in self._map_order():
+            parts.append(struct.pack(">I", h))
+            parts.append(b.serialize())
+        return b"".join(parts)
 
     @classmethod
     def of(cls, values) -> "Ref64":
@@ -60,8 +97,9 @@ class Ref64:
         return cls(out)
 
     def to_portable(self) -> bytes:
+        """serializePortable (:1254-1261): the map's entries in its iteration order."""
         parts = [struct.pack("<Q", len(self.buckets))]
-        for h, b in self.buckets:
+        for h, b in self._map_order():
             parts.append(struct.pack("<I", h))
             parts.append(b.serialize())
         return b"".join(parts)
@@ -77,7 +115,7 @@ class Ref64:
                                for h, b in self.buckets])
 
     def clone(self) -> "Ref64":
-        return Ref64([(h, b.clone()) for h, b in self.buckets])
+        return Ref64([(h, b.clone()) for h, b in self.buckets], self.signed)
 
 
 def _merge(x1: Ref64, x2: Ref64):
@@ -129,11 +167,16 @@ def bitmap_op(op: int, x1: Ref64, x2: Ref64, inplace: bool, same: bool = False) 
     return Ref64(out)
 
 
+def and_cardinality(x1: Ref64, x2: Ref64) -> int:
+    """Roaring64Bitmap.andCardinality (:562-592): per matched 48-bit key container1.andCardinality."""
+    return sum(R.op(AND, a, b).cardinality() for _, a, b in _merge(x1, x2) if a is not None and b is not None)
+
+
 def navigable_op(op: int, x1: Ref64, x2: Ref64, same: bool = False) -> Ref64:
     """Roaring64NavigableMap in-place x1.and/or/xor/andNot(x2) (:773-977): per bucket the 32-bit
     RoaringBitmap in-place op; a bucket left empty stays in the map; `same`: x2 == this."""
     if same:
-        return x1.clone() if op in (AND, OR) else Ref64()  # return / clear()
+        return x1.clone() if op in (AND, OR) else Ref64(signed=x1.signed)  # return / clear()
     out = []
     for h, a, b in _merge(x1, x2):
         if a is not None and b is not None:
@@ -148,4 +191,4 @@ def navigable_op(op: int, x1: Ref64, x2: Ref64, same: bool = False) -> Ref64:
                 continue
             r = b.clone()                   # pushBitmapForHigh(high, lowBitmap2.clone())
         out.append((h, r))
-    return Ref64(out)
+    return Ref64(out, x1.signed)

@@ -62,6 +62,7 @@ void set_release(rbgpu_set *s) {
   p.release(s->payload);
   p.release(s->mrec);
   p.release(s->krec);
+  p.release(s->kslots);
   rbgpu_ctx *ctx = s->ctx;
   s->ctx = nullptr;
   ctx_unref(ctx);
@@ -241,6 +242,26 @@ int ensure_krec(const rbgpu_set *cs) {
   }
   s->krec = k;
   s->derive_bytes += 16ull * s->nc; // each record read and written once
+  return RB_OK;
+}
+int ensure_kslots(const rbgpu_set *cs) {
+  rbgpu_set *s = const_cast<rbgpu_set *>(cs);
+  if (s->kslots) return RB_OK;
+  int rc = ensure_krec(s);
+  if (rc) return rc;
+  HIPCHK(hipSetDevice(s->ctx->device));
+  uint4 *k = nullptr;
+  if (s->ctx->pool.alloc((void **)&k, std::max<uint64_t>(s->nc, 1) * 32)) return fail(RB_ENOMEM, "key-major run slots");
+  {
+    DeriveTimer t(s);
+    launch_run_slots(s->payload, s->payload_bytes, s->krec, s->nc, k, s->ctx->stream);
+  }
+  if (hipGetLastError() != hipSuccess) {
+    s->ctx->pool.release(k);
+    return fail(RB_EDEVICE, "run-slot kernel failed");
+  }
+  s->kslots = k;
+  s->derive_bytes += 8ull * s->nc + 32ull * s->nc; // the record read, the two 16-B halves written (+ the runs read)
   return RB_OK;
 }
 } // namespace rbg

@@ -185,6 +185,10 @@ struct rbgpu_set {
   int64_t dense_lo = -2, dense_hi = -2;
   uint64_t *mrec = nullptr;
   uint64_t *krec = nullptr;
+  //   kslots               dense sets only: each krec container's run list (<= 8 runs) as two 16-B halves,
+  //                        kslots[i] runs 0..3 and kslots[nc + i] runs 4..7, key-major like krec, so a wave
+  //                        reading one key's members reads them contiguously (naive_xor's fast path)
+  uint4 *kslots = nullptr;
   double derive_ms = 0.0;         // device time spent building mrec / krec (reported, not hidden)
   uint64_t derive_bytes = 0;      // their algorithmic bytes (metadata read + records written)
   rbg::SetView view() const { return rbg::SetView{begin, key, type, card, nruns, off, payload}; }
@@ -205,6 +209,7 @@ int ensure_max_runs(const rbgpu_set *s);
 int ensure_dense(const rbgpu_set *s);
 int ensure_mrec(const rbgpu_set *s);
 int ensure_krec(const rbgpu_set *s); // needs a dense set (dense_lo >= 0)
+int ensure_kslots(const rbgpu_set *s); // needs krec
 // call accounting: zero the byte counters + record the start event / read everything back
 // zero = false: the caller's counters come zeroed some other way (the small-batch path's H2D copy)
 void stats_begin(rbgpu_ctx *ctx, bool zero = true);

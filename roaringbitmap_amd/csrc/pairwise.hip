@@ -522,8 +522,13 @@ __device__ __forceinline__ RecU load_rec(const TaskRec *r) {
 //           the left; ArrayContainer.and/andNot :184-271, BitmapContainer.and(Array) :162-172,
 //           RunContainer.and(Array) :305-336): P = F, Q = the other operand X, staged in LDS;
 //   kHeavy  everything else: P = A, Q = B as 65536-bit register bitmaps.
+#ifndef RBG_HEAVY_NOPF
+#define RBG_HEAVY_NOPF 0 // study: register-path tasks without the one-task prefetch, at 128 VGPRs, so three
+                         // light waves fit beside each heavy one on a SIMD
+#endif
 constexpr int kLightWaves = 4; // waves per SIMD of the copy + filter kernel (128 VGPRs)
-constexpr int kHeavyWaves = 2; // waves per SIMD the register-path kernel is allocated for (prefetch + bitmap)
+constexpr int kHeavyWaves = RBG_HEAVY_NOPF ? 4 : 2; // waves per SIMD the register-path kernel is allocated for
+constexpr bool kHeavyPrefetch = !RBG_HEAVY_NOPF;    // the next task's payloads in flight during this one's emission
 #ifndef RBG_STUDY
 #define RBG_STUDY 0 // study builds: per-phase s_memtime totals of a few light / heavy waves (printf)
 #endif
@@ -797,7 +802,8 @@ __global__ __launch_bounds__(256, ROLE == kRoleHeavy ? kHeavyWaves : kLightWaves
 #define RBG_HT(x)
 #endif
   load_chunks(pq, tc.pp, tc.bigp ? 16u : tc.pbytes, lane);
-  if (tc.kind == kCopy || tc.bigq) load_chunks(qq, tc.pp, 16, lane);
+  if (ROLE == kRoleHeavy && !kHeavyPrefetch) {
+  } else if (tc.kind == kCopy || tc.bigq) load_chunks(qq, tc.pp, 16, lane);
   else load_chunks(qq, tc.pq, tc.qbytes, lane);
   while (true) {
     uint64_t gn = g + stride;
@@ -823,8 +829,9 @@ __global__ __launch_bounds__(256, ROLE == kRoleHeavy ? kHeavyWaves : kLightWaves
     if (ROLE == kRoleHeavy && OP == RB_AND && tc.tp == kRun && tc.tq == kRun && !tc.bigp &&
         !tc.bigq && ((tc.rp + 3) & ~3u) + tc.rq <= 2048u) {
       int r = 0;
+      if (!kHeavyPrefetch) load_chunks(qq, tc.pq, tc.qbytes, lane);
       done = and_runs_intervals<CARD_ONLY>(pq, qq, tc.rp, tc.rq, s, dst, lane, c, r);
-      if (done) {
+      if (done && kHeavyPrefetch) {
         ty = c == 0 ? kEmpty : CARD_ONLY ? kArray : kRun;
         nr = ty == kRun ? (uint32_t)r : 0u;
         __builtin_amdgcn_sched_barrier(0);
@@ -833,6 +840,9 @@ __global__ __launch_bounds__(256, ROLE == kRoleHeavy ? kHeavyWaves : kLightWaves
           load_chunks(qq, real ? tn.pq : tn.pp, real ? tn.qbytes : 16u, lane);
         }
         load_chunks(pq, tn.pp, tn.bigp ? 16u : tn.pbytes, lane);
+      } else if (done) {
+        ty = c == 0 ? kEmpty : CARD_ONLY ? kArray : kRun;
+        nr = ty == kRun ? (uint32_t)r : 0u;
       }
     }
     if (ROLE == kRoleHeavy && !done) {
@@ -863,6 +873,11 @@ __global__ __launch_bounds__(256, ROLE == kRoleHeavy ? kHeavyWaves : kLightWaves
         lds_read_words(s, w, lane);
         wave_lds_sync();
       }
+      // without prefetch Q is loaded only now, once P's registers are free (P and Q are never live
+      // together: the wave fits 128 VGPRs)
+      if (!kHeavyPrefetch && !(OP == RB_AND && tc.tp == kRun && tc.tq == kRun && !tc.bigp && !tc.bigq &&
+                               ((tc.rp + 3) & ~3u) + tc.rq <= 2048u))
+        load_chunks(qq, tc.bigq ? tc.pp : tc.pq, tc.bigq ? 16u : tc.qbytes, lane);
       if (bitmap_payload(tc.tq, tc.cq)) {
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
@@ -893,11 +908,13 @@ __global__ __launch_bounds__(256, ROLE == kRoleHeavy ? kHeavyWaves : kLightWaves
       //      scheduler from hoisting these loads above the consumption of the current ones)
       RBG_HT(lt2 = __builtin_amdgcn_s_memtime(); lt_acc[1] += lt2 - lt1);
       __builtin_amdgcn_sched_barrier(0);
-      {
-        const bool real = has_next && !tn.bigq;
-        load_chunks(qq, real ? tn.pq : tn.pp, real ? tn.qbytes : 16u, lane);
+      if (kHeavyPrefetch) {
+        {
+          const bool real = has_next && !tn.bigq;
+          load_chunks(qq, real ? tn.pq : tn.pp, real ? tn.qbytes : 16u, lane);
+        }
+        load_chunks(pq, tn.pp, tn.bigp ? 16u : tn.pbytes, lane);
       }
-      load_chunks(pq, tn.pp, tn.bigp ? 16u : tn.pbytes, lane);
       const int ta = tc.tp, tb = tc.tq;
       const bool lazy = OP == RB_OR && tm.lazy;
       const bool eff = eff_rule<OP>(ta, tb, tc.cp, tc.cq);
@@ -969,6 +986,8 @@ __global__ __launch_bounds__(256, ROLE == kRoleHeavy ? kHeavyWaves : kLightWaves
     g = gn;
     cur = nx;
     tc = tn;
+    if (ROLE == kRoleHeavy && !kHeavyPrefetch) // this task's first payload, loaded only now
+      load_chunks(pq, tc.pp, tc.bigp ? 16u : tc.pbytes, lane);
   }
 #if RBG_STUDY
   if (ROLE == kRoleLight && lane == 0 && wv == 0 && blockIdx.x % 97 == 0)
@@ -1225,12 +1244,16 @@ static void launch_tasks(const uint8_t *pa, const uint8_t *pb, const TaskRec *re
                          const TaskMeta &tm, hipStream_t st, unsigned per_cu = 0,
                          unsigned long long *queue = nullptr) {
   if (!n) return;
+#ifndef RBG_LDS_PAD
+#define RBG_LDS_PAD 0 // study: dynamic LDS a light block reserves without using it (occupancy sensitivity)
+#endif
+  const size_t dyn = ROLE == kRoleLight ? RBG_LDS_PAD : 0;
   static unsigned occ_cap = 0; // occupancy-derived grid cap, per template instance
   if (!occ_cap) occ_cap = persistent_blocks(k_pair_tasks<OP, CARD_ONLY, ROLE>, ~0ull >> 8);
   const unsigned cap = per_cu ? std::min(occ_cap, per_cu * cu_count()) : occ_cap;
   const uint64_t want = (n + 3) / 4;
   const unsigned blocks = (unsigned)(want < cap ? want : cap);
-  k_pair_tasks<OP, CARD_ONLY, ROLE><<<blocks, 256, 0, st>>>(pa, pb, recs, n, out, tm, queue);
+  k_pair_tasks<OP, CARD_ONLY, ROLE><<<blocks, 256, dyn, st>>>(pa, pb, recs, n, out, tm, queue);
 }
 template <int OP>
 static void launch_op(bool card_only, const uint8_t *pa, const uint8_t *pb, const TaskRec *light, uint64_t nl,
@@ -1242,7 +1265,7 @@ static void launch_op(bool card_only, const uint8_t *pa, const uint8_t *pb, cons
   if (card_only) launch_tasks<OP, true, kRoleHeavy>(pa, pb, heavy, nh, out, tm, st);
   else launch_tasks<OP, false, kRoleHeavy>(pa, pb, heavy, nh, out, tm, st);
 }
-constexpr unsigned kConcLightPerCu = 2; // light blocks per CU beside the heavy kernel (2 x 128 VGPRs per SIMD)
+constexpr unsigned kConcLightPerCu = RBG_HEAVY_NOPF ? 3 : 2; // light blocks per CU beside the heavy kernel (2 x 128 VGPRs per SIMD)
 constexpr unsigned kConcHeavyPerCu = 1; // heavy blocks per CU (256 VGPRs per SIMD)
 template <int OP>
 static void launch_op_concurrent(bool card_only, const uint8_t *pa, const uint8_t *pb, const TaskRec *light,

@@ -423,6 +423,27 @@ class Context:
         L.check(L.lib().rbgpu_set64_from_portable(self.h, arr, lens.ctypes.data_as(L._U64P), n, C.byref(out)))
         return DeviceSet64(self, out.value)
 
+    def upload_legacy64(self, blobs: Sequence[bytes]) -> "DeviceSet64":
+        """Roaring64NavigableMap.deserializeLegacy per blob (rbgpu_set64_from_legacy): the signedLongs
+        flag travels with each bitmap."""
+        n = len(blobs)
+        arr = (C.c_char_p * max(n, 1))(*blobs)
+        lens = np.array([len(b) for b in blobs] or [0], np.uint64)
+        out = C.c_void_p()
+        L.check(L.lib().rbgpu_set64_from_legacy(self.h, arr, lens.ctypes.data_as(L._U64P), n, C.byref(out)))
+        return DeviceSet64(self, out.value)
+
+    def pairwise64_cardinality(self, op: int, a: "DeviceSet64", b: "DeviceSet64", a_idx=None, b_idx=None,
+                               npairs=None) -> np.ndarray:
+        """rbgpu_pairwise64_cardinality: the static op's getLongCardinality per pair (Roaring64Bitmap.
+        andCardinality for AND) without materialising the results."""
+        ai, ap = _idx_addr(a_idx)
+        bi, bp = _idx_addr(b_idx)
+        n = npairs if npairs is not None else (len(ai) if ai is not None else min(len(a), len(b)))
+        out = np.zeros(max(n, 1), np.uint64)
+        L.check(L.lib().rbgpu_pairwise64_cardinality(self.h, op, a.h, b.h, ap, bp, n, out.ctypes.data_as(L._U64P)))
+        return out[:n]
+
     def upload_values64(self, bitmaps: Sequence[np.ndarray]) -> "DeviceSet64":
         """bitmapOf(long...) per value list: buckets by the high 32 bits (rbgpu_set64_from_buckets)."""
         lows, highs, begin = [], [], [0]
@@ -736,27 +757,46 @@ class DeviceSet64:
         L.check(L.lib().rbgpu_set64_extract(self.h, first, count, C.byref(out)))
         return DeviceSet64(self.ctx, out.value)
 
+    def signed_longs(self, i: int) -> bool:
+        v = C.c_int()
+        L.check(L.lib().rbgpu_set64_get_signed_longs(self.h, i, C.byref(v)))
+        return bool(v.value)
+
     def values(self, i: int) -> np.ndarray:
-        """Every value of bitmap i, ascending unsigned: each bucket's low halves under its high."""
+        """Every value of bitmap i in its map's order: ascending unsigned, or for a signedLongs
+        Roaring64NavigableMap the buckets of negative highs first (the signed order of the longs)."""
         highs = self.highs(i)
         if not len(highs):
             return np.zeros(0, np.uint64)
         h = self.bucket_set(i).download()
-        return np.concatenate([(np.uint64(hi) << np.uint64(32)) | h.values(k).astype(np.uint64)
-                               for k, hi in enumerate(highs.tolist())])
+        parts = [(np.uint64(hi) << np.uint64(32)) | h.values(k).astype(np.uint64) for k, hi in enumerate(highs.tolist())]
+        if self.signed_longs(i):
+            parts = [p for hi, p in zip(highs.tolist(), parts) if hi >= 1 << 31] + \
+                    [p for hi, p in zip(highs.tolist(), parts) if hi < 1 << 31]
+        return np.concatenate(parts)
 
-    def serialize_portable(self) -> List[bytes]:
+    def _serialize(self, sizes_fn, ser_fn) -> List[bytes]:
         n = len(self)
         if n == 0:
             return []
         sizes = np.zeros(n, np.uint64)
-        L.check(L.lib().rbgpu_set64_portable_sizes(self.h, sizes.ctypes.data_as(L._U64P)))
+        L.check(sizes_fn(self.h, sizes.ctypes.data_as(L._U64P)))
         total = int(sizes.sum())
         buf = C.create_string_buffer(max(total, 1))
         offs = np.zeros(n + 1, np.uint64)
-        L.check(L.lib().rbgpu_set64_serialize_portable(self.h, 0, n, buf, total, offs.ctypes.data_as(L._U64P)))
+        L.check(ser_fn(self.h, 0, n, buf, total, offs.ctypes.data_as(L._U64P)))
         raw = buf.raw
         return [raw[int(offs[i]):int(offs[i + 1])] for i in range(n)]
+
+    def serialize_portable(self) -> List[bytes]:
+        return self._serialize(L.lib().rbgpu_set64_portable_sizes, L.lib().rbgpu_set64_serialize_portable)
+
+    def serialize_legacy(self) -> List[bytes]:
+        """Roaring64NavigableMap.serializeLegacy per bitmap (its default serialize)."""
+        return self._serialize(L.lib().rbgpu_set64_legacy_sizes, L.lib().rbgpu_set64_serialize_legacy)
+
+    def set_signed_longs(self, i: int, flag: bool) -> None:
+        L.check(L.lib().rbgpu_set64_set_signed_longs(self.h, i, 1 if flag else 0))
 
 
 def assemble_host(parts: Sequence[bytes]) -> bytes:

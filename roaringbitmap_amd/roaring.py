@@ -505,10 +505,28 @@ class _Bitmap64:
 
 class Roaring64NavigableMap(_Bitmap64):
     """org.roaringbitmap.longlong.Roaring64NavigableMap (longlong/Roaring64NavigableMap.java): in-place
-    and/or/xor/andNot(x2) per bucket with the 32-bit RoaringBitmap's in-place ops (:773-977)."""
+    and/or/xor/andNot(x2) per bucket with the 32-bit RoaringBitmap's in-place ops (:773-977).  serialize /
+    deserialize use the default SERIALIZATION_MODE_LEGACY format (:51, 1207-1252, 1276-1325)."""
 
     __slots__ = ()
     FLAVOR = L.RB64_NAVIGABLE
+
+    def __init__(self, dset=None, signedLongs: bool = False):
+        super().__init__(dset)
+        if signedLongs:
+            self._set.set_signed_longs(0, True)
+
+    @classmethod
+    def deserializeLegacy(cls, data: bytes):
+        """deserializeLegacy (:1295-1325): signedLongs, then the buckets (IOError on bad bytes)."""
+        return cls(default_context().upload_legacy64([data]))
+
+    deserialize = deserializeLegacy
+
+    def serializeLegacy(self) -> bytes:
+        return self._set.serialize_legacy()[0]
+
+    serialize = serializeLegacy
 
 
 class _StaticOrInPlace64(_StaticOrInPlace):
@@ -525,6 +543,12 @@ class Roaring64Bitmap(_Bitmap64):
 
     __slots__ = ()
     FLAVOR = L.RB64_BITMAP
+
+    @staticmethod
+    def andCardinality(x1, x2) -> int:
+        """Roaring64Bitmap.andCardinality (longlong/Roaring64Bitmap.java:562-592), on the device."""
+        return int(default_context().pairwise64_cardinality(L.AND, x1._set, x2._set, npairs=1)[0])
+
     and_ = _StaticOrInPlace64(L.AND)
     or_ = _StaticOrInPlace64(L.OR)
     xor = _StaticOrInPlace64(L.XOR)

@@ -1,14 +1,18 @@
 #!/bin/bash
 # Runs one gpurun call; if the pool reports a transient infrastructure failure (the command
-# never started: box not prepared / no slot), waits and asks again.  Command failures are
-# never retried.
-for attempt in 1 2 3 4 5; do
-  /usr/local/graft/bin/gpurun "$@"
-  rc=$?
+# never started: box not prepared / no slot / backing off), waits as long as it asks and asks
+# again.  Command failures are never retried.
+for attempt in 1 2 3 4 5 6 7 8 9 10; do
+  out=$(mktemp)
+  /usr/local/graft/bin/gpurun "$@" 2>&1 | tee "$out"
+  rc=${PIPESTATUS[0]}
   st=$(python3 -c "import json;print(json.load(open('gpurun_out/.last_call.json')).get('status',''))" 2>/dev/null)
+  wait_s=$(grep -o 'retry in [0-9]*s' "$out" | tail -1 | grep -o '[0-9]*')
+  rm -f "$out"
   if [ "$st" = "transient" ] || [ $rc -eq 3 ]; then
-    echo "[gpu.sh] transient ($st rc=$rc), retry $attempt after 40s" >&2
-    sleep 40
+    sleep_s=$(( ${wait_s:-30} + 15 ))
+    echo "[gpu.sh] transient ($st rc=$rc), retry $attempt after ${sleep_s}s" >&2
+    sleep $sleep_s
     continue
   fi
   exit $rc

@@ -151,13 +151,13 @@ def test_roaring64_kept_empty_container_through_later_ops(ctx, oracle):
     ref_xy = R64.bitmap_op(rb.XOR, x, y, True)
     assert xy.serialize_portable()[0] == ref_xy.to_portable()
     assert [c[2] for c in ref_xy.buckets[0][1].containers()] == [0, 0]  # two kept empty containers
-    pool = [r.to_portable() for r in (ref_xy, z_other_high, z_other_key, z_matched)]
-    s2 = ctx.upload_portable64(pool)
+    # the device result itself is the left operand (its portable bytes, card - 1 = 0xFFFF, do not read
+    # back — the reference's own reader would take 65536 values there too)
     refs = [ref_xy, z_other_high, z_other_key, z_matched]
     for opname, op in OPS.items():
         for j in (1, 2, 3):
             for inplace in (False, True):
-                got = ctx.pairwise64(rb.RB64_BITMAP, op, s2, s2, [0], [j], inplace=inplace).serialize_portable()[0]
+                got = ctx.pairwise64(rb.RB64_BITMAP, op, xy, s, [0], [j + 1], inplace=inplace).serialize_portable()[0]
                 want = R64.bitmap_op(op, refs[0], refs[j], inplace)
                 assert got == want.to_portable(), (opname, j, inplace)
 
@@ -188,3 +188,54 @@ def test_roaring64_mirror_after_empty_xor(ctx, oracle):
     assert nav.isEmpty() and len(nav._set.highs(0)) == 1
     ref = R64.navigable_op(rb.AND, R64.Ref64.of([1]), R64.Ref64.of([2]))
     assert nav.serializePortable() == ref.to_portable()
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+def test_roaring64_legacy_format_and_cardinality(ctx, oracle, seed):
+    """Roaring64NavigableMap's default (legacy) format on the device: ingest and emit round-trip the
+    oracle's bytes, signed and unsigned (parity unpinned: no reference fixture, see test_oracle64); an
+    in-place op keeps x1's signedLongs and the legacy bytes equal the oracle's.  The 64-bit cardinality
+    entry (Roaring64Bitmap.andCardinality, longlong/Roaring64Bitmap.java:562-592, and the same merge for
+    or / xor / andNot) equals the materialised static results' cardinalities."""
+    import roaringbitmap_amd as rb
+    from oracle import rbref64 as R64
+    _, refs = _pool(ctx, oracle, seed, n=8)
+    for i, r in enumerate(refs):
+        r.signed = i % 2 == 1
+    blobs = [r.to_legacy() for r in refs]
+    s = ctx.upload_legacy64(blobs)
+    assert s.serialize_legacy() == blobs
+    assert s.serialize_portable() == [r.to_portable() for r in refs]
+    n = len(refs)
+    ai = np.array([i for i in range(n) for j in range(n)], np.uint32)
+    bi = np.array([j for i in range(n) for j in range(n)], np.uint32)
+    for opname, op in OPS.items():
+        got = ctx.pairwise64(rb.RB64_NAVIGABLE, op, s, s, ai, bi, inplace=True).serialize_legacy()
+        for k in range(len(ai)):
+            i, j = int(ai[k]), int(bi[k])
+            assert got[k] == R64.navigable_op(op, refs[i], refs[j], same=i == j).to_legacy(), (opname, i, j)
+        cards = ctx.pairwise64_cardinality(op, s, s, ai, bi)
+        mat = ctx.pairwise64(rb.RB64_BITMAP, op, s, s, ai, bi).cardinalities()
+        assert np.array_equal(cards, mat), opname
+        if op == rb.AND:
+            for k in range(0, len(ai), 7):
+                assert int(cards[k]) == R64.and_cardinality(refs[ai[k]], refs[bi[k]])
+    with pytest.raises(rb.FormatError):
+        ctx.upload_legacy64([blobs[0][:-1]])
+
+
+def test_roaring64_navigable_mirror_legacy(ctx, oracle):
+    """TestRoaring64NavigableMap.testSerialization_MultipleBuckets_Signed / _Unsigned (:741-773) through
+    the mirror: serialize() is the legacy format, deserialize() restores the map and its value order."""
+    import roaringbitmap_amd as rb
+    vals = np.array([(-123) & (2**64 - 1), 123, 2**63 - 1], np.uint64)
+    for signed, order in ((True, [-123, 123, 2**63 - 1]), (False, [123, 2**63 - 1, -123])):
+        m = rb.Roaring64NavigableMap(rb.Roaring64NavigableMap.bitmapOf(vals)._set, signedLongs=signed)
+        clone = rb.Roaring64NavigableMap.deserialize(m.serialize())
+        assert clone.getLongCardinality() == 3
+        assert [int(np.int64(np.uint64(clone.select(j)))) for j in range(3)] == order
+        assert len(m.serialize()) == 1 + 4 + 3 * 4 + sum(
+            len(x) - 12 for x in [rb.Roaring64NavigableMap.bitmapOf([v]).serializePortable() for v in vals])
+    a = rb.Roaring64Bitmap.bitmapOf(vals)
+    b = rb.Roaring64Bitmap.bitmapOf(np.array([123, 5], np.uint64))
+    assert rb.Roaring64Bitmap.andCardinality(a, b) == 1

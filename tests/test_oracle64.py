@@ -60,3 +60,49 @@ def test_oracle64_ops_contract():
     assert [h for h, _ in R64.navigable_op(R.AND, x, y).buckets] == [0, 3]  # bucket 3 stays, empty
     assert R64.bitmap_op(R.XOR, x, x, True, same=True).buckets == []
     assert R64.navigable_op(R.OR, x, x, same=True).to_portable() == x.to_portable()
+
+
+def test_oracle64_legacy_format():
+    """Roaring64NavigableMap.serializeLegacy / deserializeLegacy (the default SERIALIZATION_MODE_LEGACY,
+    Roaring64NavigableMap.java:51, 1229-1240, 1295-1325): signedLongs byte, big-endian int count and highs,
+    little-endian RoaringBitmaps, in the map's order.  The reference holds no legacy fixture (parity
+    unpinned); its tests pin the size (checkSerializeBytes: 1 + 4 + sum(4 + bucket bytes),
+    TestRoaring64NavigableMap.java:66-73, 775-790) and the signed / unsigned value order after a clone
+    through this format (testSerialization_MultipleBuckets_Signed / _Unsigned, :741-773)."""
+    import struct
+
+    from oracle import rbref64 as R64
+    vals = np.array([(-123) & (2**64 - 1), 123, 2**63 - 1], np.uint64)
+    for signed, order in ((True, [(-123) & (2**64 - 1), 123, 2**63 - 1]), (False, [123, 2**63 - 1, (-123) & (2**64 - 1)])):
+        m = R64.Ref64.of(vals)
+        m.signed = signed
+        data = m.to_legacy()
+        assert len(data) == 1 + 4 + sum(4 + len(b.serialize()) for _, b in m.buckets)
+        assert data[0] == int(signed) and struct.unpack_from(">i", data, 1)[0] == 3
+        back = R64.Ref64.from_legacy(data)
+        assert back.signed == signed and back.to_legacy() == data
+        highs = [struct.unpack_from(">I", data, p)[0] for p in _legacy_high_positions(data)]
+        assert [(h << 32) | int(b.to_array()[0]) for h, b in
+                sorted(back.buckets, key=lambda hb: hb[0] if not signed else (hb[0] ^ (1 << 31)))] == order
+        assert highs == [v >> 32 for v in order]
+    rng = np.random.default_rng(3)
+    for _ in range(5):
+        v = np.unique(rng.integers(0, 2**64 - 1, 300, dtype=np.uint64) >> np.uint64(int(rng.integers(0, 40))))
+        m = R64.Ref64.of(v)
+        for signed in (False, True):
+            m.signed = signed
+            assert R64.Ref64.from_legacy(m.to_legacy()).to_legacy() == m.to_legacy()
+    with pytest.raises((IOError, ValueError, Exception)):
+        R64.Ref64.from_legacy(b"\x00\x00\x00")
+
+
+def _legacy_high_positions(data):
+    from oracle import rbref as R
+    import struct
+    (n,) = struct.unpack_from(">i", data, 1)
+    pos, out = 5, []
+    for _ in range(n):
+        out.append(pos)
+        pos += 4
+        pos += len(R.RefBitmap.deserialize(data[pos:]).serialize())
+    return out
