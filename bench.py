@@ -182,7 +182,7 @@ def parse():
     return p.parse_args()
 
 
-SECONDARY_ALL = ["pairwise_ops", "census", "bsi_range", "wide_or", "wide_and_runs", "wide_xor_runs"]
+SECONDARY_ALL = ["pairwise_async", "pairwise_ops", "census", "bsi_range", "wide_or", "wide_and_runs", "wide_xor_runs"]
 
 # Rehearsal knobs (not used by the driver): RBGPU_DIST_BACKEND=gloo keeps the collectives on the
 # host, RBGPU_SAME_DEVICE=1 puts every rank on device 0 — together they exercise the N>1 path on a
@@ -380,6 +380,38 @@ def pairwise_line(D, ctx, rb, a, b, op, steps, warmup, npairs):
                            else "torch.distributed")) if D.world > 1 else "single GPU",
         "roofline": rl,
     }
+
+
+def pairwise_async_line(D, ctx, rb, a, b, op, steps, warmup, in_bytes, out_bytes, kernel_bytes):
+    """Config 2 through rbgpu_pairwise_async: each step enqueues the next batch while the previous one
+    runs (the host's per-call work and the device-to-host wait of a synchronous call leave the device's
+    critical path); a step's result is freed (after it completes) one step later.  Bytes per step are the
+    synchronous line's (the same pairs and results)."""
+    def run(n):
+        prev = None
+        for _ in range(n):
+            r = ctx.pairwise_async(op, a, b)
+            if prev is not None:
+                prev.close()
+            prev = r
+        if prev is not None:
+            prev.wait().close()
+    run(warmup)
+    ctx.synchronize()
+    D.barrier()
+    ctx.synchronize()
+    t0 = time.perf_counter()
+    run(steps)
+    ctx.synchronize()
+    D.barrier()
+    el = D.reduce([time.perf_counter() - t0], "max")[0]
+    tot_in, tot_all = D.reduce([float(in_bytes * steps), float((in_bytes + out_bytes) * steps)])
+    return {"workload": f"config2 {OPS[op]} as the synchronous line, batches enqueued back to back "
+                        "(rbgpu_pairwise_async)",
+            "value": round(tot_in / el / 1e9, 3), "unit": "GB/s", "n_gpus": D.world, "steps": steps,
+            "ms_per_step": round(el / steps * 1e3, 4), "scaling": "weak",
+            "roofline_pct_whole_step": round(100.0 * tot_all / el / 1e9 / (HBM_PEAK_GBS * D.world), 2),
+            "note": "whole-step only: the per-kernel roofline is the synchronous line's (same kernels)"}
 
 
 def pairwise_cpu_baseline(ctx, a, b, op, seconds: float, sample: int = 50000):
@@ -747,6 +779,10 @@ def main():
                  "roofline": h["roofline"]})
     if D.world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = pairwise_cpu_baseline(ctx, a, b, op, args.cpu_seconds)
+    if "pairwise_async" in sec:
+        secondary["pairwise_" + OPS[op].lower() + "_async"] = pairwise_async_line(
+            D, ctx, rb, a, b, op, args.steps, args.warmup, h["input_bytes_per_step_per_gpu"],
+            h["output_bytes_per_step_per_gpu"], None)
     if "pairwise_ops" in sec:
         for o in range(4):
             if o == op:

@@ -214,6 +214,19 @@ int rbgpu_pairwise(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu_set *
  * (BitmapContainer.java:749-766; the static or() gives a full Run).  A pair whose operands are the
  * same bitmap object (a == b and a_idx[i] == b_idx[i]) follows the `x2 == this` branches: and / or
  * leave x1 as it is, xor / andNot clear it.  Inputs stay unchanged (results are new sets). */
+/* Asynchronous rbgpu_pairwise (SURVEY §8b threading row: "an _async variant takes a stream").  The
+ * call returns once its task kernels and compaction are enqueued; `stream` (a hipStream_t, NULL: the
+ * context's own) is ordered around the call: the caller's earlier work on it runs first, its later work
+ * runs after the result is complete.  *out is usable at once by later library calls on this context (they
+ * are stream-ordered behind it; a call that needs the result's metadata on the host waits for it), and by
+ * the host after rbgpu_set_wait.  The host thread can so prepare and enqueue the next batch while this one
+ * runs on the device.  Batches of <= 4096 pairs (the small-batch path) and more than 256 pending results
+ * per context complete before the return.  rb_stats is not updated by an asynchronous call. */
+int rbgpu_pairwise_async(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu_set *b,
+                         const uint32_t *a_idx, const uint32_t *b_idx, uint32_t npairs, void *stream,
+                         rbgpu_set **out);
+/* Wait until an asynchronous result is complete (a no-op for any other set). */
+int rbgpu_set_wait(const rbgpu_set *set);
 int rbgpu_pairwise_inplace(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu_set *b,
                            const uint32_t *a_idx, const uint32_t *b_idx, uint32_t npairs, rbgpu_set **out);
 /* RoaringBitmap.andCardinality/orCardinality/xorCardinality/andNotCardinality

@@ -110,6 +110,8 @@ SIGNATURES = {
     # index arrays as void* (engine passes plain addresses: see engine._idx_addr)
     "rbgpu_pairwise": (C.c_int, [_P, C.c_int, _P, _P, _P, _P, C.c_uint32, C.POINTER(_P)]),
     "rbgpu_pairwise_cardinality": (C.c_int, [_P, C.c_int, _P, _P, _P, _P, C.c_uint32, _U64P]),
+    "rbgpu_pairwise_async": (C.c_int, [_P, C.c_int, _P, _P, _P, _P, C.c_uint32, C.c_void_p, C.POINTER(_P)]),
+    "rbgpu_set_wait": (C.c_int, [_P]),
     "rbgpu_pairwise_inplace": (C.c_int, [_P, C.c_int, _P, _P, _P, _P, C.c_uint32, C.POINTER(_P)]),
     "rbgpu_set_run_optimize": (C.c_int, [_P, C.POINTER(_P), C.c_void_p]),
     "rbgpu_set_setup_stats": (C.c_int, [_P, C.POINTER(C.c_double), _U64P]),

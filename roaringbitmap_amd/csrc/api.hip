@@ -52,6 +52,7 @@ int set_alloc(rbgpu_ctx *ctx, rbgpu_set *s, uint32_t nb, uint64_t nc, uint64_t p
 }
 void set_release(rbgpu_set *s) {
   if (!s || !s->ctx) return;
+  (void)settle(s); // an asynchronous result's kernels may still write its buffers
   DevPool &p = s->ctx->pool;
   p.release(s->begin);
   p.release(s->key);
@@ -62,7 +63,6 @@ void set_release(rbgpu_set *s) {
   p.release(s->payload);
   p.release(s->mrec);
   p.release(s->krec);
-  p.release(s->kslots);
   rbgpu_ctx *ctx = s->ctx;
   s->ctx = nullptr;
   ctx_unref(ctx);
@@ -75,9 +75,11 @@ void ctx_unref(rbgpu_ctx *ctx) {
   for (auto &e : ctx->ev) (void)hipEventDestroy(e);
   for (auto &e : ctx->ev_side) (void)hipEventDestroy(e);
   (void)hipEventDestroy(ctx->ev_tot);
+  if (ctx->ev_ext) (void)hipEventDestroy(ctx->ev_ext);
   (void)hipFree(ctx->d_stats);
   (void)hipHostFree(ctx->h_pinned);
   (void)hipHostFree(ctx->h_stats);
+  if (ctx->h_async) (void)hipHostFree(ctx->h_async);
   if (ctx->h_stage) (void)hipHostFree(ctx->h_stage);
   if (ctx->h_small) (void)hipHostFree(ctx->h_small);
   ctx->pool.clear();
@@ -87,6 +89,20 @@ void ctx_unref(rbgpu_ctx *ctx) {
   (void)hipStreamDestroy(ctx->stream);
   if (ctx->side) (void)hipStreamDestroy(ctx->side);
   delete ctx;
+}
+int settle(const rbgpu_set *cs) {
+  if (!cs || !cs->pending) return RB_OK;
+  rbgpu_set *s = const_cast<rbgpu_set *>(cs);
+  rbgpu_ctx *ctx = s->ctx;
+  HIPCHK(hipSetDevice(ctx->device));
+  const hipError_t e = hipEventSynchronize(s->pending);
+  (void)hipEventDestroy(s->pending);
+  s->pending = nullptr;
+  s->nc = ctx->h_async[s->pend_slot];
+  ctx->async_free.push_back(s->pend_slot);
+  s->pend_slot = -1;
+  if (e != hipSuccess) return fail(RB_EDEVICE, "asynchronous call failed: %s", hipGetErrorString(e));
+  return RB_OK;
 }
 int ensure_h_begin(const rbgpu_set *cs) {
   rbgpu_set *s = const_cast<rbgpu_set *>(cs);
@@ -242,26 +258,6 @@ int ensure_krec(const rbgpu_set *cs) {
   }
   s->krec = k;
   s->derive_bytes += 16ull * s->nc; // each record read and written once
-  return RB_OK;
-}
-int ensure_kslots(const rbgpu_set *cs) {
-  rbgpu_set *s = const_cast<rbgpu_set *>(cs);
-  if (s->kslots) return RB_OK;
-  int rc = ensure_krec(s);
-  if (rc) return rc;
-  HIPCHK(hipSetDevice(s->ctx->device));
-  uint4 *k = nullptr;
-  if (s->ctx->pool.alloc((void **)&k, std::max<uint64_t>(s->nc, 1) * 32)) return fail(RB_ENOMEM, "key-major run slots");
-  {
-    DeriveTimer t(s);
-    launch_run_slots(s->payload, s->payload_bytes, s->krec, s->nc, k, s->ctx->stream);
-  }
-  if (hipGetLastError() != hipSuccess) {
-    s->ctx->pool.release(k);
-    return fail(RB_EDEVICE, "run-slot kernel failed");
-  }
-  s->kslots = k;
-  s->derive_bytes += 8ull * s->nc + 32ull * s->nc; // the record read, the two 16-B halves written (+ the runs read)
   return RB_OK;
 }
 } // namespace rbg
@@ -513,6 +509,7 @@ int rbgpu_open(int device, rbgpu_ctx **out) {
   for (auto &e : c->ev) (void)hipEventCreate(&e);
   for (auto &e : c->ev_side) (void)hipEventCreate(&e);
   (void)hipEventCreate(&c->ev_tot);
+  (void)hipEventCreateWithFlags(&c->ev_ext, hipEventDisableTiming);
   *out = c;
   return RB_OK;
 }
@@ -651,9 +648,10 @@ void rbgpu_set_free(rbgpu_set *set) {
   delete set;
 }
 uint32_t rbgpu_set_bitmap_count(const rbgpu_set *s) { return s ? s->nb : 0; }
-uint64_t rbgpu_set_container_count(const rbgpu_set *s) { return s ? s->nc : 0; }
+uint64_t rbgpu_set_container_count(const rbgpu_set *s) { return s && !settle(s) ? s->nc : 0; }
 
 int rbgpu_set_cardinalities(const rbgpu_set *s, uint64_t *out) {
+  SETTLE(s);
   if (!s || !out) return fail(RB_EINVAL, "null argument");
   rbgpu_ctx *ctx = s->ctx;
   int rc = check_ctx(ctx);
@@ -669,6 +667,7 @@ int rbgpu_set_cardinalities(const rbgpu_set *s, uint64_t *out) {
 }
 
 int rbgpu_set_download(const rbgpu_set *s, uint32_t first, uint32_t count, rb_soa *soa) {
+  SETTLE(s);
   if (!s || !soa) return fail(RB_EINVAL, "null argument");
   if ((uint64_t)first + count > s->nb) return fail(RB_EINVAL, "bitmap range out of bounds");
   HostSoA h;
@@ -696,6 +695,7 @@ int rbgpu_set_download(const rbgpu_set *s, uint32_t first, uint32_t count, rb_so
 }
 
 int rbgpu_set_serialized_sizes(const rbgpu_set *s, uint64_t *out) {
+  SETTLE(s);
   if (!s || !out) return fail(RB_EINVAL, "null argument");
   int rc = check_ctx(s->ctx);
   if (rc) return rc;
@@ -727,6 +727,7 @@ int rbgpu_set_serialized_sizes(const rbgpu_set *s, uint64_t *out) {
 }
 
 int rbgpu_set_summaries(const rbgpu_set *s, uint32_t first, uint32_t count, rb_bitmap_summary *out) {
+  SETTLE(s);
   if (!s || (count && !out)) return fail(RB_EINVAL, "null argument");
   if ((uint64_t)first + count > s->nb) return fail(RB_EINVAL, "bitmap range out of bounds");
   int rc = check_ctx(s->ctx);
@@ -761,6 +762,7 @@ int rbgpu_set_summaries(const rbgpu_set *s, uint32_t first, uint32_t count, rb_b
 }
 
 int rbgpu_set_type_stats(const rbgpu_set *s, uint64_t *out) {
+  SETTLE(s);
   if (!s || !out) return fail(RB_EINVAL, "null argument");
   int rc = check_ctx(s->ctx);
   if (rc) return rc;
@@ -804,6 +806,7 @@ __global__ void k_range_counts(const uint64_t *begin, const uint16_t *key, const
 
 int rbgpu_set_range_counts(const rbgpu_set *s, const uint32_t *members, uint32_t n, uint32_t key_lo, uint32_t key_hi,
                            uint64_t *out) {
+  SETTLE(s);
   if (!s || (n && !out)) return fail(RB_EINVAL, "null argument");
   if (key_lo > key_hi || key_hi > 65536u) return fail(RB_EINVAL, "key range [%u, %u) outside [0, 65536]", key_lo, key_hi);
   if (!members && n != s->nb) return fail(RB_EINVAL, "without a member list n must be the bitmap count");
@@ -831,6 +834,7 @@ int rbgpu_set_range_counts(const rbgpu_set *s, const uint32_t *members, uint32_t
 }
 
 int rbgpu_set_key_bytes(const rbgpu_set *s, uint64_t *out) {
+  SETTLE(s);
   if (!s || !out) return fail(RB_EINVAL, "null argument");
   int rc = check_ctx(s->ctx);
   if (rc) return rc;
@@ -854,6 +858,7 @@ int rbgpu_set_key_bytes(const rbgpu_set *s, uint64_t *out) {
 
 int rbgpu_set_serialize(const rbgpu_set *s, uint32_t first, uint32_t count, uint8_t *dst, uint64_t cap,
                         uint64_t *offsets) {
+  SETTLE(s);
   if (!s || (count && !dst)) return fail(RB_EINVAL, "null argument");
   if ((uint64_t)first + count > s->nb) return fail(RB_EINVAL, "bitmap range out of bounds");
   int rc = check_ctx(s->ctx);
@@ -876,6 +881,7 @@ int rbgpu_set_serialize(const rbgpu_set *s, uint32_t first, uint32_t count, uint
 
 int rbgpu_set_serialize_device(const rbgpu_set *s, uint32_t first, uint32_t count, uint8_t *d_dst, uint64_t cap,
                                uint64_t *offsets) {
+  SETTLE(s);
   if (!s || (count && !d_dst)) return fail(RB_EINVAL, "null argument");
   if ((uint64_t)first + count > s->nb) return fail(RB_EINVAL, "bitmap range out of bounds");
   int rc = check_ctx(s->ctx);
@@ -1050,9 +1056,13 @@ static // tasks bound up to which pairwise_impl reserves the task workspace befo
 // (58 B per task: 928 MiB at the cap)
 constexpr uint64_t kEarlyEmitTasks = 1ull << 24;
 
+// async: return once the task kernels and the compaction are enqueued (rbgpu_pairwise_async): the result
+// is pending (settle() fills its container count), the call's counters are not read back (rb_stats keeps
+// the last synchronous call's), and `ext` (if any, another stream of the caller) is ordered around the call.
 int pairwise_impl(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu_set *b, const uint32_t *a_idx,
                          const uint32_t *b_idx, uint32_t npairs, rbgpu_set **out, uint64_t *card_out,
-                         int probe = 0, bool inplace = false, bool keep_empty = false) {
+                         int probe = 0, bool inplace = false, bool keep_empty = false, bool async = false,
+                         hipStream_t ext = nullptr) {
   int rc = check_ctx(ctx);
   if (rc) return rc;
   if ((op < RB_AND || op > RB_ANDNOT) && !is_lazy_op(op)) return fail(RB_EINVAL, "bad op %d", op);
@@ -1064,9 +1074,33 @@ int pairwise_impl(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu_set *b
     if (a_idx[i] >= a->nb && a_idx[i] != kEmptyBitmap) return fail(RB_EINVAL, "a_idx[%u] out of range", i);
   for (uint32_t i = 0; b_idx && i < npairs; ++i)
     if (b_idx[i] >= b->nb && b_idx[i] != kEmptyBitmap) return fail(RB_EINVAL, "b_idx[%u] out of range", i);
-  if (!probe) {
+  if (ext == ctx->stream) ext = nullptr;
+  if (ext) { // the caller's earlier work on its stream comes first
+    HIPCHK(hipEventRecord(ctx->ev_ext, ext));
+    HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_ext, 0));
+  }
+  if (!probe) { // small batches complete before the return, asynchronous call or not
     rc = pairwise_small(ctx, op, a, b, a_idx, b_idx, npairs, out, card_out, inplace, keep_empty);
     if (rc != 1) return rc;
+  }
+  int slot = -1;
+  struct SlotGuard { // an error return gives the slot back
+    rbgpu_ctx *c;
+    int &slot;
+    ~SlotGuard() {
+      if (slot >= 0) c->async_free.push_back(slot);
+    }
+  } slot_guard{ctx, slot};
+  if (async && out) { // a pinned word for the result count; none free: the call completes synchronously
+    if (!ctx->h_async) {
+      if (hipHostMalloc((void **)&ctx->h_async, kAsyncSlots * sizeof(uint64_t)) != hipSuccess)
+        return fail(RB_ENOMEM, "pinned result-count slots");
+      for (int i = kAsyncSlots - 1; i >= 0; --i) ctx->async_free.push_back(i);
+    }
+    if (!ctx->async_free.empty()) {
+      slot = ctx->async_free.back();
+      ctx->async_free.pop_back();
+    }
   }
   const bool card_only = out == nullptr;
   const int kop = is_lazy_op(op) ? (int)RB_OR : op; // the kernels' op (lazy roles run as OR, TaskMeta::lazy)
@@ -1234,7 +1268,10 @@ int pairwise_impl(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu_set *b
   }
   // the light and heavy task kernels run concurrently (heavy on the side stream, 1 block per CU;
   // light 2 blocks per CU: 2 x 128 + 256 VGPRs per SIMD)
-  const bool conc = !probe && nlight && nheavy && nlight + nheavy >= 65536; // small batches: the
+#ifndef RBG_FORCE_SERIAL
+#define RBG_FORCE_SERIAL 0 // study: light then heavy on one stream (each kernel's standalone time)
+#endif
+  const bool conc = !RBG_FORCE_SERIAL && !probe && nlight && nheavy && nlight + nheavy >= 65536; // small batches: the
                                                   // cross-stream waits cost more than the overlap
   // the emit zeroes the queue counters before ev[1]: the side stream waits on ev[1] before its light launch
   if (!early)
@@ -1286,6 +1323,28 @@ int pairwise_impl(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu_set *b
   if (res && np && !ident_segs) launch_pair_rbegin(seg_begin, npairs, rseg, res->begin, nullptr, st);
   else if (res && !np) HIPCHK(hipMemsetAsync(res->begin, 0, 8, st));
   if (card_out && np) HIPCHK(hipMemcpyAsync(card_out, pcard, np * 8, hipMemcpyDeviceToHost, st));
+  if (slot >= 0) {
+    // the result count (stats word 8, written by the compaction's scan) into the pinned slot, the
+    // counters zeroed for the next call, and the completion event the result settles on
+    const int prc = np ? (hipMemcpyAsync(ctx->h_async + slot, ctx->d_stats + 8 * kStripes, 8, hipMemcpyDeviceToHost, st)
+                              ? RB_EDEVICE : RB_OK)
+                       : (ctx->h_async[slot] = 0, RB_OK);
+    hipEvent_t done = nullptr;
+    if (prc || hipMemsetAsync(ctx->d_stats, 0, kStatWords * kStripes * sizeof(uint64_t), st) ||
+        hipEventCreateWithFlags(&done, hipEventDisableTiming) || hipEventRecord(done, st) ||
+        (ext && hipStreamWaitEvent(ext, done, 0)) || hipGetLastError()) {
+      if (done) (void)hipEventDestroy(done);
+      (void)hipStreamSynchronize(st);
+      rbgpu_set_free(res);
+      return fail(RB_EDEVICE, "asynchronous pairwise: enqueue failed");
+    }
+    ctx->stats_clean = true;
+    res->pending = done;
+    res->pend_slot = slot;
+    slot = -1; // the result owns it now
+    *out = res;
+    return RB_OK;
+  }
   if (conc) {
     // [0] the concurrent task phase (both kernels' bytes over the union of their spans), then each
     const KernelSpan spans[3] = {{"k_pair_tasks<light>||<heavy>", 2, 4, ntasks, ctx->ev[1], ctx->ev[3], 3, 5},
@@ -1303,6 +1362,10 @@ int pairwise_impl(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu_set *b
     res->nc = nres;
     *out = res;
   }
+  if (ext) { // the caller's later work on its stream comes after this call's
+    HIPCHK(hipEventRecord(ctx->ev_ext, ctx->stream));
+    HIPCHK(hipStreamWaitEvent(ext, ctx->ev_ext, 0));
+  }
   return RB_OK;
 }
 
@@ -1312,6 +1375,7 @@ static double us_since(std::chrono::steady_clock::time_point t0) {
 
 int rbgpu_pairwise(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu_set *b, const uint32_t *a_idx,
                    const uint32_t *b_idx, uint32_t npairs, rbgpu_set **out) {
+  SETTLE(a, b);
   const auto t0 = std::chrono::steady_clock::now();
   if (!out) return fail(RB_EINVAL, "null out");
   *out = nullptr;
@@ -1320,8 +1384,23 @@ int rbgpu_pairwise(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu_set *
   return rc;
 }
 
+int rbgpu_pairwise_async(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu_set *b, const uint32_t *a_idx,
+                         const uint32_t *b_idx, uint32_t npairs, void *stream, rbgpu_set **out) {
+  SETTLE(a, b);
+  if (!out) return fail(RB_EINVAL, "null out");
+  *out = nullptr;
+  return pairwise_impl(ctx, op, a, b, a_idx, b_idx, npairs, out, nullptr, 0, false, false, true,
+                       reinterpret_cast<hipStream_t>(stream));
+}
+
+int rbgpu_set_wait(const rbgpu_set *s) {
+  if (!s) return fail(RB_EINVAL, "null argument");
+  return settle(s);
+}
+
 int rbgpu_pairwise_cardinality(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu_set *b, const uint32_t *a_idx,
                                const uint32_t *b_idx, uint32_t npairs, uint64_t *out) {
+  SETTLE(a, b);
   const auto t0 = std::chrono::steady_clock::now();
   if (!out && npairs) return fail(RB_EINVAL, "null out");
   const int rc = pairwise_impl(ctx, op, a, b, a_idx, b_idx, npairs, nullptr, out);
@@ -1340,6 +1419,7 @@ int pairwise_call(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu_set *b
 extern "C" {
 
 int rbgpu_set_run_optimize(const rbgpu_set *in, rbgpu_set **out, uint8_t *any_run) {
+  SETTLE(in);
   if (!in || !out) return fail(RB_EINVAL, "null argument");
   *out = nullptr;
   rbgpu_ctx *ctx = in->ctx;
@@ -1384,6 +1464,7 @@ int rbgpu_set_run_optimize(const rbgpu_set *in, rbgpu_set **out, uint8_t *any_ru
 
 int rbgpu_pairwise_inplace(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu_set *b, const uint32_t *a_idx,
                            const uint32_t *b_idx, uint32_t npairs, rbgpu_set **out) {
+  SETTLE(a, b);
   const auto t0 = std::chrono::steady_clock::now();
   if (!out) return fail(RB_EINVAL, "null out");
   *out = nullptr;
@@ -1397,6 +1478,7 @@ int rbgpu_pairwise_inplace(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbg
 // in place of the task kernel (mode 1: the task kernel's payload loads; 2: a streaming read of
 // a's arena).  The probe's time is in rbgpu_get_stats().main_kernel_ms.
 int rbgpu_internal_probe(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu_set *b, uint32_t npairs, int mode) {
+  SETTLE(a, b);
   if (mode != 1 && mode != 2) return fail(RB_EINVAL, "probe mode");
   rbgpu_set *res = nullptr;
   return pairwise_impl(ctx, op, a, b, nullptr, nullptr, npairs, &res, nullptr, mode);
@@ -1597,6 +1679,7 @@ int rbgpu_wide(rbgpu_ctx *ctx, int sem, const rbgpu_set *in, const uint32_t *mem
 
 int rbgpu_wide_keys(rbgpu_ctx *ctx, int sem, const rbgpu_set *in, const uint32_t *members, uint32_t n,
                     uint32_t key_lo, uint32_t key_hi, rbgpu_set **out) {
+  SETTLE(in);
   if (!out) return fail(RB_EINVAL, "null out");
   if (key_lo > key_hi || key_hi > 65536) return fail(RB_EINVAL, "bad key range [%u, %u)", key_lo, key_hi);
   *out = nullptr;
@@ -1631,6 +1714,7 @@ int rbgpu_wide_keys(rbgpu_ctx *ctx, int sem, const rbgpu_set *in, const uint32_t
 
 int rbgpu_wide_cardinality(rbgpu_ctx *ctx, int op, const rbgpu_set *in, const uint32_t *members, uint32_t n,
                            uint64_t *out) {
+  SETTLE(in);
   if (!out) return fail(RB_EINVAL, "null out");
   if (op != RB_AND && op != RB_OR) return fail(RB_EINVAL, "wide cardinality supports AND and OR");
   rbgpu_set *r = nullptr;
@@ -1645,6 +1729,7 @@ int rbgpu_wide_cardinality(rbgpu_ctx *ctx, int op, const rbgpu_set *in, const ui
 int rbgpu_bsi_compare_keys(rbgpu_ctx *ctx, const rbgpu_set *bsi, int op, uint64_t start_or_value, uint64_t end,
                            uint64_t min_value, uint64_t max_value, const rbgpu_set *found, uint32_t key_lo,
                            uint32_t key_hi, rbgpu_set **out) {
+  SETTLE(bsi, found);
   if (!out) return fail(RB_EINVAL, "null out");
   *out = nullptr;
   int rc = check_ctx(ctx);
@@ -1672,6 +1757,7 @@ int rbgpu_set_setup_stats(const rbgpu_set *s, double *ms, uint64_t *bytes) {
 }
 
 int rbgpu_set_extract(const rbgpu_set *s, uint32_t first, uint32_t count, rbgpu_set **out) {
+  SETTLE(s);
   if (!s || !out) return fail(RB_EINVAL, "null argument");
   *out = nullptr;
   if ((uint64_t)first + count > s->nb) return fail(RB_EINVAL, "bitmap range out of bounds");

@@ -701,6 +701,7 @@ int rbgpu_comm_allreduce_sum(rbgpu_comm *c, uint64_t *values, uint32_t n) {
 }
 
 int rbgpu_shard_summarize(rbgpu_comm *c, const rbgpu_set *local, rb_shard_summary *out) {
+  SETTLE(local);
   if (!c || !out) return fail(RB_EINVAL, "null argument");
   int local_rc = need_device(c);
   if (!local_rc && !local) local_rc = fail(RB_EINVAL, "null argument");
@@ -793,6 +794,7 @@ int rbgpu_bsi_compare_sharded(rbgpu_comm *c, const rbgpu_set *bsi, int op, uint6
 
 int rbgpu_shard_gather_serialized(rbgpu_comm *c, const rbgpu_set *local, const rb_shard_summary *summary, int root,
                                   uint8_t *d_dst, uint64_t cap) {
+  SETTLE(local);
   if (!c || !summary) return fail(RB_EINVAL, "null argument");
   if (root < 0 || root >= c->nranks) return fail(RB_EINVAL, "bad root %d", root); // the same on every rank
   // a bad argument on one rank is exchanged with the lengths, so every rank fails together instead of

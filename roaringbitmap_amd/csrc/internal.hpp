@@ -143,6 +143,7 @@ struct rbgpu_ctx {
   hipStream_t side = nullptr; // second stream: the heavy task kernel runs beside the light one
   hipEvent_t ev[6] = {};   // [0] call start, [1..n] around the compute kernels, [5] call end
   hipEvent_t ev_side[3] = {}; // around the kernel on `side`; [2] after the side stream's last launch
+  hipEvent_t ev_ext = {};     // ordering against a caller's stream (the asynchronous entry points)
   hipEvent_t ev_tot = {};     // pairwise: after the read-back of the scan totals (the early emit runs past it)
   rbg::DevPool pool;
   rbg::Workspace ws_pairs, ws_tasks, ws_segs; // per pair / per task / per merge-path segment
@@ -160,6 +161,9 @@ struct rbgpu_ctx {
   int refs = 1;                 // the handle + one per live set; destroyed at zero
   bool closed = false;
   bool stats_clean = false; // d_stats zeroed after the last read-back (stats_begin / stats_end)
+  // pinned words the asynchronous calls' result counts land in (kAsyncSlots, a free list)
+  uint64_t *h_async = nullptr; // [kAsyncSlots]
+  std::vector<int> async_free;
 };
 
 struct rbgpu_set {
@@ -185,10 +189,10 @@ struct rbgpu_set {
   int64_t dense_lo = -2, dense_hi = -2;
   uint64_t *mrec = nullptr;
   uint64_t *krec = nullptr;
-  //   kslots               dense sets only: each krec container's run list (<= 8 runs) as two 16-B halves,
-  //                        kslots[i] runs 0..3 and kslots[nc + i] runs 4..7, key-major like krec, so a wave
-  //                        reading one key's members reads them contiguously (naive_xor's fast path)
-  uint4 *kslots = nullptr;
+  // rbgpu_pairwise_async: the call's work is still running; `nc` arrives in the context's pinned slot
+  // `pend_slot` when `pending` completes (settle() waits for it and fills nc)
+  hipEvent_t pending = nullptr;
+  int pend_slot = -1;
   double derive_ms = 0.0;         // device time spent building mrec / krec (reported, not hidden)
   uint64_t derive_bytes = 0;      // their algorithmic bytes (metadata read + records written)
   rbg::SetView view() const { return rbg::SetView{begin, key, type, card, nruns, off, payload}; }
@@ -203,13 +207,21 @@ int pairwise_call(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu_set *b
 void ctx_unref(rbgpu_ctx *ctx);
 void set_release(rbgpu_set *s);
 int ensure_h_begin(const rbgpu_set *s);
+// A set returned by rbgpu_pairwise_async is usable by the host once its work is done: every entry point
+// that reads a set first settles it (waits, fills nc).  A no-op for every other set.
+int settle(const rbgpu_set *s);
+constexpr int kAsyncSlots = 256; // asynchronous results pending at once per context (more: complete synchronously)
+#define SETTLE(...)                                                                                    \
+  do {                                                                                                 \
+    for (const rbgpu_set *settle_s_ : {__VA_ARGS__})                                                   \
+      if (const int settle_rc_ = ::rbg::settle(settle_s_)) return settle_rc_;                           \
+  } while (0)
 int ensure_max_keys(const rbgpu_set *s);
 int ensure_max_runs(const rbgpu_set *s);
 // derived metadata of an immutable set (see rbgpu_set): computed once, then cached
 int ensure_dense(const rbgpu_set *s);
 int ensure_mrec(const rbgpu_set *s);
 int ensure_krec(const rbgpu_set *s); // needs a dense set (dense_lo >= 0)
-int ensure_kslots(const rbgpu_set *s); // needs krec
 // call accounting: zero the byte counters + record the start event / read everything back
 // zero = false: the caller's counters come zeroed some other way (the small-batch path's H2D copy)
 void stats_begin(rbgpu_ctx *ctx, bool zero = true);

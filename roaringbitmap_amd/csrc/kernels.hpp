@@ -185,11 +185,7 @@ struct XorRecords {
   Build build;
   const uint64_t *mrec, *mbase;
   uint32_t M, key_lo, key_hi;
-  const uint4 *slots = nullptr; // kCached only: the set's key-major run slots at rec's first index
-  uint64_t slots_half = 0;      // the set's nc: runs 4..7 of index i at slots[slots_half + i]
 };
-void launch_run_slots(const uint8_t *payload, uint64_t payload_bytes, const uint64_t *krec, uint64_t n, uint4 *slots,
-                      hipStream_t st);
 void launch_records_transpose(const uint64_t *mrec, const uint64_t *mbase, uint32_t M, uint32_t key_lo,
                               uint32_t key_hi, uint64_t *rec, hipStream_t st);
 void launch_wide_runs_xor(const SetView &s, const uint32_t *cid, const uint64_t *seg, const uint32_t *klist,

@@ -231,6 +231,7 @@ int rbgpu_set64_from_portable(rbgpu_ctx *ctx, const uint8_t *const *bufs, const 
 
 int rbgpu_set64_from_buckets(const rbgpu_set *buckets, const uint32_t *highs, const uint64_t *begin, uint32_t n,
                              rbgpu_set64 **out) {
+  SETTLE(buckets);
   if (!buckets || !out || !begin || (begin[n] && !highs)) return fail(RB_EINVAL, "null argument");
   *out = nullptr;
   if (begin[0] != 0 || begin[n] != buckets->nb) return fail(RB_EINVAL, "begin must cover the bucket set");

@@ -18,10 +18,6 @@
 #include "kernels.hpp"
 #include "wave.hpp"
 
-#ifndef RBG_XSLOTS
-#define RBG_XSLOTS 1 // study builds: 0 = naive_xor's fast path reads the runs through the payload arena
-#endif
-
 namespace rbg {
 
 
@@ -672,8 +668,7 @@ int wide_run(rbgpu_ctx *ctx, int sem, const rbgpu_set *in, const std::vector<uin
     // workShyAnd / naive_xor fast paths read packed records; naive_xor's key-major ones for a dense set
     // in set order are the set's cached krec
     if (in->payload_bytes >= kRecMaxPayload || ensure_mrec(in)) fast_ok = false;
-    else if (sem == RB_FAST_XOR && dense && identity && (ensure_krec(in) || (RBG_XSLOTS && ensure_kslots(in))))
-      fast_ok = false;
+    else if (sem == RB_FAST_XOR && dense && identity && ensure_krec(in)) fast_ok = false;
   }
   (void)hipGetLastError();
 
@@ -785,8 +780,6 @@ int wide_run(rbgpu_ctx *ctx, int sem, const rbgpu_set *in, const std::vector<uin
     if (dense && identity) {
       xr.rec = in->krec + (uint64_t)(key_lo - in->dense_lo) * in->nb;
       xr.build = XorRecords::kCached;
-      xr.slots = RBG_XSLOTS ? in->kslots + (uint64_t)(key_lo - in->dense_lo) * in->nb : nullptr;
-      xr.slots_half = in->nc;
     } else {
       if (pool.alloc((void **)&d_rec, std::max<uint64_t>(N, 1) * 8)) fast_ok = false;
       xr.rec = d_rec;

@@ -179,37 +179,6 @@ void launch_records_transpose(const uint64_t *mrec, const uint64_t *mbase, uint3
                                                                                       key_hi, rec);
 }
 
-// Key-major run slots (rbgpu_set::kslots): for each krec index i, runs 0..3 of its container at
-// slots[i] and runs 4..7 at slots[n + i] (zeros past nruns; containers that are not Runs of <= 8 runs
-// leave zeros and are routed by their record).  The payload arena is member-major, so the 64 members of
-// one key a window reads sat on 64 different lines, each shared with the member's neighbouring keys:
-// every line came through L2 about four times (PMC r03: 248M L2 requests per launch, 69 % hits, L2 98 %
-// busy).  In slot order a window's runs are two coalesced 1 KiB reads.
-__global__ __launch_bounds__(256) void k_run_slots(const uint8_t *__restrict__ payload, uint64_t payload_bytes,
-                                                   const uint64_t *__restrict__ krec, uint64_t n,
-                                                   uint4 *__restrict__ slots) {
-  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
-    const uint64_t r = krec[i];
-    const uint32_t typ = rec_type(r), nr = rec_nruns(r);
-    const uint64_t off = rec_off(r);
-    uint32_t w[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    if (typ == kRun && nr >= 1 && nr <= 8 && off + 4ull * nr <= payload_bytes) {
-      const uint32_t *p = reinterpret_cast<const uint32_t *>(payload + off);
-#pragma unroll
-      for (int u = 0; u < 8; ++u)
-        if ((uint32_t)u < nr) w[u] = p[u];
-    }
-    slots[i] = make_uint4(w[0], w[1], w[2], w[3]);
-    slots[n + i] = make_uint4(w[4], w[5], w[6], w[7]);
-  }
-}
-void launch_run_slots(const uint8_t *payload, uint64_t payload_bytes, const uint64_t *krec, uint64_t n, uint4 *slots,
-                      hipStream_t st) {
-  if (!n) return;
-  k_run_slots<<<(unsigned)std::min<uint64_t>((n + 255) / 256, 65536), 256, 0, st>>>(payload, payload_bytes, krec, n,
-                                                                                   slots);
-}
-
 // Members grouped by the counting sort: a gather of the packed records through the container ids (the
 // grouped count, seg[65536], can be less than the members' containers when the call is a key-range shard).
 __global__ __launch_bounds__(256) void k_records_gather(const uint64_t *__restrict__ mrec,
@@ -226,14 +195,8 @@ struct XBatch {
   uint32_t card, nr, typ;
   uint4 r; // runs 4h .. 4h+3 of the lane's container
 };
-// Where a window's run lists come from: the set's key-major slots (index i of the records) or, without
-// them, the payload arena through each record's offset.
-struct XSlots {
-  const uint4 *s0;
-  uint64_t half;
-};
-__device__ __forceinline__ XBatch load_xbatch(const SetView &s, const uint64_t *rec, const XSlots &xs, uint64_t i,
-                                              uint64_t hi, int h) {
+__device__ __forceinline__ XBatch load_xbatch(const SetView &s, const uint64_t *rec, uint64_t i, uint64_t hi,
+                                              int h) {
   XBatch b;
   b.card = 0;
   b.nr = 0;
@@ -245,7 +208,7 @@ __device__ __forceinline__ XBatch load_xbatch(const SetView &s, const uint64_t *
     b.card = rec_card(r);
     b.nr = rec_nruns(r);
     if (b.typ == kRun && b.nr <= 8 && b.nr > (uint32_t)(4 * h))
-      b.r = xs.s0 ? xs.s0[(h ? xs.half : 0) + i] : reinterpret_cast<const uint4 *>(s.payload + rec_off(r))[h];
+      b.r = reinterpret_cast<const uint4 *>(s.payload + rec_off(r))[h];
   }
   return b;
 }
@@ -269,14 +232,14 @@ struct XState {
 // One exact batch of <= 32 containers starting at `base` (the accumulator P is the LDS bitmap `acc`):
 // every step's (c_j, r_j) from the sorted run boundaries, the type maps composed, P updated.  Returns
 // false when a container of the batch does not qualify (the key goes to the generic kernel).
-__device__ __forceinline__ bool exact_batch(const SetView &s, const uint64_t *rec, const XSlots &xs, uint64_t base,
-                                            uint64_t hi, uint32_t *acc, uint32_t *R, int lane, XState &X) {
+__device__ __forceinline__ bool exact_batch(const SetView &s, const uint64_t *rec, uint64_t base, uint64_t hi,
+                                            uint32_t *acc, uint32_t *R, int lane, XState &X) {
   uint16_t *R16 = reinterpret_cast<uint16_t *>(R);
   uint16_t *pos = R16 + 2048;                       // [512] sorted position | tie/boundary bit 15
   uint2 *MC = reinterpret_cast<uint2 *>(R);         // [512] (coverage mask, c0 | c1 << 16)
   const int cj = lane >> 1, h = lane & 1;
   const uint32_t below = (1u << cj) - 1u;
-  const XBatch cur = load_xbatch(s, rec, xs, base + cj, hi, h);
+  const XBatch cur = load_xbatch(s, rec, base + cj, hi, h);
   const bool valid = base + (uint64_t)cj < hi;
   const bool bad = valid && (cur.typ != kRun || cur.nr > 8u || cur.card >= (uint32_t)kSpan);
   if (__ballot(bad)) return false;
@@ -527,37 +490,29 @@ __device__ __forceinline__ XMeta xmeta_of(uint64_t r, bool valid) {
   m.off = valid ? rec_off(r) : 0ull;
   return m;
 }
-// the two 16-B halves of member i's run list (i: a valid, clamped record index)
-__device__ __forceinline__ void run_halves(const SetView &s, const XSlots &xs, const XMeta &m, uint64_t i,
-                                           const uint8_t *&p0, const uint8_t *&p1) {
-  const bool runs = m.typ == kRun && m.nr && m.nr <= 8u;
-  // a non-Run (or invalid) member reads the arena's first 16 B instead; runs 4..7 exist only if nr > 4
-  const uint8_t *p = s.payload + (runs ? m.off : 0ull);
-  p0 = xs.s0 ? reinterpret_cast<const uint8_t *>(xs.s0 + i) : p;
-  p1 = xs.s0 ? reinterpret_cast<const uint8_t *>(xs.s0 + xs.half + i) : p + (runs && m.nr > 4u ? 16 : 0);
-}
-__device__ __forceinline__ XWin xwin_from(const SetView &s, const XSlots &xs, const XMeta &m, uint64_t i) {
+__device__ __forceinline__ XWin xwin_from(const SetView &s, const XMeta &m) {
   XWin w;
   w.typ = m.typ;
   w.card = m.card;
   w.nr = m.nr;
-  const uint8_t *p0, *p1;
-  run_halves(s, xs, m, i, p0, p1);
+  const bool runs = m.typ == kRun && m.nr && m.nr <= 8u;
+  // a non-Run (or invalid) member reads the arena's first 16 B instead; runs 4..7 exist only if nr > 4
+  const uint4 *p = reinterpret_cast<const uint4 *>(s.payload + (runs ? m.off : 0ull));
   // raw loaded values, no select on them: a select right behind the loads would make the wave wait
   // for them here, a window early (r03: every window paid the full memory latency).  Only runs u < nr
   // are ever read, and a lane whose container is not a Run of <= 8 runs routes the key first.
-  w.r0 = *reinterpret_cast<const uint4 *>(p0);
-  w.r1 = *reinterpret_cast<const uint4 *>(p1);
+  w.r0 = p[0];
+  w.r1 = p[runs && m.nr > 4u ? 1 : 0];
   w.pairx = 0;
   return w;
 }
 // the next window's runs, LDS-DMA into nb (lane-linear: r0 of lane l at nb[4l], r1 at nb[256 + 4l])
-__device__ __forceinline__ void stage_next_runs(const SetView &s, const XSlots &xs, const XMeta &m, uint64_t i,
-                                                uint32_t *nb) {
-  const uint8_t *p0, *p1;
-  run_halves(s, xs, m, i, p0, p1);
-  __builtin_amdgcn_global_load_lds((gbl_void_t *)p0, (lds_void_t *)nb, 16, 0, 0);
-  __builtin_amdgcn_global_load_lds((gbl_void_t *)p1, (lds_void_t *)(nb + 256), 16, 0, 0);
+__device__ __forceinline__ void stage_next_runs(const SetView &s, const XMeta &m, uint32_t *nb) {
+  const bool runs = m.typ == kRun && m.nr && m.nr <= 8u;
+  const uint8_t *p = s.payload + (runs ? m.off : 0ull);
+  __builtin_amdgcn_global_load_lds((gbl_void_t *)p, (lds_void_t *)nb, 16, 0, 0);
+  __builtin_amdgcn_global_load_lds((gbl_void_t *)(p + (runs && m.nr > 4u ? 16 : 0)), (lds_void_t *)(nb + 256), 16,
+                                   0, 0);
 }
 // the window staged by stage_next_runs (every load of the previous window waited for first)
 __device__ __forceinline__ XWin take_next(const XMeta &m, const uint32_t *nb, int lane) {
@@ -619,7 +574,7 @@ constexpr int kXorUnionMinC = 1024; // try a union stretch only above this c (a 
 #endif
 
 __global__ __launch_bounds__(256, 3) void k_wide_runs_xor(SetView s, const uint64_t *__restrict__ rec,
-                                                          XSlots xs, const uint64_t *__restrict__ seg,
+                                                          const uint64_t *__restrict__ seg,
                                                           const uint32_t *__restrict__ klist, uint32_t nk,
                                                           uint8_t *__restrict__ out, WideOut wo,
                                                           uint8_t *__restrict__ route, uint64_t *stats,
@@ -648,15 +603,14 @@ __global__ __launch_bounds__(256, 3) void k_wide_runs_xor(SetView s, const uint6
   XState X{3, 0, 0, 0u, 1};
   bool fail_route = false;
   uint64_t wbase = lo;
-  auto clamp = [&](uint64_t i) { return i < hi ? i : hi - 1; }; // hi > lo here
-  auto rec_at = [&](uint64_t i) { // unconditional load (clamped address, selected later)
-    return rec[clamp(i)];
+  auto rec_at = [&](uint64_t i) { // unconditional load (clamped address, selected later); hi > lo here
+    return rec[i < hi ? i : hi - 1];
   };
   const uint64_t r0 = rec_at(lo + lane), r1 = rec_at(lo + 64 + lane);
   uint32_t *nbuf = R + kNextRuns;
-  XWin W = xwin_from(s, xs, xmeta_of(r0, lo + lane < hi), clamp(lo + lane)); // window w
-  XMeta Nm = xmeta_of(r1, lo + 64 + lane < hi);                             // w+1: runs in flight into nbuf
-  stage_next_runs(s, xs, Nm, clamp(lo + 64 + lane), nbuf);
+  XWin W = xwin_from(s, xmeta_of(r0, lo + lane < hi));       // window w
+  XMeta Nm = xmeta_of(r1, lo + 64 + lane < hi);              // w+1: runs in flight into nbuf
+  stage_next_runs(s, Nm, nbuf);
   uint64_t NN = rec_at(lo + 128 + lane);                     // w+2: record in flight
   pair_xor(W);
   uint64_t base = lo;
@@ -855,14 +809,14 @@ __global__ __launch_bounds__(256, 3) void k_wide_runs_xor(SetView s, const uint6
         lds_write_words(acc, Pw, lane);
         __builtin_amdgcn_s_waitcnt(kWaitVm0); // the next window's runs land before the batch reuses R
         wave_lds_sync();
-        if (!exact_batch(s, rec, xs, base, hi, acc, R, lane, X)) {
+        if (!exact_batch(s, rec, base, hi, acc, R, lane, X)) {
           fail_route = true;
           break;
         }
         lds_read_words(acc, Pw, lane);
         wave_lds_sync();
         lds_zero(acc, lane);
-        stage_next_runs(s, xs, Nm, clamp(wbase + 64 + lane), nbuf); // the batch overwrote them: again
+        stage_next_runs(s, Nm, nbuf); // the batch overwrote them: again
         base += kXB;
         RBG_TR(++tr_e);
         RBG_TA(4);
@@ -874,7 +828,7 @@ __global__ __launch_bounds__(256, 3) void k_wide_runs_xor(SetView s, const uint6
       wbase += 64;
       W = take_next(Nm, nbuf, lane);
       Nm = xmeta_of(NN, wbase + 64 + lane < hi);
-      stage_next_runs(s, xs, Nm, clamp(wbase + 64 + lane), nbuf);
+      stage_next_runs(s, Nm, nbuf);
       NN = rec_at(wbase + 128 + lane);
       wpx = false;
     }
@@ -937,8 +891,7 @@ void launch_wide_runs_xor(const SetView &s, const uint32_t *cid, const uint64_t 
     k_records_gather<<<(unsigned)std::min<uint64_t>((xr.n + 255) / 256, 65536), 256, 0, st>>>(xr.mrec, cid, seg,
                                                                                            xr.rec);
   }
-  const XSlots xs{xr.build == XorRecords::kCached ? xr.slots : nullptr, xr.slots_half};
-  k_wide_runs_xor<<<(nk + 3) / 4, 256, 0, st>>>(s, xr.rec, xs, seg, klist, nk, out, wo, route, stats, fastfwd);
+  k_wide_runs_xor<<<(nk + 3) / 4, 256, 0, st>>>(s, xr.rec, seg, klist, nk, out, wo, route, stats, fastfwd);
 }
 
 } // namespace rbg

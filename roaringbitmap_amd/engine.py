@@ -279,6 +279,11 @@ class DeviceSet:
                                                     offs.ctypes.data_as(L._U64P)))
         return offs
 
+    def wait(self) -> "DeviceSet":
+        """rbgpu_set_wait: an asynchronous result complete (no-op otherwise)."""
+        L.check(L.lib().rbgpu_set_wait(self.h))
+        return self
+
     def setup_stats(self) -> dict:
         """rbgpu_set_setup_stats: device ms and algorithmic bytes of the derived per-set metadata so far."""
         ms, b = C.c_double(), C.c_uint64()
@@ -472,6 +477,18 @@ class Context:
         out = C.c_void_p()
         L.check(L.lib().rbgpu_pairwise64(self.h, flavor, op, 1 if inplace else 0, a.h, b.h, ap, bp, n, C.byref(out)))
         return DeviceSet64(self, out.value)
+
+    def pairwise_async(self, op: int, a: DeviceSet, b: DeviceSet, a_idx=None, b_idx=None, npairs=None,
+                       stream: int = 0) -> DeviceSet:
+        """rbgpu_pairwise_async: returns once the work is enqueued (stream: a hipStream_t address, 0 = the
+        context's own); the result settles on first use or DeviceSet.wait()."""
+        ai, ap = _idx_addr(a_idx)
+        bi, bp = _idx_addr(b_idx)
+        n = npairs if npairs is not None else (len(ai) if ai is not None else min(len(a), len(b)))
+        out = C.c_void_p()
+        L.check(L.lib().rbgpu_pairwise_async(self.h, op, a.h, b.h, ap, bp, n, C.c_void_p(stream or None),
+                                             C.byref(out)))
+        return DeviceSet(self, out.value)
 
     def pairwise_inplace(self, op: int, a: DeviceSet, b: DeviceSet, a_idx=None, b_idx=None,
                          npairs=None) -> DeviceSet:
