@@ -194,6 +194,13 @@ def lib():
             raise ImportError(
                 f"{LIB_PATH} is missing: build the HIP extension first "
                 "(python -c 'import __graft_entry__ as g; g.build()')")
+        # One HIP runtime per process: torch ships its own libamdhip64 under the same soname, and
+        # whichever loads first serves both.  Loading torch's first keeps torch.cuda usable beside the
+        # library (the reverse order leaves torch reporting "No HIP GPUs are available").
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         L = C.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
             fn = getattr(L, name)

@@ -526,13 +526,6 @@ __device__ __forceinline__ RecU load_rec(const TaskRec *r) {
 #define RBG_HEAVY_NOPF 0 // study: register-path tasks without the one-task prefetch, at 128 VGPRs, so three
                          // light waves fit beside each heavy one on a SIMD
 #endif
-// The lean register path (AND): a Run second operand is turned into words in LDS and applied from there
-// (no second 16-word register image), so the wave fits 128 VGPRs and three light waves share each SIMD with
-// it — the light tasks, which dominate AND, run on 12 waves per CU beside the heavy ones instead of 8.
-#ifndef RBG_LEAN
-#define RBG_LEAN 1 // study builds: 0 = the AND register path at 256 VGPRs, two light waves per SIMD beside it
-#endif
-template <int OP> constexpr bool kLeanHeavy = RBG_LEAN && OP == RB_AND;
 constexpr int kLightWaves = 4; // waves per SIMD of the copy + filter kernel (128 VGPRs)
 constexpr int kHeavyWaves = RBG_HEAVY_NOPF ? 4 : 2; // waves per SIMD the register-path kernel is allocated for
 constexpr bool kHeavyPrefetch = !RBG_HEAVY_NOPF;    // the next task's payloads in flight during this one's emission
@@ -770,7 +763,7 @@ __device__ __forceinline__ Chunk claim_chunk(unsigned long long *queue, uint64_t
 //                   both next payloads, then classify and emit.
 enum { kRoleLight = 0, kRoleHeavy = 1 };
 template <int OP, bool CARD_ONLY, int ROLE>
-__global__ __launch_bounds__(256, ROLE == kRoleHeavy ? (kLeanHeavy<OP> ? 4 : kHeavyWaves) : kLightWaves) void k_pair_tasks(
+__global__ __launch_bounds__(256, ROLE == kRoleHeavy ? kHeavyWaves : kLightWaves) void k_pair_tasks(
     const uint8_t *__restrict__ pay_a, const uint8_t *__restrict__ pay_b, const TaskRec *__restrict__ recs,
     uint64_t n, uint8_t *__restrict__ out, TaskMeta tm, unsigned long long *queue) {
   __shared__ __attribute__((aligned(16))) uint32_t lds[4][2048];
@@ -782,9 +775,8 @@ __global__ __launch_bounds__(256, ROLE == kRoleHeavy ? (kLeanHeavy<OP> ? 4 : kHe
   // kQueueChunk consecutive tasks from a device counter shared by every launch on it (the
   // concurrent phase's second light launch fills the CUs the heavy kernel leaves), the next chunk
   // claimed one chunk ahead so the atomic's latency is hidden
-  const uint32_t wpb = blockDim.x >> 6; // waves per block (the concurrent heavy launch may use 2)
-  const uint64_t stride = (uint64_t)gridDim.x * wpb;
-  uint64_t g = (uint64_t)blockIdx.x * wpb + wv, cend = 0, nxt = 0, nend = 0;
+  const uint64_t stride = (uint64_t)gridDim.x * 4;
+  uint64_t g = (uint64_t)blockIdx.x * 4 + wv, cend = 0, nxt = 0, nend = 0;
   uint32_t qk = (uint32_t)(g % kQueueStripes), qtried = 0;
   if (queue) {
     const Chunk c0 = claim_chunk(queue, n, qk, qtried, lane);
@@ -810,7 +802,7 @@ __global__ __launch_bounds__(256, ROLE == kRoleHeavy ? (kLeanHeavy<OP> ? 4 : kHe
 #define RBG_HT(x)
 #endif
   load_chunks(pq, tc.pp, tc.bigp ? 16u : tc.pbytes, lane);
-  if (ROLE == kRoleHeavy && (!kHeavyPrefetch || kLeanHeavy<OP>)) {
+  if (ROLE == kRoleHeavy && !kHeavyPrefetch) {
   } else if (tc.kind == kCopy || tc.bigq) load_chunks(qq, tc.pp, 16, lane);
   else load_chunks(qq, tc.pq, tc.qbytes, lane);
   while (true) {
@@ -834,8 +826,6 @@ __global__ __launch_bounds__(256, ROLE == kRoleHeavy ? (kLeanHeavy<OP> ? 4 : kHe
     uint32_t nr = 0, cw = 0xFFFFFFFFu; // cw: the card word to store when it is not c (lazy marks)
     uint8_t *dst = out + cur.out;
     bool done = false;
-    if (ROLE == kRoleHeavy && kLeanHeavy<OP>) // the lean path prefetches P only: Q now, in flight during P's build
-      load_chunks(qq, tc.bigq ? tc.pp : tc.pq, tc.bigq ? 16u : tc.qbytes, lane);
     if (ROLE == kRoleHeavy && OP == RB_AND && tc.tp == kRun && tc.tq == kRun && !tc.bigp &&
         !tc.bigq && ((tc.rp + 3) & ~3u) + tc.rq <= 2048u) {
       int r = 0;
@@ -845,7 +835,7 @@ __global__ __launch_bounds__(256, ROLE == kRoleHeavy ? (kLeanHeavy<OP> ? 4 : kHe
         ty = c == 0 ? kEmpty : CARD_ONLY ? kArray : kRun;
         nr = ty == kRun ? (uint32_t)r : 0u;
         __builtin_amdgcn_sched_barrier(0);
-        if (!kLeanHeavy<OP>) {
+        {
           const bool real = has_next && !tn.bigq;
           load_chunks(qq, real ? tn.pq : tn.pp, real ? tn.qbytes : 16u, lane);
         }
@@ -894,7 +884,7 @@ __global__ __launch_bounds__(256, ROLE == kRoleHeavy ? (kLeanHeavy<OP> ? 4 : kHe
           word_op<OP>(w[2 * k], pack2(qq[k].x, qq[k].y));
           word_op<OP>(w[2 * k + 1], pack2(qq[k].z, qq[k].w));
         }
-      } else if (tc.tq == kRun && !tc.bigq && !kLeanHeavy<OP>) {
+      } else if (tc.tq == kRun && !tc.bigq) {
         stage_run_toggles(qq, tc.rq, s, lane);
         uint64_t t[kW];
         lds_read_words(s, t, lane);
@@ -919,7 +909,7 @@ __global__ __launch_bounds__(256, ROLE == kRoleHeavy ? (kLeanHeavy<OP> ? 4 : kHe
       RBG_HT(lt2 = __builtin_amdgcn_s_memtime(); lt_acc[1] += lt2 - lt1);
       __builtin_amdgcn_sched_barrier(0);
       if (kHeavyPrefetch) {
-        if (!kLeanHeavy<OP>) {
+        {
           const bool real = has_next && !tn.bigq;
           load_chunks(qq, real ? tn.pq : tn.pp, real ? tn.qbytes : 16u, lane);
         }
@@ -1258,16 +1248,12 @@ static void launch_tasks(const uint8_t *pa, const uint8_t *pb, const TaskRec *re
 #define RBG_LDS_PAD 0 // study: dynamic LDS a light block reserves without using it (occupancy sensitivity)
 #endif
   const size_t dyn = ROLE == kRoleLight ? RBG_LDS_PAD : 0;
-#ifndef RBG_HEAVY_THREADS
-#define RBG_HEAVY_THREADS 256 // study: threads per block of a concurrent heavy launch (128: two waves per CU)
-#endif
-  const unsigned threads = ROLE == kRoleHeavy && per_cu ? RBG_HEAVY_THREADS : 256;
   static unsigned occ_cap = 0; // occupancy-derived grid cap, per template instance
   if (!occ_cap) occ_cap = persistent_blocks(k_pair_tasks<OP, CARD_ONLY, ROLE>, ~0ull >> 8);
   const unsigned cap = per_cu ? std::min(occ_cap, per_cu * cu_count()) : occ_cap;
-  const uint64_t want = (n + threads / 64 - 1) / (threads / 64);
+  const uint64_t want = (n + 3) / 4;
   const unsigned blocks = (unsigned)(want < cap ? want : cap);
-  k_pair_tasks<OP, CARD_ONLY, ROLE><<<blocks, threads, dyn, st>>>(pa, pb, recs, n, out, tm, queue);
+  k_pair_tasks<OP, CARD_ONLY, ROLE><<<blocks, 256, dyn, st>>>(pa, pb, recs, n, out, tm, queue);
 }
 template <int OP>
 static void launch_op(bool card_only, const uint8_t *pa, const uint8_t *pb, const TaskRec *light, uint64_t nl,
@@ -1279,10 +1265,7 @@ static void launch_op(bool card_only, const uint8_t *pa, const uint8_t *pb, cons
   if (card_only) launch_tasks<OP, true, kRoleHeavy>(pa, pb, heavy, nh, out, tm, st);
   else launch_tasks<OP, false, kRoleHeavy>(pa, pb, heavy, nh, out, tm, st);
 }
-#ifndef RBG_CONC_LIGHT
-#define RBG_CONC_LIGHT 2
-#endif
-constexpr unsigned kConcLightPerCu = RBG_HEAVY_NOPF ? 3 : RBG_CONC_LIGHT; // light blocks per CU beside the heavy kernel (2 x 128 VGPRs per SIMD)
+constexpr unsigned kConcLightPerCu = RBG_HEAVY_NOPF ? 3 : 2; // light blocks per CU beside the heavy kernel (2 x 128 VGPRs per SIMD)
 constexpr unsigned kConcHeavyPerCu = 1; // heavy blocks per CU (256 VGPRs per SIMD)
 template <int OP>
 static void launch_op_concurrent(bool card_only, const uint8_t *pa, const uint8_t *pb, const TaskRec *light,
@@ -1294,19 +1277,17 @@ static void launch_op_concurrent(bool card_only, const uint8_t *pa, const uint8_
   // runs heavy then light, the library stream light then heavy, and a second launch of a kind
   // takes whatever tasks of that kind are left (AND: the light tasks dominate; OR / XOR: the heavy).
   unsigned long long *hq = queue ? queue + kHeavyQueueOffset : nullptr;
-  // a lean heavy wave (128 VGPRs) leaves three light waves per SIMD room, else two
-  const unsigned lpc = kLeanHeavy<OP> ? 3u : kConcLightPerCu;
   // heavy first: its blocks need the larger register slot
   (void)hipEventRecord(ev_h0, side);
   if (card_only) launch_tasks<OP, true, kRoleHeavy>(pa, pb, heavy, nh, out, tm, side, kConcHeavyPerCu, hq);
   else launch_tasks<OP, false, kRoleHeavy>(pa, pb, heavy, nh, out, tm, side, kConcHeavyPerCu, hq);
   (void)hipEventRecord(ev_h1, side);
-  if (card_only) launch_tasks<OP, true, kRoleLight>(pa, pb, light, nl, out, tm, st, lpc, queue);
-  else launch_tasks<OP, false, kRoleLight>(pa, pb, light, nl, out, tm, st, lpc, queue);
+  if (card_only) launch_tasks<OP, true, kRoleLight>(pa, pb, light, nl, out, tm, st, kConcLightPerCu, queue);
+  else launch_tasks<OP, false, kRoleLight>(pa, pb, light, nl, out, tm, st, kConcLightPerCu, queue);
   (void)hipEventRecord(light_done, st);
   if (queue) {
-    if (card_only) launch_tasks<OP, true, kRoleLight>(pa, pb, light, nl, out, tm, side, lpc, queue);
-    else launch_tasks<OP, false, kRoleLight>(pa, pb, light, nl, out, tm, side, lpc, queue);
+    if (card_only) launch_tasks<OP, true, kRoleLight>(pa, pb, light, nl, out, tm, side, kConcLightPerCu, queue);
+    else launch_tasks<OP, false, kRoleLight>(pa, pb, light, nl, out, tm, side, kConcLightPerCu, queue);
     if (card_only) launch_tasks<OP, true, kRoleHeavy>(pa, pb, heavy, nh, out, tm, st, kConcHeavyPerCu, hq);
     else launch_tasks<OP, false, kRoleHeavy>(pa, pb, heavy, nh, out, tm, st, kConcHeavyPerCu, hq);
   }
