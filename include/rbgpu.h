@@ -370,6 +370,19 @@ int rbgpu_set64_from_legacy(rbgpu_ctx *ctx, const uint8_t *const *bufs, const ui
 int rbgpu_set64_legacy_sizes(const rbgpu_set64 *set, uint64_t *out);
 int rbgpu_set64_serialize_legacy(const rbgpu_set64 *set, uint32_t first, uint32_t count, uint8_t *dst,
                                  uint64_t cap, uint64_t *offsets);
+/* Roaring64Bitmap.serialize / deserialize (longlong/Roaring64Bitmap.java:880-908 -> HighLowContainer
+ * .serialize / deserialize, longlong/HighLowContainer.java:230-254): an empty tag, the ART over the 6-byte
+ * high keys (art/Art.java:309-391, art/Node.java:326-400, Node4/16/48/256 and LeafNode bodies) and the
+ * Containers arrays (art/Containers.java:210-303), little-endian.  Ingest reads any tree and null-slot
+ * layout (a card-0 container — a kept-empty xor result — holds no value and is dropped); emit writes the
+ * canonical stream of the containers inserted in ascending key order (path-compressed tree, smallest node
+ * type per child count, container i at index i of one ArrayList-grown array).  Parity unpinned: the
+ * reference holds no fixture of this format. */
+int rbgpu_set64_from_art(rbgpu_ctx *ctx, const uint8_t *const *bufs, const uint64_t *lens, uint32_t n,
+                         rbgpu_set64 **out);
+int rbgpu_set64_art_sizes(const rbgpu_set64 *set, uint64_t *out);
+int rbgpu_set64_serialize_art(const rbgpu_set64 *set, uint32_t first, uint32_t count, uint8_t *dst,
+                              uint64_t cap, uint64_t *offsets);
 /* new Roaring64NavigableMap(signedLongs) for bitmap i: the order its two serializations write the buckets */
 int rbgpu_set64_set_signed_longs(rbgpu_set64 *set, uint32_t i, int signed_longs);
 int rbgpu_set64_get_signed_longs(const rbgpu_set64 *set, uint32_t i, int *signed_longs);

@@ -128,6 +128,9 @@ SIGNATURES = {
     "rbgpu_set64_from_legacy": (C.c_int, [_P, C.POINTER(C.c_char_p), _U64P, C.c_uint32, C.POINTER(_P)]),
     "rbgpu_set64_legacy_sizes": (C.c_int, [_P, _U64P]),
     "rbgpu_set64_serialize_legacy": (C.c_int, [_P, C.c_uint32, C.c_uint32, C.c_void_p, C.c_uint64, _U64P]),
+    "rbgpu_set64_from_art": (C.c_int, [_P, C.POINTER(C.c_char_p), _U64P, C.c_uint32, C.POINTER(_P)]),
+    "rbgpu_set64_art_sizes": (C.c_int, [_P, _U64P]),
+    "rbgpu_set64_serialize_art": (C.c_int, [_P, C.c_uint32, C.c_uint32, C.c_void_p, C.c_uint64, _U64P]),
     "rbgpu_set64_set_signed_longs": (C.c_int, [_P, C.c_uint32, C.c_int]),
     "rbgpu_set64_get_signed_longs": (C.c_int, [_P, C.c_uint32, C.POINTER(C.c_int)]),
     "rbgpu_pairwise64_cardinality": (C.c_int, [_P, C.c_int, _P, _P, _P, _P, C.c_uint32, _U64P]),

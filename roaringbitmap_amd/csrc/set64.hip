@@ -162,9 +162,331 @@ int bucket_pairs(const rbgpu_set64 *a, const rbgpu_set64 *b, int op, bool inplac
   return RB_OK;
 }
 
+// ---- Roaring64Bitmap.serialize: HighLowContainer = ART over the 6-byte high keys + Containers
+// (longlong/HighLowContainer.java:230-254, art/Art.java:309-391, art/Node*.java, art/Containers.java:210-303).
+// Little-endian fields (the writers reverse bytes around DataOutput), node type ordinals NODE4 / NODE16 /
+// NODE48 / NODE256 / LEAF_NODE = 0..4.  Parity unpinned: no reference fixture holds this format.
+constexpr uint8_t kArtLeaf = 4;
+constexpr uint32_t kArtBody[4] = {4, 16, 256, 32}; // Node4 int key, Node16 2 longs, Node48 childIndex, Node256 mask
+uint8_t key_byte(uint64_t k48, int d) { return (uint8_t)(k48 >> (8 * (5 - d))); }
+
+// Writes (dst != nullptr) or measures the canonical ART of the ascending keys: the path-compressed radix
+// tree with the smallest node type per child count — what inserting the keys with no removal builds
+// (Node4 / 16 / 48 grow at their 5th / 17th / 49th child: Node4.java:90-108, Node16.java:140-180,
+// Node48.java:180-200) — leaf i holding container index i; Node48 children in slots of key order.
+struct ArtOut {
+  uint8_t *dst;
+  uint64_t pos = 0;
+  void put(uint8_t b) {
+    if (dst) dst[pos] = b;
+    ++pos;
+  }
+  void put_le(uint64_t v, int n) {
+    for (int i = 0; i < n; ++i) put((uint8_t)(v >> (8 * i)));
+  }
+};
+void art_nodes(const std::vector<uint64_t> &k, size_t lo, size_t hi, int depth, ArtOut &o) {
+  if (hi - lo == 1) { // LeafNode (art/LeafNode.java:43-47): header (no prefix), key bytes, container index
+    o.put(kArtLeaf);
+    o.put_le(0, 2);
+    o.put(0);
+    for (int d = 0; d < 6; ++d) o.put(key_byte(k[lo], d));
+    o.put_le(lo, 8);
+    return;
+  }
+  int p = 0; // the keys' common bytes from `depth`: the node's compressed prefix
+  while (depth + p < 6 && key_byte(k[lo], depth + p) == key_byte(k[hi - 1], depth + p)) ++p;
+  const int d = depth + p;
+  std::vector<size_t> starts;
+  for (size_t i = lo; i < hi; ++i)
+    if (i == lo || key_byte(k[i], d) != key_byte(k[i - 1], d)) starts.push_back(i);
+  const size_t n = starts.size();
+  const uint8_t t = n <= 4 ? 0 : n <= 16 ? 1 : n <= 48 ? 2 : 3;
+  o.put(t); // Node.serializeHeader (art/Node.java:326-335): type, count (reversed short), prefix length, prefix
+  o.put_le(n, 2);
+  o.put((uint8_t)p);
+  for (int j = 0; j < p; ++j) o.put(key_byte(k[lo], depth + j));
+  uint8_t kb[256];
+  for (size_t c = 0; c < n; ++c) kb[c] = key_byte(k[starts[c]], d);
+  if (t == 0) { // Node4.key: child c's byte at bits (3 - c) * 8, written as reverseBytes
+    for (int c = 3; c >= 0; --c) o.put((size_t)c < n ? kb[c] : 0);
+  } else if (t == 1) { // Node16.firstV / secondV: bytes 0-7 / 8-15 big-endian, each long reversed
+    for (int h = 0; h < 2; ++h)
+      for (int c = 7; c >= 0; --c) o.put((size_t)(8 * h + c) < n ? kb[8 * h + c] : 0);
+  } else if (t == 2) { // Node48.childIndex: key byte -> child slot (0xFF empty), 8 keys per long, reversed
+    uint8_t ci[256];
+    std::memset(ci, 0xFF, sizeof ci);
+    for (size_t c = 0; c < n; ++c) ci[kb[c]] = (uint8_t)c;
+    for (int l = 0; l < 32; ++l)
+      for (int j = 7; j >= 0; --j) o.put(ci[8 * l + j]);
+  } else { // Node256.bitmapMask: bit k & 63 of long k >> 6, little endian
+    uint64_t m[4] = {0, 0, 0, 0};
+    for (size_t c = 0; c < n; ++c) m[kb[c] >> 6] |= 1ull << (kb[c] & 63);
+    for (int l = 0; l < 4; ++l) o.put_le(m[l], 8);
+  }
+  for (size_t c = 0; c < n; ++c) art_nodes(k, starts[c], c + 1 < n ? starts[c + 1] : hi, d + 1, o);
+}
+// Containers.grow from a 1-slot array (ArrayList growth: old + old / 2, at least the count)
+uint64_t art_capacity(uint64_t n) {
+  uint64_t cap = 1;
+  for (uint64_t m = 2; m <= n; ++m)
+    if (m > cap) cap = std::max(cap + (cap >> 1), m);
+  return cap;
+}
+
+// One 64-bit bitmap's containers in ascending 48-bit key order, from the downloaded bucket SoA.
+struct ArtView {
+  std::vector<uint64_t> key;
+  std::vector<uint64_t> cont; // container index in the SoA
+};
+ArtView art_view(const rbgpu_set64 *s, uint32_t i, const rb_soa &soa) {
+  ArtView v;
+  for (uint64_t e = s->begin[i]; e < s->begin[i + 1]; ++e) { // directory: ascending unsigned highs
+    const uint32_t b = s->idx[e];
+    for (uint64_t c = soa.begin[b]; c < soa.begin[b + 1]; ++c) {
+      v.key.push_back(((uint64_t)s->high[e] << 16) | soa.key[c]);
+      v.cont.push_back(c);
+    }
+  }
+  return v;
+}
+// Writes (dst) or measures one bitmap's stream.
+uint64_t art_stream(const ArtView &v, const rb_soa &soa, uint8_t *dst) {
+  ArtOut o{dst};
+  if (v.key.empty()) { // HighLowContainer.serialize: EMPTY_TAG
+    o.put(0);
+    return o.pos;
+  }
+  o.put(1);
+  o.put_le(v.key.size(), 8); // Art.keySize
+  art_nodes(v.key, 0, v.key.size(), 0, o);
+  const uint64_t n = v.key.size(), cap = art_capacity(n);
+  o.put_le(1, 4);  // Containers.serialize: one first-level array,
+  o.put(0xFE);     // NOT_TRIMMED_MARK
+  o.put_le(cap, 4);
+  for (uint64_t j = 0; j < n; ++j) {
+    const uint64_t c = v.cont[j];
+    const uint8_t ty = soa.type[c];
+    o.put(1); // NOT_NULL_MARK, containerType (0 Run, 1 Bitmap, 2 Array), cardinality, writeArray
+    o.put(ty == RB_RUN ? 0 : ty == RB_BITMAP ? 1 : 2);
+    o.put_le(soa.card[c], 4);
+    if (ty == RB_RUN) o.put_le(soa.nruns[c], 2);
+    const uint64_t bytes = payload_bytes(ty, soa.card[c], soa.nruns[c]);
+    if (dst) std::memcpy(dst + o.pos, soa.payload + soa.offset[c], bytes);
+    o.pos += bytes;
+  }
+  for (uint64_t j = n; j < cap; ++j) o.put(0); // NULL_MARK slots of the grown array
+  o.put_le(n, 8);     // containerSize
+  o.put_le(0, 4);     // firstLevelIdx
+  o.put_le(n - 1, 4); // secondLevelIdx
+  return o.pos;
+}
+
+// The bucket set downloaded as host SoA (the ART writers need every container's payload).
+struct HostBuckets {
+  rb_soa soa{};
+  std::vector<uint64_t> begin, offset;
+  std::vector<uint16_t> key, nruns;
+  std::vector<uint8_t> type, payload;
+  std::vector<uint32_t> card;
+};
+int download_buckets(const rbgpu_set64 *s, HostBuckets &h) {
+  const rbgpu_set *b = s->buckets;
+  h.begin.assign(b->nb + 1, 0);
+  h.soa = rb_soa{};
+  h.soa.begin = h.begin.data();
+  if (!b->nb) return RB_OK;
+  int rc = rbgpu_set_download(b, 0, b->nb, &h.soa); // sizes first (key == NULL)
+  if (rc) return rc;
+  h.key.resize(std::max<uint64_t>(h.soa.n_containers, 1));
+  h.type.resize(h.key.size());
+  h.card.resize(h.key.size());
+  h.nruns.resize(h.key.size());
+  h.offset.resize(h.key.size());
+  h.payload.resize(std::max<uint64_t>(h.soa.payload_bytes, 16));
+  h.soa.key = h.key.data();
+  h.soa.type = h.type.data();
+  h.soa.card = h.card.data();
+  h.soa.nruns = h.nruns.data();
+  h.soa.offset = h.offset.data();
+  h.soa.payload = h.payload.data();
+  return rbgpu_set_download(b, 0, b->nb, &h.soa);
+}
+
 } // namespace
 
 extern "C" {
+
+int rbgpu_set64_from_art(rbgpu_ctx *ctx, const uint8_t *const *bufs, const uint64_t *lens, uint32_t n,
+                         rbgpu_set64 **out) {
+  if (!ctx || !out || (n && (!bufs || !lens))) return fail(RB_EINVAL, "null argument");
+  *out = nullptr;
+  // every bucket's containers into one host SoA, then one upload (rbgpu_set_from_soa validates them)
+  std::vector<uint64_t> begin{0}, offset;
+  std::vector<uint16_t> key, nruns;
+  std::vector<uint8_t> type, payload;
+  std::vector<uint32_t> card;
+  rbgpu_set64 *s = new rbgpu_set64;
+  s->ctx = ctx;
+  s->begin.push_back(0);
+  auto bad = [&](uint32_t i, const char *what) {
+    delete s;
+    return fail(RB_EFORMAT, "64-bit bitmap %u: %s", i, what);
+  };
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint8_t *p = bufs[i];
+    const uint64_t len = lens[i];
+    if (!p || len < 1) return bad(i, "truncated");
+    if (p[0] > 1) return bad(i, "bad empty tag");
+    if (p[0] == 0) { // EMPTY_TAG: nothing follows
+      if (len != 1) return bad(i, "trailing bytes after the empty tag");
+      s->begin.push_back(s->high.size());
+      s->sgn.push_back(0);
+      continue;
+    }
+    uint64_t pos = 9; // the tag, Art.keySize
+    if (len < pos) return bad(i, "truncated");
+    // preorder walk of the nodes (art/Art.java:373-391): an internal node's `count` children follow it
+    std::vector<std::pair<uint64_t, uint64_t>> leaves; // (48-bit key, container index)
+    uint64_t pending = 1;
+    while (pending) {
+      --pending;
+      if (pos + 4 > len) return bad(i, "truncated ART node");
+      const uint8_t t = p[pos];
+      const uint32_t cnt = rd16(p + pos + 1), plen = p[pos + 3];
+      pos += 4 + plen;
+      if (t == kArtLeaf) {
+        if (pos + 14 > len) return bad(i, "truncated ART leaf");
+        uint64_t k = 0, ci;
+        for (int d = 0; d < 6; ++d) k = (k << 8) | p[pos + d];
+        std::memcpy(&ci, p + pos + 6, 8);
+        leaves.push_back({k, ci});
+        pos += 14;
+      } else {
+        if (t > 3) return bad(i, "bad ART node type");
+        if (cnt < 2 || cnt > 256) return bad(i, "bad ART node child count");
+        pos += kArtBody[t];
+        pending += cnt;
+      }
+    }
+    if (pos + 4 > len) return bad(i, "truncated containers");
+    const uint32_t nfirst = rd32(p + pos);
+    pos += 4;
+    struct C {
+      uint8_t t;
+      uint32_t card;
+      uint16_t nr;
+      uint64_t at;
+    };
+    std::vector<std::pair<uint64_t, C>> conts; // (container index, container) in index order
+    for (uint32_t f = 0; f < nfirst; ++f) {
+      if (pos + 5 > len) return bad(i, "truncated containers");
+      const uint32_t nsecond = rd32(p + pos + 1);
+      pos += 5;
+      for (uint32_t j = 0; j < nsecond; ++j) {
+        if (pos + 1 > len) return bad(i, "truncated containers");
+        const uint8_t tag = p[pos++];
+        if (tag == 0) continue; // NULL_MARK
+        if (tag != 1 || pos + 5 > len) return bad(i, "bad container null tag");
+        const uint8_t ct = p[pos];
+        C c{};
+        c.card = rd32(p + pos + 1);
+        pos += 5;
+        uint64_t bytes;
+        if (ct == 0) { // Run: nbrruns, then (value, length) pairs
+          if (pos + 2 > len) return bad(i, "truncated run container");
+          c.t = RB_RUN;
+          c.nr = rd16(p + pos);
+          pos += 2;
+          bytes = 4ull * c.nr;
+        } else if (ct == 1) {
+          c.t = RB_BITMAP;
+          bytes = 8192;
+        } else if (ct == 2) {
+          c.t = RB_ARRAY;
+          if (c.card > 4096) return bad(i, "array container over 4096 values");
+          bytes = 2ull * c.card;
+        } else {
+          return bad(i, "bad container type");
+        }
+        if (pos + bytes > len) return bad(i, "truncated container payload");
+        c.at = pos;
+        pos += bytes;
+        conts.push_back({((uint64_t)f << 32) | j, c});
+      }
+    }
+    if (pos + 16 != len) return bad(i, "bad length after the containers");
+    std::sort(leaves.begin(), leaves.end());
+    for (size_t l = 1; l < leaves.size(); ++l)
+      if (leaves[l].first == leaves[l - 1].first) return bad(i, "duplicate ART key");
+    // buckets: the leaves grouped by their high 32 bits (a kept-empty container holds no value: skipped)
+    int64_t cur_high = -1;
+    for (const auto &lf : leaves) {
+      const auto it = std::lower_bound(conts.begin(), conts.end(), lf.second,
+                                       [](const std::pair<uint64_t, C> &x, uint64_t v) { return x.first < v; });
+      if (it == conts.end() || it->first != lf.second) return bad(i, "ART leaf without a container");
+      const C &c = it->second;
+      if (c.card == 0) continue;
+      const uint32_t high = (uint32_t)(lf.first >> 16);
+      if ((int64_t)high != cur_high) {
+        if (s->idx.size() + 1 >= kEmptyBitmap) return bad(i, "too many buckets");
+        s->high.push_back(high);
+        s->idx.push_back((uint32_t)(begin.size() - 1));
+        begin.push_back(begin.back());
+        cur_high = high;
+      }
+      key.push_back((uint16_t)(lf.first & 0xFFFF));
+      type.push_back(c.t);
+      card.push_back(c.card);
+      nruns.push_back(c.t == RB_RUN ? c.nr : 0);
+      offset.push_back(payload.size());
+      const uint64_t bytes = payload_bytes(c.t, c.card, c.nr);
+      payload.insert(payload.end(), p + c.at, p + c.at + bytes);
+      payload.resize((payload.size() + 15) & ~size_t(15));
+      ++begin.back();
+    }
+    s->begin.push_back(s->high.size());
+    s->sgn.push_back(0);
+  }
+  rb_soa soa{(uint32_t)(begin.size() - 1), key.size(), payload.size(), begin.data(), key.data(), type.data(),
+             card.data(), nruns.data(), offset.data(), payload.data()};
+  const int rc = soa.n_bitmaps ? rbgpu_set_from_soa(ctx, &soa, &s->buckets)
+                               : ((s->buckets = empty_set(ctx)) ? RB_OK : fail(RB_ENOMEM, "empty bucket set"));
+  if (rc) {
+    delete s;
+    return rc;
+  }
+  *out = s;
+  return RB_OK;
+}
+
+int rbgpu_set64_art_sizes(const rbgpu_set64 *s, uint64_t *out) {
+  if (!s || !out) return fail(RB_EINVAL, "null argument");
+  HostBuckets h;
+  const int rc = download_buckets(s, h);
+  if (rc) return rc;
+  for (uint32_t i = 0; i < s->n(); ++i) out[i] = art_stream(art_view(s, i, h.soa), h.soa, nullptr);
+  return RB_OK;
+}
+
+int rbgpu_set64_serialize_art(const rbgpu_set64 *s, uint32_t first, uint32_t count, uint8_t *dst, uint64_t cap,
+                              uint64_t *offsets) {
+  if (!s || (count && !dst)) return fail(RB_EINVAL, "null argument");
+  if ((uint64_t)first + count > s->n()) return fail(RB_EINVAL, "bitmap range out of bounds");
+  HostBuckets h;
+  const int rc = download_buckets(s, h);
+  if (rc) return rc;
+  uint64_t pos = 0;
+  for (uint32_t i = first; i < first + count; ++i) {
+    const ArtView v = art_view(s, i, h.soa);
+    const uint64_t need = art_stream(v, h.soa, nullptr);
+    if (pos + need > cap) return fail(RB_EINVAL, "destination buffer too small (%llu needed)", (unsigned long long)(pos + need));
+    if (offsets) offsets[i - first] = pos;
+    pos += art_stream(v, h.soa, dst + pos);
+  }
+  if (offsets) offsets[count] = pos;
+  return RB_OK;
+}
 
 int rbgpu_set64_from_portable(rbgpu_ctx *ctx, const uint8_t *const *bufs, const uint64_t *lens, uint32_t n,
                               rbgpu_set64 **out) {

@@ -438,6 +438,15 @@ class Context:
         L.check(L.lib().rbgpu_set64_from_legacy(self.h, arr, lens.ctypes.data_as(L._U64P), n, C.byref(out)))
         return DeviceSet64(self, out.value)
 
+    def upload_art64(self, blobs: Sequence[bytes]) -> "DeviceSet64":
+        """Roaring64Bitmap.deserialize per blob (rbgpu_set64_from_art: the ART + Containers stream)."""
+        n = len(blobs)
+        arr = (C.c_char_p * max(n, 1))(*blobs)
+        lens = np.array([len(b) for b in blobs] or [0], np.uint64)
+        out = C.c_void_p()
+        L.check(L.lib().rbgpu_set64_from_art(self.h, arr, lens.ctypes.data_as(L._U64P), n, C.byref(out)))
+        return DeviceSet64(self, out.value)
+
     def pairwise64_cardinality(self, op: int, a: "DeviceSet64", b: "DeviceSet64", a_idx=None, b_idx=None,
                                npairs=None) -> np.ndarray:
         """rbgpu_pairwise64_cardinality: the static op's getLongCardinality per pair (Roaring64Bitmap.
@@ -811,6 +820,10 @@ class DeviceSet64:
     def serialize_legacy(self) -> List[bytes]:
         """Roaring64NavigableMap.serializeLegacy per bitmap (its default serialize)."""
         return self._serialize(L.lib().rbgpu_set64_legacy_sizes, L.lib().rbgpu_set64_serialize_legacy)
+
+    def serialize_art(self) -> List[bytes]:
+        """Roaring64Bitmap.serialize per bitmap (rbgpu_set64_serialize_art)."""
+        return self._serialize(L.lib().rbgpu_set64_art_sizes, L.lib().rbgpu_set64_serialize_art)
 
     def set_signed_longs(self, i: int, flag: bool) -> None:
         L.check(L.lib().rbgpu_set64_set_signed_longs(self.h, i, 1 if flag else 0))

@@ -549,6 +549,15 @@ class Roaring64Bitmap(_Bitmap64):
         """Roaring64Bitmap.andCardinality (longlong/Roaring64Bitmap.java:562-592), on the device."""
         return int(default_context().pairwise64_cardinality(L.AND, x1._set, x2._set, npairs=1)[0])
 
+    @classmethod
+    def deserialize(cls, data: bytes):
+        """deserialize (:905-908): HighLowContainer's ART + Containers stream (rbgpu_set64_from_art)."""
+        return cls(default_context().upload_art64([data]))
+
+    def serialize(self) -> bytes:
+        """serialize (:880-882), the canonical stream of this bitmap (rbgpu_set64_serialize_art)."""
+        return self._set.serialize_art()[0]
+
     and_ = _StaticOrInPlace64(L.AND)
     or_ = _StaticOrInPlace64(L.OR)
     xor = _StaticOrInPlace64(L.XOR)

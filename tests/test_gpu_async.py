@@ -59,3 +59,56 @@ def test_async_caller_stream_and_small_batch(ctx, pairs, oracle):
     got = ctx.pairwise_async(rb.AND, small, small, ai, ai + 1).serialize()
     for i in range(29):
         assert got[i] == oracle.op(rb.AND, refs[i], refs[i + 1]).serialize()
+
+
+def _digest(s):
+    """Per-bitmap cardinalities and serialized sizes, container type counts, and the bytes of three
+    1000-bitmap windows (head, middle, tail: the tail's tasks run last in the task kernels)."""
+    n = len(s)
+    wins = [s.serialize(lo, min(1000, n - lo)) for lo in (0, n // 2, max(0, n - 1000))]
+    return (s.cardinalities().tobytes(), s.serialized_sizes().tobytes(), s.type_stats(), int(s.n_containers), wins)
+
+
+def test_async_pipeline_back_to_back(ctx, pairs):
+    """Pipelined calls (one segment per pair): call k+1's count / scan / emit run on the front stream while
+    call k's task kernels run, its workspaces alternating between two sets.  Eight calls in flight with
+    alternating ops (each workspace set reused by a different op), a synchronous call and an indexed
+    (non-pipelined) asynchronous call in between, each equal to the synchronous result."""
+    import roaringbitmap_amd as rb
+    a, b = pairs
+    ops = [rb.AND, rb.OR, rb.XOR, rb.ANDNOT, rb.OR, rb.AND, rb.ANDNOT, rb.XOR]
+    want = {}
+    for op in set(ops):
+        w = ctx.pairwise(op, a, b)
+        want[op] = _digest(w)
+        w.close()
+    pend = [ctx.pairwise_async(op, a, b) for op in ops[:4]]
+    mid = ctx.pairwise(rb.XOR, a, b)  # synchronous, behind four pending calls
+    idx = np.arange(len(a), dtype=np.uint32)
+    pend += [ctx.pairwise_async(op, a, b, idx, idx) for op in ops[4:5]]  # indexed: the non-pipelined path
+    pend += [ctx.pairwise_async(op, a, b) for op in ops[5:]]
+    assert _digest(mid) == want[rb.XOR]
+    mid.close()
+    for op, r in zip(ops, pend):
+        assert _digest(r) == want[op], op
+        r.close()
+
+
+def test_async_pipeline_release_order(ctx, pairs):
+    """The bench's pattern: each step's result freed one step later (its free waits for it), 12 steps."""
+    import roaringbitmap_amd as rb
+    a, b = pairs
+    w = ctx.pairwise(rb.AND, a, b)
+    want = _digest(w)
+    w.close()
+    prev, got = None, []
+    for i in range(12):
+        r = ctx.pairwise_async(rb.AND, a, b)
+        if prev is not None:
+            if i % 4 == 0:
+                got.append(_digest(prev))
+            prev.close()
+        prev = r
+    got.append(_digest(prev.wait()))
+    prev.close()
+    assert all(g == want for g in got)

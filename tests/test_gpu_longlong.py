@@ -239,3 +239,38 @@ def test_roaring64_navigable_mirror_legacy(ctx, oracle):
     a = rb.Roaring64Bitmap.bitmapOf(vals)
     b = rb.Roaring64Bitmap.bitmapOf(np.array([123, 5], np.uint64))
     assert rb.Roaring64Bitmap.andCardinality(a, b) == 1
+
+
+def test_roaring64_art_format(ctx, oracle):
+    """Roaring64Bitmap.serialize / deserialize (HighLowContainer: ART + Containers) on the device: ingest
+    and emit equal the oracle's canonical bytes for sets covering every node type, a stream with another
+    container placement (null slots, permuted indices) reads back to the same set, and the static ops'
+    results emit the oracle's bytes — an xor's kept-empty containers included (parity unpinned: no
+    reference fixture, see test_oracle64.test_oracle64_art_format)."""
+    import roaringbitmap_amd as rb
+    from oracle import rbref64 as R64
+    from test_oracle64 import _art_sets
+    sets = _art_sets()
+    blobs = [r.to_art() for r in sets]
+    s = ctx.upload_art64(blobs)
+    assert s.serialize_art() == blobs
+    assert s.serialize_portable() == [r.to_portable() for r in sets]
+    other = []
+    for r in sets:
+        n = sum(len(b.containers()) for _, b in r.buckets)
+        other.append(r.to_art(slots=list(np.random.default_rng(n).permutation(n + 2)[:n]), cap=n + 2) if n else b"\x00")
+    assert ctx.upload_art64(other).serialize_art() == blobs
+    p, refs = _pool(ctx, oracle, 5, n=6)
+    n = len(refs)
+    ai = np.array([i for i in range(n) for j in range(n)], np.uint32)
+    bi = np.array([j for i in range(n) for j in range(n)], np.uint32)
+    for opname, op in OPS.items():
+        got = ctx.pairwise64(rb.RB64_BITMAP, op, p, p, ai, bi).serialize_art()
+        for k in range(len(ai)):
+            want = R64.bitmap_op(op, refs[int(ai[k])], refs[int(bi[k])], False).to_art()
+            assert got[k] == want, (opname, int(ai[k]), int(bi[k]))
+    x = rb.Roaring64Bitmap.bitmapOf(np.array([1, 2, (7 << 40) | 3], np.uint64))
+    y = rb.Roaring64Bitmap.deserialize(x.serialize())
+    assert np.array_equal(y.toArray(), x.toArray())
+    with pytest.raises(rb.FormatError):
+        ctx.upload_art64([blobs[2][:-1]])

@@ -106,3 +106,58 @@ def _legacy_high_positions(data):
         pos += 4
         pos += len(R.RefBitmap.deserialize(data[pos:]).serialize())
     return out
+
+
+def _art_sets():
+    """64-bit sets whose ARTs cover every node type: one 48-bit key; two keys differing in the last byte
+    (a Node4 with a 5-byte prefix); 5 / 17 / 49 children under one node (Node16 / Node48 / Node256 by
+    growth); keys spread over the 48-bit space (several levels, prefixes of every length)."""
+    from oracle import rbref64 as R64
+    rng = np.random.default_rng(11)
+    out = [R64.Ref64(), R64.Ref64.of([5]), R64.Ref64.of([5, (1 << 16) | 7])]
+    for nkids in (5, 17, 49, 300):
+        keys = np.arange(nkids, dtype=np.uint64) * np.uint64(3)
+        out.append(R64.Ref64.of((keys << np.uint64(16)) | np.uint64(9)))
+    spread = rng.integers(0, 1 << 48, size=200, dtype=np.uint64)
+    vals = [(spread << np.uint64(16)) | rng.integers(0, 65536, size=200).astype(np.uint64)]
+    for k in rng.choice(200, 20, replace=False):  # some dense keys (Bitmap / Run containers)
+        vals.append((spread[k] << np.uint64(16)) + np.arange(5000, 30000, dtype=np.uint64))
+    r = R64.Ref64.of(np.concatenate(vals))
+    for _, b in r.buckets[::2]:
+        b.run_optimize()
+    out.append(r)
+    return out
+
+
+def test_oracle64_art_format():
+    """Roaring64Bitmap.serialize / deserialize (HighLowContainer: ART + Containers) restated in
+    oracle/rbref64.py.  Parity unpinned: the reference holds no fixture of this format, so this pins the
+    restatement by one hand-decoded stream (two 48-bit keys differing in the last byte: a Node4 with a
+    5-byte prefix over two leaves, one 2-slot container array) and round trips over every node type."""
+    from oracle import rbref64 as R64
+    two = R64.Ref64.of([5, (1 << 16) | 7]).to_art()
+    want = bytes.fromhex(
+        "01" "0200000000000000"                         # NOT_EMPTY_TAG, Art.keySize = 2 (LE long)
+        "00" "0200" "05" "0000000000" "00000100"        # Node4: count 2, prefix 00x5, key bytes 0, 1 (reversed int)
+        "04" "0000" "00" "000000000000" "0000000000000000"  # LeafNode: key 0, container index 0
+        "04" "0000" "00" "000000000001" "0100000000000000"  # LeafNode: key 1, container index 1
+        "01000000" "fe" "02000000"                      # one first-level array, NOT_TRIMMED_MARK, 2 slots
+        "01" "02" "01000000" "0500"                     # NOT_NULL, ArrayContainer (type 2), card 1, value 5
+        "01" "02" "01000000" "0700"
+        "0200000000000000" "00000000" "01000000")       # containerSize, firstLevelIdx, secondLevelIdx
+    assert two == want
+    assert R64.Ref64().to_art() == b"\x00"
+    for r in _art_sets():
+        data = r.to_art()
+        back = R64.Ref64.from_art(data)
+        assert np.array_equal(back.to_array(), r.to_array())
+        assert back.to_art() == data
+        n = sum(len(b.containers()) for _, b in r.buckets)
+        if n > 1:  # another container placement (a history with removals): same set
+            slots = list(np.random.default_rng(n).permutation(n + 3)[:n])
+            other = r.to_art(slots=slots, cap=n + 3)
+            assert other != data and np.array_equal(R64.Ref64.from_art(other).to_array(), r.to_array())
+    # the root's type byte (after the tag and the key count): 5 / 17 / 49 children grow Node16 / 48 / 256
+    assert [r.to_art()[9] for r in _art_sets()[3:6]] == [1, 2, 3]
+    with pytest.raises((IOError, Exception)):
+        R64.Ref64.from_art(two[:-1])
