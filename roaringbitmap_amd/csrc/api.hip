@@ -1062,8 +1062,9 @@ static int pairwise_small(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgp
 // probe: 0 = the product path; 1 / 2 = measurement probes (rbgpu_internal_probe) in place of the
 // task kernel — results are not produced.
 static // tasks bound up to which pairwise_impl reserves the task workspace before the totals are read back
-// (58 B per task: 928 MiB at the cap)
-constexpr uint64_t kEarlyEmitTasks = 1ull << 24;
+// (58 B per task: 464 MiB at the cap; the bound a.nc + b.nc can far exceed the real count — an AND of
+// mostly disjoint keys — and the workspace stays grown, so the cap is set just above config 2's 6.1M)
+constexpr uint64_t kEarlyEmitTasks = 1ull << 23;
 
 // async: return once the task kernels and the compaction are enqueued (rbgpu_pairwise_async): the result
 // is pending (settle() fills its container count), the call's counters are not read back (rb_stats keeps

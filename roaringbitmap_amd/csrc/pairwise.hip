@@ -526,9 +526,6 @@ __device__ __forceinline__ RecU load_rec(const TaskRec *r) {
 #define RBG_HEAVY_NOPF 0 // study: register-path tasks without the one-task prefetch, at 128 VGPRs, so three
                          // light waves fit beside each heavy one on a SIMD
 #endif
-#ifndef RBG_LIGHT_ROWS
-#define RBG_LIGHT_ROWS 0 // study: the light role loads only the payload rows a task has (uniform branches)
-#endif
 constexpr int kLightWaves = 4; // waves per SIMD of the copy + filter kernel (128 VGPRs)
 constexpr int kHeavyWaves = RBG_HEAVY_NOPF ? 4 : 2; // waves per SIMD the register-path kernel is allocated for
 constexpr bool kHeavyPrefetch = !RBG_HEAVY_NOPF;    // the next task's payloads in flight during this one's emission
@@ -951,8 +948,7 @@ __global__ __launch_bounds__(256, ROLE == kRoleHeavy ? kHeavyWaves : kLightWaves
       }
       {
         const bool real = has_next && tn.kind != kCopy && !tn.bigq;
-        if (RBG_LIGHT_ROWS) load_chunks_rows(qq, real ? tn.pq : tn.pp, real ? tn.qbytes : 16u, lane);
-        else load_chunks(qq, real ? tn.pq : tn.pp, real ? tn.qbytes : 16u, lane);
+        load_chunks(qq, real ? tn.pq : tn.pp, real ? tn.qbytes : 16u, lane);
       }
       RBG_LT(lt2 = __builtin_amdgcn_s_memtime(); lt_acc[tc.kind == kFilter ? 1 + (tc.tq == kBitmap ? 0 : tc.tq == kArray ? 1 : 2) : 4] += lt2 - lt1);
       // ---- phase 2: filter F against the staged X, in value order (adjacent lanes, adjacent values)
@@ -971,8 +967,7 @@ __global__ __launch_bounds__(256, ROLE == kRoleHeavy ? kHeavyWaves : kLightWaves
         nr = tc.rp;
       }
       RBG_LT(lt_acc[5] += __builtin_amdgcn_s_memtime() - lt2);
-      if (RBG_LIGHT_ROWS) load_chunks_rows(pq, tn.pp, tn.bigp ? 16u : tn.pbytes, lane);
-      else load_chunks(pq, tn.pp, tn.bigp ? 16u : tn.pbytes, lane);
+      load_chunks(pq, tn.pp, tn.bigp ? 16u : tn.pbytes, lane);
     }
     wave_lds_sync(); // the next task restages the same LDS image
     if (lane == 0) {

@@ -297,15 +297,6 @@ __device__ __forceinline__ void load_chunks(uint4 (&q)[8], const uint8_t *p, uin
 #pragma unroll
   for (int i = 0; i < 8; ++i) q[i] = load_chunk_row(rs, i, lane);
 }
-// Only the rows the payload reaches (wave-uniform branches): rows past it keep their old contents,
-// which no reader looks at (readers stop at the payload's own count).
-__device__ __forceinline__ void load_chunks_rows(uint4 (&q)[8], const uint8_t *p, uint32_t bytes, int lane) {
-  const __amdgpu_buffer_rsrc_t rs = chunk_rsrc(p, bytes);
-  const uint32_t rows = __builtin_amdgcn_readfirstlane((bytes + 1023u) >> 10);
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-    if ((uint32_t)i < rows || i == 0) q[i] = load_chunk_row(rs, i, lane);
-}
 // lanes below this one with their bit set in m
 __device__ __forceinline__ uint32_t mbcnt64(uint64_t m) {
   return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));

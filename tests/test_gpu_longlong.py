@@ -274,3 +274,23 @@ def test_roaring64_art_format(ctx, oracle):
     assert np.array_equal(y.toArray(), x.toArray())
     with pytest.raises(rb.FormatError):
         ctx.upload_art64([blobs[2][:-1]])
+
+
+def test_roaring64_kept_empty_through_later_ops(ctx, oracle):
+    """ADVICE r03 (low): x.xor(y) keeps an empty container under its key (Roaring64Bitmap.java:468-495);
+    a later in-place andNot / or with a bitmap lacking that high leaves x's unmatched key untouched
+    (:599-628, 392-419), and the static forms clone it — the empty container stays in the bytes (ART
+    stream, the oracle's canonical writer) while the values agree."""
+    import roaringbitmap_amd as rb
+    from oracle import rbref64 as R64
+    H = np.uint64(5 << 32)
+    xv, yv, zv = H | np.arange(3, dtype=np.uint64), H | np.arange(3, dtype=np.uint64), np.array([1 << 40], np.uint64)
+    for op, name in ((rb.ANDNOT, "andNot"), (rb.OR, "or_")):
+        x, y, z = (rb.Roaring64Bitmap.bitmapOf(v) for v in (xv, yv, zv))
+        x.xor(y)
+        ref = R64.bitmap_op(rb.XOR, R64.Ref64.of(xv), R64.Ref64.of(yv), True)
+        assert x.serialize() == ref.to_art() and x.isEmpty()
+        getattr(x, name)(z)
+        ref_i = R64.bitmap_op(op, ref, R64.Ref64.of(zv), True)
+        assert x.serialize() == ref_i.to_art(), name
+        assert np.array_equal(x.toArray(), ref_i.to_array())
