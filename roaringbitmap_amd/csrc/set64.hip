@@ -162,7 +162,8 @@ int bucket_pairs(const rbgpu_set64 *a, const rbgpu_set64 *b, int op, bool inplac
   return RB_OK;
 }
 
-// ---- Roaring64Bitmap.serialize: HighLowContainer = ART over the 6-byte high keys + Containers
+// ---- ART codec (host only; scripts/art_host_check.py compiles this part alone)
+// Roaring64Bitmap.serialize: HighLowContainer = ART over the 6-byte high keys + Containers
 // (longlong/HighLowContainer.java:230-254, art/Art.java:309-391, art/Node*.java, art/Containers.java:210-303).
 // Little-endian fields (the writers reverse bytes around DataOutput), node type ordinals NODE4 / NODE16 /
 // NODE48 / NODE256 / LEAF_NODE = 0..4.  Parity unpinned: no reference fixture holds this format.
@@ -239,17 +240,6 @@ struct ArtView {
   std::vector<uint64_t> key;
   std::vector<uint64_t> cont; // container index in the SoA
 };
-ArtView art_view(const rbgpu_set64 *s, uint32_t i, const rb_soa &soa) {
-  ArtView v;
-  for (uint64_t e = s->begin[i]; e < s->begin[i + 1]; ++e) { // directory: ascending unsigned highs
-    const uint32_t b = s->idx[e];
-    for (uint64_t c = soa.begin[b]; c < soa.begin[b + 1]; ++c) {
-      v.key.push_back(((uint64_t)s->high[e] << 16) | soa.key[c]);
-      v.cont.push_back(c);
-    }
-  }
-  return v;
-}
 // Writes (dst) or measures one bitmap's stream.
 uint64_t art_stream(const ArtView &v, const rb_soa &soa, uint8_t *dst) {
   ArtOut o{dst};
@@ -280,6 +270,114 @@ uint64_t art_stream(const ArtView &v, const rb_soa &soa, uint8_t *dst) {
   o.put_le(0, 4);     // firstLevelIdx
   o.put_le(n - 1, 4); // secondLevelIdx
   return o.pos;
+}
+
+// One stream's containers in ascending 48-bit key order (nullptr) or what is wrong with it.  Reads any
+// tree shape and container-slot layout: the preorder node walk (art/Art.java:373-391: an internal node's
+// `count` children follow it), then the Containers arrays (art/Containers.java:276-303, the type codes of
+// instanceContainer :352-378), each leaf's container found by its index.
+struct ArtCont {
+  uint64_t key; // high 48 bits
+  uint8_t t;    // rb_type
+  uint32_t card;
+  uint16_t nr;
+  const uint8_t *payload;
+};
+const char *art_parse(const uint8_t *p, uint64_t len, std::vector<ArtCont> &out) {
+  out.clear();
+  if (!p || len < 1) return "truncated";
+  if (p[0] > 1) return "bad empty tag";
+  if (p[0] == 0) return len == 1 ? nullptr : "trailing bytes after the empty tag"; // EMPTY_TAG
+  uint64_t pos = 9; // the tag, Art.keySize
+  if (len < pos) return "truncated";
+  std::vector<std::pair<uint64_t, uint64_t>> leaves; // (48-bit key, container index)
+  uint64_t pending = 1;
+  while (pending) {
+    --pending;
+    if (pos + 4 > len) return "truncated ART node";
+    const uint8_t t = p[pos];
+    const uint32_t cnt = rd16(p + pos + 1), plen = p[pos + 3];
+    pos += 4 + plen;
+    if (t == kArtLeaf) {
+      if (pos + 14 > len) return "truncated ART leaf";
+      uint64_t k = 0, ci;
+      for (int d = 0; d < 6; ++d) k = (k << 8) | p[pos + d];
+      std::memcpy(&ci, p + pos + 6, 8);
+      leaves.push_back({k, ci});
+      pos += 14;
+    } else {
+      if (t > 3) return "bad ART node type";
+      if (cnt < 2 || cnt > 256) return "bad ART node child count";
+      pos += kArtBody[t];
+      pending += cnt;
+    }
+  }
+  if (pos + 4 > len) return "truncated containers";
+  const uint32_t nfirst = rd32(p + pos);
+  pos += 4;
+  std::vector<std::pair<uint64_t, ArtCont>> conts; // (container index, container) in index order
+  for (uint32_t f = 0; f < nfirst; ++f) {
+    if (pos + 5 > len) return "truncated containers";
+    const uint32_t nsecond = rd32(p + pos + 1);
+    pos += 5;
+    for (uint32_t j = 0; j < nsecond; ++j) {
+      if (pos + 1 > len) return "truncated containers";
+      const uint8_t tag = p[pos++];
+      if (tag == 0) continue; // NULL_MARK
+      if (tag != 1 || pos + 5 > len) return "bad container null tag";
+      const uint8_t ct = p[pos];
+      ArtCont c{};
+      c.card = rd32(p + pos + 1);
+      pos += 5;
+      uint64_t bytes;
+      if (ct == 0) { // Run: nbrruns, then (value, length) pairs
+        if (pos + 2 > len) return "truncated run container";
+        c.t = RB_RUN;
+        c.nr = rd16(p + pos);
+        pos += 2;
+        bytes = 4ull * c.nr;
+      } else if (ct == 1) {
+        c.t = RB_BITMAP;
+        bytes = 8192;
+      } else if (ct == 2) {
+        c.t = RB_ARRAY;
+        if (c.card > 4096) return "array container over 4096 values";
+        bytes = 2ull * c.card;
+      } else {
+        return "bad container type";
+      }
+      if (pos + bytes > len) return "truncated container payload";
+      c.payload = p + pos;
+      pos += bytes;
+      conts.push_back({((uint64_t)f << 32) | j, c});
+    }
+  }
+  if (pos + 16 != len) return "bad length after the containers";
+  std::sort(leaves.begin(), leaves.end());
+  for (size_t l = 1; l < leaves.size(); ++l)
+    if (leaves[l].first == leaves[l - 1].first) return "duplicate ART key";
+  for (const auto &lf : leaves) {
+    const auto it = std::lower_bound(conts.begin(), conts.end(), lf.second,
+                                     [](const std::pair<uint64_t, ArtCont> &x, uint64_t v) { return x.first < v; });
+    if (it == conts.end() || it->first != lf.second) return "ART leaf without a container";
+    ArtCont c = it->second;
+    c.key = lf.first;
+    out.push_back(c);
+  }
+  return nullptr;
+}
+// ---- end of the ART codec
+
+ArtView art_view(const rbgpu_set64 *s, uint32_t i, const rb_soa &soa) {
+  ArtView v;
+  for (uint64_t e = s->begin[i]; e < s->begin[i + 1]; ++e) { // directory: ascending unsigned highs
+    const uint32_t b = s->idx[e];
+    for (uint64_t c = soa.begin[b]; c < soa.begin[b + 1]; ++c) {
+      v.key.push_back(((uint64_t)s->high[e] << 16) | soa.key[c]);
+      v.cont.push_back(c);
+    }
+  }
+  return v;
 }
 
 // The bucket set downloaded as host SoA (the ART writers need every container's payload).
@@ -336,98 +434,13 @@ int rbgpu_set64_from_art(rbgpu_ctx *ctx, const uint8_t *const *bufs, const uint6
   for (uint32_t i = 0; i < n; ++i) {
     const uint8_t *p = bufs[i];
     const uint64_t len = lens[i];
-    if (!p || len < 1) return bad(i, "truncated");
-    if (p[0] > 1) return bad(i, "bad empty tag");
-    if (p[0] == 0) { // EMPTY_TAG: nothing follows
-      if (len != 1) return bad(i, "trailing bytes after the empty tag");
-      s->begin.push_back(s->high.size());
-      s->sgn.push_back(0);
-      continue;
-    }
-    uint64_t pos = 9; // the tag, Art.keySize
-    if (len < pos) return bad(i, "truncated");
-    // preorder walk of the nodes (art/Art.java:373-391): an internal node's `count` children follow it
-    std::vector<std::pair<uint64_t, uint64_t>> leaves; // (48-bit key, container index)
-    uint64_t pending = 1;
-    while (pending) {
-      --pending;
-      if (pos + 4 > len) return bad(i, "truncated ART node");
-      const uint8_t t = p[pos];
-      const uint32_t cnt = rd16(p + pos + 1), plen = p[pos + 3];
-      pos += 4 + plen;
-      if (t == kArtLeaf) {
-        if (pos + 14 > len) return bad(i, "truncated ART leaf");
-        uint64_t k = 0, ci;
-        for (int d = 0; d < 6; ++d) k = (k << 8) | p[pos + d];
-        std::memcpy(&ci, p + pos + 6, 8);
-        leaves.push_back({k, ci});
-        pos += 14;
-      } else {
-        if (t > 3) return bad(i, "bad ART node type");
-        if (cnt < 2 || cnt > 256) return bad(i, "bad ART node child count");
-        pos += kArtBody[t];
-        pending += cnt;
-      }
-    }
-    if (pos + 4 > len) return bad(i, "truncated containers");
-    const uint32_t nfirst = rd32(p + pos);
-    pos += 4;
-    struct C {
-      uint8_t t;
-      uint32_t card;
-      uint16_t nr;
-      uint64_t at;
-    };
-    std::vector<std::pair<uint64_t, C>> conts; // (container index, container) in index order
-    for (uint32_t f = 0; f < nfirst; ++f) {
-      if (pos + 5 > len) return bad(i, "truncated containers");
-      const uint32_t nsecond = rd32(p + pos + 1);
-      pos += 5;
-      for (uint32_t j = 0; j < nsecond; ++j) {
-        if (pos + 1 > len) return bad(i, "truncated containers");
-        const uint8_t tag = p[pos++];
-        if (tag == 0) continue; // NULL_MARK
-        if (tag != 1 || pos + 5 > len) return bad(i, "bad container null tag");
-        const uint8_t ct = p[pos];
-        C c{};
-        c.card = rd32(p + pos + 1);
-        pos += 5;
-        uint64_t bytes;
-        if (ct == 0) { // Run: nbrruns, then (value, length) pairs
-          if (pos + 2 > len) return bad(i, "truncated run container");
-          c.t = RB_RUN;
-          c.nr = rd16(p + pos);
-          pos += 2;
-          bytes = 4ull * c.nr;
-        } else if (ct == 1) {
-          c.t = RB_BITMAP;
-          bytes = 8192;
-        } else if (ct == 2) {
-          c.t = RB_ARRAY;
-          if (c.card > 4096) return bad(i, "array container over 4096 values");
-          bytes = 2ull * c.card;
-        } else {
-          return bad(i, "bad container type");
-        }
-        if (pos + bytes > len) return bad(i, "truncated container payload");
-        c.at = pos;
-        pos += bytes;
-        conts.push_back({((uint64_t)f << 32) | j, c});
-      }
-    }
-    if (pos + 16 != len) return bad(i, "bad length after the containers");
-    std::sort(leaves.begin(), leaves.end());
-    for (size_t l = 1; l < leaves.size(); ++l)
-      if (leaves[l].first == leaves[l - 1].first) return bad(i, "duplicate ART key");
-    // buckets: the leaves grouped by their high 32 bits (a kept-empty container holds no value: skipped)
+    std::vector<ArtCont> conts;
+    if (const char *why = art_parse(p, len, conts)) return bad(i, why);
+    // buckets: the containers grouped by their high 32 bits (a kept-empty container holds no value: skipped)
     int64_t cur_high = -1;
-    for (const auto &lf : leaves) {
-      const auto it = std::lower_bound(conts.begin(), conts.end(), lf.second,
-                                       [](const std::pair<uint64_t, C> &x, uint64_t v) { return x.first < v; });
-      if (it == conts.end() || it->first != lf.second) return bad(i, "ART leaf without a container");
-      const C &c = it->second;
+    for (const ArtCont &c : conts) {
       if (c.card == 0) continue;
-      const uint32_t high = (uint32_t)(lf.first >> 16);
+      const uint32_t high = (uint32_t)(c.key >> 16);
       if ((int64_t)high != cur_high) {
         if (s->idx.size() + 1 >= kEmptyBitmap) return bad(i, "too many buckets");
         s->high.push_back(high);
@@ -435,13 +448,13 @@ int rbgpu_set64_from_art(rbgpu_ctx *ctx, const uint8_t *const *bufs, const uint6
         begin.push_back(begin.back());
         cur_high = high;
       }
-      key.push_back((uint16_t)(lf.first & 0xFFFF));
+      key.push_back((uint16_t)(c.key & 0xFFFF));
       type.push_back(c.t);
       card.push_back(c.card);
       nruns.push_back(c.t == RB_RUN ? c.nr : 0);
       offset.push_back(payload.size());
       const uint64_t bytes = payload_bytes(c.t, c.card, c.nr);
-      payload.insert(payload.end(), p + c.at, p + c.at + bytes);
+      payload.insert(payload.end(), c.payload, c.payload + bytes);
       payload.resize((payload.size() + 15) & ~size_t(15));
       ++begin.back();
     }
