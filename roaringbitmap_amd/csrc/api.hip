@@ -1066,6 +1066,9 @@ static // tasks bound up to which pairwise_impl reserves the task workspace befo
 // mostly disjoint keys — and the workspace stays grown, so the cap is set just above config 2's 6.1M)
 constexpr uint64_t kEarlyEmitTasks = 1ull << 23;
 
+#ifndef RBG_PIPELINE
+#define RBG_PIPELINE 0 // the pipelined front phase: implemented, not yet measured on the GPU (off until it is)
+#endif
 // async: return once the task kernels and the compaction are enqueued (rbgpu_pairwise_async): the result
 // is pending (settle() fills its container count), the call's counters are not read back (rb_stats keeps
 // the last synchronous call's), and `ext` (if any, another stream of the caller) is ordered around the call.
@@ -1107,7 +1110,7 @@ int pairwise_impl(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu_set *b
         return fail(RB_ENOMEM, "pinned result-count slots");
       for (int i = kAsyncSlots - 1; i >= 0; --i) ctx->async_free.push_back(i);
     }
-    if (!ctx->front) { // the pipeline's stream, events and counter scratch (see `pipe` below)
+    if (RBG_PIPELINE && !ctx->front) { // the pipeline's stream, events and counter scratch (see `pipe` below)
       hipStream_t fs = nullptr;
       if (hipEventCreateWithFlags(&ctx->ev_front, hipEventDisableTiming) != hipSuccess ||
           hipEventCreateWithFlags(&ctx->ev_pipe[0], hipEventDisableTiming) != hipSuccess ||
@@ -1186,7 +1189,7 @@ int pairwise_impl(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu_set *b
   // the totals' read-back and the emit — goes on ctx->front with the workspace set `par`, so it runs in
   // the tail of the previous call's task kernels instead of after its compaction; the task kernels wait
   // for it on the call's stream.  The counters of the front phase go to a scratch (never read back).
-  const bool pipe = slot >= 0 && ident_segs && !card_out &&
+  const bool pipe = RBG_PIPELINE && slot >= 0 && ident_segs && !card_out &&
                     std::min<uint64_t>(a->nc + b->nc, np * (uint64_t)seg_keys) <= kEarlyEmitTasks;
   int par = 0;
   hipStream_t fst = st;
@@ -1374,7 +1377,8 @@ int pairwise_impl(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu_set *b
     hipEvent_t done = nullptr;
     if (prc || hipMemsetAsync(ctx->d_stats, 0, kStatWords * kStripes * sizeof(uint64_t), st) ||
         hipEventCreateWithFlags(&done, hipEventDisableTiming) || hipEventRecord(done, st) ||
-        hipEventRecord(ctx->ev_pipe[par], st) || (ext && hipStreamWaitEvent(ext, done, 0)) || hipGetLastError()) {
+        (ctx->front && hipEventRecord(ctx->ev_pipe[par], st)) || (ext && hipStreamWaitEvent(ext, done, 0)) ||
+        hipGetLastError()) {
       if (done) (void)hipEventDestroy(done);
       (void)hipStreamSynchronize(st);
       rbgpu_set_free(res);

@@ -162,7 +162,7 @@ int bucket_pairs(const rbgpu_set64 *a, const rbgpu_set64 *b, int op, bool inplac
   return RB_OK;
 }
 
-// ---- ART codec (host only; scripts/art_host_check.py compiles this part alone)
+// ---- ART codec (host only; tests/test_art_host.py compiles this part alone)
 // Roaring64Bitmap.serialize: HighLowContainer = ART over the 6-byte high keys + Containers
 // (longlong/HighLowContainer.java:230-254, art/Art.java:309-391, art/Node*.java, art/Containers.java:210-303).
 // Little-endian fields (the writers reverse bytes around DataOutput), node type ordinals NODE4 / NODE16 /

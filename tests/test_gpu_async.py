@@ -70,10 +70,10 @@ def _digest(s):
 
 
 def test_async_pipeline_back_to_back(ctx, pairs):
-    """Pipelined calls (one segment per pair): call k+1's count / scan / emit run on the front stream while
-    call k's task kernels run, its workspaces alternating between two sets.  Eight calls in flight with
-    alternating ops (each workspace set reused by a different op), a synchronous call and an indexed
-    (non-pipelined) asynchronous call in between, each equal to the synchronous result."""
+    """Eight calls in flight with alternating ops, a synchronous call and an indexed asynchronous call in
+    between, each equal to the synchronous result.  In a build with RBG_PIPELINE=1 (api.hip) the identity-
+    paired calls are pipelined — call k+1's count / scan / emit on the front stream while call k's task
+    kernels run, the workspaces alternating between two sets — and this is the test of that schedule."""
     import roaringbitmap_amd as rb
     a, b = pairs
     ops = [rb.AND, rb.OR, rb.XOR, rb.ANDNOT, rb.OR, rb.AND, rb.ANDNOT, rb.XOR]
