@@ -23,9 +23,12 @@ def test_comm_wide_sharded_gather(ctx, oracle, comm):
     import roaringbitmap_amd as rb
     vals = load_realdata("census1881_srt")[:40] + synthetic_bitmaps(30, seed=3, max_keys=12, key_space=40)
     s = ctx.upload_values(vals, run_optimize=True)
+    refs = [oracle.RefBitmap.deserialize(x) for x in s.serialize()]
     for sem in (rb.FAST_OR, rb.FAST_XOR, rb.WORKSHY_AND, rb.PAR_OR, rb.NAIVE_AND):
         want = ctx.wide(sem, s)
         want_bytes = want.serialize()[0]
+        if sem in (rb.NAIVE_AND, rb.FAST_XOR):  # the shard path pinned to the oracle directly
+            assert want_bytes == oracle.wide(sem, refs).serialize()
         local, summ = comm.wide_sharded(sem, s, (0, 65536))
         assert summ["serialized_size"] == len(want_bytes)
         assert summ["cardinality"] == int(want.cardinalities()[0])
