@@ -50,7 +50,16 @@ def _containers_of(blob: bytes, meta=None):
     for i in range(n):
         key, card = kc[2 * i], kc[2 * i + 1] + 1
         if meta is not None and meta[i][2] == 0:
-            out.append((key, _ARRAY, 0, 0, b""))
+            # A kept-empty container keeps the type its xor produced: an empty Run xor Run is a Run
+            # (RunContainer.xor -> toEfficientContainer, RunContainer.java:2445-2482, 2326-2335: the
+            # 2 <= min(8192, 2) tie goes to Run), its payload the run count 0; an empty Array / Bitmap
+            # xor is an Array with no payload (ArrayContainer.java:1311-1336, BitmapContainer.java:1381-1422).
+            if runs[i]:
+                (nr,) = struct.unpack_from("<H", blob, pos)
+                out.append((key, _RUN, 0, nr, b""))
+                pos += 2 + 4 * nr
+            else:
+                out.append((key, _ARRAY, 0, 0, b""))
             continue
         if runs[i]:
             (nr,) = struct.unpack_from("<H", blob, pos)
@@ -124,7 +133,9 @@ class Ref64:
             b = R.RefBitmap.deserialize(data[pos:])
             pos += len(b.serialize())
             out.append((h, b))
-        out.sort(key=lambda hb: hb[0])  # kept in unsigned order; `signed` restores the map's order
+        # highToBitmap.put: the TreeMap orders the highs, a repeated high keeps the bitmap read last
+        last = {h: b for h, b in out}
+        out = sorted(last.items())  # kept in unsigned order; `signed` restores the map's order
         return cls(out, signed)
 
     def to_legacy(self) -> bytes:

@@ -53,6 +53,11 @@ int set_alloc(rbgpu_ctx *ctx, rbgpu_set *s, uint32_t nb, uint64_t nc, uint64_t p
 void set_release(rbgpu_set *s) {
   if (!s || !s->ctx) return;
   (void)settle(s); // an asynchronous result's kernels may still write its buffers
+  if (s->read_done) { // ... and a pending call that takes this set as an input may still read them
+    (void)hipEventSynchronize(s->read_done);
+    (void)hipEventDestroy(s->read_done);
+    s->read_done = nullptr;
+  }
   DevPool &p = s->ctx->pool;
   p.release(s->begin);
   p.release(s->key);
@@ -100,6 +105,7 @@ void ctx_unref(rbgpu_ctx *ctx) {
   delete ctx;
 }
 int settle(const rbgpu_set *cs) {
+  if (cs && cs->failed) return fail(RB_EDEVICE, "the asynchronous call that produced this set failed");
   if (!cs || !cs->pending) return RB_OK;
   rbgpu_set *s = const_cast<rbgpu_set *>(cs);
   rbgpu_ctx *ctx = s->ctx;
@@ -107,10 +113,15 @@ int settle(const rbgpu_set *cs) {
   const hipError_t e = hipEventSynchronize(s->pending);
   (void)hipEventDestroy(s->pending);
   s->pending = nullptr;
-  s->nc = ctx->h_async[s->pend_slot];
+  // the slot is only read when the call completed; a failed call leaves the set failed (sticky), not a
+  // set whose container count is whatever the pinned word held
+  s->nc = e == hipSuccess ? ctx->h_async[s->pend_slot] : 0;
   ctx->async_free.push_back(s->pend_slot);
   s->pend_slot = -1;
-  if (e != hipSuccess) return fail(RB_EDEVICE, "asynchronous call failed: %s", hipGetErrorString(e));
+  if (e != hipSuccess) {
+    s->failed = true;
+    return fail(RB_EDEVICE, "asynchronous call failed: %s", hipGetErrorString(e));
+  }
   return RB_OK;
 }
 int ensure_h_begin(const rbgpu_set *cs) {
@@ -1384,6 +1395,19 @@ int pairwise_impl(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu_set *b
       rbgpu_set_free(res);
       return fail(RB_EDEVICE, "asynchronous pairwise: enqueue failed");
     }
+    // the inputs stay allocated until the call is done with them: set_release waits for this
+    for (const rbgpu_set *in : {a, b}) {
+      rbgpu_set *m = const_cast<rbgpu_set *>(in);
+      if ((!m->read_done && hipEventCreateWithFlags(&m->read_done, hipEventDisableTiming)) ||
+          hipEventRecord(m->read_done, st)) {
+        (void)hipStreamSynchronize(st);
+        res->pending = done;
+        res->pend_slot = slot;
+        slot = -1;
+        rbgpu_set_free(res);
+        return fail(RB_EDEVICE, "asynchronous pairwise: enqueue failed");
+      }
+    }
     ctx->stats_clean = true;
     ctx->pipe_used[par] = true; // (a non-pipelined asynchronous call used set 0)
     res->pending = done;
@@ -1550,7 +1574,9 @@ static int empty_result(rbgpu_ctx *ctx, rbgpu_set **out) {
     return rc;
   }
   const uint64_t hb[2] = {0, 0};
-  HIPCHK(hipMemcpy(e->begin, hb, 16, hipMemcpyHostToDevice));
+  // on the library stream (it is non-blocking: a null-stream copy would not be ordered after its kernels)
+  HIPCHK(hipMemcpyAsync(e->begin, hb, 16, hipMemcpyHostToDevice, ctx->stream));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
   e->h_begin = {0, 0};
   *out = e;
   return RB_OK;

@@ -204,6 +204,10 @@ struct rbgpu_set {
   // `pend_slot` when `pending` completes (settle() waits for it and fills nc)
   hipEvent_t pending = nullptr;
   int pend_slot = -1;
+  bool failed = false;            // its asynchronous call failed: every later use reports RB_EDEVICE
+  // the last asynchronous call that reads this set as an input completes at `read_done` (its kernels may
+  // still read the buffers after the call returned): freeing the set waits for it
+  hipEvent_t read_done = nullptr;
   double derive_ms = 0.0;         // device time spent building mrec / krec (reported, not hidden)
   uint64_t derive_bytes = 0;      // their algorithmic bytes (metadata read + records written)
   rbg::SetView view() const { return rbg::SetView{begin, key, type, card, nruns, off, payload}; }

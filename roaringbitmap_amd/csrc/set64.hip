@@ -90,7 +90,8 @@ rbgpu_set *empty_set(rbgpu_ctx *ctx) {
     return nullptr;
   }
   const uint64_t z = 0;
-  if (hipMemcpy(s->begin, &z, 8, hipMemcpyHostToDevice) != hipSuccess) {
+  if (hipMemcpyAsync(s->begin, &z, 8, hipMemcpyHostToDevice, ctx->stream) != hipSuccess ||
+      hipStreamSynchronize(ctx->stream) != hipSuccess) {
     rbgpu_set_free(s);
     return nullptr;
   }
@@ -799,11 +800,7 @@ int rbgpu_set64_from_legacy(rbgpu_ctx *ctx, const uint8_t *const *bufs, const ui
       delete s;
       return fail(RB_EFORMAT, "64-bit bitmap %u: truncated", i);
     }
-    if (p[0] > 1) {
-      delete s;
-      return fail(RB_EFORMAT, "64-bit bitmap %u: bad signedLongs byte", i);
-    }
-    const bool sgn = p[0] != 0;
+    const bool sgn = p[0] != 0; // DataInput.readBoolean: any non-zero byte is true
     const uint32_t nb = be32(p + 1);
     uint64_t pos = 5;
     std::vector<std::pair<uint32_t, uint64_t>> ent; // (high, blob index) in the map's order
@@ -819,11 +816,6 @@ int rbgpu_set64_from_legacy(rbgpu_ctx *ctx, const uint8_t *const *bufs, const ui
         delete s;
         return fail(RB_EFORMAT, "64-bit bitmap %u: bucket %llu is not a RoaringBitmap", i, (unsigned long long)k);
       }
-      // the map's comparator order (signed or unsigned ints), strictly increasing (TreeMap keys)
-      if (!ent.empty() && (sgn ? (int32_t)h <= (int32_t)ent.back().first : h <= ent.back().first)) {
-        delete s;
-        return fail(RB_EINVAL, "64-bit bitmap %u: bucket highs not strictly increasing", i);
-      }
       ent.push_back({h, blobs.size()});
       blobs.push_back(p + pos);
       blens.push_back(bl);
@@ -833,10 +825,14 @@ int rbgpu_set64_from_legacy(rbgpu_ctx *ctx, const uint8_t *const *bufs, const ui
       delete s;
       return fail(RB_EFORMAT, "64-bit bitmap %u: %llu trailing bytes", i, (unsigned long long)(len - pos));
     }
+    // highToBitmap.put(high, bitmap) per entry (:1309-1320): the TreeMap orders the highs whatever the
+    // stream's order, and a repeated high keeps the bitmap read last (kept here in unsigned order; the
+    // map's signed order is applied on output)
     std::stable_sort(ent.begin(), ent.end(), [](const auto &x, const auto &y) { return x.first < y.first; });
-    for (const auto &e : ent) {
-      s->high.push_back(e.first);
-      s->idx.push_back((uint32_t)e.second);
+    for (size_t e = 0; e < ent.size(); ++e) {
+      if (e + 1 < ent.size() && ent[e + 1].first == ent[e].first) continue; // replaced by a later put
+      s->high.push_back(ent[e].first);
+      s->idx.push_back((uint32_t)ent[e].second);
     }
     s->begin.push_back(s->high.size());
     s->sgn.push_back(sgn);

@@ -644,6 +644,8 @@ class HostTransport:
         import torch
         self.dist, self.group = dist, group
         self.rank, self.world = dist.get_rank(group), dist.get_world_size(group)
+        # the library numbers peers within the group; torch.distributed's send / recv take global ranks
+        glob = (lambda p: p) if group is None else (lambda p: dist.get_global_rank(group, p))
 
         def all_gather(_user, send, recv, nbytes):
             try:
@@ -670,7 +672,7 @@ class HostTransport:
 
         def send(_user, buf, nbytes, peer):
             try:
-                dist.send(torch.frombuffer(bytearray(C.string_at(buf, int(nbytes))), dtype=torch.uint8), dst=int(peer),
+                dist.send(torch.frombuffer(bytearray(C.string_at(buf, int(nbytes))), dtype=torch.uint8), dst=glob(int(peer)),
                           group=group)
                 return 0
             except Exception:  # noqa: BLE001
@@ -679,7 +681,7 @@ class HostTransport:
         def recv(_user, buf, nbytes, peer):
             try:
                 t = torch.zeros(int(nbytes), dtype=torch.uint8)
-                dist.recv(t, src=int(peer), group=group)
+                dist.recv(t, src=glob(int(peer)), group=group)
                 C.memmove(buf, bytes(t.numpy().tobytes()), int(nbytes))
                 return 0
             except Exception:  # noqa: BLE001

@@ -43,6 +43,28 @@ def test_async_free_pending_and_chain(ctx, pairs, oracle):
     assert int(x.wait().n_containers) == int(ctx.pairwise(rb.AND, a, b).n_containers)
 
 
+def test_async_input_freed_before_wait(ctx, pairs):
+    """an input freed while an asynchronous call still reads it.  The free waits for the
+    context's pending work before its blocks return to the pool, so sets allocated right after (their
+    blocks recycled, written by an upload and an empty result) do not overwrite what the pending kernels
+    read: the result equals the synchronous one."""
+    import roaringbitmap_amd as rb
+    a, b = pairs
+    a2 = ctx.pairwise(rb.OR, a, a)   # fresh sets with a's / b's values
+    b2 = ctx.pairwise(rb.OR, b, b)
+    want = {op: _digest(ctx.pairwise(op, a2, b2)) for op in (rb.OR, rb.XOR)}
+    r1 = ctx.pairwise_async(rb.OR, a2, b2)
+    r2 = ctx.pairwise_async(rb.XOR, a2, b2)
+    a2.close()
+    b2.close()
+    junk = [ctx.pairwise(rb.AND, a, a), ctx.upload_values([np.arange(0, 70000, 7, dtype=np.uint32)] * 8),
+            ctx.pairwise(rb.AND, a, b, np.zeros(0, np.uint32), np.zeros(0, np.uint32))]
+    assert _digest(r1.wait()) == want[rb.OR]
+    assert _digest(r2.wait()) == want[rb.XOR]
+    for x in junk + [r1, r2]:
+        x.close()
+
+
 def test_async_caller_stream_and_small_batch(ctx, pairs, oracle):
     import torch
 

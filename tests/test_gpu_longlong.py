@@ -224,6 +224,28 @@ def test_roaring64_legacy_format_and_cardinality(ctx, oracle, seed):
         ctx.upload_legacy64([blobs[0][:-1]])
 
 
+def test_roaring64_legacy_hand_built_streams(ctx, oracle):
+    """deserializeLegacy (Roaring64NavigableMap.java:1295-1324) reads the flag with readBoolean
+    (any non-zero byte is true) and puts each (high, bitmap) into a TreeMap: highs in any stream order are
+    ordered by the map and a repeated high keeps the bitmap read last.  A hand-built stream with flag byte 7,
+    highs 9, 2, 9, 5 reads back as the oracle's map (signed, highs 2 / 5 / 9, the second bitmap of 9)."""
+    import struct
+
+    from oracle import rbref as R
+    from oracle import rbref64 as R64
+    parts = [(9, [1, 2, 3]), (2, [7]), (9, [100, 200]), (5, list(range(70000, 90000)))]
+    blob = bytes([7]) + struct.pack(">i", len(parts)) + b"".join(
+        struct.pack(">I", h) + R.RefBitmap.of(np.array(v, np.uint32)).serialize() for h, v in parts)
+    want = R64.Ref64.from_legacy(blob)
+    assert want.signed and [h for h, _ in want.buckets] == [2, 5, 9]
+    s = ctx.upload_legacy64([blob])
+    assert s.signed_longs(0)
+    assert list(s.highs(0)) == [2, 5, 9]
+    assert s.serialize_legacy() == [want.to_legacy()]
+    assert s.serialize_portable() == [want.to_portable()]
+    assert np.array_equal(s.values(0), want.to_array())
+
+
 def test_roaring64_navigable_mirror_legacy(ctx, oracle):
     """TestRoaring64NavigableMap.testSerialization_MultipleBuckets_Signed / _Unsigned (:741-773) through
     the mirror: serialize() is the legacy format, deserialize() restores the map and its value order."""
@@ -274,6 +296,38 @@ def test_roaring64_art_format(ctx, oracle):
     assert np.array_equal(y.toArray(), x.toArray())
     with pytest.raises(rb.FormatError):
         ctx.upload_art64([blobs[2][:-1]])
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3, 5])
+def test_roaring64_kept_empty_container_types(ctx, oracle, seed):
+    """Every container of a static Roaring64Bitmap.xor(x_i, x_j) — the kept-empty ones included — has the
+    oracle's key, type, cardinality and run count in the device's bucket view (rbgpu_set64_bucket_set ->
+    download), i.e. the kernel's type choice, apart from any writer: an empty Run xor Run is a Run, an
+    empty Array / Bitmap xor an Array (RunContainer.java:2445-2482, 2326-2335; ArrayContainer.java:
+    1311-1336; BitmapContainer.java:1381-1422; Roaring64Bitmap.java:421-460 puts with no isEmpty check).
+    Seed 5 is GPUTEST_r04's failing pool."""
+    import roaringbitmap_amd as rb
+    from oracle import rbref64 as R64
+    p, refs = _pool(ctx, oracle, seed, n=6)
+    n = len(refs)
+    ai = np.array([i for i in range(n) for j in range(n)], np.uint32)
+    bi = np.array([j for i in range(n) for j in range(n)], np.uint32)
+    res = ctx.pairwise64(rb.RB64_BITMAP, rb.XOR, p, p, ai, bi)
+    kept_empty = {0: 0, 2: 0}
+    for k in range(len(ai)):
+        want = R64.bitmap_op(rb.XOR, refs[int(ai[k])], refs[int(bi[k])], False)
+        assert [int(h) for h in res.highs(k)] == [h for h, _ in want.buckets], k
+        if not want.buckets:
+            continue
+        h = res.bucket_set(k).download()
+        got = [(int(h.key[c]), int(h.type[c]), int(h.card[c]), int(h.nruns[c])) for c in range(len(h.key))]
+        exp = [c for _, b in want.buckets for c in b.containers()]
+        assert got == exp, (int(ai[k]), int(bi[k]))
+        for c in exp:
+            if c[2] == 0:
+                kept_empty[c[1]] = kept_empty.get(c[1], 0) + 1
+    if seed == 5:  # the pool holds both kinds of kept-empty containers
+        assert kept_empty[0] > 0 and kept_empty[2] > 0, kept_empty
 
 
 def test_roaring64_kept_empty_through_later_ops(ctx, oracle):

@@ -161,3 +161,30 @@ def test_oracle64_art_format():
     assert [r.to_art()[9] for r in _art_sets()[3:6]] == [1, 2, 3]
     with pytest.raises((IOError, Exception)):
         R64.Ref64.from_art(two[:-1])
+
+
+def test_oracle64_art_kept_empty_types():
+    """Roaring64Bitmap.xor(x, x) keeps every container empty under its key (Roaring64Bitmap.java:421-460:
+    put with no isEmpty check) with the type its container xor returns: an empty Run xor Run is a Run
+    (RunContainer.java:2445-2482 -> toEfficientContainer :2326-2335, 2 + 4*0 <= min(8192, 2*0 + 2), the tie
+    goes to Run), an empty Array xor Array or Bitmap xor Bitmap an Array (ArrayContainer.java:1311-1336,
+    BitmapContainer.java:1381-1422).  The ART stream carries that type byte (art/Containers.java: 0 Run with
+    its run count, 2 Array) — the case GPUTEST_r04 found the restatement typing every empty container as an
+    Array."""
+    from oracle import rbref64 as R64
+    run = np.arange(100, 20000, dtype=np.uint64)                      # one Run after runOptimize
+    arr = (np.uint64(1) << np.uint64(16)) + np.arange(0, 900, 3, dtype=np.uint64)      # an Array
+    bmp = (np.uint64(2) << np.uint64(16)) + np.arange(0, 60000, 3, dtype=np.uint64)    # a Bitmap
+    x = R64.Ref64.of(np.concatenate([run, arr, bmp]))
+    for _, b in x.buckets:
+        b.run_optimize()
+    assert [c[1] for c in x.buckets[0][1].containers()] == [2, 0, 1]   # Run, Array, Bitmap (rbref enum)
+    r = R64.bitmap_op(R64.XOR, x, x, False)
+    assert [(c[1], c[2]) for c in r.buckets[0][1].containers()] == [(2, 0), (0, 0), (0, 0)]
+    art = r.to_art()
+    # three leaves after the Node4 root; the container array follows: 1 first-level array, 0xFE, 3 slots
+    at = art.index(bytes([1, 0, 0, 0, 0xFE, 3, 0, 0, 0])) + 9
+    assert art[at:at + 8] == bytes([1, 0, 0, 0, 0, 0, 0, 0])          # NOT_NULL, Run, card 0, nbrruns 0
+    assert art[at + 8:at + 14] == bytes([1, 2, 0, 0, 0, 0])           # NOT_NULL, Array, card 0
+    assert art[at + 14:at + 20] == bytes([1, 2, 0, 0, 0, 0])
+    assert R64.Ref64.from_art(art).buckets == []                     # no values

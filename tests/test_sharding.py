@@ -437,3 +437,45 @@ def test_gloo_host_transport_exchange_in_c(world):
         errs = out[f"errors{r}"]
         # summarize (the last rank's null shard), gather (the root's small destination), naive_and order
         assert len(errs) == 3, (r, errs)
+
+
+def _rank_host_comm_subgroup(rank, world, port, q):
+    """a HostTransport over a non-default group maps the library's group-relative peers to the
+    global ranks torch.distributed's send / recv take.  World 3, the group {1, 2}: global rank 1 is the
+    group's root, so a gather with group-relative peers sent as global ones would reach rank 0 / hang."""
+    import torch.distributed as dist
+
+    from oracle import rbref as R
+    from roaringbitmap_amd.engine import HostComm, HostTransport
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    comm = None
+    try:
+        grp = dist.new_group([1, 2])
+        if rank == 0:
+            q.put(torch_obj_recv(dist, 1))
+            return
+        comm = HostComm(HostTransport(dist, grp))
+        one = np.concatenate([(k << 16) + (np.arange(100, 3000) if k % 2 else np.arange(0, 4000, 7))
+                              for k in range(12)]).astype(np.uint32)
+        ref = R.RefBitmap.of(one)
+        ref.run_optimize()
+        v = ref.to_array()
+        lo, hi = (0, 5) if comm.rank == 0 else (5, 12)
+        sub = R.RefBitmap.of(v[((v >> 16) >= lo) & ((v >> 16) < hi)])
+        sub.run_optimize()
+        summ = comm.summarize_serialized(sub.serialize())
+        data = comm.gather_host(sub.serialize(), summ)
+        if comm.rank == 0:
+            torch_obj_send(dist, {"rank": rank, "group_rank": comm.rank, "world": comm.nranks,
+                                  "ok": data == ref.serialize(), "card": summ["cardinality"] == ref.cardinality()})
+    finally:
+        if comm is not None:
+            comm.close()
+        dist.destroy_process_group()
+
+
+def test_gloo_host_transport_subgroup():
+    out = _spawn(_rank_host_comm_subgroup, world=3)
+    assert out == {"rank": 1, "group_rank": 0, "world": 2, "ok": True, "card": True}
