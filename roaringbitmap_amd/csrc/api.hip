@@ -77,15 +77,6 @@ void ctx_unref(rbgpu_ctx *ctx) {
   (void)hipSetDevice(ctx->device);
   (void)hipStreamSynchronize(ctx->stream);
   if (ctx->side) (void)hipStreamSynchronize(ctx->side);
-  if (ctx->front) {
-    (void)hipStreamSynchronize(ctx->front);
-    (void)hipEventDestroy(ctx->ev_front);
-    for (auto &e : ctx->ev_pipe) (void)hipEventDestroy(e);
-    (void)hipFree(ctx->d_stats_front);
-    ctx->ws_tasks2.destroy();
-    ctx->ws_segs2.destroy();
-    (void)hipStreamDestroy(ctx->front);
-  }
   for (auto &e : ctx->ev) (void)hipEventDestroy(e);
   for (auto &e : ctx->ev_side) (void)hipEventDestroy(e);
   (void)hipEventDestroy(ctx->ev_tot);
@@ -1077,9 +1068,6 @@ static // tasks bound up to which pairwise_impl reserves the task workspace befo
 // mostly disjoint keys — and the workspace stays grown, so the cap is set just above config 2's 6.1M)
 constexpr uint64_t kEarlyEmitTasks = 1ull << 23;
 
-#ifndef RBG_PIPELINE
-#define RBG_PIPELINE 0 // the pipelined front phase: implemented, not yet measured on the GPU (off until it is)
-#endif
 // async: return once the task kernels and the compaction are enqueued (rbgpu_pairwise_async): the result
 // is pending (settle() fills its container count), the call's counters are not read back (rb_stats keeps
 // the last synchronous call's), and `ext` (if any, another stream of the caller) is ordered around the call.
@@ -1120,16 +1108,6 @@ int pairwise_impl(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu_set *b
       if (hipHostMalloc((void **)&ctx->h_async, kAsyncSlots * sizeof(uint64_t)) != hipSuccess)
         return fail(RB_ENOMEM, "pinned result-count slots");
       for (int i = kAsyncSlots - 1; i >= 0; --i) ctx->async_free.push_back(i);
-    }
-    if (RBG_PIPELINE && !ctx->front) { // the pipeline's stream, events and counter scratch (see `pipe` below)
-      hipStream_t fs = nullptr;
-      if (hipEventCreateWithFlags(&ctx->ev_front, hipEventDisableTiming) != hipSuccess ||
-          hipEventCreateWithFlags(&ctx->ev_pipe[0], hipEventDisableTiming) != hipSuccess ||
-          hipEventCreateWithFlags(&ctx->ev_pipe[1], hipEventDisableTiming) != hipSuccess ||
-          hipMalloc((void **)&ctx->d_stats_front, kStatWords * kStripes * sizeof(uint64_t)) != hipSuccess ||
-          hipStreamCreateWithFlags(&fs, hipStreamNonBlocking) != hipSuccess)
-        return fail(RB_EDEVICE, "asynchronous pipeline setup failed");
-      ctx->front = fs;
     }
     if (!ctx->async_free.empty()) {
       slot = ctx->async_free.back();
@@ -1196,24 +1174,6 @@ int pairwise_impl(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu_set *b
   // pair): seg_begin is the identity and the count kernel, its scan and the read-back are skipped
   const bool ident_segs = !host_segs && np && !a_idx && !b_idx && !ensure_max_keys(a) && !ensure_max_keys(b) &&
                           (uint64_t)(a->max_keys + b->max_keys) <= seg_keys;
-  // Pipelined asynchronous call (one segment per pair, early emission): the front phase — count, scans,
-  // the totals' read-back and the emit — goes on ctx->front with the workspace set `par`, so it runs in
-  // the tail of the previous call's task kernels instead of after its compaction; the task kernels wait
-  // for it on the call's stream.  The counters of the front phase go to a scratch (never read back).
-  const bool pipe = RBG_PIPELINE && slot >= 0 && ident_segs && !card_out &&
-                    std::min<uint64_t>(a->nc + b->nc, np * (uint64_t)seg_keys) <= kEarlyEmitTasks;
-  int par = 0;
-  hipStream_t fst = st;
-  uint64_t *cstats = ctx->d_stats;
-  if (pipe) {
-    par = ctx->pipe_par;
-    ctx->pipe_par ^= 1;
-    // the last call that used this workspace set (two pipelined calls back) has completed
-    if (ctx->pipe_used[par]) HIPCHK(hipEventSynchronize(ctx->ev_pipe[par]));
-    fst = ctx->front;
-    if (ext) HIPCHK(hipStreamWaitEvent(fst, ctx->ev_ext, 0));
-    cstats = ctx->d_stats_front;
-  }
   if (host_segs) {
     ns = reinterpret_cast<const uint64_t *>(ctx->h_stage + np * 4 * ((d_aidx != nullptr) + (d_bidx != nullptr)))[np];
   } else if (ident_segs) {
@@ -1229,8 +1189,8 @@ int pairwise_impl(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu_set *b
   // ---- per segment: counts, block totals and their scans, result counts / offsets
   const uint64_t nblk = pair_blocks(ns);
   need = aligned256(ns * 4) + 3 * aligned256((ns + 1) * 8) + 10 * aligned256((nblk + 1) * 8) + 4 * 256;
-  Workspace &G = par ? ctx->ws_segs2 : ctx->ws_segs;
-  if (G.reserve(need, fst) != hipSuccess) return fail(RB_ENOMEM, "segment workspace");
+  Workspace &G = ctx->ws_segs;
+  if (G.reserve(need, st) != hipSuccess) return fail(RB_ENOMEM, "segment workspace");
   uint32_t *seg_pair = G.take<uint32_t>(std::max<uint64_t>(ns, 1));
   uint64_t *cnt = G.take<uint64_t>(ns + 1); // per segment, packed (pack_seg_counts)
   PairCountArrays bt{G.take<uint64_t>(nblk + 1), G.take<uint64_t>(nblk + 1), G.take<uint64_t>(nblk + 1),
@@ -1244,13 +1204,13 @@ int pairwise_impl(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu_set *b
   if (!ident_segs) launch_seg_fill(pa, seg_begin, seg_pair, st);
   pa.seg_pair = ident_segs ? nullptr : seg_pair;
   pa.nseg = ns;
-  launch_pair_count(pa, cnt, bt, cstats, fst);
+  launch_pair_count(pa, cnt, bt, ctx->d_stats, st);
   if (ns) {
     const uint64_t *scan_in[4] = {bt.task, bt.light, bt.big, bt.small};
     uint64_t *scan_out[4] = {bs.task, bs.light, bs.big, bs.small};
-    scan_blocks_multi(scan_in, scan_out, 4, nblk, d_tot, fst);
+    scan_blocks_multi(scan_in, scan_out, 4, nblk, d_tot, st);
   }
-  HIPCHK(hipMemcpyAsync(tot, d_tot, 4 * 8, hipMemcpyDeviceToHost, fst));
+  HIPCHK(hipMemcpyAsync(tot, d_tot, 4 * 8, hipMemcpyDeviceToHost, st));
   // Early emission: with identity pairing every container of A and of B takes at most one task, so
   // a.nc + b.nc bounds the task count before the totals are on the host.  The task workspace is then
   // sized by that bound and the emit kernel reads the totals on the device: it runs while the host
@@ -1272,8 +1232,8 @@ int pairwise_impl(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu_set *b
     const uint64_t nt1 = std::max<uint64_t>(nt, 1);
     const size_t tneed = aligned256(nt1 * sizeof(TaskRec)) + aligned256(nt1) + 2 * aligned256(nt1 * 8) +
                          aligned256(kQueueWords * 8) + 256;
-    Workspace &T = par ? ctx->ws_tasks2 : ctx->ws_tasks;
-    if (T.reserve(tneed, fst) != hipSuccess)
+    Workspace &T = ctx->ws_tasks;
+    if (T.reserve(tneed, st) != hipSuccess)
       return fail(RB_ENOMEM, "task workspace (%llu tasks)", (unsigned long long)nt);
     light = T.take<TaskRec>(nt1);
     tm.type = T.take<uint8_t>(nt1);
@@ -1284,13 +1244,9 @@ int pairwise_impl(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu_set *b
   };
   if (early) {
     if ((rc = take_tasks(tbound))) return rc;
-    HIPCHK(hipEventRecord(ctx->ev_tot, fst));
+    HIPCHK(hipEventRecord(ctx->ev_tot, st));
     launch_pair_emit(pa, cnt, bs, 0, light, nullptr, tm, task_begin, d_tot, tbound, queue,
-                     fst);
-    if (pipe) { // the call's stream (its task kernels, compaction) after the front phase
-      HIPCHK(hipEventRecord(ctx->ev_front, fst));
-      HIPCHK(hipStreamWaitEvent(st, ctx->ev_front, 0));
-    }
+                     st);
     HIPCHK(hipEventSynchronize(ctx->ev_tot));
   } else {
     HIPCHK(hipStreamSynchronize(st));
@@ -1388,7 +1344,7 @@ int pairwise_impl(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu_set *b
     hipEvent_t done = nullptr;
     if (prc || hipMemsetAsync(ctx->d_stats, 0, kStatWords * kStripes * sizeof(uint64_t), st) ||
         hipEventCreateWithFlags(&done, hipEventDisableTiming) || hipEventRecord(done, st) ||
-        (ctx->front && hipEventRecord(ctx->ev_pipe[par], st)) || (ext && hipStreamWaitEvent(ext, done, 0)) ||
+        (ext && hipStreamWaitEvent(ext, done, 0)) ||
         hipGetLastError()) {
       if (done) (void)hipEventDestroy(done);
       (void)hipStreamSynchronize(st);
@@ -1409,7 +1365,6 @@ int pairwise_impl(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu_set *b
       }
     }
     ctx->stats_clean = true;
-    ctx->pipe_used[par] = true; // (a non-pipelined asynchronous call used set 0)
     res->pending = done;
     res->pend_slot = slot;
     slot = -1; // the result owns it now

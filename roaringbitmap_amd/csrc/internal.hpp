@@ -164,17 +164,6 @@ struct rbgpu_ctx {
   // pinned words the asynchronous calls' result counts land in (kAsyncSlots, a free list)
   uint64_t *h_async = nullptr; // [kAsyncSlots]
   std::vector<int> async_free;
-  // Pipelined asynchronous calls (rbgpu_pairwise_async, one segment per pair): a call's front phase
-  // (count, scans, task emission) runs on `front` while the previous call's task kernels still run on
-  // `stream`, so its workspaces alternate between two sets; ev_pipe[p] marks the end of the last
-  // call that used set p (its compaction), pipe_par the set the next pipelined call takes.
-  hipStream_t front = nullptr;
-  hipEvent_t ev_front = {};   // after a pipelined call's emit: its task kernels wait on it
-  hipEvent_t ev_pipe[2] = {};
-  bool pipe_used[2] = {false, false};
-  int pipe_par = 0;
-  rbg::Workspace ws_tasks2, ws_segs2; // the second workspace set
-  uint64_t *d_stats_front = nullptr;  // the front phase's counters (not read back: async calls report none)
 };
 
 struct rbgpu_set {

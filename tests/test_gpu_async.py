@@ -91,11 +91,10 @@ def _digest(s):
     return (s.cardinalities().tobytes(), s.serialized_sizes().tobytes(), s.type_stats(), int(s.n_containers), wins)
 
 
-def test_async_pipeline_back_to_back(ctx, pairs):
+def test_async_back_to_back(ctx, pairs):
     """Eight calls in flight with alternating ops, a synchronous call and an indexed asynchronous call in
-    between, each equal to the synchronous result.  In a build with RBG_PIPELINE=1 (api.hip) the identity-
-    paired calls are pipelined — call k+1's count / scan / emit on the front stream while call k's task
-    kernels run, the workspaces alternating between two sets — and this is the test of that schedule."""
+    between, each equal to the synchronous result (the calls share the context's workspaces in stream
+    order)."""
     import roaringbitmap_amd as rb
     a, b = pairs
     ops = [rb.AND, rb.OR, rb.XOR, rb.ANDNOT, rb.OR, rb.AND, rb.ANDNOT, rb.XOR]
@@ -116,7 +115,7 @@ def test_async_pipeline_back_to_back(ctx, pairs):
         r.close()
 
 
-def test_async_pipeline_release_order(ctx, pairs):
+def test_async_release_order(ctx, pairs):
     """The bench's pattern: each step's result freed one step later (its free waits for it), 12 steps."""
     import roaringbitmap_amd as rb
     a, b = pairs
