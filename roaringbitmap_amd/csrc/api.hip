@@ -979,9 +979,10 @@ static int pairwise_small(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgp
   hipStream_t st = ctx->stream;
   const bool card_only = out == nullptr;
   const uint64_t E1 = std::max<uint64_t>(E, 1);
+  const size_t argb = nslot + nidx + 4ull * nblocks; // slot table, indices, block table
   const size_t need = aligned256(8ull * np) + aligned256(4 * E1) + aligned256(2 * E1) + aligned256(E1 + 32) +
                       aligned256(4 * E1) + aligned256(2 * E1) + aligned256(32ull * nblocks) +
-                      aligned256(8ull * (np + 1)) + 256;
+                      aligned256(8ull * (np + 1)) + aligned256(argb) + 256;
   if (ctx->ws_pairs.reserve(need, st) != hipSuccess) return fail(RB_ENOMEM, "pair workspace");
   Workspace &W = ctx->ws_pairs;
   SmallPairArgs sa{};
@@ -993,6 +994,16 @@ static int pairwise_small(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgp
   sa.bidx = b_idx ? d_idx + (a_idx ? np : 0) : nullptr;
   sa.np = np;
   sa.blk = reinterpret_cast<const uint32_t *>(ctx->d_small + (reinterpret_cast<uint8_t *>(blk) - ctx->h_small));
+  const char *dv = getenv("RBGPU_SMALL_DEVARGS");
+  if (dv && dv[0] == '1') { // study: the argument tables copied to device memory first
+    uint8_t *dargs = W.take<uint8_t>(argb);
+    HIPCHK(hipMemcpyAsync(dargs, ctx->h_small + nout, argb, hipMemcpyHostToDevice, st));
+    sa.slot = reinterpret_cast<const uint64_t *>(dargs);
+    const uint32_t *di = reinterpret_cast<const uint32_t *>(dargs + nslot);
+    sa.aidx = a_idx ? di : nullptr;
+    sa.bidx = b_idx ? di + (a_idx ? np : 0) : nullptr;
+    sa.blk = reinterpret_cast<const uint32_t *>(dargs + (reinterpret_cast<uint8_t *>(blk) - (ctx->h_small + nout)));
+  }
   sa.cap = cap;
   sa.pcard = card_out ? W.take<uint64_t>(np) : nullptr;
   uint32_t *xpos = W.take<uint32_t>(E1);

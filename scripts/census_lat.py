@@ -19,11 +19,12 @@ from datasets import load_realdata  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--calls", type=int, default=400)
+    ap.add_argument("--npairs", type=int, default=0, help="first N pairs only (0: all 199)")
     args = ap.parse_args()
     ctx = rb.Context(0)
     vals = load_realdata("census1881")
     s = ctx.upload_values(vals)
-    n = len(vals) - 1
+    n = args.npairs or len(vals) - 1
     ai = np.arange(n, dtype=np.uint32)
     bi = ai + 1
     res = {}
