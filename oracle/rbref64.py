@@ -100,6 +100,25 @@ def _blob_of(conts) -> bytes:
     return head + b"".join(bodies)
 
 
+def _bitmap_of(conts) -> "R.RefBitmap":
+    """The RefBitmap of [(key, type, card, nruns, payload)], empty Array / Run containers included: those are
+    made the way the reference makes them, as the xor of two equal one-value containers of that type (the
+    bitmap's other containers, unmatched, are cloned with their types)."""
+    if all(c[2] for c in conts):
+        return R.RefBitmap.deserialize(_blob_of(conts))
+    full, ph = [], []
+    for key, t, card, nr, payload in conts:
+        if card:
+            full.append((key, t, card, nr, payload))
+            continue
+        if t == _BITMAP or nr:
+            raise IOError("non-canonical empty container")
+        x = (key, _RUN, 1, 1, struct.pack("<HH", 0, 0)) if t == _RUN else (key, _ARRAY, 1, 0, struct.pack("<H", 0))
+        full.append(x)
+        ph.append(x)
+    return R.xor_keep_empty(R.RefBitmap.deserialize(_blob_of(full)), R.RefBitmap.deserialize(_blob_of(ph)))
+
+
 class Ref64:
     """[(high, RefBitmap)] in ascending unsigned high order; `signed`: Roaring64NavigableMap's signedLongs
     (its TreeMap then iterates the highs as signed ints, which fixes the serialized bucket order)."""
@@ -245,10 +264,10 @@ class Ref64:
         groups = {}
         for key48, idx in sorted(leaves):
             typ, card, nr, payload = conts[idx]
-            if card == 0:
-                continue  # a kept-empty xor container holds no value (absent from the bucket view)
+            # an empty container (a kept-empty xor result) is kept: Containers.deserialize reads it back
+            # like any other (art/Containers.java:276-303)
             groups.setdefault(key48 >> 16, []).append((key48 & 0xFFFF, typ, card, nr, payload))
-        return cls([(h, R.RefBitmap.deserialize(_blob_of(cs))) for h, cs in sorted(groups.items())])
+        return cls([(h, _bitmap_of(cs)) for h, cs in sorted(groups.items())])
 
     def to_art(self, slots=None, cap=None) -> bytes:
         """Roaring64Bitmap.serialize (:880-882) of the bitmap built by inserting its containers in ascending

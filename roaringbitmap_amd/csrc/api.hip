@@ -623,6 +623,14 @@ int rbgpu_set_from_serialized_device(rbgpu_ctx *ctx, const uint8_t *d_bytes, con
 }
 
 int rbgpu_set_from_soa(rbgpu_ctx *ctx, const rb_soa *soa, rbgpu_set **out) {
+  return rbg::set_from_soa(ctx, soa, out, false);
+}
+}  // extern "C"
+
+namespace rbg {
+// allow_empty: an empty Array (card 0, no payload) or Run (card 0, no runs) is kept — the containers a
+// Roaring64Bitmap xor leaves under their keys, read back from its own serialized form (set64.hip)
+int set_from_soa(rbgpu_ctx *ctx, const rb_soa *soa, rbgpu_set **out, bool allow_empty) {
   int rc = check_ctx(ctx);
   if (rc) return rc;
   if (!soa || !out) return fail(RB_EINVAL, "null argument");
@@ -645,13 +653,17 @@ int rbgpu_set_from_soa(rbgpu_ctx *ctx, const rb_soa *soa, rbgpu_set **out) {
   for (uint64_t i = 0; i < nc; ++i) {
     const uint64_t bytes = payload_bytes(h.type[i], h.card[i], h.nruns[i]);
     if (soa->offset[i] + bytes > soa->payload_bytes) return fail(RB_EINVAL, "container %llu payload out of range", (unsigned long long)i);
-    rc = validate_container(h.type[i], h.card[i], h.nruns[i], soa->payload + soa->offset[i], err);
+    const bool empty_ok = allow_empty && h.card[i] == 0 && h.type[i] != RB_BITMAP && h.nruns[i] == 0;
+    rc = empty_ok ? RB_OK : validate_container(h.type[i], h.card[i], h.nruns[i], soa->payload + soa->offset[i], err);
     if (rc) return fail(rc, "container %llu: %s", (unsigned long long)i, err.c_str());
     h.off[i] = soa->offset[i];
   }
   h.payload.assign(soa->payload, soa->payload + soa->payload_bytes);
   return upload_host(ctx, h, out);
 }
+}  // namespace rbg
+
+extern "C" {
 
 void rbgpu_set_free(rbgpu_set *set) {
   if (!set) return;

@@ -214,6 +214,8 @@ int ensure_h_begin(const rbgpu_set *s);
 // A set returned by rbgpu_pairwise_async is usable by the host once its work is done: every entry point
 // that reads a set first settles it (waits, fills nc).  A no-op for every other set.
 int settle(const rbgpu_set *s);
+// rbgpu_set_from_soa; allow_empty keeps empty Array / Run containers (a Roaring64Bitmap's kept-empty ones)
+int set_from_soa(rbgpu_ctx *ctx, const rb_soa *soa, rbgpu_set **out, bool allow_empty);
 constexpr int kAsyncSlots = 256; // asynchronous results pending at once per context (more: complete synchronously)
 #define SETTLE(...)                                                                                    \
   do {                                                                                                 \

@@ -437,10 +437,12 @@ int rbgpu_set64_from_art(rbgpu_ctx *ctx, const uint8_t *const *bufs, const uint6
     const uint64_t len = lens[i];
     std::vector<ArtCont> conts;
     if (const char *why = art_parse(p, len, conts)) return bad(i, why);
-    // buckets: the containers grouped by their high 32 bits (a kept-empty container holds no value: skipped)
+    // buckets: the containers grouped by their high 32 bits.  An empty container (what Roaring64Bitmap.xor
+    // leaves under its key) is kept, as Containers.deserialize keeps it (art/Containers.java:276-303): it
+    // holds no value, but it is serialized again and later ops see it like any other container
     int64_t cur_high = -1;
     for (const ArtCont &c : conts) {
-      if (c.card == 0) continue;
+      if (c.card == 0 && (c.t == RB_BITMAP || (c.t == RB_RUN && c.nr))) return bad(i, "non-canonical empty container");
       const uint32_t high = (uint32_t)(c.key >> 16);
       if ((int64_t)high != cur_high) {
         if (s->idx.size() + 1 >= kEmptyBitmap) return bad(i, "too many buckets");
@@ -464,7 +466,7 @@ int rbgpu_set64_from_art(rbgpu_ctx *ctx, const uint8_t *const *bufs, const uint6
   }
   rb_soa soa{(uint32_t)(begin.size() - 1), key.size(), payload.size(), begin.data(), key.data(), type.data(),
              card.data(), nruns.data(), offset.data(), payload.data()};
-  const int rc = soa.n_bitmaps ? rbgpu_set_from_soa(ctx, &soa, &s->buckets)
+  const int rc = soa.n_bitmaps ? set_from_soa(ctx, &soa, &s->buckets, true)
                                : ((s->buckets = empty_set(ctx)) ? RB_OK : fail(RB_ENOMEM, "empty bucket set"));
   if (rc) {
     delete s;

@@ -330,6 +330,34 @@ def test_roaring64_kept_empty_container_types(ctx, oracle, seed):
         assert kept_empty[0] > 0 and kept_empty[2] > 0, kept_empty
 
 
+def test_roaring64_art_round_trip_kept_empty(ctx, oracle):
+    """Roaring64Bitmap.deserialize keeps the empty containers an xor left in the stream
+    (art/Containers.java:276-303 reads every non-null slot), so deserialize -> serialize returns the same bytes,
+    and a later op treats those containers like the ones the xor produced on the device."""
+    import roaringbitmap_amd as rb
+    from oracle import rbref64 as R64
+    run = np.arange(100, 20000, dtype=np.uint64)
+    arr = (np.uint64(1) << np.uint64(16)) + np.arange(0, 900, 3, dtype=np.uint64)
+    other = (np.uint64(5) << np.uint64(32)) + np.arange(10, dtype=np.uint64)
+    x, y = R64.Ref64.of(np.concatenate([run, arr, other])), R64.Ref64.of(np.concatenate([run, arr]))
+    for r in (x, y):
+        for _, b in r.buckets:
+            b.run_optimize()
+    xy = R64.bitmap_op(rb.XOR, x, y, False)
+    art = xy.to_art()
+    s = ctx.upload_art64([art, y.to_art()])
+    assert s.serialize_art() == [art, y.to_art()]
+    assert s.serialize_portable()[0] == xy.to_portable()
+    assert np.array_equal(s.values(0), other)
+    h = s.bucket_set(0).download()
+    assert [(int(h.type[c]), int(h.card[c])) for c in range(len(h.key))] == [(2, 0), (0, 0), (2, 10)]
+    dev = ctx.pairwise64(rb.RB64_BITMAP, rb.XOR, s, s, [0], [0]).serialize_art()[0]  # from the device result
+    for op in (rb.AND, rb.OR, rb.XOR, rb.ANDNOT):
+        got = ctx.pairwise64(rb.RB64_BITMAP, op, s, s, [0], [1]).serialize_art()[0]
+        assert got == R64.bitmap_op(op, xy, y, False).to_art(), op
+    assert dev == R64.bitmap_op(rb.XOR, xy, xy, False).to_art()
+
+
 def test_roaring64_kept_empty_through_later_ops(ctx, oracle):
     """ADVICE r03 (low): x.xor(y) keeps an empty container under its key (Roaring64Bitmap.java:468-495);
     a later in-place andNot / or with a bitmap lacking that high leaves x's unmatched key untouched

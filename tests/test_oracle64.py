@@ -187,4 +187,6 @@ def test_oracle64_art_kept_empty_types():
     assert art[at:at + 8] == bytes([1, 0, 0, 0, 0, 0, 0, 0])          # NOT_NULL, Run, card 0, nbrruns 0
     assert art[at + 8:at + 14] == bytes([1, 2, 0, 0, 0, 0])           # NOT_NULL, Array, card 0
     assert art[at + 14:at + 20] == bytes([1, 2, 0, 0, 0, 0])
-    assert R64.Ref64.from_art(art).buckets == []                     # no values
+    back = R64.Ref64.from_art(art)       # Containers.deserialize keeps the empty containers
+    assert back.to_art() == art and back.cardinality() == 0
+    assert [(c[1], c[2]) for c in back.buckets[0][1].containers()] == [(2, 0), (0, 0), (0, 0)]
