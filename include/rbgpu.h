@@ -291,6 +291,10 @@ int rbgpu_set_extract(const rbgpu_set *set, uint32_t first, uint32_t count, rbgp
  * *bytes = their algorithmic bytes (metadata read + records written).  A caller that uploads a fresh
  * set per aggregation pays this once per set on top of the call. */
 int rbgpu_set_setup_stats(const rbgpu_set *set, double *ms, uint64_t *bytes);
+/* The same split by derived item: ms[0] / bytes[0] the dense-layout check, [1] the packed member-major
+ * records (workShyAnd's fast path), [2] the key-major records (naive_xor's; built from [1] when the set
+ * has it, else straight from the set's metadata).  What a fresh set costs a path: [0] + the items it uses. */
+int rbgpu_set_setup_parts(const rbgpu_set *set, double ms[3], uint64_t bytes[3]);
 
 /* ---- synthetic inputs for the benchmark (device-side generator, SplitMix64) ---------- */
 enum rb_workload {

@@ -115,6 +115,7 @@ SIGNATURES = {
     "rbgpu_pairwise_inplace": (C.c_int, [_P, C.c_int, _P, _P, _P, _P, C.c_uint32, C.POINTER(_P)]),
     "rbgpu_set_run_optimize": (C.c_int, [_P, C.POINTER(_P), C.c_void_p]),
     "rbgpu_set_setup_stats": (C.c_int, [_P, C.POINTER(C.c_double), _U64P]),
+    "rbgpu_set_setup_parts": (C.c_int, [_P, C.POINTER(C.c_double), _U64P]),
     "rbgpu_set64_from_portable": (C.c_int, [_P, C.POINTER(C.c_char_p), _U64P, C.c_uint32, C.POINTER(_P)]),
     "rbgpu_set64_from_buckets": (C.c_int, [_P, _U32P, _U64P, C.c_uint32, C.POINTER(_P)]),
     "rbgpu_set64_free": (None, [_P]),

@@ -87,6 +87,7 @@ void ctx_unref(rbgpu_ctx *ctx) {
   if (ctx->h_async) (void)hipHostFree(ctx->h_async);
   if (ctx->h_stage) (void)hipHostFree(ctx->h_stage);
   if (ctx->h_small) (void)hipHostFree(ctx->h_small);
+  if (ctx->d_small_ctr) (void)hipFree(ctx->d_small_ctr);
   ctx->pool.clear();
   ctx->ws_pairs.destroy();
   ctx->ws_tasks.destroy();
@@ -174,14 +175,17 @@ namespace {
 struct DeriveTimer {
   hipEvent_t e0 = nullptr, e1 = nullptr;
   rbgpu_set *s;
-  explicit DeriveTimer(rbgpu_set *s_) : s(s_) {
+  int part;
+  DeriveTimer(rbgpu_set *s_, int part_) : s(s_), part(part_) {
     if (hipEventCreate(&e0) == hipSuccess && hipEventCreate(&e1) == hipSuccess) (void)hipEventRecord(e0, s->ctx->stream);
   }
   ~DeriveTimer() {
     float ms = 0.f;
     if (e0 && e1 && hipEventRecord(e1, s->ctx->stream) == hipSuccess && hipEventSynchronize(e1) == hipSuccess &&
-        hipEventElapsedTime(&ms, e0, e1) == hipSuccess)
+        hipEventElapsedTime(&ms, e0, e1) == hipSuccess) {
       s->derive_ms += ms;
+      s->part_ms[part] += ms;
+    }
     if (e0) (void)hipEventDestroy(e0);
     if (e1) (void)hipEventDestroy(e1);
   }
@@ -207,14 +211,18 @@ int ensure_dense(const rbgpu_set *cs) {
   HIPCHK(hipStreamSynchronize(st));
   uint32_t bad = 1;
   if ((uint64_t)k0 + cnt <= 65536) {
-    HIPCHK(hipMemsetAsync(d, 0, 4, st));
-    launch_dense_check(s->view(), s->nb, k0, (uint32_t)cnt, d, st);
+    {
+      DeriveTimer t(s, 0);
+      HIPCHK(hipMemsetAsync(d, 0, 4, st));
+      launch_dense_check(s->view(), s->nb, k0, (uint32_t)cnt, d, st);
+    }
     HIPCHK(hipMemcpyAsync(&bad, d, 4, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
     LAUNCHCHK();
   }
   s->ctx->pool.release(d);
   s->derive_bytes += 2ull * s->nc; // the keys
+  s->part_bytes[0] += 2ull * s->nc;
   if (!bad) {
     s->dense_lo = k0;
     s->dense_hi = (int64_t)k0 + (int64_t)cnt;
@@ -229,7 +237,7 @@ int ensure_mrec(const rbgpu_set *cs) {
   uint64_t *m = nullptr;
   if (s->ctx->pool.alloc((void **)&m, std::max<uint64_t>(s->nc, 1) * 8)) return fail(RB_ENOMEM, "packed records");
   {
-    DeriveTimer t(s);
+    DeriveTimer t(s, 1);
     launch_pack_records(s->view(), s->nc, m, s->ctx->stream);
   }
   if (hipGetLastError() != hipSuccess) {
@@ -238,15 +246,16 @@ int ensure_mrec(const rbgpu_set *cs) {
   }
   s->mrec = m;
   s->derive_bytes += 24ull * s->nc; // 16 B of metadata read, an 8-B record written per container
+  s->part_bytes[1] += 24ull * s->nc;
   return RB_OK;
 }
 int ensure_krec(const rbgpu_set *cs) {
   rbgpu_set *s = const_cast<rbgpu_set *>(cs);
   if (s->krec) return RB_OK;
   int rc = ensure_dense(s);
-  if (!rc) rc = ensure_mrec(s);
   if (rc) return rc;
   if (s->dense_lo < 0) return fail(RB_EINVAL, "key-major records need a dense set");
+  if (s->payload_bytes >= kRecMaxPayload) return fail(RB_EINVAL, "packed records hold 40-bit payload offsets");
   HIPCHK(hipSetDevice(s->ctx->device));
   hipStream_t st = s->ctx->stream;
   uint64_t *k = nullptr, *mb = nullptr;
@@ -257,10 +266,15 @@ int ensure_krec(const rbgpu_set *cs) {
   // member bases in set order: container of bitmap b at key x is h_begin[b] + x - dense_lo
   std::vector<uint64_t> hb(s->nb);
   for (uint32_t b = 0; b < s->nb; ++b) hb[b] = s->h_begin[b] - (uint64_t)s->dense_lo;
+  // from mrec when the set already has it (16 B per container), else from the SoA itself (15 B of metadata
+  // read, an 8-B record written: k_records_direct)
+  const bool from_mrec = s->mrec != nullptr;
   {
-    DeriveTimer t(s);
-    if (hipMemcpyAsync(mb, hb.data(), s->nb * 8ull, hipMemcpyHostToDevice, st) == hipSuccess)
-      launch_records_transpose(s->mrec, mb, s->nb, (uint32_t)s->dense_lo, (uint32_t)s->dense_hi, k, st);
+    DeriveTimer t(s, 2);
+    if (hipMemcpyAsync(mb, hb.data(), s->nb * 8ull, hipMemcpyHostToDevice, st) == hipSuccess) {
+      if (from_mrec) launch_records_transpose(s->mrec, mb, s->nb, (uint32_t)s->dense_lo, (uint32_t)s->dense_hi, k, st);
+      else launch_records_direct(s->view(), mb, s->nb, (uint32_t)s->dense_lo, (uint32_t)s->dense_hi, k, st);
+    }
   }
   s->ctx->pool.release(mb);
   if (hipGetLastError() != hipSuccess) {
@@ -268,7 +282,8 @@ int ensure_krec(const rbgpu_set *cs) {
     return fail(RB_EDEVICE, "key-major record kernel failed");
   }
   s->krec = k;
-  s->derive_bytes += 16ull * s->nc; // each record read and written once
+  s->derive_bytes += (from_mrec ? 16ull : 23ull) * s->nc;
+  s->part_bytes[2] += (from_mrec ? 16ull : 23ull) * s->nc;
   return RB_OK;
 }
 } // namespace rbg
@@ -937,94 +952,114 @@ static int pairwise_small(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgp
   int rc = ensure_h_begin(a);
   if (!rc) rc = ensure_h_begin(b);
   if (rc) return rc;
-  // host memory the kernels read / write in place (no copy engine on the call's path): 8 result
-  // words, slot[np + 1] (u64), then a_idx[np], b_idx[np] (u32)
-  // blocks per pair (small_pair_nsub), at most ~16K blocks in all
+  // per pair: first containers and counts (from the host CSR), first slot (merged keys <= na + nb), first
+  // block (small_pair_nsub blocks per pair, at most ~16K blocks in all), the x1.op(x1) flag
+  if (a->nc >= (1ull << 32) || b->nc >= (1ull << 32)) return 1; // 32-bit container indices in the tables
   const uint32_t cap = std::max<uint32_t>(1, std::min<uint32_t>(2048, 16384 / np));
-  uint64_t nblocks64 = 0;
-  for (uint32_t p = 0; p < np; ++p) {
-    const uint32_t ai = a_idx ? a_idx[p] : p, bi = b_idx ? b_idx[p] : p;
-    nblocks64 += small_pair_nsub(bm_conts(a, ai) + bm_conts(b, bi), cap);
+  const bool inl = np <= kSmallInline;
+  const uint64_t nid = (np + 31) / 32;
+  std::vector<uint32_t> &tabv = ctx->small_tab; // [ident nid | i0 np | j0 np | nab np | slot np + 1 | blk np + 1]
+  SmallTabInline *ti = inl ? &ctx->small_inline : nullptr;
+  uint32_t *ident, *ti0, *tj0, *tnab, *slot, *blk;
+  if (inl) {
+    ident = ti->ident, ti0 = ti->i0, tj0 = ti->j0, tnab = ti->nab, slot = ti->slot, blk = nullptr;
+  } else {
+    tabv.assign(nid + 5ull * np + 2, 0u);
+    ident = tabv.data(), ti0 = ident + nid, tj0 = ti0 + np, tnab = tj0 + np, slot = tnab + np, blk = slot + np + 1;
   }
-  const size_t nout = 64, nslot = 8 * (np + 1ull), nidx = 4ull * np * ((a_idx != nullptr) + (b_idx != nullptr));
-  const size_t blob = nout + nslot + nidx + 4 * nblocks64;
-  if (blob > ctx->h_small_cap) {
-    if (ctx->h_small) (void)hipHostFree(ctx->h_small);
-    ctx->h_small = ctx->d_small = nullptr;
-    ctx->h_small_cap = 0;
-    const size_t cap = std::max<size_t>(blob, 64 * 1024);
-    if (hipHostMalloc((void **)&ctx->h_small, cap, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
-      return fail(RB_ENOMEM, "host-visible staging");
-    if (hipHostGetDevicePointer((void **)&ctx->d_small, ctx->h_small, 0) != hipSuccess) {
-      (void)hipHostFree(ctx->h_small);
-      ctx->h_small = nullptr;
-      return fail(RB_EDEVICE, "host-visible staging has no device address");
-    }
-    ctx->h_small_cap = cap;
-  }
-  uint64_t *hout = reinterpret_cast<uint64_t *>(ctx->h_small);
-  uint64_t *slot = reinterpret_cast<uint64_t *>(ctx->h_small + nout), acc = 0;
+  std::memset(ident, 0, 4 * nid);
+  uint64_t acc = 0;
   uint32_t max_keys = 0;
   for (uint32_t p = 0; p < np; ++p) {
     const uint32_t ai = a_idx ? a_idx[p] : p, bi = b_idx ? b_idx[p] : p;
-    const uint64_t nk = bm_conts(a, ai) + bm_conts(b, bi);
-    if (nk > kSmallPairKeys) return 1;
+    const uint64_t na = bm_conts(a, ai), nb = bm_conts(b, bi), nk = na + nb;
+    if (na > kSmallPairKeys || nb > kSmallPairKeys || nk > kSmallPairKeys) return 1;
     max_keys = std::max(max_keys, (uint32_t)nk);
-    slot[p] = acc;
+    ti0[p] = ai == kEmptyBitmap ? 0u : (uint32_t)a->h_begin[ai];
+    tj0[p] = bi == kEmptyBitmap ? 0u : (uint32_t)b->h_begin[bi];
+    tnab[p] = (uint32_t)na | ((uint32_t)nb << 16);
+    if (inplace && a == b && ai == bi && ai != kEmptyBitmap) ident[p >> 5] |= 1u << (p & 31);
+    slot[p] = (uint32_t)acc;
     acc += nk;
     if (acc > kSmallSlots) return 1;
   }
-  slot[np] = acc;
+  slot[np] = (uint32_t)acc;
   rc = ensure_max_runs(a);
   if (!rc) rc = ensure_max_runs(b);
   if (rc) return rc;
   if (a->max_runs > 2048 || b->max_runs > 2048) return 1; // a copy would not fit its 8 KiB slot
   const uint64_t E = acc;
-  uint8_t *hp = ctx->h_small + nout + nslot;
-  if (a_idx) std::memcpy(hp, a_idx, 4ull * np), hp += 4ull * np;
-  if (b_idx) std::memcpy(hp, b_idx, 4ull * np), hp += 4ull * np;
-  uint32_t *blk = reinterpret_cast<uint32_t *>(hp);
+  // merged keys per wave: 1, or doubled until the blocks fit the resident ones (one round of blocks)
+  const uint64_t resident = small_resident_blocks();
+  auto blocks_for = [&](uint32_t kpw) {
+    uint64_t n = 0;
+    for (uint32_t p = 0; p < np; ++p) n += small_pair_nsub(slot[p + 1] - slot[p], cap, kpw);
+    return n;
+  };
+  uint32_t kpw = 1;
+  uint64_t nblocks64 = blocks_for(1);
+  while (nblocks64 > resident && kpw < 64) {
+    kpw *= 2;
+    nblocks64 = blocks_for(kpw);
+  }
   const uint32_t nblocks = (uint32_t)nblocks64;
-  for (uint32_t p = 0, k = 0; p < np; ++p)
-    for (uint32_t j = 0, nj = small_pair_nsub(slot[p + 1] - slot[p], cap); j < nj; ++j) blk[k++] = p | (j << 12);
+  for (uint32_t p = 0, k = 0; p <= np; ++p) {
+    if (inl) ti->blk[p] = (uint16_t)k;
+    else blk[p] = k;
+    if (p < np) k += small_pair_nsub(slot[p + 1] - slot[p], cap, kpw);
+  }
+  // host-visible words the last block writes the call's results to (8 words)
+  if (!ctx->h_small) {
+    if (hipHostMalloc((void **)&ctx->h_small, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
+      return fail(RB_ENOMEM, "host-visible result words");
+    if (hipHostGetDevicePointer((void **)&ctx->d_small, ctx->h_small, 0) != hipSuccess) {
+      (void)hipHostFree(ctx->h_small);
+      ctx->h_small = nullptr;
+      return fail(RB_EDEVICE, "host-visible result words have no device address");
+    }
+  }
+  if (!ctx->d_small_ctr) { // the finished-block count and the counters; the last block of every call resets them
+    if (hipMalloc((void **)&ctx->d_small_ctr, 512) != hipSuccess) return fail(RB_ENOMEM, "block counters");
+    if (hipMemset(ctx->d_small_ctr, 0, 512) != hipSuccess) return fail(RB_EDEVICE, "block counters");
+  }
+  uint64_t *hout = reinterpret_cast<uint64_t *>(ctx->h_small);
 
   hipStream_t st = ctx->stream;
   const bool card_only = out == nullptr;
   const uint64_t E1 = std::max<uint64_t>(E, 1);
-  const size_t argb = nslot + nidx + 4ull * nblocks; // slot table, indices, block table
-  const size_t need = aligned256(8ull * np) + aligned256(4 * E1) + aligned256(2 * E1) + aligned256(E1 + 32) +
-                      aligned256(4 * E1) + aligned256(2 * E1) + aligned256(32ull * nblocks) +
-                      aligned256(8ull * (np + 1)) + aligned256(argb) + 256;
+  const size_t tabb = inl ? 0 : 4 * tabv.size();
+  const size_t need = aligned256(8ull * np) + aligned256(4 * E1) + aligned256(8 * E1) + aligned256(tabb) +
+                      aligned256(32ull * nblocks) + 256;
   if (ctx->ws_pairs.reserve(need, st) != hipSuccess) return fail(RB_ENOMEM, "pair workspace");
   Workspace &W = ctx->ws_pairs;
   SmallPairArgs sa{};
   sa.A = a->view();
   sa.B = b->view();
-  sa.slot = reinterpret_cast<const uint64_t *>(ctx->d_small + nout);
-  const uint32_t *d_idx = reinterpret_cast<const uint32_t *>(ctx->d_small + nout + nslot);
-  sa.aidx = a_idx ? d_idx : nullptr;
-  sa.bidx = b_idx ? d_idx + (a_idx ? np : 0) : nullptr;
   sa.np = np;
-  sa.blk = reinterpret_cast<const uint32_t *>(ctx->d_small + (reinterpret_cast<uint8_t *>(blk) - ctx->h_small));
-  const char *dv = getenv("RBGPU_SMALL_DEVARGS");
-  if (dv && dv[0] == '1') { // study: the argument tables copied to device memory first
-    uint8_t *dargs = W.take<uint8_t>(argb);
-    HIPCHK(hipMemcpyAsync(dargs, ctx->h_small + nout, argb, hipMemcpyHostToDevice, st));
-    sa.slot = reinterpret_cast<const uint64_t *>(dargs);
-    const uint32_t *di = reinterpret_cast<const uint32_t *>(dargs + nslot);
-    sa.aidx = a_idx ? di : nullptr;
-    sa.bidx = b_idx ? di + (a_idx ? np : 0) : nullptr;
-    sa.blk = reinterpret_cast<const uint32_t *>(dargs + (reinterpret_cast<uint8_t *>(blk) - (ctx->h_small + nout)));
+  SmallTabDev dt{};
+  if (!inl) { // larger batches: the tables in device memory, one copy from pinned staging
+    if (tabb > ctx->h_stage_cap) {
+      if (ctx->h_stage) (void)hipHostFree(ctx->h_stage);
+      ctx->h_stage = nullptr;
+      ctx->h_stage_cap = 0;
+      if (hipHostMalloc((void **)&ctx->h_stage, tabb) != hipSuccess) return fail(RB_ENOMEM, "pinned staging");
+      ctx->h_stage_cap = tabb;
+    }
+    std::memcpy(ctx->h_stage, tabv.data(), tabb);
+    uint32_t *d = W.take<uint32_t>(tabv.size());
+    HIPCHK(hipMemcpyAsync(d, ctx->h_stage, tabb, hipMemcpyHostToDevice, st));
+    dt = SmallTabDev{d, d + nid, d + nid + np, d + nid + 2ull * np, d + nid + 3ull * np, d + nid + 4ull * np + 1};
   }
-  sa.cap = cap;
   sa.pcard = card_out ? W.take<uint64_t>(np) : nullptr;
   uint32_t *xpos = W.take<uint32_t>(E1);
-  sa.skey = W.take<uint16_t>(E1);
-  sa.stype = W.take<uint8_t>(E1 + 32); // + 32: the compaction reads type bytes 8 at a time
-  sa.scard = W.take<uint32_t>(E1);
-  sa.snruns = W.take<uint16_t>(E1);
-  sa.bstat = W.take<uint64_t>(4ull * nblocks);
-  sa.dslot = W.take<uint64_t>(np + 1ull);
+  sa.smeta = W.take<uint64_t>(E1);
+  sa.ctr = ctx->d_small_ctr;
+  const char *stv = getenv("RBGPU_SMALL_STAMPS"); // study: per-block timeline to stderr
+  const bool stamps = stv && stv[0] == '1';
+  if (stamps) {
+    sa.stamps = W.take<uint64_t>(4ull * nblocks);
+    HIPCHK(hipMemsetAsync(sa.stamps, 0, 32ull * nblocks, st));
+  }
 
   rbgpu_set *res = nullptr;
   if (!card_only) {
@@ -1036,8 +1071,8 @@ static int pairwise_small(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgp
     }
     sa.arena = res->payload;
   }
-  // per-kernel events only when asked for (RBGPU_SMALL_KERNEL_TIMES=1, the bench's breakdown): the call
-  // is a few tens of microseconds and each timed marker sits between its launches
+  // kernel events only when asked for (RBGPU_SMALL_KERNEL_TIMES=1, the bench's breakdown): the call is a
+  // few tens of microseconds
   const char *kt = getenv("RBGPU_SMALL_KERNEL_TIMES");
   const bool ktimes = kt && kt[0] == '1';
   stats_begin(ctx, false);
@@ -1050,19 +1085,19 @@ static int pairwise_small(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgp
   sa.hout = reinterpret_cast<uint64_t *>(ctx->d_small);
   sa.lazy = is_lazy_op(op) ? op : 0;
   sa.inplace = inplace;
-  sa.same = a == b;
   sa.keep_empty = keep_empty;
-  launch_pair_small(is_lazy_op(op) ? (int)RB_OR : op, card_only, sa, max_keys, nblocks, st);
+  launch_pair_small(is_lazy_op(op) ? (int)RB_OR : op, card_only, sa, ti, dt, max_keys, nblocks, st);
   if (ktimes) HIPCHK(hipEventRecord(ctx->ev[2], st));
-  launch_pair_small_compact(sa, st);
-  if (ktimes) HIPCHK(hipEventRecord(ctx->ev[3], st));
   if (card_out) HIPCHK(hipMemcpyAsync(card_out, sa.pcard, 8ull * np, hipMemcpyDeviceToHost, st));
   HIPCHK(hipEventRecord(ctx->ev[5], st));
-  if (hipStreamSynchronize(st) != hipSuccess || hipGetLastError() != hipSuccess) {
-    if (res) rbgpu_set_free(res);
-    return fail(RB_EDEVICE, "small-batch pairwise kernels failed");
+  {
+    const hipError_t e1 = hipStreamSynchronize(st), e2 = hipGetLastError();
+    if (e1 != hipSuccess || e2 != hipSuccess) {
+      if (res) rbgpu_set_free(res);
+      return fail(RB_EDEVICE, "small-batch pairwise kernel failed: %s", hipGetErrorString(e1 != hipSuccess ? e1 : e2));
+    }
   }
-  // the result words, written by the compaction kernel straight into host memory
+  // the result words, written by the last block straight into host memory
   uint64_t *w = ctx->words;
   for (int i = 0; i < kStatWords; ++i) w[i] = 0;
   w[0] = hout[1];           // input bytes with key arrays
@@ -1070,8 +1105,41 @@ static int pairwise_small(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgp
   w[1] = hout[3];           // output bytes
   w[7] = hout[4];           // result cardinality
   const uint64_t nres = hout[0];
-  const KernelSpan spans[2] = {{"k_pair_small", 6, 1, E}, {"k_pair_small_compact", -1, -1, E}};
-  rc = stats_fill(ctx, E, nres, spans, ktimes ? 2 : 0);
+  if (stamps) { // block start / keys aligned / work done, and the compaction's end (last block), in us
+    std::vector<uint64_t> h(4ull * nblocks);
+    HIPCHK(hipMemcpy(h.data(), sa.stamps, 32ull * nblocks, hipMemcpyDeviceToHost));
+    uint64_t t0 = ~0ull, tend = 0, tlast = 0;
+    double align = 0, work = 0;
+    for (uint32_t i = 0; i < nblocks; ++i) {
+      t0 = std::min(t0, h[4 * i]);
+      tend = std::max(tend, h[4 * i + 2]);
+      tlast = std::max(tlast, h[4 * i + 3]);
+      align += (double)(h[4 * i + 1] - h[4 * i]);
+      work += (double)(h[4 * i + 2] - h[4 * i + 1]);
+    }
+    uint64_t late = 0;
+    for (uint32_t i = 0; i < nblocks; ++i) late = std::max(late, h[4 * i] - t0);
+    std::vector<uint64_t> dur(nblocks), wk(nblocks);
+    uint32_t ilast = 0;
+    for (uint32_t i = 0; i < nblocks; ++i) {
+      dur[i] = h[4 * i + 2] - h[4 * i];
+      wk[i] = h[4 * i + 2] - h[4 * i + 1];
+      if (h[4 * i + 2] > h[4 * ilast + 2]) ilast = i;
+    }
+    std::vector<uint64_t> ds = dur;
+    std::sort(ds.begin(), ds.end());
+    uint32_t pl = 0;
+    for (uint32_t p = 0; p < np; ++p)
+      if ((inl ? (uint32_t)ti->blk[p] : blk[p]) <= ilast) pl = p;
+    fprintf(stderr, "small stamps: block duration p50 %.2f p90 %.2f max %.2f us; latest block %u (pair %u, %u keys, "
+                    "work %.2f us, kpw %u)\n", ds[nblocks / 2] / 100.0, ds[nblocks * 9 / 10] / 100.0,
+            ds[nblocks - 1] / 100.0, ilast, pl, (unsigned)(slot[pl + 1] - slot[pl]), wk[ilast] / 100.0, kpw);
+    fprintf(stderr, "small stamps: blocks %u E %llu | last start +%.2f us, last work end +%.2f us, compaction end +%.2f us | "
+                    "mean align %.2f us, mean work %.2f us\n", nblocks, (unsigned long long)E, late / 100.0,
+            (tend - t0) / 100.0, (tlast - t0) / 100.0, align / nblocks / 100.0, work / nblocks / 100.0);
+  }
+  const KernelSpan spans[1] = {{"k_pair_small", 6, 1, E}};
+  rc = stats_fill(ctx, E, nres, spans, ktimes ? 1 : 0);
   if (rc) {
     if (res) rbgpu_set_free(res);
     return rc;
@@ -1804,6 +1872,15 @@ int rbgpu_set_setup_stats(const rbgpu_set *s, double *ms, uint64_t *bytes) {
   if (!s || !ms || !bytes) return fail(RB_EINVAL, "null argument");
   *ms = s->derive_ms;
   *bytes = s->derive_bytes;
+  return RB_OK;
+}
+
+int rbgpu_set_setup_parts(const rbgpu_set *s, double *ms, uint64_t *bytes) {
+  if (!s || !ms || !bytes) return fail(RB_EINVAL, "null argument");
+  for (int i = 0; i < 3; ++i) {
+    ms[i] = s->part_ms[i];
+    bytes[i] = s->part_bytes[i];
+  }
   return RB_OK;
 }
 

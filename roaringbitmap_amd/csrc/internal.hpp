@@ -154,8 +154,10 @@ struct rbgpu_ctx {
   size_t h_stage_cap = 0;
   // host memory the GPU reads and writes directly (pinned, mapped, coherent): the small-batch
   // pairwise call's arguments and result words, so that call needs no copy engine
-  uint8_t *h_small = nullptr, *d_small = nullptr;
-  size_t h_small_cap = 0;
+  uint8_t *h_small = nullptr, *d_small = nullptr; // small-batch result words (host-visible, 64 B)
+  uint64_t *d_small_ctr = nullptr;                  // small-batch finished-block count and counters
+  rbg::SmallTabInline small_inline{};               // small-batch tables passed in the kernel arguments
+  std::vector<uint32_t> small_tab;                  // ... or copied to device memory (larger batches)
   rb_stats last{};
   uint64_t words[rbg::kStatWords] = {}; // the last call's counters, summed over stripes
   int refs = 1;                 // the handle + one per live set; destroyed at zero
@@ -199,6 +201,8 @@ struct rbgpu_set {
   hipEvent_t read_done = nullptr;
   double derive_ms = 0.0;         // device time spent building mrec / krec (reported, not hidden)
   uint64_t derive_bytes = 0;      // their algorithmic bytes (metadata read + records written)
+  double part_ms[3] = {0, 0, 0};  // per derived item: 0 dense check, 1 mrec, 2 krec (rbgpu_set_setup_parts)
+  uint64_t part_bytes[3] = {0, 0, 0};
   rbg::SetView view() const { return rbg::SetView{begin, key, type, card, nruns, off, payload}; }
 };
 

@@ -108,42 +108,65 @@ void launch_compact_write(const uint64_t *task_begin, uint64_t nseg, const TaskM
                           uint64_t *rseg, uint64_t *rbegin, hipStream_t st);
 
 // small batches (<= kSmallPairs pairs, <= kSmallPairKeys keys per pair, <= kSmallSlots merged keys in
-// all): one kernel per call computes every pair into one 8 KiB slot per merged key, one single-block
-// kernel compacts the slots into the result CSR
+// all): ONE kernel per call computes every pair into one 8 KiB slot per merged key, and its last block to
+// finish compacts the slots into the result CSR (pairwise.hip, k_pair_small)
 constexpr uint32_t kSmallPairs = 4096, kSmallPairKeys = 4096, kSmallSlots = 32768;
+// The call's tables, per pair: first container of its A and B bitmaps (i0, j0) and their container counts
+// (na | nb << 16; the host has the CSR), first slot (prefix of na + nb, np + 1 entries), first block
+// (np + 1), and the x1.op(x1) in-place flag.  Up to kSmallInline pairs they travel in the kernel arguments
+// (no copy, no host-memory reads); larger batches copy them to device memory first.
+constexpr uint32_t kSmallInline = 200;
+struct SmallTabInline {
+  uint32_t ident[(kSmallInline + 31) / 32];
+  uint32_t i0[kSmallInline], j0[kSmallInline], nab[kSmallInline], slot[kSmallInline + 1];
+  uint16_t blk[kSmallInline + 1];
+  __device__ uint32_t a0(uint32_t p) const { return i0[p]; }
+  __device__ uint32_t b0(uint32_t p) const { return j0[p]; }
+  __device__ uint32_t counts(uint32_t p) const { return nab[p]; }
+  __device__ bool same(uint32_t p) const { return (ident[p >> 5] >> (p & 31)) & 1u; }
+  __device__ uint32_t slot_at(uint32_t p) const { return slot[p]; }
+  __device__ uint32_t blk_at(uint32_t p) const { return blk[p]; }
+};
+struct SmallTabDev {
+  const uint32_t *ident, *i0, *j0, *nab, *slot, *blk;
+  __device__ uint32_t a0(uint32_t p) const { return i0[p]; }
+  __device__ uint32_t b0(uint32_t p) const { return j0[p]; }
+  __device__ uint32_t counts(uint32_t p) const { return nab[p]; }
+  __device__ bool same(uint32_t p) const { return (ident[p >> 5] >> (p & 31)) & 1u; }
+  __device__ uint32_t slot_at(uint32_t p) const { return slot[p]; }
+  __device__ uint32_t blk_at(uint32_t p) const { return blk[p]; }
+};
 struct SmallPairArgs {
   SetView A, B;
-  const uint32_t *aidx, *bidx; // may be null (identity)
-  const uint64_t *slot;        // [np + 1] first slot of pair p (prefix of its key counts)
   uint32_t np;
   uint8_t *arena;              // slot t's payload at t * 8 KiB (null for cardinality only)
-  uint16_t *skey;              // per slot
-  uint8_t *stype;
-  uint32_t *scard;
-  uint16_t *snruns;
+  uint64_t *smeta;             // [E] per slot: key, type, card word, run count (small_meta; sc1 stores)
   uint64_t *pcard;             // [np] result cardinality per pair, or null
-  uint64_t *bstat;             // [4 * blocks] per block: input bytes, key-array bytes, output bytes, cardinality
-  uint64_t *dslot;             // [np + 1] device copy of slot (written by the first kernel)
+  uint64_t *ctr;               // [0] finished blocks, [8 + 8k] k = 0..3: input bytes, key-array bytes, output
+                               // bytes, result cardinality (agent atomics; zero between calls: the last block
+                               // resets them)
   int lazy;                    // 0, or the priorityqueue_or role of an OR call (TaskMeta::lazy)
-  int inplace, same;           // in-place x1.op(x2) (PairArgs::inplace / same)
+  int inplace;                 // in-place x1.op(x2) (PairArgs::inplace)
   int keep_empty;              // TaskMeta::keep_empty
-  const uint32_t *blk;         // [blocks] pair | block-within-pair << 12 (host-visible)
-  uint32_t cap;                // most blocks per pair
-  // the compaction kernel's: E slots, nblocks blocks, slot -> result position scratch (used above
+  // the compaction's: E slots, nblocks blocks, slot -> result position scratch (used above
   // kSmallXposLds slots), result SoA (key null: cardinality only), result CSR or null, host-visible
   // words: [0] result containers, [1..4] the summed counters
   uint32_t E, nblocks;
   uint32_t *xpos;
   uint64_t *rbegin, *hout;
   OutView out;
+  uint64_t *stamps; // study (RBGPU_SMALL_STAMPS=1): per block 4 s_memrealtime stamps, else null
 };
-// blocks of one pair with nk keys (na + nb): a wave per merged key, 4 waves per block, at most `cap`
-__host__ __device__ inline uint32_t small_pair_nsub(uint64_t nk, uint32_t cap) {
-  const uint64_t b = (nk + 3) / 4;
+// blocks of one pair with nk keys (na + nb): kpw merged keys per wave, 4 waves per block, at most `cap`
+__host__ __device__ inline uint32_t small_pair_nsub(uint64_t nk, uint32_t cap, uint32_t kpw) {
+  const uint64_t b = (nk + 4ull * kpw - 1) / (4ull * kpw);
   return (uint32_t)(b < 1 ? 1 : b > cap ? cap : b);
 }
-void launch_pair_small(int op, bool card_only, const SmallPairArgs &a, uint32_t max_keys, uint32_t nblocks, hipStream_t st);
-void launch_pair_small_compact(const SmallPairArgs &a, hipStream_t st);
+static_assert(sizeof(SmallTabInline) + sizeof(SmallPairArgs) + 16 <= 4096, "kernel arguments within 4 KiB");
+// blocks of 256 threads resident at once (2 per CU: the register path takes up to 256 VGPRs)
+unsigned small_resident_blocks();
+void launch_pair_small(int op, bool card_only, const SmallPairArgs &a, const SmallTabInline *inl,
+                       const SmallTabDev &dev, uint32_t max_keys, uint32_t nblocks, hipStream_t st);
 
 // ---- wide.hip: per-key reduction outputs (one 8 KiB slot per active key q)
 struct WideOut {
@@ -186,6 +209,8 @@ struct XorRecords {
   const uint64_t *mrec, *mbase;
   uint32_t M, key_lo, key_hi;
 };
+void launch_records_direct(const SetView &s, const uint64_t *mbase, uint32_t M, uint32_t key_lo, uint32_t key_hi,
+                           uint64_t *rec, hipStream_t st);
 void launch_records_transpose(const uint64_t *mrec, const uint64_t *mbase, uint32_t M, uint32_t key_lo,
                               uint32_t key_hi, uint64_t *rec, hipStream_t st);
 void launch_wide_runs_xor(const SetView &s, const uint32_t *cid, const uint64_t *seg, const uint32_t *klist,

@@ -1343,55 +1343,61 @@ __device__ __forceinline__ uint32_t lower_bound_u16(const uint16_t *k, uint32_t 
   return lo;
 }
 
-// The compaction kernel (one block of 1024 threads after k_pair_small): drop the empty slots, write
-// the result SoA and CSR (slot t's payload stays at t * 8 KiB), add up the blocks' counters and write
-// the call's result words to host-visible memory.  Latency-bound (a chain of dependent global round
-// trips), so every independent load — type bytes, block counters, slot table — is issued up front, and
-// the slot -> result position map stays in LDS (E <= kSmallXposLds) for the CSR.  (Running it in the
-// last block of k_pair_small instead needs an agent-scope release per block — an L2 write-back on a
-// multi-XCD part: 104 vs 29 us measured.)
-constexpr uint32_t kSmallXposLds = 16384;
-__global__ __launch_bounds__(1024) void k_pair_small_compact(SmallPairArgs a) {
-  extern __shared__ uint32_t xl[]; // [E] when E <= kSmallXposLds
-  __shared__ uint32_t wtot[16];
-  __shared__ uint64_t red[16 * 4];
+// Per-slot metadata of k_pair_small, one 8-B word per slot: card word (17-bit value + its two lazy marks,
+// bits 0-18), type (bits 19-20; 3 = dropped), key (24-39), run count (40-55).
+__device__ __forceinline__ uint64_t small_meta(uint32_t key, int ty, uint32_t cw, uint32_t nr) {
+  const uint64_t c = (cw & 0x1FFFFu) | ((cw & kLazyCard) ? 1u << 17 : 0u) | ((cw & kRunAsBitmap) ? 1u << 18 : 0u);
+  return c | ((uint64_t)(ty == (int)kEmpty ? 3u : (uint32_t)ty) << 19) | ((uint64_t)key << 24) | ((uint64_t)nr << 40);
+}
+__device__ __forceinline__ bool meta_empty(uint64_t m) { return ((m >> 19) & 3u) == 3u; }
+__device__ __forceinline__ uint32_t meta_cw(uint64_t m) {
+  return (uint32_t)(m & 0x1FFFFu) | ((m >> 17) & 1u ? kLazyCard : 0u) | ((m >> 18) & 1u ? kRunAsBitmap : 0u);
+}
+// Cross-block hand-off (MI355X_MICROARCH.md, inter-workgroup visibility, first table row): every block's
+// slot words and counters are stored sc1, each storing wave waits for them, then one agent-scope add per
+// block; the block whose add comes last reads them with sc1 loads.  The slot payloads stay plain stores:
+// nothing in the launch reads them.
+__device__ __forceinline__ void st_sc1(uint64_t *p, uint64_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t ld_sc1(const uint64_t *p) {
+  return __hip_atomic_load(const_cast<uint64_t *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// The compaction, run by the last block of k_pair_small: drop the empty slots, write the result SoA and
+// CSR (slot t's payload stays at t * 8 KiB), add up the blocks' counters and write the call's result words
+// to host-visible memory.  xl: the block's LDS scratch (the slot -> result position map when E fits it).
+constexpr uint32_t kSmallXposLds = 8192;
+template <class Tab>
+__device__ void small_compact(const SmallPairArgs &a, const Tab &tab, uint32_t *xl, uint32_t *wtot) {
   const uint32_t nt = blockDim.x, E = a.E;
-  const bool lds_x = E <= kSmallXposLds;
-  uint32_t *xpos = lds_x ? xl : a.xpos;
+  uint32_t *xpos = E <= kSmallXposLds ? xl : a.xpos;
   const OutView &out = a.out;
-  // independent loads first: the first tile's type bytes, the block counters, the slot table
-  const uint32_t lo0 = 8 * threadIdx.x;
-  uint64_t tw = lo0 < E ? *reinterpret_cast<const uint64_t *>(a.stype + lo0) : ~0ull;
-  uint64_t v[4] = {0, 0, 0, 0};
-  for (uint32_t b = threadIdx.x; b < a.nblocks; b += nt)
-    for (int k = 0; k < 4; ++k) v[k] += a.bstat[4ull * b + k];
-  uint64_t ds[4];
+  // the summed counters (the blocks' atomics) and the first tile of slot words: independent loads first
+  uint64_t v = threadIdx.x < 4 ? ld_sc1(a.ctr + 8 + 8 * threadIdx.x) : 0;
+  constexpr int kPer = 16; // slot words per thread and tile
+  uint32_t base = 0;       // results of the tiles before
+  for (uint32_t t0 = 0; t0 < E; t0 += kPer * nt) {
+    const uint32_t lo = t0 + kPer * threadIdx.x;
+    uint64_t m[kPer];
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const uint32_t p = threadIdx.x + k * nt;
-    ds[k] = p <= a.np ? a.dslot[p] : 0;
-  }
-  uint32_t base = 0; // results of the tiles before
-  for (uint32_t t0 = 0; t0 < E; t0 += 8 * nt) {
-    const uint32_t lo = t0 + lo0;
-    if (t0) tw = lo < E ? *reinterpret_cast<const uint64_t *>(a.stype + lo) : ~0ull;
+    for (int k = 0; k < kPer; ++k) m[k] = lo + k < E ? ld_sc1(a.smeta + lo + k) : (3ull << 19);
     uint32_t cnt = 0;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) cnt += lo + k < E && ((tw >> (8 * k)) & 0xFF) != (uint64_t)kEmpty;
+    for (int k = 0; k < kPer; ++k) cnt += !meta_empty(m[k]);
     uint32_t tot;
     uint32_t r = base + block_xscan(cnt, wtot, tot);
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
+    for (int k = 0; k < kPer; ++k) {
       const uint32_t t = lo + k;
       if (t >= E) break;
       xpos[t] = r;
-      const uint32_t ty = (uint32_t)((tw >> (8 * k)) & 0xFF);
-      if (ty == (uint32_t)kEmpty) continue;
+      if (meta_empty(m[k])) continue;
       if (out.key) {
-        out.key[r] = a.skey[t];
-        out.type[r] = (uint8_t)ty;
-        out.card[r] = a.scard[t];
-        out.nruns[r] = a.snruns[t];
+        out.key[r] = (uint16_t)(m[k] >> 24);
+        out.type[r] = (uint8_t)((m[k] >> 19) & 3u);
+        out.card[r] = meta_cw(m[k]);
+        out.nruns[r] = (uint16_t)(m[k] >> 40);
         out.off[r] = (uint64_t)t * kBitmapBytes;
       }
       ++r;
@@ -1399,64 +1405,66 @@ __global__ __launch_bounds__(1024) void k_pair_small_compact(SmallPairArgs a) {
     base += tot;
   }
   __syncthreads();
-  if (a.rbegin) {
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const uint32_t p = threadIdx.x + k * nt;
-      if (p <= a.np) a.rbegin[p] = ds[k] < E ? xpos[ds[k]] : base;
-    }
-    for (uint32_t p = threadIdx.x + 4 * nt; p <= a.np; p += nt) { // (np <= kSmallPairs = 4 * 1024)
-      const uint64_t t = a.dslot[p];
+  if (a.rbegin)
+    for (uint32_t p = threadIdx.x; p <= a.np; p += nt) {
+      const uint32_t t = tab.slot_at(p);
       a.rbegin[p] = t < E ? xpos[t] : base;
     }
-  }
   if (a.pcard) // per-pair result cardinality (RoaringBitmap.andCardinality etc.)
     for (uint32_t p = threadIdx.x; p < a.np; p += nt) {
       uint64_t c = 0;
-      for (uint64_t t = a.dslot[p]; t < a.dslot[p + 1]; ++t)
-        if (a.stype[t] != kEmpty) c += a.scard[t];
+      for (uint32_t t = tab.slot_at(p), te = tab.slot_at(p + 1); t < te; ++t) {
+        const uint64_t m = ld_sc1(a.smeta + t);
+        if (!meta_empty(m)) c += m & 0x1FFFFu;
+      }
       a.pcard[p] = c;
     }
-  const int lane = lane_id(), wv = threadIdx.x >> 6;
-  for (int k = 0; k < 4; ++k) {
-    const uint64_t x = wave_sum_u64(v[k]);
-    if (lane == 0) red[4 * wv + k] = x;
-  }
-  __syncthreads();
   if (threadIdx.x < 4) {
-    uint64_t x = 0;
-    for (uint32_t w = 0; w < (nt >> 6); ++w) x += red[4 * w + threadIdx.x];
-    a.hout[1 + threadIdx.x] = x;
+    a.hout[1 + threadIdx.x] = v;
+    __hip_atomic_store(a.ctr + 8 + 8 * threadIdx.x, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  if (threadIdx.x == 0) a.hout[0] = base;
+  if (threadIdx.x == 0) {
+    a.hout[0] = base;
+    __hip_atomic_store(a.ctr, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); // ready for the next call
+  }
 }
 
 // Dynamic LDS of k_pair_small: per wave an 8 KiB scratch, then the merged-key list, the keys and the
 // match prefix, each sized by the batch's largest na + nb (kmax).
-constexpr int kSmallLdsMax = 160 * 1024;
+constexpr int kSmallLdsMax = 96 * 1024; // >= small_lds_bytes(4, kSmallPairKeys) (~64 KiB), beside the static LDS
 // (All LDS of the kernel is in the dynamic region, whose base stays 16-B aligned — the 8 KiB scratch
 // takes 16-B accesses.)
-__host__ __device__ inline uint32_t small_lds_bytes(uint32_t waves, uint32_t kmax) {
+__host__ __device__ constexpr uint32_t small_lds_bytes(uint32_t waves, uint32_t kmax) {
   return waves * 8192u + 64u + 4u * kmax + 2u * kmax + 2u * (kmax + 1) + 16u;
 }
 constexpr int kSmallWaves = 2; // waves per SIMD of the small-batch kernel (the register path takes ~235 VGPRs; 3 and 4 spill)
-template <int OP, bool CARD_ONLY>
-__global__ __launch_bounds__(256, kSmallWaves) void k_pair_small(SmallPairArgs a, uint32_t kmax) {
+template <int OP, bool CARD_ONLY, class Tab>
+__global__ __launch_bounds__(256, kSmallWaves) void k_pair_small(SmallPairArgs a, uint32_t kmax, Tab tab) {
   extern __shared__ __attribute__((aligned(16))) uint8_t dyn_lds[];
+  __shared__ uint32_t s_last;
   const uint32_t nw = blockDim.x >> 6;
   uint32_t *wtot = reinterpret_cast<uint32_t *>(dyn_lds + nw * 8192u); // [16] block-scan wave totals
   uint32_t *ent = wtot + 16; // merged key: A index | B index << 16
   uint16_t *K = reinterpret_cast<uint16_t *>(ent + kmax);             // A's keys, then B's
   uint16_t *mpref = K + kmax;                                          // matched keys among A[0, i)
   const int lane = lane_id(), wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  // small_pair_nsub blocks per pair (the host's block table names each block's pair and rank): each
-  // aligns the keys (cheap, in LDS) and its waves take the merged keys e = nw * sub + wv, + nw * nsub, ...
-  const uint32_t bk = a.blk[blockIdx.x], p = bk & 0xFFFu, sub = bk >> 12, nt = blockDim.x;
-  const uint32_t ai = a.aidx ? a.aidx[p] : p, bi = a.bidx ? a.bidx[p] : p;
-  const bool ident = a.inplace && a.same && ai == bi && ai != kEmptyBitmap; // x1.op(x1) in place
-  const uint64_t i0 = ai == kEmptyBitmap ? 0 : a.A.begin[ai], j0 = bi == kEmptyBitmap ? 0 : a.B.begin[bi];
-  const uint32_t na = ai == kEmptyBitmap ? 0u : (uint32_t)(a.A.begin[ai + 1] - i0);
-  const uint32_t nb = bi == kEmptyBitmap ? 0u : (uint32_t)(a.B.begin[bi + 1] - j0);
+  const uint64_t st0 = a.stamps ? __builtin_amdgcn_s_memrealtime() : 0;
+  // the block's pair and rank within it: the last pair whose first block is <= blockIdx.x (the host's
+  // per-pair block prefix; small_pair_nsub blocks per pair)
+  uint32_t p = 0;
+  {
+    uint32_t lo = 0, hi = a.np; // blk_at(lo) <= blockIdx.x < blk_at(hi)
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (tab.blk_at(mid) <= blockIdx.x) lo = mid;
+      else hi = mid;
+    }
+    p = lo;
+  }
+  const uint32_t sub = blockIdx.x - tab.blk_at(p), nsub = tab.blk_at(p + 1) - tab.blk_at(p), nt = blockDim.x;
+  const bool ident = tab.same(p); // x1.op(x1) in place
+  const uint64_t i0 = tab.a0(p), j0 = tab.b0(p);
+  const uint32_t na = tab.counts(p) & 0xFFFFu, nb = tab.counts(p) >> 16;
   for (uint32_t t = threadIdx.x; t < na; t += nt) K[t] = a.A.key[i0 + t];
   for (uint32_t t = threadIdx.x; t < nb; t += nt) K[na + t] = a.B.key[j0 + t];
   __syncthreads();
@@ -1487,20 +1495,16 @@ __global__ __launch_bounds__(256, kSmallWaves) void k_pair_small(SmallPairArgs a
   }
   __syncthreads();
   const uint32_t nu = na + nb - matches;
+  const uint64_t st1 = a.stamps ? __builtin_amdgcn_s_memrealtime() : 0;
   // ---- one wave per merged key
   uint32_t *s = reinterpret_cast<uint32_t *>(dyn_lds) + wv * 2048;
-  const uint64_t slot0 = a.slot[p], slot1 = a.slot[p + 1];
-  const uint32_t nsub = small_pair_nsub(slot1 - slot0, a.cap);
-  if (sub == 0 && threadIdx.x == 0) { // a device copy of the slot table for the compaction kernel
-    a.dslot[p] = slot0;
-    if (p + 1 == a.np) a.dslot[p + 1] = slot1;
-  }
+  const uint32_t slot0 = tab.slot_at(p), slot1 = tab.slot_at(p + 1);
   const uint64_t keyb = sub == 0 && wv == 0 && lane == 0 ? 2ull * (na + nb) : 0ull;
   uint64_t inb = keyb, outb = 0, csum = 0;
   for (uint32_t e = nw * sub + wv; e < nu; e += nw * nsub) {
     const uint32_t en = ent[e], ia = en & 0xFFFF, ib = en >> 16;
     const bool has_a = ia != 0xFFFFu, has_b = ib != 0xFFFFu;
-    const uint64_t slot = slot0 + e;
+    const uint64_t slot = (uint64_t)slot0 + e;
     uint8_t *dst = a.arena + slot * kBitmapBytes;
     int ty = kEmpty, c = 0, nr = 0;
     uint32_t cw = 0xFFFFFFFFu; // the card word to store when it is not c (priorityqueue_or's lazy marks)
@@ -1574,10 +1578,7 @@ __global__ __launch_bounds__(256, kSmallWaves) void k_pair_small(SmallPairArgs a
       if (CARD_ONLY) ty = kArray;
     }
     if (lane == 0) {
-      a.skey[slot] = has_a ? KA[ia] : KB[ib];
-      a.stype[slot] = (uint8_t)ty;
-      a.scard[slot] = cw != 0xFFFFFFFFu ? cw : (uint32_t)c;
-      a.snruns[slot] = (uint16_t)nr;
+      st_sc1(a.smeta + slot, small_meta(has_a ? KA[ia] : KB[ib], ty, cw != 0xFFFFFFFFu ? cw : (uint32_t)c, (uint32_t)nr));
       if (ty != kEmpty) {
         csum += (uint64_t)c;
         if (!CARD_ONLY) outb += alg_bytes(ty, (uint32_t)c, (uint32_t)nr) + 16;
@@ -1586,9 +1587,9 @@ __global__ __launch_bounds__(256, kSmallWaves) void k_pair_small(SmallPairArgs a
   }
   // slots past the merged keys hold nothing
   if (sub == 0)
-    for (uint64_t t = slot0 + nu + threadIdx.x; t < slot1; t += nt) a.stype[t] = kEmpty;
-  // the block's counters (input with key arrays, key arrays, output, result cardinality) into its
-  // own record: no atomics and no zeroing before the call; the compaction kernel adds them up
+    for (uint32_t t = slot0 + nu + threadIdx.x; t < slot1; t += nt) st_sc1(a.smeta + t, 3ull << 19);
+  // the block's counters (input with key arrays, key arrays, output, result cardinality): one agent
+  // atomic per block and counter, read by the last block
   uint64_t v[4] = {inb, keyb, outb, csum};
   __syncthreads(); // wtot is reused below
   uint64_t *red = reinterpret_cast<uint64_t *>(dyn_lds); // every wave is past its scratch use
@@ -1600,48 +1601,67 @@ __global__ __launch_bounds__(256, kSmallWaves) void k_pair_small(SmallPairArgs a
   if (threadIdx.x < 4) {
     uint64_t x = 0;
     for (uint32_t w = 0; w < nw; ++w) x += red[4 * w + threadIdx.x];
-    a.bstat[4 * (uint64_t)blockIdx.x + threadIdx.x] = x;
+    if (x) __hip_atomic_fetch_add(a.ctr + 8 + 8 * threadIdx.x, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
+  // ---- the last block to finish compacts (see st_sc1): every storing wave's stores done, one add
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (a.stamps && threadIdx.x == 0) {
+    a.stamps[4ull * blockIdx.x] = st0;
+    a.stamps[4ull * blockIdx.x + 1] = st1;
+    a.stamps[4ull * blockIdx.x + 2] = __builtin_amdgcn_s_memrealtime();
+  }
+  if (threadIdx.x == 0)
+    s_last = __hip_atomic_fetch_add(a.ctr, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == a.nblocks - 1ull;
+  __syncthreads();
+  if (!s_last) return;
+  small_compact(a, tab, reinterpret_cast<uint32_t *>(dyn_lds), wtot);
+  if (a.stamps && threadIdx.x == 0) a.stamps[4ull * blockIdx.x + 3] = __builtin_amdgcn_s_memrealtime();
 }
 
-template <int OP>
-static void launch_small_op(bool card_only, const SmallPairArgs &a, unsigned waves, unsigned nblocks, uint32_t kmax,
-                            hipStream_t st) {
-  static bool attr = false; // allow the whole 160 KiB of a CU to one block
+template <int OP, bool CARD_ONLY, class Tab>
+static void launch_small_tab(const SmallPairArgs &a, const Tab &tab, unsigned waves, unsigned nblocks, uint32_t kmax,
+                             hipStream_t st) {
+  static bool attr = false; // allow more than the default 64 KiB of dynamic LDS
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_pair_small<OP, true>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, kSmallLdsMax);
-    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_pair_small<OP, false>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, kSmallLdsMax);
+    if (hipFuncSetAttribute(reinterpret_cast<const void *>(&k_pair_small<OP, CARD_ONLY, Tab>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, kSmallLdsMax) != hipSuccess)
+      (void)hipGetLastError(); // (the launch reports a real failure)
     attr = true;
   }
-  const uint32_t lds = small_lds_bytes(waves, kmax);
-  if (card_only) k_pair_small<OP, true><<<nblocks, 64 * waves, lds, st>>>(a, kmax);
-  else k_pair_small<OP, false><<<nblocks, 64 * waves, lds, st>>>(a, kmax);
+  // the compaction's LDS map of E <= kSmallXposLds slots fits the waves' scratch (4 x 8 KiB)
+  static_assert(kSmallXposLds * 4 <= 4 * 8192, "slot map inside the scratch");
+  static_assert(small_lds_bytes(4, kSmallPairKeys) <= kSmallLdsMax, "LDS of the largest small batch");
+  k_pair_small<OP, CARD_ONLY, Tab><<<nblocks, 64 * waves, small_lds_bytes(waves, kmax), st>>>(a, kmax, tab);
 }
+template <int OP>
+static void launch_small_op(bool card_only, const SmallPairArgs &a, const SmallTabInline *inl, const SmallTabDev &dev,
+                            unsigned waves, unsigned nblocks, uint32_t kmax, hipStream_t st) {
+  if (inl) {
+    if (card_only) launch_small_tab<OP, true>(a, *inl, waves, nblocks, kmax, st);
+    else launch_small_tab<OP, false>(a, *inl, waves, nblocks, kmax, st);
+  } else {
+    if (card_only) launch_small_tab<OP, true>(a, dev, waves, nblocks, kmax, st);
+    else launch_small_tab<OP, false>(a, dev, waves, nblocks, kmax, st);
+  }
+}
+unsigned small_resident_blocks() { return 2 * cu_count(); }
 // The call is latency-bound (a wave's merged keys run one after the other): 4 waves per block and
 // enough blocks per pair that each wave takes ~1 merged key — sized per pair (small_pair_nsub), so a
 // batch of small pairs with one large pair launches no idle blocks for the small ones (census: a
-// uniform 10 blocks per pair left ~60 % of the waves without a key after the alignment).
-void launch_pair_small_compact(const SmallPairArgs &a, hipStream_t st) {
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_pair_small_compact),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 4 * kSmallXposLds);
-    attr = true;
-  }
-  k_pair_small_compact<<<1, 1024, a.E <= kSmallXposLds ? 4 * a.E : 0, st>>>(a);
-}
-void launch_pair_small(int op, bool card_only, const SmallPairArgs &a, uint32_t max_keys, uint32_t nblocks,
-                       hipStream_t st) {
+// uniform 10 blocks per pair left ~60 % of the waves without a key after the alignment) — but no more
+// than run at once: a second round of blocks starts only as the first ends (census, 812 blocks: the
+// last started 11 us in), so the host doubles the keys per wave until the blocks fit.
+void launch_pair_small(int op, bool card_only, const SmallPairArgs &a, const SmallTabInline *inl,
+                       const SmallTabDev &dev, uint32_t max_keys, uint32_t nblocks, hipStream_t st) {
   if (!a.np) return;
   const uint32_t kmax = std::max(1u, max_keys);
   const unsigned waves = 4;
   switch (op) {
-  case RB_AND: launch_small_op<RB_AND>(card_only, a, waves, nblocks, kmax, st); break;
-  case RB_OR: launch_small_op<RB_OR>(card_only, a, waves, nblocks, kmax, st); break;
-  case RB_XOR: launch_small_op<RB_XOR>(card_only, a, waves, nblocks, kmax, st); break;
-  default: launch_small_op<RB_ANDNOT>(card_only, a, waves, nblocks, kmax, st); break;
+  case RB_AND: launch_small_op<RB_AND>(card_only, a, inl, dev, waves, nblocks, kmax, st); break;
+  case RB_OR: launch_small_op<RB_OR>(card_only, a, inl, dev, waves, nblocks, kmax, st); break;
+  case RB_XOR: launch_small_op<RB_XOR>(card_only, a, inl, dev, waves, nblocks, kmax, st); break;
+  default: launch_small_op<RB_ANDNOT>(card_only, a, inl, dev, waves, nblocks, kmax, st); break;
   }
 }
 

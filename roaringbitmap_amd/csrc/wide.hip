@@ -667,8 +667,10 @@ int wide_run(rbgpu_ctx *ctx, int sem, const rbgpu_set *in, const std::vector<uin
   if (fast_ok && (sem == RB_WORKSHY_AND || sem == RB_FAST_XOR)) {
     // workShyAnd / naive_xor fast paths read packed records; naive_xor's key-major ones for a dense set
     // in set order are the set's cached krec
-    if (in->payload_bytes >= kRecMaxPayload || ensure_mrec(in)) fast_ok = false;
-    else if (sem == RB_FAST_XOR && dense && identity && ensure_krec(in)) fast_ok = false;
+    // (a dense set's krec is built from its SoA when it has no mrec: naive_xor then never needs mrec)
+    if (in->payload_bytes >= kRecMaxPayload) fast_ok = false;
+    else if (sem == RB_FAST_XOR && dense && identity) fast_ok = !ensure_krec(in);
+    else if (ensure_mrec(in)) fast_ok = false;
   }
   (void)hipGetLastError();
 

@@ -179,6 +179,45 @@ void launch_records_transpose(const uint64_t *mrec, const uint64_t *mbase, uint3
                                                                                       key_hi, rec);
 }
 
+// The same key-major records straight from the set's SoA (no member-major mrec first): a dense set's first
+// naive_xor reads its metadata once (15 B per container: type, card, nruns, offset) and writes the 8-B
+// records transposed, instead of packing mrec (24 B) and transposing it (16 B).  Same 64 x 64 tiles: the
+// loads run along keys (a member's containers are consecutive), the stores along members.
+__global__ __launch_bounds__(256) void k_records_direct(SetView s, const uint64_t *__restrict__ mbase, uint32_t M,
+                                                        uint32_t key_lo, uint32_t key_hi, uint64_t *__restrict__ rec) {
+  __shared__ uint64_t tile[64][65];
+  const uint32_t k0 = key_lo + blockIdx.x * 64, m0 = blockIdx.y * 64;
+  const uint32_t t = threadIdx.x, kx = t & 63, ry = t >> 6;
+  uint64_t rb[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) rb[j] = mbase[min(m0 + ry + 4 * j, M - 1)];
+  const uint32_t k = min(k0 + kx, key_hi - 1);
+  uint8_t ty[16];
+  uint32_t cd[16];
+  uint16_t nr[16];
+  uint64_t of[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) { // all 64 loads in flight at once
+    const uint64_t i = rb[j] + k;
+    ty[j] = s.type[i];
+    cd[j] = s.card[i];
+    nr[j] = s.nruns[i];
+    of[j] = s.off[i];
+  }
+#pragma unroll
+  for (int j = 0; j < 16; ++j) tile[ry + 4 * j][kx] = pack_rec(ty[j], cd[j], nr[j], of[j]);
+  __syncthreads();
+  for (uint32_t r = ry; r < 64; r += 4) { // writes along members
+    const uint32_t kw = k0 + r, i = m0 + kx;
+    if (i < M && kw < key_hi) rec[(uint64_t)(kw - key_lo) * M + i] = tile[kx][r];
+  }
+}
+void launch_records_direct(const SetView &s, const uint64_t *mbase, uint32_t M, uint32_t key_lo, uint32_t key_hi,
+                           uint64_t *rec, hipStream_t st) {
+  if (!M || key_hi <= key_lo) return;
+  k_records_direct<<<dim3((key_hi - key_lo + 63) / 64, (M + 63) / 64), 256, 0, st>>>(s, mbase, M, key_lo, key_hi, rec);
+}
+
 // Members grouped by the counting sort: a gather of the packed records through the container ids (the
 // grouped count, seg[65536], can be less than the members' containers when the call is a key-range shard).
 __global__ __launch_bounds__(256) void k_records_gather(const uint64_t *__restrict__ mrec,

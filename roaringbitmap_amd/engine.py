@@ -290,6 +290,12 @@ class DeviceSet:
         L.check(L.lib().rbgpu_set_setup_stats(self.h, C.byref(ms), C.byref(b)))
         return {"ms": round(ms.value, 4), "bytes": int(b.value)}
 
+    def setup_parts(self) -> dict:
+        """rbgpu_set_setup_parts: {item: {ms, bytes}} for the dense check, mrec and krec built so far."""
+        ms, b = (C.c_double * 3)(), np.zeros(3, np.uint64)
+        L.check(L.lib().rbgpu_set_setup_parts(self.h, ms, b.ctypes.data_as(L._U64P)))
+        return {k: {"ms": round(ms[i], 4), "bytes": int(b[i])} for i, k in enumerate(("dense_check", "mrec", "krec"))}
+
     def download(self, first: int = 0, count: Optional[int] = None) -> HostSoA:
         count = len(self) - first if count is None else count
         q = L.RbSoa()
