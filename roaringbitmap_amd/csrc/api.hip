@@ -991,9 +991,10 @@ static int pairwise_small(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgp
   const uint64_t E = acc;
   // merged keys per wave: 1, or doubled until the blocks fit the resident ones (one round of blocks)
   const uint64_t resident = small_resident_blocks();
+  auto nsub = [&](uint32_t p, uint32_t kpw) { return small_pair_nsub(slot[p + 1] - slot[p], cap, kpw); };
   auto blocks_for = [&](uint32_t kpw) {
     uint64_t n = 0;
-    for (uint32_t p = 0; p < np; ++p) n += small_pair_nsub(slot[p + 1] - slot[p], cap, kpw);
+    for (uint32_t p = 0; p < np; ++p) n += nsub(p, kpw);
     return n;
   };
   uint32_t kpw = 1;
@@ -1006,7 +1007,7 @@ static int pairwise_small(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgp
   for (uint32_t p = 0, k = 0; p <= np; ++p) {
     if (inl) ti->blk[p] = (uint16_t)k;
     else blk[p] = k;
-    if (p < np) k += small_pair_nsub(slot[p + 1] - slot[p], cap, kpw);
+    if (p < np) k += nsub(p, kpw);
   }
   // host-visible words the last block writes the call's results to (8 words)
   if (!ctx->h_small) {
@@ -1028,8 +1029,7 @@ static int pairwise_small(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgp
   const bool card_only = out == nullptr;
   const uint64_t E1 = std::max<uint64_t>(E, 1);
   const size_t tabb = inl ? 0 : 4 * tabv.size();
-  const size_t need = aligned256(8ull * np) + aligned256(4 * E1) + aligned256(8 * E1) + aligned256(tabb) +
-                      aligned256(32ull * nblocks) + 256;
+  const size_t need = aligned256(8ull * np) + aligned256(4 * E1) + aligned256(8 * E1) + aligned256(tabb) + 256;
   if (ctx->ws_pairs.reserve(need, st) != hipSuccess) return fail(RB_ENOMEM, "pair workspace");
   Workspace &W = ctx->ws_pairs;
   SmallPairArgs sa{};
@@ -1054,12 +1054,6 @@ static int pairwise_small(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgp
   uint32_t *xpos = W.take<uint32_t>(E1);
   sa.smeta = W.take<uint64_t>(E1);
   sa.ctr = ctx->d_small_ctr;
-  const char *stv = getenv("RBGPU_SMALL_STAMPS"); // study: per-block timeline to stderr
-  const bool stamps = stv && stv[0] == '1';
-  if (stamps) {
-    sa.stamps = W.take<uint64_t>(4ull * nblocks);
-    HIPCHK(hipMemsetAsync(sa.stamps, 0, 32ull * nblocks, st));
-  }
 
   rbgpu_set *res = nullptr;
   if (!card_only) {
@@ -1105,39 +1099,6 @@ static int pairwise_small(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgp
   w[1] = hout[3];           // output bytes
   w[7] = hout[4];           // result cardinality
   const uint64_t nres = hout[0];
-  if (stamps) { // block start / keys aligned / work done, and the compaction's end (last block), in us
-    std::vector<uint64_t> h(4ull * nblocks);
-    HIPCHK(hipMemcpy(h.data(), sa.stamps, 32ull * nblocks, hipMemcpyDeviceToHost));
-    uint64_t t0 = ~0ull, tend = 0, tlast = 0;
-    double align = 0, work = 0;
-    for (uint32_t i = 0; i < nblocks; ++i) {
-      t0 = std::min(t0, h[4 * i]);
-      tend = std::max(tend, h[4 * i + 2]);
-      tlast = std::max(tlast, h[4 * i + 3]);
-      align += (double)(h[4 * i + 1] - h[4 * i]);
-      work += (double)(h[4 * i + 2] - h[4 * i + 1]);
-    }
-    uint64_t late = 0;
-    for (uint32_t i = 0; i < nblocks; ++i) late = std::max(late, h[4 * i] - t0);
-    std::vector<uint64_t> dur(nblocks), wk(nblocks);
-    uint32_t ilast = 0;
-    for (uint32_t i = 0; i < nblocks; ++i) {
-      dur[i] = h[4 * i + 2] - h[4 * i];
-      wk[i] = h[4 * i + 2] - h[4 * i + 1];
-      if (h[4 * i + 2] > h[4 * ilast + 2]) ilast = i;
-    }
-    std::vector<uint64_t> ds = dur;
-    std::sort(ds.begin(), ds.end());
-    uint32_t pl = 0;
-    for (uint32_t p = 0; p < np; ++p)
-      if ((inl ? (uint32_t)ti->blk[p] : blk[p]) <= ilast) pl = p;
-    fprintf(stderr, "small stamps: block duration p50 %.2f p90 %.2f max %.2f us; latest block %u (pair %u, %u keys, "
-                    "work %.2f us, kpw %u)\n", ds[nblocks / 2] / 100.0, ds[nblocks * 9 / 10] / 100.0,
-            ds[nblocks - 1] / 100.0, ilast, pl, (unsigned)(slot[pl + 1] - slot[pl]), wk[ilast] / 100.0, kpw);
-    fprintf(stderr, "small stamps: blocks %u E %llu | last start +%.2f us, last work end +%.2f us, compaction end +%.2f us | "
-                    "mean align %.2f us, mean work %.2f us\n", nblocks, (unsigned long long)E, late / 100.0,
-            (tend - t0) / 100.0, (tlast - t0) / 100.0, align / nblocks / 100.0, work / nblocks / 100.0);
-  }
   const KernelSpan spans[1] = {{"k_pair_small", 6, 1, E}};
   rc = stats_fill(ctx, E, nres, spans, ktimes ? 1 : 0);
   if (rc) {

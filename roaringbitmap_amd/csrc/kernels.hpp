@@ -155,9 +155,10 @@ struct SmallPairArgs {
   uint32_t *xpos;
   uint64_t *rbegin, *hout;
   OutView out;
-  uint64_t *stamps; // study (RBGPU_SMALL_STAMPS=1): per block 4 s_memrealtime stamps, else null
 };
-// blocks of one pair with nk keys (na + nb): kpw merged keys per wave, 4 waves per block, at most `cap`
+// blocks of one pair of nk = na + nb keys: up to kpw merged keys per wave, 4 waves per block, at most `cap`
+// (a floor of one wave per key of the larger side — a matched key takes the costly register path — measured
+// slower on census: 769 blocks, two rounds)
 __host__ __device__ inline uint32_t small_pair_nsub(uint64_t nk, uint32_t cap, uint32_t kpw) {
   const uint64_t b = (nk + 4ull * kpw - 1) / (4ull * kpw);
   return (uint32_t)(b < 1 ? 1 : b > cap ? cap : b);

@@ -1429,13 +1429,13 @@ __device__ void small_compact(const SmallPairArgs &a, const Tab &tab, uint32_t *
   }
 }
 
-// Dynamic LDS of k_pair_small: per wave an 8 KiB scratch, then the merged-key list, the keys and the
-// match prefix, each sized by the batch's largest na + nb (kmax).
+// Dynamic LDS of k_pair_small: per wave an 8 KiB scratch, then the merged-key list, the keys, the match
+// prefix and the work order, each sized by the batch's largest na + nb (kmax).
 constexpr int kSmallLdsMax = 96 * 1024; // >= small_lds_bytes(4, kSmallPairKeys) (~64 KiB), beside the static LDS
 // (All LDS of the kernel is in the dynamic region, whose base stays 16-B aligned — the 8 KiB scratch
 // takes 16-B accesses.)
 __host__ __device__ constexpr uint32_t small_lds_bytes(uint32_t waves, uint32_t kmax) {
-  return waves * 8192u + 64u + 4u * kmax + 2u * kmax + 2u * (kmax + 1) + 16u;
+  return waves * 8192u + 64u + 4u * kmax + 2u * kmax + 2u * (kmax + 1) + 2u * kmax + 16u;
 }
 constexpr int kSmallWaves = 2; // waves per SIMD of the small-batch kernel (the register path takes ~235 VGPRs; 3 and 4 spill)
 template <int OP, bool CARD_ONLY, class Tab>
@@ -1447,8 +1447,8 @@ __global__ __launch_bounds__(256, kSmallWaves) void k_pair_small(SmallPairArgs a
   uint32_t *ent = wtot + 16; // merged key: A index | B index << 16
   uint16_t *K = reinterpret_cast<uint16_t *>(ent + kmax);             // A's keys, then B's
   uint16_t *mpref = K + kmax;                                          // matched keys among A[0, i)
+  uint16_t *ord = mpref + kmax + 1;                                    // merged positions in work order
   const int lane = lane_id(), wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint64_t st0 = a.stamps ? __builtin_amdgcn_s_memrealtime() : 0;
   // the block's pair and rank within it: the last pair whose first block is <= blockIdx.x (the host's
   // per-pair block prefix; small_pair_nsub blocks per pair)
   uint32_t p = 0;
@@ -1495,13 +1495,31 @@ __global__ __launch_bounds__(256, kSmallWaves) void k_pair_small(SmallPairArgs a
   }
   __syncthreads();
   const uint32_t nu = na + nb - matches;
-  const uint64_t st1 = a.stamps ? __builtin_amdgcn_s_memrealtime() : 0;
+  // ---- work order: the matched keys first (each takes the register path, the costly kind), then the rest,
+  //      dealt to the pair's waves back and forth (below), so a matched key rarely waits behind another
+  //      (census: a pair of 55 matched keys among 66 had two waves with two of them)
+  {
+    const uint32_t per2 = (nu + nt - 1) / nt, e0 = min(threadIdx.x * per2, nu), e1 = min(e0 + per2, nu);
+    uint32_t mc = 0;
+    for (uint32_t e = e0; e < e1; ++e) mc += (ent[e] & 0xFFFFu) != 0xFFFFu && (ent[e] >> 16) != 0xFFFFu;
+    uint32_t mtot;
+    uint32_t mb = block_xscan(mc, wtot, mtot), ub = e0 - mb;
+    for (uint32_t e = e0; e < e1; ++e) {
+      if ((ent[e] & 0xFFFFu) != 0xFFFFu && (ent[e] >> 16) != 0xFFFFu) ord[mb++] = (uint16_t)e;
+      else ord[mtot + ub++] = (uint16_t)e;
+    }
+    __syncthreads();
+  }
   // ---- one wave per merged key
   uint32_t *s = reinterpret_cast<uint32_t *>(dyn_lds) + wv * 2048;
   const uint32_t slot0 = tab.slot_at(p), slot1 = tab.slot_at(p + 1);
   const uint64_t keyb = sub == 0 && wv == 0 && lane == 0 ? 2ull * (na + nb) : 0ull;
   uint64_t inb = keyb, outb = 0, csum = 0;
-  for (uint32_t e = nw * sub + wv; e < nu; e += nw * nsub) {
+  const uint32_t gw = nw * sub + wv, W = nw * nsub; // this wave among the pair's
+  for (uint32_t k = 0; k * W < nu; ++k) {
+    const uint32_t pos = (k & 1) ? (k + 1) * W - 1 - gw : k * W + gw;
+    if (pos >= nu) continue;
+    const uint32_t e = ord[pos];
     const uint32_t en = ent[e], ia = en & 0xFFFF, ib = en >> 16;
     const bool has_a = ia != 0xFFFFu, has_b = ib != 0xFFFFu;
     const uint64_t slot = (uint64_t)slot0 + e;
@@ -1606,17 +1624,11 @@ __global__ __launch_bounds__(256, kSmallWaves) void k_pair_small(SmallPairArgs a
   // ---- the last block to finish compacts (see st_sc1): every storing wave's stores done, one add
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (a.stamps && threadIdx.x == 0) {
-    a.stamps[4ull * blockIdx.x] = st0;
-    a.stamps[4ull * blockIdx.x + 1] = st1;
-    a.stamps[4ull * blockIdx.x + 2] = __builtin_amdgcn_s_memrealtime();
-  }
   if (threadIdx.x == 0)
     s_last = __hip_atomic_fetch_add(a.ctr, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == a.nblocks - 1ull;
   __syncthreads();
   if (!s_last) return;
   small_compact(a, tab, reinterpret_cast<uint32_t *>(dyn_lds), wtot);
-  if (a.stamps && threadIdx.x == 0) a.stamps[4ull * blockIdx.x + 3] = __builtin_amdgcn_s_memrealtime();
 }
 
 template <int OP, bool CARD_ONLY, class Tab>

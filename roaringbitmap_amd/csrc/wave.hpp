@@ -671,12 +671,16 @@ __device__ __forceinline__ uint32_t emit_container(int type, const uint64_t (&w)
   return 4u * (uint32_t)runs;
 }
 
-// Copy a payload (multiple of 16 bytes after rounding; slots are 16-B padded).
+// Copy a payload (multiple of 16 bytes after rounding; slots are 16-B padded), 8 KiB per round with every
+// load of the round in flight before its stores (a load -> store loop waits one memory latency per 1 KiB:
+// the compiler cannot move a load above the previous iteration's store)
 __device__ __forceinline__ void copy_payload(const uint8_t *src, uint8_t *dst, uint64_t bytes, int lane) {
-  const uint4 *a = reinterpret_cast<const uint4 *>(src);
-  uint4 *b = reinterpret_cast<uint4 *>(dst);
-  const uint64_t n = (bytes + 15) >> 4;
-  for (uint64_t i = lane; i < n; i += 64) b[i] = a[i];
+  for (uint64_t o = 0; o < bytes; o += kBitmapBytes) {
+    const uint32_t nb = (uint32_t)min<uint64_t>(bytes - o, (uint64_t)kBitmapBytes);
+    uint4 q[8];
+    load_chunks(q, src + o, nb, lane);
+    store_chunks(q, dst + o, nb, lane);
+  }
 }
 
 } // namespace rbg

@@ -1,5 +1,5 @@
 #!/bin/bash
-# The full GPU suite, then the census latency per op (with and without per-kernel events).
+# The full GPU suite, then the census latency per op.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 O=gpurun_out/r5sc
 mkdir -p $O
