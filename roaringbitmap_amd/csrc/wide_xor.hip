@@ -183,6 +183,8 @@ void launch_records_transpose(const uint64_t *mrec, const uint64_t *mbase, uint3
 // naive_xor reads its metadata once (15 B per container: type, card, nruns, offset) and writes the 8-B
 // records transposed, instead of packing mrec (24 B) and transposing it (16 B).  Same 64 x 64 tiles: the
 // loads run along keys (a member's containers are consecutive), the stores along members.
+// (Measured: 64 x 64 tiles dealt key-tile-major, 128 x 32 and 256 x 16 tiles, and 8 x 8 / 16 x 16 groups of
+// tiles dealt together all build config 4's records in 2.0-2.3 ms, profiles/r05/krec.)
 __global__ __launch_bounds__(256) void k_records_direct(SetView s, const uint64_t *__restrict__ mbase, uint32_t M,
                                                         uint32_t key_lo, uint32_t key_hi, uint64_t *__restrict__ rec) {
   __shared__ uint64_t tile[64][65];
