@@ -258,25 +258,27 @@ int ensure_krec(const rbgpu_set *cs) {
   if (s->payload_bytes >= kRecMaxPayload) return fail(RB_EINVAL, "packed records hold 40-bit payload offsets");
   HIPCHK(hipSetDevice(s->ctx->device));
   hipStream_t st = s->ctx->stream;
-  uint64_t *k = nullptr, *mb = nullptr;
-  if (s->ctx->pool.alloc((void **)&k, std::max<uint64_t>(s->nc, 1) * 8) || s->ctx->pool.alloc((void **)&mb, s->nb * 8ull)) {
-    s->ctx->pool.release(k);
-    return fail(RB_ENOMEM, "key-major records");
-  }
-  // member bases in set order: container of bitmap b at key x is h_begin[b] + x - dense_lo
-  std::vector<uint64_t> hb(s->nb);
-  for (uint32_t b = 0; b < s->nb; ++b) hb[b] = s->h_begin[b] - (uint64_t)s->dense_lo;
-  // from mrec when the set already has it (16 B per container), else from the SoA itself (15 B of metadata
-  // read, an 8-B record written: k_records_direct)
+  uint64_t *k = nullptr;
+  if (s->ctx->pool.alloc((void **)&k, std::max<uint64_t>(s->nc, 1) * 8)) return fail(RB_ENOMEM, "key-major records");
+  // member m's container at key x is begin[m] + x - dense_lo: the set's own device begin array, no host
+  // table copied up (a pageable 32 KiB copy cost ~0.8 ms inside the timed setup).  From mrec when the set
+  // already has it (16 B per container), else from the SoA itself (15 B of metadata read, an 8-B record
+  // written: k_records_direct).
   const bool from_mrec = s->mrec != nullptr;
+  const SetView v = s->view();
+  // two containers per load: member m's first container begin[m] at an even index and the arrays aligned for it
+  bool even_bases = !((uintptr_t)v.type & 1) && !((uintptr_t)v.card & 7) && !((uintptr_t)v.nruns & 3) &&
+                    !((uintptr_t)v.off & 15);
+  for (uint32_t b = 0; b < s->nb && even_bases; ++b) even_bases = !(s->h_begin[b] & 1);
   {
     DeriveTimer t(s, 2);
-    if (hipMemcpyAsync(mb, hb.data(), s->nb * 8ull, hipMemcpyHostToDevice, st) == hipSuccess) {
-      if (from_mrec) launch_records_transpose(s->mrec, mb, s->nb, (uint32_t)s->dense_lo, (uint32_t)s->dense_hi, k, st);
-      else launch_records_direct(s->view(), mb, s->nb, (uint32_t)s->dense_lo, (uint32_t)s->dense_hi, k, st);
-    }
+    if (from_mrec)
+      launch_records_transpose(s->mrec, v.begin, (uint64_t)s->dense_lo, s->nb, (uint32_t)s->dense_lo,
+                               (uint32_t)s->dense_hi, k, st);
+    else
+      launch_records_direct(v, v.begin, (uint64_t)s->dense_lo, s->nb, (uint32_t)s->dense_lo, (uint32_t)s->dense_hi, k, st,
+                            even_bases);
   }
-  s->ctx->pool.release(mb);
   if (hipGetLastError() != hipSuccess) {
     s->ctx->pool.release(k);
     return fail(RB_EDEVICE, "key-major record kernel failed");

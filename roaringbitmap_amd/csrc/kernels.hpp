@@ -210,9 +210,11 @@ struct XorRecords {
   const uint64_t *mrec, *mbase;
   uint32_t M, key_lo, key_hi;
 };
-void launch_records_direct(const SetView &s, const uint64_t *mbase, uint32_t M, uint32_t key_lo, uint32_t key_hi,
-                           uint64_t *rec, hipStream_t st);
-void launch_records_transpose(const uint64_t *mrec, const uint64_t *mbase, uint32_t M, uint32_t key_lo,
+// member m's container at key k is mbase[m] - bias + k (a dense set: mbase = the set's begin, bias = key_lo)
+// pairs: every mbase[m] - bias + key_lo is even (two containers per lane, 128-key tiles)
+void launch_records_direct(const SetView &s, const uint64_t *mbase, uint64_t bias, uint32_t M, uint32_t key_lo,
+                           uint32_t key_hi, uint64_t *rec, hipStream_t st, bool pairs = false);
+void launch_records_transpose(const uint64_t *mrec, const uint64_t *mbase, uint64_t bias, uint32_t M, uint32_t key_lo,
                               uint32_t key_hi, uint64_t *rec, hipStream_t st);
 void launch_wide_runs_xor(const SetView &s, const uint32_t *cid, const uint64_t *seg, const uint32_t *klist,
                           uint32_t nk, uint8_t *out, const WideOut &wo, uint8_t *route, uint64_t *stats,

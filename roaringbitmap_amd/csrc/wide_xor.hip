@@ -152,14 +152,15 @@ __device__ __forceinline__ uint32_t compose(uint32_t later, uint32_t earlier) {
 // records (mrec) transposed through LDS, so both the reads (along keys) and the writes (along members)
 // are coalesced.
 __global__ __launch_bounds__(256) void k_records_transpose(const uint64_t *__restrict__ mrec,
-                                                           const uint64_t *__restrict__ mbase, uint32_t M,
-                                                           uint32_t key_lo, uint32_t key_hi, uint64_t *__restrict__ rec) {
+                                                           const uint64_t *__restrict__ mbase, uint64_t bias,
+                                                           uint32_t M, uint32_t key_lo, uint32_t key_hi,
+                                                           uint64_t *__restrict__ rec) {
   __shared__ uint64_t tile[64][65]; // [member][key], padded against bank conflicts on the column reads
   const uint32_t k0 = key_lo + blockIdx.x * 64, m0 = blockIdx.y * 64;
   const uint32_t t = threadIdx.x, kx = t & 63, ry = t >> 6;
   uint64_t rb[16];
 #pragma unroll
-  for (int j = 0; j < 16; ++j) rb[j] = mbase[min(m0 + ry + 4 * j, M - 1)];
+  for (int j = 0; j < 16; ++j) rb[j] = mbase[min(m0 + ry + 4 * j, M - 1)] - bias;
   const uint32_t k = min(k0 + kx, key_hi - 1);
   uint64_t v[16];
 #pragma unroll
@@ -172,10 +173,10 @@ __global__ __launch_bounds__(256) void k_records_transpose(const uint64_t *__res
     if (i < M && kw < key_hi) rec[(uint64_t)(kw - key_lo) * M + i] = tile[kx][r];
   }
 }
-void launch_records_transpose(const uint64_t *mrec, const uint64_t *mbase, uint32_t M, uint32_t key_lo,
+void launch_records_transpose(const uint64_t *mrec, const uint64_t *mbase, uint64_t bias, uint32_t M, uint32_t key_lo,
                               uint32_t key_hi, uint64_t *rec, hipStream_t st) {
   if (!M || key_hi <= key_lo) return;
-  k_records_transpose<<<dim3((key_hi - key_lo + 63) / 64, (M + 63) / 64), 256, 0, st>>>(mrec, mbase, M, key_lo,
+  k_records_transpose<<<dim3((key_hi - key_lo + 63) / 64, (M + 63) / 64), 256, 0, st>>>(mrec, mbase, bias, M, key_lo,
                                                                                       key_hi, rec);
 }
 
@@ -185,14 +186,15 @@ void launch_records_transpose(const uint64_t *mrec, const uint64_t *mbase, uint3
 // loads run along keys (a member's containers are consecutive), the stores along members.
 // (Measured: 64 x 64 tiles dealt key-tile-major, 128 x 32 and 256 x 16 tiles, and 8 x 8 / 16 x 16 groups of
 // tiles dealt together all build config 4's records in 2.0-2.3 ms, profiles/r05/krec.)
-__global__ __launch_bounds__(256) void k_records_direct(SetView s, const uint64_t *__restrict__ mbase, uint32_t M,
-                                                        uint32_t key_lo, uint32_t key_hi, uint64_t *__restrict__ rec) {
+__global__ __launch_bounds__(256) void k_records_direct(SetView s, const uint64_t *__restrict__ mbase, uint64_t bias,
+                                                        uint32_t M, uint32_t key_lo, uint32_t key_hi,
+                                                        uint64_t *__restrict__ rec) {
   __shared__ uint64_t tile[64][65];
   const uint32_t k0 = key_lo + blockIdx.x * 64, m0 = blockIdx.y * 64;
   const uint32_t t = threadIdx.x, kx = t & 63, ry = t >> 6;
   uint64_t rb[16];
 #pragma unroll
-  for (int j = 0; j < 16; ++j) rb[j] = mbase[min(m0 + ry + 4 * j, M - 1)];
+  for (int j = 0; j < 16; ++j) rb[j] = mbase[min(m0 + ry + 4 * j, M - 1)] - bias;
   const uint32_t k = min(k0 + kx, key_hi - 1);
   uint8_t ty[16];
   uint32_t cd[16];
@@ -214,10 +216,57 @@ __global__ __launch_bounds__(256) void k_records_direct(SetView s, const uint64_
     if (i < M && kw < key_hi) rec[(uint64_t)(kw - key_lo) * M + i] = tile[kx][r];
   }
 }
-void launch_records_direct(const SetView &s, const uint64_t *mbase, uint32_t M, uint32_t key_lo, uint32_t key_hi,
-                           uint64_t *rec, hipStream_t st) {
+// The same with 128-key tiles and two containers per lane (u16 / 8-B / 4-B / 16-B loads, 16-B stores): every
+// load row is whole 128-B lines (a 64-key row of the u8 types is half a line).  Needs even container bases,
+// an even key count and an even member count, as a dense set of whole 65536-key members has; other sets
+// take the 64 x 64 tiles above.
+__global__ __launch_bounds__(256) void k_records_direct2(SetView s, const uint64_t *__restrict__ mbase, uint64_t bias,
+                                                         uint32_t M, uint32_t key_lo, uint32_t key_hi,
+                                                         uint64_t *__restrict__ rec) {
+  __shared__ uint64_t tile[64][129]; // [member][key]
+  const uint32_t k0 = key_lo + blockIdx.x * 128, m0 = blockIdx.y * 64;
+  const uint32_t t = threadIdx.x, kx = t & 63, ry = t >> 6;
+  uint64_t rb[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) rb[j] = mbase[min(m0 + ry + 4 * j, M - 1)] - bias;
+  const uint32_t k = min(k0 + 2 * kx, key_hi - 2);
+  uint32_t ty[16], nr[16];
+  uint2 cd[16];
+  uint4 of[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) { // all 64 loads in flight at once
+    const uint64_t i = rb[j] + k;
+    ty[j] = *reinterpret_cast<const uint16_t *>(s.type + i);
+    cd[j] = *reinterpret_cast<const uint2 *>(s.card + i);
+    nr[j] = *reinterpret_cast<const uint32_t *>(s.nruns + i);
+    of[j] = *reinterpret_cast<const uint4 *>(s.off + i);
+  }
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    tile[ry + 4 * j][2 * kx] = pack_rec(ty[j] & 0xFFu, cd[j].x, nr[j] & 0xFFFFu, of[j].x | ((uint64_t)of[j].y << 32));
+    tile[ry + 4 * j][2 * kx + 1] = pack_rec(ty[j] >> 8, cd[j].y, nr[j] >> 16, of[j].z | ((uint64_t)of[j].w << 32));
+  }
+  __syncthreads();
+  const uint32_t lx = t & 31, rr = t >> 5; // a key row is 32 lanes x 2 members: 8 rows per pass
+  const uint32_t i = m0 + 2 * lx;
+  for (uint32_t r = rr; r < 128; r += 8) {
+    const uint32_t kw = k0 + r;
+    if (i < M && kw < key_hi) {
+      const uint64_t a = tile[2 * lx][r], b = tile[2 * lx + 1][r];
+      *reinterpret_cast<uint4 *>(rec + (uint64_t)(kw - key_lo) * M + i) =
+          make_uint4((uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32));
+    }
+  }
+}
+void launch_records_direct(const SetView &s, const uint64_t *mbase, uint64_t bias, uint32_t M, uint32_t key_lo,
+                           uint32_t key_hi, uint64_t *rec, hipStream_t st, bool pairs) {
   if (!M || key_hi <= key_lo) return;
-  k_records_direct<<<dim3((key_hi - key_lo + 63) / 64, (M + 63) / 64), 256, 0, st>>>(s, mbase, M, key_lo, key_hi, rec);
+  if (pairs && !(M & 1) && !((key_hi - key_lo) & 1))
+    k_records_direct2<<<dim3((key_hi - key_lo + 127) / 128, (M + 63) / 64), 256, 0, st>>>(s, mbase, bias, M, key_lo,
+                                                                                          key_hi, rec);
+  else
+    k_records_direct<<<dim3((key_hi - key_lo + 63) / 64, (M + 63) / 64), 256, 0, st>>>(s, mbase, bias, M, key_lo,
+                                                                                      key_hi, rec);
 }
 
 // Members grouped by the counting sort: a gather of the packed records through the container ids (the
@@ -927,7 +976,7 @@ void launch_wide_runs_xor(const SetView &s, const uint32_t *cid, const uint64_t 
   const char *e = getenv("RBGPU_XOR_NO_FASTFWD");
   const int fastfwd = !(e && e[0] == '1');
   if (xr.build == XorRecords::kTranspose) {
-    launch_records_transpose(xr.mrec, xr.mbase, xr.M, xr.key_lo, xr.key_hi, xr.rec, st);
+    launch_records_transpose(xr.mrec, xr.mbase, 0, xr.M, xr.key_lo, xr.key_hi, xr.rec, st);
   } else if (xr.build == XorRecords::kGather && xr.n) {
     k_records_gather<<<(unsigned)std::min<uint64_t>((xr.n + 255) / 256, 65536), 256, 0, st>>>(xr.mrec, cid, seg,
                                                                                            xr.rec);

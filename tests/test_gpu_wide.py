@@ -563,13 +563,16 @@ def test_dense_sets_skip_grouping(ctx, oracle):
 def test_dense_run_shard_records(ctx, oracle):
     """Config-4 shape generated as a key-range shard (dense_lo > 0): workShyAnd through the packed
     records, naive_xor through the set's cached key-major records (set order) and through per-call
-    transposed records (reversed order), naive_or through dense ids — all equal to the oracle."""
+    transposed records (reversed order), naive_or through dense ids — all equal to the oracle.  Even
+    member and key counts build the key-major records two containers per lane (128-key tiles); an odd
+    key count (odd member bases) or an odd member count takes the 64 x 64 tiles."""
     import roaringbitmap_amd as rb
-    a = ctx.generate_keys(rb.WL_WIDE_RUNS, 40, 300, 700, seed=5)
-    refs = [oracle.RefBitmap.deserialize(b) for b in a.serialize()]
-    for members in (np.arange(40, dtype=np.uint32), np.arange(39, -1, -1, dtype=np.uint32)):
-        for sem in ("FAST_OR", "FAST_AND", "WORKSHY_AND", "FAST_XOR", "PAR_XOR"):
-            _check(ctx, oracle, a, refs, sem, members)
-        # the cached records are reused call after call
-        for _ in range(2):
-            _check(ctx, oracle, a, refs, "FAST_XOR", members)
+    for nb, lo, hi in ((40, 300, 700), (40, 300, 701), (41, 300, 700)):
+        a = ctx.generate_keys(rb.WL_WIDE_RUNS, nb, lo, hi, seed=5)
+        refs = [oracle.RefBitmap.deserialize(b) for b in a.serialize()]
+        for members in (np.arange(nb, dtype=np.uint32), np.arange(nb - 1, -1, -1, dtype=np.uint32)):
+            for sem in ("FAST_OR", "FAST_AND", "WORKSHY_AND", "FAST_XOR", "PAR_XOR"):
+                _check(ctx, oracle, a, refs, sem, members)
+            # the cached records are reused call after call
+            for _ in range(2):
+                _check(ctx, oracle, a, refs, "FAST_XOR", members)
