@@ -87,13 +87,126 @@ __device__ __forceinline__ WalkMeta pick_meta(const WalkMeta (&m)[kWalkRegs], ui
   return r;
 }
 
+// Array ⊙ Array as a merge (ArrayContainer.and / or / xor / andNot of two Arrays, ArrayContainer.java:
+// 184-227, 949-973, 1311-1336, 243-271): both sorted arrays in the wave's 8 KiB LDS scratch and a merge
+// path over them instead of two 65536-bit register images.  Lane l walks the merged positions
+// [l n / 64, (l + 1) n / 64) of A and B (A first on equal values: a value in both arrays is the pair
+// A[i], B[j] next to each other, wherever the lanes' ranges split), once to count the values it keeps
+// and once, after a wave scan of the counts, to store them.  With ca + cb <= kMergeMax the result is an
+// Array (ArrayContainer.or / xor merge below DEFAULT_MAX_SIZE; and / andNot are subsets of A), the type
+// the register path gives these pairs; OR and XOR are symmetric, so either operand may be A.
+#ifndef RBG_SMALL_MERGE
+#define RBG_SMALL_MERGE 1 // study builds: 0 sends small-batch Array pairs through the register path
+#endif
+#ifndef RBG_LIGHT_MERGE
+#define RBG_LIGHT_MERGE 1 // study builds: 0 leaves OR / XOR Array pairs to the heavy (register path) kernel
+#endif
+constexpr uint32_t kMergeMax = 4088; // ca + cb: A at 0, B 16-B aligned after it, both in 8 KiB
+template <int OP>
+__device__ __forceinline__ bool merge_keep(bool from_a, bool matched) {
+  if (OP == RB_AND) return from_a && matched;
+  if (OP == RB_ANDNOT) return from_a && !matched;
+  if (OP == RB_OR) return from_a || !matched;
+  return !matched; // XOR
+}
+template <int OP, bool STORE>
+__device__ __forceinline__ uint32_t merge_walk(const uint16_t *A, uint32_t ca, const uint16_t *B, uint32_t cb,
+                                               uint32_t i, uint32_t j, uint32_t steps, uint16_t *out) {
+  constexpr uint32_t kEnd = 0x10000u; // past every u16 value
+  uint32_t av = i < ca ? A[i] : kEnd, bv = j < cb ? B[j] : kEnd;
+  uint32_t prev_a = i ? A[i - 1] : kEnd + 1; // the last A value before this position
+  uint32_t cnt = 0;
+  for (uint32_t d = 0; d < steps; ++d) {
+    if (av <= bv) { // A's value (both kEnd is impossible: the walk stays below ca + cb)
+      if (merge_keep<OP>(true, av == bv)) {
+        if (STORE) out[cnt] = (uint16_t)av;
+        ++cnt;
+      }
+      prev_a = av;
+      ++i;
+      av = i < ca ? A[i] : kEnd;
+    } else {
+      if (merge_keep<OP>(false, prev_a == bv)) {
+        if (STORE) out[cnt] = (uint16_t)bv;
+        ++cnt;
+      }
+      ++j;
+      bv = j < cb ? B[j] : kEnd;
+    }
+  }
+  return cnt;
+}
+__device__ __forceinline__ uint32_t merge_boff(uint32_t ca) { return (ca + 7u) & ~7u; } // B's first value (u16)
+// the two preloaded payloads (register chunks of ca / cb sorted u16 values) as A and B in the scratch
+__device__ __forceinline__ void merge_stage(const uint4 (&q)[8], uint32_t ca, const uint4 (&r)[8], uint32_t cb,
+                                            uint32_t *s, int lane) {
+  uint4 *s4 = reinterpret_cast<uint4 *>(s);
+  const uint32_t na4 = (2u * ca + 15u) >> 4, nb4 = (2u * cb + 15u) >> 4, b4 = merge_boff(ca) >> 3;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const uint32_t c = (uint32_t)lane + 64u * k;
+    if (c < na4) s4[c] = q[k];
+    if (c < nb4) s4[b4 + c] = r[k];
+  }
+  wave_lds_sync();
+}
+template <int OP, bool STORE>
+__device__ __forceinline__ uint32_t merge_run(const uint32_t *s, uint32_t ca, uint32_t cb, uint16_t *out, int lane) {
+  const uint16_t *A = reinterpret_cast<const uint16_t *>(s), *B = A + merge_boff(ca);
+  const uint32_t n = ca + cb;
+  const uint32_t d0 = ((uint32_t)lane * n) >> 6, d1 = ((uint32_t)(lane + 1) * n) >> 6;
+  // merge path: the number of A values among the first d0 merged values (A first on ties)
+  uint32_t lo = d0 > cb ? d0 - cb : 0u, hi = min(d0, ca);
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (A[mid] <= B[d0 - mid - 1]) lo = mid + 1;
+    else hi = mid;
+  }
+  const uint32_t cnt = merge_walk<OP, false>(A, ca, B, cb, lo, d0 - lo, d1 - d0, nullptr);
+  const uint32_t incl = wave_scan_u32(cnt, lane), tot = readlane(incl, 63);
+  if (STORE && tot) merge_walk<OP, true>(A, ca, B, cb, lo, d0 - lo, d1 - d0, out + (incl - cnt));
+  wave_lds_sync(); // the next task restages the scratch
+  return tot;
+}
+
+// The same pairs through an LDS image instead (study: RBG_LIGHT_MERGE=2): A's values ORed into a zeroed
+// 8 KiB image, B's ORed (OR) or XORed (XOR) in, the image read into registers, counted and emitted as the
+// register path's Array emission does.
+template <int OP, bool STORE>
+__device__ __forceinline__ uint32_t image_run(const uint4 (&q)[8], uint32_t ca, const uint4 (&r)[8], uint32_t cb,
+                                              uint32_t *s, uint8_t *out, int lane) {
+  stage_from_chunks(kArray, q, ca, 0, s, lane);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int c = lane + 64 * i, n = min(8, (int)cb - 8 * c);
+    if (n > 0) {
+      const uint32_t x[8] = {r[i].x & 0xFFFF, r[i].x >> 16, r[i].y & 0xFFFF, r[i].y >> 16,
+                             r[i].z & 0xFFFF, r[i].z >> 16, r[i].w & 0xFFFF, r[i].w >> 16};
+      or_chunk_values<OP == RB_XOR>(x, n, s);
+    }
+  }
+  wave_lds_sync();
+  uint64_t w[kW];
+  lds_read_words(s, w, lane);
+  wave_lds_sync();
+  const uint32_t c = wave_sum_u32(lane_card(w));
+  if (STORE && c) emit_container(kArray, w, (int)c, 0, out, s, lane);
+  return c;
+}
+
 // A task is "light" when its result is a subset of one Array operand (AND with an Array, ANDNOT
 // with an Array on the left) or when it is an unmatched copy; everything else is "heavy".
-__device__ __forceinline__ bool light_task(int op, int ta, int tb) {
+// An OR / XOR of two Arrays of <= kMergeMax values in all is light too (merge_run).  `op` is the call's
+// op (a lazy op is never light) or, in the task kernels, the kernel's op with `lazy` set.
+__device__ __forceinline__ bool merge_task(int op, int ta, int tb, uint32_t ca, uint32_t cb, bool lazy = false) {
+  return RBG_LIGHT_MERGE && (op == RB_OR || op == RB_XOR) && !lazy && ta == kArray && tb == kArray &&
+         ca + cb <= kMergeMax;
+}
+__device__ __forceinline__ bool light_task(int op, int ta, int tb, uint32_t ca, uint32_t cb, bool lazy = false) {
   if (ta < 0 || tb < 0) return true;
   if (op == RB_AND) return ta == kArray || tb == kArray;
   if (op == RB_ANDNOT) return ta == kArray;
-  return false;
+  return merge_task(op, ta, tb, ca, cb, lazy);
 }
 
 // Striped accounting (stats word w, stripe = block mod kStripes) of N counters: one atomic per block
@@ -245,7 +358,7 @@ __device__ __forceinline__ void pair_walk(const PairArgs &a, uint64_t sg, PairCo
   // one result slot from the two sides' container metadata (ta / tb < 0: no container on that side)
   auto slot_v = [&](int ta, uint32_t ca, uint32_t ra, uint64_t oa, int tb, uint32_t cb, uint32_t rb, uint64_t ob,
                     uint16_t key, bool big, uint64_t bytes) {
-    const bool lt = light_task(a.op, ta, tb);
+    const bool lt = light_task(a.op, ta, tb, ca, cb);
     if (!EMIT) {
       uint64_t b = 0;
       if (ta >= 0) b += alg_bytes(ta, ca, ra) + 16;
@@ -532,7 +645,7 @@ constexpr bool kHeavyPrefetch = !RBG_HEAVY_NOPF;    // the next task's payloads 
 #ifndef RBG_STUDY
 #define RBG_STUDY 0 // study builds: per-phase s_memtime totals of a few light / heavy waves (printf)
 #endif
-enum { kCopy = 0, kFilter = 1, kHeavy = 2 };
+enum { kCopy = 0, kFilter = 1, kHeavy = 2, kMerge = 3 };
 struct Task {
   int kind;
   bool bigp, bigq;       // payload exceeds 8 KiB (Run with > 2047 runs): direct path from global
@@ -542,14 +655,14 @@ struct Task {
   uint32_t cp, cq, rp, rq;
 };
 template <int OP>
-__device__ __forceinline__ Task decode_task(const RecU &r, const uint8_t *pay_a, const uint8_t *pay_b) {
+__device__ __forceinline__ Task decode_task(const RecU &r, const uint8_t *pay_a, const uint8_t *pay_b, bool lazy) {
   Task T;
   const uint32_t ta = desc_type(r.da), tb = desc_type(r.db);
   const uint32_t ca = desc_card(r.da), cb = desc_card(r.db);
-  const bool p_is_a = ta != kAbsent && !(light_task(OP, (int)ta, (int)tb) && tb == kArray &&
-                                         (ta != kArray || (OP != RB_ANDNOT && cb < ca)));
+  const bool lt = light_task(OP, (int)ta, (int)tb, ca, cb, lazy);
+  const bool p_is_a = ta != kAbsent && !(lt && tb == kArray && (ta != kArray || (OP != RB_ANDNOT && cb < ca)));
   if (ta == kAbsent || tb == kAbsent) T.kind = kCopy;
-  else T.kind = light_task(OP, (int)ta, (int)tb) ? kFilter : kHeavy;
+  else T.kind = !lt ? kHeavy : merge_task(OP, (int)ta, (int)tb, ca, cb, lazy) ? kMerge : kFilter;
   // kFilter: F is the Array (ANDNOT: always A; AND of two Arrays: the smaller, A on ties)
   T.pp = p_is_a ? pay_a + r.pa : pay_b + r.pb;
   T.pq = p_is_a ? pay_b + r.pb : pay_a + r.pa;
@@ -790,7 +903,7 @@ __global__ __launch_bounds__(256, ROLE == kRoleHeavy ? kHeavyWaves : kLightWaves
   uint32_t *s = lds[wv];
   uint16_t *ob = stage[ROLE == kRoleLight ? wv : 0];
   RecU cur = load_rec(recs + g);
-  Task tc = decode_task<OP>(cur, pay_a, pay_b);
+  Task tc = decode_task<OP>(cur, pay_a, pay_b, tm.lazy != 0);
   uint4 pq[8], qq[8];
 #if RBG_STUDY
   uint64_t lt_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, lt0 = 0, lt1 = 0, lt2 = 0; // decode, stage B/A/R, copy, filter, iteration, tasks
@@ -819,7 +932,7 @@ __global__ __launch_bounds__(256, ROLE == kRoleHeavy ? kHeavyWaves : kLightWaves
     RBG_LT(lt0 = __builtin_amdgcn_s_memtime());
     RBG_HT(lt0 = __builtin_amdgcn_s_memtime());
     const RecU nx = load_rec(recs + (has_next ? gn : g));
-    const Task tn = decode_task<OP>(nx, pay_a, pay_b);
+    const Task tn = decode_task<OP>(nx, pay_a, pay_b, tm.lazy != 0);
     RBG_LT(lt1 = __builtin_amdgcn_s_memtime(); lt_acc[0] += lt1 - lt0);
     RBG_HT(lt1 = __builtin_amdgcn_s_memtime(); lt_acc[0] += lt1 - lt0);
     int ty = kEmpty, c = 0;
@@ -942,6 +1055,9 @@ __global__ __launch_bounds__(256, ROLE == kRoleHeavy ? kHeavyWaves : kLightWaves
       if (tc.kind == kFilter) {
         if (tc.bigq) stage_big_runs(tc.pq, tc.rq, s, lane); // only a Run payload exceeds 8 KiB
         else stage_from_chunks(tc.tq, qq, tc.cq, tc.rq, s, lane);
+      } else if (tc.kind == kMerge) {
+        if (RBG_LIGHT_MERGE == 2) c = (int)image_run<OP, !CARD_ONLY>(pq, tc.cp, qq, tc.cq, s, dst, lane);
+        else merge_stage(pq, tc.cp, qq, tc.cq, s, lane);
       } else if (!CARD_ONLY) {
         if (tc.bigp) copy_payload(tc.pp, dst, tc.pbytes, lane);
         else store_chunks(pq, dst, tc.pbytes, lane);
@@ -961,6 +1077,9 @@ __global__ __launch_bounds__(256, ROLE == kRoleHeavy ? kHeavyWaves : kLightWaves
         c = OP == RB_ANDNOT ? filter_rows_linear<true, !CARD_ONLY>(pq, (int)tc.cp, s, ob, tb, o, lane)
                             : filter_rows_linear<false, !CARD_ONLY>(pq, (int)tc.cp, s, ob, tb, o, lane);
         ty = c ? kArray : kEmpty;
+      } else if (tc.kind == kMerge) {
+        if (RBG_LIGHT_MERGE != 2) c = (int)merge_run<OP, !CARD_ONLY>(s, tc.cp, tc.cq, reinterpret_cast<uint16_t *>(dst), lane);
+        ty = c || (OP == RB_XOR && tm.keep_empty && !CARD_ONLY) ? (int)kArray : (int)kEmpty;
       } else {
         ty = tc.tp;
         c = (int)tc.cp;
@@ -1020,7 +1139,7 @@ __global__ __launch_bounds__(256, 4) void k_probe_tasks(const uint8_t *__restric
   uint64_t g = (uint64_t)blockIdx.x * 4 + wv;
   if (g >= n) return;
   RecU cur = load_rec(recs + g);
-  Task tc = decode_task<OP>(cur, pay_a, pay_b);
+  Task tc = decode_task<OP>(cur, pay_a, pay_b, false);
   uint4 pq[8], qq[8];
   load_chunks(pq, tc.pp, tc.bigp ? 16u : tc.pbytes, lane);
   if (tc.kind == kCopy || tc.bigq) load_chunks(qq, tc.pp, 16, lane);
@@ -1030,7 +1149,7 @@ __global__ __launch_bounds__(256, 4) void k_probe_tasks(const uint8_t *__restric
     const uint64_t gn = g + stride;
     const bool has_next = gn < n;
     const RecU nx = load_rec(recs + (has_next ? gn : g));
-    const Task tn = decode_task<OP>(nx, pay_a, pay_b);
+    const Task tn = decode_task<OP>(nx, pay_a, pay_b, false);
     acc ^= fold_chunks(qq);
     {
       const bool real = has_next && tn.kind != kCopy && !tn.bigq;
@@ -1526,7 +1645,21 @@ __global__ __launch_bounds__(256, kSmallWaves) void k_pair_small(SmallPairArgs a
     uint8_t *dst = a.arena + slot * kBitmapBytes;
     int ty = kEmpty, c = 0, nr = 0;
     uint32_t cw = 0xFFFFFFFFu; // the card word to store when it is not c (priorityqueue_or's lazy marks)
-    if (has_a && has_b && !ident) {
+    if (RBG_SMALL_MERGE && has_a && has_b && !ident && a.A.type[i0 + ia] == kArray &&
+        a.B.type[j0 + ib] == kArray && !(OP == RB_OR && a.lazy) && a.A.card[i0 + ia] + a.B.card[j0 + ib] <= kMergeMax) {
+      // two Arrays: the merge (merge_run), an Array result
+      const uint64_t xa = i0 + ia, xb = j0 + ib;
+      const uint32_t ca = a.A.card[xa], cb = a.B.card[xb];
+      if (lane == 0) inb += alg_bytes(kArray, ca, 0) + alg_bytes(kArray, cb, 0) + 32;
+      {
+        uint4 q[8], r[8];
+        load_chunks(q, a.A.payload + a.A.off[xa], 2u * ca, lane);
+        load_chunks(r, a.B.payload + a.B.off[xb], 2u * cb, lane);
+        merge_stage(q, ca, r, cb, s, lane);
+      }
+      c = (int)merge_run<OP, !CARD_ONLY>(s, ca, cb, reinterpret_cast<uint16_t *>(dst), lane);
+      ty = c || (OP == RB_XOR && a.keep_empty && !CARD_ONLY) ? (int)kArray : (int)kEmpty;
+    } else if (has_a && has_b && !ident) {
       const uint64_t xa = i0 + ia, xb = j0 + ib;
       const int ta = a.A.type[xa], tb = a.B.type[xb];
       const uint32_t ca = a.A.card[xa], cb = a.B.card[xb], ra = a.A.nruns[xa], rb = a.B.nruns[xb];

@@ -72,6 +72,61 @@ def test_two_sets_and_identity_pairs(ctx, oracle):
         assert got == [oracle.op(op, ra[i], rbs[i]).serialize() for i in range(50)]
 
 
+def _array_pair_bitmaps(rng):
+    """Bitmaps of Array containers only, sized around the small-batch merge path's bounds (ca + cb <= 4088
+    takes the merge, above it the register path): equal, disjoint, interleaved, nested and random arrays
+    on shared keys, so ties fall on and off the merge's 64 lane boundaries."""
+    def arr(key, lows):
+        return (np.uint32(key) << np.uint32(16)) | np.asarray(sorted(set(int(x) for x in lows)), np.uint32)
+
+    def rnd(n, lo=0, hi=65536):
+        return rng.choice(np.arange(lo, hi), size=n, replace=False)
+
+    base = rnd(4000)
+    sizes = [(1, 1), (1, 4000), (4000, 88), (4000, 89), (4096, 1), (2000, 2000), (3000, 1088), (63, 65), (640, 640)]
+    left, right = [], []
+    for k, (na, nb) in enumerate(sizes):
+        a = rnd(na)
+        shared = a[: min(na, nb) // 2]
+        b = np.concatenate([shared, rnd(nb)])[:nb]
+        left.append(arr(k, a))
+        right.append(arr(k, b))
+    # equal arrays (XOR empty, AND = A), disjoint evens / odds, nested (B inside A), one value apart
+    left.append(arr(20, base[:1500]))
+    right.append(arr(20, base[:1500]))
+    left.append(arr(21, np.arange(0, 4000, 2)))
+    right.append(arr(21, np.arange(1, 4000, 2)))
+    left.append(arr(22, base[:3000]))
+    right.append(arr(22, base[1000:1500]))
+    left.append(arr(23, np.arange(100, 2100)))
+    right.append(arr(23, np.arange(101, 2101)))
+    a_bms, b_bms = [], []
+    for i in range(len(left)):  # one bitmap per case, and one holding every case's key
+        a_bms.append(left[i])
+        b_bms.append(right[i])
+    a_bms.append(np.concatenate(left))
+    b_bms.append(np.concatenate(right))
+    return a_bms, b_bms
+
+
+def test_array_pairs_merge_path(ctx, oracle):
+    """Array x Array keys of the small-batch kernel (merge path) against the oracle, bytes and
+    cardinalities, for all four ops and both operand orders."""
+    rng = np.random.default_rng(77)
+    a_bms, b_bms = _array_pair_bitmaps(rng)
+    a = ctx.upload_values(a_bms, run_optimize=False)
+    b = ctx.upload_values(b_bms, run_optimize=False)
+    ra, rbs = _ref_list(oracle, a.serialize()), _ref_list(oracle, b.serialize())
+    for op in OPS.values():
+        for x, y, rx, ry in ((a, b, ra, rbs), (b, a, rbs, ra)):
+            got = ctx.pairwise(op, x, y).serialize()
+            cards = ctx.pairwise_cardinality(op, x, y)
+            for i in range(len(a_bms)):
+                ref = oracle.op(op, rx[i], ry[i])
+                assert got[i] == ref.serialize(), (op, i)
+                assert int(cards[i]) == ref.cardinality(), (op, i)
+
+
 def test_fixtures_through_the_device(ctx, oracle):
     w, wo = fixture_bytes("bitmapwithruns.bin"), fixture_bytes("bitmapwithoutruns.bin")
     s = ctx.upload_serialized([w, wo])
