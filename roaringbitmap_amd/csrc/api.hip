@@ -452,6 +452,7 @@ int set_gather(const rbgpu_set *s, const uint32_t *idx, uint32_t n, rbgpu_set **
 // waits anyway), so the next call starts its kernels without one; a call that did not reach
 // stats_end leaves them dirty and the next stats_begin zeroes them.
 void stats_begin(rbgpu_ctx *ctx, bool zero) {
+  ctx->stats_pending = false;
   if (zero && !ctx->stats_clean)
     (void)hipMemsetAsync(ctx->d_stats, 0, kStatWords * kStripes * sizeof(uint64_t), ctx->stream);
   ctx->stats_clean = false;
@@ -473,7 +474,8 @@ int stats_end(rbgpu_ctx *ctx, uint64_t tasks, uint64_t result_containers, const 
   }
   return stats_fill(ctx, tasks, result_containers, k, n);
 }
-int stats_fill(rbgpu_ctx *ctx, uint64_t tasks, uint64_t result_containers, const KernelSpan *k, int n) {
+int stats_fill(rbgpu_ctx *ctx, uint64_t tasks, uint64_t result_containers, const KernelSpan *k, int n, bool timed) {
+  ctx->stats_pending = false;
   const uint64_t *w = ctx->words;
   rb_stats &s = ctx->last;
   s = rb_stats{};
@@ -483,13 +485,13 @@ int stats_fill(rbgpu_ctx *ctx, uint64_t tasks, uint64_t result_containers, const
   s.result_cardinality = w[7];
   s.result_containers = result_containers;
   float ms = 0;
-  s.total_ms = hipEventElapsedTime(&ms, ctx->ev[0], ctx->ev[5]) == hipSuccess ? ms : 0.0;
+  s.total_ms = timed && hipEventElapsedTime(&ms, ctx->ev[0], ctx->ev[5]) == hipSuccess ? ms : 0.0;
   s.n_kernels = (uint32_t)std::min(n, 4);
   int best = -1;
   for (int i = 0; i < (int)s.n_kernels; ++i) {
     std::snprintf(s.kernel_name[i], sizeof s.kernel_name[i], "%s", k[i].name);
     hipEvent_t e0 = k[i].e0 ? k[i].e0 : ctx->ev[1 + i], e1 = k[i].e1 ? k[i].e1 : ctx->ev[2 + i];
-    s.kernel_ms[i] = hipEventElapsedTime(&ms, e0, e1) == hipSuccess ? ms : 0.0;
+    s.kernel_ms[i] = timed && hipEventElapsedTime(&ms, e0, e1) == hipSuccess ? ms : 0.0;
     s.kernel_bytes[i] = (k[i].in_word >= 0 ? w[k[i].in_word] : 0) + (k[i].out_word >= 0 ? w[k[i].out_word] : 0) +
                         (k[i].in2 >= 0 ? w[k[i].in2] : 0) + (k[i].out2 >= 0 ? w[k[i].out2] : 0);
     s.kernel_items[i] = k[i].items;
@@ -559,6 +561,16 @@ int rbgpu_synchronize(rbgpu_ctx *ctx) {
 
 int rbgpu_get_stats(rbgpu_ctx *ctx, rb_stats *out) {
   if (!ctx || !out) return fail(RB_EINVAL, "null argument");
+  if (ctx->stats_pending) { // a small batch returned before its end was signalled: its times now
+    ctx->stats_pending = false;
+    float ms = 0.f;
+    if (hipEventSynchronize(ctx->ev[5]) == hipSuccess) {
+      if (hipEventElapsedTime(&ms, ctx->ev[0], ctx->ev[5]) == hipSuccess) ctx->last.total_ms = ms;
+      if (ctx->stats_pending_k && hipEventElapsedTime(&ms, ctx->ev[1], ctx->ev[2]) == hipSuccess)
+        ctx->last.kernel_ms[0] = ctx->last.main_kernel_ms = ms;
+    }
+    (void)hipGetLastError();
+  }
   *out = ctx->last;
   return RB_OK;
 }
@@ -946,6 +958,9 @@ static uint32_t pairwise_seg_keys(const rbgpu_set *a, const rbgpu_set *b, uint64
 static inline uint64_t bm_conts(const rbgpu_set *s, uint32_t i) {
   return i == kEmptyBitmap ? 0 : s->h_begin[i + 1] - s->h_begin[i];
 }
+#ifndef RBG_SMALL_POLL
+#define RBG_SMALL_POLL 1 // study builds: 0 waits for the stream
+#endif
 static int pairwise_small(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu_set *b, const uint32_t *a_idx,
                           const uint32_t *b_idx, uint32_t np, rbgpu_set **out, uint64_t *card_out, bool inplace,
                           bool keep_empty) {
@@ -1079,6 +1094,7 @@ static int pairwise_small(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgp
   sa.rbegin = res ? res->begin : nullptr;
   if (res) sa.out = OutView{res->key, res->type, res->card, res->nruns, res->off};
   sa.hout = reinterpret_cast<uint64_t *>(ctx->d_small);
+  sa.seq = ++ctx->small_seq;
   sa.lazy = is_lazy_op(op) ? op : 0;
   sa.inplace = inplace;
   sa.keep_empty = keep_empty;
@@ -1086,8 +1102,25 @@ static int pairwise_small(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgp
   if (ktimes) HIPCHK(hipEventRecord(ctx->ev[2], st));
   if (card_out) HIPCHK(hipMemcpyAsync(card_out, sa.pcard, 8ull * np, hipMemcpyDeviceToHost, st));
   HIPCHK(hipEventRecord(ctx->ev[5], st));
+  // The last block writes the result words to host memory and then the call's sequence number: the host
+  // returns once it reads that number, without waiting for the kernel's end to be signalled (the kernel has
+  // no work left by then, and later calls on the stream are ordered behind it).  Per-pair cardinalities
+  // come back by a copy, so those calls wait for the stream; a kernel that never writes the number (a
+  // fault) is caught by the stream wait after a bounded spin.
+  bool seen = false;
+  if (RBG_SMALL_POLL && !card_out) {
+    const volatile uint64_t *flag = reinterpret_cast<const volatile uint64_t *>(ctx->h_small) + 5;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t it = 0;; ++it) {
+      if (__atomic_load_n(const_cast<const uint64_t *>(flag), __ATOMIC_ACQUIRE) == sa.seq) {
+        seen = true;
+        break;
+      }
+      if ((it & 1023u) == 1023u && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(50)) break;
+    }
+  }
   {
-    const hipError_t e1 = hipStreamSynchronize(st), e2 = hipGetLastError();
+    const hipError_t e1 = seen ? hipSuccess : hipStreamSynchronize(st), e2 = hipGetLastError();
     if (e1 != hipSuccess || e2 != hipSuccess) {
       if (res) rbgpu_set_free(res);
       return fail(RB_EDEVICE, "small-batch pairwise kernel failed: %s", hipGetErrorString(e1 != hipSuccess ? e1 : e2));
@@ -1102,7 +1135,9 @@ static int pairwise_small(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgp
   w[7] = hout[4];           // result cardinality
   const uint64_t nres = hout[0];
   const KernelSpan spans[1] = {{"k_pair_small", 6, 1, E}};
-  rc = stats_fill(ctx, E, nres, spans, ktimes ? 1 : 0);
+  rc = stats_fill(ctx, E, nres, spans, ktimes ? 1 : 0, !seen);
+  ctx->stats_pending = seen;
+  ctx->stats_pending_k = seen && ktimes;
   if (rc) {
     if (res) rbgpu_set_free(res);
     return rc;

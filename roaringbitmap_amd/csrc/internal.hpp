@@ -156,6 +156,9 @@ struct rbgpu_ctx {
   // pairwise call's arguments and result words, so that call needs no copy engine
   uint8_t *h_small = nullptr, *d_small = nullptr; // small-batch result words (host-visible, 64 B)
   uint64_t *d_small_ctr = nullptr;                  // small-batch finished-block count and counters
+  uint64_t small_seq = 0;   // small-batch calls launched (the kernel's last block writes it to h_small[5])
+  bool stats_pending = false; // ctx->last's times wait for their events (a small batch returned on h_small[5])
+  bool stats_pending_k = false; // ... and the kernel's own pair (RBGPU_SMALL_KERNEL_TIMES)
   rbg::SmallTabInline small_inline{};               // small-batch tables passed in the kernel arguments
   std::vector<uint32_t> small_tab;                  // ... or copied to device memory (larger batches)
   rb_stats last{};
@@ -249,7 +252,8 @@ struct KernelSpan {
 int stats_end(rbgpu_ctx *ctx, uint64_t tasks, uint64_t result_containers, const KernelSpan *k, int n,
               const uint64_t *d_src = nullptr);
 // stats_end's second half: ctx->words already hold the call's counters and the stream is idle
-int stats_fill(rbgpu_ctx *ctx, uint64_t tasks, uint64_t result_containers, const KernelSpan *k, int n);
+int stats_fill(rbgpu_ctx *ctx, uint64_t tasks, uint64_t result_containers, const KernelSpan *k, int n,
+               bool timed = true);
 // wide.hip
 // keys outside [key_lo, key_hi) produce no result containers (key-range shard of the aggregation)
 int wide_run(rbgpu_ctx *ctx, int sem, const rbgpu_set *in, const std::vector<uint32_t> &members, uint32_t key_lo,

@@ -153,7 +153,8 @@ struct SmallPairArgs {
   // words: [0] result containers, [1..4] the summed counters
   uint32_t E, nblocks;
   uint32_t *xpos;
-  uint64_t *rbegin, *hout;
+  uint64_t *rbegin, *hout; // hout: host-visible result words [0..4], and [5] = seq once they are written
+  uint64_t seq;
   OutView out;
 };
 // blocks of one pair of nk = na + nb keys: up to kpw merged keys per wave, 4 waves per block, at most `cap`

@@ -94,12 +94,9 @@ __device__ __forceinline__ WalkMeta pick_meta(const WalkMeta (&m)[kWalkRegs], ui
 // A[i], B[j] next to each other, wherever the lanes' ranges split), once to count the values it keeps
 // and once, after a wave scan of the counts, to store them.  With ca + cb <= kMergeMax the result is an
 // Array (ArrayContainer.or / xor merge below DEFAULT_MAX_SIZE; and / andNot are subsets of A), the type
-// the register path gives these pairs; OR and XOR are symmetric, so either operand may be A.
+// the register path gives these pairs.  Used by the small-batch kernel (k_pair_small).
 #ifndef RBG_SMALL_MERGE
 #define RBG_SMALL_MERGE 1 // study builds: 0 sends small-batch Array pairs through the register path
-#endif
-#ifndef RBG_LIGHT_MERGE
-#define RBG_LIGHT_MERGE 1 // study builds: 0 leaves OR / XOR Array pairs to the heavy (register path) kernel
 #endif
 constexpr uint32_t kMergeMax = 4088; // ca + cb: A at 0, B 16-B aligned after it, both in 8 KiB
 template <int OP>
@@ -169,44 +166,17 @@ __device__ __forceinline__ uint32_t merge_run(const uint32_t *s, uint32_t ca, ui
   return tot;
 }
 
-// The same pairs through an LDS image instead (study: RBG_LIGHT_MERGE=2): A's values ORed into a zeroed
-// 8 KiB image, B's ORed (OR) or XORed (XOR) in, the image read into registers, counted and emitted as the
-// register path's Array emission does.
-template <int OP, bool STORE>
-__device__ __forceinline__ uint32_t image_run(const uint4 (&q)[8], uint32_t ca, const uint4 (&r)[8], uint32_t cb,
-                                              uint32_t *s, uint8_t *out, int lane) {
-  stage_from_chunks(kArray, q, ca, 0, s, lane);
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int c = lane + 64 * i, n = min(8, (int)cb - 8 * c);
-    if (n > 0) {
-      const uint32_t x[8] = {r[i].x & 0xFFFF, r[i].x >> 16, r[i].y & 0xFFFF, r[i].y >> 16,
-                             r[i].z & 0xFFFF, r[i].z >> 16, r[i].w & 0xFFFF, r[i].w >> 16};
-      or_chunk_values<OP == RB_XOR>(x, n, s);
-    }
-  }
-  wave_lds_sync();
-  uint64_t w[kW];
-  lds_read_words(s, w, lane);
-  wave_lds_sync();
-  const uint32_t c = wave_sum_u32(lane_card(w));
-  if (STORE && c) emit_container(kArray, w, (int)c, 0, out, s, lane);
-  return c;
-}
-
 // A task is "light" when its result is a subset of one Array operand (AND with an Array, ANDNOT
 // with an Array on the left) or when it is an unmatched copy; everything else is "heavy".
-// An OR / XOR of two Arrays of <= kMergeMax values in all is light too (merge_run).  `op` is the call's
-// op (a lazy op is never light) or, in the task kernels, the kernel's op with `lazy` set.
-__device__ __forceinline__ bool merge_task(int op, int ta, int tb, uint32_t ca, uint32_t cb, bool lazy = false) {
-  return RBG_LIGHT_MERGE && (op == RB_OR || op == RB_XOR) && !lazy && ta == kArray && tb == kArray &&
-         ca + cb <= kMergeMax;
-}
-__device__ __forceinline__ bool light_task(int op, int ta, int tb, uint32_t ca, uint32_t cb, bool lazy = false) {
+// (OR / XOR of two Arrays through merge_run in the light (copy + filter) kernel instead of the heavy
+// register path measured slower:
+// config 2 OR 12.84 -> 14.09 ms, XOR 10.59 -> 12.85 — the light kernel, already the L2-bound one, became
+// the long pole; an LDS-image form of the same tasks 15.8 / 14.2 ms.  profiles/r05/merge.)
+__device__ __forceinline__ bool light_task(int op, int ta, int tb) {
   if (ta < 0 || tb < 0) return true;
   if (op == RB_AND) return ta == kArray || tb == kArray;
   if (op == RB_ANDNOT) return ta == kArray;
-  return merge_task(op, ta, tb, ca, cb, lazy);
+  return false;
 }
 
 // Striped accounting (stats word w, stripe = block mod kStripes) of N counters: one atomic per block
@@ -358,7 +328,7 @@ __device__ __forceinline__ void pair_walk(const PairArgs &a, uint64_t sg, PairCo
   // one result slot from the two sides' container metadata (ta / tb < 0: no container on that side)
   auto slot_v = [&](int ta, uint32_t ca, uint32_t ra, uint64_t oa, int tb, uint32_t cb, uint32_t rb, uint64_t ob,
                     uint16_t key, bool big, uint64_t bytes) {
-    const bool lt = light_task(a.op, ta, tb, ca, cb);
+    const bool lt = light_task(a.op, ta, tb);
     if (!EMIT) {
       uint64_t b = 0;
       if (ta >= 0) b += alg_bytes(ta, ca, ra) + 16;
@@ -645,7 +615,7 @@ constexpr bool kHeavyPrefetch = !RBG_HEAVY_NOPF;    // the next task's payloads 
 #ifndef RBG_STUDY
 #define RBG_STUDY 0 // study builds: per-phase s_memtime totals of a few light / heavy waves (printf)
 #endif
-enum { kCopy = 0, kFilter = 1, kHeavy = 2, kMerge = 3 };
+enum { kCopy = 0, kFilter = 1, kHeavy = 2 };
 struct Task {
   int kind;
   bool bigp, bigq;       // payload exceeds 8 KiB (Run with > 2047 runs): direct path from global
@@ -655,14 +625,14 @@ struct Task {
   uint32_t cp, cq, rp, rq;
 };
 template <int OP>
-__device__ __forceinline__ Task decode_task(const RecU &r, const uint8_t *pay_a, const uint8_t *pay_b, bool lazy) {
+__device__ __forceinline__ Task decode_task(const RecU &r, const uint8_t *pay_a, const uint8_t *pay_b) {
   Task T;
   const uint32_t ta = desc_type(r.da), tb = desc_type(r.db);
   const uint32_t ca = desc_card(r.da), cb = desc_card(r.db);
-  const bool lt = light_task(OP, (int)ta, (int)tb, ca, cb, lazy);
-  const bool p_is_a = ta != kAbsent && !(lt && tb == kArray && (ta != kArray || (OP != RB_ANDNOT && cb < ca)));
+  const bool p_is_a = ta != kAbsent && !(light_task(OP, (int)ta, (int)tb) && tb == kArray &&
+                                         (ta != kArray || (OP != RB_ANDNOT && cb < ca)));
   if (ta == kAbsent || tb == kAbsent) T.kind = kCopy;
-  else T.kind = !lt ? kHeavy : merge_task(OP, (int)ta, (int)tb, ca, cb, lazy) ? kMerge : kFilter;
+  else T.kind = light_task(OP, (int)ta, (int)tb) ? kFilter : kHeavy;
   // kFilter: F is the Array (ANDNOT: always A; AND of two Arrays: the smaller, A on ties)
   T.pp = p_is_a ? pay_a + r.pa : pay_b + r.pb;
   T.pq = p_is_a ? pay_b + r.pb : pay_a + r.pa;
@@ -903,7 +873,7 @@ __global__ __launch_bounds__(256, ROLE == kRoleHeavy ? kHeavyWaves : kLightWaves
   uint32_t *s = lds[wv];
   uint16_t *ob = stage[ROLE == kRoleLight ? wv : 0];
   RecU cur = load_rec(recs + g);
-  Task tc = decode_task<OP>(cur, pay_a, pay_b, tm.lazy != 0);
+  Task tc = decode_task<OP>(cur, pay_a, pay_b);
   uint4 pq[8], qq[8];
 #if RBG_STUDY
   uint64_t lt_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, lt0 = 0, lt1 = 0, lt2 = 0; // decode, stage B/A/R, copy, filter, iteration, tasks
@@ -932,7 +902,7 @@ __global__ __launch_bounds__(256, ROLE == kRoleHeavy ? kHeavyWaves : kLightWaves
     RBG_LT(lt0 = __builtin_amdgcn_s_memtime());
     RBG_HT(lt0 = __builtin_amdgcn_s_memtime());
     const RecU nx = load_rec(recs + (has_next ? gn : g));
-    const Task tn = decode_task<OP>(nx, pay_a, pay_b, tm.lazy != 0);
+    const Task tn = decode_task<OP>(nx, pay_a, pay_b);
     RBG_LT(lt1 = __builtin_amdgcn_s_memtime(); lt_acc[0] += lt1 - lt0);
     RBG_HT(lt1 = __builtin_amdgcn_s_memtime(); lt_acc[0] += lt1 - lt0);
     int ty = kEmpty, c = 0;
@@ -1055,9 +1025,6 @@ __global__ __launch_bounds__(256, ROLE == kRoleHeavy ? kHeavyWaves : kLightWaves
       if (tc.kind == kFilter) {
         if (tc.bigq) stage_big_runs(tc.pq, tc.rq, s, lane); // only a Run payload exceeds 8 KiB
         else stage_from_chunks(tc.tq, qq, tc.cq, tc.rq, s, lane);
-      } else if (tc.kind == kMerge) {
-        if (RBG_LIGHT_MERGE == 2) c = (int)image_run<OP, !CARD_ONLY>(pq, tc.cp, qq, tc.cq, s, dst, lane);
-        else merge_stage(pq, tc.cp, qq, tc.cq, s, lane);
       } else if (!CARD_ONLY) {
         if (tc.bigp) copy_payload(tc.pp, dst, tc.pbytes, lane);
         else store_chunks(pq, dst, tc.pbytes, lane);
@@ -1077,9 +1044,6 @@ __global__ __launch_bounds__(256, ROLE == kRoleHeavy ? kHeavyWaves : kLightWaves
         c = OP == RB_ANDNOT ? filter_rows_linear<true, !CARD_ONLY>(pq, (int)tc.cp, s, ob, tb, o, lane)
                             : filter_rows_linear<false, !CARD_ONLY>(pq, (int)tc.cp, s, ob, tb, o, lane);
         ty = c ? kArray : kEmpty;
-      } else if (tc.kind == kMerge) {
-        if (RBG_LIGHT_MERGE != 2) c = (int)merge_run<OP, !CARD_ONLY>(s, tc.cp, tc.cq, reinterpret_cast<uint16_t *>(dst), lane);
-        ty = c || (OP == RB_XOR && tm.keep_empty && !CARD_ONLY) ? (int)kArray : (int)kEmpty;
       } else {
         ty = tc.tp;
         c = (int)tc.cp;
@@ -1139,7 +1103,7 @@ __global__ __launch_bounds__(256, 4) void k_probe_tasks(const uint8_t *__restric
   uint64_t g = (uint64_t)blockIdx.x * 4 + wv;
   if (g >= n) return;
   RecU cur = load_rec(recs + g);
-  Task tc = decode_task<OP>(cur, pay_a, pay_b, false);
+  Task tc = decode_task<OP>(cur, pay_a, pay_b);
   uint4 pq[8], qq[8];
   load_chunks(pq, tc.pp, tc.bigp ? 16u : tc.pbytes, lane);
   if (tc.kind == kCopy || tc.bigq) load_chunks(qq, tc.pp, 16, lane);
@@ -1149,7 +1113,7 @@ __global__ __launch_bounds__(256, 4) void k_probe_tasks(const uint8_t *__restric
     const uint64_t gn = g + stride;
     const bool has_next = gn < n;
     const RecU nx = load_rec(recs + (has_next ? gn : g));
-    const Task tn = decode_task<OP>(nx, pay_a, pay_b, false);
+    const Task tn = decode_task<OP>(nx, pay_a, pay_b);
     acc ^= fold_chunks(qq);
     {
       const bool real = has_next && tn.kind != kCopy && !tn.bigq;
@@ -1538,13 +1502,21 @@ __device__ void small_compact(const SmallPairArgs &a, const Tab &tab, uint32_t *
       }
       a.pcard[p] = c;
     }
+  // the result words to host memory by one thread, then the call's sequence number with a system-scope
+  // release: the host may return as soon as it reads that number (pairwise_small), before the kernel's
+  // end is signalled
+  uint64_t *vs = reinterpret_cast<uint64_t *>(wtot);
+  __syncthreads(); // wtot's last readers (the scans) are done
   if (threadIdx.x < 4) {
-    a.hout[1 + threadIdx.x] = v;
+    vs[threadIdx.x] = v;
     __hip_atomic_store(a.ctr + 8 + 8 * threadIdx.x, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
+  __syncthreads();
   if (threadIdx.x == 0) {
-    a.hout[0] = base;
     __hip_atomic_store(a.ctr, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); // ready for the next call
+    for (int k = 0; k < 4; ++k) a.hout[1 + k] = vs[k];
+    a.hout[0] = base;
+    __hip_atomic_store(a.hout + 5, a.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
 

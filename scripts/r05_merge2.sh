@@ -11,3 +11,10 @@ RBGPU_LIB=abvar/img/librbgpu.so timeout -k 10 300 python -u -m pytest tests/test
 tail -1 $O/tests_img.txt
 bash scripts/r05_ab_ops.sh main nolm img || exit 1
 bash scripts/r05_stamps.sh stamps stamps_nm || exit 1
+for round in 1 2; do
+  for v in main nopoll; do
+    lib=abvar/$v/librbgpu.so; [ "$v" = main ] && lib=roaringbitmap_amd/librbgpu.so
+    RBGPU_LIB=$lib timeout -k 10 120 python scripts/census_lat.py --calls 300 > $O/census_$v$round.json || exit 1
+    echo "census $v $round $(cat $O/census_$v$round.json)"
+  done
+done
