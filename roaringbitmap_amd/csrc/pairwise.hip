@@ -106,30 +106,35 @@ __device__ __forceinline__ bool merge_keep(bool from_a, bool matched) {
   if (OP == RB_OR) return from_a || !matched;
   return !matched; // XOR
 }
-template <int OP, bool STORE>
-__device__ __forceinline__ uint32_t merge_walk(const uint16_t *A, uint32_t ca, const uint16_t *B, uint32_t cb,
-                                               uint32_t i, uint32_t j, uint32_t steps, uint16_t *out) {
+// One lane's walk, branch-free (a divergent if / else ran both arms and paid two LDS latencies per
+// step): one LDS read per step, the next value of the side just taken.  A and B are one u16 array in LDS
+// (B at boff).  Kept values go to out[0..) (STORE), or with STAGE to the lane's own LDS range stage[0..)
+// — a single walk, copied out afterwards.  (Holding each side's next value one step ahead gained nothing:
+// the compiler waits for the read at the top of the next step either way.)
+template <int OP, bool STORE, bool STAGE>
+__device__ __forceinline__ uint32_t merge_walk(uint16_t *S, uint32_t ca, uint32_t boff, uint32_t cb, uint32_t i,
+                                               uint32_t j, uint32_t steps, uint16_t *out, uint16_t *stage) {
   constexpr uint32_t kEnd = 0x10000u; // past every u16 value
-  uint32_t av = i < ca ? A[i] : kEnd, bv = j < cb ? B[j] : kEnd;
-  uint32_t prev_a = i ? A[i - 1] : kEnd + 1; // the last A value before this position
+  auto rd = [&](bool valid, uint32_t idx) { // the read unconditional (clamped), the value selected
+    const uint32_t x = S[min(idx, 4095u)];
+    return valid ? x : kEnd;
+  };
+  uint32_t av = rd(i < ca, i), bv = rd(j < cb, boff + j);
+  uint32_t prev_a = i ? S[i - 1] : kEnd + 1; // the last A value before this position
   uint32_t cnt = 0;
   for (uint32_t d = 0; d < steps; ++d) {
-    if (av <= bv) { // A's value (both kEnd is impossible: the walk stays below ca + cb)
-      if (merge_keep<OP>(true, av == bv)) {
-        if (STORE) out[cnt] = (uint16_t)av;
-        ++cnt;
-      }
-      prev_a = av;
-      ++i;
-      av = i < ca ? A[i] : kEnd;
-    } else {
-      if (merge_keep<OP>(false, prev_a == bv)) {
-        if (STORE) out[cnt] = (uint16_t)bv;
-        ++cnt;
-      }
-      ++j;
-      bv = j < cb ? B[j] : kEnd;
-    }
+    const bool ta = av <= bv; // A's value (both kEnd is impossible: the walk stays below ca + cb)
+    const uint32_t v = ta ? av : bv;
+    const bool keep = merge_keep<OP>(ta, ta ? av == bv : prev_a == bv);
+    if (STAGE && keep) stage[cnt] = (uint16_t)v;
+    else if (STORE && keep) out[cnt] = (uint16_t)v;
+    cnt += keep;
+    prev_a = ta ? av : prev_a;
+    i += ta;
+    j += !ta;
+    const uint32_t nx = rd(ta ? i < ca : j < cb, ta ? i : boff + j);
+    av = ta ? nx : av;
+    bv = ta ? bv : nx;
   }
   return cnt;
 }
@@ -148,9 +153,10 @@ __device__ __forceinline__ void merge_stage(const uint4 (&q)[8], uint32_t ca, co
   wave_lds_sync();
 }
 template <int OP, bool STORE>
-__device__ __forceinline__ uint32_t merge_run(const uint32_t *s, uint32_t ca, uint32_t cb, uint16_t *out, int lane) {
-  const uint16_t *A = reinterpret_cast<const uint16_t *>(s), *B = A + merge_boff(ca);
-  const uint32_t n = ca + cb;
+__device__ __forceinline__ uint32_t merge_run(uint32_t *s, uint32_t ca, uint32_t cb, uint16_t *out, int lane) {
+  uint16_t *A = reinterpret_cast<uint16_t *>(s);
+  const uint32_t boff = merge_boff(ca), n = ca + cb;
+  const uint16_t *B = A + boff;
   const uint32_t d0 = ((uint32_t)lane * n) >> 6, d1 = ((uint32_t)(lane + 1) * n) >> 6;
   // merge path: the number of A values among the first d0 merged values (A first on ties)
   uint32_t lo = d0 > cb ? d0 - cb : 0u, hi = min(d0, ca);
@@ -159,9 +165,27 @@ __device__ __forceinline__ uint32_t merge_run(const uint32_t *s, uint32_t ca, ui
     if (A[mid] <= B[d0 - mid - 1]) lo = mid + 1;
     else hi = mid;
   }
-  const uint32_t cnt = merge_walk<OP, false>(A, ca, B, cb, lo, d0 - lo, d1 - d0, nullptr);
+  // one walk into a per-lane LDS stage (lane l's at sbase + d0, its merged range) when it fits beside A
+  // and B, else a counting walk and a storing walk
+  const uint32_t sbase = (boff + cb + 7u) & ~7u;
+  const bool staged = STORE && sbase + n <= 4096u; // wave-uniform
+  uint32_t cnt;
+  if (staged) cnt = merge_walk<OP, false, true>(A, ca, boff, cb, lo, d0 - lo, d1 - d0, nullptr, A + sbase + d0);
+  else cnt = merge_walk<OP, false, false>(A, ca, boff, cb, lo, d0 - lo, d1 - d0, nullptr, nullptr);
   const uint32_t incl = wave_scan_u32(cnt, lane), tot = readlane(incl, 63);
-  if (STORE && tot) merge_walk<OP, true>(A, ca, B, cb, lo, d0 - lo, d1 - d0, out + (incl - cnt));
+  if (STORE && tot) { // out: a 16-B aligned slot
+    uint16_t *o = out + (incl - cnt);
+    if (staged) { // compacted in LDS over A (every lane is past its walk), then whole 16-B stores
+      const uint16_t *st = A + sbase + d0;
+      for (uint32_t k = 0; k < cnt; ++k) A[incl - cnt + k] = st[k];
+      wave_lds_sync();
+      const uint4 *a4 = reinterpret_cast<const uint4 *>(A);
+      uint4 *o4 = reinterpret_cast<uint4 *>(out);
+      for (uint32_t c = (uint32_t)lane; 16u * c < 2u * tot; c += 64u) o4[c] = a4[c];
+    } else {
+      merge_walk<OP, true, false>(A, ca, boff, cb, lo, d0 - lo, d1 - d0, o, nullptr);
+    }
+  }
   wave_lds_sync(); // the next task restages the scratch
   return tot;
 }
@@ -1456,8 +1480,10 @@ __device__ void small_compact(const SmallPairArgs &a, const Tab &tab, uint32_t *
   const uint32_t nt = blockDim.x, E = a.E;
   uint32_t *xpos = E <= kSmallXposLds ? xl : a.xpos;
   const OutView &out = a.out;
-  // the summed counters (the blocks' atomics) and the first tile of slot words: independent loads first
+  // the summed counters (the blocks' atomics), the result CSR's first slot table entry and the first tile
+  // of slot words: independent loads first
   uint64_t v = threadIdx.x < 4 ? ld_sc1(a.ctr + 8 + 8 * threadIdx.x) : 0;
+  const uint32_t slot_own = a.rbegin && threadIdx.x <= a.np ? tab.slot_at(threadIdx.x) : 0u;
   constexpr int kPer = 16; // slot words per thread and tile
   uint32_t base = 0;       // results of the tiles before
   for (uint32_t t0 = 0; t0 < E; t0 += kPer * nt) {
@@ -1490,7 +1516,7 @@ __device__ void small_compact(const SmallPairArgs &a, const Tab &tab, uint32_t *
   __syncthreads();
   if (a.rbegin)
     for (uint32_t p = threadIdx.x; p <= a.np; p += nt) {
-      const uint32_t t = tab.slot_at(p);
+      const uint32_t t = p == threadIdx.x ? slot_own : tab.slot_at(p);
       a.rbegin[p] = t < E ? xpos[t] : base;
     }
   if (a.pcard) // per-pair result cardinality (RoaringBitmap.andCardinality etc.)

@@ -7,7 +7,7 @@ mkdir -p $O
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 for v in "$@"; do
   RBGPU_LIB=abvar/$v/librbgpu.so RBGPU_SMALL_STAMPS=1 timeout -k 10 120 python scripts/census_lat.py --calls 3 > $O/$v.json 2> $O/$v.err || { tail $O/$v.err; exit 1; }
-  echo "== $v"; grep stamps $O/$v.err | tail -8
+  echo "== $v"; grep -A4 "stamps blocks" $O/$v.err | tail -10
 done
 for v in "$@"; do
   RBGPU_LIB=abvar/$v/librbgpu.so timeout -k 10 120 python scripts/census_lat.py --calls 200 > $O/$v.lat.json || exit 1
