@@ -587,10 +587,20 @@ int bsi_compare(rbgpu_ctx *ctx, const rbgpu_set *bsi, int op, uint64_t start, ui
     scan_blocks_multi(in1, out1, 1, 256, nullptr, st);
     k_bsi_list<<<256, 256, 0, st>>>(frow, key_lo, key_hi, d_pos, d_klist);
   }
-  HIPCHK(hipMemcpyAsync(ctx->h_pinned, d_pos + 256, 8, hipMemcpyDeviceToHost, st));
-  HIPCHK(hipStreamSynchronize(st));
-  LAUNCHCHK();
-  const uint32_t nk = (uint32_t)ctx->h_pinned[0];
+  // the number of keys of F: over the whole key range it is F's container count, from the host copy of
+  // its CSR (no read-back, so the host runs ahead to the chain's launch); a key-range shard reads it back
+  uint32_t nk = 0;
+  const rbgpu_set *fs = found ? found : bsi;
+  const uint32_t fb = found ? 0u : nbits;
+  if (key_lo == 0 && key_hi >= 65536 && !ensure_h_begin(fs)) {
+    nk = (uint32_t)(fs->h_begin[fb + 1] - fs->h_begin[fb]);
+    LAUNCHCHK();
+  } else {
+    HIPCHK(hipMemcpyAsync(ctx->h_pinned, d_pos + 256, 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    LAUNCHCHK();
+    nk = (uint32_t)ctx->h_pinned[0];
+  }
   // result set: one 8 KiB slot per key of F, compacted at the end
   rbgpu_set *res = new rbgpu_set;
   int rc = set_alloc(ctx, res, 1, nk, (uint64_t)std::max<uint32_t>(nk, 1) * kBitmapBytes);
