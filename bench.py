@@ -574,6 +574,16 @@ def run_bsi(args, D, ctx, rb, steps=5, warmup=2):
            "roofline": roofline(last["main_kernel"], km, kb, pmc_traffic("rbg::k_bsi_range"), D, {
                "note": "the fused kernel reads every slice container once for both comparators (GE and LE); "
                        "algorithmic bytes count that one read"})}
+    # the index's key tables, built on its first compare (the warmup) and kept with the set: what a caller
+    # that builds a fresh index per query pays on top of the step
+    su = d.setup_parts()["bsi_tables"]
+    out["setup"] = {"ms": su["ms"], "bytes": su["bytes"],
+                    "what": "rbgpu_set_setup_parts[3] of this rank's index: key -> container tables of its slices "
+                            "and ebM, and ebM's key list, once per index before the warmup step, not inside the "
+                            "timed steps"}
+    with_setup = el / steps * 1e3 + D.reduce([float(su["ms"])], "max")[0]
+    out["ms_per_step_with_setup"] = round(with_setup, 4)
+    out["value_with_setup"] = round(tot_in / steps / (with_setup * 1e-3) / 1e9, 3)
     d.close()
     if not args.no_cpu_baseline and D.world == 1:
         out["cpu_baseline"] = bsi_cpu_baseline(ctx, rb)

@@ -293,8 +293,9 @@ int rbgpu_set_extract(const rbgpu_set *set, uint32_t first, uint32_t count, rbgp
 int rbgpu_set_setup_stats(const rbgpu_set *set, double *ms, uint64_t *bytes);
 /* The same split by derived item: ms[0] / bytes[0] the dense-layout check, [1] the packed member-major
  * records (workShyAnd's fast path), [2] the key-major records (naive_xor's; built from [1] when the set
- * has it, else straight from the set's metadata).  What a fresh set costs a path: [0] + the items it uses. */
-int rbgpu_set_setup_parts(const rbgpu_set *set, double ms[3], uint64_t bytes[3]);
+ * has it, else straight from the set's metadata), [3] a BitSliceIndex set's key -> container tables and
+ * ebM key list (rbgpu_bsi_compare).  What a fresh set costs a path: the items it uses. */
+int rbgpu_set_setup_parts(const rbgpu_set *set, double ms[4], uint64_t bytes[4]);
 
 /* ---- synthetic inputs for the benchmark (device-side generator, SplitMix64) ---------- */
 enum rb_workload {

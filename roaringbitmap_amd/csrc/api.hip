@@ -68,6 +68,8 @@ void set_release(rbgpu_set *s) {
   p.release(s->payload);
   p.release(s->mrec);
   p.release(s->krec);
+  p.release(s->bsi_table);
+  p.release(s->bsi_klist);
   rbgpu_ctx *ctx = s->ctx;
   s->ctx = nullptr;
   ctx_unref(ctx);
@@ -169,28 +171,6 @@ int ensure_max_runs(const rbgpu_set *cs) {
   s->max_runs = (int64_t)m;
   return RB_OK;
 }
-// Derived metadata (rbgpu_set): built once per set on the set's stream, timed with events so the cost
-// is reported (rbgpu_set_derive_ms), then cached — the set is immutable.
-namespace {
-struct DeriveTimer {
-  hipEvent_t e0 = nullptr, e1 = nullptr;
-  rbgpu_set *s;
-  int part;
-  DeriveTimer(rbgpu_set *s_, int part_) : s(s_), part(part_) {
-    if (hipEventCreate(&e0) == hipSuccess && hipEventCreate(&e1) == hipSuccess) (void)hipEventRecord(e0, s->ctx->stream);
-  }
-  ~DeriveTimer() {
-    float ms = 0.f;
-    if (e0 && e1 && hipEventRecord(e1, s->ctx->stream) == hipSuccess && hipEventSynchronize(e1) == hipSuccess &&
-        hipEventElapsedTime(&ms, e0, e1) == hipSuccess) {
-      s->derive_ms += ms;
-      s->part_ms[part] += ms;
-    }
-    if (e0) (void)hipEventDestroy(e0);
-    if (e1) (void)hipEventDestroy(e1);
-  }
-};
-} // namespace
 int ensure_dense(const rbgpu_set *cs) {
   rbgpu_set *s = const_cast<rbgpu_set *>(cs);
   if (s->dense_lo != -2) return RB_OK;
@@ -1875,7 +1855,7 @@ int rbgpu_set_setup_stats(const rbgpu_set *s, double *ms, uint64_t *bytes) {
 
 int rbgpu_set_setup_parts(const rbgpu_set *s, double *ms, uint64_t *bytes) {
   if (!s || !ms || !bytes) return fail(RB_EINVAL, "null argument");
-  for (int i = 0; i < 3; ++i) {
+  for (int i = 0; i < 4; ++i) {
     ms[i] = s->part_ms[i];
     bytes[i] = s->part_bytes[i];
   }

@@ -526,6 +526,51 @@ static int min_max_shortcut(int op, uint64_t a, uint64_t b, uint64_t mn, uint64_
   }
 }
 
+// The set's key -> container tables (rows 0..nbits: its slices and ebM; row nbits + 1: a call's foundSet)
+// and ebM's key list, built on the set's first compare and kept with it (sets are immutable): the device
+// time and bytes are the set's setup part 3 (rbgpu_set_setup_parts).
+static int ensure_bsi_tables(rbgpu_ctx *ctx, const rbgpu_set *cs, uint32_t nbits) {
+  rbgpu_set *s = const_cast<rbgpu_set *>(cs);
+  if (s->bsi_table) return RB_OK;
+  int rc = ensure_h_begin(s);
+  if (rc) return rc;
+  hipStream_t st = ctx->stream;
+  int32_t *t = nullptr;
+  uint32_t *kl = nullptr;
+  uint64_t *bt = nullptr, *bts = nullptr;
+  if (ctx->pool.alloc((void **)&t, (nbits + 2ull) * 65536 * 4) || ctx->pool.alloc((void **)&kl, 65536 * 4ull) ||
+      ctx->pool.alloc((void **)&bt, 65537 * 8ull) || ctx->pool.alloc((void **)&bts, 65537 * 8ull)) {
+    for (void *p : {(void *)t, (void *)kl, (void *)bt}) ctx->pool.release(p);
+    return fail(RB_ENOMEM, "bsi tables");
+  }
+  {
+    DeriveTimer tm(s, 3);
+    HIPCHK(hipMemsetAsync(t, 0xFF, (nbits + 1ull) * 65536 * 4, st));
+    k_bsi_index<<<dim3(64, nbits + 1), 256, 0, st>>>(s->view(), 0, t);
+    const int32_t *frow = t + (uint64_t)nbits * 65536;
+    k_bsi_active<<<256, 256, 0, st>>>(frow, 0, 65536, bt);
+    const uint64_t *in1[1] = {bt};
+    uint64_t *out1[1] = {bts};
+    scan_blocks_multi(in1, out1, 1, 256, nullptr, st);
+    k_bsi_list<<<256, 256, 0, st>>>(frow, 0, 65536, bts, kl);
+  }
+  ctx->pool.release(bt); // stream-ordered: the pool hands them only to later work on this stream
+  ctx->pool.release(bts);
+  if (hipGetLastError() != hipSuccess) {
+    ctx->pool.release(t);
+    ctx->pool.release(kl);
+    return fail(RB_EDEVICE, "bsi table kernels failed");
+  }
+  s->bsi_table = t;
+  s->bsi_klist = kl;
+  s->bsi_nk = (uint32_t)(s->h_begin[nbits + 1] - s->h_begin[nbits]);
+  // keys read, table entries written (4 B per container), ebM's key list written
+  const uint64_t b = 6ull * (s->h_begin[nbits + 1] - s->h_begin[0]) + 4ull * s->bsi_nk;
+  s->derive_bytes += b;
+  s->part_bytes[3] += b;
+  return RB_OK;
+}
+
 int bsi_compare(rbgpu_ctx *ctx, const rbgpu_set *bsi, int op, uint64_t start, uint64_t end, uint64_t vmin,
                 uint64_t vmax, const rbgpu_set *found, uint32_t key_lo, uint32_t key_hi, rbgpu_set **out) {
   const uint32_t nbits = bsi->nb - 1;
@@ -562,48 +607,56 @@ int bsi_compare(rbgpu_ctx *ctx, const rbgpu_set *bsi, int op, uint64_t start, ui
     const uint32_t ai = nbits, bi = 0;
     return rbgpu_pairwise(ctx, RB_AND, bsi, found, &ai, &bi, 1, out);
   }
-  // key -> container tables: rows 0..nbits-1 slices, nbits ebM, nbits+1 foundSet
-  const uint32_t rows = nbits + 2;
-  int32_t *d_table = nullptr;
-  uint64_t *d_active = nullptr, *d_pos = nullptr, *d_tmp = nullptr;
-  uint32_t *d_klist = nullptr;
-  const uint64_t tw = std::max<uint64_t>(scan_tmp_words(65536), 1);
-  if (ctx->pool.alloc((void **)&d_table, (uint64_t)rows * 65536 * 4) ||
-      ctx->pool.alloc((void **)&d_active, 65537 * 8ull) || ctx->pool.alloc((void **)&d_pos, 65537 * 8ull) ||
-      ctx->pool.alloc((void **)&d_tmp, tw * 8) || ctx->pool.alloc((void **)&d_klist, 65536 * 4ull))
-    return fail(RB_ENOMEM, "bsi tables");
+  // key -> container tables: rows 0..nbits-1 slices, nbits ebM (the set's, cached), nbits+1 foundSet
+  int rc = ensure_bsi_tables(ctx, bsi, nbits);
+  if (rc) return rc;
+  int32_t *d_table = bsi->bsi_table;
+  if (found) {
+    int32_t *frow = d_table + (uint64_t)(nbits + 1) * 65536;
+    HIPCHK(hipMemsetAsync(frow, 0xFF, 65536 * 4, st));
+    k_bsi_index<<<dim3(64, 1), 256, 0, st>>>(found->view(), 0, frow);
+  }
+  // F's keys: ebM's over the whole key range are the set's cached list; a foundSet's or a shard's are
+  // listed per call, and their count comes from F's host CSR over the whole range, else by a read-back
+  uint32_t nk = 0;
+  const uint32_t *d_klist = nullptr;
+  uint64_t *d_active = nullptr, *d_pos = nullptr;
+  uint32_t *d_kl = nullptr;
   auto release = [&]() {
-    for (void *p : {(void *)d_table, (void *)d_active, (void *)d_pos, (void *)d_tmp, (void *)d_klist})
-      ctx->pool.release(p);
+    for (void *p : {(void *)d_active, (void *)d_pos, (void *)d_kl}) ctx->pool.release(p);
   };
-  HIPCHK(hipMemsetAsync(d_table, 0xFF, (uint64_t)rows * 65536 * 4, st));
-  k_bsi_index<<<dim3(64, nbits + 1), 256, 0, st>>>(bsi->view(), 0, d_table);
-  if (found) k_bsi_index<<<dim3(64, 1), 256, 0, st>>>(found->view(), 0, d_table + (uint64_t)(nbits + 1) * 65536);
-  {
+  const bool full = key_lo == 0 && key_hi >= 65536;
+  if (!found && full) {
+    d_klist = bsi->bsi_klist;
+    nk = bsi->bsi_nk;
+  } else {
+    if (ctx->pool.alloc((void **)&d_active, 65537 * 8ull) || ctx->pool.alloc((void **)&d_pos, 65537 * 8ull) ||
+        ctx->pool.alloc((void **)&d_kl, 65536 * 4ull)) {
+      release();
+      return fail(RB_ENOMEM, "bsi key list");
+    }
     const int32_t *frow = d_table + (uint64_t)(found ? nbits + 1 : nbits) * 65536;
     k_bsi_active<<<256, 256, 0, st>>>(frow, key_lo, key_hi, d_active);
     const uint64_t *in1[1] = {d_active};
     uint64_t *out1[1] = {d_pos};
     scan_blocks_multi(in1, out1, 1, 256, nullptr, st);
-    k_bsi_list<<<256, 256, 0, st>>>(frow, key_lo, key_hi, d_pos, d_klist);
-  }
-  // the number of keys of F: over the whole key range it is F's container count, from the host copy of
-  // its CSR (no read-back, so the host runs ahead to the chain's launch); a key-range shard reads it back
-  uint32_t nk = 0;
-  const rbgpu_set *fs = found ? found : bsi;
-  const uint32_t fb = found ? 0u : nbits;
-  if (key_lo == 0 && key_hi >= 65536 && !ensure_h_begin(fs)) {
-    nk = (uint32_t)(fs->h_begin[fb + 1] - fs->h_begin[fb]);
-    LAUNCHCHK();
-  } else {
-    HIPCHK(hipMemcpyAsync(ctx->h_pinned, d_pos + 256, 8, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
-    LAUNCHCHK();
-    nk = (uint32_t)ctx->h_pinned[0];
+    k_bsi_list<<<256, 256, 0, st>>>(frow, key_lo, key_hi, d_pos, d_kl);
+    d_klist = d_kl;
+    const rbgpu_set *fs = found ? found : bsi;
+    const uint32_t fb = found ? 0u : nbits;
+    if (full && !ensure_h_begin(fs)) {
+      nk = (uint32_t)(fs->h_begin[fb + 1] - fs->h_begin[fb]);
+      LAUNCHCHK();
+    } else {
+      HIPCHK(hipMemcpyAsync(ctx->h_pinned, d_pos + 256, 8, hipMemcpyDeviceToHost, st));
+      HIPCHK(hipStreamSynchronize(st));
+      LAUNCHCHK();
+      nk = (uint32_t)ctx->h_pinned[0];
+    }
   }
   // result set: one 8 KiB slot per key of F, compacted at the end
   rbgpu_set *res = new rbgpu_set;
-  int rc = set_alloc(ctx, res, 1, nk, (uint64_t)std::max<uint32_t>(nk, 1) * kBitmapBytes);
+  rc = set_alloc(ctx, res, 1, nk, (uint64_t)std::max<uint32_t>(nk, 1) * kBitmapBytes);
   if (rc) {
     delete res;
     release();

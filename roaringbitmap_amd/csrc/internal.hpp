@@ -204,8 +204,14 @@ struct rbgpu_set {
   hipEvent_t read_done = nullptr;
   double derive_ms = 0.0;         // device time spent building mrec / krec (reported, not hidden)
   uint64_t derive_bytes = 0;      // their algorithmic bytes (metadata read + records written)
-  double part_ms[3] = {0, 0, 0};  // per derived item: 0 dense check, 1 mrec, 2 krec (rbgpu_set_setup_parts)
-  uint64_t part_bytes[3] = {0, 0, 0};
+  // per derived item: 0 dense check, 1 mrec, 2 krec, 3 BSI key tables (rbgpu_set_setup_parts)
+  double part_ms[4] = {0, 0, 0, 0};
+  uint64_t part_bytes[4] = {0, 0, 0, 0};
+  // BitSliceIndex compare (bsi.hip): key -> container tables of the set's bitmaps (one row each, then one
+  // scratch row for a call's foundSet) and the keys of its last bitmap (ebM), built on first use
+  int32_t *bsi_table = nullptr;
+  uint32_t *bsi_klist = nullptr;
+  uint32_t bsi_nk = 0;
   rbg::SetView view() const { return rbg::SetView{begin, key, type, card, nruns, off, payload}; }
 };
 
@@ -218,6 +224,26 @@ int pairwise_call(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu_set *b
 void ctx_unref(rbgpu_ctx *ctx);
 void set_release(rbgpu_set *s);
 int ensure_h_begin(const rbgpu_set *s);
+// Derived metadata (rbgpu_set): built once per set on the set's stream, timed with events so the cost
+// is reported (rbgpu_set_derive_ms), then cached — the set is immutable.
+struct DeriveTimer {
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  rbgpu_set *s;
+  int part;
+  DeriveTimer(rbgpu_set *s_, int part_) : s(s_), part(part_) {
+    if (hipEventCreate(&e0) == hipSuccess && hipEventCreate(&e1) == hipSuccess) (void)hipEventRecord(e0, s->ctx->stream);
+  }
+  ~DeriveTimer() {
+    float ms = 0.f;
+    if (e0 && e1 && hipEventRecord(e1, s->ctx->stream) == hipSuccess && hipEventSynchronize(e1) == hipSuccess &&
+        hipEventElapsedTime(&ms, e0, e1) == hipSuccess) {
+      s->derive_ms += ms;
+      s->part_ms[part] += ms;
+    }
+    if (e0) (void)hipEventDestroy(e0);
+    if (e1) (void)hipEventDestroy(e1);
+  }
+};
 // A set returned by rbgpu_pairwise_async is usable by the host once its work is done: every entry point
 // that reads a set first settles it (waits, fills nc).  A no-op for every other set.
 int settle(const rbgpu_set *s);

@@ -291,10 +291,12 @@ class DeviceSet:
         return {"ms": round(ms.value, 4), "bytes": int(b.value)}
 
     def setup_parts(self) -> dict:
-        """rbgpu_set_setup_parts: {item: {ms, bytes}} for the dense check, mrec and krec built so far."""
-        ms, b = (C.c_double * 3)(), np.zeros(3, np.uint64)
+        """rbgpu_set_setup_parts: {item: {ms, bytes}} for the dense check, mrec, krec and the BSI key tables
+        built so far."""
+        ms, b = (C.c_double * 4)(), np.zeros(4, np.uint64)
         L.check(L.lib().rbgpu_set_setup_parts(self.h, ms, b.ctypes.data_as(L._U64P)))
-        return {k: {"ms": round(ms[i], 4), "bytes": int(b[i])} for i, k in enumerate(("dense_check", "mrec", "krec"))}
+        return {k: {"ms": round(ms[i], 4), "bytes": int(b[i])}
+                for i, k in enumerate(("dense_check", "mrec", "krec", "bsi_tables"))}
 
     def download(self, first: int = 0, count: Optional[int] = None) -> HostSoA:
         count = len(self) - first if count is None else count

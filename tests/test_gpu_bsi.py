@@ -45,6 +45,9 @@ def test_bsi_all_ops_bytes(ctx, oracle, seed):
                         got = ctx.bsi_compare(op, d, p, end, int(mn), int(mx), f_dev).serialize()[0]
                         want = oracle.bsi_compare(rsl, rebm, op, p, end, f_ref, int(mn), int(mx)).serialize()
                         assert got == want, (name, n, nbits, ro, p, end, f_dev is not None)
+            # the index's key tables were built once and reused by every compare above (a foundSet's row
+            # rebuilt per call in their scratch row)
+            assert d.setup_parts()["bsi_tables"]["bytes"] > 0
 
 
 def test_bsi_reference_known_answers(ctx, oracle):
