@@ -12,6 +12,7 @@ void scan_exclusive(const uint64_t *in, uint64_t *out, uint64_t n, uint64_t *tmp
 void scan_exclusive_multi(const uint64_t *const *in, uint64_t *const *out, int k, uint64_t n, uint64_t *tmp,
                           uint64_t *totals, hipStream_t st);
 // the same for short arrays (per-block totals, n up to ~1M) in one launch; totals may be null
+void launch_noop(hipStream_t st);
 void scan_blocks_multi(const uint64_t *const *in, uint64_t *const *out, int k, uint64_t n, uint64_t *totals,
                        hipStream_t st);
 

@@ -224,4 +224,8 @@ void scan_exclusive_multi(const uint64_t *const *in, uint64_t *const *out, int k
   k_gather_totals<<<1, k, 0, st>>>(m, n, totals);
 }
 
+// An empty dispatch (DeriveTimer): the stream's next event is stamped only once the queue has reached it.
+__global__ void k_noop() {}
+void launch_noop(hipStream_t st) { k_noop<<<1, 64, 0, st>>>(); }
+
 } // namespace rbg
