@@ -520,6 +520,16 @@ int rbgpu_open(int device, rbgpu_ctx **out) {
   for (auto &e : c->ev_side) (void)hipEventCreate(&e);
   (void)hipEventCreate(&c->ev_tot);
   (void)hipEventCreateWithFlags(&c->ev_ext, hipEventDisableTiming);
+  // every source file's code object now, not inside the first call of each kind: HIP loads a code object at
+  // the first launch of one of its kernels (~1 ms each), which otherwise lands in that call's time and in a
+  // set's first-use setup (rbgpu_set_setup_parts)
+  for (auto w : {warm_pairwise, warm_scan, warm_wide, warm_wide_runs, warm_wide_xor, warm_bsi, warm_codec, warm_setops,
+                 warm_generate})
+    w(c->stream);
+  if (hipStreamSynchronize(c->stream) != hipSuccess || hipGetLastError() != hipSuccess) {
+    rbgpu_close(c);
+    return fail(RB_EDEVICE, "context creation failed on device %d (kernel load)", device);
+  }
   *out = c;
   return RB_OK;
 }

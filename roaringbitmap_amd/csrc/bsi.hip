@@ -689,4 +689,8 @@ int bsi_compare(rbgpu_ctx *ctx, const rbgpu_set *bsi, int op, uint64_t start, ui
   return RB_OK;
 }
 
+// this file's code object, loaded at context creation (warm_code_objects, api.hip)
+__global__ void k_warm_bsi() {}
+void warm_bsi(hipStream_t st) { k_warm_bsi<<<1, 64, 0, st>>>(); }
+
 } // namespace rbg

@@ -579,4 +579,8 @@ int serialize_device(const rbgpu_set *s, uint32_t first, uint32_t count, uint8_t
   return RB_OK;
 }
 
+// this file's code object, loaded at context creation (warm_code_objects, api.hip)
+__global__ void k_warm_codec() {}
+void warm_codec(hipStream_t st) { k_warm_codec<<<1, 64, 0, st>>>(); }
+
 } // namespace rbg

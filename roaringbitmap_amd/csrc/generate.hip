@@ -169,6 +169,10 @@ void launch_gen_emit(const GenSpec &g, uint64_t n, const uint8_t *type, const ui
   k_gen_emit<<<(unsigned)std::min<uint64_t>((n + 3) / 4, 1u << 20), 256, 0, st>>>(g, n, type, off, payload);
 }
 
+// this file's code object, loaded at context creation (warm_code_objects, api.hip)
+__global__ void k_warm_generate() {}
+void warm_generate(hipStream_t st) { k_warm_generate<<<1, 64, 0, st>>>(); }
+
 } // namespace rbg
 
 // ===================================================================== host side

@@ -227,8 +227,7 @@ int ensure_h_begin(const rbgpu_set *s);
 // Derived metadata (rbgpu_set): built once per set on the set's stream, timed with events so the cost
 // is reported (rbgpu_set_derive_ms), then cached — the set is immutable.  The start event follows an empty
 // dispatch: an event recorded on an idle stream is stamped when the host records it, so it would also time
-// the host's launch calls and, on a fresh process, the mapping of a newly allocated buffer, which holds the
-// next dispatch back (~0.9 ms for 2 GiB: profiles/r05/krec) — an allocator cost, not the set's.
+// the host's launch calls (scripts/micro/idle_event.cpp).
 struct DeriveTimer {
   hipEvent_t e0 = nullptr, e1 = nullptr;
   rbgpu_set *s;

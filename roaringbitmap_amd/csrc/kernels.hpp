@@ -13,6 +13,16 @@ void scan_exclusive_multi(const uint64_t *const *in, uint64_t *const *out, int k
                           uint64_t *totals, hipStream_t st);
 // the same for short arrays (per-block totals, n up to ~1M) in one launch; totals may be null
 void launch_noop(hipStream_t st);
+// one empty launch per source file: HIP loads a file's code object at the first launch of any of its kernels
+void warm_bsi(hipStream_t st);
+void warm_codec(hipStream_t st);
+void warm_generate(hipStream_t st);
+void warm_pairwise(hipStream_t st);
+void warm_scan(hipStream_t st);
+void warm_setops(hipStream_t st);
+void warm_wide(hipStream_t st);
+void warm_wide_runs(hipStream_t st);
+void warm_wide_xor(hipStream_t st);
 void scan_blocks_multi(const uint64_t *const *in, uint64_t *const *out, int k, uint64_t n, uint64_t *totals,
                        hipStream_t st);
 

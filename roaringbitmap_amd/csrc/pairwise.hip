@@ -1809,4 +1809,8 @@ void launch_pair_small(int op, bool card_only, const SmallPairArgs &a, const Sma
   }
 }
 
+// this file's code object, loaded at context creation (warm_code_objects, api.hip)
+__global__ void k_warm_pairwise() {}
+void warm_pairwise(hipStream_t st) { k_warm_pairwise<<<1, 64, 0, st>>>(); }
+
 } // namespace rbg

@@ -228,4 +228,8 @@ void scan_exclusive_multi(const uint64_t *const *in, uint64_t *const *out, int k
 __global__ void k_noop() {}
 void launch_noop(hipStream_t st) { k_noop<<<1, 64, 0, st>>>(); }
 
+// this file's code object, loaded at context creation (warm_code_objects, api.hip)
+__global__ void k_warm_scan() {}
+void warm_scan(hipStream_t st) { k_warm_scan<<<1, 64, 0, st>>>(); }
+
 } // namespace rbg

@@ -114,4 +114,8 @@ void launch_run_optimize(const SetView &s, uint64_t n, uint8_t *type, uint16_t *
   if (nb && any_run) k_any_run<<<(nb + 3) / 4, 256, 0, st>>>(s.begin, type, nb, any_run);
 }
 
+// this file's code object, loaded at context creation (warm_code_objects, api.hip)
+__global__ void k_warm_setops() {}
+void warm_setops(hipStream_t st) { k_warm_setops<<<1, 64, 0, st>>>(); }
+
 } // namespace rbg

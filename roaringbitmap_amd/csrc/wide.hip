@@ -843,4 +843,8 @@ int wide_run(rbgpu_ctx *ctx, int sem, const rbgpu_set *in, const std::vector<uin
   return RB_OK;
 }
 
+// this file's code object, loaded at context creation (warm_code_objects, api.hip)
+__global__ void k_warm_wide() {}
+void warm_wide(hipStream_t st) { k_warm_wide<<<1, 64, 0, st>>>(); }
+
 } // namespace rbg

@@ -542,4 +542,8 @@ bool launch_wide_runs(int sem, const SetView &s, const uint64_t *mrec, const Cid
   }
 }
 
+// this file's code object, loaded at context creation (warm_code_objects, api.hip)
+__global__ void k_warm_wide_runs() {}
+void warm_wide_runs(hipStream_t st) { k_warm_wide_runs<<<1, 64, 0, st>>>(); }
+
 } // namespace rbg

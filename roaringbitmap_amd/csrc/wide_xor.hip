@@ -984,4 +984,8 @@ void launch_wide_runs_xor(const SetView &s, const uint32_t *cid, const uint64_t 
   k_wide_runs_xor<<<(nk + 3) / 4, 256, 0, st>>>(s, xr.rec, seg, klist, nk, out, wo, route, stats, fastfwd);
 }
 
+// this file's code object, loaded at context creation (warm_code_objects, api.hip)
+__global__ void k_warm_wide_xor() {}
+void warm_wide_xor(hipStream_t st) { k_warm_wide_xor<<<1, 64, 0, st>>>(); }
+
 } // namespace rbg
