@@ -540,15 +540,17 @@ def run_bsi(args, D, ctx, rb, steps=5, warmup=2):
     def step():
         if comm is not None:  # rbgpu_bsi_compare_sharded: local key range + summary all-gather in librbgpu
             r, summ = comm.bsi_compare_sharded(rb.BSI_RANGE, d, BSI_LO, BSI_HI, vmin, vmax, kr)
-            st, card = ctx.stats(), summ["cardinality"]
+            st, card = ctx.stats_raw(), summ["cardinality"]
         else:
             r = ctx.bsi_compare(rb.BSI_RANGE, d, BSI_LO, BSI_HI, vmin, vmax, key_range=kr)
-            st = ctx.stats()
+            st = ctx.stats_raw()  # the struct; converted to a dict after the timed loop
             card = sb.finish(r, kr, r.summaries()[0]).cardinality if sb is not None else None
         r.close()
         return st, card
 
+    from roaringbitmap_amd.engine import stats_dict
     el, sts = timed(D, ctx, steps, warmup, step)
+    sts = [(stats_dict(s), c) for s, c in sts]
     in_b = sum(s["input_bytes"] for s, _ in sts)
     tot_in = D.reduce([float(in_b)])[0]
     last = sts[-1][0]

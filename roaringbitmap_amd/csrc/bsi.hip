@@ -561,9 +561,21 @@ static int ensure_bsi_tables(rbgpu_ctx *ctx, const rbgpu_set *cs, uint32_t nbits
     ctx->pool.release(kl);
     return fail(RB_EDEVICE, "bsi table kernels failed");
   }
+  s->bsi_nk = (uint32_t)(s->h_begin[nbits + 1] - s->h_begin[nbits]);
+  if (s->bsi_nk) { // ebM's first and last key: a key-range shard that holds them all takes the cached list
+    uint32_t *h = reinterpret_cast<uint32_t *>(ctx->h_pinned);
+    if (hipMemcpyAsync(h, kl, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipMemcpyAsync(h + 1, kl + s->bsi_nk - 1, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess) {
+      ctx->pool.release(t);
+      ctx->pool.release(kl);
+      return fail(RB_EDEVICE, "bsi key list read-back failed");
+    }
+    s->bsi_kmin = h[0];
+    s->bsi_kmax = h[1];
+  }
   s->bsi_table = t;
   s->bsi_klist = kl;
-  s->bsi_nk = (uint32_t)(s->h_begin[nbits + 1] - s->h_begin[nbits]);
   // keys read, table entries written (4 B per container), ebM's key list written
   const uint64_t b = 6ull * (s->h_begin[nbits + 1] - s->h_begin[0]) + 4ull * s->bsi_nk;
   s->derive_bytes += b;
@@ -626,7 +638,8 @@ int bsi_compare(rbgpu_ctx *ctx, const rbgpu_set *bsi, int op, uint64_t start, ui
     for (void *p : {(void *)d_active, (void *)d_pos, (void *)d_kl}) ctx->pool.release(p);
   };
   const bool full = key_lo == 0 && key_hi >= 65536;
-  if (!found && full) {
+  if (!found && (full || !bsi->bsi_nk || (key_lo <= bsi->bsi_kmin && bsi->bsi_kmax < key_hi))) {
+    // every key of ebM lies in the range (the whole range, or a shard holding the index's own keys)
     d_klist = bsi->bsi_klist;
     nk = bsi->bsi_nk;
   } else {

@@ -211,7 +211,7 @@ struct rbgpu_set {
   // scratch row for a call's foundSet) and the keys of its last bitmap (ebM), built on first use
   int32_t *bsi_table = nullptr;
   uint32_t *bsi_klist = nullptr;
-  uint32_t bsi_nk = 0;
+  uint32_t bsi_nk = 0, bsi_kmin = 0, bsi_kmax = 0; // ebM's key count and first / last key
   rbg::SetView view() const { return rbg::SetView{begin, key, type, card, nruns, off, payload}; }
 };
 
