@@ -484,6 +484,36 @@ int stats_fill(rbgpu_ctx *ctx, uint64_t tasks, uint64_t result_containers, const
   }
   return RB_OK;
 }
+// Host-visible result words a one-launch call's last block writes (8 words: [5] = the call's sequence
+// number, written last) and the device counters it resets (pairwise_small, the fused BSI compare).
+int ensure_call_words(rbgpu_ctx *ctx) {
+  if (!ctx->h_small) {
+    if (hipHostMalloc((void **)&ctx->h_small, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
+      return fail(RB_ENOMEM, "host-visible result words");
+    if (hipHostGetDevicePointer((void **)&ctx->d_small, ctx->h_small, 0) != hipSuccess) {
+      (void)hipHostFree(ctx->h_small);
+      ctx->h_small = nullptr;
+      return fail(RB_EDEVICE, "host-visible result words have no device address");
+    }
+  }
+  if (!ctx->d_small_ctr) { // the finished-block count and the counters; the last block of every call resets them
+    if (hipMalloc((void **)&ctx->d_small_ctr, 512) != hipSuccess) return fail(RB_ENOMEM, "block counters");
+    if (hipMemset(ctx->d_small_ctr, 0, 512) != hipSuccess) return fail(RB_EDEVICE, "block counters");
+  }
+  return RB_OK;
+}
+// Spins (bounded) until the call's last block has written `seq` after its result words: the host returns
+// without waiting for the kernel's end to be signalled (it has no work left by then, and later calls on the
+// stream are ordered behind it).  false: not seen in time — the caller waits for the stream, which also
+// reports a fault.
+bool wait_call_seq(rbgpu_ctx *ctx, uint64_t seq) {
+  const volatile uint64_t *flag = reinterpret_cast<const volatile uint64_t *>(ctx->h_small) + 5;
+  const auto t0 = std::chrono::steady_clock::now();
+  for (uint32_t it = 0;; ++it) {
+    if (__atomic_load_n(const_cast<const uint64_t *>(flag), __ATOMIC_ACQUIRE) == seq) return true;
+    if ((it & 1023u) == 1023u && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(50)) return false;
+  }
+}
 } // namespace rbg
 
 // ===================================================================== C ABI
@@ -1016,20 +1046,8 @@ static int pairwise_small(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgp
     else blk[p] = k;
     if (p < np) k += nsub(p, kpw);
   }
-  // host-visible words the last block writes the call's results to (8 words)
-  if (!ctx->h_small) {
-    if (hipHostMalloc((void **)&ctx->h_small, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
-      return fail(RB_ENOMEM, "host-visible result words");
-    if (hipHostGetDevicePointer((void **)&ctx->d_small, ctx->h_small, 0) != hipSuccess) {
-      (void)hipHostFree(ctx->h_small);
-      ctx->h_small = nullptr;
-      return fail(RB_EDEVICE, "host-visible result words have no device address");
-    }
-  }
-  if (!ctx->d_small_ctr) { // the finished-block count and the counters; the last block of every call resets them
-    if (hipMalloc((void **)&ctx->d_small_ctr, 512) != hipSuccess) return fail(RB_ENOMEM, "block counters");
-    if (hipMemset(ctx->d_small_ctr, 0, 512) != hipSuccess) return fail(RB_EDEVICE, "block counters");
-  }
+  rc = ensure_call_words(ctx);
+  if (rc) return rc;
   uint64_t *hout = reinterpret_cast<uint64_t *>(ctx->h_small);
 
   hipStream_t st = ctx->stream;
@@ -1092,23 +1110,9 @@ static int pairwise_small(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgp
   if (ktimes) HIPCHK(hipEventRecord(ctx->ev[2], st));
   if (card_out) HIPCHK(hipMemcpyAsync(card_out, sa.pcard, 8ull * np, hipMemcpyDeviceToHost, st));
   HIPCHK(hipEventRecord(ctx->ev[5], st));
-  // The last block writes the result words to host memory and then the call's sequence number: the host
-  // returns once it reads that number, without waiting for the kernel's end to be signalled (the kernel has
-  // no work left by then, and later calls on the stream are ordered behind it).  Per-pair cardinalities
-  // come back by a copy, so those calls wait for the stream; a kernel that never writes the number (a
-  // fault) is caught by the stream wait after a bounded spin.
-  bool seen = false;
-  if (RBG_SMALL_POLL && !card_out) {
-    const volatile uint64_t *flag = reinterpret_cast<const volatile uint64_t *>(ctx->h_small) + 5;
-    const auto t0 = std::chrono::steady_clock::now();
-    for (uint32_t it = 0;; ++it) {
-      if (__atomic_load_n(const_cast<const uint64_t *>(flag), __ATOMIC_ACQUIRE) == sa.seq) {
-        seen = true;
-        break;
-      }
-      if ((it & 1023u) == 1023u && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(50)) break;
-    }
-  }
+  // The last block writes the result words to host memory and then the call's sequence number
+  // (wait_call_seq); per-pair cardinalities come back by a copy, so those calls wait for the stream.
+  const bool seen = RBG_SMALL_POLL && !card_out && wait_call_seq(ctx, sa.seq);
   {
     const hipError_t e1 = seen ? hipSuccess : hipStreamSynchronize(st), e2 = hipGetLastError();
     if (e1 != hipSuccess || e2 != hipSuccess) {

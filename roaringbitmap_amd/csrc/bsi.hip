@@ -349,19 +349,37 @@ __device__ __forceinline__ Meta bsi_final_ge_le(uint64_t (&t)[kW], const uint64_
   }
   return rm;
 }
+// RANGE's one launch: per key both chains and the final AND (bsi_range_key), then the call's tail in the
+// last block to finish (the hand-off of wave.hpp's st_sc1 / ld_sc1): the keyed results compacted into the
+// result SoA and CSR, the counters and the result count written to host-visible words, the call's sequence
+// number last (the host returns on it: wait_call_seq).
+struct BsiTail {
+  uint64_t *kmeta;  // [nk] per key: card (bits 0-16), type (19-20; 3 = none), key (24-39), run count (40-55)
+  uint64_t *ctr;    // [0] finished blocks, [8] / [16] / [24] input bytes / output bytes / cardinality
+  OutView ov;
+  uint64_t *rbegin; // [2]
+  uint64_t *hout;   // host-visible: [0] result containers, [1..3] the counters, [5] = seq
+  uint64_t seq;
+  uint32_t nblocks;
+};
+__device__ __forceinline__ uint64_t bsi_meta(uint32_t key, int ty, uint32_t card, uint32_t nr) {
+  return (card & 0x1FFFFu) | ((uint64_t)(ty == (int)kEmpty ? 3u : (uint32_t)ty) << 19) | ((uint64_t)key << 24) |
+         ((uint64_t)nr << 40);
+}
 __global__ __launch_bounds__(128, 2) void k_bsi_range(SetView bsi, SetView fnd, int has_found,
                                                       const int32_t *__restrict__ table, uint32_t nbits,
                                                       uint64_t start, uint64_t end, const uint32_t *__restrict__ klist,
-                                                      uint32_t nk, uint8_t *__restrict__ out, WideOut wo,
-                                                      uint64_t *stats) {
+                                                      uint32_t nk, uint8_t *__restrict__ out, BsiTail tl) {
   __shared__ __attribute__((aligned(16))) uint32_t lds[2][3][2048];
+  __shared__ uint64_t red[2][3];
+  __shared__ uint32_t s_last, wt[4];
   const int lane = lane_id();
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t q = xcd_swizzle(blockIdx.x, gridDim.x) * 2 + wv;
-  if (q >= nk) return;
+  uint64_t inb = 0, outb = 0, csum = 0;
+  if (q < nk) { // wave-uniform
   uint32_t *sS = lds[wv][0], *sG = lds[wv][1], *sL = lds[wv][2];
   const uint32_t key = klist[q];
-  uint64_t inb = 0;
   uint64_t eg[kW], el[kW];
   Meta eqg = stage_global(bsi, table[(uint64_t)nbits * 65536 + key], sS, lane);
   if (eqg.present) {
@@ -460,14 +478,68 @@ __global__ __launch_bounds__(128, 2) void k_bsi_range(SetView bsi, SetView fnd, 
   wave_lds_sync();
   const int ty = rm.present ? rm.type : kEmpty;
   if (rm.present) emit_container(ty, t, rm.card, rm.runs, out + (uint64_t)q * kBitmapBytes, sS, lane);
+  if (lane == 0)
+    st_sc1(tl.kmeta + q, bsi_meta(key, ty, rm.present ? (uint32_t)rm.card : 0u, ty == kRun ? (uint32_t)rm.runs : 0u));
+  if (rm.present) {
+    outb = payload_bytes(ty, rm.card, rm.runs) + (ty == kRun ? 2 : 0) + 16;
+    csum = (uint64_t)rm.card;
+  }
+  } // q < nk
+  // ---- the block's counters (one agent atomic per counter), then the finished-block add
   if (lane == 0) {
-    wo.type[q] = (uint8_t)ty;
-    wo.card[q] = (uint32_t)(rm.present ? rm.card : 0);
-    wo.nruns[q] = (uint16_t)(ty == kRun ? rm.runs : 0);
-    if (inb) atomicAdd((unsigned long long *)&stats[0 * kStripes + (q & (kStripes - 1))], (unsigned long long)inb);
-    if (rm.present)
-      atomicAdd((unsigned long long *)&stats[1 * kStripes + (q & (kStripes - 1))],
-                (unsigned long long)(payload_bytes(ty, rm.card, rm.runs) + (ty == kRun ? 2 : 0) + 16));
+    red[wv][0] = inb;
+    red[wv][1] = outb;
+    red[wv][2] = csum;
+  }
+  __syncthreads();
+  if (threadIdx.x < 3) {
+    const uint64_t x = red[0][threadIdx.x] + red[1][threadIdx.x];
+    if (x) __hip_atomic_fetch_add(tl.ctr + 8 + 8 * threadIdx.x, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0)
+    s_last = __hip_atomic_fetch_add(tl.ctr, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == tl.nblocks - 1ull;
+  __syncthreads();
+  if (!s_last) return;
+  // ---- the last block: the keyed results compacted in key order (dropped keys leave no container)
+  const uint64_t v = threadIdx.x < 3 ? ld_sc1(tl.ctr + 8 + 8 * threadIdx.x) : 0;
+  constexpr int kPer = 16;
+  uint32_t base = 0;
+  for (uint32_t t0 = 0; t0 < nk; t0 += kPer * blockDim.x) {
+    const uint32_t lo = t0 + kPer * threadIdx.x;
+    uint64_t m[kPer];
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) m[k] = lo + k < nk ? ld_sc1(tl.kmeta + lo + k) : (3ull << 19);
+    uint32_t cnt = 0;
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) cnt += ((m[k] >> 19) & 3u) != 3u;
+    uint32_t tot;
+    uint32_t r = base + block_xscan(cnt, wt, tot);
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+      if (((m[k] >> 19) & 3u) == 3u) continue;
+      tl.ov.key[r] = (uint16_t)(m[k] >> 24);
+      tl.ov.type[r] = (uint8_t)((m[k] >> 19) & 3u);
+      tl.ov.card[r] = (uint32_t)(m[k] & 0x1FFFFu);
+      tl.ov.nruns[r] = (uint16_t)(m[k] >> 40);
+      tl.ov.off[r] = (uint64_t)(lo + k) * kBitmapBytes;
+      ++r;
+    }
+    base += tot;
+  }
+  if (threadIdx.x < 3) {
+    red[0][threadIdx.x] = v;
+    __hip_atomic_store(tl.ctr + 8 + 8 * threadIdx.x, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __hip_atomic_store(tl.ctr, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); // ready for the next call
+    tl.rbegin[0] = 0;
+    tl.rbegin[1] = base;
+    for (int k = 0; k < 3; ++k) tl.hout[1 + k] = red[0][k];
+    tl.hout[0] = base;
+    __hip_atomic_store(tl.hout + 5, tl.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
 
@@ -583,6 +655,50 @@ static int ensure_bsi_tables(rbgpu_ctx *ctx, const rbgpu_set *cs, uint32_t nbits
   return RB_OK;
 }
 
+// RANGE over nk >= 1 keys of F: k_bsi_range writes the result set (CSR, SoA, payload slots) and the call's
+// counters itself; the host returns on the call's sequence number (wait_call_seq).
+static int bsi_range_one_launch(rbgpu_ctx *ctx, const rbgpu_set *bsi, const rbgpu_set *found, const int32_t *d_table,
+                                uint32_t nbits, uint64_t start, uint64_t end, const uint32_t *d_klist, uint32_t nk,
+                                rbgpu_set *res) {
+  hipStream_t st = ctx->stream;
+  int rc = ensure_call_words(ctx);
+  if (rc) return rc;
+  uint64_t *kmeta = nullptr;
+  if (ctx->pool.alloc((void **)&kmeta, 8ull * nk)) return fail(RB_ENOMEM, "bsi key results");
+  const uint32_t nblocks = nblk(nk, 2);
+  BsiTail tl{kmeta, ctx->d_small_ctr, OutView{res->key, res->type, res->card, res->nruns, res->off}, res->begin,
+             reinterpret_cast<uint64_t *>(ctx->d_small), ++ctx->small_seq, nblocks};
+  HIPCHK(hipEventRecord(ctx->ev[1], st));
+  k_bsi_range<<<nblocks, 128, 0, st>>>(bsi->view(), found ? found->view() : bsi->view(), found != nullptr, d_table,
+                                       nbits, start, end, d_klist, nk, res->payload, tl);
+  HIPCHK(hipEventRecord(ctx->ev[2], st));
+  HIPCHK(hipEventRecord(ctx->ev[5], st));
+  ctx->pool.release(kmeta); // stream-ordered: handed out again only to later work on this stream
+  const bool seen = wait_call_seq(ctx, tl.seq);
+  {
+    const hipError_t e1 = seen ? hipSuccess : hipStreamSynchronize(st), e2 = hipGetLastError();
+    if (e1 != hipSuccess || e2 != hipSuccess)
+      return fail(RB_EDEVICE, "bsi range kernel failed: %s", hipGetErrorString(e1 != hipSuccess ? e1 : e2));
+  }
+  const uint64_t *hout = reinterpret_cast<const uint64_t *>(ctx->h_small);
+  uint64_t *w = ctx->words;
+  for (int i = 0; i < kStatWords; ++i) w[i] = 0;
+  w[0] = hout[1]; // input bytes
+  w[1] = hout[2]; // output bytes
+  w[7] = hout[3]; // result cardinality
+  w[8] = hout[0]; // result containers
+  const uint64_t nres = hout[0];
+  const KernelSpan spans[1] = {{"k_bsi_range", 0, 1, 2ull * nk}};
+  rc = stats_fill(ctx, nk, nres, spans, 1, !seen);
+  ctx->stats_pending = seen;
+  ctx->stats_pending_k = seen;
+  if (rc) return rc;
+  ctx->last.result_containers = nres;
+  res->nc = nres;
+  res->h_begin = {0, nres};
+  return RB_OK;
+}
+
 int bsi_compare(rbgpu_ctx *ctx, const rbgpu_set *bsi, int op, uint64_t start, uint64_t end, uint64_t vmin,
                 uint64_t vmax, const rbgpu_set *found, uint32_t key_lo, uint32_t key_hi, rbgpu_set **out) {
   const uint32_t nbits = bsi->nb - 1;
@@ -675,16 +791,22 @@ int bsi_compare(rbgpu_ctx *ctx, const rbgpu_set *bsi, int op, uint64_t start, ui
     release();
     return rc;
   }
+  if (op == 6 && nk) { // RANGE: one launch (k_bsi_range's tail compacts and hands the results to the host)
+    rc = bsi_range_one_launch(ctx, bsi, found, d_table, nbits, start, end, d_klist, nk, res);
+    release();
+    if (rc) {
+      rbgpu_set_free(res);
+      return rc;
+    }
+    *out = res;
+    return RB_OK;
+  }
   KeyedSlots fin;
   rc = fin.alloc(ctx, nk, false);
   if (!rc) {
     HIPCHK(hipEventRecord(ctx->ev[1], st));
     if (op != 6) {
       bsi_chain(ctx, bsi, nbits, op, start, found, d_table, d_klist, nk, res->payload, fin.wo);
-    } else if (nk) { // RANGE: both chains in one pass, then the keyed static AND in-kernel
-      k_bsi_range<<<nblk(nk, 2), 128, 0, st>>>(bsi->view(), found ? found->view() : bsi->view(), found != nullptr,
-                                               d_table, nbits, start, end, d_klist, nk, res->payload, fin.wo,
-                                               ctx->d_stats);
     }
     HIPCHK(hipEventRecord(ctx->ev[2], st));
     rc = compact_keyed(ctx, d_klist, nk, fin.wo, res);

@@ -224,6 +224,8 @@ int pairwise_call(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu_set *b
 void ctx_unref(rbgpu_ctx *ctx);
 void set_release(rbgpu_set *s);
 int ensure_h_begin(const rbgpu_set *s);
+int ensure_call_words(rbgpu_ctx *ctx);
+bool wait_call_seq(rbgpu_ctx *ctx, uint64_t seq);
 // Derived metadata (rbgpu_set): built once per set on the set's stream, timed with events so the cost
 // is reported (rbgpu_set_derive_ms), then cached — the set is immutable.  The start event follows an empty
 // dispatch: an event recorded on an idle stream is stamped when the host records it, so it would also time

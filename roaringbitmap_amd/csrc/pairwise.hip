@@ -248,22 +248,6 @@ __device__ __forceinline__ void block_sums(const uint64_t (&v)[N], uint64_t (&su
   __syncthreads();
 }
 
-// exclusive block-wide prefix of v (blockDim.x a multiple of 64, <= 1024); *total = the sum
-__device__ __forceinline__ uint32_t block_xscan(uint32_t v, uint32_t *wtot, uint32_t &total) {
-  const int lane = lane_id(), w = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  const uint32_t inc = wave_scan_u32(v, lane);
-  if (lane == 63) wtot[w] = inc;
-  __syncthreads();
-  uint32_t before = 0;
-  total = 0;
-  for (int i = 0; i < nw; ++i) {
-    const uint32_t t = wtot[i];
-    if (i < w) before += t;
-    total += t;
-  }
-  __syncthreads();
-  return before + inc - v;
-}
 
 // ---------------------------------------------------------------- key alignment by merge path
 // A pair is cut into segments of <= a.seg_keys merged keys (merge path over the two sorted key lists,
@@ -1460,16 +1444,8 @@ __device__ __forceinline__ bool meta_empty(uint64_t m) { return ((m >> 19) & 3u)
 __device__ __forceinline__ uint32_t meta_cw(uint64_t m) {
   return (uint32_t)(m & 0x1FFFFu) | ((m >> 17) & 1u ? kLazyCard : 0u) | ((m >> 18) & 1u ? kRunAsBitmap : 0u);
 }
-// Cross-block hand-off (MI355X_MICROARCH.md, inter-workgroup visibility, first table row): every block's
-// slot words and counters are stored sc1, each storing wave waits for them, then one agent-scope add per
-// block; the block whose add comes last reads them with sc1 loads.  The slot payloads stay plain stores:
-// nothing in the launch reads them.
-__device__ __forceinline__ void st_sc1(uint64_t *p, uint64_t v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ uint64_t ld_sc1(const uint64_t *p) {
-  return __hip_atomic_load(const_cast<uint64_t *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
+// Cross-block hand-off: st_sc1 / ld_sc1 (wave.hpp); the slot payloads stay plain stores: nothing in the
+// launch reads them.
 
 // The compaction, run by the last block of k_pair_small: drop the empty slots, write the result SoA and
 // CSR (slot t's payload stays at t * 8 KiB), add up the blocks' counters and write the call's result words

@@ -280,6 +280,32 @@ __device__ __forceinline__ void stage_container(int type, const uint8_t *p, uint
   wave_lds_sync();
 }
 
+// exclusive block-wide prefix of v (blockDim.x a multiple of 64, <= 1024); *total = the sum
+__device__ __forceinline__ uint32_t block_xscan(uint32_t v, uint32_t *wtot, uint32_t &total) {
+  const int lane = lane_id(), w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const uint32_t inc = wave_scan_u32(v, lane);
+  if (lane == 63) wtot[w] = inc;
+  __syncthreads();
+  uint32_t before = 0;
+  total = 0;
+  for (int i = 0; i < nw; ++i) {
+    const uint32_t t = wtot[i];
+    if (i < w) before += t;
+    total += t;
+  }
+  __syncthreads();
+  return before + inc - v;
+}
+// Cross-block hand-off (MI355X_MICROARCH.md, inter-workgroup visibility, first table row): every block's
+// words and counters are stored sc1, each storing wave waits for them (s_waitcnt vmcnt(0)), then one
+// agent-scope add per block; the block whose add comes last reads them with sc1 loads.
+__device__ __forceinline__ void st_sc1(uint64_t *p, uint64_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t ld_sc1(const uint64_t *p) {
+  return __hip_atomic_load(const_cast<uint64_t *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // ---------------------------------------------------------------- register-preloaded payloads
 // A payload of at most 8 KiB as 8 uint4 per lane: chunk c = lane + 64*i (16 bytes) in q[i].
 // Buffer loads: a 32-bit per-lane offset against a wave-uniform descriptor, and lanes past the
