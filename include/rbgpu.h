@@ -139,6 +139,9 @@ typedef struct rb_stats {
 
 /* ---- context ---------------------------------------------------------------------- */
 int rbgpu_device_count(void);
+/* A context: one stream pair, an allocation cache and the library's kernels loaded on the device (every
+ * source file's code object is loaded here, ~1 ms each, so no later call pays a first-launch load).
+ * Open one per device and keep it for the process. */
 int rbgpu_open(int device, rbgpu_ctx **out);
 void rbgpu_close(rbgpu_ctx *ctx);
 const char *rbgpu_last_error(void);
