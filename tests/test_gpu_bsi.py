@@ -124,3 +124,36 @@ def test_bsi_key_range_shards(ctx, oracle):
                 assert serialize_parts(hs) == want, (name, src, f is not None)
     with pytest.raises(rb.InvalidArgument):
         ctx.bsi_compare(rb.BSI_GE, d, 3, 0, 0, vmax, key_range=(5, 70000))
+
+
+def test_bsi_range_one_launch_handoff(ctx, oracle):
+    """RANGE runs as one launch whose last block hands the result count and counters to host-visible
+    words, behind a per-context sequence number that the small-batch pairwise path shares: empty and
+    one-key answers, and RANGE calls interleaved with small pairwise calls on the same context, all equal
+    the oracle; the call's device times are read when the stats are asked for."""
+    import roaringbitmap_amd as rb
+    rng = np.random.default_rng(5)
+    cols, vals = _case(rng, 70000, 12, 1 << 20)
+    sl, ebm, mn, mx = oracle.bsi_build(cols, vals)
+    d, rsl, rebm = _device_bsi(ctx, oracle, sl, ebm, False)
+    one_key = oracle.RefBitmap.of(np.unique(cols[cols < 65536]).astype(np.uint32))
+    found1 = ctx.upload_serialized([one_key.serialize()])
+    absent = int(max(set(range(int(mn), int(mx) + 1)) - set(int(v) for v in vals), default=int(mn)))
+    pair_bms = [np.unique(rng.integers(0, 1 << 18, size=n)).astype(np.uint32) for n in (100, 3000, 20000, 5)]
+    p = ctx.upload_values(pair_bms)
+    prefs = [oracle.RefBitmap.deserialize(b) for b in p.serialize()]
+    cases = [(absent, absent, None, None), (int(mn), int(mx), None, None), (int(vals[0]), int(vals[0]), found1, one_key),
+             (absent, absent, found1, one_key)]
+    for it in range(6):
+        lo, hi, f_dev, f_ref = cases[it % len(cases)]
+        r = ctx.bsi_compare(rb.BSI_RANGE, d, lo, hi, int(mn), int(mx), f_dev)
+        st = ctx.stats()
+        want = oracle.bsi_compare(rsl, rebm, rb.BSI_RANGE, lo, hi, f_ref, int(mn), int(mx))
+        assert r.serialize()[0] == want.serialize(), (it, lo, hi)
+        if (lo, hi) != (int(mn), int(mx)):  # (the whole value range is compareUsingMinMax's shortcut: no kernel)
+            assert st["result_cardinality"] == want.cardinality()
+            assert st["total_ms"] > 0.0 and st["main_kernel_ms"] > 0.0
+        for op in (rb.AND, rb.OR):  # small batches on the same context between the compares
+            got = ctx.pairwise(op, p, p, [0, 1, 2], [1, 2, 3]).serialize()
+            assert got == [oracle.op(op, prefs[i], prefs[i + 1]).serialize() for i in range(3)]
+            assert ctx.stats()["total_ms"] > 0.0

@@ -100,12 +100,21 @@ def _array_pair_bitmaps(rng):
     right.append(arr(22, base[1000:1500]))
     left.append(arr(23, np.arange(100, 2100)))
     right.append(arr(23, np.arange(101, 2101)))
+    # one side of <= 64 values (closed-form placement) and just above it: all / none / some of it in the
+    # other side, below / above every value of the other side, the extreme values 0 and 65535
+    big = np.sort(rnd(3000, 1000, 60000))
+    for k, small in enumerate((big[::47][:64], rnd(64, 0, 1000), np.concatenate([[0, 65535], big[5:40:7], rnd(20, 60001, 65535)]),
+                               big[::46][:65], np.array([65535]), np.array([0, 999]))):
+        left.append(arr(24 + k, big))
+        right.append(arr(24 + k, small))
+        left.append(arr(40 + k, small))
+        right.append(arr(40 + k, big))
     a_bms, b_bms = [], []
     for i in range(len(left)):  # one bitmap per case, and one holding every case's key
         a_bms.append(left[i])
         b_bms.append(right[i])
-    a_bms.append(np.concatenate(left))
-    b_bms.append(np.concatenate(right))
+    a_bms.append(np.sort(np.concatenate(left)))
+    b_bms.append(np.sort(np.concatenate(right)))
     return a_bms, b_bms
 
 
