@@ -228,8 +228,30 @@ int rbgpu_pairwise(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu_set *
 int rbgpu_pairwise_async(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu_set *b,
                          const uint32_t *a_idx, const uint32_t *b_idx, uint32_t npairs, void *stream,
                          rbgpu_set **out);
-/* Wait until an asynchronous result is complete (a no-op for any other set). */
+/* Wait until an asynchronous result is complete, and until the kernel of a call that returned on its last
+ * block's sequence word (small batches, BSI RANGE: the host had the result before the kernel's end was
+ * signalled) has ended (a no-op for any other set). */
 int rbgpu_set_wait(const rbgpu_set *set);
+/* Device addresses of a set's SoA in HBM (the layout of rb_soa), for a caller's own device work on results
+ * where they are — the hand-off of a Java caller's MemorySegment over device memory.  Valid while the set
+ * lives; the call never blocks.  Device work may read them once it is ordered after the call that produced
+ * the set: on the `stream` given to rbgpu_pairwise_async (its later work runs after the result is complete,
+ * small batches included), or after rbgpu_set_wait.  n_containers of a pending asynchronous result is
+ * RB_UNKNOWN_COUNT until it is settled; the device's begin[n_bitmaps] holds it once the call is complete. */
+#define RB_UNKNOWN_COUNT 0xFFFFFFFFFFFFFFFFull
+typedef struct rb_device_view {
+  uint32_t n_bitmaps;
+  uint64_t n_containers;
+  uint64_t payload_bytes; /* capacity of the payload arena */
+  const uint64_t *begin;
+  const uint16_t *key;
+  const uint8_t *type;
+  const uint32_t *card;
+  const uint16_t *nruns;
+  const uint64_t *offset;
+  const uint8_t *payload;
+} rb_device_view;
+int rbgpu_set_device_view(const rbgpu_set *set, rb_device_view *out);
 int rbgpu_pairwise_inplace(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu_set *b,
                            const uint32_t *a_idx, const uint32_t *b_idx, uint32_t npairs, rbgpu_set **out);
 /* RoaringBitmap.andCardinality/orCardinality/xorCardinality/andNotCardinality

@@ -1844,4 +1844,88 @@ int rbref_pairwise_batch(int op, const rbref_bitmap *const *a, const rbref_bitma
   return RBREF_OK;
 }
 
+// compareUsingMinMax (bsi/src/main/java/org/roaringbitmap/bsi/buffer/... RoaringBitmapSliceIndex.java:505-577):
+// 1 = all (ebM, or ebM AND foundSet), 0 = empty, -1 = evaluate
+static int bsi_min_max(int op, uint64_t a, uint64_t b, uint64_t mn, uint64_t mx) {
+  switch (op) {
+  case RBREF_BSI_LT: return a > mx ? 1 : a <= mn ? 0 : -1;
+  case RBREF_BSI_LE: return a >= mx ? 1 : a < mn ? 0 : -1;
+  case RBREF_BSI_GT: return a < mn ? 1 : a >= mx ? 0 : -1;
+  case RBREF_BSI_GE: return a <= mn ? 1 : a > mx ? 0 : -1;
+  case RBREF_BSI_EQ: return (mn == mx && mn == a) ? 1 : (a < mn || a > mx) ? 0 : -1;
+  case RBREF_BSI_NEQ: return mn == mx ? (mn == a ? 0 : 1) : -1;
+  default: return (a <= mn && b >= mx) ? 1 : (a > mx || b < mn) ? 0 : -1;
+  }
+}
+// oNeilCompare (RoaringBitmapSliceIndex.java:432-472): the slices top-down, GT / LT / EQ kept as bitmaps
+static BM *bsi_oneil(const rbref_bitmap *const *sl, size_t ns, const BM &ebm, int op, uint64_t pred, const BM *found) {
+  const BM &fixed = found ? *found : ebm;
+  std::unique_ptr<BM> gt(new BM), lt(new BM), eq(new BM(ebm));
+  for (size_t k = ns; k-- > 0;) {
+    const BM &s = *sl[k];
+    if ((pred >> k) & 1) {
+      std::unique_ptr<BM> d(bm_op(RBREF_ANDNOT, *eq, s));
+      lt.reset(bm_op(RBREF_OR, *lt, *d));
+      eq.reset(bm_op(RBREF_AND, *eq, s));
+    } else {
+      std::unique_ptr<BM> d(bm_op(RBREF_AND, *eq, s));
+      gt.reset(bm_op(RBREF_OR, *gt, *d));
+      eq.reset(bm_op(RBREF_ANDNOT, *eq, s));
+    }
+  }
+  eq.reset(bm_op(RBREF_AND, fixed, *eq));
+  switch (op) {
+  case RBREF_BSI_EQ: return eq.release();
+  case RBREF_BSI_NEQ: return bm_op(RBREF_ANDNOT, fixed, *eq);
+  case RBREF_BSI_GT: return bm_op(RBREF_AND, *gt, fixed);
+  case RBREF_BSI_LT: return bm_op(RBREF_AND, *lt, fixed);
+  case RBREF_BSI_LE: {
+    std::unique_ptr<BM> u(bm_op(RBREF_OR, *lt, *eq));
+    return bm_op(RBREF_AND, *u, fixed);
+  }
+  default: { // GE
+    std::unique_ptr<BM> u(bm_op(RBREF_OR, *gt, *eq));
+    return bm_op(RBREF_AND, *u, fixed);
+  }
+  }
+}
+
+rbref_bitmap *rbref_bsi_compare(const rbref_bitmap *const *sl, size_t ns, const rbref_bitmap *ebm, int op,
+                                uint64_t start, uint64_t end, const rbref_bitmap *found, uint64_t vmin, uint64_t vmax) {
+  // compare (RoaringBitmapSliceIndex.java:475-503)
+  const int sc = bsi_min_max(op, start, end, vmin, vmax);
+  if (sc == 1) return found ? bm_op(RBREF_AND, *ebm, *found) : new BM(*ebm);
+  if (sc == 0) return new BM;
+  if (op == RBREF_BSI_RANGE) {
+    std::unique_ptr<BM> ge(bsi_oneil(sl, ns, *ebm, RBREF_BSI_GE, start, found)),
+        le(bsi_oneil(sl, ns, *ebm, RBREF_BSI_LE, end, found));
+    return bm_op(RBREF_AND, *ge, *le);
+  }
+  return bsi_oneil(sl, ns, *ebm, op, start, found);
+}
+
+uint64_t rbref_bsi_compare_keys(const rbref_bitmap *const *per_key, size_t nkeys, size_t ns, int op, uint64_t start,
+                                uint64_t end, uint64_t vmin, uint64_t vmax, int threads) {
+  if (threads < 1) threads = 1;
+  std::vector<uint64_t> cards(threads, 0);
+  auto work = [&](int t) {
+    const size_t lo = nkeys * t / threads, hi = nkeys * (t + 1) / threads;
+    for (size_t k = lo; k < hi; ++k) {
+      const rbref_bitmap *const *key = per_key + k * (ns + 1);
+      std::unique_ptr<BM> r(rbref_bsi_compare(key, ns, key[ns], op, start, end, nullptr, vmin, vmax));
+      cards[t] += bm_card(*r);
+    }
+  };
+  if (threads == 1) {
+    work(0);
+  } else {
+    std::vector<std::thread> th;
+    for (int t = 0; t < threads; ++t) th.emplace_back(work, t);
+    for (auto &x : th) x.join();
+  }
+  uint64_t c = 0;
+  for (uint64_t v : cards) c += v;
+  return c;
+}
+
 } // extern "C"

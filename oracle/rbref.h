@@ -110,6 +110,21 @@ int64_t rbref_wide_cardinality(int op, const rbref_bitmap *const *bitmaps, size_
 int rbref_pairwise_batch(int op, const rbref_bitmap *const *a, const rbref_bitmap *const *b,
                          size_t npairs, int threads, uint64_t *total_card, uint64_t *total_containers);
 
+/* BitSliceIndex compare (bsi/.../RoaringBitmapSliceIndex.java:475-577; the static ops of
+ * Roaring64BitmapSliceIndex.compare are the same Container and/or/andNot): compareUsingMinMax, then
+ * oNeilCompare (:432-472), RANGE as GE(start) AND LE(end).  slices[0..nslices) low bit first, ebm the
+ * existence bitmap, found NULL or the foundSet; op is BitmapSliceIndex.Operation's ordinal (EQ, NEQ, LE, LT,
+ * GE, GT, RANGE).  Values unsigned.  The C++ twin of oracle/rbref.py bsi_compare. */
+enum { RBREF_BSI_EQ = 0, RBREF_BSI_NEQ, RBREF_BSI_LE, RBREF_BSI_LT, RBREF_BSI_GE, RBREF_BSI_GT, RBREF_BSI_RANGE };
+rbref_bitmap *rbref_bsi_compare(const rbref_bitmap *const *slices, size_t nslices, const rbref_bitmap *ebm, int op,
+                                uint64_t start, uint64_t end, const rbref_bitmap *found, uint64_t vmin, uint64_t vmax);
+/* CPU-baseline helper: the compare over nkeys independent indexes (per high key: nslices slices then ebM,
+ * per_key[k * (nslices + 1) + i]), keys split over `threads` host threads in contiguous ranges, the way a
+ * key-parallel BSI (BitSliceIndexBase.java:99-166's parallel split) divides the work.  Returns the total
+ * result cardinality. */
+uint64_t rbref_bsi_compare_keys(const rbref_bitmap *const *per_key, size_t nkeys, size_t nslices, int op,
+                                uint64_t start, uint64_t end, uint64_t vmin, uint64_t vmax, int threads);
+
 #ifdef __cplusplus
 }
 #endif

@@ -54,6 +54,10 @@ def _load():
         "rbref_wide_mt": (P, [C.c_int, C.POINTER(P), C.c_size_t, C.c_int]),
         "rbref_pairwise_batch": (C.c_int, [C.c_int, C.POINTER(P), C.POINTER(P), C.c_size_t, C.c_int,
                                            C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
+        "rbref_bsi_compare": (P, [C.POINTER(P), C.c_size_t, P, C.c_int, C.c_uint64, C.c_uint64, P, C.c_uint64,
+                                  C.c_uint64]),
+        "rbref_bsi_compare_keys": (C.c_uint64, [C.POINTER(P), C.c_size_t, C.c_size_t, C.c_int, C.c_uint64,
+                                               C.c_uint64, C.c_uint64, C.c_uint64, C.c_int]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -305,3 +309,18 @@ def bsi_compare(slices, ebm, op_, start, end, found, vmin, vmax):
     if op_ == BSI_RANGE:
         return op(AND, _oneil(slices, ebm, BSI_GE, start, found), _oneil(slices, ebm, BSI_LE, end, found))
     return _oneil(slices, ebm, op_, start, found)
+
+
+def bsi_compare_cpp(slices, ebm, op_, start, end, found, vmin, vmax) -> RefBitmap:
+    """rbref_bsi_compare: the C++ twin of bsi_compare (the same compareUsingMinMax / oNeilCompare steps over
+    the same static ops), which the BSI CPU baseline times without the interpreter in the loop."""
+    return RefBitmap(lib().rbref_bsi_compare(_handles(slices), len(slices), ebm.h, op_, start, end,
+                                             found.h if found is not None else None, vmin, vmax))
+
+
+def bsi_compare_keys(per_key, op_, start, end, vmin, vmax, threads: int = 1) -> int:
+    """rbref_bsi_compare_keys: per_key = [(slices, ebm)] of independent per-high-key indexes, compared on
+    `threads` host threads (contiguous key ranges); the total result cardinality."""
+    ns = len(per_key[0][0]) if per_key else 0
+    flat = [b for sl, eb in per_key for b in list(sl) + [eb]]
+    return int(lib().rbref_bsi_compare_keys(_handles(flat), len(per_key), ns, op_, start, end, vmin, vmax, threads))

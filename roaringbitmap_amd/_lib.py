@@ -41,6 +41,13 @@ class RbSoa(C.Structure):
     ]
 
 
+class RbDeviceView(C.Structure):  # rb_device_view: the rb_soa layout with device addresses
+    _fields_ = RbSoa._fields_
+
+
+UNKNOWN_COUNT = 0xFFFFFFFFFFFFFFFF  # RB_UNKNOWN_COUNT
+
+
 class RbBitmapSummary(C.Structure):
     _fields_ = [("cardinality", C.c_uint64), ("n_containers", C.c_uint64), ("n_run_containers", C.c_uint64),
                 ("payload_bytes", C.c_uint64), ("size_in_bytes", C.c_uint64)]
@@ -112,6 +119,7 @@ SIGNATURES = {
     "rbgpu_pairwise_cardinality": (C.c_int, [_P, C.c_int, _P, _P, _P, _P, C.c_uint32, _U64P]),
     "rbgpu_pairwise_async": (C.c_int, [_P, C.c_int, _P, _P, _P, _P, C.c_uint32, C.c_void_p, C.POINTER(_P)]),
     "rbgpu_set_wait": (C.c_int, [_P]),
+    "rbgpu_set_device_view": (C.c_int, [_P, C.POINTER(RbDeviceView)]),
     "rbgpu_pairwise_inplace": (C.c_int, [_P, C.c_int, _P, _P, _P, _P, C.c_uint32, C.POINTER(_P)]),
     "rbgpu_set_run_optimize": (C.c_int, [_P, C.POINTER(_P), C.c_void_p]),
     "rbgpu_set_setup_stats": (C.c_int, [_P, C.POINTER(C.c_double), _U64P]),

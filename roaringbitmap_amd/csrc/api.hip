@@ -83,6 +83,7 @@ void ctx_unref(rbgpu_ctx *ctx) {
   for (auto &e : ctx->ev_side) (void)hipEventDestroy(e);
   (void)hipEventDestroy(ctx->ev_tot);
   if (ctx->ev_ext) (void)hipEventDestroy(ctx->ev_ext);
+  if (ctx->ev_seq) (void)hipEventDestroy(ctx->ev_seq);
   (void)hipFree(ctx->d_stats);
   (void)hipHostFree(ctx->h_pinned);
   (void)hipHostFree(ctx->h_stats);
@@ -514,6 +515,48 @@ bool wait_call_seq(rbgpu_ctx *ctx, uint64_t seq) {
     if ((it & 1023u) == 1023u && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(50)) return false;
   }
 }
+int seq_begin(rbgpu_ctx *ctx) {
+  if (ctx->seq_settled >= ctx->seq_recorded) return RB_OK;
+  const hipError_t q = hipEventQuery(ctx->ev_seq);
+  if (q == hipSuccess) {
+    ctx->seq_settled = ctx->seq_recorded;
+    return RB_OK;
+  }
+  if (q == hipErrorNotReady) return RB_OK; // still running: this call's work queues behind it
+  (void)hipGetLastError();
+  return fail(RB_EDEVICE, "an earlier one-launch call's kernel failed after the call returned: %s", hipGetErrorString(q));
+}
+int seq_end(rbgpu_ctx *ctx, uint64_t seq, bool poll, const char *what, bool *seen) {
+  *seen = false;
+  HIPCHK(hipEventRecord(ctx->ev_seq, ctx->stream));
+  ctx->seq_recorded = seq;
+  const bool s = poll && wait_call_seq(ctx, seq);
+  const hipError_t e1 = s ? hipSuccess : hipStreamSynchronize(ctx->stream), e2 = hipGetLastError();
+  if (e1 != hipSuccess || e2 != hipSuccess)
+    return fail(RB_EDEVICE, "%s kernel failed: %s", what, hipGetErrorString(e1 != hipSuccess ? e1 : e2));
+  if (!s) {
+    ctx->seq_settled = seq;
+    const uint64_t got = __atomic_load_n(reinterpret_cast<const uint64_t *>(ctx->h_small) + 5, __ATOMIC_ACQUIRE);
+    if (got != seq) { // no block saw itself last: the counters are not this call's, and nor are the words
+      (void)hipMemsetAsync(ctx->d_small_ctr, 0, 512, ctx->stream);
+      (void)hipStreamSynchronize(ctx->stream);
+      return fail(RB_EDEVICE, "%s: the kernel ended without handing over call %llu's result words (found %llu)", what,
+                  (unsigned long long)seq, (unsigned long long)got);
+    }
+  }
+  *seen = s;
+  return RB_OK;
+}
+int seq_settle(rbgpu_ctx *ctx, uint64_t seq) {
+  if (!seq || seq <= ctx->seq_settled) return RB_OK;
+  const hipError_t e = hipEventSynchronize(ctx->ev_seq); // recorded behind call seq or a later one
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    return fail(RB_EDEVICE, "one-launch kernel failed: %s", hipGetErrorString(e));
+  }
+  ctx->seq_settled = ctx->seq_recorded;
+  return RB_OK;
+}
 } // namespace rbg
 
 // ===================================================================== C ABI
@@ -550,6 +593,7 @@ int rbgpu_open(int device, rbgpu_ctx **out) {
   for (auto &e : c->ev_side) (void)hipEventCreate(&e);
   (void)hipEventCreate(&c->ev_tot);
   (void)hipEventCreateWithFlags(&c->ev_ext, hipEventDisableTiming);
+  (void)hipEventCreateWithFlags(&c->ev_seq, hipEventDisableTiming);
   // every source file's code object now, not inside the first call of each kind: HIP loads a code object at
   // the first launch of one of its kernels (~1 ms each), which otherwise lands in that call's time and in a
   // set's first-use setup (rbgpu_set_setup_parts)
@@ -584,12 +628,15 @@ int rbgpu_get_stats(rbgpu_ctx *ctx, rb_stats *out) {
   if (ctx->stats_pending) { // a small batch returned before its end was signalled: its times now
     ctx->stats_pending = false;
     float ms = 0.f;
-    if (hipEventSynchronize(ctx->ev[5]) == hipSuccess) {
-      if (hipEventElapsedTime(&ms, ctx->ev[0], ctx->ev[5]) == hipSuccess) ctx->last.total_ms = ms;
-      if (ctx->stats_pending_k && hipEventElapsedTime(&ms, ctx->ev[1], ctx->ev[2]) == hipSuccess)
-        ctx->last.kernel_ms[0] = ctx->last.main_kernel_ms = ms;
+    const hipError_t e = hipEventSynchronize(ctx->ev[5]);
+    if (e != hipSuccess) { // the kernel faulted after its last block handed the result over
+      (void)hipGetLastError();
+      return fail(RB_EDEVICE, "the last call's kernel failed after the call returned: %s", hipGetErrorString(e));
     }
-    (void)hipGetLastError();
+    ctx->seq_settled = std::max(ctx->seq_settled, ctx->seq_recorded); // ev[5] follows the last one-launch kernel
+    if (hipEventElapsedTime(&ms, ctx->ev[0], ctx->ev[5]) == hipSuccess) ctx->last.total_ms = ms;
+    if (ctx->stats_pending_k && hipEventElapsedTime(&ms, ctx->ev[1], ctx->ev[2]) == hipSuccess)
+      ctx->last.kernel_ms[0] = ctx->last.main_kernel_ms = ms;
   }
   *out = ctx->last;
   return RB_OK;
@@ -1047,6 +1094,7 @@ static int pairwise_small(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgp
     if (p < np) k += nsub(p, kpw);
   }
   rc = ensure_call_words(ctx);
+  if (!rc) rc = seq_begin(ctx);
   if (rc) return rc;
   uint64_t *hout = reinterpret_cast<uint64_t *>(ctx->h_small);
 
@@ -1112,13 +1160,11 @@ static int pairwise_small(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgp
   HIPCHK(hipEventRecord(ctx->ev[5], st));
   // The last block writes the result words to host memory and then the call's sequence number
   // (wait_call_seq); per-pair cardinalities come back by a copy, so those calls wait for the stream.
-  const bool seen = RBG_SMALL_POLL && !card_out && wait_call_seq(ctx, sa.seq);
-  {
-    const hipError_t e1 = seen ? hipSuccess : hipStreamSynchronize(st), e2 = hipGetLastError();
-    if (e1 != hipSuccess || e2 != hipSuccess) {
-      if (res) rbgpu_set_free(res);
-      return fail(RB_EDEVICE, "small-batch pairwise kernel failed: %s", hipGetErrorString(e1 != hipSuccess ? e1 : e2));
-    }
+  bool seen = false;
+  rc = seq_end(ctx, sa.seq, RBG_SMALL_POLL && !card_out, "small-batch pairwise", &seen);
+  if (rc) {
+    if (res) rbgpu_set_free(res);
+    return rc;
   }
   // the result words, written by the last block straight into host memory
   uint64_t *w = ctx->words;
@@ -1139,6 +1185,7 @@ static int pairwise_small(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgp
   ctx->last.result_containers = nres;
   if (res) {
     res->nc = nres;
+    res->end_seq = seen ? sa.seq : 0;
     *out = res;
   }
   return RB_OK;
@@ -1176,6 +1223,12 @@ int pairwise_impl(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu_set *b
   }
   if (!probe) { // small batches complete before the return, asynchronous call or not
     rc = pairwise_small(ctx, op, a, b, a_idx, b_idx, npairs, out, card_out, inplace, keep_empty);
+    if (rc == RB_OK && ext) {
+      // the host returned on the last block's sequence word, before the kernel's end (and its L2 write-back):
+      // the caller's later work on its stream waits for that end, as after the general path below
+      HIPCHK(hipEventRecord(ctx->ev_ext, ctx->stream));
+      HIPCHK(hipStreamWaitEvent(ext, ctx->ev_ext, 0));
+    }
     if (rc != 1) return rc;
   }
   int slot = -1;
@@ -1504,7 +1557,16 @@ int rbgpu_pairwise_async(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu
 
 int rbgpu_set_wait(const rbgpu_set *s) {
   if (!s) return fail(RB_EINVAL, "null argument");
-  return settle(s);
+  const int rc = settle(s);
+  return rc ? rc : seq_settle(s->ctx, s->end_seq);
+}
+
+int rbgpu_set_device_view(const rbgpu_set *s, rb_device_view *out) {
+  if (!s || !out) return fail(RB_EINVAL, "null argument");
+  if (s->failed) return fail(RB_EDEVICE, "the asynchronous call that produced this set failed");
+  *out = rb_device_view{s->nb, s->pending ? RB_UNKNOWN_COUNT : s->nc, s->payload_bytes, s->begin, s->key, s->type,
+                        s->card, s->nruns, s->off, s->payload};
+  return RB_OK;
 }
 
 int rbgpu_pairwise_cardinality(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgpu_set *b, const uint32_t *a_idx,

@@ -612,12 +612,15 @@ static int ensure_bsi_tables(rbgpu_ctx *ctx, const rbgpu_set *cs, uint32_t nbits
   uint64_t *bt = nullptr, *bts = nullptr;
   if (ctx->pool.alloc((void **)&t, (nbits + 2ull) * 65536 * 4) || ctx->pool.alloc((void **)&kl, 65536 * 4ull) ||
       ctx->pool.alloc((void **)&bt, 65537 * 8ull) || ctx->pool.alloc((void **)&bts, 65537 * 8ull)) {
-    for (void *p : {(void *)t, (void *)kl, (void *)bt}) ctx->pool.release(p);
+    for (void *p : {(void *)t, (void *)kl, (void *)bt, (void *)bts}) ctx->pool.release(p);
     return fail(RB_ENOMEM, "bsi tables");
   }
   {
     DeriveTimer tm(s, 3);
-    HIPCHK(hipMemsetAsync(t, 0xFF, (nbits + 1ull) * 65536 * 4, st));
+    if (hipMemsetAsync(t, 0xFF, (nbits + 1ull) * 65536 * 4, st) != hipSuccess) {
+      for (void *p : {(void *)t, (void *)kl, (void *)bt, (void *)bts}) ctx->pool.release(p);
+      return fail(RB_EDEVICE, "bsi table memset failed");
+    }
     k_bsi_index<<<dim3(64, nbits + 1), 256, 0, st>>>(s->view(), 0, t);
     const int32_t *frow = t + (uint64_t)nbits * 65536;
     k_bsi_active<<<256, 256, 0, st>>>(frow, 0, 65536, bt);
@@ -662,6 +665,7 @@ static int bsi_range_one_launch(rbgpu_ctx *ctx, const rbgpu_set *bsi, const rbgp
                                 rbgpu_set *res) {
   hipStream_t st = ctx->stream;
   int rc = ensure_call_words(ctx);
+  if (!rc) rc = seq_begin(ctx);
   if (rc) return rc;
   uint64_t *kmeta = nullptr;
   if (ctx->pool.alloc((void **)&kmeta, 8ull * nk)) return fail(RB_ENOMEM, "bsi key results");
@@ -674,12 +678,9 @@ static int bsi_range_one_launch(rbgpu_ctx *ctx, const rbgpu_set *bsi, const rbgp
   HIPCHK(hipEventRecord(ctx->ev[2], st));
   HIPCHK(hipEventRecord(ctx->ev[5], st));
   ctx->pool.release(kmeta); // stream-ordered: handed out again only to later work on this stream
-  const bool seen = wait_call_seq(ctx, tl.seq);
-  {
-    const hipError_t e1 = seen ? hipSuccess : hipStreamSynchronize(st), e2 = hipGetLastError();
-    if (e1 != hipSuccess || e2 != hipSuccess)
-      return fail(RB_EDEVICE, "bsi range kernel failed: %s", hipGetErrorString(e1 != hipSuccess ? e1 : e2));
-  }
+  bool seen = false;
+  rc = seq_end(ctx, tl.seq, true, "bsi range", &seen);
+  if (rc) return rc;
   const uint64_t *hout = reinterpret_cast<const uint64_t *>(ctx->h_small);
   uint64_t *w = ctx->words;
   for (int i = 0; i < kStatWords; ++i) w[i] = 0;
@@ -696,6 +697,7 @@ static int bsi_range_one_launch(rbgpu_ctx *ctx, const rbgpu_set *bsi, const rbgp
   ctx->last.result_containers = nres;
   res->nc = nres;
   res->h_begin = {0, nres};
+  res->end_seq = seen ? tl.seq : 0;
   return RB_OK;
 }
 
@@ -715,7 +717,13 @@ int bsi_compare(rbgpu_ctx *ctx, const rbgpu_set *bsi, int op, uint64_t start, ui
     return rc;
   }
   if (sc >= 0) {
-    // all = foundSet == null ? ebM.clone() : and(ebM, foundSet); empty = new bitmap
+    // all = foundSet == null ? ebM.clone() : and(ebM, foundSet); empty = new bitmap.  rb_stats describes this
+    // call's answer (no compare kernel ran: no kernel times), not the previous call's
+    auto shortcut_stats = [&](rbgpu_set *r, uint64_t card) {
+      for (int i = 0; i < kStatWords; ++i) ctx->words[i] = 0;
+      ctx->words[7] = card;
+      return stats_fill(ctx, 0, r->nc, nullptr, 0, false);
+    };
     if (sc == 0) {
       rbgpu_set *e = new rbgpu_set;
       const int rc = set_alloc(ctx, e, 1, 0, 16);
@@ -729,11 +737,21 @@ int bsi_compare(rbgpu_ctx *ctx, const rbgpu_set *bsi, int op, uint64_t start, ui
       LAUNCHCHK();
       e->h_begin = {0, 0};
       *out = e;
-      return RB_OK;
+      return shortcut_stats(e, 0);
     }
-    if (!found) return rbgpu_set_extract(bsi, nbits, 1, out);
+    if (!found) {
+      int rc = rbgpu_set_extract(bsi, nbits, 1, out);
+      uint64_t card = 0;
+      if (!rc) rc = rbgpu_set_cardinalities(*out, &card);
+      if (!rc) rc = shortcut_stats(*out, card);
+      if (rc && *out) {
+        rbgpu_set_free(*out);
+        *out = nullptr;
+      }
+      return rc;
+    }
     const uint32_t ai = nbits, bi = 0;
-    return rbgpu_pairwise(ctx, RB_AND, bsi, found, &ai, &bi, 1, out);
+    return rbgpu_pairwise(ctx, RB_AND, bsi, found, &ai, &bi, 1, out); // its own stats: the AND's answer
   }
   // key -> container tables: rows 0..nbits-1 slices, nbits ebM (the set's, cached), nbits+1 foundSet
   int rc = ensure_bsi_tables(ctx, bsi, nbits);

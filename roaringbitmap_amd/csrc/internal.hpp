@@ -157,6 +157,13 @@ struct rbgpu_ctx {
   uint8_t *h_small = nullptr, *d_small = nullptr; // small-batch result words (host-visible, 64 B)
   uint64_t *d_small_ctr = nullptr;                  // small-batch finished-block count and counters
   uint64_t small_seq = 0;   // small-batch calls launched (the kernel's last block writes it to h_small[5])
+  // A one-launch call returns on its sequence word, before its kernel's end is signalled (and before the
+  // kernel-end release writes other XCDs' payload stores back from their L2s).  ev_seq is recorded behind
+  // the latest such kernel, whose sequence number is seq_recorded; seq_settled is the highest sequence
+  // number known complete.  Later work on `stream` is ordered behind the kernel anyway; a use anywhere
+  // else (a caller's stream, rbgpu_set_wait, rbgpu_set_device_view) waits for ev_seq (seq_settle).
+  hipEvent_t ev_seq = nullptr;
+  uint64_t seq_recorded = 0, seq_settled = 0;
   bool stats_pending = false; // ctx->last's times wait for their events (a small batch returned on h_small[5])
   bool stats_pending_k = false; // ... and the kernel's own pair (RBGPU_SMALL_KERNEL_TIMES)
   rbg::SmallTabInline small_inline{};               // small-batch tables passed in the kernel arguments
@@ -202,6 +209,9 @@ struct rbgpu_set {
   // the last asynchronous call that reads this set as an input completes at `read_done` (its kernels may
   // still read the buffers after the call returned): freeing the set waits for it
   hipEvent_t read_done = nullptr;
+  // written by the one-launch call with this sequence number (0: none): complete for the host's purposes
+  // (nc known), but its kernel may not have ended (rbgpu_ctx::ev_seq)
+  uint64_t end_seq = 0;
   double derive_ms = 0.0;         // device time spent building mrec / krec (reported, not hidden)
   uint64_t derive_bytes = 0;      // their algorithmic bytes (metadata read + records written)
   // per derived item: 0 dense check, 1 mrec, 2 krec, 3 BSI key tables (rbgpu_set_setup_parts)
@@ -226,6 +236,15 @@ void set_release(rbgpu_set *s);
 int ensure_h_begin(const rbgpu_set *s);
 int ensure_call_words(rbgpu_ctx *ctx);
 bool wait_call_seq(rbgpu_ctx *ctx, uint64_t seq);
+// The one-launch hand-off around a kernel whose last block writes the result words and then `seq`:
+// seq_begin surfaces a fault of an earlier one-launch kernel that ended after its call returned
+// (non-blocking); seq_end records ev_seq behind the kernel, waits for the sequence word (else for the
+// stream) and fails with RB_EDEVICE when the words are not this call's — then the finished-block counters
+// are re-zeroed, since no block of the call saw itself last.  seq_settle waits for the kernel
+// end of call `seq` (a no-op once known complete).
+int seq_begin(rbgpu_ctx *ctx);
+int seq_end(rbgpu_ctx *ctx, uint64_t seq, bool poll, const char *what, bool *seen);
+int seq_settle(rbgpu_ctx *ctx, uint64_t seq);
 // Derived metadata (rbgpu_set): built once per set on the set's stream, timed with events so the cost
 // is reported (rbgpu_set_derive_ms), then cached — the set is immutable.  The start event follows an empty
 // dispatch: an event recorded on an idle stream is stamped when the host records it, so it would also time

@@ -662,6 +662,13 @@ constexpr int kXorUnionMinC = 1024; // try a union stretch only above this c (a 
 #ifndef RBG_STUDY
 #define RBG_STUDY 0 // study builds: per-key stretch counts of three keys (printf)
 #endif
+// Study builds (a per-pass counter split): RBG_XOR_DUP = 1 runs every union window's marks +
+// |P \ U'| check twice, 2 its toggles three times, 3 every union flush twice.  Each repeat leaves the result
+// unchanged (OR marks are idempotent, three XOR toggles equal one, a flush of a zeroed image adds nothing), so
+// the kernel's extra time and counters under a variant are that pass's marginal cost at full occupancy.
+#ifndef RBG_XOR_DUP
+#define RBG_XOR_DUP 0
+#endif
 
 __global__ __launch_bounds__(256, 3) void k_wide_runs_xor(SetView s, const uint64_t *__restrict__ rec,
                                                           const uint64_t *__restrict__ seg,
@@ -773,6 +780,8 @@ __global__ __launch_bounds__(256, 3) void k_wide_runs_xor(SetView s, const uint6
               (uint16_t)(__popcll(Pw[2 * k]) | (__popcll(Pw[2 * k + 1]) << 8));
         wave_lds_sync();
       }
+      int L = 0;
+      for (int rep = 0; rep < (RBG_XOR_DUP == 1 ? 2 : 1); ++rep) {
       if (mem) {
         const uint32_t rw[8] = {W.r0.x, W.r0.y, W.r0.z, W.r0.w, W.r1.x, W.r1.y, W.r1.z, W.r1.w};
 #pragma unroll
@@ -809,13 +818,19 @@ __global__ __launch_bounds__(256, 3) void k_wide_runs_xor(SetView s, const uint6
         }
         ls = (ls & 0xFFFFu) + (ls >> 16);
       }
-      const int L = (int)wave_sum_u32(ls);
+      L = (int)wave_sum_u32(ls);
+      if (RBG_XOR_DUP == 1) wave_lds_sync();
+      }
       RBG_TA(0);
       const int rub = X.r + usum + wnr; // >= every r_j of the stretch (Run flavour)
       if (urun ? (2 + 4 * rub <= min(kBitmapBytes, 2 * L + 2)) : L >= kRunArrayThreshold) {
         usum += wnr;
         if (mem) {
           toggle_runs(W, acc);
+          if (RBG_XOR_DUP == 2) {
+            toggle_runs(W, acc);
+            toggle_runs(W, acc);
+          }
           X.inb += 4u * W.nr + 2u + 16u;
         }
         ++upend;
@@ -832,6 +847,7 @@ __global__ __launch_bounds__(256, 3) void k_wide_runs_xor(SetView s, const uint6
         if (upend) {
           RBG_TR(++tr_f);
           flush_union();
+          if (RBG_XOR_DUP == 3) flush_union();
           RBG_TA(2);
           continue;
         }

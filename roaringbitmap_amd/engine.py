@@ -279,6 +279,16 @@ class DeviceSet:
                                                     offs.ctypes.data_as(L._U64P)))
         return offs
 
+    def device_view(self) -> dict:
+        """rbgpu_set_device_view: device addresses of the SoA (never blocks; n_containers is None while an
+        asynchronous result is pending)."""
+        v = L.RbDeviceView()
+        L.check(L.lib().rbgpu_set_device_view(self.h, C.byref(v)))
+        d = {f: getattr(v, f) or 0 for f, _ in L.RbDeviceView._fields_}
+        if d["n_containers"] == L.UNKNOWN_COUNT:
+            d["n_containers"] = None
+        return d
+
     def wait(self) -> "DeviceSet":
         """rbgpu_set_wait: an asynchronous result complete (no-op otherwise)."""
         L.check(L.lib().rbgpu_set_wait(self.h))

@@ -83,6 +83,68 @@ def test_async_caller_stream_and_small_batch(ctx, pairs, oracle):
         assert got[i] == oracle.op(rb.AND, refs[i], refs[i + 1]).serialize()
 
 
+def _hip():
+    import ctypes
+    for name in ("libamdhip64.so", "/opt/rocm/lib/libamdhip64.so"):
+        try:
+            h = ctypes.CDLL(name)
+        except OSError:
+            continue
+        h.hipMemcpyAsync.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p]
+        h.hipMemcpyAsync.restype = ctypes.c_int
+        return h
+    raise RuntimeError("libamdhip64 not found")
+
+
+def test_async_small_batch_caller_stream_consumer(ctx, oracle):
+    """a <= 4096-pair batch returns on its last block's sequence word, before the kernel's end
+    is signalled; the caller's stream must still see the complete result.  The consumer is device work on the
+    caller's torch stream only (copies out of the result's HBM addresses from rbgpu_set_device_view, then torch
+    kernels over them), queued right behind the call and read with nothing but that stream's own
+    synchronisation; every container's metadata and payload equals the oracle's result."""
+    import torch
+
+    import roaringbitmap_amd as rb
+    from roaringbitmap_amd.engine import HostSoA
+    hip = _hip()
+    bms = synthetic_bitmaps(64, seed=11)
+    small = ctx.upload_values(bms, run_optimize=True)
+    refs = [oracle.RefBitmap.deserialize(x) for x in small.serialize()]
+    ai = np.arange(63, dtype=np.uint32)
+    dev = torch.device("cuda", ctx.device)
+    s = torch.cuda.Stream(device=dev)
+    for rep, op in enumerate((rb.OR, rb.XOR, rb.AND, rb.ANDNOT, rb.OR)):
+        with torch.cuda.stream(s):  # earlier work on the caller's stream: the call runs after it
+            busy = torch.ones(1 << 22, device=dev).cumsum(0)
+        r = ctx.pairwise_async(op, small, small, ai, ai + 1, stream=s.cuda_stream)
+        v = r.device_view()
+        nc = v["n_containers"]
+        assert nc is not None  # the small path knows its count at the return
+        with torch.cuda.stream(s):
+            out = {}
+            for f, dt, n in (("begin", torch.int64, 64), ("key", torch.int16, nc), ("type", torch.uint8, nc),
+                             ("card", torch.int32, nc), ("nruns", torch.int16, nc), ("offset", torch.int64, nc),
+                             ("payload", torch.uint8, int(v["payload_bytes"]))):
+                t = torch.empty(max(n, 1), dtype=dt, device=dev)
+                nbytes = n * t.element_size()
+                if nbytes:
+                    assert hip.hipMemcpyAsync(t.data_ptr(), v[f], nbytes, 3, s.cuda_stream) == 0
+                out[f] = t[:n]
+            # a torch kernel over the payload on the same stream (reads what the copies brought over)
+            chk = out["payload"].to(torch.int64).sum()
+            host = {f: t.to("cpu", non_blocking=False) for f, t in out.items()}
+        assert int(chk.item()) == int(host["payload"].to(torch.int64).sum())
+        h = HostSoA(begin=host["begin"].numpy().view(np.uint64)[:64].copy(),
+                    key=host["key"].numpy().view(np.uint16), type=host["type"].numpy(),
+                    card=host["card"].numpy().view(np.uint32), nruns=host["nruns"].numpy().view(np.uint16),
+                    offset=host["offset"].numpy().view(np.uint64), payload=host["payload"].numpy())
+        want = [oracle.op(op, refs[i], refs[i + 1]).serialize() for i in range(63)]
+        got = ctx.upload_soa(h).serialize()
+        assert got == want, (rep, op)
+        del busy
+        r.close()
+
+
 def _digest(s):
     """Per-bitmap cardinalities and serialized sizes, container type counts, and the bytes of three
     1000-bitmap windows (head, middle, tail: the tail's tasks run last in the task kernels)."""

@@ -150,9 +150,15 @@ def test_bsi_range_one_launch_handoff(ctx, oracle):
         st = ctx.stats()
         want = oracle.bsi_compare(rsl, rebm, rb.BSI_RANGE, lo, hi, f_ref, int(mn), int(mx))
         assert r.serialize()[0] == want.serialize(), (it, lo, hi)
+        assert st["result_cardinality"] == want.cardinality()  # the shortcut's answer too
+        assert st["result_containers"] == r.n_containers
         if (lo, hi) != (int(mn), int(mx)):  # (the whole value range is compareUsingMinMax's shortcut: no kernel)
-            assert st["result_cardinality"] == want.cardinality()
             assert st["total_ms"] > 0.0 and st["main_kernel_ms"] > 0.0
+        else:
+            assert st["tasks"] == 0
+        r.wait()  # the one-launch kernel's end (rbgpu_set_wait), then its SoA through the device view
+        v = r.device_view()
+        assert v["n_containers"] == r.n_containers and v["n_bitmaps"] == 1
         for op in (rb.AND, rb.OR):  # small batches on the same context between the compares
             got = ctx.pairwise(op, p, p, [0, 1, 2], [1, 2, 3]).serialize()
             assert got == [oracle.op(op, prefs[i], prefs[i + 1]).serialize() for i in range(3)]

@@ -142,6 +142,38 @@ def test_bsi_known_answers(oracle):
     assert len(q(R.BSI_EQ, 1, s=eq)) == 50
 
 
+def test_bsi_cpp_twin_matches_restatement(oracle):
+    """rbref_bsi_compare (C++, the BSI CPU baseline's engine) gives the Python restatement's bytes — itself pinned
+    by R64BSITest's known answers above — for every operation, with and without a foundSet, across the min/max
+    shortcut's edges; rbref_bsi_compare_keys' total over per-key indexes is the same at 1 and 4 threads."""
+    R = oracle
+    rng = np.random.default_rng(21)
+    for trial in range(4):
+        n = int(rng.integers(50, 40000))
+        cols = rng.integers(0, 1 << 18, n)
+        vals = rng.integers(0, 1 << int(rng.integers(3, 40)), n, dtype=np.uint64)
+        sl, ebm, mn, mx = R.bsi_build(cols, vals)
+        found = R.RefBitmap.of(np.unique(rng.integers(0, 1 << 18, 3000)).astype(np.uint32))
+        for op in range(7):
+            for a, b in ((mn, mx), (mn - 1 if mn else 0, mx + 1), (int(vals[0]), int(vals[-1])),
+                         (int(rng.integers(mn, mx + 1)), int(rng.integers(mn, mx + 1))), (mx + 1, mx + 5)):
+                lo, hi = min(a, b), max(a, b)
+                for f in (None, found):
+                    want = R.bsi_compare(sl, ebm, op, lo, hi, f, mn, mx).serialize()
+                    assert R.bsi_compare_cpp(sl, ebm, op, lo, hi, f, mn, mx).serialize() == want, (trial, op, lo, hi)
+    per_key = []
+    for k in range(6):
+        cols = rng.integers(0, 65536, 5000)
+        vals = rng.integers(0, 1 << 20, 5000, dtype=np.uint64)
+        sl, ebm, _, _ = R.bsi_build(cols, vals)
+        sl = sl + [R.RefBitmap.of(np.zeros(0, np.uint32))] * (20 - len(sl))  # one slice count for every key
+        per_key.append((sl, ebm))
+    want = sum(R.bsi_compare(sl, eb, R.BSI_RANGE, 1000, 600000, None, 0, (1 << 20) - 1).cardinality()
+               for sl, eb in per_key)
+    for th in (1, 4):
+        assert R.bsi_compare_keys(per_key, R.BSI_RANGE, 1000, 600000, 0, (1 << 20) - 1, th) == want
+
+
 @pytest.mark.parametrize("sem", ["FAST_OR", "FAST_AND", "WORKSHY_AND", "FAST_XOR", "PAR_OR", "PAR_XOR"])
 def test_key_parallel_restatement_matches(oracle, sem):
     """rbref_wide_mt (the all-cores CPU baseline) gives the single-threaded oracle's bytes for every
