@@ -13,6 +13,7 @@ SETS=("SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_
       "FETCH_SIZE"
       "WRITE_SIZE")
 libs=("base" "${@}")
+O=${PMC_OUT:-$O}
 for v in "${libs[@]}"; do
   if [ "$v" = base ]; then unset RBGPU_LIB; else export RBGPU_LIB=$PWD/abvar/$v/librbgpu.so; fi
   i=0
