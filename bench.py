@@ -40,7 +40,7 @@ OPS = ["AND", "OR", "XOR", "ANDNOT"]
 
 
 def _traffic_json():
-    for rnd in ("r05", "r03", "r02", "r01"):
+    for rnd in ("r06", "r05", "r03", "r02", "r01"):
         p = os.path.join(ROOT, "profiles", rnd, "traffic.json")
         if os.path.exists(p):
             return p
@@ -635,9 +635,13 @@ WIDE_WORKLOADS = {
 # the all-core CPU baseline of each wide semantic: ParallelAggregation where the reference has one,
 # else the same per-key semantic key-parallel (oracle rbref_wide_mt)
 WIDE_PARALLEL = {"FAST_OR": "PAR_OR", "FAST_XOR": "PAR_XOR", "FAST_AND": "FAST_AND"}
-# the derived per-set items (rbgpu_set_setup_parts) each wide path builds on a fresh set
-WIDE_SETUP_PARTS = {"FAST_OR": ("dense_check",), "FAST_AND": ("dense_check", "mrec"),
+# the derived per-set items (rbgpu_set_setup_parts) each wide path builds on a fresh set (workShyAnd reads the
+# set's own run counts and offsets since round 6: no packed records)
+WIDE_SETUP_PARTS = {"FAST_OR": ("dense_check",), "FAST_AND": ("dense_check",),
                     "FAST_XOR": ("dense_check", "krec")}
+# bytes per container a config-4 kernel must read besides the payload arena (at least once per launch):
+# naive_xor its key-major 8-B record, workShyAnd the u16 run count and the u64 payload offset
+WIDE_META_BYTES = {"FAST_XOR": 8, "FAST_AND": 10}
 
 
 def run_wide(args, name, D, ctx, rb, nbitmaps, steps, warmup, a=None):
@@ -696,6 +700,15 @@ def run_wide(args, name, D, ctx, rb, nbitmaps, steps, warmup, a=None):
                            else "torch.distributed (ShardedWide)")) if D.world > 1 else "single GPU",
         "roofline": roofline(last["main_kernel"], k_ms, k_bytes, pmc_traffic(pmc_name), D),
     }
+    if sem_name in WIDE_META_BYTES:
+        # the traffic calibration's known byte count: every metadata record and every payload
+        # byte of the set must come from HBM at least once per launch (the arena is GBs, far past the 256 MiB
+        # Infinity Cache), plus the results written; the PMC figure is checked against it
+        prov = WIDE_META_BYTES[sem_name] * local_conts + a.payload_capacity
+        rl = out["roofline"]
+        rl["provable_min_read_bytes"] = int(prov)
+        if rl.get("traffic"):
+            rl["traffic_vs_provable_read"] = round(rl["traffic"] / prov, 3)
     # the per-set metadata the kernels derived on the set's first use (outside the timed steps; a caller
     # that uploads a fresh set per call pays it once per set): the items this line's path needs on a fresh set
     parts = a.setup_parts()
@@ -703,9 +716,9 @@ def run_wide(args, name, D, ctx, rb, nbitmaps, steps, warmup, a=None):
     su = {"ms": round(sum(parts[k]["ms"] for k in need), 4), "bytes": sum(parts[k]["bytes"] for k in need)}
     out["setup"] = {"ms": su["ms"], "bytes": su["bytes"], "parts": {k: parts[k] for k in need},
                     "what": "rbgpu_set_setup_parts of this rank's set: the derived metadata this path builds on a "
-                            "fresh set (dense-layout check; workShyAnd: packed 8-B container records, k_pack_records; "
-                            "naive_xor: key-major records straight from the set's metadata, k_records_direct), once "
-                            "per set before the warmup step, not inside the timed steps"}
+                            "fresh set (dense-layout check; naive_xor: key-major 8-B records straight from the set's "
+                            "metadata, k_records_direct2; workShyAnd reads the set's own metadata and builds none), "
+                            "once per set before the warmup step, not inside the timed steps"}
     # what a caller that uploads a fresh set for every call pays (the reference builds its per-call state each
     # time: FastAggregation.java:356-396, 576-582): the step plus this path's setup, max over ranks
     su_ms = D.reduce([float(su["ms"])], "max")[0]

@@ -163,6 +163,11 @@ int rbgpu_set_from_soa(rbgpu_ctx *ctx, const rb_soa *soa, rbgpu_set **out);
 void rbgpu_set_free(rbgpu_set *set);
 uint32_t rbgpu_set_bitmap_count(const rbgpu_set *set);
 uint64_t rbgpu_set_container_count(const rbgpu_set *set);
+/* Bytes of the set's payload arena in HBM (every container payload padded to 16 B; a result set's arena also
+ * holds its slots' padding).  What a kernel reading every payload once must fetch at least — the bench's
+ * provable-minimum traffic for the config-4 lines (no Java counterpart: RoaringBitmap.getSizeInBytes counts
+ * the serialized sizes, rbgpu_set_summaries). */
+uint64_t rbgpu_set_payload_capacity(const rbgpu_set *set);
 /* RoaringBitmap.getCardinality per bitmap (computed on device). */
 int rbgpu_set_cardinalities(const rbgpu_set *set, uint64_t *out /* [n_bitmaps] */);
 /* RoaringBitmap.serializedSizeInBytes per bitmap — RoaringArray.java:947-953 */

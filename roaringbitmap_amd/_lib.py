@@ -109,6 +109,7 @@ SIGNATURES = {
     "rbgpu_set_free": (None, [_P]),
     "rbgpu_set_bitmap_count": (C.c_uint32, [_P]),
     "rbgpu_set_container_count": (C.c_uint64, [_P]),
+    "rbgpu_set_payload_capacity": (C.c_uint64, [_P]),
     "rbgpu_set_cardinalities": (C.c_int, [_P, _U64P]),
     "rbgpu_set_serialized_sizes": (C.c_int, [_P, _U64P]),
     "rbgpu_set_serialize": (C.c_int, [_P, C.c_uint32, C.c_uint32, C.c_void_p, C.c_uint64, _U64P]),

@@ -135,6 +135,16 @@ template <class T, class Cmp> struct JavaHeap {
   }
 };
 
+// A compute-phase kernel span of a call's accounting (stats_end / stats_fill): kernels k = 0..n-1 ran between
+// events ev[1+k] and ev[2+k] unless the span names its own (e0, e1); its algorithmic bytes are the counters
+// in_word + out_word (+ in2 + out2: a concurrent pair), -1 = none.
+struct KernelSpan {
+  const char *name;
+  int in_word, out_word;
+  uint64_t items;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  int in2 = -1, out2 = -1;
+};
 } // namespace rbg
 
 struct rbgpu_ctx {
@@ -154,7 +164,8 @@ struct rbgpu_ctx {
   size_t h_stage_cap = 0;
   // host memory the GPU reads and writes directly (pinned, mapped, coherent): the small-batch
   // pairwise call's arguments and result words, so that call needs no copy engine
-  uint8_t *h_small = nullptr, *d_small = nullptr; // small-batch result words (host-visible, 64 B)
+  uint8_t *h_small = nullptr, *d_small = nullptr; // one-launch result words (host-visible, 256 B: [0, 8) small batches
+                                                  // and BSI RANGE, [kTailWord, +10) the general pipeline's tail)
   uint64_t *d_small_ctr = nullptr;                  // small-batch finished-block count and counters
   uint64_t small_seq = 0;   // small-batch calls launched (the kernel's last block writes it to h_small[5])
   // A one-launch call returns on its sequence word, before its kernel's end is signalled (and before the
@@ -164,6 +175,11 @@ struct rbgpu_ctx {
   // else (a caller's stream, rbgpu_set_wait, rbgpu_set_device_view) waits for ev_seq (seq_settle).
   hipEvent_t ev_seq = nullptr;
   uint64_t seq_recorded = 0, seq_settled = 0;
+  // a general-pipeline call that returned on its compaction's tail (CallTail): its kernel spans, timed when the
+  // stats are asked for (rbgpu_get_stats; 0 = none pending)
+  rbg::KernelSpan pend_spans[4];
+  int pend_n = 0;
+  uint64_t pend_tasks = 0;
   bool stats_pending = false; // ctx->last's times wait for their events (a small batch returned on h_small[5])
   bool stats_pending_k = false; // ... and the kernel's own pair (RBGPU_SMALL_KERNEL_TIMES)
   rbg::SmallTabInline small_inline{};               // small-batch tables passed in the kernel arguments
@@ -235,7 +251,7 @@ void ctx_unref(rbgpu_ctx *ctx);
 void set_release(rbgpu_set *s);
 int ensure_h_begin(const rbgpu_set *s);
 int ensure_call_words(rbgpu_ctx *ctx);
-bool wait_call_seq(rbgpu_ctx *ctx, uint64_t seq);
+bool wait_call_seq(rbgpu_ctx *ctx, uint64_t seq, int word = 5);
 // The one-launch hand-off around a kernel whose last block writes the result words and then `seq`:
 // seq_begin surfaces a fault of an earlier one-launch kernel that ended after its call returned
 // (non-blocking); seq_end records ev_seq behind the kernel, waits for the sequence word (else for the
@@ -243,7 +259,7 @@ bool wait_call_seq(rbgpu_ctx *ctx, uint64_t seq);
 // are re-zeroed, since no block of the call saw itself last.  seq_settle waits for the kernel
 // end of call `seq` (a no-op once known complete).
 int seq_begin(rbgpu_ctx *ctx);
-int seq_end(rbgpu_ctx *ctx, uint64_t seq, bool poll, const char *what, bool *seen);
+int seq_end(rbgpu_ctx *ctx, uint64_t seq, bool poll, const char *what, bool *seen, int word = 5);
 int seq_settle(rbgpu_ctx *ctx, uint64_t seq);
 // Derived metadata (rbgpu_set): built once per set on the set's stream, timed with events so the cost
 // is reported (rbgpu_set_derive_ms), then cached — the set is immutable.  The start event follows an empty
@@ -293,13 +309,6 @@ void stats_begin(rbgpu_ctx *ctx, bool zero = true);
 // Compute-phase kernels k = 0..n-1 ran between events ev[1+k] and ev[2+k]; their algorithmic
 // bytes are d_stats[in_word[k]] + d_stats[out_word[k]] (-1: none).
 // A span may name its own events (e0, e1) and two more byte words (in2, out2: a concurrent pair).
-struct KernelSpan {
-  const char *name;
-  int in_word, out_word;
-  uint64_t items;
-  hipEvent_t e0 = nullptr, e1 = nullptr;
-  int in2 = -1, out2 = -1;
-};
 // d_src: the counters (default ctx->d_stats)
 int stats_end(rbgpu_ctx *ctx, uint64_t tasks, uint64_t result_containers, const KernelSpan *k, int n,
               const uint64_t *d_src = nullptr);

@@ -2,6 +2,11 @@
 #pragma once
 #include "common.hpp"
 
+// workShyAnd's run fast path reads the set's SoA metadata directly instead of packed per-set records (mrec):
+// no setup pass on a fresh set (wide_runs.hip AndRec)
+#ifndef RBG_AND_SOA
+#define RBG_AND_SOA 1 // study builds: 0 packs the set's records (mrec) on its first workShyAnd and reads those
+#endif
 namespace rbg {
 
 // ---- scan.hip
@@ -114,9 +119,18 @@ void launch_probe(int op, int mode, const uint8_t *pa, const uint8_t *pb, uint64
 // segment's first result index to rseg and / or rbegin (either may be null)
 void launch_compact_count(const uint64_t *task_begin, uint64_t nseg, const uint8_t *ttype, uint64_t *bk,
                           hipStream_t st);
+// The compaction's one-launch tail (round 6, VERDICT r05 #2a): the last block to finish sums the call's
+// striped counters, zeroes them for the next call and writes the sums and then `seq` (system-scope release)
+// to host-visible words, so the host returns on them instead of a counters copy, a memset and a stream wait.
+struct CallTail {
+  uint64_t *ctr;   // finished-block count (reset by the last block)
+  uint64_t *hout;  // host-visible words: [0, kStatWords) the summed counters, [kStatWords] = seq; null: no tail
+  uint64_t seq;
+};
+constexpr int kTailWord = 16; // the general pipeline's words in the context's host-visible block (after the small path's)
 void launch_compact_write(const uint64_t *task_begin, uint64_t nseg, const TaskMeta &tm, const uint64_t *bks,
                           const OutView &out, const uint32_t *seg_pair, uint64_t *pair_card, uint64_t *stats,
-                          uint64_t *rseg, uint64_t *rbegin, hipStream_t st);
+                          uint64_t *rseg, uint64_t *rbegin, hipStream_t st, const CallTail &tail = CallTail{});
 
 // small batches (<= kSmallPairs pairs, <= kSmallPairKeys keys per pair, <= kSmallSlots merged keys in
 // all): ONE kernel per call computes every pair into one 8 KiB slot per merged key, and its last block to

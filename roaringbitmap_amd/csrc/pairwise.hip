@@ -1220,7 +1220,8 @@ __global__ __launch_bounds__(kPairThreads) void k_compact_count(const uint64_t *
 __global__ __launch_bounds__(kPairThreads) void k_compact_write(const uint64_t *tb, uint64_t nseg, TaskMeta tm,
                                                                 const uint64_t *bks, OutView out,
                                                                 const uint32_t *seg_pair, uint64_t *pair_card,
-                                                                uint64_t *stats, uint64_t *rseg, uint64_t *rbegin) {
+                                                                uint64_t *stats, uint64_t *rseg, uint64_t *rbegin,
+                                                                CallTail tail) {
   __shared__ uint32_t wtot[kPairThreads / 64];
   const uint64_t b0 = (uint64_t)blockIdx.x * kPairThreads, be = min(b0 + kPairThreads, nseg);
   const uint64_t p = b0 + threadIdx.x;
@@ -1294,6 +1295,30 @@ __global__ __launch_bounds__(kPairThreads) void k_compact_write(const uint64_t *
     const int words[4] = {1, 4, 5, 7};
     const uint64_t vals[4] = {outb[0] + outb[1], outb[0], outb[1], card_sum};
     stat_add_block(stats, words, vals);
+  }
+  if (!tail.hout) return;
+  // ---- the last block to finish hands the call's counters to the host (the hand-off of wave.hpp st_sc1):
+  //      every thread's stores and atomics done, then one agent-scope add per block
+  __shared__ uint32_t s_last;
+  __shared__ uint64_t s_sum[kStatWords];
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0)
+    s_last = __hip_atomic_fetch_add(tail.ctr, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1ull;
+  __syncthreads();
+  if (!s_last) return;
+  static_assert(kStripes == 64, "a wave sums one counter's stripes");
+  const int lane = lane_id(), wv = threadIdx.x >> 6;
+  for (int w = wv; w < kStatWords; w += kPairThreads / 64) { // the other blocks' atomics live in L2: sc1 loads
+    const uint64_t x = wave_sum_u64(ld_sc1(stats + w * kStripes + lane));
+    stats[w * kStripes + lane] = 0ull; // zeroed for the next call (stream order: its kernels start after this one)
+    if (lane == 0) s_sum[w] = x;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 0; w < kStatWords; ++w) tail.hout[w] = s_sum[w];
+    __hip_atomic_store(tail.ctr, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); // ready for the next call
+    __hip_atomic_store(tail.hout + kStatWords, tail.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
 
@@ -1445,10 +1470,11 @@ void launch_compact_count(const uint64_t *task_begin, uint64_t nseg, const uint8
 }
 void launch_compact_write(const uint64_t *task_begin, uint64_t nseg, const TaskMeta &tm, const uint64_t *bks,
                           const OutView &out, const uint32_t *seg_pair, uint64_t *pair_card, uint64_t *stats,
-                          uint64_t *rseg, uint64_t *rbegin, hipStream_t st) {
+                          uint64_t *rseg, uint64_t *rbegin, hipStream_t st, const CallTail &tail) {
   if (!nseg) return;
   k_compact_write<<<blocks_for(nseg, kPairThreads), kPairThreads, 0, st>>>(task_begin, nseg, tm, bks, out,
-                                                                           seg_pair, pair_card, stats, rseg, rbegin);
+                                                                           seg_pair, pair_card, stats, rseg, rbegin,
+                                                                           tail);
 }
 
 // ---------------------------------------------------------------- small batches: two launches

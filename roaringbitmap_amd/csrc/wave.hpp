@@ -298,7 +298,13 @@ __device__ __forceinline__ uint32_t block_xscan(uint32_t v, uint32_t *wtot, uint
 }
 // Cross-block hand-off (MI355X_MICROARCH.md, inter-workgroup visibility, first table row): every block's
 // words and counters are stored sc1, each storing wave waits for them (s_waitcnt vmcnt(0)), then one
-// agent-scope add per block; the block whose add comes last reads them with sc1 loads.
+// agent-scope add per block; the block whose add comes last reads them with sc1 loads.  This leans on the
+// gfx94x / gfx95x meaning of sc1 (relaxed agent-scope atomics go to the device-coherent L2) and on vmcnt
+// covering stores and no-return atomics — not on the HIP memory model's release / acquire pairs:
+// other targets are refused at compile time rather than given a hand-off that could read stale words.
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__) && !defined(__gfx942__)
+#error "the one-launch hand-off (st_sc1 / ld_sc1 + s_waitcnt vmcnt) is written for gfx942 / gfx950"
+#endif
 __device__ __forceinline__ void st_sc1(uint64_t *p, uint64_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }

@@ -670,7 +670,7 @@ int wide_run(rbgpu_ctx *ctx, int sem, const rbgpu_set *in, const std::vector<uin
     // (a dense set's krec is built from its SoA when it has no mrec: naive_xor then never needs mrec)
     if (in->payload_bytes >= kRecMaxPayload) fast_ok = false;
     else if (sem == RB_FAST_XOR && dense && identity) fast_ok = !ensure_krec(in);
-    else if (ensure_mrec(in)) fast_ok = false;
+    else if (!(RBG_AND_SOA && sem == RB_WORKSHY_AND) && ensure_mrec(in)) fast_ok = false;
   }
   (void)hipGetLastError();
 

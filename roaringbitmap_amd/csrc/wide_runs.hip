@@ -269,7 +269,35 @@ __device__ __forceinline__ int and_slot(int b, int k, int lane) { return (b * kA
 __device__ __forceinline__ uint32_t iv_s(uint32_t x) { return x & 0xFFFF; }
 __device__ __forceinline__ uint32_t iv_e(uint32_t x) { return x >> 16; }
 
-template <int KB, bool DENSE>
+// A member's record at step t: the packed 8-B mrec record (when the set already has one), or (SOA, the
+// default since round 6) the set's own run-count / offset arrays read directly: no per-set record pass, so a
+// fresh set pays nothing before the call (config 4: kernel 1.64 ms + a 1.14-ms k_pack_records
+// on a fresh set -> 1.93 ms with the type load, profiles/r06/and).  Raw loaded values; the fields are taken
+// apart only where a step uses them.
+template <bool SOA> struct AndRec;
+template <> struct AndRec<false> {
+  uint64_t r;
+  __device__ __forceinline__ void load(const SetView &, const uint64_t *mrec, uint64_t id) { r = mrec[id]; }
+  __device__ __forceinline__ uint32_t typ() const { return rec_type(r); }
+  __device__ __forceinline__ uint32_t nr() const { return rec_nruns(r); }
+  __device__ __forceinline__ uint64_t off() const { return rec_off(r); }
+};
+// (no type load: a container has a run count > 0 exactly when it is a Run — the SoA stores 0 for the others —
+// and any other type routes the key, so "not a Run" is all the step needs)
+template <> struct AndRec<true> {
+  uint32_t n;
+  uint64_t o;
+  __device__ __forceinline__ void load(const SetView &s, const uint64_t *, uint64_t id) {
+    n = s.nruns[id];
+    o = s.off[id];
+  }
+  __device__ __forceinline__ uint32_t typ() const { return n ? (uint32_t)kRun : (uint32_t)kArray; }
+  // the packed record's nruns field saturates at 15: the same test (> kMaxRunsFast routes the key)
+  __device__ __forceinline__ uint32_t nr() const { return min(n, 15u); }
+  __device__ __forceinline__ uint64_t off() const { return o; }
+};
+
+template <int KB, bool DENSE, bool SOA>
 __global__ __launch_bounds__(256) void k_wide_runs_and(SetView s, const uint64_t *__restrict__ mrec, CidMap cm,
                                                        const uint64_t *__restrict__ seg, const uint32_t *__restrict__ klist,
                                                        uint32_t nk, uint8_t *__restrict__ out, WideOut wo,
@@ -319,12 +347,12 @@ __global__ __launch_bounds__(256) void k_wide_runs_and(SetView s, const uint64_t
       else return cm.cid[blo + m];
     };
     const uint32_t cadd = DENSE ? bkey : 0u;
-    auto ld_runs = [&](uint64_t r) -> AndRuns { // a non-Run record reads the arena's first 16 B instead
-      const bool runs = rec_type(r) == (uint32_t)kRun && rec_nruns(r) <= (uint32_t)kMaxRunsFast;
-      const uint4 *pp = reinterpret_cast<const uint4 *>(s.payload + (runs ? rec_off(r) : 0ull));
+    auto ld_runs = [&](const AndRec<SOA> &r) -> AndRuns { // a non-Run record reads the arena's first 16 B instead
+      const bool runs = r.typ() == (uint32_t)kRun && r.nr() <= (uint32_t)kMaxRunsFast;
+      const uint4 *pp = reinterpret_cast<const uint4 *>(s.payload + (runs ? r.off() : 0ull));
       AndRuns p;
       p.r0 = pp[0];
-      p.r1 = pp[runs && rec_nruns(r) > 4u ? 1 : 0];
+      p.r1 = pp[runs && r.nr() > 4u ? 1 : 0];
       return p;
     };
     // Rings indexed modulo their length, the loop unrolled over kAndU steps so every slot index is a
@@ -333,10 +361,12 @@ __global__ __launch_bounds__(256) void k_wide_runs_and(SetView s, const uint64_t
     // t + i (i < Dp + Dr), C[t % Dc] = id of t + Dp + Dr.  (The runs a step reads were requested at the
     // end of step t - Dp: Dp - 1 whole steps earlier.)
     AndRuns P[kAndDp];
-    uint64_t R[kAndDp + kAndDr];
+    AndRec<SOA> R[kAndDp + kAndDr];
     uint32_t C[kAndDc];
 #pragma unroll
-    for (int i = 0; i < kAndDp + kAndDr; ++i) R[i] = mrec[ld_cid((uint32_t)i) + cadd];
+    // container ids are u32 and a dense member's base is biased by -dense_lo: the sum wraps in 32 bits (a
+    // 64-bit sum of the raw id and the key pointed past the arrays of a key-range shard)
+    for (int i = 0; i < kAndDp + kAndDr; ++i) R[i].load(s, mrec, (uint32_t)(ld_cid((uint32_t)i) + cadd));
 #pragma unroll
     for (int i = 0; i < kAndDc; ++i) C[i] = ld_cid((uint32_t)(kAndDp + kAndDr + i));
 #pragma unroll
@@ -345,8 +375,8 @@ __global__ __launch_bounds__(256) void k_wide_runs_and(SetView s, const uint64_t
 #pragma unroll
       for (int j = 0; j < kAndU; ++j) {
         const uint32_t t = t0 + (uint32_t)j;
-        const uint64_t rt = R[j % (kAndDp + kAndDr)];
-        const AndMeta mt{rec_type(rt), rec_nruns(rt)};
+        const AndRec<SOA> &rt = R[j % (kAndDp + kAndDr)];
+        const AndMeta mt{rt.typ(), rt.nr()};
         const AndRuns &pt = P[j % kAndDp];
         if (t < cnt && !bad) {
           if (mt.typ != kRun || mt.nr > (uint32_t)kMaxRunsFast) {
@@ -418,7 +448,7 @@ __global__ __launch_bounds__(256) void k_wide_runs_and(SetView s, const uint64_t
         // loop's back edge, which waits for the loads)
         __builtin_amdgcn_sched_barrier(0);
         P[j % kAndDp] = ld_runs(R[(j + kAndDp) % (kAndDp + kAndDr)]); // record loaded kAndDr steps ago
-        R[j % (kAndDp + kAndDr)] = mrec[C[j % kAndDc] + cadd];        // id loaded kAndDc steps ago
+        R[j % (kAndDp + kAndDr)].load(s, mrec, (uint32_t)(C[j % kAndDc] + cadd)); // id loaded kAndDc steps ago
         C[j % kAndDc] = ld_cid(t + (uint32_t)(kAndDp + kAndDr + kAndDc));
       }
       // every lane's list empty (or routed): the remaining containers change nothing
@@ -526,12 +556,16 @@ bool launch_wide_runs(int sem, const SetView &s, const uint64_t *mrec, const Cid
   switch (sem) {
   case RB_FAST_OR: k_wide_runs<RB_FAST_OR><<<g, 256, 0, st>>>(s, cm, seg, klist, nk, out, wo, route, stats); return true;
   case RB_WORKSHY_AND: {
-    if (!mrec) return false;
-    const unsigned waves = (nk + kAndKeys - 1) / kAndKeys;
-    if (cm.cid)
-      k_wide_runs_and<kAndKeys, false><<<(waves + 3) / 4, 256, 0, st>>>(s, mrec, cm, seg, klist, nk, out, wo, route, stats);
-    else
-      k_wide_runs_and<kAndKeys, true><<<(waves + 3) / 4, 256, 0, st>>>(s, mrec, cm, seg, klist, nk, out, wo, route, stats);
+    // no mrec: the SoA-reading kernel (RBG_AND_SOA builds, wide.hip then builds no records)
+    if (!mrec && !RBG_AND_SOA) return false;
+    const unsigned waves = (nk + kAndKeys - 1) / kAndKeys, gb = (waves + 3) / 4;
+    if (cm.cid) {
+      if (mrec) k_wide_runs_and<kAndKeys, false, false><<<gb, 256, 0, st>>>(s, mrec, cm, seg, klist, nk, out, wo, route, stats);
+      else k_wide_runs_and<kAndKeys, false, true><<<gb, 256, 0, st>>>(s, mrec, cm, seg, klist, nk, out, wo, route, stats);
+    } else {
+      if (mrec) k_wide_runs_and<kAndKeys, true, false><<<gb, 256, 0, st>>>(s, mrec, cm, seg, klist, nk, out, wo, route, stats);
+      else k_wide_runs_and<kAndKeys, true, true><<<gb, 256, 0, st>>>(s, mrec, cm, seg, klist, nk, out, wo, route, stats);
+    }
     return true;
   }
   case RB_FAST_XOR: // batch-parallel metrics over key-major records (wide_xor.hip)

@@ -549,6 +549,7 @@ struct XWin { // one container per lane: the fast-forward window
   uint32_t typ, card, nr;
   uint4 r0, r1;
   uint32_t pairx; // even lanes: |C_lane ⊕ C_lane+1| (set by pair_xor)
+  uint32_t best;  // the lane's longest run, start | (len - 1) << 16 (set by pair_xor)
 };
 // A window's loads form a chain (record -> run list), so they are software-pipelined over three windows:
 // the records of window w+2 and the runs of w+1 are in flight while window w is processed, and every
@@ -594,6 +595,7 @@ __device__ __forceinline__ XWin xwin_from(const SetView &s, const XMeta &m) {
   w.r0 = p[0];
   w.r1 = p[runs && m.nr > 4u ? 1 : 0];
   w.pairx = 0;
+  w.best = 0;
   return w;
 }
 // the next window's runs, LDS-DMA into nb (lane-linear: r0 of lane l at nb[4l], r1 at nb[256 + 4l])
@@ -614,6 +616,7 @@ __device__ __forceinline__ XWin take_next(const XMeta &m, const uint32_t *nb, in
   w.r0 = reinterpret_cast<const uint4 *>(nb)[lane];
   w.r1 = reinterpret_cast<const uint4 *>(nb)[64 + lane];
   w.pairx = 0;
+  w.best = 0;
   __builtin_amdgcn_s_waitcnt(kWaitLgkm0); // read before the next DMA overwrites the slot
   return w;
 }
@@ -621,30 +624,67 @@ __device__ __forceinline__ XWin take_next(const XMeta &m, const uint32_t *nb, in
 // even lanes whose neighbour is in the window): |C_l ∩ C_l+1| is at least the overlap of the two
 // containers' longest runs (members that share a core run overlap there); the neighbour's longest run
 // comes over by DPP.
-__device__ __forceinline__ void pair_xor(XWin &w) {
+// the lane's longest run as its run word, start | (len - 1) << 16 (the last of equal lengths; 0 without runs)
+__device__ __forceinline__ uint32_t longest_run(const XWin &w) {
   const uint32_t a[8] = {w.r0.x, w.r0.y, w.r0.z, w.r0.w, w.r1.x, w.r1.y, w.r1.z, w.r1.w};
-  uint32_t best = 0; // (len - 1) << 16 | start of the longest run
+  uint32_t best = 0;
 #pragma unroll
-  for (int u = 0; u < 8; ++u) {
-    const uint32_t key = (a[u] >> 16) << 16 | (a[u] & 0xFFFF);
-    if ((uint32_t)u < w.nr && (key >> 16) >= (best >> 16)) best = key;
-  }
+  for (int u = 0; u < 8; ++u)
+    if ((uint32_t)u < w.nr && (a[u] >> 16) >= (best >> 16)) best = a[u];
+  return best;
+}
+__device__ __forceinline__ void pair_xor(XWin &w) {
+  const uint32_t best = longest_run(w);
+  w.best = best;
   const uint32_t nbest = dpp<0x130>(best), cb = dpp<0x130>(w.card); // wave_shl:1 — lane l reads lane l+1
   const int sa = (int)(best & 0xFFFF), ea = sa + (int)(best >> 16);
   const int sb = (int)(nbest & 0xFFFF), eb = sb + (int)(nbest >> 16);
   const int inter = w.nr ? max(0, min(ea, eb) - max(sa, sb) + 1) : 0;
   w.pairx = w.card + cb - 2u * (uint32_t)inter;
 }
-// the boundary toggles of the lane's runs into the toggle image
-__device__ __forceinline__ void toggle_runs(const XWin &w, uint32_t *acc) {
+// Core-run de-duplication (round 6; PMC profiles/r06/xor): the members of a key usually share a run (config
+// 4: every member holds the key's 1024-value core), so all 64 lanes of a window toggled the same two bits and
+// marked the same U' words — same-address LDS atomics, serialised 64 (toggles) and 8 (marks, one copy per
+// lane & 7) deep: 120 bank-conflict cycles per window, ~70 % of the toggle pass's conflicts (a duplicated
+// toggle pass cost +1.18 ms, +503M conflict cycles).  A wave-uniform candidate run `core` (a lane's longest)
+// is handled once: its toggles by parity (k lanes toggling the same bit is the bit toggled k mod 2 times —
+// one ballot, one atomic by lane 0), its marks once per union stretch (marks are idempotent and U' is only
+// cleared when a stretch starts).  Any run that is not exactly the candidate takes the atomics as before, so
+// results do not depend on the choice.
+constexpr uint32_t kNoCore = 0xFFFFFFFFu;
+// the marks of one run word into the touched-word mask copy Mc (1 bit per 64-bit word of the container)
+__device__ __forceinline__ void mark_run(uint32_t *Mc, uint32_t rw) {
+  const uint32_t st = rw & 0xFFFF, en = st + (rw >> 16);
+  const uint32_t w0 = st >> 6, w1 = en >> 6, d0 = w0 >> 5, d1 = w1 >> 5;
+  const uint32_t mlo = 0xFFFFFFFFu << (w0 & 31), mhi = 0xFFFFFFFFu >> (31 - (w1 & 31));
+  atomicOr(&Mc[d0], d0 == d1 ? (mlo & mhi) : mlo);
+  if (d1 != d0) {
+    atomicOr(&Mc[d1], mhi);
+    for (uint32_t d = d0 + 1; d < d1; ++d) atomicOr(&Mc[d], 0xFFFFFFFFu); // runs over 2048 values
+  }
+}
+// the boundary toggles of the active lanes' runs into the toggle image, the candidate's by parity (above);
+// every lane of the wave calls it (ballots)
+__device__ __forceinline__ void toggle_runs_core(const XWin &w, uint32_t *acc, bool act, uint32_t core, int lane) {
+  const uint32_t cs = core == kNoCore ? 0x1FFFFu : (core & 0xFFFFu);
+  const uint32_t ce = core == kNoCore ? 0x3FFFFu : cs + (core >> 16) + 1;
   const uint32_t rw[8] = {w.r0.x, w.r0.y, w.r0.z, w.r0.w, w.r1.x, w.r1.y, w.r1.z, w.r1.w};
+  bool hs = false, he = false;
 #pragma unroll
   for (int u = 0; u < 8; ++u) {
-    if ((uint32_t)u < w.nr) {
+    if (act && (uint32_t)u < w.nr) {
       const uint32_t st = rw[u] & 0xFFFF, e1 = st + (rw[u] >> 16) + 1;
-      atomicXor(&acc[st >> 5], 1u << (st & 31));
-      if (e1 < (uint32_t)kSpan) atomicXor(&acc[e1 >> 5], 1u << (e1 & 31));
+      const bool ms = st == cs, me = e1 == ce;
+      hs = hs || ms;
+      he = he || me;
+      if (!ms) atomicXor(&acc[st >> 5], 1u << (st & 31));
+      if (!me && e1 < (uint32_t)kSpan) atomicXor(&acc[e1 >> 5], 1u << (e1 & 31));
     }
+  }
+  const uint64_t bs = __ballot(hs), be = __ballot(he);
+  if (lane == 0) {
+    if (__popcll(bs) & 1) atomicXor(&acc[cs >> 5], 1u << (cs & 31));
+    if ((__popcll(be) & 1) && ce < (uint32_t)kSpan) atomicXor(&acc[ce >> 5], 1u << (ce & 31));
   }
 }
 constexpr int kXorMinFast = 8; // shortest stretch worth a fast-forward (an exact batch costs ~32 stretches' steps)
@@ -668,6 +708,9 @@ constexpr int kXorUnionMinC = 1024; // try a union stretch only above this c (a 
 // the kernel's extra time and counters under a variant are that pass's marginal cost at full occupancy.
 #ifndef RBG_XOR_DUP
 #define RBG_XOR_DUP 0
+#endif
+#ifndef RBG_XOR_CORE
+#define RBG_XOR_CORE 0 // study builds: 1 de-duplicates the core run's toggles and marks (slower: DESIGN.md §7 r06)
 #endif
 
 __global__ __launch_bounds__(256, 3) void k_wide_runs_xor(SetView s, const uint64_t *__restrict__ rec,
@@ -721,6 +764,7 @@ __global__ __launch_bounds__(256, 3) void k_wide_runs_xor(SetView s, const uint6
   bool urun = false; // flavour of the pending stretch: Run (every step stays a Run) or AB
   int usum = 0;      // Run flavour: Σ nruns of the pending windows (r_j <= X.r + usum)
   bool wpx = true;   // W.pairx is current
+  uint32_t ccore = kNoCore; // the pending union stretch's candidate core run (wave-uniform), already in U'
 #if RBG_STUDY
   int tr_u = 0, tr_f = 0, tr_rej = 0, tr_p = 0, tr_pb = 0, tr_e = 0;
 #define RBG_TR(x) x
@@ -778,26 +822,19 @@ __global__ __launch_bounds__(256, 3) void k_wide_runs_xor(SetView s, const uint6
         for (int k = 0; k < 8; ++k)
           reinterpret_cast<uint16_t *>(pcT)[64 * k + lane] =
               (uint16_t)(__popcll(Pw[2 * k]) | (__popcll(Pw[2 * k + 1]) << 8));
+        ccore = readlane(longest_run(W), 0); // lane 0 is a member of every union window (posw == 0)
         wave_lds_sync();
+        if (lane == 0 && RBG_XOR_CORE) mark_run(M, ccore); // once for the stretch (copy 0)
       }
+      const uint32_t mcore = RBG_XOR_CORE ? ccore : kNoCore;
       int L = 0;
       for (int rep = 0; rep < (RBG_XOR_DUP == 1 ? 2 : 1); ++rep) {
       if (mem) {
         const uint32_t rw[8] = {W.r0.x, W.r0.y, W.r0.z, W.r0.w, W.r1.x, W.r1.y, W.r1.z, W.r1.w};
+        uint32_t *Mc = M + kMStride * (lane & (kMCopies - 1));
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          if ((uint32_t)u < W.nr) {
-            const uint32_t st = rw[u] & 0xFFFF, en = st + (rw[u] >> 16);
-            const uint32_t w0 = st >> 6, w1 = en >> 6, d0 = w0 >> 5, d1 = w1 >> 5;
-            const uint32_t mlo = 0xFFFFFFFFu << (w0 & 31), mhi = 0xFFFFFFFFu >> (31 - (w1 & 31));
-            uint32_t *Mc = M + kMStride * (lane & (kMCopies - 1));
-            atomicOr(&Mc[d0], d0 == d1 ? (mlo & mhi) : mlo);
-            if (d1 != d0) {
-              atomicOr(&Mc[d1], mhi);
-              for (uint32_t d = d0 + 1; d < d1; ++d) atomicOr(&Mc[d], 0xFFFFFFFFu); // runs over 2048 values
-            }
-          }
-        }
+        for (int u = 0; u < 8; ++u)
+          if ((uint32_t)u < W.nr && rw[u] != mcore) mark_run(Mc, rw[u]); // the candidate is in U' already
       }
       wave_lds_sync();
       // |P \ U'|: lane l sums the popcounts of words 16 l .. 16 l + 15 not in U'
@@ -825,14 +862,8 @@ __global__ __launch_bounds__(256, 3) void k_wide_runs_xor(SetView s, const uint6
       const int rub = X.r + usum + wnr; // >= every r_j of the stretch (Run flavour)
       if (urun ? (2 + 4 * rub <= min(kBitmapBytes, 2 * L + 2)) : L >= kRunArrayThreshold) {
         usum += wnr;
-        if (mem) {
-          toggle_runs(W, acc);
-          if (RBG_XOR_DUP == 2) {
-            toggle_runs(W, acc);
-            toggle_runs(W, acc);
-          }
-          X.inb += 4u * W.nr + 2u + 16u;
-        }
+        for (int rep = 0; rep < (RBG_XOR_DUP == 2 ? 3 : 1); ++rep) toggle_runs_core(W, acc, mem, mcore, lane);
+        if (mem) X.inb += 4u * W.nr + 2u + 16u;
         ++upend;
         RBG_TR(++tr_u);
         RBG_TA(1);
@@ -882,10 +913,9 @@ __global__ __launch_bounds__(256, 3) void k_wide_runs_xor(SetView s, const uint6
       // leading members within the bounds (all 64 when posw == 0 and ~okm == 0: ctz of 0 is undefined)
       const uint32_t B = fastfwd ? min(~okm ? (uint32_t)__builtin_ctzll(~okm) : 64u, wlen - posw) : 0u;
       if (B >= kXorMinFast || (B >= 1 && posw + B == wlen)) {
-        if ((uint32_t)lane >= posw && (uint32_t)lane < posw + B) {
-          toggle_runs(W, acc);
-          X.inb += 4u * W.nr + 2u + 16u;
-        }
+        const bool act = (uint32_t)lane >= posw && (uint32_t)lane < posw + B;
+        toggle_runs_core(W, acc, act, RBG_XOR_CORE ? readlane(W.best, (int)posw) : kNoCore, lane);
+        if (act) X.inb += 4u * W.nr + 2u + 16u;
         wave_lds_sync();
         uint64_t t[kW];
         lds_read_words(acc, t, lane);
@@ -997,7 +1027,10 @@ void launch_wide_runs_xor(const SetView &s, const uint32_t *cid, const uint64_t 
     k_records_gather<<<(unsigned)std::min<uint64_t>((xr.n + 255) / 256, 65536), 256, 0, st>>>(xr.mrec, cid, seg,
                                                                                            xr.rec);
   }
-  k_wide_runs_xor<<<(nk + 3) / 4, 256, 0, st>>>(s, xr.rec, seg, klist, nk, out, wo, route, stats, fastfwd);
+#ifndef RBG_XOR_LDS_PAD
+#define RBG_XOR_LDS_PAD 0 // study: dynamic LDS a block reserves without using it (8192: 2 waves per SIMD instead of 3)
+#endif
+  k_wide_runs_xor<<<(nk + 3) / 4, 256, RBG_XOR_LDS_PAD, st>>>(s, xr.rec, seg, klist, nk, out, wo, route, stats, fastfwd);
 }
 
 // this file's code object, loaded at context creation (warm_code_objects, api.hip)

@@ -211,6 +211,11 @@ class DeviceSet:
     def n_containers(self) -> int:
         return int(L.lib().rbgpu_set_container_count(self.h))
 
+    @property
+    def payload_capacity(self) -> int:
+        """rbgpu_set_payload_capacity: bytes of the HBM payload arena (16-B padded payloads)."""
+        return int(L.lib().rbgpu_set_payload_capacity(self.h))
+
     def run_optimize(self):
         """RoaringBitmap.runOptimize of every bitmap on the device (rbgpu_set_run_optimize): the new set
         and, per bitmap, runOptimize's return value (it holds a Run container)."""

@@ -16,6 +16,14 @@ root, out, cmd = sys.argv[1], sys.argv[2], sys.argv[3]
 # every other kernel's FETCH_SIZE is reported raw (a lower bound: its access widths are uncalibrated,
 # MI355X_MICROARCH.md HBM section), with the x2 figure beside it as the upper bound
 STREAM16 = ("k_pair_tasks", "k_wide_reduce", "k_bsi_range", "k_bsi_chain", "k_pair_small<")
+# Round 6 calibration (scripts/micro/fetch_calib.cpp, profiles/r06/calib): on known 4-GiB reads FETCH_SIZE is
+# TCC_EA0_RDREQ x 64 B with TCC_BUBBLE = 0 — coalesced 8-B and 16-B per lane reads issue 128-B requests (FETCH =
+# 1/2 of the bytes), scattered 16-B pieces of 64-B segments issue 64-B requests (FETCH = the bytes).  naive_xor's
+# reads are its coalesced key-major records and its run lists by LDS-DMA: FETCH x 1 falls below what the kernel
+# provably reads (records + payload arena, bench.py provable_min_read_bytes) and FETCH x 2 lies just above it, so
+# both streams are 128-B requests and x 2 is the calibrated figure.  workShyAnd (SoA reads: 2-B and 8-B metadata
+# rows, 16-B run loads) mixes the two shapes: raw is its lower bound, x 2 its upper bound.
+WIDE128 = ("k_wide_runs_xor",)
 vals = collections.defaultdict(lambda: collections.defaultdict(list))
 for f in sorted(glob.glob(f"{root}/p*/run_counter_collection.csv")):
     for row in csv.DictReader(open(f)):
@@ -27,12 +35,14 @@ for (name, grid), c in vals.items():
     if "FETCH_SIZE" not in c or "WRITE_SIZE" not in c:
         continue
     raw = 1024.0 * sum(c["FETCH_SIZE"]) / len(c["FETCH_SIZE"])
-    calibrated = any(k in name for k in STREAM16)
+    calibrated = any(k in name for k in STREAM16 + WIDE128)
     fetch = 2.0 * raw if calibrated else raw
     write = 1024.0 * sum(c["WRITE_SIZE"]) / len(c["WRITE_SIZE"])
     g = {"grid": grid, "fetch_bytes": int(fetch), "write_bytes": int(write), "traffic_bytes": int(fetch + write),
          "dispatches": len(c["FETCH_SIZE"]),
-         "fetch_correction": "x2 (16-B/lane streaming reads)" if calibrated else "raw (uncalibrated widths: lower bound)",
+         "fetch_correction": ("x2 (128-B line requests: records + LDS-DMA run lists; calibrated, profiles/r06/calib)"
+                              if any(k in name for k in WIDE128) else "x2 (16-B/lane streaming reads)") if calibrated
+                             else "raw (mixed or uncalibrated widths: lower bound; traffic_bytes_x2 the upper)",
          "traffic_bytes_x2": int(2.0 * raw + write)}
     res.setdefault(name, []).append(g)
 for name in res:

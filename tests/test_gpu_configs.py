@@ -50,6 +50,39 @@ def _check_canonical(h):
 
 
 # ---------------------------------------------------------------- config 2
+@pytest.mark.parametrize("opname", ["AND", "OR"])
+def test_config2_call_tail(ctx, monkeypatch, opname):
+    """RBGPU_CALL_TAIL=1: the synchronous 1M-pair call returns on its compaction's tail (the last block hands the
+    summed counters and a sequence number to host-visible words): its result, counters and kernel spans equal
+    the default stream-wait form's, rb_stats times its kernels when asked, small batches sharing the sequence
+    counter interleave with it, and rbgpu_set_wait / the device view work on its result."""
+    import roaringbitmap_amd as rb
+    op = OPS[opname]
+    n = 300_000
+    a, b = ctx.generate(rb.WL_FILTER_POSTING, n, seed=7)
+    small = ctx.generate(rb.WL_FILTER_POSTING, 100, seed=8)
+    got = {}
+    for form in ("0", "1", "1"):
+        monkeypatch.setenv("RBGPU_CALL_TAIL", form)
+        r = ctx.pairwise(op, a, b)
+        st = ctx.stats()
+        s2 = ctx.pairwise(op, small[0], small[1])  # a small batch between (the shared sequence counter)
+        assert len(s2) == 100
+        r.wait()
+        v = r.device_view()
+        assert v["n_containers"] == r.n_containers and v["n_bitmaps"] == n
+        key = (st["tasks"], st["input_bytes"], st["output_bytes"], st["result_cardinality"], st["result_containers"],
+               tuple(k["name"] for k in st["kernels"]), tuple(k["bytes"] for k in st["kernels"]))
+        assert st["total_ms"] > 0 and st["main_kernel_ms"] > 0 and all(k["ms"] > 0 for k in st["kernels"])
+        digest = (r.cardinalities().tobytes(), r.serialize(0, 500), r.serialize(n - 500, 500), r.type_stats())
+        got.setdefault("stats", key)
+        got.setdefault("digest", digest)
+        assert key == got["stats"], form
+        assert digest == got["digest"], form
+        r.close()
+        s2.close()
+
+
 @pytest.mark.parametrize("opname", list(OPS))
 def test_config2_million_pairs(ctx, oracle, opname):
     """Config 2 at bench size: 1M device-generated (filter, posting-list) pairs, one batched call.
