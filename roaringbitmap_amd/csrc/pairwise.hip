@@ -651,6 +651,9 @@ __device__ __forceinline__ RecU load_rec(const TaskRec *r) {
 #define RBG_HEAVY_NOPF 0 // study: register-path tasks without the one-task prefetch, at 128 VGPRs, so three
                          // light waves fit beside each heavy one on a SIMD
 #endif
+#ifndef RBG_BAL_EMIT
+#define RBG_BAL_EMIT 0 // study builds: 1 emits register-path Array / Run results by per-lane cursor walks (slower)
+#endif
 constexpr int kLightWaves = 4; // waves per SIMD of the copy + filter kernel (128 VGPRs)
 constexpr int kHeavyWaves = RBG_HEAVY_NOPF ? 4 : 2; // waves per SIMD the register-path kernel is allocated for
 constexpr bool kHeavyPrefetch = !RBG_HEAVY_NOPF;    // the next task's payloads in flight during this one's emission
@@ -894,6 +897,9 @@ __global__ __launch_bounds__(256, ROLE == kRoleHeavy ? kHeavyWaves : kLightWaves
   __shared__ __attribute__((aligned(16))) uint32_t lds[4][2048];
   __shared__ __attribute__((aligned(16))) uint16_t stage[ROLE == kRoleLight ? 4 : 1][kStageVals];
   __shared__ uint4 tbuf[ROLE == kRoleLight ? 4 : 1][32]; // per-wave half-row transpose (filter_rows_linear)
+  // register path: a second 8 KiB per wave for the balanced Array / Run emission (wave.hpp emit_container_bal)
+  __shared__ __attribute__((aligned(16))) uint32_t estage[ROLE == kRoleHeavy && RBG_BAL_EMIT ? 4 : 1]
+                                                        [ROLE == kRoleHeavy && RBG_BAL_EMIT ? 2048 : 4];
   const int lane = lane_id();
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   // static schedule (queue == nullptr): wave w takes tasks w, w + stride, ...; dynamic: chunks of
@@ -1059,7 +1065,10 @@ __global__ __launch_bounds__(256, ROLE == kRoleHeavy ? kHeavyWaves : kLightWaves
         if (ty == kRun) r = 1; // LR's Run is the full container: one run
       } else ty = type_ab(c);
       if (CARD_ONLY) ty = c ? kArray : kEmpty;
-      else if (ty != kEmpty) emit_container(bits ? (int)kBitmap : ty, w, c, r, dst, s, lane);
+      else if (ty != kEmpty) {
+        if (RBG_BAL_EMIT) emit_container_bal(bits ? (int)kBitmap : ty, w, c, r, dst, s, estage[wv], lane);
+        else emit_container(bits ? (int)kBitmap : ty, w, c, r, dst, s, lane);
+      }
       nr = ty == kRun ? (uint32_t)r : 0u;
       RBG_HT(lt_acc[3 + (ty == kBitmap ? 0 : ty == kArray ? 1 : 2)] += __builtin_amdgcn_s_memtime() - lt2);
     } else if (ROLE != kRoleHeavy) {

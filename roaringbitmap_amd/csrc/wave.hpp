@@ -703,6 +703,131 @@ __device__ __forceinline__ uint32_t emit_container(int type, const uint64_t (&w)
   return 4u * (uint32_t)runs;
 }
 
+// ---------------------------------------------------------------- balanced emission (round 6)
+// emit_container's Array / Run loops run per word: a word's trip count is the largest bit count any lane has in
+// that word, so a container pays Σ over its 16 word slots of the wave's maximum (OR's Run results: ~37 % of a
+// register-path wave).  Here each lane owns 16 CONSECUTIVE words (1024 bit positions), counts
+// its values / run starts, one wave scan ranks them, and ONE loop per lane walks its own bits with a cursor
+// over the LDS image: the trip count is the largest per-lane total, ~2-3x fewer trips.  The image is stored
+// transposed (word 16 q + j at u64 index 64 j + q, q = the walking lane) so lanes reading their j-th words hit
+// distinct banks; the results go to a second 8 KiB LDS stage `o2` and leave as 16-B blocks.
+__device__ __forceinline__ uint32_t tword(uint32_t g) { return ((g & 15u) << 6) | (g >> 4); }
+__device__ __forceinline__ void lds_write_words_t(uint32_t *s, const uint64_t (&w)[kW], int lane) {
+  uint64_t *s64 = reinterpret_cast<uint64_t *>(s);
+#pragma unroll
+  for (int k = 0; k < 8; ++k)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) s64[tword((uint32_t)(128 * k + 2 * lane + h))] = w[2 * k + h];
+}
+// the 16-B blocks of `bytes` bytes of the stage to out (slots are 16-B padded; the pad is written as zeros)
+__device__ __forceinline__ uint32_t pad_word(uint32_t v, int valid) { // valid bytes of the word, from the low end
+  return valid >= 4 ? v : valid <= 0 ? 0u : v & ((1u << (8 * valid)) - 1u);
+}
+__device__ __forceinline__ void stage_out(const uint32_t *o2, uint32_t bytes, uint8_t *out, int lane) {
+  const uint4 *s4 = reinterpret_cast<const uint4 *>(o2);
+  uint4 *o = reinterpret_cast<uint4 *>(out);
+  for (uint32_t i = lane; i * 16 < bytes; i += 64) {
+    uint4 v = s4[i];
+    const int rem = (int)(bytes - i * 16);
+    if (rem < 16) v = make_uint4(pad_word(v.x, rem), pad_word(v.y, rem - 4), pad_word(v.z, rem - 8), pad_word(v.w, rem - 12));
+    o[i] = v;
+  }
+}
+__device__ __forceinline__ uint32_t emit_array_bal(const uint64_t (&w)[kW], int card, uint8_t *out, uint32_t *s,
+                                                   uint32_t *o2, int lane) {
+  lds_write_words_t(s, w, lane);
+  wave_lds_sync();
+  const uint64_t *s64 = reinterpret_cast<const uint64_t *>(s);
+  uint32_t cnt = 0;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) cnt += (uint32_t)__popcll(s64[64 * j + lane]);
+  uint32_t pos = wave_scan_u32(cnt, lane) - cnt;
+  uint16_t *v16 = reinterpret_cast<uint16_t *>(o2);
+  uint32_t j = 0;
+  uint64_t cur = s64[lane], nxt = s64[64 + lane];
+  const uint32_t base = (uint32_t)lane << 10;
+  for (uint32_t t = 0; t < cnt; ++t) {
+    while (cur == 0) { // the next non-empty word (its successor already in flight)
+      ++j;
+      cur = nxt;
+      nxt = j < 15 ? s64[64 * (j + 1) + lane] : 0ull;
+    }
+    v16[pos++] = (uint16_t)(base + (j << 6) + (uint32_t)__builtin_ctzll(cur));
+    cur &= cur - 1;
+  }
+  wave_lds_sync();
+  const uint32_t bytes = 2u * (uint32_t)card;
+  stage_out(o2, bytes, out, lane);
+  wave_lds_sync();
+  return bytes;
+}
+// Run: a lane takes the runs that START in its words; each run's end is the first run end at or after its start
+// (it may lie in a later lane's words: the end cursor walks on through the image)
+__device__ __forceinline__ uint32_t emit_run_bal(const uint64_t (&w)[kW], int runs, uint8_t *out, uint32_t *s,
+                                                 uint32_t *o2, int lane) {
+  lds_write_words_t(s, w, lane);
+  wave_lds_sync();
+  const uint64_t *s64 = reinterpret_cast<const uint64_t *>(s);
+  const uint32_t g0 = 16u * (uint32_t)lane;
+  // the top bit of the word before the lane's first (run starts: a set bit whose predecessor is clear)
+  const uint64_t top0 = lane ? s64[tword(g0 - 1)] >> 63 : 0ull;
+  uint32_t cnt = 0;
+  {
+    uint64_t p = top0;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const uint64_t v = s64[64 * j + lane];
+      cnt += (uint32_t)__popcll(v & ~((v << 1) | p));
+      p = v >> 63;
+    }
+  }
+  const uint32_t pos = wave_scan_u32(cnt, lane) - cnt;
+  uint32_t js = 0;
+  uint64_t vs = s64[lane], xs = vs & ~((vs << 1) | top0);
+  uint32_t ge = 0;            // end cursor: word index, its word, the next word's bit 0, the word's unread ends
+  uint64_t ve = 0, vn = 0, xe = 0;
+  bool einit = false;
+  for (uint32_t t = 0; t < cnt; ++t) {
+    while (xs == 0) {
+      const uint64_t p = vs >> 63;
+      ++js;
+      vs = s64[64 * js + lane];
+      xs = vs & ~((vs << 1) | p);
+    }
+    const uint32_t sb = (uint32_t)__builtin_ctzll(xs);
+    xs &= xs - 1;
+    const uint32_t st = ((g0 + js) << 6) + sb;
+    if (!einit) { // the end cursor starts at the first start
+      einit = true;
+      ge = g0 + js;
+      ve = vs;
+      vn = ge < 1023 ? s64[tword(ge + 1)] : 0ull;
+      xe = (ve & ~((ve >> 1) | ((vn & 1ull) << 63))) & (~0ull << sb);
+    }
+    while (xe == 0) {
+      ++ge;
+      ve = vn;
+      vn = ge < 1023 ? s64[tword(ge + 1)] : 0ull;
+      xe = ve & ~((ve >> 1) | ((vn & 1ull) << 63));
+    }
+    const uint32_t en = (ge << 6) + (uint32_t)__builtin_ctzll(xe);
+    xe &= xe - 1;
+    o2[pos + t] = st | ((en - st) << 16);
+  }
+  wave_lds_sync();
+  const uint32_t bytes = 4u * (uint32_t)runs;
+  stage_out(o2, bytes, out, lane);
+  wave_lds_sync();
+  return bytes;
+}
+// emit_container with the balanced Array / Run emission; o2: a second 8 KiB LDS stage of the wave
+__device__ __forceinline__ uint32_t emit_container_bal(int type, const uint64_t (&w)[kW], int card, int runs,
+                                                       uint8_t *out, uint32_t *s, uint32_t *o2, int lane) {
+  if (type == kArray) return emit_array_bal(w, card, out, s, o2, lane);
+  if (type == kRun) return emit_run_bal(w, runs, out, s, o2, lane);
+  return emit_container(type, w, card, runs, out, s, lane);
+}
+
 // Copy a payload (multiple of 16 bytes after rounding; slots are 16-B padded), 8 KiB per round with every
 // load of the round in flight before its stores (a load -> store loop waits one memory latency per 1 KiB:
 // the compiler cannot move a load above the previous iteration's store)
