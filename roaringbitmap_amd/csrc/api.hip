@@ -83,7 +83,6 @@ void ctx_unref(rbgpu_ctx *ctx) {
   for (auto &e : ctx->ev_side) (void)hipEventDestroy(e);
   (void)hipEventDestroy(ctx->ev_tot);
   if (ctx->ev_ext) (void)hipEventDestroy(ctx->ev_ext);
-  if (ctx->ev_seq) (void)hipEventDestroy(ctx->ev_seq);
   (void)hipFree(ctx->d_stats);
   (void)hipHostFree(ctx->h_pinned);
   (void)hipHostFree(ctx->h_stats);
@@ -518,7 +517,7 @@ bool wait_call_seq(rbgpu_ctx *ctx, uint64_t seq, int word) {
 }
 int seq_begin(rbgpu_ctx *ctx) {
   if (ctx->seq_settled >= ctx->seq_recorded) return RB_OK;
-  const hipError_t q = hipEventQuery(ctx->ev_seq);
+  const hipError_t q = hipEventQuery(ctx->ev[5]);
   if (q == hipSuccess) {
     ctx->seq_settled = ctx->seq_recorded;
     return RB_OK;
@@ -529,8 +528,7 @@ int seq_begin(rbgpu_ctx *ctx) {
 }
 int seq_end(rbgpu_ctx *ctx, uint64_t seq, bool poll, const char *what, bool *seen, int word) {
   *seen = false;
-  HIPCHK(hipEventRecord(ctx->ev_seq, ctx->stream));
-  ctx->seq_recorded = seq;
+  ctx->seq_recorded = seq; // ctx->ev[5], recorded by the caller behind the kernel, marks its end
   const bool s = poll && wait_call_seq(ctx, seq, word);
   const hipError_t e1 = s ? hipSuccess : hipStreamSynchronize(ctx->stream), e2 = hipGetLastError();
   if (e1 != hipSuccess || e2 != hipSuccess)
@@ -550,7 +548,7 @@ int seq_end(rbgpu_ctx *ctx, uint64_t seq, bool poll, const char *what, bool *see
 }
 int seq_settle(rbgpu_ctx *ctx, uint64_t seq) {
   if (!seq || seq <= ctx->seq_settled) return RB_OK;
-  const hipError_t e = hipEventSynchronize(ctx->ev_seq); // recorded behind call seq or a later one
+  const hipError_t e = hipEventSynchronize(ctx->ev[5]); // recorded behind call seq or a later one
   if (e != hipSuccess) {
     (void)hipGetLastError();
     return fail(RB_EDEVICE, "one-launch kernel failed: %s", hipGetErrorString(e));
@@ -594,7 +592,6 @@ int rbgpu_open(int device, rbgpu_ctx **out) {
   for (auto &e : c->ev_side) (void)hipEventCreate(&e);
   (void)hipEventCreate(&c->ev_tot);
   (void)hipEventCreateWithFlags(&c->ev_ext, hipEventDisableTiming);
-  (void)hipEventCreateWithFlags(&c->ev_seq, hipEventDisableTiming);
   // every source file's code object now, not inside the first call of each kind: HIP loads a code object at
   // the first launch of one of its kernels (~1 ms each), which otherwise lands in that call's time and in a
   // set's first-use setup (rbgpu_set_setup_parts)

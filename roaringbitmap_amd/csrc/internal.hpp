@@ -169,11 +169,11 @@ struct rbgpu_ctx {
   uint64_t *d_small_ctr = nullptr;                  // small-batch finished-block count and counters
   uint64_t small_seq = 0;   // small-batch calls launched (the kernel's last block writes it to h_small[5])
   // A one-launch call returns on its sequence word, before its kernel's end is signalled (and before the
-  // kernel-end release writes other XCDs' payload stores back from their L2s).  ev_seq is recorded behind
-  // the latest such kernel, whose sequence number is seq_recorded; seq_settled is the highest sequence
-  // number known complete.  Later work on `stream` is ordered behind the kernel anyway; a use anywhere
-  // else (a caller's stream, rbgpu_set_wait, rbgpu_set_device_view) waits for ev_seq (seq_settle).
-  hipEvent_t ev_seq = nullptr;
+  // kernel-end release writes other XCDs' payload stores back from their L2s).  ev[5] is recorded behind
+  // the latest such kernel (or behind a later call's work on the same stream), whose sequence number is
+  // seq_recorded; seq_settled is the highest sequence number known complete.  Later work on `stream` is
+  // ordered behind the kernel anyway; a use anywhere else (a caller's stream, rbgpu_set_wait) waits for ev[5]
+  // (seq_settle).
   uint64_t seq_recorded = 0, seq_settled = 0;
   // a general-pipeline call that returned on its compaction's tail (CallTail): its kernel spans, timed when the
   // stats are asked for (rbgpu_get_stats; 0 = none pending)
@@ -226,7 +226,7 @@ struct rbgpu_set {
   // still read the buffers after the call returned): freeing the set waits for it
   hipEvent_t read_done = nullptr;
   // written by the one-launch call with this sequence number (0: none): complete for the host's purposes
-  // (nc known), but its kernel may not have ended (rbgpu_ctx::ev_seq)
+  // (nc known), but its kernel may not have ended (rbgpu_ctx::seq_recorded)
   uint64_t end_seq = 0;
   double derive_ms = 0.0;         // device time spent building mrec / krec (reported, not hidden)
   uint64_t derive_bytes = 0;      // their algorithmic bytes (metadata read + records written)
@@ -254,7 +254,7 @@ int ensure_call_words(rbgpu_ctx *ctx);
 bool wait_call_seq(rbgpu_ctx *ctx, uint64_t seq, int word = 5);
 // The one-launch hand-off around a kernel whose last block writes the result words and then `seq`:
 // seq_begin surfaces a fault of an earlier one-launch kernel that ended after its call returned
-// (non-blocking); seq_end records ev_seq behind the kernel, waits for the sequence word (else for the
+// (non-blocking); seq_end (ctx->ev[5] recorded behind the kernel) waits for the sequence word (else for the
 // stream) and fails with RB_EDEVICE when the words are not this call's — then the finished-block counters
 // are re-zeroed, since no block of the call saw itself last.  seq_settle waits for the kernel
 // end of call `seq` (a no-op once known complete).

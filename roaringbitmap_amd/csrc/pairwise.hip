@@ -651,6 +651,9 @@ __device__ __forceinline__ RecU load_rec(const TaskRec *r) {
 #define RBG_HEAVY_NOPF 0 // study: register-path tasks without the one-task prefetch, at 128 VGPRs, so three
                          // light waves fit beside each heavy one on a SIMD
 #endif
+#ifndef RBG_HEAVY_MERGE
+#define RBG_HEAVY_MERGE 0 // study builds: 1 merges OR / XOR of two small Arrays here (slower: DESIGN.md §7 r06)
+#endif
 #ifndef RBG_BAL_EMIT
 #define RBG_BAL_EMIT 0 // study builds: 1 emits register-path Array / Run results by per-lane cursor walks (slower)
 #endif
@@ -975,6 +978,26 @@ __global__ __launch_bounds__(256, ROLE == kRoleHeavy ? kHeavyWaves : kLightWaves
         ty = c == 0 ? kEmpty : CARD_ONLY ? kArray : kRun;
         nr = ty == kRun ? (uint32_t)r : 0u;
       }
+    }
+    if (ROLE == kRoleHeavy && RBG_HEAVY_MERGE && !done && (OP == RB_OR || OP == RB_XOR) && !tm.lazy &&
+        tc.tp == kArray && tc.tq == kArray && tc.cp + tc.cq <= kMergeMax) {
+      // ---- Array OR / XOR Array as a merge (merge_run, the small-batch kernel's): the result is an Array
+      //      (c <= ca + cb <= 4088), the register path's type, without two 65536-bit images and the per-word
+      //      emission loops.  In this kernel, not the copy + filter one (there it made the L2-bound light
+      //      kernel the long pole: profiles/r05/merge).
+      merge_stage(pq, tc.cp, qq, tc.cq, s, lane);
+      __builtin_amdgcn_sched_barrier(0);
+      if (kHeavyPrefetch) { // the staged payloads' registers are free: the next task's loads go out now
+        {
+          const bool real = has_next && !tn.bigq;
+          load_chunks(qq, real ? tn.pq : tn.pp, real ? tn.qbytes : 16u, lane);
+        }
+        load_chunks(pq, tn.pp, tn.bigp ? 16u : tn.pbytes, lane);
+      }
+      c = (int)merge_run<OP, !CARD_ONLY>(s, tc.cp, tc.cq, reinterpret_cast<uint16_t *>(dst), lane);
+      ty = CARD_ONLY ? (c ? kArray : kEmpty) : (c || (OP == RB_XOR && tm.keep_empty)) ? kArray : kEmpty;
+      nr = 0;
+      done = true;
     }
     if (ROLE == kRoleHeavy && !done) {
       // ---- the result as a register bitmap: P = A, Q = B (never swapped: ANDNOT and the type
