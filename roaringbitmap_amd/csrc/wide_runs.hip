@@ -242,10 +242,13 @@ __global__ __launch_bounds__(256) void k_wide_runs(SetView s, CidMap cm,
 // latency per step).  A key with another container type, > 8 runs or a list overflow is routed to the
 // generic kernel (route[q] = 1): results are identical.
 constexpr int kAndCap = 16;
-constexpr int kAndDc = 3; // steps between a container id's load and its record's load
-constexpr int kAndDr = 3; // steps between a record's load and its runs' load
-constexpr int kAndDp = 3; // steps between the runs' load and their use
-constexpr int kAndU = 6;  // steps per unrolled loop trip: a multiple of Dp, Dp + Dr and Dc
+#ifndef RBG_AND_RING
+#define RBG_AND_RING 3 // study builds: steps every link of the load chain spans (2, 3, 4)
+#endif
+constexpr int kAndDc = RBG_AND_RING; // steps between a container id's load and its record's load
+constexpr int kAndDr = RBG_AND_RING; // steps between a record's load and its runs' load
+constexpr int kAndDp = RBG_AND_RING; // steps between the runs' load and their use
+constexpr int kAndU = 2 * RBG_AND_RING; // steps per unrolled loop trip: a multiple of Dp, Dp + Dr and Dc
 static_assert(kAndU % kAndDp == 0 && kAndU % (kAndDp + kAndDr) == 0 && kAndU % kAndDc == 0, "ring periods");
 struct AndMeta {
   uint32_t typ, nr;
@@ -547,7 +550,10 @@ __global__ __launch_bounds__(256) void k_wide_runs_and(SetView s, const uint64_t
   }
 }
 
-constexpr int kAndKeys = 16; // keys per wave of the lane-parallel workShyAnd
+#ifndef RBG_AND_KEYS
+#define RBG_AND_KEYS 16 // study builds: keys per wave (8, 16, 32)
+#endif
+constexpr int kAndKeys = RBG_AND_KEYS; // keys per wave of the lane-parallel workShyAnd
 
 bool launch_wide_runs(int sem, const SetView &s, const uint64_t *mrec, const CidMap &cm, const uint64_t *seg,
                       const uint32_t *klist, uint32_t nk, uint8_t *out, const WideOut &wo, uint8_t *route,

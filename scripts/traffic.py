@@ -21,9 +21,10 @@ STREAM16 = ("k_pair_tasks", "k_wide_reduce", "k_bsi_range", "k_bsi_chain", "k_pa
 # 1/2 of the bytes), scattered 16-B pieces of 64-B segments issue 64-B requests (FETCH = the bytes).  naive_xor's
 # reads are its coalesced key-major records and its run lists by LDS-DMA: FETCH x 1 falls below what the kernel
 # provably reads (records + payload arena, bench.py provable_min_read_bytes) and FETCH x 2 lies just above it, so
-# both streams are 128-B requests and x 2 is the calibrated figure.  workShyAnd (SoA reads: 2-B and 8-B metadata
-# rows, 16-B run loads) mixes the two shapes: raw is its lower bound, x 2 its upper bound.
-WIDE128 = ("k_wide_runs_xor",)
+# both streams are 128-B requests and x 2 is the calibrated figure.  workShyAnd is the same case: its 16 lanes of a
+# member read 16 consecutive keys' run counts, offsets and run lists — consecutive containers, whole lines — and
+# raw FETCH (5.2 GB) falls below the run arena alone (6.4 GB), so its requests are 128-B lines too.
+WIDE128 = ("k_wide_runs_xor", "k_wide_runs_and")
 vals = collections.defaultdict(lambda: collections.defaultdict(list))
 for f in sorted(glob.glob(f"{root}/p*/run_counter_collection.csv")):
     for row in csv.DictReader(open(f)):
@@ -40,7 +41,7 @@ for (name, grid), c in vals.items():
     write = 1024.0 * sum(c["WRITE_SIZE"]) / len(c["WRITE_SIZE"])
     g = {"grid": grid, "fetch_bytes": int(fetch), "write_bytes": int(write), "traffic_bytes": int(fetch + write),
          "dispatches": len(c["FETCH_SIZE"]),
-         "fetch_correction": ("x2 (128-B line requests: records + LDS-DMA run lists; calibrated, profiles/r06/calib)"
+         "fetch_correction": ("x2 (128-B line requests; raw < the kernel's provable reads; calibrated, profiles/r06/calib)"
                               if any(k in name for k in WIDE128) else "x2 (16-B/lane streaming reads)") if calibrated
                              else "raw (mixed or uncalibrated widths: lower bound; traffic_bytes_x2 the upper)",
          "traffic_bytes_x2": int(2.0 * raw + write)}
