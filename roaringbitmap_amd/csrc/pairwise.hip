@@ -545,7 +545,10 @@ constexpr uint32_t kEmitStage = 640; // records (25 KiB); a block with more stor
 // cnt: the segments' counts, bs: the exclusive scans of the block totals (bs.x[blockIdx]); every
 // segment's task offset is also stored in task_begin[p] (task_begin[nseg] = the total) for the
 // compaction.
-__global__ __launch_bounds__(kPairThreads) void k_pair_emit(PairArgs a, const uint64_t *cnt, PairCountArrays bs,
+#ifndef RBG_EMIT_WAVES
+#define RBG_EMIT_WAVES 1 // study builds: waves per SIMD the emit is compiled for (1: no bound; 119 VGPRs = 4 waves)
+#endif
+__global__ __launch_bounds__(kPairThreads, RBG_EMIT_WAVES) void k_pair_emit(PairArgs a, const uint64_t *cnt, PairCountArrays bs,
                                                             uint64_t small_base, TaskRec *light, TaskRec *heavy,
                                                             TaskMeta tm, uint64_t *task_begin, const uint64_t *tot,
                                                             uint64_t cap, unsigned long long *zero_q) {

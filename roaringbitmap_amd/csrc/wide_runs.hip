@@ -243,7 +243,7 @@ __global__ __launch_bounds__(256) void k_wide_runs(SetView s, CidMap cm,
 // generic kernel (route[q] = 1): results are identical.
 constexpr int kAndCap = 16;
 #ifndef RBG_AND_RING
-#define RBG_AND_RING 3 // study builds: steps every link of the load chain spans (2, 3, 4)
+#define RBG_AND_RING 2 // steps every link of the load chain spans (at 32 keys: 2 1.55, 3 1.64, 4 1.67 ms)
 #endif
 constexpr int kAndDc = RBG_AND_RING; // steps between a container id's load and its record's load
 constexpr int kAndDr = RBG_AND_RING; // steps between a record's load and its runs' load
@@ -551,7 +551,7 @@ __global__ __launch_bounds__(256) void k_wide_runs_and(SetView s, const uint64_t
 }
 
 #ifndef RBG_AND_KEYS
-#define RBG_AND_KEYS 16 // study builds: keys per wave (8, 16, 32)
+#define RBG_AND_KEYS 32 // keys per wave (round 6 A/B, profiles/r06/and: 8 2.14, 16 1.80, 32 1.64, 64 1.94 ms)
 #endif
 constexpr int kAndKeys = RBG_AND_KEYS; // keys per wave of the lane-parallel workShyAnd
 

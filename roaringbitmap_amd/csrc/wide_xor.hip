@@ -687,7 +687,10 @@ __device__ __forceinline__ void toggle_runs_core(const XWin &w, uint32_t *acc, b
     if ((__popcll(be) & 1) && ce < (uint32_t)kSpan) atomicXor(&acc[ce >> 5], 1u << (ce & 31));
   }
 }
-constexpr int kXorMinFast = 8; // shortest stretch worth a fast-forward (an exact batch costs ~32 stretches' steps)
+#ifndef RBG_XOR_MIN_FAST
+#define RBG_XOR_MIN_FAST 8 // study builds (A/B of the heuristic)
+#endif
+constexpr int kXorMinFast = RBG_XOR_MIN_FAST; // shortest stretch worth a fast-forward (an exact batch costs ~32 stretches' steps)
 // Union stretches.  The pair bounds above limit an AB stretch to about one window when the members'
 // XOR can reach the accumulator's size (config 4: |C ⊕ C'| ~ 900 per pair, ~29k per window against
 // c ~ 32k), so every window paid a toggle -> word conversion and a re-measure (~600 of ~1100 VALU per
@@ -698,7 +701,10 @@ constexpr int kXorMinFast = 8; // shortest stretch worth a fast-forward (an exac
 // per run).  While |P \ U'| >= 32 every step of an AB-typed accumulator is AB(c_j) (c_j >= 32, never
 // empty), so the windows' toggles accumulate in the toggle image with no conversion at all; the stretch
 // closes (one conversion, one re-measure of c) when the next window would push |P \ U'| below 32.
-constexpr int kXorUnionMinC = 1024; // try a union stretch only above this c (a heuristic: results do not depend on it)
+#ifndef RBG_XOR_UNION_MINC
+#define RBG_XOR_UNION_MINC 1024 // study builds (A/B of the heuristic)
+#endif
+constexpr int kXorUnionMinC = RBG_XOR_UNION_MINC; // try a union stretch only above this c (a heuristic: results do not depend on it)
 #ifndef RBG_STUDY
 #define RBG_STUDY 0 // study builds: per-key stretch counts of three keys (printf)
 #endif
