@@ -640,8 +640,8 @@ WIDE_PARALLEL = {"FAST_OR": "PAR_OR", "FAST_XOR": "PAR_XOR", "FAST_AND": "FAST_A
 WIDE_SETUP_PARTS = {"FAST_OR": ("dense_check",), "FAST_AND": ("dense_check",),
                     "FAST_XOR": ("dense_check", "krec")}
 # bytes per container a config-4 kernel must read besides the payload arena (at least once per launch):
-# naive_xor its key-major 8-B record, workShyAnd the u16 run count and the u64 payload offset
-WIDE_META_BYTES = {"FAST_XOR": 8, "FAST_AND": 10}
+# naive_xor its key-major 4-B record, workShyAnd the u16 run count and the u64 payload offset
+WIDE_META_BYTES = {"FAST_XOR": 4, "FAST_AND": 10}
 
 
 def run_wide(args, name, D, ctx, rb, nbitmaps, steps, warmup, a=None):
@@ -716,7 +716,7 @@ def run_wide(args, name, D, ctx, rb, nbitmaps, steps, warmup, a=None):
     su = {"ms": round(sum(parts[k]["ms"] for k in need), 4), "bytes": sum(parts[k]["bytes"] for k in need)}
     out["setup"] = {"ms": su["ms"], "bytes": su["bytes"], "parts": {k: parts[k] for k in need},
                     "what": "rbgpu_set_setup_parts of this rank's set: the derived metadata this path builds on a "
-                            "fresh set (dense-layout check; naive_xor: key-major 8-B records straight from the set's "
+                            "fresh set (dense-layout check; naive_xor: key-major 4-B records straight from the set's "
                             "metadata, k_records_direct2; workShyAnd reads the set's own metadata and builds none), "
                             "once per set before the warmup step, not inside the timed steps"}
     # what a caller that uploads a fresh set for every call pays (the reference builds its per-call state each

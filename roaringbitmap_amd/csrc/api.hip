@@ -235,20 +235,18 @@ int ensure_krec(const rbgpu_set *cs) {
   int rc = ensure_dense(s);
   if (rc) return rc;
   if (s->dense_lo < 0) return fail(RB_EINVAL, "key-major records need a dense set");
-  if (s->payload_bytes >= kRecMaxPayload) return fail(RB_EINVAL, "packed records hold 40-bit payload offsets");
   HIPCHK(hipSetDevice(s->ctx->device));
   hipStream_t st = s->ctx->stream;
-  uint64_t *k = nullptr;
-  if (s->ctx->pool.alloc((void **)&k, std::max<uint64_t>(s->nc, 1) * 8)) return fail(RB_ENOMEM, "key-major records");
+  uint32_t *k = nullptr;
+  if (s->ctx->pool.alloc((void **)&k, std::max<uint64_t>(s->nc, 1) * 4)) return fail(RB_ENOMEM, "key-major records");
   // member m's container at key x is begin[m] + x - dense_lo: the set's own device begin array, no host
   // table copied up (a pageable 32 KiB copy cost ~0.8 ms inside the timed setup).  From mrec when the set
-  // already has it (16 B per container), else from the SoA itself (15 B of metadata read, an 8-B record
-  // written: k_records_direct).
+  // already has it (12 B per container), else from the SoA itself (the run count and the offset, 10 B read, a
+  // 4-B record written: k_records_direct).
   const bool from_mrec = s->mrec != nullptr;
   const SetView v = s->view();
   // two containers per load: member m's first container begin[m] at an even index and the arrays aligned for it
-  bool even_bases = !((uintptr_t)v.type & 1) && !((uintptr_t)v.card & 7) && !((uintptr_t)v.nruns & 3) &&
-                    !((uintptr_t)v.off & 15);
+  bool even_bases = !((uintptr_t)v.nruns & 3) && !((uintptr_t)v.off & 15);
   for (uint32_t b = 0; b < s->nb && even_bases; ++b) even_bases = !(s->h_begin[b] & 1);
   {
     DeriveTimer t(s, 2);
@@ -264,8 +262,8 @@ int ensure_krec(const rbgpu_set *cs) {
     return fail(RB_EDEVICE, "key-major record kernel failed");
   }
   s->krec = k;
-  s->derive_bytes += (from_mrec ? 16ull : 23ull) * s->nc;
-  s->part_bytes[2] += (from_mrec ? 16ull : 23ull) * s->nc;
+  s->derive_bytes += (from_mrec ? 12ull : 14ull) * s->nc;
+  s->part_bytes[2] += (from_mrec ? 12ull : 14ull) * s->nc;
   return RB_OK;
 }
 } // namespace rbg
@@ -289,6 +287,11 @@ int upload_host(rbgpu_ctx *ctx, const HostSoA &h, rbgpu_set **out) {
     }
   }
   const uint64_t total = nbig * kBitmapBytes + small;
+  // a run count only on Run containers: workShyAnd's SoA reads and naive_xor's records take "nruns > 0" for
+  // "a Run", so an Array / Bitmap entry's count (which the format ignores) is stored as 0
+  std::vector<uint16_t> nruns(h.nruns.begin(), h.nruns.begin() + nc);
+  for (uint64_t i = 0; i < nc; ++i)
+    if (h.type[i] != RB_RUN) nruns[i] = 0;
   std::vector<uint8_t> staged(std::max<uint64_t>(total, 16), 0);
   for (uint64_t i = 0; i < nc; ++i)
     std::memcpy(staged.data() + off[i], h.payload.data() + h.off[i], payload_bytes(h.type[i], h.card[i], h.nruns[i]));
@@ -303,7 +306,7 @@ int upload_host(rbgpu_ctx *ctx, const HostSoA &h, rbgpu_set **out) {
     return n ? hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, st) : hipSuccess;
   };
   if (cp(s->begin, h.begin.data(), (h.nb + 1) * 8) || cp(s->key, h.key.data(), nc * 2) ||
-      cp(s->type, h.type.data(), nc) || cp(s->card, h.card.data(), nc * 4) || cp(s->nruns, h.nruns.data(), nc * 2) ||
+      cp(s->type, h.type.data(), nc) || cp(s->card, h.card.data(), nc * 4) || cp(s->nruns, nruns.data(), nc * 2) ||
       cp(s->off, off.data(), nc * 8) || cp(s->payload, staged.data(), total) || hipStreamSynchronize(st)) {
     set_release(s);
     delete s;

@@ -82,5 +82,19 @@ __host__ __device__ inline uint32_t rec_card(uint64_t r) { return (uint32_t)(r >
 __host__ __device__ inline uint32_t rec_nruns(uint64_t r) { return (uint32_t)(r >> 57) & 15u; }
 __host__ __device__ inline uint64_t rec_off(uint64_t r) { return r & ((1ull << 40) - 1); }
 constexpr uint64_t kRecMaxPayload = 1ull << 40;
+// naive_xor's 4-B member record (round 6; rbgpu_set::krec and the per-call records): a Run of 1..8 runs as
+// its 16-B payload unit (29 bits) and nruns - 1 (3 bits); any other container — another type, more runs,
+// an offset past 8 GiB or not 16-B aligned — is kXBad (its key goes to the generic kernel).  The card is
+// not stored: the kernel sums it from the runs it loads anyway.
+constexpr uint32_t kXBad = 0xFFFFFFFFu;
+__host__ __device__ inline uint32_t pack_xrec(bool run, uint32_t nr, uint64_t off) {
+  const uint64_t u = off >> 4;
+  return run && nr >= 1u && nr <= 8u && !(off & 15u) && u < (1ull << 29) - 1u ? (uint32_t)(u << 3) | (nr - 1u) : kXBad;
+}
+__host__ __device__ inline bool xrec_ok(uint32_t r) { return r != kXBad; }
+__host__ __device__ inline uint32_t xrec_nruns(uint32_t r) { return r != kXBad ? (r & 7u) + 1u : 0u; }
+__host__ __device__ inline uint64_t xrec_off(uint32_t r) { return r != kXBad ? (uint64_t)(r >> 3) << 4 : 0ull; }
+// the same from a packed 8-B record
+__host__ __device__ inline uint32_t xrec_of(uint64_t m) { return pack_xrec(rec_type(m) == (uint32_t)kRun, rec_nruns(m), rec_off(m)); }
 
 } // namespace rbg

@@ -213,10 +213,10 @@ struct rbgpu_set {
   //   dense_lo / dense_hi  every bitmap holds exactly the high keys [dense_lo, dense_hi) (-1: no; -2: unknown)
   //   mrec                 one packed 8-B record per container in set order (pack_rec: payload offset,
   //                        card, min(nruns, 15), type) — one load instead of four metadata arrays
-  //   krec                 dense sets only: the same records key-major, krec[(k - dense_lo) * nb + b]
+  //   krec                 dense sets only: naive_xor's 4-B records (pack_xrec) key-major, krec[(k - dense_lo) * nb + b]
   int64_t dense_lo = -2, dense_hi = -2;
   uint64_t *mrec = nullptr;
-  uint64_t *krec = nullptr;
+  uint32_t *krec = nullptr;
   // rbgpu_pairwise_async: the call's work is still running; `nc` arrives in the context's pinned slot
   // `pend_slot` when `pending` completes (settle() waits for it and fills nc)
   hipEvent_t pending = nullptr;

@@ -224,13 +224,13 @@ struct KeyCids {
     return cid ? cid[i] : (uint32_t)(mbase[i - lo] + key);
   }
 };
-// naive_xor's key-major member records (wide_xor.hip): `rec` holds one packed record (pack_rec) per
+// naive_xor's key-major member records (wide_xor.hip): `rec` holds one 4-B record (pack_xrec) per
 // grouped container, in grouped order.  kCached: `rec` is the set's krec (dense set, members in set
 // order: nothing to build); kTranspose: dense members in another order, transposed per call from the
 // set's mrec through mbase; kGather: grouped by the counting sort, gathered through the ids.
 struct XorRecords {
   enum Build { kCached = 0, kTranspose = 1, kGather = 2 };
-  uint64_t *rec;
+  uint32_t *rec;
   uint64_t n;
   Build build;
   const uint64_t *mrec, *mbase;
@@ -239,9 +239,9 @@ struct XorRecords {
 // member m's container at key k is mbase[m] - bias + k (a dense set: mbase = the set's begin, bias = key_lo)
 // pairs: every mbase[m] - bias + key_lo is even (two containers per lane, 128-key tiles)
 void launch_records_direct(const SetView &s, const uint64_t *mbase, uint64_t bias, uint32_t M, uint32_t key_lo,
-                           uint32_t key_hi, uint64_t *rec, hipStream_t st, bool pairs = false);
+                           uint32_t key_hi, uint32_t *rec, hipStream_t st, bool pairs = false);
 void launch_records_transpose(const uint64_t *mrec, const uint64_t *mbase, uint64_t bias, uint32_t M, uint32_t key_lo,
-                              uint32_t key_hi, uint64_t *rec, hipStream_t st);
+                              uint32_t key_hi, uint32_t *rec, hipStream_t st);
 void launch_wide_runs_xor(const SetView &s, const uint32_t *cid, const uint64_t *seg, const uint32_t *klist,
                           uint32_t nk, uint8_t *out, const WideOut &wo, uint8_t *route, uint64_t *stats,
                           const XorRecords &xr, hipStream_t st);

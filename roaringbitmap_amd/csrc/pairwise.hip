@@ -236,6 +236,22 @@ __device__ __forceinline__ bool light_task(int op, int ta, int tb) {
   if (op == RB_ANDNOT) return ta == kArray;
   return false;
 }
+// Round 6: an OR with a Bitmap operand of more than 4096 values (canonical, no lazy marks) holds all of that
+// operand's values, so its LR type (BitmapContainer.or(Array / Bitmap / Run), BitmapContainer.java:1073-1110;
+// RunContainer.or(Bitmap)) is known before the OR: a Bitmap, or the full Run when c = 65536 (and a Bitmap even
+// then for BitmapContainer.ior(ArrayContainer), :749-766).  Such a task needs no register image and no
+// emission loops: the copy + filter kernel ORs the staged other operand into it row by row (kBits), at that
+// kernel's occupancy.  Only the plain OR: the lazy roles keep the register path's lazy types.
+#ifndef RBG_OR_BITS
+#define RBG_OR_BITS 0 // study builds: 1 sends them to the copy + filter kernel (slower: config 2 OR 13.12 vs 12.36 ms)
+#endif
+__device__ __forceinline__ bool big_bitmap(int t, uint32_t c) {
+  return t == kBitmap && !(c & kCardMarks) && c > (uint32_t)kMaxArray;
+}
+__device__ __forceinline__ bool bits_task(int op, int ta, uint32_t ca, int tb, uint32_t cb) {
+  return RBG_OR_BITS && op == RB_OR && (uint32_t)ta <= 2u && (uint32_t)tb <= 2u &&
+         (big_bitmap(ta, ca) || big_bitmap(tb, cb));
+}
 
 // Striped accounting (stats word w, stripe = block mod kStripes) of N counters: one atomic per block
 // and counter, by a thread of the block after an LDS reduction (every thread of the block must call
@@ -370,7 +386,7 @@ __device__ __forceinline__ void pair_walk(const PairArgs &a, uint64_t sg, PairCo
   // one result slot from the two sides' container metadata (ta / tb < 0: no container on that side)
   auto slot_v = [&](int ta, uint32_t ca, uint32_t ra, uint64_t oa, int tb, uint32_t cb, uint32_t rb, uint64_t ob,
                     uint16_t key, bool big, uint64_t bytes) {
-    const bool lt = light_task(a.op, ta, tb);
+    const bool lt = light_task(a.op, ta, tb) || bits_task(a.op, ta, ca, tb, cb);
     if (!EMIT) {
       uint64_t b = 0;
       if (ta >= 0) b += alg_bytes(ta, ca, ra) + 16;
@@ -661,28 +677,38 @@ __device__ __forceinline__ RecU load_rec(const TaskRec *r) {
 #define RBG_BAL_EMIT 0 // study builds: 1 emits register-path Array / Run results by per-lane cursor walks (slower)
 #endif
 constexpr int kLightWaves = 4; // waves per SIMD of the copy + filter kernel (128 VGPRs)
-constexpr int kHeavyWaves = RBG_HEAVY_NOPF ? 4 : 2; // waves per SIMD the register-path kernel is allocated for
+#ifndef RBG_HEAVY_WAVES
+#define RBG_HEAVY_WAVES (RBG_HEAVY_NOPF ? 4 : 2)
+#endif
+constexpr int kHeavyWaves = RBG_HEAVY_WAVES; // waves per SIMD the register-path kernel is allocated for
 constexpr bool kHeavyPrefetch = !RBG_HEAVY_NOPF;    // the next task's payloads in flight during this one's emission
 #ifndef RBG_STUDY
 #define RBG_STUDY 0 // study builds: per-phase s_memtime totals of a few light / heavy waves (printf)
 #endif
-enum { kCopy = 0, kFilter = 1, kHeavy = 2 };
+enum { kCopy = 0, kFilter = 1, kHeavy = 2, kBits = 3 };
 struct Task {
   int kind;
   bool bigp, bigq;       // payload exceeds 8 KiB (Run with > 2047 runs): direct path from global
+  bool p_is_a;           // P is A's container (kBits: the inplace Bitmap.ior(Array) rule reads it)
   const uint8_t *pp, *pq;
   uint32_t pbytes, qbytes;
   int tp, tq;            // container types of P and Q
   uint32_t cp, cq, rp, rq;
 };
-template <int OP>
+// LIGHT: the copy + filter kernel's view, where a matched OR pair is a kBits task (bits_task: the walk sends
+// no other matched OR pair there); P is then the large Bitmap (A's when both qualify)
+template <int OP, bool LIGHT>
 __device__ __forceinline__ Task decode_task(const RecU &r, const uint8_t *pay_a, const uint8_t *pay_b) {
   Task T;
   const uint32_t ta = desc_type(r.da), tb = desc_type(r.db);
   const uint32_t ca = desc_card(r.da), cb = desc_card(r.db);
-  const bool p_is_a = ta != kAbsent && !(light_task(OP, (int)ta, (int)tb) && tb == kArray &&
-                                         (ta != kArray || (OP != RB_ANDNOT && cb < ca)));
+  const bool bits = LIGHT && RBG_OR_BITS && OP == RB_OR && ta != kAbsent && tb != kAbsent;
+  const bool p_is_a = bits ? big_bitmap((int)ta, ca)
+                           : ta != kAbsent && !(light_task(OP, (int)ta, (int)tb) && tb == kArray &&
+                                                (ta != kArray || (OP != RB_ANDNOT && cb < ca)));
+  T.p_is_a = p_is_a;
   if (ta == kAbsent || tb == kAbsent) T.kind = kCopy;
+  else if (bits) T.kind = kBits;
   else T.kind = light_task(OP, (int)ta, (int)tb) ? kFilter : kHeavy;
   // kFilter: F is the Array (ANDNOT: always A; AND of two Arrays: the smaller, A on ties)
   T.pp = p_is_a ? pay_a + r.pa : pay_b + r.pb;
@@ -927,7 +953,7 @@ __global__ __launch_bounds__(256, ROLE == kRoleHeavy ? kHeavyWaves : kLightWaves
   uint32_t *s = lds[wv];
   uint16_t *ob = stage[ROLE == kRoleLight ? wv : 0];
   RecU cur = load_rec(recs + g);
-  Task tc = decode_task<OP>(cur, pay_a, pay_b);
+  Task tc = decode_task<OP, ROLE == kRoleLight>(cur, pay_a, pay_b);
   uint4 pq[8], qq[8];
 #if RBG_STUDY
   uint64_t lt_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, lt0 = 0, lt1 = 0, lt2 = 0; // decode, stage B/A/R, copy, filter, iteration, tasks
@@ -956,7 +982,7 @@ __global__ __launch_bounds__(256, ROLE == kRoleHeavy ? kHeavyWaves : kLightWaves
     RBG_LT(lt0 = __builtin_amdgcn_s_memtime());
     RBG_HT(lt0 = __builtin_amdgcn_s_memtime());
     const RecU nx = load_rec(recs + (has_next ? gn : g));
-    const Task tn = decode_task<OP>(nx, pay_a, pay_b);
+    const Task tn = decode_task<OP, ROLE == kRoleLight>(nx, pay_a, pay_b);
     RBG_LT(lt1 = __builtin_amdgcn_s_memtime(); lt_acc[0] += lt1 - lt0);
     RBG_HT(lt1 = __builtin_amdgcn_s_memtime(); lt_acc[0] += lt1 - lt0);
     int ty = kEmpty, c = 0;
@@ -1098,8 +1124,8 @@ __global__ __launch_bounds__(256, ROLE == kRoleHeavy ? kHeavyWaves : kLightWaves
       nr = ty == kRun ? (uint32_t)r : 0u;
       RBG_HT(lt_acc[3 + (ty == kBitmap ? 0 : ty == kArray ? 1 : 2)] += __builtin_amdgcn_s_memtime() - lt2);
     } else if (ROLE != kRoleHeavy) {
-      // ---- phase 1: stage X (filter) or store the clone (copy)
-      if (tc.kind == kFilter) {
+      // ---- phase 1: stage X (filter; kBits: the other operand) or store the clone (copy)
+      if (tc.kind == kFilter || tc.kind == kBits) {
         if (tc.bigq) stage_big_runs(tc.pq, tc.rq, s, lane); // only a Run payload exceeds 8 KiB
         else stage_from_chunks(tc.tq, qq, tc.cq, tc.rq, s, lane);
       } else if (!CARD_ONLY) {
@@ -1121,6 +1147,34 @@ __global__ __launch_bounds__(256, ROLE == kRoleHeavy ? kHeavyWaves : kLightWaves
         c = OP == RB_ANDNOT ? filter_rows_linear<true, !CARD_ONLY>(pq, (int)tc.cp, s, ob, tb, o, lane)
                             : filter_rows_linear<false, !CARD_ONLY>(pq, (int)tc.cp, s, ob, tb, o, lane);
         ty = c ? kArray : kEmpty;
+      } else if (tc.kind == kBits) {
+        // ---- OR into the large Bitmap P (bits_task): the rows ORed and counted first, then stored — as the
+        //      Bitmap, or as the full Run (one run [0, 65535], 16-B padded) unless Bitmap.ior(Array) keeps it
+        const uint4 *s4 = reinterpret_cast<const uint4 *>(s);
+        uint32_t cl = 0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const uint4 x = s4[k * 64 + lane];
+          pq[k] = make_uint4(pq[k].x | x.x, pq[k].y | x.y, pq[k].z | x.z, pq[k].w | x.w);
+          cl += __popc(pq[k].x) + __popc(pq[k].y) + __popc(pq[k].z) + __popc(pq[k].w);
+        }
+        c = (int)wave_sum_u32(cl);
+        const bool keep_bitmap = tm.inplace && tc.p_is_a && tc.tq == kArray;
+        ty = c == kSpan && !keep_bitmap ? kRun : kBitmap;
+        nr = ty == kRun ? 1u : 0u;
+        if (!CARD_ONLY) {
+          uint4 *o4 = reinterpret_cast<uint4 *>(dst);
+          if (ty == kRun) {
+            if (lane == 0) o4[0] = make_uint4(0xFFFF0000u, 0u, 0u, 0u);
+          } else {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) o4[k * 64 + lane] = pq[k];
+          }
+        }
+        if (CARD_ONLY) { // the card-only kernels mark a non-empty result as an Array (as the register path)
+          ty = kArray;
+          nr = 0;
+        }
       } else {
         ty = tc.tp;
         c = (int)tc.cp;
@@ -1180,7 +1234,7 @@ __global__ __launch_bounds__(256, 4) void k_probe_tasks(const uint8_t *__restric
   uint64_t g = (uint64_t)blockIdx.x * 4 + wv;
   if (g >= n) return;
   RecU cur = load_rec(recs + g);
-  Task tc = decode_task<OP>(cur, pay_a, pay_b);
+  Task tc = decode_task<OP, false>(cur, pay_a, pay_b);
   uint4 pq[8], qq[8];
   load_chunks(pq, tc.pp, tc.bigp ? 16u : tc.pbytes, lane);
   if (tc.kind == kCopy || tc.bigq) load_chunks(qq, tc.pp, 16, lane);
@@ -1190,7 +1244,7 @@ __global__ __launch_bounds__(256, 4) void k_probe_tasks(const uint8_t *__restric
     const uint64_t gn = g + stride;
     const bool has_next = gn < n;
     const RecU nx = load_rec(recs + (has_next ? gn : g));
-    const Task tn = decode_task<OP>(nx, pay_a, pay_b);
+    const Task tn = decode_task<OP, false>(nx, pay_a, pay_b);
     acc ^= fold_chunks(qq);
     {
       const bool real = has_next && tn.kind != kCopy && !tn.bigq;

@@ -690,7 +690,8 @@ int wide_run(rbgpu_ctx *ctx, int sem, const rbgpu_set *in, const std::vector<uin
   const bool sorted = !dense && !horizontal; // the counting sort runs
   uint32_t *d_mem = nullptr, *d_cid2 = nullptr, *d_klist = nullptr, *d_Hc = nullptr;
   uint64_t *d_bnd = nullptr, *d_H = nullptr, *d_tot = nullptr, *d_seg = nullptr, *d_active = nullptr,
-           *d_apos = nullptr, *d_tmp = nullptr, *d_rec = nullptr, *d_mbase = nullptr;
+           *d_apos = nullptr, *d_tmp = nullptr, *d_mbase = nullptr;
+  uint32_t *d_rec = nullptr;
   const uint64_t N1 = std::max<uint64_t>(N, 1);
   const uint64_t tmpw = std::max<uint64_t>(scan_tmp_words(65537), 1);
   auto alloc_if = [&](bool need, void **p, uint64_t bytes) { return need ? (bool)pool.alloc(p, bytes) : false; };
@@ -783,7 +784,7 @@ int wide_run(rbgpu_ctx *ctx, int sem, const rbgpu_set *in, const std::vector<uin
       xr.rec = in->krec + (uint64_t)(key_lo - in->dense_lo) * in->nb;
       xr.build = XorRecords::kCached;
     } else {
-      if (pool.alloc((void **)&d_rec, std::max<uint64_t>(N, 1) * 8)) fast_ok = false;
+      if (pool.alloc((void **)&d_rec, std::max<uint64_t>(N, 1) * 4)) fast_ok = false;
       xr.rec = d_rec;
       xr.build = dense ? XorRecords::kTranspose : XorRecords::kGather;
     }

@@ -146,16 +146,17 @@ __device__ __forceinline__ uint32_t compose(uint32_t later, uint32_t earlier) {
 // members), so a wave walking one key's members reads type / card / nruns / off as four lines per
 // member, ~5 L2 requests per container with the payload: the kernel was L2-request-bound (PMC:
 // TCC_BUSY 91 % of the kernel, 1.36G TCC requests per launch, 77 % hits) with its VALU at ~60 %.
-// So the kernel reads each (key, member) as one packed 8-B record (pack_rec, common.hpp) in key order.
-// For a dense set read in member order the records are the set's cached krec (built once per set,
-// rbgpu_set); any other member list gets them per call: 64-key x 64-member tiles of the set's packed
-// records (mrec) transposed through LDS, so both the reads (along keys) and the writes (along members)
-// are coalesced.
+// So the kernel reads each (key, member) as one 4-B record (pack_xrec, common.hpp: the payload's 16-B unit and
+// the run count; round 6 — 8-B records with the card and type before, whose build read 15 B and wrote 8 B per
+// container) in key order.  For a dense set read in member order the records are the set's cached krec
+// (built once per set, rbgpu_set); any other member list gets them per call: 64-key x 64-member tiles of the
+// set's packed records (mrec) transposed through LDS, so both the reads (along keys) and the writes (along
+// members) are coalesced.
 __global__ __launch_bounds__(256) void k_records_transpose(const uint64_t *__restrict__ mrec,
                                                            const uint64_t *__restrict__ mbase, uint64_t bias,
                                                            uint32_t M, uint32_t key_lo, uint32_t key_hi,
-                                                           uint64_t *__restrict__ rec) {
-  __shared__ uint64_t tile[64][65]; // [member][key], padded against bank conflicts on the column reads
+                                                           uint32_t *__restrict__ rec) {
+  __shared__ uint32_t tile[64][65]; // [member][key], padded against bank conflicts on the column reads
   const uint32_t k0 = key_lo + blockIdx.x * 64, m0 = blockIdx.y * 64;
   const uint32_t t = threadIdx.x, kx = t & 63, ry = t >> 6;
   uint64_t rb[16];
@@ -166,7 +167,7 @@ __global__ __launch_bounds__(256) void k_records_transpose(const uint64_t *__res
 #pragma unroll
   for (int j = 0; j < 16; ++j) v[j] = mrec[rb[j] + k]; // all 16 loads in flight at once
 #pragma unroll
-  for (int j = 0; j < 16; ++j) tile[ry + 4 * j][kx] = v[j];
+  for (int j = 0; j < 16; ++j) tile[ry + 4 * j][kx] = xrec_of(v[j]);
   __syncthreads();
   for (uint32_t r = ry; r < 64; r += 4) { // writes along members
     const uint32_t kw = k0 + r, i = m0 + kx;
@@ -174,92 +175,82 @@ __global__ __launch_bounds__(256) void k_records_transpose(const uint64_t *__res
   }
 }
 void launch_records_transpose(const uint64_t *mrec, const uint64_t *mbase, uint64_t bias, uint32_t M, uint32_t key_lo,
-                              uint32_t key_hi, uint64_t *rec, hipStream_t st) {
+                              uint32_t key_hi, uint32_t *rec, hipStream_t st) {
   if (!M || key_hi <= key_lo) return;
   k_records_transpose<<<dim3((key_hi - key_lo + 63) / 64, (M + 63) / 64), 256, 0, st>>>(mrec, mbase, bias, M, key_lo,
                                                                                       key_hi, rec);
 }
 
 // The same key-major records straight from the set's SoA (no member-major mrec first): a dense set's first
-// naive_xor reads its metadata once (15 B per container: type, card, nruns, offset) and writes the 8-B
-// records transposed, instead of packing mrec (24 B) and transposing it (16 B).  Same 64 x 64 tiles: the
-// loads run along keys (a member's containers are consecutive), the stores along members.
+// naive_xor reads the run count and the payload offset once (10 B per container; a container with a run count
+// is a Run — rbgpu_set_from_soa stores 0 for the others) and writes the 4-B records transposed.  Same 64 x 64
+// tiles: the loads run along keys (a member's containers are consecutive), the stores along members.
 // (Measured: 64 x 64 tiles dealt key-tile-major, 128 x 32 and 256 x 16 tiles, and 8 x 8 / 16 x 16 groups of
 // tiles dealt together all build config 4's records in 2.0-2.3 ms, profiles/r05/krec.)
 __global__ __launch_bounds__(256) void k_records_direct(SetView s, const uint64_t *__restrict__ mbase, uint64_t bias,
                                                         uint32_t M, uint32_t key_lo, uint32_t key_hi,
-                                                        uint64_t *__restrict__ rec) {
-  __shared__ uint64_t tile[64][65];
+                                                        uint32_t *__restrict__ rec) {
+  __shared__ uint32_t tile[64][65];
   const uint32_t k0 = key_lo + blockIdx.x * 64, m0 = blockIdx.y * 64;
   const uint32_t t = threadIdx.x, kx = t & 63, ry = t >> 6;
   uint64_t rb[16];
 #pragma unroll
   for (int j = 0; j < 16; ++j) rb[j] = mbase[min(m0 + ry + 4 * j, M - 1)] - bias;
   const uint32_t k = min(k0 + kx, key_hi - 1);
-  uint8_t ty[16];
-  uint32_t cd[16];
-  uint16_t nr[16];
+  uint32_t nr[16];
   uint64_t of[16];
 #pragma unroll
-  for (int j = 0; j < 16; ++j) { // all 64 loads in flight at once
+  for (int j = 0; j < 16; ++j) { // all 32 loads in flight at once
     const uint64_t i = rb[j] + k;
-    ty[j] = s.type[i];
-    cd[j] = s.card[i];
     nr[j] = s.nruns[i];
     of[j] = s.off[i];
   }
 #pragma unroll
-  for (int j = 0; j < 16; ++j) tile[ry + 4 * j][kx] = pack_rec(ty[j], cd[j], nr[j], of[j]);
+  for (int j = 0; j < 16; ++j) tile[ry + 4 * j][kx] = pack_xrec(nr[j] != 0, nr[j], of[j]);
   __syncthreads();
   for (uint32_t r = ry; r < 64; r += 4) { // writes along members
     const uint32_t kw = k0 + r, i = m0 + kx;
     if (i < M && kw < key_hi) rec[(uint64_t)(kw - key_lo) * M + i] = tile[kx][r];
   }
 }
-// The same with 128-key tiles and two containers per lane (u16 / 8-B / 4-B / 16-B loads, 16-B stores): every
-// load row is whole 128-B lines (a 64-key row of the u8 types is half a line).  Needs even container bases,
-// an even key count and an even member count, as a dense set of whole 65536-key members has; other sets
-// take the 64 x 64 tiles above.
+// The same with 128-key tiles and two containers per lane (4-B run-count pairs, 16-B offset pairs, 8-B record
+// pairs stored): every load row is whole 128-B lines.  Needs even container bases, an even key count and an
+// even member count, as a dense set of whole 65536-key members has; other sets take the 64 x 64 tiles above.
 __global__ __launch_bounds__(256) void k_records_direct2(SetView s, const uint64_t *__restrict__ mbase, uint64_t bias,
                                                          uint32_t M, uint32_t key_lo, uint32_t key_hi,
-                                                         uint64_t *__restrict__ rec) {
-  __shared__ uint64_t tile[64][129]; // [member][key]
+                                                         uint32_t *__restrict__ rec) {
+  __shared__ uint32_t tile[64][129]; // [member][key]
   const uint32_t k0 = key_lo + blockIdx.x * 128, m0 = blockIdx.y * 64;
   const uint32_t t = threadIdx.x, kx = t & 63, ry = t >> 6;
   uint64_t rb[16];
 #pragma unroll
   for (int j = 0; j < 16; ++j) rb[j] = mbase[min(m0 + ry + 4 * j, M - 1)] - bias;
   const uint32_t k = min(k0 + 2 * kx, key_hi - 2);
-  uint32_t ty[16], nr[16];
-  uint2 cd[16];
+  uint32_t nr[16];
   uint4 of[16];
 #pragma unroll
-  for (int j = 0; j < 16; ++j) { // all 64 loads in flight at once
+  for (int j = 0; j < 16; ++j) { // all 32 loads in flight at once
     const uint64_t i = rb[j] + k;
-    ty[j] = *reinterpret_cast<const uint16_t *>(s.type + i);
-    cd[j] = *reinterpret_cast<const uint2 *>(s.card + i);
     nr[j] = *reinterpret_cast<const uint32_t *>(s.nruns + i);
     of[j] = *reinterpret_cast<const uint4 *>(s.off + i);
   }
 #pragma unroll
   for (int j = 0; j < 16; ++j) {
-    tile[ry + 4 * j][2 * kx] = pack_rec(ty[j] & 0xFFu, cd[j].x, nr[j] & 0xFFFFu, of[j].x | ((uint64_t)of[j].y << 32));
-    tile[ry + 4 * j][2 * kx + 1] = pack_rec(ty[j] >> 8, cd[j].y, nr[j] >> 16, of[j].z | ((uint64_t)of[j].w << 32));
+    const uint32_t n0 = nr[j] & 0xFFFFu, n1 = nr[j] >> 16;
+    tile[ry + 4 * j][2 * kx] = pack_xrec(n0 != 0, n0, of[j].x | ((uint64_t)of[j].y << 32));
+    tile[ry + 4 * j][2 * kx + 1] = pack_xrec(n1 != 0, n1, of[j].z | ((uint64_t)of[j].w << 32));
   }
   __syncthreads();
   const uint32_t lx = t & 31, rr = t >> 5; // a key row is 32 lanes x 2 members: 8 rows per pass
   const uint32_t i = m0 + 2 * lx;
   for (uint32_t r = rr; r < 128; r += 8) {
     const uint32_t kw = k0 + r;
-    if (i < M && kw < key_hi) {
-      const uint64_t a = tile[2 * lx][r], b = tile[2 * lx + 1][r];
-      *reinterpret_cast<uint4 *>(rec + (uint64_t)(kw - key_lo) * M + i) =
-          make_uint4((uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32));
-    }
+    if (i < M && kw < key_hi)
+      *reinterpret_cast<uint2 *>(rec + (uint64_t)(kw - key_lo) * M + i) = make_uint2(tile[2 * lx][r], tile[2 * lx + 1][r]);
   }
 }
 void launch_records_direct(const SetView &s, const uint64_t *mbase, uint64_t bias, uint32_t M, uint32_t key_lo,
-                           uint32_t key_hi, uint64_t *rec, hipStream_t st, bool pairs) {
+                           uint32_t key_hi, uint32_t *rec, hipStream_t st, bool pairs) {
   if (!M || key_hi <= key_lo) return;
   if (pairs && !(M & 1) && !((key_hi - key_lo) & 1))
     k_records_direct2<<<dim3((key_hi - key_lo + 127) / 128, (M + 63) / 64), 256, 0, st>>>(s, mbase, bias, M, key_lo,
@@ -273,10 +264,10 @@ void launch_records_direct(const SetView &s, const uint64_t *mbase, uint64_t bia
 // grouped count, seg[65536], can be less than the members' containers when the call is a key-range shard).
 __global__ __launch_bounds__(256) void k_records_gather(const uint64_t *__restrict__ mrec,
                                                         const uint32_t *__restrict__ cid,
-                                                        const uint64_t *__restrict__ seg, uint64_t *__restrict__ rec) {
+                                                        const uint64_t *__restrict__ seg, uint32_t *__restrict__ rec) {
   const uint64_t n = seg[65536];
   for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256)
-    rec[i] = mrec[cid[i]];
+    rec[i] = xrec_of(mrec[cid[i]]);
 }
 
 namespace {
@@ -285,21 +276,25 @@ struct XBatch {
   uint32_t card, nr, typ;
   uint4 r; // runs 4h .. 4h+3 of the lane's container
 };
-__device__ __forceinline__ XBatch load_xbatch(const SetView &s, const uint64_t *rec, uint64_t i, uint64_t hi,
-                                              int h) {
+// Lane pair (2j, 2j + 1) holds container j of the batch, lane h of the pair its runs 4h .. 4h+3; the card is
+// summed from both halves' run lengths (the 4-B records carry none).  Every lane calls it (DPP).
+__device__ __forceinline__ XBatch load_xbatch(const SetView &s, const uint32_t *rec, uint64_t i, uint64_t hi, int h,
+                                              int lane) {
   XBatch b;
-  b.card = 0;
   b.nr = 0;
   b.typ = kRun;
   b.r = make_uint4(0, 0, 0, 0);
   if (i < hi) {
-    const uint64_t r = rec[i];
-    b.typ = rec_type(r);
-    b.card = rec_card(r);
-    b.nr = rec_nruns(r);
-    if (b.typ == kRun && b.nr <= 8 && b.nr > (uint32_t)(4 * h))
-      b.r = reinterpret_cast<const uint4 *>(s.payload + rec_off(r))[h];
+    const uint32_t r = rec[i];
+    b.typ = xrec_ok(r) ? (uint32_t)kRun : (uint32_t)kArray; // kArray: any container the batch cannot take
+    b.nr = xrec_nruns(r);
+    if (xrec_ok(r) && b.nr > (uint32_t)(4 * h)) b.r = reinterpret_cast<const uint4 *>(s.payload + xrec_off(r))[h];
   }
+  const uint32_t w[4] = {b.r.x, b.r.y, b.r.z, b.r.w};
+  uint32_t c = 0;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) c += (uint32_t)(4 * h + u) < b.nr ? (w[u] >> 16) + 1u : 0u;
+  b.card = c + xor_lane<1>(c, lane);
   return b;
 }
 
@@ -322,14 +317,14 @@ struct XState {
 // One exact batch of <= 32 containers starting at `base` (the accumulator P is the LDS bitmap `acc`):
 // every step's (c_j, r_j) from the sorted run boundaries, the type maps composed, P updated.  Returns
 // false when a container of the batch does not qualify (the key goes to the generic kernel).
-__device__ __forceinline__ bool exact_batch(const SetView &s, const uint64_t *rec, uint64_t base, uint64_t hi,
+__device__ __forceinline__ bool exact_batch(const SetView &s, const uint32_t *rec, uint64_t base, uint64_t hi,
                                             uint32_t *acc, uint32_t *R, int lane, XState &X) {
   uint16_t *R16 = reinterpret_cast<uint16_t *>(R);
   uint16_t *pos = R16 + 2048;                       // [512] sorted position | tie/boundary bit 15
   uint2 *MC = reinterpret_cast<uint2 *>(R);         // [512] (coverage mask, c0 | c1 << 16)
   const int cj = lane >> 1, h = lane & 1;
   const uint32_t below = (1u << cj) - 1u;
-  const XBatch cur = load_xbatch(s, rec, base + cj, hi, h);
+  const XBatch cur = load_xbatch(s, rec, base + cj, hi, h, lane);
   const bool valid = base + (uint64_t)cj < hi;
   const bool bad = valid && (cur.typ != kRun || cur.nr > 8u || cur.card >= (uint32_t)kSpan);
   if (__ballot(bad)) return false;
@@ -567,54 +562,89 @@ typedef __attribute__((address_space(1))) void gbl_void_t;
 constexpr int kWaitVm0 = 0x0F70;   // s_waitcnt vmcnt(0)
 constexpr int kWaitLgkm0 = 0xC07F; // s_waitcnt lgkmcnt(0)
 struct XMeta {
-  uint32_t typ, card, nr;
+  uint32_t typ, nr;
   uint64_t off;
 };
 // The loads are unconditional (addresses clamped to valid memory, results selected afterwards): a load
 // under a branch makes the waitcnt pass assume the worst at the merge and wait for every load in flight,
-// which would expose the whole chain's latency at every window.
-__device__ __forceinline__ XMeta xmeta_of(uint64_t r, bool valid) {
+// which would expose the whole chain's latency at every window.  A record the fast path cannot take reads as
+// kArray (the window routes the key).
+__device__ __forceinline__ XMeta xmeta_of(uint32_t r, bool valid) {
   XMeta m;
-  m.typ = valid ? rec_type(r) : (uint32_t)kRun;
-  m.card = valid ? rec_card(r) : 0u;
-  m.nr = valid ? rec_nruns(r) : 0u;
-  m.off = valid ? rec_off(r) : 0ull;
+  m.typ = !valid || xrec_ok(r) ? (uint32_t)kRun : (uint32_t)kArray;
+  m.nr = valid ? xrec_nruns(r) : 0u;
+  m.off = valid ? xrec_off(r) : 0ull;
   return m;
+}
+// a container's card from its (<= 8) runs: the runs u < nr of r0 | r1
+__device__ __forceinline__ uint32_t runs_card(const uint4 &r0, const uint4 &r1, uint32_t nr) {
+  const uint32_t w[8] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};
+  uint32_t c = 0;
+#pragma unroll
+  for (int u = 0; u < 8; ++u) c += (uint32_t)u < nr ? (w[u] >> 16) + 1u : 0u;
+  return c;
 }
 __device__ __forceinline__ XWin xwin_from(const SetView &s, const XMeta &m) {
   XWin w;
   w.typ = m.typ;
-  w.card = m.card;
   w.nr = m.nr;
   const bool runs = m.typ == kRun && m.nr && m.nr <= 8u;
   // a non-Run (or invalid) member reads the arena's first 16 B instead; runs 4..7 exist only if nr > 4
   const uint4 *p = reinterpret_cast<const uint4 *>(s.payload + (runs ? m.off : 0ull));
-  // raw loaded values, no select on them: a select right behind the loads would make the wave wait
-  // for them here, a window early (r03: every window paid the full memory latency).  Only runs u < nr
-  // are ever read, and a lane whose container is not a Run of <= 8 runs routes the key first.
+  // raw loaded values, no select on them: only runs u < nr are ever read, and a lane whose container is
+  // not a Run of <= 8 runs routes the key first.  (The card waits for them: only the first window loads here.)
   w.r0 = p[0];
   w.r1 = p[runs && m.nr > 4u ? 1 : 0];
+  w.card = runs_card(w.r0, w.r1, w.nr);
   w.pairx = 0;
   w.best = 0;
   return w;
 }
+// Round 6: the DMA is issued from inline asm.  Through the builtin the compiler knows that a vmcnt event
+// writes LDS and, lacking alias scopes, made the window's FIRST LDS access (the first mark, the M clear, the
+// first toggle) wait vmcnt(0): the runs of w+1 and the record of w+2, issued at the advance a few dozen
+// instructions earlier, were waited for in every window — the prefetch hid nothing (r06 ISA).  Hidden from
+// the waitcnt pass, the DMA is waited for only where its slot is read (take_next) or rewritten (exact
+// batches), each by an explicit vmcnt(0); the compiler's own vmcnt waits stay correct (loads return in
+// order, so an extra untracked load only makes them wait longer).
+#ifndef RBG_XOR_DMA_ASM
+#define RBG_XOR_DMA_ASM 1
+#endif
+__device__ __forceinline__ void wait_vm0() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 // the next window's runs, LDS-DMA into nb (lane-linear: r0 of lane l at nb[4l], r1 at nb[256 + 4l])
 __device__ __forceinline__ void stage_next_runs(const SetView &s, const XMeta &m, uint32_t *nb) {
   const bool runs = m.typ == kRun && m.nr && m.nr <= 8u;
   const uint8_t *p = s.payload + (runs ? m.off : 0ull);
+  const uint8_t *p1 = p + (runs && m.nr > 4u ? 16 : 0);
+#if RBG_XOR_DMA_ASM
+  const uint32_t l0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_void_t *)nb);
+  // m0 is reserved: the clobber tells the compiler, which sets m0 nowhere else in this kernel (ISA-checked)
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+  asm volatile("s_mov_b32 m0, %2\n\t"
+               "s_nop 0\n\t"
+               "global_load_lds_dwordx4 %0, off\n\t"
+               "s_add_u32 m0, m0, 0x400\n\t"
+               "s_nop 0\n\t"
+               "global_load_lds_dwordx4 %1, off"
+               :
+               : "v"(p), "v"(p1), "s"(l0)
+               : "memory", "m0");
+#pragma clang diagnostic pop
+#else
   __builtin_amdgcn_global_load_lds((gbl_void_t *)p, (lds_void_t *)nb, 16, 0, 0);
-  __builtin_amdgcn_global_load_lds((gbl_void_t *)(p + (runs && m.nr > 4u ? 16 : 0)), (lds_void_t *)(nb + 256), 16,
-                                   0, 0);
+  __builtin_amdgcn_global_load_lds((gbl_void_t *)p1, (lds_void_t *)(nb + 256), 16, 0, 0);
+#endif
 }
 // the window staged by stage_next_runs (every load of the previous window waited for first)
 __device__ __forceinline__ XWin take_next(const XMeta &m, const uint32_t *nb, int lane) {
-  __builtin_amdgcn_s_waitcnt(kWaitVm0);
+  wait_vm0();
   XWin w;
   w.typ = m.typ;
-  w.card = m.card;
   w.nr = m.nr;
   w.r0 = reinterpret_cast<const uint4 *>(nb)[lane];
   w.r1 = reinterpret_cast<const uint4 *>(nb)[64 + lane];
+  w.card = runs_card(w.r0, w.r1, w.nr);
   w.pairx = 0;
   w.best = 0;
   __builtin_amdgcn_s_waitcnt(kWaitLgkm0); // read before the next DMA overwrites the slot
@@ -719,7 +749,7 @@ constexpr int kXorUnionMinC = RBG_XOR_UNION_MINC; // try a union stretch only ab
 #define RBG_XOR_CORE 0 // study builds: 1 de-duplicates the core run's toggles and marks (slower: DESIGN.md §7 r06)
 #endif
 
-__global__ __launch_bounds__(256, 3) void k_wide_runs_xor(SetView s, const uint64_t *__restrict__ rec,
+__global__ __launch_bounds__(256, 3) void k_wide_runs_xor(SetView s, const uint32_t *__restrict__ rec,
                                                           const uint64_t *__restrict__ seg,
                                                           const uint32_t *__restrict__ klist, uint32_t nk,
                                                           uint8_t *__restrict__ out, WideOut wo,
@@ -737,7 +767,7 @@ __global__ __launch_bounds__(256, 3) void k_wide_runs_xor(SetView s, const uint6
   uint32_t *R = reg_all[wv];
   const uint32_t key = klist[q];
   const uint64_t lo = seg[key], hi = seg[key + 1];
-  if (hi <= lo || rec_type(rec[lo]) != (uint32_t)kRun) { // (no member) / first container not a Run: the generic kernel
+  if (hi <= lo || !xrec_ok(rec[lo])) { // (no member) / first container not a Run of <= 8 runs: the generic kernel
     if (lane == 0) route[q] = 1;
     return;
   }
@@ -752,12 +782,12 @@ __global__ __launch_bounds__(256, 3) void k_wide_runs_xor(SetView s, const uint6
   auto rec_at = [&](uint64_t i) { // unconditional load (clamped address, selected later); hi > lo here
     return rec[i < hi ? i : hi - 1];
   };
-  const uint64_t r0 = rec_at(lo + lane), r1 = rec_at(lo + 64 + lane);
+  const uint32_t r0 = rec_at(lo + lane), r1 = rec_at(lo + 64 + lane);
   uint32_t *nbuf = R + kNextRuns;
   XWin W = xwin_from(s, xmeta_of(r0, lo + lane < hi));       // window w
   XMeta Nm = xmeta_of(r1, lo + 64 + lane < hi);              // w+1: runs in flight into nbuf
   stage_next_runs(s, Nm, nbuf);
-  uint64_t NN = rec_at(lo + 128 + lane);                     // w+2: record in flight
+  uint32_t NN = rec_at(lo + 128 + lane);                     // w+2: record in flight
   pair_xor(W);
   uint64_t base = lo;
   // union stretch state: windows whose toggles are pending in acc (P = Pw, X describe the accumulator
@@ -949,7 +979,7 @@ __global__ __launch_bounds__(256, 3) void k_wide_runs_xor(SetView s, const uint6
           X.rvalid = 1;
         }
         lds_write_words(acc, Pw, lane);
-        __builtin_amdgcn_s_waitcnt(kWaitVm0); // the next window's runs land before the batch reuses R
+        wait_vm0(); // the next window's runs land before the batch reuses R
         wave_lds_sync();
         if (!exact_batch(s, rec, base, hi, acc, R, lane, X)) {
           fail_route = true;
@@ -976,6 +1006,7 @@ __global__ __launch_bounds__(256, 3) void k_wide_runs_xor(SetView s, const uint6
     }
     RBG_TA(5);
   }
+  wait_vm0(); // no DMA into this block's LDS outlives the wave
   if (fail_route) {
     if (lane == 0) route[q] = 1;
     return;
