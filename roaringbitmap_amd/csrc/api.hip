@@ -229,6 +229,26 @@ int ensure_mrec(const rbgpu_set *cs) {
   s->part_bytes[1] += 24ull * s->nc;
   return RB_OK;
 }
+// naive_xor's key-major 4-B records of keys [a, b) into k (the set's whole dense range laid out from dense_lo).
+// (Round 6 also built them in two key chunks on the side stream beside the first call's kernel: the build slowed
+// the kernel beside it about as much as it hid, profiles/r06/xor/krec_overlap.)
+// Member m's container at key x is begin[m] + x - dense_lo: the set's own device begin array, no host table
+// copied up (a pageable 32 KiB copy cost ~0.8 ms inside the timed setup).  From mrec when the set already has it
+// (12 B per container), else from the SoA itself (the run count and the offset, 10 B read, a 4-B record
+// written: k_records_direct).  Returns the bytes it moves.
+uint64_t build_krec_range(const rbgpu_set *s, uint32_t *k, uint32_t a, uint32_t b, hipStream_t st) {
+  const SetView v = s->view();
+  uint32_t *dst = k + (uint64_t)(a - (uint32_t)s->dense_lo) * s->nb;
+  if (s->mrec) {
+    launch_records_transpose(s->mrec, v.begin, (uint64_t)s->dense_lo, s->nb, a, b, dst, st);
+    return 12ull * s->nb * (b - a);
+  }
+  // two containers per load: member m's first container begin[m] at an even index and the arrays aligned for it
+  bool even_bases = !((uintptr_t)v.nruns & 3) && !((uintptr_t)v.off & 15) && !((a - (uint32_t)s->dense_lo) & 1);
+  for (uint32_t m = 0; m < s->nb && even_bases; ++m) even_bases = !(s->h_begin[m] & 1);
+  launch_records_direct(v, v.begin, (uint64_t)s->dense_lo, s->nb, a, b, dst, st, even_bases);
+  return 14ull * s->nb * (b - a);
+}
 int ensure_krec(const rbgpu_set *cs) {
   rbgpu_set *s = const_cast<rbgpu_set *>(cs);
   if (s->krec) return RB_OK;
@@ -236,34 +256,20 @@ int ensure_krec(const rbgpu_set *cs) {
   if (rc) return rc;
   if (s->dense_lo < 0) return fail(RB_EINVAL, "key-major records need a dense set");
   HIPCHK(hipSetDevice(s->ctx->device));
-  hipStream_t st = s->ctx->stream;
   uint32_t *k = nullptr;
   if (s->ctx->pool.alloc((void **)&k, std::max<uint64_t>(s->nc, 1) * 4)) return fail(RB_ENOMEM, "key-major records");
-  // member m's container at key x is begin[m] + x - dense_lo: the set's own device begin array, no host
-  // table copied up (a pageable 32 KiB copy cost ~0.8 ms inside the timed setup).  From mrec when the set
-  // already has it (12 B per container), else from the SoA itself (the run count and the offset, 10 B read, a
-  // 4-B record written: k_records_direct).
-  const bool from_mrec = s->mrec != nullptr;
-  const SetView v = s->view();
-  // two containers per load: member m's first container begin[m] at an even index and the arrays aligned for it
-  bool even_bases = !((uintptr_t)v.nruns & 3) && !((uintptr_t)v.off & 15);
-  for (uint32_t b = 0; b < s->nb && even_bases; ++b) even_bases = !(s->h_begin[b] & 1);
+  uint64_t bytes;
   {
     DeriveTimer t(s, 2);
-    if (from_mrec)
-      launch_records_transpose(s->mrec, v.begin, (uint64_t)s->dense_lo, s->nb, (uint32_t)s->dense_lo,
-                               (uint32_t)s->dense_hi, k, st);
-    else
-      launch_records_direct(v, v.begin, (uint64_t)s->dense_lo, s->nb, (uint32_t)s->dense_lo, (uint32_t)s->dense_hi, k, st,
-                            even_bases);
+    bytes = build_krec_range(s, k, (uint32_t)s->dense_lo, (uint32_t)s->dense_hi, s->ctx->stream);
   }
   if (hipGetLastError() != hipSuccess) {
     s->ctx->pool.release(k);
     return fail(RB_EDEVICE, "key-major record kernel failed");
   }
   s->krec = k;
-  s->derive_bytes += (from_mrec ? 12ull : 14ull) * s->nc;
-  s->part_bytes[2] += (from_mrec ? 12ull : 14ull) * s->nc;
+  s->derive_bytes += bytes;
+  s->part_bytes[2] += bytes;
   return RB_OK;
 }
 } // namespace rbg

@@ -303,6 +303,7 @@ int ensure_max_runs(const rbgpu_set *s);
 int ensure_dense(const rbgpu_set *s);
 int ensure_mrec(const rbgpu_set *s);
 int ensure_krec(const rbgpu_set *s); // needs a dense set (dense_lo >= 0)
+uint64_t build_krec_range(const rbgpu_set *s, uint32_t *k, uint32_t a, uint32_t b, hipStream_t st);
 // call accounting: zero the byte counters + record the start event / read everything back
 // zero = false: the caller's counters come zeroed some other way (the small-batch path's H2D copy)
 void stats_begin(rbgpu_ctx *ctx, bool zero = true);

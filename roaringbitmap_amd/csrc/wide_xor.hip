@@ -553,7 +553,10 @@ struct XWin { // one container per lane: the fast-forward window
 // rotation (W = N) made the compiler load into temporaries and copy them right away, which waited for
 // the loads just issued — every window paid the full memory latency (r03 ISA).
 constexpr int kNextRuns = 768; // u32 offset in the wave's region of the next window's runs (r0 x 64 | r1 x 64)
-constexpr int kMCopies = 8, kMStride = 33; // touched-word mask copies (lane & 7), strided over distinct banks
+#ifndef RBG_XOR_MCOPIES
+#define RBG_XOR_MCOPIES 8 // study builds (A/B of the copy count)
+#endif
+constexpr int kMCopies = RBG_XOR_MCOPIES, kMStride = 33; // touched-word mask copies (lane % copies), strided over distinct banks
 constexpr int kPcT = 272;                  // u32 offset of pcT (16-B aligned, after the mask copies)
 static_assert(kMCopies * kMStride <= kPcT && kPcT + 256 <= kNextRuns && kNextRuns + 512 <= kXRegion,
               "mask copies, pcT and the next runs inside the region");
@@ -745,6 +748,9 @@ constexpr int kXorUnionMinC = RBG_XOR_UNION_MINC; // try a union stretch only ab
 #ifndef RBG_XOR_DUP
 #define RBG_XOR_DUP 0
 #endif
+#ifndef RBG_XOR_CORE_MARKS
+#define RBG_XOR_CORE_MARKS 0 // study builds: 1 de-duplicates the core run's marks only (toggles as before)
+#endif
 #ifndef RBG_XOR_CORE
 #define RBG_XOR_CORE 0 // study builds: 1 de-duplicates the core run's toggles and marks (slower: DESIGN.md §7 r06)
 #endif
@@ -860,9 +866,10 @@ __global__ __launch_bounds__(256, 3) void k_wide_runs_xor(SetView s, const uint3
               (uint16_t)(__popcll(Pw[2 * k]) | (__popcll(Pw[2 * k + 1]) << 8));
         ccore = readlane(longest_run(W), 0); // lane 0 is a member of every union window (posw == 0)
         wave_lds_sync();
-        if (lane == 0 && RBG_XOR_CORE) mark_run(M, ccore); // once for the stretch (copy 0)
+        if (lane == 0 && (RBG_XOR_CORE || RBG_XOR_CORE_MARKS)) mark_run(M, ccore); // once for the stretch (copy 0)
       }
       const uint32_t mcore = RBG_XOR_CORE ? ccore : kNoCore;
+      const uint32_t mkcore = RBG_XOR_CORE || RBG_XOR_CORE_MARKS ? ccore : kNoCore;
       int L = 0;
       for (int rep = 0; rep < (RBG_XOR_DUP == 1 ? 2 : 1); ++rep) {
       if (mem) {
@@ -870,7 +877,7 @@ __global__ __launch_bounds__(256, 3) void k_wide_runs_xor(SetView s, const uint3
         uint32_t *Mc = M + kMStride * (lane & (kMCopies - 1));
 #pragma unroll
         for (int u = 0; u < 8; ++u)
-          if ((uint32_t)u < W.nr && rw[u] != mcore) mark_run(Mc, rw[u]); // the candidate is in U' already
+          if ((uint32_t)u < W.nr && rw[u] != mkcore) mark_run(Mc, rw[u]); // the candidate is in U' already
       }
       wave_lds_sync();
       // |P \ U'|: lane l sums the popcounts of words 16 l .. 16 l + 15 not in U'

@@ -576,3 +576,36 @@ def test_dense_run_shard_records(ctx, oracle):
             # the cached records are reused call after call
             for _ in range(2):
                 _check(ctx, oracle, a, refs, "FAST_XOR", members)
+
+
+def test_soa_run_count_on_non_run_containers_is_ignored(ctx, oracle):
+    """The format ignores the run count of an Array / Bitmap entry; rbgpu_set_from_soa stores 0 there, since
+    workShyAnd's SoA reads and naive_xor's 4-B records take "run count > 0" for "a Run" (round 6).  A key whose
+    members are Runs and one Array with a stray count of 3 must still come out as the oracle's."""
+    import roaringbitmap_amd as rb
+    from type_pins import ARRAY, RUN, one_container_soa, oracle_bitmap, r, u
+    conts = [(RUN, u(r(0, 3000), r(5000, 5100))), (RUN, u(r(100, 2900), r(5050, 5060))),
+             (ARRAY, np.arange(0, 6000, 3, dtype=np.uint32)), (RUN, r(200, 2000))]
+    soa = one_container_soa(conts)
+    soa.nruns[2] = 3  # the Array's stray run count
+    s = ctx.upload_soa(soa)
+    assert int(s.download().nruns[2]) == 0
+    refs = [oracle_bitmap(oracle, t, v) for t, v in conts]
+    for sem_name in ("WORKSHY_AND", "FAST_AND", "FAST_XOR", "FAST_OR"):
+        for members in ([0, 1, 2, 3], [2, 0, 1], [0, 1, 3]):
+            _check(ctx, oracle, s, refs, sem_name, np.array(members, np.uint32))
+
+
+def test_xor_records_first_call_and_reuse(ctx, oracle):
+    """naive_xor on a fresh dense set builds the key-major 4-B records on its first call, from the SoA or — when the
+    set already has packed records (a call in another member order built them) — from those; the calls after it
+    reuse them.  Even and odd key / member counts (two-container and 64 x 64 tiles)."""
+    import roaringbitmap_amd as rb
+    for nb, lo, hi, mrec_first in ((64, 0, 1024, False), (33, 100, 613, True), (40, 256, 512, False)):
+        a = ctx.generate_keys(rb.WL_WIDE_RUNS, nb, lo, hi, seed=9)
+        refs = [oracle.RefBitmap.deserialize(b) for b in a.serialize()]
+        ident = np.arange(nb, dtype=np.uint32)
+        seq = ([ident[::-1].copy()] if mrec_first else []) + [ident, ident]
+        for members in seq:
+            _check(ctx, oracle, a, refs, "FAST_XOR", members)
+        a.close()
