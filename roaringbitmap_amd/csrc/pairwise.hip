@@ -21,6 +21,19 @@ namespace rbg {
 
 constexpr int kPairThreads = 256;
 
+#ifndef RBG_SMALL_STUDY
+#define RBG_SMALL_STUDY 0 // study builds: per-block phase times (s_memrealtime) into g_small_study (rbgpu_internal_small_study)
+#endif
+#if RBG_SMALL_STUDY
+constexpr int kStudyWords = 32; // per block: t0, align, 4 wave ends, 4 key counts, done, compact end, pair, sub, nu, last;
+                                // 16 + 4 w: wave w's slowest key (ticks, result | operand types, operand cards, merge phases)
+__device__ uint64_t g_small_study[8192 * kStudyWords];
+__device__ uint64_t g_merge_ts[8192 * 4][6]; // per wave: merge_run's phase stamps of its last merge
+#define RBG_MT(i) if (lane == 0) g_merge_ts[min(blockIdx.x, 8191u) * 4 + (threadIdx.x >> 6)][i] = __builtin_amdgcn_s_memrealtime()
+#else
+#define RBG_MT(i)
+#endif
+
 __device__ __forceinline__ bool keeps_a_only(int op) { return op != RB_AND; }
 __device__ __forceinline__ bool keeps_b_only(int op) { return op == RB_OR || op == RB_XOR || is_lazy_op(op); }
 
@@ -191,6 +204,7 @@ __device__ __forceinline__ uint32_t merge_run(uint32_t *s, uint32_t ca, uint32_t
     wave_lds_sync(); // the next task restages the scratch
     return tot;
   }
+  RBG_MT(0);
   const uint32_t d0 = ((uint32_t)lane * n) >> 6, d1 = ((uint32_t)(lane + 1) * n) >> 6;
   // merge path: the number of A values among the first d0 merged values (A first on ties)
   uint32_t lo = d0 > cb ? d0 - cb : 0u, hi = min(d0, ca);
@@ -203,19 +217,34 @@ __device__ __forceinline__ uint32_t merge_run(uint32_t *s, uint32_t ca, uint32_t
   // and B, else a counting walk and a storing walk
   const uint32_t sbase = (boff + cb + 7u) & ~7u;
   const bool staged = STORE && sbase + n <= 4096u; // wave-uniform
+  RBG_MT(1);
   uint32_t cnt;
   if (staged) cnt = merge_walk<OP, false, true>(A, ca, boff, cb, lo, d0 - lo, d1 - d0, nullptr, A + sbase + d0);
   else cnt = merge_walk<OP, false, false>(A, ca, boff, cb, lo, d0 - lo, d1 - d0, nullptr, nullptr);
+  RBG_MT(2);
   const uint32_t incl = wave_scan_u32(cnt, lane), tot = readlane(incl, 63);
   if (STORE && tot) { // out: a 16-B aligned slot
     uint16_t *o = out + (incl - cnt);
     if (staged) { // compacted in LDS over A (every lane is past its walk), then whole 16-B stores
       const uint16_t *st = A + sbase + d0;
-      for (uint32_t k = 0; k < cnt; ++k) A[incl - cnt + k] = st[k];
+      // eight reads, then eight writes: one value at a time, each write waited for the read before it (the
+      // compiler cannot tell the stage from the output), ~2 LDS latencies per kept value — 4 us of an OR call's
+      // slowest key (census: 2057 | 2 values, profiles/r06/small)
+      uint16_t *o16 = A + (incl - cnt);
+      for (uint32_t k = 0; k < cnt; k += 8) {
+        uint16_t v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = st[min(k + (uint32_t)u, 4095u - (sbase + d0))];
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          if (k + (uint32_t)u < cnt) o16[k + u] = v[u];
+      }
       wave_lds_sync();
+      RBG_MT(3);
       const uint4 *a4 = reinterpret_cast<const uint4 *>(A);
       uint4 *o4 = reinterpret_cast<uint4 *>(out);
       for (uint32_t c = (uint32_t)lane; 16u * c < 2u * tot; c += 64u) o4[c] = a4[c];
+      RBG_MT(4);
     } else {
       merge_walk<OP, true, false>(A, ca, boff, cb, lo, d0 - lo, d1 - d0, o, nullptr);
     }
@@ -1599,51 +1628,74 @@ __device__ __forceinline__ uint32_t meta_cw(uint64_t m) {
 // The compaction, run by the last block of k_pair_small: drop the empty slots, write the result SoA and
 // CSR (slot t's payload stays at t * 8 KiB), add up the blocks' counters and write the call's result words
 // to host-visible memory.  xl: the block's LDS scratch (the slot -> result position map when E fits it).
+#if RBG_SMALL_STUDY
+#define RBG_SS(i) if (threadIdx.x == 0) g_small_study[8191 * kStudyWords + (i)] = __builtin_amdgcn_s_memrealtime()
+#else
+#define RBG_SS(i)
+#endif
 constexpr uint32_t kSmallXposLds = 8192;
+constexpr uint32_t kXposEmpty = 1u << 31; // xpos flag: the slot holds no result (positions stay < 2^31)
 template <class Tab>
 __device__ void small_compact(const SmallPairArgs &a, const Tab &tab, uint32_t *xl, uint32_t *wtot) {
   const uint32_t nt = blockDim.x, E = a.E;
   uint32_t *xpos = E <= kSmallXposLds ? xl : a.xpos;
   const OutView &out = a.out;
+  RBG_SS(0);
   // the summed counters (the blocks' atomics), the result CSR's first slot table entry and the first tile
   // of slot words: independent loads first
   uint64_t v = threadIdx.x < 4 ? ld_sc1(a.ctr + 8 + 8 * threadIdx.x) : 0;
   const uint32_t slot_own = a.rbegin && threadIdx.x <= a.np ? tab.slot_at(threadIdx.x) : 0u;
   constexpr int kPer = 16; // slot words per thread and tile
   uint32_t base = 0;       // results of the tiles before
+  // Tiles of kPer x 256 slots, thread x taking slots x, x + 256, ...: the loads and the result SoA stores run in
+  // slot order (coalesced), and a slot's result position is its row's base + the wave totals before it in the
+  // row + its rank in its wave's ballot — one barrier per tile.  (A thread owning 16 consecutive slots needed a
+  // block scan and stored its results 16 apart from its neighbours': every store touched 64 lines.)
+  const int lane = lane_id(), wv = threadIdx.x >> 6;
+  uint32_t(*rowtot)[4] = reinterpret_cast<uint32_t(*)[4]>(wtot); // [kPer][4 waves] (wtot holds 64 words)
+  static_assert(kPer * 4 <= 64, "row totals within wtot");
   for (uint32_t t0 = 0; t0 < E; t0 += kPer * nt) {
-    const uint32_t lo = t0 + kPer * threadIdx.x;
     uint64_t m[kPer];
 #pragma unroll
-    for (int k = 0; k < kPer; ++k) m[k] = lo + k < E ? ld_sc1(a.smeta + lo + k) : (3ull << 19);
-    uint32_t cnt = 0;
-#pragma unroll
-    for (int k = 0; k < kPer; ++k) cnt += !meta_empty(m[k]);
-    uint32_t tot;
-    uint32_t r = base + block_xscan(cnt, wtot, tot);
+    for (int k = 0; k < kPer; ++k) {
+      const uint32_t t = t0 + (uint32_t)k * nt + threadIdx.x;
+      m[k] = t < E ? ld_sc1(a.smeta + t) : (3ull << 19);
+    }
+    uint32_t pre[kPer];
 #pragma unroll
     for (int k = 0; k < kPer; ++k) {
-      const uint32_t t = lo + k;
-      if (t >= E) break;
-      xpos[t] = r;
-      if (meta_empty(m[k])) continue;
-      if (out.key) {
-        out.key[r] = (uint16_t)(m[k] >> 24);
-        out.type[r] = (uint8_t)((m[k] >> 19) & 3u);
-        out.card[r] = meta_cw(m[k]);
-        out.nruns[r] = (uint16_t)(m[k] >> 40);
-        out.off[r] = (uint64_t)t * kBitmapBytes;
-      }
-      ++r;
+      const uint64_t b = __ballot(!meta_empty(m[k]));
+      pre[k] = mbcnt64(b);
+      if (lane == 0) rowtot[k][wv] = (uint32_t)__popcll(b);
     }
-    base += tot;
+    __syncthreads();
+    uint32_t rb = base;
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+      const uint32_t w0 = rowtot[k][0], w1 = rowtot[k][1], w2 = rowtot[k][2], w3 = rowtot[k][3];
+      const uint32_t before = (wv > 0 ? w0 : 0u) + (wv > 1 ? w1 : 0u) + (wv > 2 ? w2 : 0u);
+      const uint32_t r = rb + before + pre[k], t = t0 + (uint32_t)k * nt + threadIdx.x;
+      rb += w0 + w1 + w2 + w3;
+      if (t >= E) continue;
+      const bool e = meta_empty(m[k]);
+      xpos[t] = r | (e ? kXposEmpty : 0u);
+      if (e || !out.key) continue;
+      out.key[r] = (uint16_t)(m[k] >> 24);
+      out.type[r] = (uint8_t)((m[k] >> 19) & 3u);
+      out.card[r] = meta_cw(m[k]);
+      out.nruns[r] = (uint16_t)(m[k] >> 40);
+      out.off[r] = (uint64_t)t * kBitmapBytes;
+    }
+    base = rb;
+    __syncthreads(); // the row totals are read; the next tile rewrites them
   }
-  __syncthreads();
+  RBG_SS(1);
   if (a.rbegin)
     for (uint32_t p = threadIdx.x; p <= a.np; p += nt) {
       const uint32_t t = p == threadIdx.x ? slot_own : tab.slot_at(p);
-      a.rbegin[p] = t < E ? xpos[t] : base;
+      a.rbegin[p] = t < E ? xpos[t] & ~kXposEmpty : base;
     }
+  RBG_SS(2);
   if (a.pcard) // per-pair result cardinality (RoaringBitmap.andCardinality etc.)
     for (uint32_t p = threadIdx.x; p < a.np; p += nt) {
       uint64_t c = 0;
@@ -1657,6 +1709,7 @@ __device__ void small_compact(const SmallPairArgs &a, const Tab &tab, uint32_t *
   // release: the host may return as soon as it reads that number (pairwise_small), before the kernel's
   // end is signalled
   uint64_t *vs = reinterpret_cast<uint64_t *>(wtot);
+  RBG_SS(3);
   __syncthreads(); // wtot's last readers (the scans) are done
   if (threadIdx.x < 4) {
     vs[threadIdx.x] = v;
@@ -1669,6 +1722,7 @@ __device__ void small_compact(const SmallPairArgs &a, const Tab &tab, uint32_t *
     a.hout[0] = base;
     // (a vmcnt(0) wait and a relaxed store instead of the release measured the same: profiles/r05/merge)
     __hip_atomic_store(a.hout + 5, a.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    RBG_SS(4);
   }
 }
 
@@ -1678,16 +1732,22 @@ constexpr int kSmallLdsMax = 96 * 1024; // >= small_lds_bytes(4, kSmallPairKeys)
 // (All LDS of the kernel is in the dynamic region, whose base stays 16-B aligned — the 8 KiB scratch
 // takes 16-B accesses.)
 __host__ __device__ constexpr uint32_t small_lds_bytes(uint32_t waves, uint32_t kmax) {
-  return waves * 8192u + 64u + 4u * kmax + 2u * kmax + 2u * (kmax + 1) + 2u * kmax + 16u;
+  return waves * 8192u + 256u + 4u * kmax + 2u * kmax + 2u * (kmax + 1) + 2u * kmax + 16u;
 }
 constexpr int kSmallWaves = 2; // waves per SIMD of the small-batch kernel (the register path takes ~235 VGPRs; 3 and 4 spill)
 template <int OP, bool CARD_ONLY, class Tab>
 __global__ __launch_bounds__(256, kSmallWaves) void k_pair_small(SmallPairArgs a, uint32_t kmax, Tab tab) {
   extern __shared__ __attribute__((aligned(16))) uint8_t dyn_lds[];
   __shared__ uint32_t s_last;
+#if RBG_SMALL_STUDY
+  __shared__ uint64_t s_t[8];
+  __shared__ uint32_t s_keys[4];
+  __shared__ uint64_t s_slow[4][3];
+  if (threadIdx.x == 0) s_t[0] = __builtin_amdgcn_s_memrealtime();
+#endif
   const uint32_t nw = blockDim.x >> 6;
-  uint32_t *wtot = reinterpret_cast<uint32_t *>(dyn_lds + nw * 8192u); // [16] block-scan wave totals
-  uint32_t *ent = wtot + 16; // merged key: A index | B index << 16
+  uint32_t *wtot = reinterpret_cast<uint32_t *>(dyn_lds + nw * 8192u); // [64] block-scan wave totals / row totals
+  uint32_t *ent = wtot + 64; // merged key: A index | B index << 16
   uint16_t *K = reinterpret_cast<uint16_t *>(ent + kmax);             // A's keys, then B's
   uint16_t *mpref = K + kmax;                                          // matched keys among A[0, i)
   uint16_t *ord = mpref + kmax + 1;                                    // merged positions in work order
@@ -1696,11 +1756,19 @@ __global__ __launch_bounds__(256, kSmallWaves) void k_pair_small(SmallPairArgs a
   // per-pair block prefix; small_pair_nsub blocks per pair)
   uint32_t p = 0;
   {
+    // 64 probes per round, one per lane (a binary search was ~8 dependent loads of the table, the first step of
+    // every block's critical path: profiles/r06/small): the probes increase with the lane, so the lanes whose
+    // probe passes are a prefix
     uint32_t lo = 0, hi = a.np; // blk_at(lo) <= blockIdx.x < blk_at(hi)
     while (hi - lo > 1) {
-      const uint32_t mid = (lo + hi) >> 1;
-      if (tab.blk_at(mid) <= blockIdx.x) lo = mid;
-      else hi = mid;
+      const uint32_t span = hi - lo;
+      const uint32_t q = lo + (uint32_t)(((uint64_t)span * (uint32_t)(lane + 1)) / 65u); // in [lo, hi)
+      const bool le = q > lo && tab.blk_at(q) <= blockIdx.x;
+      const uint64_t m = __ballot(le), gt = __ballot(q > lo && !le);
+      const uint32_t nlo = m ? (uint32_t)readlane(q, 63 - __builtin_clzll(m)) : lo;
+      const uint32_t nhi = gt ? (uint32_t)readlane(q, __builtin_ctzll(gt)) : hi;
+      lo = nlo;
+      hi = nhi;
     }
     p = lo;
   }
@@ -1754,6 +1822,11 @@ __global__ __launch_bounds__(256, kSmallWaves) void k_pair_small(SmallPairArgs a
     __syncthreads();
   }
   // ---- one wave per merged key
+#if RBG_SMALL_STUDY
+  if (threadIdx.x == 0) s_t[1] = __builtin_amdgcn_s_memrealtime();
+  uint32_t st_keys = 0;
+  uint64_t sl_dur = 0, sl_d1 = 0, sl_d2 = 0;
+#endif
   uint32_t *s = reinterpret_cast<uint32_t *>(dyn_lds) + wv * 2048;
   const uint32_t slot0 = tab.slot_at(p), slot1 = tab.slot_at(p + 1);
   const uint64_t keyb = sub == 0 && wv == 0 && lane == 0 ? 2ull * (na + nb) : 0ull;
@@ -1763,6 +1836,10 @@ __global__ __launch_bounds__(256, kSmallWaves) void k_pair_small(SmallPairArgs a
     const uint32_t pos = (k & 1) ? (k + 1) * W - 1 - gw : k * W + gw;
     if (pos >= nu) continue;
     const uint32_t e = ord[pos];
+#if RBG_SMALL_STUDY
+    ++st_keys;
+    const uint64_t st_k0 = __builtin_amdgcn_s_memrealtime();
+#endif
     const uint32_t en = ent[e], ia = en & 0xFFFF, ib = en >> 16;
     const bool has_a = ia != 0xFFFFu, has_b = ib != 0xFFFFu;
     const uint64_t slot = (uint64_t)slot0 + e;
@@ -1775,6 +1852,7 @@ __global__ __launch_bounds__(256, kSmallWaves) void k_pair_small(SmallPairArgs a
       const uint64_t xa = i0 + ia, xb = j0 + ib;
       const uint32_t ca = a.A.card[xa], cb = a.B.card[xb];
       if (lane == 0) inb += alg_bytes(kArray, ca, 0) + alg_bytes(kArray, cb, 0) + 32;
+      RBG_MT(5);
       {
         uint4 q[8], r[8];
         load_chunks(q, a.A.payload + a.A.off[xa], 2u * ca, lane);
@@ -1859,7 +1937,36 @@ __global__ __launch_bounds__(256, kSmallWaves) void k_pair_small(SmallPairArgs a
         if (!CARD_ONLY) outb += alg_bytes(ty, (uint32_t)c, (uint32_t)nr) + 16;
       }
     }
+#if RBG_SMALL_STUDY
+    {
+      const uint64_t d = __builtin_amdgcn_s_memrealtime() - st_k0;
+      if (d > sl_dur) {
+        const uint32_t ta = has_a ? a.A.type[i0 + ia] : 3u, tb = has_b ? a.B.type[j0 + ib] : 3u;
+        const uint32_t ca = has_a ? a.A.card[i0 + ia] : 0u, cb = has_b ? a.B.card[j0 + ib] : 0u;
+        const uint32_t ra = has_a ? a.A.nruns[i0 + ia] : 0u, rb = has_b ? a.B.nruns[j0 + ib] : 0u;
+        sl_dur = d;
+        if (lane == 0) { // merge phases relative to the key's start (0 when the key took no merge)
+          const uint64_t *mt = g_merge_ts[min(blockIdx.x, 8191u) * 4 + wv];
+          g_small_study[min(blockIdx.x, 8191u) * kStudyWords + 19 + 4 * wv] =
+              mt[5] >= st_k0 ? ((mt[5] - st_k0) | (mt[1] - mt[5]) << 12 | (mt[2] - mt[1]) << 24 | (mt[3] - mt[2]) << 36 |
+                                (mt[4] - mt[3]) << 48)
+                             : 0ull;
+        }
+        sl_d1 = ta | (tb << 2) | ((uint64_t)(ty & 0xFF) << 8) | ((uint64_t)(nr & 0xFFFF) << 16) | ((uint64_t)(uint32_t)c << 32);
+        sl_d2 = (uint64_t)ca | ((uint64_t)cb << 20) | ((uint64_t)(ra & 0xFFF) << 40) | ((uint64_t)(rb & 0xFFF) << 52);
+      }
+    }
+#endif
   }
+#if RBG_SMALL_STUDY
+  if (lane == 0) {
+    s_keys[wv] = st_keys;
+    s_t[2 + wv] = __builtin_amdgcn_s_memrealtime();
+    s_slow[wv][0] = sl_dur;
+    s_slow[wv][1] = sl_d1;
+    s_slow[wv][2] = sl_d2;
+  }
+#endif
   // slots past the merged keys hold nothing
   if (sub == 0)
     for (uint32_t t = slot0 + nu + threadIdx.x; t < slot1; t += nt) st_sc1(a.smeta + t, 3ull << 19);
@@ -1884,9 +1991,40 @@ __global__ __launch_bounds__(256, kSmallWaves) void k_pair_small(SmallPairArgs a
   if (threadIdx.x == 0)
     s_last = __hip_atomic_fetch_add(a.ctr, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == a.nblocks - 1ull;
   __syncthreads();
+#if RBG_SMALL_STUDY
+  uint64_t *gs = g_small_study + (uint64_t)min(blockIdx.x, 8191u) * kStudyWords;
+  if (threadIdx.x == 0) {
+    gs[0] = s_t[0];
+    gs[1] = s_t[1];
+    for (int w = 0; w < 4; ++w) gs[2 + w] = s_t[2 + w];
+    for (int w = 0; w < 4; ++w) gs[6 + w] = s_keys[w];
+    gs[10] = __builtin_amdgcn_s_memrealtime();
+    gs[11] = 0;
+    gs[12] = p;
+    gs[13] = sub | ((uint64_t)nsub << 32);
+    gs[14] = nu;
+    gs[15] = s_last;
+    for (int w = 0; w < 4; ++w) {
+      gs[16 + 4 * w] = s_slow[w][0];
+      gs[17 + 4 * w] = s_slow[w][1];
+      gs[18 + 4 * w] = s_slow[w][2];
+    }
+  }
+#endif
   if (!s_last) return;
   small_compact(a, tab, reinterpret_cast<uint32_t *>(dyn_lds), wtot);
+#if RBG_SMALL_STUDY
+  __syncthreads();
+  if (threadIdx.x == 0) gs[11] = __builtin_amdgcn_s_memrealtime();
+#endif
 }
+#if RBG_SMALL_STUDY
+} // namespace rbg
+extern "C" int rbgpu_internal_small_study(uint64_t *host, uint64_t words) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(rbg::g_small_study), words * 8) == hipSuccess ? 0 : -1;
+}
+namespace rbg {
+#endif
 
 template <int OP, bool CARD_ONLY, class Tab>
 static void launch_small_tab(const SmallPairArgs &a, const Tab &tab, unsigned waves, unsigned nblocks, uint32_t kmax,
