@@ -28,7 +28,7 @@ constexpr int kPairThreads = 256;
 constexpr int kStudyWords = 32; // per block: t0, align, 4 wave ends, 4 key counts, done, compact end, pair, sub, nu, last;
                                 // 16 + 4 w: wave w's slowest key (ticks, result | operand types, operand cards, merge phases)
 __device__ uint64_t g_small_study[8192 * kStudyWords];
-__device__ uint64_t g_merge_ts[8192 * 4][6]; // per wave: merge_run's phase stamps of its last merge
+__device__ uint64_t g_merge_ts[8192 * 4][8]; // per wave: merge_run's phase stamps of its last merge
 #define RBG_MT(i) if (lane == 0) g_merge_ts[min(blockIdx.x, 8191u) * 4 + (threadIdx.x >> 6)][i] = __builtin_amdgcn_s_memrealtime()
 #else
 #define RBG_MT(i)
@@ -193,6 +193,74 @@ __device__ __forceinline__ uint32_t merge_small_side(const uint16_t *A, uint32_t
   if (STORE && kept) out[mbcnt64(bk)] = (uint16_t)sv;
   return (uint32_t)__popcll(bk);
 }
+// OR / XOR of two Arrays, or ANDNOT with B small, when one side S has <= 64 values and the other L many (census:
+// the slowest keys of the small-batch kernel are ~2000 | <= 40 values — a 30-step merged walk, its scan and its
+// stage copy, profiles/r06/small).  Each S value finds its place in L (one binary search per lane); then, in the
+// merged order without deletions M (L's values and the inserted S values), a bit marks each inserted S value (INS)
+// and each deleted L value (DEL: XOR / ANDNOT drop L's values equal to an S value; OR drops nothing and inserts
+// only the unmatched S values).  One sweep over M, 64 positions a step: an L item is L[j - inserted before it], an
+// S item the next inserted value, and each kept item goes to j - deleted before it.  The steps depend on nothing
+// but two running counts, so their LDS reads pipeline.  Returns the result count; kLopsidedNo when the bitmaps
+// do not fit beside the staged arrays (the caller walks).
+constexpr uint32_t kLopsidedNo = 0xFFFFFFFFu;
+#ifndef RBG_LOPSIDED
+#define RBG_LOPSIDED 0 // study builds: 1 takes lopsided pairs off the walk (census: the slowest keys unchanged, r06)
+#endif
+template <int OP, bool STORE>
+__device__ __forceinline__ uint32_t merge_lopsided(uint16_t *A, uint32_t ca, uint32_t boff, uint32_t cb, uint16_t *out,
+                                                   int lane) {
+  const bool s_is_b = OP == RB_ANDNOT || cb <= ca; // ANDNOT: the caller sends B small
+  const uint16_t *L = s_is_b ? A : A + boff, *S = s_is_b ? A + boff : A;
+  const uint32_t cl = s_is_b ? ca : cb, cs = s_is_b ? cb : ca;
+  const uint32_t sbase = (boff + cb + 7u) & ~7u;         // u16 index past the staged arrays, 16-B aligned
+  const uint32_t nwin = (cl + cs + 63u) >> 6, nw = 2u * nwin; // 64-position windows of M, two u32 words each
+  if (sbase + 4u * nw + 64u > 4096u) return kLopsidedNo;
+  uint32_t *INS = reinterpret_cast<uint32_t *>(A + sbase), *DEL = INS + nw;
+  uint16_t *SL = reinterpret_cast<uint16_t *>(DEL + nw); // the inserted S values in order
+  for (uint32_t w = (uint32_t)lane; w < 2u * nw; w += 64u) INS[w] = 0u;
+  // S value of this lane: its place in L (lower bound) and whether L holds it
+  const bool live = (uint32_t)lane < cs;
+  const uint32_t sv = live ? S[lane] : 0x10000u;
+  uint32_t lo = 0, hi = live ? cl : 0u;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (L[mid] < sv) lo = mid + 1;
+    else hi = mid;
+  }
+  const bool matched = live && lo < cl && L[min(lo, cl - 1u)] == sv;
+  const bool ins = live && !matched && OP != RB_ANDNOT;
+  const bool del = matched && OP != RB_OR;
+  const uint64_t im = __ballot(ins), dm = __ballot(del);
+  const uint32_t ri = mbcnt64(im);
+  wave_lds_sync(); // the bitmaps are zero
+  // positions in M: an inserted S value at lb + (inserted before it); a matched L value at lb + (inserted before
+  // it) — inserted S values below a matched one are exactly the lanes below it
+  const uint32_t pm = lo + ri;
+  if (ins) {
+    atomicOr(&INS[pm >> 5], 1u << (pm & 31));
+    SL[ri] = (uint16_t)sv;
+  }
+  if (del) atomicOr(&DEL[pm >> 5], 1u << (pm & 31));
+  wave_lds_sync();
+  const uint32_t M = cl + (uint32_t)__popcll(im), kept = M - (uint32_t)__popcll(dm);
+  if (STORE && kept) {
+    const uint64_t below = (1ull << lane) - 1ull; // lane 0: 0
+    uint32_t insb = 0, delb = 0;                   // inserted / deleted items before the window
+#pragma unroll 4
+    for (uint32_t k = 0; k < nwin; ++k) {
+      const uint64_t iw = pack2(INS[2 * k], INS[2 * k + 1]), dw = pack2(DEL[2 * k], DEL[2 * k + 1]);
+      const uint32_t j = 64u * k + (uint32_t)lane;
+      const bool is_s = (iw >> lane) & 1ull, is_d = (dw >> lane) & 1ull;
+      const uint32_t r = insb + (uint32_t)__popcll(iw & below);
+      const uint32_t v = is_s ? SL[min(r, 63u)] : L[min(j - r, cl - 1u)];
+      if (j < M && !is_d) out[j - delb - (uint32_t)__popcll(dw & below)] = (uint16_t)v;
+      insb += (uint32_t)__popcll(iw);
+      delb += (uint32_t)__popcll(dw);
+    }
+  }
+  wave_lds_sync(); // the next task restages the scratch
+  return kept;
+}
 template <int OP, bool STORE>
 __device__ __forceinline__ uint32_t merge_run(uint32_t *s, uint32_t ca, uint32_t cb, uint16_t *out, int lane) {
   uint16_t *A = reinterpret_cast<uint16_t *>(s);
@@ -203,6 +271,11 @@ __device__ __forceinline__ uint32_t merge_run(uint32_t *s, uint32_t ca, uint32_t
     const uint32_t tot = merge_small_side<OP, STORE>(A, ca, B, cb, out, lane);
     wave_lds_sync(); // the next task restages the scratch
     return tot;
+  }
+  // one side of <= 64 values into the other: insertions / deletions (merge_lopsided)
+  if (RBG_LOPSIDED && (((OP == RB_OR || OP == RB_XOR) && min(ca, cb) <= 64u) || (OP == RB_ANDNOT && cb <= 64u))) {
+    const uint32_t tot = merge_lopsided<OP, STORE>(A, ca, boff, cb, out, lane);
+    if (tot != kLopsidedNo) return tot;
   }
   RBG_MT(0);
   const uint32_t d0 = ((uint32_t)lane * n) >> 6, d1 = ((uint32_t)(lane + 1) * n) >> 6;
@@ -1734,6 +1807,9 @@ constexpr int kSmallLdsMax = 96 * 1024; // >= small_lds_bytes(4, kSmallPairKeys)
 __host__ __device__ constexpr uint32_t small_lds_bytes(uint32_t waves, uint32_t kmax) {
   return waves * 8192u + 256u + 4u * kmax + 2u * kmax + 2u * (kmax + 1) + 2u * kmax + 16u;
 }
+#ifndef RBG_SMALL_ONE_STAGE
+#define RBG_SMALL_ONE_STAGE 1 // study builds: 0 inlines the staging code once per operand
+#endif
 constexpr int kSmallWaves = 2; // waves per SIMD of the small-batch kernel (the register path takes ~235 VGPRs; 3 and 4 spill)
 template <int OP, bool CARD_ONLY, class Tab>
 __global__ __launch_bounds__(256, kSmallWaves) void k_pair_small(SmallPairArgs a, uint32_t kmax, Tab tab) {
@@ -1860,6 +1936,7 @@ __global__ __launch_bounds__(256, kSmallWaves) void k_pair_small(SmallPairArgs a
         merge_stage(q, ca, r, cb, s, lane);
       }
       c = (int)merge_run<OP, !CARD_ONLY>(s, ca, cb, reinterpret_cast<uint16_t *>(dst), lane);
+      RBG_MT(6);
       ty = c || (OP == RB_XOR && a.keep_empty && !CARD_ONLY) ? (int)kArray : (int)kEmpty;
     } else if (has_a && has_b && !ident) {
       const uint64_t xa = i0 + ia, xb = j0 + ib;
@@ -1869,6 +1946,44 @@ __global__ __launch_bounds__(256, kSmallWaves) void k_pair_small(SmallPairArgs a
       const uint32_t ba = (uint32_t)payload_bytes(ta, ca, ra), bb = (uint32_t)payload_bytes(tb, cb, rb);
       if (lane == 0) inb += alg_bytes(ta, ca, ra) + alg_bytes(tb, cb, rb) + 32;
       uint64_t w[kW];
+#if RBG_SMALL_ONE_STAGE
+      // both operands through ONE copy of the staging code (a loop of two): this kernel's code (82 KB, of which
+      // each staging copy ~17 KB) outgrew the instruction cache, and its misses sat on the slowest keys' path
+      // (SQC_ICACHE_MISSES, profiles/r06/small)
+#pragma unroll 1
+      for (int side = 0; side < 2; ++side) {
+        const int t = side ? tb : ta;
+        const uint32_t c_ = side ? cb : ca, r_ = side ? rb : ra, b_ = side ? bb : ba;
+        const uint8_t *p_ = side ? pb : pa;
+        uint4 q[8];
+        if (bitmap_payload(t, c_)) {
+          load_chunks(q, p_, kBitmapBytes, lane);
+        } else {
+          if (b_ > (uint32_t)kBitmapBytes) stage_big_runs(p_, r_, s, lane);
+          else {
+            load_chunks(q, p_, b_, lane);
+            stage_from_chunks(t, q, c_, r_, s, lane);
+          }
+          const uint4 *s4 = reinterpret_cast<const uint4 *>(s);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) q[k] = s4[k * 64 + lane];
+          wave_lds_sync();
+        }
+        if (side == 0) {
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            w[2 * k] = pack2(q[k].x, q[k].y);
+            w[2 * k + 1] = pack2(q[k].z, q[k].w);
+          }
+        } else {
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            word_op<OP>(w[2 * k], pack2(q[k].x, q[k].y));
+            word_op<OP>(w[2 * k + 1], pack2(q[k].z, q[k].w));
+          }
+        }
+      }
+#else
       uint4 q[8];
       if (bitmap_payload(ta, ca)) {
         load_bitmap(pa, w, lane);
@@ -1899,6 +2014,7 @@ __global__ __launch_bounds__(256, kSmallWaves) void k_pair_small(SmallPairArgs a
         word_op<OP>(w[2 * k], pack2(q[k].x, q[k].y));
         word_op<OP>(w[2 * k + 1], pack2(q[k].z, q[k].w));
       }
+#endif
       const bool lazy = OP == RB_OR && a.lazy;
       const bool eff = eff_rule<OP>(ta, tb, ca, cb);
       int r;
@@ -1947,10 +2063,12 @@ __global__ __launch_bounds__(256, kSmallWaves) void k_pair_small(SmallPairArgs a
         sl_dur = d;
         if (lane == 0) { // merge phases relative to the key's start (0 when the key took no merge)
           const uint64_t *mt = g_merge_ts[min(blockIdx.x, 8191u) * 4 + wv];
+          const uint64_t tend = __builtin_amdgcn_s_memrealtime();
           g_small_study[min(blockIdx.x, 8191u) * kStudyWords + 19 + 4 * wv] =
-              mt[5] >= st_k0 ? ((mt[5] - st_k0) | (mt[1] - mt[5]) << 12 | (mt[2] - mt[1]) << 24 | (mt[3] - mt[2]) << 36 |
-                                (mt[4] - mt[3]) << 48)
+              mt[5] >= st_k0 ? ((mt[5] - st_k0) | (mt[1] - mt[5]) << 10 | (mt[2] - mt[1]) << 20 | (mt[3] - mt[2]) << 30 |
+                                (mt[4] - mt[3]) << 40 | (mt[6] - mt[4]) << 50)
                              : 0ull;
+          g_small_study[min(blockIdx.x, 8191u) * kStudyWords + 31 - wv] = mt[6] >= st_k0 ? tend - mt[6] : 0ull;
         }
         sl_d1 = ta | (tb << 2) | ((uint64_t)(ty & 0xFF) << 8) | ((uint64_t)(nr & 0xFFFF) << 16) | ((uint64_t)(uint32_t)c << 32);
         sl_d2 = (uint64_t)ca | ((uint64_t)cb << 20) | ((uint64_t)(ra & 0xFFF) << 40) | ((uint64_t)(rb & 0xFFF) << 52);

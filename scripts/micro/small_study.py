@@ -65,14 +65,15 @@ for blk in b:
     for w in range(4):
         d, d1, d2, d3 = int(blk[16 + 4 * w]), int(blk[17 + 4 * w]), int(blk[18 + 4 * w]), int(blk[19 + 4 * w])
         if d:
-            keys.append((d / 100.0, d1, d2, d3))
+            keys.append((d / 100.0, d1, d2, d3, int(blk[31 - w])))
 keys.sort(reverse=True)
 print("slowest keys (us): operands A | B -> result")
-for d, d1, d2, d3 in keys[:12]:
+for d, d1, d2, d3, d4 in keys[:12]:
     ta, tb, ty, nr, c = d1 & 3, (d1 >> 2) & 3, (d1 >> 8) & 0xFF, (d1 >> 16) & 0xFFFF, d1 >> 32
     ca, cb, ra, rb = d2 & 0xFFFFF, (d2 >> 20) & 0xFFFFF, (d2 >> 40) & 0xFFF, (d2 >> 52) & 0xFFF
-    mp = [((d3 >> (12 * i)) & 0xFFF) / 100.0 for i in range(5)] if d3 else None
-    ph = f"  merge: start {mp[0]:.2f} load+stage+search {mp[1]:.2f} walk {mp[2]:.2f} scan+copy {mp[3]:.2f} out {mp[4]:.2f}" if mp else ""
+    mp = [((d3 >> (10 * i)) & 0x3FF) / 100.0 for i in range(6)] if d3 else None
+    ph = (f"  merge: start {mp[0]:.2f} load+stage+search {mp[1]:.2f} walk {mp[2]:.2f} scan+copy {mp[3]:.2f} "
+          f"out {mp[4]:.2f} return {mp[5]:.2f} after {d4 / 100.0:.2f}") if mp else ""
     print(f"  {d:6.2f}  {TN[ta]}(c={ca},r={ra}) | {TN[tb]}(c={cb},r={rb}) -> {TN.get(ty, ty)}(c={c},r={nr}){ph}")
 ds = np.array([k[0] for k in keys])
 print("key durations (us):", q(ds))
