@@ -90,6 +90,7 @@ void ctx_unref(rbgpu_ctx *ctx) {
   if (ctx->h_stage) (void)hipHostFree(ctx->h_stage);
   if (ctx->h_small) (void)hipHostFree(ctx->h_small);
   if (ctx->d_small_ctr) (void)hipFree(ctx->d_small_ctr);
+  if (ctx->d_small_slots) (void)hipFree(ctx->d_small_slots);
   ctx->pool.clear();
   ctx->ws_pairs.destroy();
   ctx->ws_tasks.destroy();
@@ -510,6 +511,10 @@ int ensure_call_words(rbgpu_ctx *ctx) {
     if (hipMalloc((void **)&ctx->d_small_ctr, 512) != hipSuccess) return fail(RB_ENOMEM, "block counters");
     if (hipMemset(ctx->d_small_ctr, 0, 512) != hipSuccess) return fail(RB_EDEVICE, "block counters");
   }
+  if (!ctx->d_small_slots) { // every word kSlotUnset (all ones) between calls: each call's compaction resets its own
+    if (hipMalloc((void **)&ctx->d_small_slots, 16ull * kSmallSlots) != hipSuccess) return fail(RB_ENOMEM, "slot words");
+    if (hipMemset(ctx->d_small_slots, 0xFF, 16ull * kSmallSlots) != hipSuccess) return fail(RB_EDEVICE, "slot words");
+  }
   return RB_OK;
 }
 // Spins (bounded) until the call's last block has written `seq` after its result words: the host returns
@@ -547,6 +552,7 @@ int seq_end(rbgpu_ctx *ctx, uint64_t seq, bool poll, const char *what, bool *see
     const uint64_t got = __atomic_load_n(reinterpret_cast<const uint64_t *>(ctx->h_small) + word, __ATOMIC_ACQUIRE);
     if (got != seq) { // no block saw itself last: the counters are not this call's, and nor are the words
       (void)hipMemsetAsync(ctx->d_small_ctr, 0, 512, ctx->stream);
+      if (ctx->d_small_slots) (void)hipMemsetAsync(ctx->d_small_slots, 0xFF, 16ull * kSmallSlots, ctx->stream);
       (void)hipStreamSynchronize(ctx->stream);
       return fail(RB_EDEVICE, "%s: the kernel ended without handing over call %llu's result words (found %llu)", what,
                   (unsigned long long)seq, (unsigned long long)got);
@@ -1119,7 +1125,7 @@ static int pairwise_small(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgp
   const bool card_only = out == nullptr;
   const uint64_t E1 = std::max<uint64_t>(E, 1);
   const size_t tabb = inl ? 0 : 4 * tabv.size();
-  const size_t need = aligned256(8ull * np) + aligned256(4 * E1) + aligned256(8 * E1) + aligned256(tabb) + 256;
+  const size_t need = aligned256(8ull * np) + aligned256(4 * E1) + aligned256(tabb) + 256;
   if (ctx->ws_pairs.reserve(need, st) != hipSuccess) return fail(RB_ENOMEM, "pair workspace");
   Workspace &W = ctx->ws_pairs;
   SmallPairArgs sa{};
@@ -1142,7 +1148,7 @@ static int pairwise_small(rbgpu_ctx *ctx, int op, const rbgpu_set *a, const rbgp
   }
   sa.pcard = card_out ? W.take<uint64_t>(np) : nullptr;
   uint32_t *xpos = W.take<uint32_t>(E1);
-  sa.smeta = W.take<uint64_t>(E1);
+  sa.smeta = ctx->d_small_slots;
   sa.ctr = ctx->d_small_ctr;
 
   rbgpu_set *res = nullptr;

@@ -167,6 +167,7 @@ struct rbgpu_ctx {
   uint8_t *h_small = nullptr, *d_small = nullptr; // one-launch result words (host-visible, 256 B: [0, 8) small batches
                                                   // and BSI RANGE, [kTailWord, +10) the general pipeline's tail)
   uint64_t *d_small_ctr = nullptr;                  // small-batch finished-block count and counters
+  uint64_t *d_small_slots = nullptr;                // small-batch slot words, [2][kSmallSlots] (k_pair_small's kSlotUnset)
   uint64_t small_seq = 0;   // small-batch calls launched (the kernel's last block writes it to h_small[5])
   // A one-launch call returns on its sequence word, before its kernel's end is signalled (and before the
   // kernel-end release writes other XCDs' payload stores back from their L2s).  ev[5] is recorded behind

@@ -165,11 +165,11 @@ struct SmallPairArgs {
   SetView A, B;
   uint32_t np;
   uint8_t *arena;              // slot t's payload at t * 8 KiB (null for cardinality only)
-  uint64_t *smeta;             // [E] per slot: key, type, card word, run count (small_meta; sc1 stores)
+  uint64_t *smeta;             // [2][kSmallSlots] per slot: key, type, card word, run count (small_meta), then
+                               // input bytes | card << 32 — sc1 stores the compaction polls for (kSlotUnset
+                               // between calls: the context's buffer, reset by the compaction)
   uint64_t *pcard;             // [np] result cardinality per pair, or null
-  uint64_t *ctr;               // [0] finished blocks, [8 + 8k] k = 0..3: input bytes, key-array bytes, output
-                               // bytes, result cardinality (agent atomics; zero between calls: the last block
-                               // resets them)
+  uint64_t *ctr;               // [0] started blocks (agent atomic; zero between calls: the last block resets it)
   int lazy;                    // 0, or the priorityqueue_or role of an OR call (TaskMeta::lazy)
   int inplace;                 // in-place x1.op(x2) (PairArgs::inplace)
   int keep_empty;              // TaskMeta::keep_empty

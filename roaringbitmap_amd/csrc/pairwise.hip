@@ -171,9 +171,14 @@ __device__ __forceinline__ void merge_stage(const uint4 (&q)[8], uint32_t ca, co
 // placement for OR / XOR / ANDNOT with B small — the large side's values moved by offsets, each lane over
 // its slice — measured slower than the staged walk on census, 41 vs 39 µs per OR call, its per-value 2-B
 // stores; AND 32.2 → 31.0 µs: profiles/r05/merge/small_side_ab.txt.)
-template <int OP, bool STORE>
+// A merge's result count goes to `pub` before its first payload store (k_pair_small publishes the slot word there, so
+// the word is not queued behind the payload stores: NoPub elsewhere).
+struct NoPub {
+  __device__ void operator()(uint32_t) const {}
+};
+template <int OP, bool STORE, class Pub = NoPub>
 __device__ __forceinline__ uint32_t merge_small_side(const uint16_t *A, uint32_t ca, const uint16_t *B, uint32_t cb,
-                                                     uint16_t *out, int lane) {
+                                                     uint16_t *out, int lane, const Pub &pub = Pub()) {
   constexpr uint32_t kEnd = 0x10000u;
   const bool s_is_b = OP == RB_AND && cb <= ca; // the small side S (AND: either; ANDNOT: A)
   const uint16_t *L = s_is_b ? A : B, *S = s_is_b ? B : A;
@@ -190,6 +195,7 @@ __device__ __forceinline__ uint32_t merge_small_side(const uint16_t *A, uint32_t
   const bool m = live && lo < cl && at == sv;
   const bool kept = OP == RB_AND ? m : live && !m;
   const uint64_t bk = __ballot(kept);
+  pub((uint32_t)__popcll(bk));
   if (STORE && kept) out[mbcnt64(bk)] = (uint16_t)sv;
   return (uint32_t)__popcll(bk);
 }
@@ -261,21 +267,25 @@ __device__ __forceinline__ uint32_t merge_lopsided(uint16_t *A, uint32_t ca, uin
   wave_lds_sync(); // the next task restages the scratch
   return kept;
 }
-template <int OP, bool STORE>
-__device__ __forceinline__ uint32_t merge_run(uint32_t *s, uint32_t ca, uint32_t cb, uint16_t *out, int lane) {
+template <int OP, bool STORE, class Pub = NoPub>
+__device__ __forceinline__ uint32_t merge_run(uint32_t *s, uint32_t ca, uint32_t cb, uint16_t *out, int lane,
+                                              const Pub &pub = Pub()) {
   uint16_t *A = reinterpret_cast<uint16_t *>(s);
   const uint32_t boff = merge_boff(ca), n = ca + cb;
   const uint16_t *B = A + boff;
   // a result of the small side's values only: one ballot (merge_small_side)
   if ((OP == RB_AND && min(ca, cb) <= 64u) || (OP == RB_ANDNOT && ca <= 64u && cb > 64u)) {
-    const uint32_t tot = merge_small_side<OP, STORE>(A, ca, B, cb, out, lane);
+    const uint32_t tot = merge_small_side<OP, STORE>(A, ca, B, cb, out, lane, pub);
     wave_lds_sync(); // the next task restages the scratch
     return tot;
   }
   // one side of <= 64 values into the other: insertions / deletions (merge_lopsided)
   if (RBG_LOPSIDED && (((OP == RB_OR || OP == RB_XOR) && min(ca, cb) <= 64u) || (OP == RB_ANDNOT && cb <= 64u))) {
     const uint32_t tot = merge_lopsided<OP, STORE>(A, ca, boff, cb, out, lane);
-    if (tot != kLopsidedNo) return tot;
+    if (tot != kLopsidedNo) {
+      pub(tot); // (study path: published after its stores)
+      return tot;
+    }
   }
   RBG_MT(0);
   const uint32_t d0 = ((uint32_t)lane * n) >> 6, d1 = ((uint32_t)(lane + 1) * n) >> 6;
@@ -296,6 +306,7 @@ __device__ __forceinline__ uint32_t merge_run(uint32_t *s, uint32_t ca, uint32_t
   else cnt = merge_walk<OP, false, false>(A, ca, boff, cb, lo, d0 - lo, d1 - d0, nullptr, nullptr);
   RBG_MT(2);
   const uint32_t incl = wave_scan_u32(cnt, lane), tot = readlane(incl, 63);
+  pub(tot);
   if (STORE && tot) { // out: a 16-B aligned slot
     uint16_t *o = out + (incl - cnt);
     if (staged) { // compacted in LDS over A (every lane is past its walk), then whole 16-B stores
@@ -1692,11 +1703,16 @@ __device__ __forceinline__ uint64_t small_meta(uint32_t key, int ty, uint32_t cw
   return c | ((uint64_t)(ty == (int)kEmpty ? 3u : (uint32_t)ty) << 19) | ((uint64_t)key << 24) | ((uint64_t)nr << 40);
 }
 __device__ __forceinline__ bool meta_empty(uint64_t m) { return ((m >> 19) & 3u) == 3u; }
+// A slot's words before its key publishes them (small_meta never sets bits 56-63, the aux word's card is <= 65536):
+// the context's slot words (rbgpu_ctx::d_small_slots, [2][kSmallSlots]: slot words, then aux words = the key's input
+// bytes | its card << 32) are all kSlotUnset between calls — set so at allocation, and reset by each call's
+// compaction after its hand-off.
+constexpr uint64_t kSlotUnset = ~0ull;
 __device__ __forceinline__ uint32_t meta_cw(uint64_t m) {
   return (uint32_t)(m & 0x1FFFFu) | ((m >> 17) & 1u ? kLazyCard : 0u) | ((m >> 18) & 1u ? kRunAsBitmap : 0u);
 }
-// Cross-block hand-off: st_sc1 / ld_sc1 (wave.hpp); the slot payloads stay plain stores: nothing in the
-// launch reads them.
+// Cross-block hand-off: st_sc1 / ld_sc1 (wave.hpp) of the slot words, which the compaction polls for (their
+// values replace kSlotUnset); the slot payloads stay plain stores: nothing in the launch reads them.
 
 // The compaction, run by the last block of k_pair_small: drop the empty slots, write the result SoA and
 // CSR (slot t's payload stays at t * 8 KiB), add up the blocks' counters and write the call's result words
@@ -1714,10 +1730,16 @@ __device__ void small_compact(const SmallPairArgs &a, const Tab &tab, uint32_t *
   uint32_t *xpos = E <= kSmallXposLds ? xl : a.xpos;
   const OutView &out = a.out;
   RBG_SS(0);
-  // the summed counters (the blocks' atomics), the result CSR's first slot table entry and the first tile
-  // of slot words: independent loads first
-  uint64_t v = threadIdx.x < 4 ? ld_sc1(a.ctr + 8 + 8 * threadIdx.x) : 0;
+  // the result CSR's first slot table entry and the first tile of slot words: independent loads first
   const uint32_t slot_own = a.rbegin && threadIdx.x <= a.np ? tab.slot_at(threadIdx.x) : 0u;
+  // the call's counters, summed from the slot words: input bytes (with the key arrays), key-array bytes, output
+  // bytes, result cardinality
+  uint64_t pin = 0, pkey = 0, pout = 0, pcs = 0;
+  for (uint32_t q = threadIdx.x; q < a.np; q += nt) {
+    const uint32_t ab = tab.counts(q);
+    pkey += 2ull * ((ab & 0xFFFFu) + (ab >> 16));
+  }
+  bool bad = false; // a slot word that never came (bounded polls: the host then finds no hand-over)
   constexpr int kPer = 16; // slot words per thread and tile
   uint32_t base = 0;       // results of the tiles before
   // Tiles of kPer x 256 slots, thread x taking slots x, x + 256, ...: the loads and the result SoA stores run in
@@ -1728,11 +1750,41 @@ __device__ void small_compact(const SmallPairArgs &a, const Tab &tab, uint32_t *
   uint32_t(*rowtot)[4] = reinterpret_cast<uint32_t(*)[4]>(wtot); // [kPer][4 waves] (wtot holds 64 words)
   static_assert(kPer * 4 <= 64, "row totals within wtot");
   for (uint32_t t0 = 0; t0 < E; t0 += kPer * nt) {
-    uint64_t m[kPer];
+    uint64_t m[kPer], x[kPer];
 #pragma unroll
     for (int k = 0; k < kPer; ++k) {
       const uint32_t t = t0 + (uint32_t)k * nt + threadIdx.x;
       m[k] = t < E ? ld_sc1(a.smeta + t) : (3ull << 19);
+      x[k] = t < E ? ld_sc1(a.smeta + kSmallSlots + t) : 0ull;
+    }
+    // a block still on its keys has not published: poll, every missing word of the tile in each round trip
+    // (2^16 rounds, ~0.1 s, then the call fails instead of hanging)
+    for (uint32_t it = 0; it < (1u << 16); ++it) {
+      bool miss = false;
+#pragma unroll
+      for (int k = 0; k < kPer; ++k) miss = miss || m[k] == kSlotUnset || x[k] == kSlotUnset;
+      if (!miss) break;
+      __builtin_amdgcn_s_sleep(2);
+#pragma unroll
+      for (int k = 0; k < kPer; ++k) {
+        const uint32_t t = t0 + (uint32_t)k * nt + threadIdx.x;
+        if (m[k] == kSlotUnset) m[k] = ld_sc1(a.smeta + t);
+        if (x[k] == kSlotUnset) x[k] = ld_sc1(a.smeta + kSmallSlots + t);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+      if (m[k] == kSlotUnset || x[k] == kSlotUnset) {
+        bad = true;
+        m[k] = 3ull << 19;
+        x[k] = 0ull;
+      }
+      pin += (uint32_t)x[k];
+      if (!meta_empty(m[k])) {
+        const uint32_t cc = (uint32_t)(x[k] >> 32);
+        pcs += cc;
+        if (out.key) pout += alg_bytes((int)((m[k] >> 19) & 3u), cc, (uint32_t)(m[k] >> 40) & 0xFFFFu) + 16;
+      }
     }
     uint32_t pre[kPer];
 #pragma unroll
@@ -1784,19 +1836,41 @@ __device__ void small_compact(const SmallPairArgs &a, const Tab &tab, uint32_t *
   uint64_t *vs = reinterpret_cast<uint64_t *>(wtot);
   RBG_SS(3);
   __syncthreads(); // wtot's last readers (the scans) are done
-  if (threadIdx.x < 4) {
-    vs[threadIdx.x] = v;
-    __hip_atomic_store(a.ctr + 8 + 8 * threadIdx.x, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  {
+    const uint64_t s0 = wave_sum_u64(pin + pkey), s1 = wave_sum_u64(pkey), s2 = wave_sum_u64(pout), s3 = wave_sum_u64(pcs);
+    if (lane == 0) {
+      vs[4 * wv] = s0;
+      vs[4 * wv + 1] = s1;
+      vs[4 * wv + 2] = s2;
+      vs[4 * wv + 3] = s3;
+    }
   }
-  __syncthreads();
+  const bool fail = __syncthreads_or(bad);
   if (threadIdx.x == 0) {
     __hip_atomic_store(a.ctr, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); // ready for the next call
-    for (int k = 0; k < 4; ++k) a.hout[1 + k] = vs[k];
-    a.hout[0] = base;
-    // (a vmcnt(0) wait and a relaxed store instead of the release measured the same: profiles/r05/merge)
-    __hip_atomic_store(a.hout + 5, a.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (!fail) {
+      for (int k = 0; k < 4; ++k) {
+        uint64_t t = 0;
+        for (uint32_t w = 0; w < (nt >> 6); ++w) t += vs[4 * w + k];
+        a.hout[1 + k] = t;
+      }
+      a.hout[0] = base;
+      // the words are host memory (fine-grained: no device cache holds them), so their stores done is all the host
+      // needs before the number; a system-scope release would also write this XCD's L2 back, where the other
+      // blocks' payload stores may still be landing (+1.7 us on census; the payloads reach a consumer through the
+      // stream, wait_call_seq)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store(a.hout + 5, a.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
     RBG_SS(4);
   }
+  // the slot words back to kSlotUnset for the next call, after the hand-off (the next kernel on the stream starts
+  // after this one ends; after a failed call the host resets them, seq_end)
+  if (!fail)
+    for (uint32_t t = threadIdx.x; t < E; t += nt) {
+      a.smeta[t] = kSlotUnset;
+      a.smeta[kSmallSlots + t] = kSlotUnset;
+    }
 }
 
 // Dynamic LDS of k_pair_small: per wave an 8 KiB scratch, then the merged-key list, the keys, the match
@@ -1852,8 +1926,21 @@ __global__ __launch_bounds__(256, kSmallWaves) void k_pair_small(SmallPairArgs a
   const bool ident = tab.same(p); // x1.op(x1) in place
   const uint64_t i0 = tab.a0(p), j0 = tab.b0(p);
   const uint32_t na = tab.counts(p) & 0xFFFFu, nb = tab.counts(p) >> 16;
+#ifndef RBG_SMALL_TICKET
+#define RBG_SMALL_TICKET 0 // study builds: 1 elects the compaction block by a start ticket instead of the last block id
+#endif
+#if RBG_SMALL_TICKET
+  // the block's start ticket (the compaction's election, below), its round trip beside the key loads'
+  uint64_t tk = 0;
+  if (threadIdx.x == 0) tk = __hip_atomic_fetch_add(a.ctr, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#endif
   for (uint32_t t = threadIdx.x; t < na; t += nt) K[t] = a.A.key[i0 + t];
   for (uint32_t t = threadIdx.x; t < nb; t += nt) K[na + t] = a.B.key[j0 + t];
+#if RBG_SMALL_TICKET
+  if (threadIdx.x == 0) s_last = tk == a.nblocks - 1ull;
+#else
+  if (threadIdx.x == 0) s_last = blockIdx.x == gridDim.x - 1;
+#endif
   __syncthreads();
   const uint16_t *KA = K, *KB = K + na;
   // ---- merged key order (RoaringBitmap.and/or/xor/andNot key loops, RoaringBitmap.java:377-473,
@@ -1905,8 +1992,12 @@ __global__ __launch_bounds__(256, kSmallWaves) void k_pair_small(SmallPairArgs a
 #endif
   uint32_t *s = reinterpret_cast<uint32_t *>(dyn_lds) + wv * 2048;
   const uint32_t slot0 = tab.slot_at(p), slot1 = tab.slot_at(p + 1);
-  const uint64_t keyb = sub == 0 && wv == 0 && lane == 0 ? 2ull * (na + nb) : 0ull;
-  uint64_t inb = keyb, outb = 0, csum = 0;
+  // slots past the merged keys hold nothing
+  if (sub == 0)
+    for (uint32_t t = slot0 + nu + threadIdx.x; t < slot1; t += nt) {
+      st_sc1(a.smeta + t, 3ull << 19);
+      st_sc1(a.smeta + kSmallSlots + t, 0ull);
+    }
   const uint32_t gw = nw * sub + wv, W = nw * nsub; // this wave among the pair's
   for (uint32_t k = 0; k * W < nu; ++k) {
     const uint32_t pos = (k & 1) ? (k + 1) * W - 1 - gw : k * W + gw;
@@ -1918,16 +2009,25 @@ __global__ __launch_bounds__(256, kSmallWaves) void k_pair_small(SmallPairArgs a
 #endif
     const uint32_t en = ent[e], ia = en & 0xFFFF, ib = en >> 16;
     const bool has_a = ia != 0xFFFFu, has_b = ib != 0xFFFFu;
+    const uint32_t kkey = has_a ? KA[ia] : KB[ib];
     const uint64_t slot = (uint64_t)slot0 + e;
     uint8_t *dst = a.arena + slot * kBitmapBytes;
     int ty = kEmpty, c = 0, nr = 0;
     uint32_t cw = 0xFFFFFFFFu; // the card word to store when it is not c (priorityqueue_or's lazy marks)
+    // the key's slot word and its aux word (input bytes | card << 32), by lane 0, BEFORE the key's payload
+    // stores: issued after them, the words (and the compaction polling for them) would wait for those stores
+    auto publish = [&](int ty_, uint32_t c_, uint32_t nr_, uint32_t cw_, uint32_t inb_) {
+      if (lane == 0) {
+        st_sc1(a.smeta + slot, small_meta(kkey, ty_, cw_ != 0xFFFFFFFFu ? cw_ : c_, nr_));
+        st_sc1(a.smeta + kSmallSlots + slot, (uint64_t)inb_ | ((uint64_t)c_ << 32));
+      }
+    };
     if (RBG_SMALL_MERGE && has_a && has_b && !ident && a.A.type[i0 + ia] == kArray &&
         a.B.type[j0 + ib] == kArray && !(OP == RB_OR && a.lazy) && a.A.card[i0 + ia] + a.B.card[j0 + ib] <= kMergeMax) {
       // two Arrays: the merge (merge_run), an Array result
       const uint64_t xa = i0 + ia, xb = j0 + ib;
       const uint32_t ca = a.A.card[xa], cb = a.B.card[xb];
-      if (lane == 0) inb += alg_bytes(kArray, ca, 0) + alg_bytes(kArray, cb, 0) + 32;
+      const uint32_t kin = (uint32_t)(alg_bytes(kArray, ca, 0) + alg_bytes(kArray, cb, 0) + 32);
       RBG_MT(5);
       {
         uint4 q[8], r[8];
@@ -1935,16 +2035,18 @@ __global__ __launch_bounds__(256, kSmallWaves) void k_pair_small(SmallPairArgs a
         load_chunks(r, a.B.payload + a.B.off[xb], 2u * cb, lane);
         merge_stage(q, ca, r, cb, s, lane);
       }
-      c = (int)merge_run<OP, !CARD_ONLY>(s, ca, cb, reinterpret_cast<uint16_t *>(dst), lane);
+      auto mty = [&](uint32_t n) { return n || (OP == RB_XOR && a.keep_empty && !CARD_ONLY) ? (int)kArray : (int)kEmpty; };
+      c = (int)merge_run<OP, !CARD_ONLY>(s, ca, cb, reinterpret_cast<uint16_t *>(dst), lane,
+                                         [&](uint32_t n) { publish(mty(n), n, 0u, 0xFFFFFFFFu, kin); });
       RBG_MT(6);
-      ty = c || (OP == RB_XOR && a.keep_empty && !CARD_ONLY) ? (int)kArray : (int)kEmpty;
+      ty = mty((uint32_t)c);
     } else if (has_a && has_b && !ident) {
       const uint64_t xa = i0 + ia, xb = j0 + ib;
       const int ta = a.A.type[xa], tb = a.B.type[xb];
       const uint32_t ca = a.A.card[xa], cb = a.B.card[xb], ra = a.A.nruns[xa], rb = a.B.nruns[xb];
       const uint8_t *pa = a.A.payload + a.A.off[xa], *pb = a.B.payload + a.B.off[xb];
       const uint32_t ba = (uint32_t)payload_bytes(ta, ca, ra), bb = (uint32_t)payload_bytes(tb, cb, rb);
-      if (lane == 0) inb += alg_bytes(ta, ca, ra) + alg_bytes(tb, cb, rb) + 32;
+      const uint32_t kin = (uint32_t)(alg_bytes(ta, ca, ra) + alg_bytes(tb, cb, rb) + 32);
       uint64_t w[kW];
 #if RBG_SMALL_ONE_STAGE
       // both operands through ONE copy of the staging code (a loop of two): this kernel's code (82 KB, of which
@@ -2032,26 +2134,22 @@ __global__ __launch_bounds__(256, kSmallWaves) void k_pair_small(SmallPairArgs a
         if (ty == kRun) r = 1; // LR's Run is the full container: one run
       } else ty = type_ab(c);
       if (CARD_ONLY) ty = c ? kArray : kEmpty;
-      else if (ty != kEmpty) emit_container(bits ? (int)kBitmap : ty, w, c, r, dst, s, lane);
       nr = ty == kRun ? r : 0;
+      publish(ty, (uint32_t)c, (uint32_t)nr, cw, kin);
+      if (!CARD_ONLY && ty != kEmpty) emit_container(bits ? (int)kBitmap : ty, w, c, r, dst, s, lane);
     } else if (ident ? (OP == RB_AND || OP == RB_OR) : has_a ? keeps_a_only(OP) : keeps_b_only(OP)) {
       // x.and(x) / x.or(x) in place leave x's own containers
       // unmatched key: RoaringArray.appendCopy (RoaringArray.java:184-205)
       const SetView &S = has_a ? a.A : a.B;
       const uint64_t x = has_a ? i0 + ia : j0 + ib;
-      ty = S.type[x];
+      const int sty = S.type[x];
       c = (int)S.card[x];
       nr = S.nruns[x];
-      if (lane == 0) inb += alg_bytes(ty, (uint32_t)c, (uint32_t)nr) + 16;
-      if (!CARD_ONLY) copy_payload(S.payload + S.off[x], dst, payload_bytes(ty, (uint32_t)c, (uint32_t)nr), lane);
-      if (CARD_ONLY) ty = kArray;
-    }
-    if (lane == 0) {
-      st_sc1(a.smeta + slot, small_meta(has_a ? KA[ia] : KB[ib], ty, cw != 0xFFFFFFFFu ? cw : (uint32_t)c, (uint32_t)nr));
-      if (ty != kEmpty) {
-        csum += (uint64_t)c;
-        if (!CARD_ONLY) outb += alg_bytes(ty, (uint32_t)c, (uint32_t)nr) + 16;
-      }
+      ty = CARD_ONLY ? (int)kArray : sty;
+      publish(ty, (uint32_t)c, (uint32_t)nr, cw, (uint32_t)(alg_bytes(sty, (uint32_t)c, (uint32_t)nr) + 16));
+      if (!CARD_ONLY) copy_payload(S.payload + S.off[x], dst, payload_bytes(sty, (uint32_t)c, (uint32_t)nr), lane);
+    } else {
+      publish(kEmpty, 0u, 0u, 0xFFFFFFFFu, 0u); // a key the op drops
     }
 #if RBG_SMALL_STUDY
     {
@@ -2085,31 +2183,11 @@ __global__ __launch_bounds__(256, kSmallWaves) void k_pair_small(SmallPairArgs a
     s_slow[wv][2] = sl_d2;
   }
 #endif
-  // slots past the merged keys hold nothing
-  if (sub == 0)
-    for (uint32_t t = slot0 + nu + threadIdx.x; t < slot1; t += nt) st_sc1(a.smeta + t, 3ull << 19);
-  // the block's counters (input with key arrays, key arrays, output, result cardinality): one agent
-  // atomic per block and counter, read by the last block
-  uint64_t v[4] = {inb, keyb, outb, csum};
-  __syncthreads(); // wtot is reused below
-  uint64_t *red = reinterpret_cast<uint64_t *>(dyn_lds); // every wave is past its scratch use
-  for (int k = 0; k < 4; ++k) {
-    const uint64_t x = wave_sum_u64(v[k]);
-    if (lane == 0) red[4 * wv + k] = x;
-  }
-  __syncthreads();
-  if (threadIdx.x < 4) {
-    uint64_t x = 0;
-    for (uint32_t w = 0; w < nw; ++w) x += red[4 * w + threadIdx.x];
-    if (x) __hip_atomic_fetch_add(a.ctr + 8 + 8 * threadIdx.x, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  // ---- the last block to finish compacts (see st_sc1): every storing wave's stores done, one add
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0)
-    s_last = __hip_atomic_fetch_add(a.ctr, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == a.nblocks - 1ull;
-  __syncthreads();
+  // ---- the last block to START compacts (s_last, its start ticket): every other block has started, so its
+  //      waiting for their slot words cannot block them; the others just end, their payload stores in flight
+  //      (nothing in the launch reads a payload; the stream contract covers the rest, wait_call_seq)
 #if RBG_SMALL_STUDY
+  __syncthreads();
   uint64_t *gs = g_small_study + (uint64_t)min(blockIdx.x, 8191u) * kStudyWords;
   if (threadIdx.x == 0) {
     gs[0] = s_t[0];
@@ -2128,6 +2206,9 @@ __global__ __launch_bounds__(256, kSmallWaves) void k_pair_small(SmallPairArgs a
       gs[18 + 4 * w] = s_slow[w][2];
     }
   }
+#else
+  if (!s_last) return;
+  __syncthreads(); // the block's waves are past their scratch use
 #endif
   if (!s_last) return;
   small_compact(a, tab, reinterpret_cast<uint32_t *>(dyn_lds), wtot);
