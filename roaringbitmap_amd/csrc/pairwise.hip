@@ -212,9 +212,9 @@ constexpr uint32_t kLopsidedNo = 0xFFFFFFFFu;
 #ifndef RBG_LOPSIDED
 #define RBG_LOPSIDED 0 // study builds: 1 takes lopsided pairs off the walk (census: the slowest keys unchanged, r06)
 #endif
-template <int OP, bool STORE>
+template <int OP, bool STORE, class Pub = NoPub>
 __device__ __forceinline__ uint32_t merge_lopsided(uint16_t *A, uint32_t ca, uint32_t boff, uint32_t cb, uint16_t *out,
-                                                   int lane) {
+                                                   int lane, const Pub &pub = Pub()) {
   const bool s_is_b = OP == RB_ANDNOT || cb <= ca; // ANDNOT: the caller sends B small
   const uint16_t *L = s_is_b ? A : A + boff, *S = s_is_b ? A + boff : A;
   const uint32_t cl = s_is_b ? ca : cb, cs = s_is_b ? cb : ca;
@@ -249,6 +249,7 @@ __device__ __forceinline__ uint32_t merge_lopsided(uint16_t *A, uint32_t ca, uin
   if (del) atomicOr(&DEL[pm >> 5], 1u << (pm & 31));
   wave_lds_sync();
   const uint32_t M = cl + (uint32_t)__popcll(im), kept = M - (uint32_t)__popcll(dm);
+  pub(kept); // the count is known before the sweep
   if (STORE && kept) {
     const uint64_t below = (1ull << lane) - 1ull; // lane 0: 0
     uint32_t insb = 0, delb = 0;                   // inserted / deleted items before the window
@@ -281,11 +282,8 @@ __device__ __forceinline__ uint32_t merge_run(uint32_t *s, uint32_t ca, uint32_t
   }
   // one side of <= 64 values into the other: insertions / deletions (merge_lopsided)
   if (RBG_LOPSIDED && (((OP == RB_OR || OP == RB_XOR) && min(ca, cb) <= 64u) || (OP == RB_ANDNOT && cb <= 64u))) {
-    const uint32_t tot = merge_lopsided<OP, STORE>(A, ca, boff, cb, out, lane);
-    if (tot != kLopsidedNo) {
-      pub(tot); // (study path: published after its stores)
-      return tot;
-    }
+    const uint32_t tot = merge_lopsided<OP, STORE>(A, ca, boff, cb, out, lane, pub);
+    if (tot != kLopsidedNo) return tot;
   }
   RBG_MT(0);
   const uint32_t d0 = ((uint32_t)lane * n) >> 6, d1 = ((uint32_t)(lane + 1) * n) >> 6;
