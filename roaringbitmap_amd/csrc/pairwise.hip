@@ -210,7 +210,7 @@ __device__ __forceinline__ uint32_t merge_small_side(const uint16_t *A, uint32_t
 // do not fit beside the staged arrays (the caller walks).
 constexpr uint32_t kLopsidedNo = 0xFFFFFFFFu;
 #ifndef RBG_LOPSIDED
-#define RBG_LOPSIDED 0 // study builds: 1 takes lopsided pairs off the walk (census: the slowest keys unchanged, r06)
+#define RBG_LOPSIDED 1 // lopsided pairs off the walk, counted before the store sweep (0: the walk; profiles/r06/small/early)
 #endif
 template <int OP, bool STORE, class Pub = NoPub>
 __device__ __forceinline__ uint32_t merge_lopsided(uint16_t *A, uint32_t ca, uint32_t boff, uint32_t cb, uint16_t *out,
