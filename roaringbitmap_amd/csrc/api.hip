@@ -507,7 +507,7 @@ int ensure_call_words(rbgpu_ctx *ctx) {
       return fail(RB_EDEVICE, "host-visible result words have no device address");
     }
   }
-  if (!ctx->d_small_ctr) { // the finished-block count and the counters; the last block of every call resets them
+  if (!ctx->d_small_ctr) { // block tickets and counters of the one-launch kernels; each call's last block resets its own
     if (hipMalloc((void **)&ctx->d_small_ctr, 512) != hipSuccess) return fail(RB_ENOMEM, "block counters");
     if (hipMemset(ctx->d_small_ctr, 0, 512) != hipSuccess) return fail(RB_EDEVICE, "block counters");
   }

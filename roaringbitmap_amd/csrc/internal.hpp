@@ -166,7 +166,7 @@ struct rbgpu_ctx {
   // pairwise call's arguments and result words, so that call needs no copy engine
   uint8_t *h_small = nullptr, *d_small = nullptr; // one-launch result words (host-visible, 256 B: [0, 8) small batches
                                                   // and BSI RANGE, [kTailWord, +10) the general pipeline's tail)
-  uint64_t *d_small_ctr = nullptr;                  // small-batch finished-block count and counters
+  uint64_t *d_small_ctr = nullptr;                  // one-launch kernels' block tickets and counters (BSI, call tail)
   uint64_t *d_small_slots = nullptr;                // small-batch slot words, [2][kSmallSlots] (k_pair_small's kSlotUnset)
   uint64_t small_seq = 0;   // small-batch calls launched (the kernel's last block writes it to h_small[5])
   // A one-launch call returns on its sequence word, before its kernel's end is signalled (and before the
@@ -256,8 +256,8 @@ bool wait_call_seq(rbgpu_ctx *ctx, uint64_t seq, int word = 5);
 // The one-launch hand-off around a kernel whose last block writes the result words and then `seq`:
 // seq_begin surfaces a fault of an earlier one-launch kernel that ended after its call returned
 // (non-blocking); seq_end (ctx->ev[5] recorded behind the kernel) waits for the sequence word (else for the
-// stream) and fails with RB_EDEVICE when the words are not this call's — then the finished-block counters
-// are re-zeroed, since no block of the call saw itself last.  seq_settle waits for the kernel
+// stream) and fails with RB_EDEVICE when the words are not this call's — then the block counters and slot words
+// are reset, since no block of the call handed over.  seq_settle waits for the kernel
 // end of call `seq` (a no-op once known complete).
 int seq_begin(rbgpu_ctx *ctx);
 int seq_end(rbgpu_ctx *ctx, uint64_t seq, bool poll, const char *what, bool *seen, int word = 5);
