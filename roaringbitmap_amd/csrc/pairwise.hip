@@ -2181,9 +2181,10 @@ __global__ __launch_bounds__(256, kSmallWaves) void k_pair_small(SmallPairArgs a
     s_slow[wv][2] = sl_d2;
   }
 #endif
-  // ---- the last block to START compacts (s_last, its start ticket): every other block has started, so its
-  //      waiting for their slot words cannot block them; the others just end, their payload stores in flight
-  //      (nothing in the launch reads a payload; the stream contract covers the rest, wait_call_seq)
+  // ---- the last block compacts (s_last; RBG_SMALL_TICKET: the last to start): it is the only block that waits,
+  //      and the blocks it waits for wait on nothing, so they finish whatever the dispatch order (its polls are
+  //      bounded besides); the others just end, their payload stores in flight (nothing in the launch reads a
+  //      payload; the stream contract covers the rest, wait_call_seq)
 #if RBG_SMALL_STUDY
   __syncthreads();
   uint64_t *gs = g_small_study + (uint64_t)min(blockIdx.x, 8191u) * kStudyWords;
