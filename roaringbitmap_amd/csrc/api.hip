@@ -247,7 +247,10 @@ uint64_t build_krec_range(const rbgpu_set *s, uint32_t *k, uint32_t a, uint32_t 
   // two containers per load: member m's first container begin[m] at an even index and the arrays aligned for it
   bool even_bases = !((uintptr_t)v.nruns & 3) && !((uintptr_t)v.off & 15) && !((a - (uint32_t)s->dense_lo) & 1);
   for (uint32_t m = 0; m < s->nb && even_bases; ++m) even_bases = !(s->h_begin[m] & 1);
-  launch_records_direct(v, v.begin, (uint64_t)s->dense_lo, s->nb, a, b, dst, st, even_bases);
+  // four per load: container indices begin[m] - dense_lo + a in fours, the arrays aligned for 8-B / 16-B loads
+  bool quads = !((uintptr_t)v.nruns & 7) && !((uintptr_t)v.off & 15);
+  for (uint32_t m = 0; m < s->nb && quads; ++m) quads = !((s->h_begin[m] - (uint64_t)s->dense_lo + a) & 3);
+  launch_records_direct(v, v.begin, (uint64_t)s->dense_lo, s->nb, a, b, dst, st, even_bases, quads);
   return 14ull * s->nb * (b - a);
 }
 int ensure_krec(const rbgpu_set *cs) {

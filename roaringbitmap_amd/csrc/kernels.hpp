@@ -239,7 +239,7 @@ struct XorRecords {
 // member m's container at key k is mbase[m] - bias + k (a dense set: mbase = the set's begin, bias = key_lo)
 // pairs: every mbase[m] - bias + key_lo is even (two containers per lane, 128-key tiles)
 void launch_records_direct(const SetView &s, const uint64_t *mbase, uint64_t bias, uint32_t M, uint32_t key_lo,
-                           uint32_t key_hi, uint32_t *rec, hipStream_t st, bool pairs = false);
+                           uint32_t key_hi, uint32_t *rec, hipStream_t st, bool pairs = false, bool quads = false);
 void launch_records_transpose(const uint64_t *mrec, const uint64_t *mbase, uint64_t bias, uint32_t M, uint32_t key_lo,
                               uint32_t key_hi, uint32_t *rec, hipStream_t st);
 void launch_wide_runs_xor(const SetView &s, const uint32_t *cid, const uint64_t *seg, const uint32_t *klist,

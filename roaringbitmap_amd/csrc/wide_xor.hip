@@ -249,10 +249,54 @@ __global__ __launch_bounds__(256) void k_records_direct2(SetView s, const uint64
       *reinterpret_cast<uint2 *>(rec + (uint64_t)(kw - key_lo) * M + i) = make_uint2(tile[2 * lx][r], tile[2 * lx + 1][r]);
   }
 }
+// The same with 256-key x 32-member tiles, four containers per lane (8-B run-count quads, two 16-B offset pairs):
+// a member's load row is 2 KiB of offsets (a whole HBM page) and 512 B of run counts, and a key's store row one
+// 128-B line.  Needs container indices and the key count in fours (quads, build_krec_range).
+#ifndef RBG_REC_QUAD
+#define RBG_REC_QUAD 0 // study builds: 1 builds dense records by the 256 x 32 tiles
+#endif
+__global__ __launch_bounds__(256) void k_records_direct4(SetView s, const uint64_t *__restrict__ mbase, uint64_t bias,
+                                                         uint32_t M, uint32_t key_lo, uint32_t key_hi,
+                                                         uint32_t *__restrict__ rec) {
+  __shared__ uint32_t tile[32][257]; // [member][key]
+  const uint32_t k0 = key_lo + blockIdx.x * 256, m0 = blockIdx.y * 32;
+  const uint32_t t = threadIdx.x, kx = t & 63, ry = t >> 6;
+  uint64_t rb[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) rb[j] = mbase[min(m0 + ry + 4 * j, M - 1)] - bias;
+  const uint32_t k = min(k0 + 4 * kx, key_hi - 4);
+  uint2 nr[8];
+  uint4 o0[8], o1[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { // all 24 loads in flight at once
+    const uint64_t i = rb[j] + k;
+    nr[j] = *reinterpret_cast<const uint2 *>(s.nruns + i);
+    o0[j] = *reinterpret_cast<const uint4 *>(s.off + i);
+    o1[j] = *reinterpret_cast<const uint4 *>(s.off + i + 2);
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const uint32_t n[4] = {nr[j].x & 0xFFFFu, nr[j].x >> 16, nr[j].y & 0xFFFFu, nr[j].y >> 16};
+    const uint64_t o[4] = {o0[j].x | ((uint64_t)o0[j].y << 32), o0[j].z | ((uint64_t)o0[j].w << 32),
+                           o1[j].x | ((uint64_t)o1[j].y << 32), o1[j].z | ((uint64_t)o1[j].w << 32)};
+#pragma unroll
+    for (int u = 0; u < 4; ++u) tile[ry + 4 * j][4 * kx + u] = pack_xrec(n[u] != 0, n[u], o[u]);
+  }
+  __syncthreads();
+  const uint32_t lx = t & 31, rr = t >> 5; // a key row is 32 members x 4 B: 8 rows per pass
+  const uint32_t i = m0 + lx;
+  for (uint32_t r = rr; r < 256; r += 8) {
+    const uint32_t kw = k0 + r;
+    if (i < M && kw < key_hi) rec[(uint64_t)(kw - key_lo) * M + i] = tile[lx][r];
+  }
+}
 void launch_records_direct(const SetView &s, const uint64_t *mbase, uint64_t bias, uint32_t M, uint32_t key_lo,
-                           uint32_t key_hi, uint32_t *rec, hipStream_t st, bool pairs) {
+                           uint32_t key_hi, uint32_t *rec, hipStream_t st, bool pairs, bool quads) {
   if (!M || key_hi <= key_lo) return;
-  if (pairs && !(M & 1) && !((key_hi - key_lo) & 1))
+  if (RBG_REC_QUAD && quads && !((key_hi - key_lo) & 3))
+    k_records_direct4<<<dim3((key_hi - key_lo + 255) / 256, (M + 31) / 32), 256, 0, st>>>(s, mbase, bias, M, key_lo,
+                                                                                         key_hi, rec);
+  else if (pairs && !(M & 1) && !((key_hi - key_lo) & 1))
     k_records_direct2<<<dim3((key_hi - key_lo + 127) / 128, (M + 63) / 64), 256, 0, st>>>(s, mbase, bias, M, key_lo,
                                                                                           key_hi, rec);
   else
